@@ -1,0 +1,207 @@
+"""oracle -- TEST INFRASTRUCTURE ONLY.
+
+ctypes access to
+  * ``liboracle.so``            -- our scalar C restatement of the srsLTE receive path (the checker,
+                                   and bench.py's ``cpu_baseline`` "port");
+  * ``_ref/libsrslte_ref.so``   -- the srsLTE 20.10.1 reference compiled from its own sources
+                                   (``make -C oracle ref``), used to generate/validate golden vectors and
+                                   as the "reference" CPU baseline where the .so is present.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg may import this
+package, and only as the checker -- the product path (``srsran_amd``) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+_REF = None
+
+i16p = np.ctypeslib.ndpointer(np.int16, flags="C_CONTIGUOUS")
+u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+u16p = np.ctypeslib.ndpointer(np.uint16, flags="C_CONTIGUOUS")
+u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+
+
+def build(ref: bool = False) -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    if ref and os.path.isdir("/root/reference/lib"):
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+
+
+def lib() -> C.CDLL:
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.orc_cb_index.argtypes = [C.c_uint32]
+        L.orc_cb_size.restype = C.c_uint32
+        L.orc_cb_size.argtypes = [C.c_int]
+        L.orc_qpp.argtypes = [C.c_uint32, u16p]
+        L.orc_tdec_nsb.restype = C.c_uint32
+        L.orc_tdec_nsb.argtypes = [C.c_uint32]
+        L.orc_tdec_buf_len.restype = C.c_uint32
+        L.orc_tdec_buf_len.argtypes = [C.c_uint32]
+        L.orc_tdec_pack_input.argtypes = [i16p, C.c_uint32, i16p]
+        L.orc_tdec_run.argtypes = [i16p, C.c_uint32, C.c_uint32, u8p, C.c_void_p, C.c_void_p]
+        L.orc_tdec_run_generic.argtypes = [i16p, C.c_uint32, C.c_uint32, u8p]
+        L.orc_tcod_encode.argtypes = [u8p, C.c_uint32, u8p]
+        L.orc_crc.restype = C.c_uint32
+        L.orc_crc.argtypes = [u8p, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.orc_cbsegm.argtypes = [C.c_uint32, u32p]
+        L.orc_tdec_run_batch.argtypes = [i16p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u8p, C.c_int]
+        _LIB = L
+    return _LIB
+
+
+def ref_available() -> bool:
+    return os.path.exists(os.path.join(HERE, "_ref", "libsrslte_ref.so"))
+
+
+def ref() -> C.CDLL:
+    global _REF
+    if _REF is None:
+        L = C.CDLL(os.path.join(HERE, "_ref", "libsrslte_ref.so"))
+        L.ref_tdec_new.restype = C.c_void_p
+        L.ref_tdec_new.argtypes = [C.c_uint32, C.c_int]
+        L.ref_tdec_free.argtypes = [C.c_void_p]
+        L.ref_tdec_run.argtypes = [C.c_void_p, i16p, C.c_uint32, C.c_uint32, u8p, C.c_void_p]
+        L.ref_tcod_encode.argtypes = [u8p, u8p, C.c_uint32]
+        L.ref_crc_byte.restype = C.c_uint32
+        L.ref_crc_byte.argtypes = [C.c_uint32, C.c_int, u8p, C.c_int]
+        L.ref_cbsegm.argtypes = [C.c_uint32, u32p]
+        L.ref_rm_turbo_rx.argtypes = [i16p, C.c_uint32, i16p, C.c_uint32, C.c_uint32]
+        L.ref_tdec_run_batch.argtypes = [i16p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u8p, C.c_int]
+        L.ref_demod_soft_s.argtypes = [C.c_int, f32p, i16p, C.c_int]
+        L.ref_scramble_s.argtypes = [C.c_uint32, i16p, C.c_int, C.c_int]
+        _REF = L
+    return _REF
+
+
+# ------------------------------------------------------------------ thin helpers
+
+def cb_sizes() -> list[int]:
+    L = lib()
+    return [int(L.orc_cb_size(i)) for i in range(188)]
+
+
+def qpp(K: int) -> np.ndarray:
+    out = np.zeros(K, np.uint16)
+    assert lib().orc_qpp(K, out) == 0
+    return out
+
+
+def tdec_nsb(K: int) -> int:
+    return int(lib().orc_tdec_nsb(K))
+
+
+def tdec_buf_len(K: int) -> int:
+    return int(lib().orc_tdec_buf_len(K))
+
+
+def tdec_pack_input(lin: np.ndarray, K: int) -> np.ndarray:
+    buf = np.zeros(tdec_buf_len(K), np.int16)
+    lib().orc_tdec_pack_input(np.ascontiguousarray(lin, np.int16), K, buf)
+    return buf
+
+
+def tdec_run(buf: np.ndarray, K: int, nhalf: int, trace: bool = False, llr: bool = False):
+    out = np.zeros(K // 8, np.uint8)
+    tr = np.zeros((nhalf, K // 8), np.uint8) if trace else None
+    lo = np.zeros(K, np.int16) if llr else None
+    rc = lib().orc_tdec_run(np.ascontiguousarray(buf, np.int16), K, nhalf, out,
+                            tr.ctypes.data if tr is not None else None,
+                            lo.ctypes.data if lo is not None else None)
+    assert rc == 0
+    res = [out]
+    if trace:
+        res.append(tr)
+    if llr:
+        res.append(lo)
+    return res[0] if len(res) == 1 else tuple(res)
+
+
+def tdec_run_generic(lin: np.ndarray, K: int, nhalf: int) -> np.ndarray:
+    out = np.zeros(K // 8, np.uint8)
+    assert lib().orc_tdec_run_generic(np.ascontiguousarray(lin, np.int16), K, nhalf, out) == 0
+    return out
+
+
+def tdec_run_batch(bufs: np.ndarray, K: int, nhalf: int, nthreads: int) -> np.ndarray:
+    bufs = np.ascontiguousarray(bufs, np.int16)
+    out = np.zeros((bufs.shape[0], K // 8), np.uint8)
+    lib().orc_tdec_run_batch(bufs, bufs.shape[1], bufs.shape[0], K, nhalf, out, nthreads)
+    return out
+
+
+def tcod_encode(bits: np.ndarray, K: int) -> np.ndarray:
+    out = np.zeros(3 * K + 12, np.uint8)
+    assert lib().orc_tcod_encode(np.ascontiguousarray(bits, np.uint8), K, out) == 0
+    return out
+
+
+CRC24A = (0x1864CFB, 24)
+CRC24B = (0x1800063, 24)
+CRC16 = (0x11021, 16)
+CRC8 = (0x19B, 8)
+
+
+def crc(data_bytes: np.ndarray, nbits: int, poly_order=CRC24A) -> int:
+    return int(lib().orc_crc(np.ascontiguousarray(data_bytes, np.uint8), nbits, poly_order[0], poly_order[1]))
+
+
+def cbsegm(tbs: int) -> dict:
+    r = np.zeros(6, np.uint32)
+    assert lib().orc_cbsegm(tbs, r) == 0
+    return dict(zip(["C", "K1", "K2", "C1", "C2", "F"], [int(v) for v in r]))
+
+
+# ------------------------------------------------------------------ test-vector synthesis
+
+def awgn_llrs(rng: np.random.Generator, coded_bits: np.ndarray, ebno_db: float, scale: float = 100.0) -> np.ndarray:
+    """BPSK + AWGN at Eb/N0 for a rate-1/3 code, LLR = int16(scale * (+-1 + sigma*n)) as
+    turbodecoder_test.c:236-247 does (positive = bit 1).  numpy RNG replaces glibc rand()."""
+    esno_db = ebno_db + 10 * np.log10(1.0 / 3.0)
+    sigma = 10 ** (-esno_db / 20)
+    sym = np.where(coded_bits.astype(bool), 1.0, -1.0).astype(np.float32)
+    y = sym + np.float32(sigma) * rng.standard_normal(sym.shape).astype(np.float32)
+    return np.trunc(scale * y).clip(-32768, 32767).astype(np.int16)
+
+
+def make_cb(rng: np.random.Generator, K: int, ebno_db: float, scale: float = 100.0):
+    """Random info bits -> encoder-ordered int16 LLRs (3K+12) -> AUTO-layout decoder buffer."""
+    bits = rng.integers(0, 2, K, dtype=np.uint8)
+    coded = tcod_encode(bits, K)
+    lin = awgn_llrs(rng, coded, ebno_db, scale)
+    return bits, lin, tdec_pack_input(lin, K)
+
+
+# ------------------------------------------------------------------ reference wrappers
+
+class RefTdec:
+    """The reference decoder (AUTO, or GENERIC manual + force_not_sb)."""
+
+    def __init__(self, generic: bool = False, max_K: int = 6144):
+        self.L = ref()
+        self.h = self.L.ref_tdec_new(max_K, 1 if generic else 0)
+
+    def run(self, buf: np.ndarray, K: int, nhalf: int, trace: bool = False):
+        b = np.array(buf, np.int16, copy=True)
+        out = np.zeros(K // 8, np.uint8)
+        tr = np.zeros((nhalf, K // 8), np.uint8) if trace else None
+        assert self.L.ref_tdec_run(self.h, b, K, nhalf, out, tr.ctypes.data if tr is not None else None) == 0
+        return (out, tr) if trace else out
+
+    def __del__(self):
+        try:
+            self.L.ref_tdec_free(self.h)
+        except Exception:
+            pass
