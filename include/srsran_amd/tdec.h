@@ -1,0 +1,88 @@
+/*
+ * include/srsran_amd/tdec.h -- C ABI of the MI355X (gfx950) turbo decoder.
+ *
+ * Two levels, both plain C (pointers + sizes, no HIP/torch types in the signatures):
+ *
+ * 1. Batched GPU API (the product entry point).  Decodes N code blocks of one size K in one call,
+ *    bit-exact with srslte_tdec_run_all() of the srsLTE 20.10.1 AVX2 build in AUTO mode.
+ *    Replaces the per-CB loop around srslte_tdec_run_all / srslte_tdec_iteration in
+ *    lib/src/phy/phch/sch.c:363-488 (decode_tb_cb) and lib/src/phy/fec/test/turbodecoder_test.c:251-260.
+ *
+ * 2. srslte_tdec_* drop-in (srsran_amd/srslte_compat.h): the exact per-CB API of
+ *    lib/include/srslte/phy/fec/turbodecoder.h:97-121 implemented on top of (1).
+ *
+ * Input format (per code block): the decoder buffer that srslte_rm_turbo_rx_lut() produces for K
+ * (rm_turbo.c:397-454), i.e. 3*(K+32)+12 int16:
+ *   K > 800 (and K%16==0): 16-window sub-block layout, stream s at s*(K+32), step j of window w
+ *                          at j*16+w, 12 tail LLRs at 3*(K+32);
+ *   400 < K <= 800:         the same with 8 windows;
+ *   K <= 400:               linear [x0 z0 z'0 x1 ...] then the 12 tails at 3*K.
+ * Output: K/8 bytes, bit = LLR > 0, MSB first (srslte_tdec_*_decision_byte).
+ *
+ * Error codes follow srslte (config.h:57-64): 0 success, -1 error, -2 invalid inputs.
+ */
+#ifndef SRSRAN_AMD_TDEC_H
+#define SRSRAN_AMD_TDEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MI355_SUCCESS 0
+#define MI355_ERROR -1
+#define MI355_ERROR_INVALID_INPUTS -2
+
+typedef struct mi355_tdec_batch mi355_tdec_batch_t;
+
+/* Create a batch decoder bound to HIP device `device`.  Workspace grows on demand. */
+int  mi355_tdec_batch_create(mi355_tdec_batch_t** q, int device);
+void mi355_tdec_batch_destroy(mi355_tdec_batch_t* q);
+
+/* Device-resident batch decode, asynchronous on `stream` (a hipStream_t, NULL = the library's own
+ * stream).  d_in: n buffers of `in_stride` int16 each (in_stride even, >= 3*(K+32)+12).
+ * d_out: n rows of `out_stride` bytes (>= K/8).  nhalf = srslte "iterations" (half-iterations). */
+int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
+                             const int16_t*      d_in,
+                             size_t              in_stride,
+                             uint32_t            n,
+                             uint32_t            K,
+                             uint32_t            nhalf,
+                             uint8_t*            d_out,
+                             size_t              out_stride,
+                             void*               stream);
+
+/* Host-buffer convenience wrapper: copy in, decode, copy out, synchronise. */
+int mi355_tdec_batch_run(mi355_tdec_batch_t* q,
+                         const int16_t*      in,
+                         size_t              in_stride,
+                         uint32_t            n,
+                         uint32_t            K,
+                         uint32_t            nhalf,
+                         uint8_t*            out,
+                         size_t              out_stride);
+
+/* Kernel timing: when enabled, every MAP (half-iteration) kernel launch is bracketed by HIP events on
+ * the launch stream; mi355_tdec_batch_kernel_stats() synchronises, returns the summed kernel time in
+ * milliseconds and the launch count since the last call, and resets both. */
+void mi355_tdec_batch_set_profiling(mi355_tdec_batch_t* q, int enable);
+int  mi355_tdec_batch_kernel_stats(mi355_tdec_batch_t* q, double* ms, uint32_t* launches);
+
+/* Number of trellis windows the reference AVX2 build uses for K (turbodecoder.c:381-393): 16, 8 or 0. */
+uint32_t mi355_tdec_autoimp_get_subblocks(uint32_t long_cb);
+
+/* Minimal device-memory helpers so hosts without a HIP toolchain can stage buffers. */
+void* mi355_dev_alloc(size_t bytes, int device);
+void  mi355_dev_free(void* p);
+int   mi355_memcpy_h2d(void* dst, const void* src, size_t bytes);
+int   mi355_memcpy_d2h(void* dst, const void* src, size_t bytes);
+int   mi355_memset_dev(void* dst, int value, size_t bytes);
+int   mi355_device_sync(void);
+int   mi355_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,78 @@
+// srsran_amd/csrc/tdec_internal.h -- device-side argument blocks shared by the turbo-decoder
+// kernels (tdec_kernels.hip) and the host runtime (tdec_runtime.cpp).  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TDEC_INF 10000   // turbodecoder_win.h:151 / turbodecoder_gen.c:37
+#define TDEC_WARMUP 40   // win_overlap_len, turbodecoder_win.h:149
+#define TDEC_SEG 8       // beta checkpoint spacing (rows) of the window kernel
+
+namespace mi355 {
+
+// Packed lane-major layout of one window-mode code block (DESIGN.md "HBM layout"):
+//   u32 [NL = NSB/2 lanes][Lp steps]; low int16 = window 2l, high int16 = window 2l+1.
+struct TdecWinArgs {
+  const uint32_t* S;    // systematic
+  const uint32_t* P0;   // parity 1
+  const uint32_t* P1;   // parity 2 (interleaved order)
+  uint32_t*       A1;   // a-priori of DEC1 (natural order)
+  uint32_t*       E;    // DEC1 extrinsic -> DEC2 input (interleaved order)
+  uint32_t*       D;    // decision LLRs (natural order)
+  const int16_t*  T;    // 12 tail LLRs per code block (encoder order)
+  uint32_t*       ckpt; // [cb][l][nseg][8] beta checkpoints
+  const uint32_t* dstE; // [NL][Lp] (lo,hi) int16 offsets: natural -> interleaved position
+  const uint32_t* dstA; // [NL][Lp] (lo,hi) int16 offsets: interleaved -> natural position
+  int             ncb, L, Lp, nseg, n, write_d;
+};
+
+struct TdecPrepArgs {
+  const int16_t* in;  // softbuffer-layout inputs
+  size_t         stride;
+  uint32_t *     S, *P0, *P1;
+  int16_t*       T;
+  int            ncb, L, Lp;
+};
+
+struct TdecDecideArgs {
+  const uint32_t* D;
+  uint8_t*        out;
+  size_t          out_stride;
+  int             ncb, L, Lp;
+};
+
+// generic (single-window, wrapping) decoder for K <= 400: two code blocks per lane
+struct TdecGenArgs {
+  const uint32_t* S;    // [pair][K+3] (lo = cb 2p, hi = cb 2p+1), natural order incl. tail
+  const uint32_t* P0;
+  const uint32_t* P1;
+  uint32_t*       A1;   // [pair][Kp]
+  uint32_t*       E;    // [pair][Kp] interleaved order; E[K..K+2] = DEC2 systematic tail x'_K..
+  uint32_t*       D;    // [pair][Kp] natural order
+  uint32_t*       ckpt; // [pair][nseg][8]
+  const uint16_t* pi;   // [2K]: QPP forward table pi[0..K), then its inverse
+  int             npair, K, Kp, nseg, n, write_d;
+};
+
+struct TdecGenPrepArgs {
+  const int16_t* in;
+  size_t         stride;
+  uint32_t *     S, *P0, *P1, *E;
+  int            ncb, npair, K, Kp;
+};
+
+struct TdecGenDecideArgs {
+  const uint32_t* D;
+  uint8_t*        out;
+  size_t          out_stride;
+  int             ncb, K, Kp;
+};
+
+hipError_t tdec_win_launch_prep(int nsb, const TdecPrepArgs& a, hipStream_t s);
+hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s);
+hipError_t tdec_win_launch_decide(int nsb, const TdecDecideArgs& a, hipStream_t s);
+hipError_t tdec_gen_launch_prep(const TdecGenPrepArgs& a, hipStream_t s);
+hipError_t tdec_gen_launch_halfit(const TdecGenArgs& a, hipStream_t s);
+hipError_t tdec_gen_launch_decide(const TdecGenDecideArgs& a, hipStream_t s);
+
+} // namespace mi355

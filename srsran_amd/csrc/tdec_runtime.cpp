@@ -1,0 +1,388 @@
+// srsran_amd/csrc/tdec_runtime.cpp -- host runtime behind include/srsran_amd/tdec.h.
+//
+// Owns the device workspace, the per-K interleaver/destination tables and the launch sequence
+//   prep (softbuffer layout -> packed lane-major) -> nhalf x MAP half-iteration -> decision bytes.
+// All launches of one call go to one stream; nothing in the launch path allocates or synchronises
+// once the workspace has grown to the batch size, so a caller can capture it in a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <stdio.h>
+#include <string.h>
+#include <vector>
+
+#include "../../include/srsran_amd/tdec.h"
+#include "lte_qpp_table.h"
+#include "tdec_internal.h"
+
+using namespace mi355;
+
+#define CHECK_HIP(x)                                                                                                   \
+  do {                                                                                                                 \
+    hipError_t e_ = (x);                                                                                               \
+    if (e_ != hipSuccess) {                                                                                            \
+      fprintf(stderr, "[srsran_amd] %s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));                 \
+      return MI355_ERROR;                                                                                              \
+    }                                                                                                                  \
+  } while (0)
+
+namespace {
+
+int cb_index(uint32_t K)
+{
+  for (int i = 0; i < LTE_NOF_CB_SIZES; i++) {
+    if (lte_qpp_table[i][0] == K) return i;
+    if (lte_qpp_table[i][0] > K) break;
+  }
+  return -1;
+}
+
+uint32_t round_up(uint32_t v, uint32_t m) { return (v + m - 1) / m * m; }
+
+struct KTables {
+  uint32_t* dstE = nullptr; // window mode
+  uint32_t* dstA = nullptr;
+  uint16_t* pi   = nullptr; // generic mode
+};
+
+struct Geometry {
+  uint32_t K, nsb, L, Lp, nl, nseg; // window mode (nsb > 0)
+  uint32_t npair, Kp;               // generic mode (nsb == 0)
+};
+
+Geometry geometry(uint32_t K, uint32_t ncb)
+{
+  Geometry g{};
+  g.K   = K;
+  g.nsb = mi355_tdec_autoimp_get_subblocks(K);
+  if (g.nsb) {
+    g.L    = K / g.nsb;
+    g.Lp   = round_up(g.L, TDEC_SEG);
+    g.nl   = g.nsb / 2;
+    g.nseg = (g.L + TDEC_SEG - 1) / TDEC_SEG;
+  } else {
+    g.npair = (ncb + 1) / 2;
+    g.Kp    = round_up(K + 3, TDEC_SEG);
+    g.nseg  = (K + TDEC_SEG - 1) / TDEC_SEG;
+  }
+  return g;
+}
+
+} // namespace
+
+struct mi355_tdec_batch {
+  int                          device = 0;
+  hipStream_t                  own    = nullptr;
+  char*                        ws     = nullptr;
+  size_t                       ws_cap = 0;
+  std::map<uint32_t, KTables>  tables;
+  bool                         prof = false;
+  std::vector<hipEvent_t>      ev;
+  size_t                       ev_used = 0;
+  std::mutex                   mu;
+};
+
+static int get_tables(mi355_tdec_batch_t* q, const Geometry& g, KTables** out)
+{
+  auto it = q->tables.find(g.K);
+  if (it != q->tables.end()) {
+    *out = &it->second;
+    return MI355_SUCCESS;
+  }
+  const uint32_t K   = g.K;
+  const int      idx = cb_index(K);
+  if (idx < 0) return MI355_ERROR_INVALID_INPUTS;
+  const uint64_t        f1 = lte_qpp_table[idx][1], f2 = lte_qpp_table[idx][2];
+  std::vector<uint16_t> pi(K), inv(K);
+  for (uint64_t m = 0; m < K; m++) {
+    pi[m]       = (uint16_t)((f1 * m + f2 * m * m) % K);
+    inv[pi[m]]  = (uint16_t)m;
+  }
+  KTables t;
+  if (g.nsb) {
+    auto off = [&](uint32_t p) -> uint32_t {
+      uint32_t w = p / g.L, j = p % g.L;
+      return ((w >> 1) * g.Lp + j) * 2 + (w & 1);
+    };
+    std::vector<uint32_t> dE((size_t)g.nl * g.Lp, 0), dA((size_t)g.nl * g.Lp, 0);
+    for (uint32_t l = 0; l < g.nl; l++) {
+      for (uint32_t j = 0; j < g.L; j++) {
+        uint32_t n0 = (2 * l) * g.L + j, n1 = (2 * l + 1) * g.L + j;
+        dE[(size_t)l * g.Lp + j] = off(inv[n0]) | (off(inv[n1]) << 16);
+        dA[(size_t)l * g.Lp + j] = off(pi[n0]) | (off(pi[n1]) << 16);
+      }
+    }
+    CHECK_HIP(hipMalloc(&t.dstE, dE.size() * 4));
+    CHECK_HIP(hipMalloc(&t.dstA, dA.size() * 4));
+    CHECK_HIP(hipMemcpy(t.dstE, dE.data(), dE.size() * 4, hipMemcpyHostToDevice));
+    CHECK_HIP(hipMemcpy(t.dstA, dA.data(), dA.size() * 4, hipMemcpyHostToDevice));
+  } else {
+    std::vector<uint16_t> both(pi);
+    both.insert(both.end(), inv.begin(), inv.end());
+    CHECK_HIP(hipMalloc(&t.pi, 2 * K * 2));
+    CHECK_HIP(hipMemcpy(t.pi, both.data(), 2 * K * 2, hipMemcpyHostToDevice));
+  }
+  auto r = q->tables.emplace(K, t);
+  *out   = &r.first->second;
+  return MI355_SUCCESS;
+}
+
+static size_t ws_bytes(const Geometry& g, uint32_t n)
+{
+  if (g.nsb) {
+    const size_t arr = (size_t)n * g.nl * g.Lp * 4;
+    return 6 * arr + round_up(n * 12 * 2, 256) + (size_t)n * g.nl * g.nseg * 32 + 6 * 256;
+  }
+  const size_t arr = (size_t)g.npair * g.Kp * 4;
+  return 6 * arr + (size_t)g.npair * 16 + (size_t)g.npair * g.nseg * 32 + 8 * 256;
+}
+
+static int ensure_ws(mi355_tdec_batch_t* q, size_t bytes)
+{
+  if (bytes <= q->ws_cap) return MI355_SUCCESS;
+  if (q->ws) {
+    CHECK_HIP(hipDeviceSynchronize());
+    CHECK_HIP(hipFree(q->ws));
+    q->ws = nullptr;
+  }
+  size_t cap = bytes + bytes / 8;
+  CHECK_HIP(hipMalloc(&q->ws, cap));
+  q->ws_cap = cap;
+  return MI355_SUCCESS;
+}
+
+static hipEvent_t next_event(mi355_tdec_batch_t* q)
+{
+  if (q->ev_used == q->ev.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    q->ev.push_back(e);
+  }
+  return q->ev[q->ev_used++];
+}
+
+extern "C" {
+
+uint32_t mi355_tdec_autoimp_get_subblocks(uint32_t long_cb)
+{
+  if (!(long_cb % 16) && long_cb > 800) return 16;
+  if (!(long_cb % 8) && long_cb > 400) return 8;
+  return 0;
+}
+
+int mi355_tdec_batch_create(mi355_tdec_batch_t** q, int device)
+{
+  if (!q) return MI355_ERROR_INVALID_INPUTS;
+  int ndev = 0;
+  CHECK_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return MI355_ERROR_INVALID_INPUTS;
+  CHECK_HIP(hipSetDevice(device));
+  auto* b   = new mi355_tdec_batch;
+  b->device = device;
+  if (hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking) != hipSuccess) {
+    delete b;
+    return MI355_ERROR;
+  }
+  *q = b;
+  return MI355_SUCCESS;
+}
+
+void mi355_tdec_batch_destroy(mi355_tdec_batch_t* q)
+{
+  if (!q) return;
+  (void)hipSetDevice(q->device);
+  (void)hipDeviceSynchronize();
+  for (auto& kv : q->tables) {
+    (void)hipFree(kv.second.dstE);
+    (void)hipFree(kv.second.dstA);
+    (void)hipFree(kv.second.pi);
+  }
+  for (auto e : q->ev) (void)hipEventDestroy(e);
+  if (q->ws) (void)hipFree(q->ws);
+  if (q->own) (void)hipStreamDestroy(q->own);
+  delete q;
+}
+
+void mi355_tdec_batch_set_profiling(mi355_tdec_batch_t* q, int enable)
+{
+  if (q) q->prof = enable != 0;
+}
+
+int mi355_tdec_batch_kernel_stats(mi355_tdec_batch_t* q, double* ms, uint32_t* launches)
+{
+  if (!q) return MI355_ERROR_INVALID_INPUTS;
+  double total = 0;
+  for (size_t i = 0; i + 1 < q->ev_used; i += 2) {
+    CHECK_HIP(hipEventSynchronize(q->ev[i + 1]));
+    float t = 0;
+    CHECK_HIP(hipEventElapsedTime(&t, q->ev[i], q->ev[i + 1]));
+    total += t;
+  }
+  if (ms) *ms = total;
+  if (launches) *launches = (uint32_t)(q->ev_used / 2);
+  q->ev_used = 0;
+  return MI355_SUCCESS;
+}
+
+int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
+                             const int16_t*      d_in,
+                             size_t              in_stride,
+                             uint32_t            n,
+                             uint32_t            K,
+                             uint32_t            nhalf,
+                             uint8_t*            d_out,
+                             size_t              out_stride,
+                             void*               stream)
+{
+  if (!q || !d_in || !d_out || nhalf == 0 || cb_index(K) < 0) return MI355_ERROR_INVALID_INPUTS;
+  if (in_stride < 3 * (size_t)(K + 32) + 12 || (in_stride & 1) || out_stride < K / 8) {
+    return MI355_ERROR_INVALID_INPUTS;
+  }
+  if (n == 0) return MI355_SUCCESS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t s = stream ? (hipStream_t)stream : q->own;
+
+  const Geometry g = geometry(K, n);
+  KTables*       t = nullptr;
+  int            r = get_tables(q, g, &t);
+  if (r) return r;
+  if ((r = ensure_ws(q, ws_bytes(g, n)))) return r;
+
+  char* p     = q->ws;
+  auto  carve = [&](size_t bytes) {
+    char* c = p;
+    p += ((bytes + 255) / 256) * 256;
+    return c;
+  };
+
+  if (g.nsb) {
+    const size_t arr = (size_t)n * g.nl * g.Lp * 4;
+    auto*        S   = (uint32_t*)carve(arr);
+    auto*        P0  = (uint32_t*)carve(arr);
+    auto*        P1  = (uint32_t*)carve(arr);
+    auto*        A1  = (uint32_t*)carve(arr);
+    auto*        E   = (uint32_t*)carve(arr);
+    auto*        D   = (uint32_t*)carve(arr);
+    auto*        T   = (int16_t*)carve((size_t)n * 12 * 2);
+    auto*        CK  = (uint32_t*)carve((size_t)n * g.nl * g.nseg * 32);
+
+    TdecPrepArgs pa{d_in, in_stride, S, P0, P1, T, (int)n, (int)g.L, (int)g.Lp};
+    CHECK_HIP(tdec_win_launch_prep(g.nsb, pa, s));
+    for (uint32_t h = 0; h < nhalf; h++) {
+      TdecWinArgs wa{S, P0, P1, A1, E, D, T, CK, t->dstE, t->dstA,
+                     (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == nhalf};
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      if (q->prof) {
+        e0 = next_event(q);
+        e1 = next_event(q);
+        if (e0) (void)hipEventRecord(e0, s);
+      }
+      CHECK_HIP(tdec_win_launch_halfit(g.nsb, wa, s));
+      if (q->prof && e1) (void)hipEventRecord(e1, s);
+    }
+    TdecDecideArgs da{D, d_out, out_stride, (int)n, (int)g.L, (int)g.Lp};
+    CHECK_HIP(tdec_win_launch_decide(g.nsb, da, s));
+  } else {
+    const size_t arr = (size_t)g.npair * g.Kp * 4;
+    auto*        S   = (uint32_t*)carve(arr);
+    auto*        P0  = (uint32_t*)carve(arr);
+    auto*        P1  = (uint32_t*)carve(arr);
+    auto*        A1  = (uint32_t*)carve(arr);
+    auto*        E   = (uint32_t*)carve(arr);
+    auto*        D   = (uint32_t*)carve(arr);
+    auto*        CK  = (uint32_t*)carve((size_t)g.npair * g.nseg * 32);
+
+    TdecGenPrepArgs pa{d_in, in_stride, S, P0, P1, E, (int)n, (int)g.npair, (int)K, (int)g.Kp};
+    CHECK_HIP(tdec_gen_launch_prep(pa, s));
+    for (uint32_t h = 0; h < nhalf; h++) {
+      TdecGenArgs ga{S, P0, P1, A1, E, D, CK, t->pi,
+                     (int)g.npair, (int)K, (int)g.Kp, (int)g.nseg, (int)h, h + 1 == nhalf};
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      if (q->prof) {
+        e0 = next_event(q);
+        e1 = next_event(q);
+        if (e0) (void)hipEventRecord(e0, s);
+      }
+      CHECK_HIP(tdec_gen_launch_halfit(ga, s));
+      if (q->prof && e1) (void)hipEventRecord(e1, s);
+    }
+    TdecGenDecideArgs da{D, d_out, out_stride, (int)n, (int)K, (int)g.Kp};
+    CHECK_HIP(tdec_gen_launch_decide(da, s));
+  }
+  return MI355_SUCCESS;
+}
+
+int mi355_tdec_batch_run(mi355_tdec_batch_t* q,
+                         const int16_t*      in,
+                         size_t              in_stride,
+                         uint32_t            n,
+                         uint32_t            K,
+                         uint32_t            nhalf,
+                         uint8_t*            out,
+                         size_t              out_stride)
+{
+  if (!q || !in || !out) return MI355_ERROR_INVALID_INPUTS;
+  if (n == 0) return MI355_SUCCESS;
+  CHECK_HIP(hipSetDevice(q->device));
+  int16_t* din  = nullptr;
+  uint8_t* dout = nullptr;
+  CHECK_HIP(hipMalloc(&din, (size_t)n * in_stride * 2));
+  CHECK_HIP(hipMalloc(&dout, (size_t)n * out_stride));
+  CHECK_HIP(hipMemcpyAsync(din, in, (size_t)n * in_stride * 2, hipMemcpyHostToDevice, q->own));
+  int r = mi355_tdec_batch_run_dev(q, din, in_stride, n, K, nhalf, dout, out_stride, q->own);
+  if (r == MI355_SUCCESS) {
+    CHECK_HIP(hipMemcpyAsync(out, dout, (size_t)n * out_stride, hipMemcpyDeviceToHost, q->own));
+    CHECK_HIP(hipStreamSynchronize(q->own));
+  }
+  (void)hipFree(din);
+  (void)hipFree(dout);
+  return r;
+}
+
+void* mi355_dev_alloc(size_t bytes, int device)
+{
+  void* p = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  return p;
+}
+
+void mi355_dev_free(void* p)
+{
+  if (p) (void)hipFree(p);
+}
+
+int mi355_memcpy_h2d(void* dst, const void* src, size_t bytes)
+{
+  CHECK_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return MI355_SUCCESS;
+}
+
+int mi355_memcpy_d2h(void* dst, const void* src, size_t bytes)
+{
+  CHECK_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return MI355_SUCCESS;
+}
+
+int mi355_memset_dev(void* dst, int value, size_t bytes)
+{
+  CHECK_HIP(hipMemset(dst, value, bytes));
+  return MI355_SUCCESS;
+}
+
+int mi355_device_sync(void)
+{
+  CHECK_HIP(hipDeviceSynchronize());
+  return MI355_SUCCESS;
+}
+
+int mi355_device_count(void)
+{
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+} // extern "C"

@@ -1,0 +1,139 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors in tests/golden/ from the srsLTE reference compiled from its own
+sources (``make -C oracle ref`` -> oracle/_ref/libsrslte_ref.so).  Run in the survey container only
+(needs /root/reference); the resulting .npz files are committed and are the parity anchor on the GPU box.
+
+    python tests/golden/make_golden.py
+
+Contents
+  tdec_auto.npz      AUTO-mode decoder (generic / 8-window / 16-window by K): inputs in the softbuffer
+                     layout, decision bytes after every half-iteration 1..8 (srslte_tdec_iteration),
+                     including failing code blocks, saturating and full-range int16 inputs.
+  tdec_generic.npz   GENERIC manual decoder + force_not_sb on linear input (turbodecoder_test -d 1).
+  tcod_known.npz     the reference test's own known-answer vector (turbodecoder_test.h:69-125).
+  crc_cbsegm.npz     CRC24A/24B/16/8 checksums and CB segmentation for a TBS sweep.
+"""
+from __future__ import annotations
+
+import os
+import re
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import oracle  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+REF_TEST_H = "/root/reference/lib/src/phy/fec/test/turbodecoder_test.h"
+NHALF = 8
+
+
+def gen_tdec_auto(rng):
+    ref = oracle.RefTdec()
+    cases = []
+    # (K, kind, ebno)  kind: awgn (scale 100 as turbodecoder_test), big (scale 4000 -> saturation),
+    #                        rand (uniform full-range int16 -> saturation + wrap everywhere)
+    Ks = [40, 104, 400, 408, 512, 800, 816, 1024, 1056, 2048, 5312, 6144]
+    for K in Ks:
+        cases += [(K, "awgn", 0.5), (K, "awgn", 4.0)]
+    cases += [(6144, "big", 2.0), (512, "big", 2.0), (200, "big", 2.0),
+              (6144, "rand", 0.0), (512, "rand", 0.0), (104, "rand", 0.0)]
+    data = {}
+    for ci, (K, kind, eb) in enumerate(cases):
+        if kind == "rand":
+            bits = np.zeros(K, np.uint8)
+            lin = rng.integers(-32768, 32768, 3 * K + 12, dtype=np.int16)
+            buf = oracle.tdec_pack_input(lin, K)
+        else:
+            bits, lin, buf = oracle.make_cb(rng, K, eb, scale=100.0 if kind == "awgn" else 4000.0)
+        out, tr = ref.run(buf, K, NHALF, trace=True)
+        data[f"c{ci}_K"] = np.int32(K)
+        data[f"c{ci}_kind"] = np.array(kind)
+        data[f"c{ci}_ebno"] = np.float32(eb)
+        data[f"c{ci}_bits"] = bits
+        data[f"c{ci}_buf"] = buf
+        data[f"c{ci}_trace"] = tr
+    data["ncases"] = np.int32(len(cases))
+    data["nhalf"] = np.int32(NHALF)
+    np.savez_compressed(os.path.join(OUT, "tdec_auto.npz"), **data)
+    print("tdec_auto.npz:", len(cases), "cases")
+
+
+def gen_tdec_generic(rng):
+    ref = oracle.RefTdec(generic=True)
+    data = {}
+    cases = [(6144, 6.0), (6144, 1.0), (1024, 1.0)]
+    for ci, (K, eb) in enumerate(cases):
+        bits, lin, _ = oracle.make_cb(rng, K, eb)
+        buf = np.zeros(oracle.tdec_buf_len(K), np.int16)
+        buf[: 3 * K + 12] = lin
+        out, tr = ref.run(buf, K, NHALF, trace=True)
+        data[f"c{ci}_K"] = np.int32(K)
+        data[f"c{ci}_lin"] = lin
+        data[f"c{ci}_bits"] = bits
+        data[f"c{ci}_trace"] = tr
+    data["ncases"] = np.int32(len(cases))
+    np.savez_compressed(os.path.join(OUT, "tdec_generic.npz"), **data)
+    print("tdec_generic.npz:", len(cases), "cases")
+
+
+def gen_tcod_known():
+    """The reference's own fixture: 504 info bits and their 1524 coded bits."""
+    txt = open(REF_TEST_H).read()
+
+    def arr(name):
+        m = re.search(name + r"\[[A-Z_0-9 *+]*\]\s*=\s*\{([^}]*)\}", txt)
+        return np.array([int(v) for v in m.group(1).replace("\n", " ").split(",") if v.strip()], np.uint8)
+
+    kd, kde = arr("known_data"), arr("known_data_encoded")
+    assert kd.size == 504 and kde.size == 3 * 504 + 12, (kd.size, kde.size)
+    # cross-check with the compiled reference encoder
+    out = np.zeros(kde.size, np.uint8)
+    oracle.ref().ref_tcod_encode(kd.copy(), out, 504)
+    # Finding: the fixture differs from the reference encoder (srslte_tcod_encode) in exactly one bit,
+    # index 1512 = the first tail bit x_K.  turbodecoder_test -k only feeds the fixture to the decoder
+    # and never compares it with the encoder, so the discrepancy is latent in the reference.
+    diff = np.nonzero(out != kde)[0]
+    assert list(diff) == [1512], diff
+    np.savez_compressed(os.path.join(OUT, "tcod_known.npz"), known_data=kd, known_data_encoded=kde,
+                        ref_encoder_out=out, fixture_vs_encoder_diff=diff.astype(np.int32))
+    print("tcod_known.npz")
+
+
+def gen_crc_cbsegm(rng):
+    L = oracle.ref()
+    polys = {"crc24a": (0x1864CFB, 24), "crc24b": (0x1800063, 24), "crc16": (0x11021, 16), "crc8": (0x19B, 8)}
+    data = {}
+    msgs = [rng.integers(0, 256, n, dtype=np.uint8) for n in (1, 3, 5, 64, 768, 12243)]
+    for i, m in enumerate(msgs):
+        data[f"msg{i}"] = m
+        for name, (p, o) in polys.items():
+            data[f"msg{i}_{name}"] = np.uint32(L.ref_crc_byte(p, o, m.copy(), 8 * m.size))
+    data["nmsg"] = np.int32(len(msgs))
+    tbs = np.array([0, 16, 40, 104, 1000, 6120, 6144, 6168, 15840, 30576, 75376, 97896, 149776, 391656], np.uint32)
+    seg = np.zeros((tbs.size, 6), np.uint32)
+    for i, t in enumerate(tbs):
+        r = np.zeros(6, np.uint32)
+        assert L.ref_cbsegm(int(t), r) == 0
+        seg[i] = r
+    data["tbs"] = tbs
+    data["cbsegm"] = seg
+    np.savez_compressed(os.path.join(OUT, "crc_cbsegm.npz"), **data)
+    print("crc_cbsegm.npz")
+
+
+def main():
+    oracle.build(ref=True)
+    if not oracle.ref_available():
+        sys.exit("oracle/_ref/libsrslte_ref.so is not available (needs /root/reference)")
+    rng = np.random.default_rng(20201010)
+    gen_tdec_auto(rng)
+    gen_tdec_generic(rng)
+    gen_tcod_known()
+    gen_crc_cbsegm(rng)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,62 @@
+"""CPU: the oracle (our scalar C restatement) against the reference's golden vectors.
+
+This pins the checker itself before any GPU result is compared with it."""
+import numpy as np
+import pytest
+
+import oracle
+from golden_io import load, tdec_auto_cases, tdec_generic_cases
+
+
+@pytest.mark.parametrize("case", tdec_auto_cases(), ids=lambda c: f"K{c['K']}-{c['kind']}-{c['ebno']}")
+def test_oracle_tdec_auto_matches_reference_every_half_iteration(case):
+    K = case["K"]
+    out, tr = oracle.tdec_run(case["buf"], K, case["trace"].shape[0], trace=True)
+    np.testing.assert_array_equal(tr, case["trace"])
+    np.testing.assert_array_equal(out, case["trace"][-1])
+
+
+@pytest.mark.parametrize("case", tdec_generic_cases(), ids=lambda c: f"K{c['K']}")
+def test_oracle_tdec_generic_matches_reference(case):
+    out = oracle.tdec_run_generic(case["lin"], case["K"], case["trace"].shape[0])
+    np.testing.assert_array_equal(out, case["trace"][-1])
+
+
+def test_golden_decodes_at_high_snr():
+    # sanity of the fixtures themselves: the 4 dB (test units) AWGN cases are (nearly) error-free
+    for c in tdec_auto_cases():
+        if c["kind"] == "awgn" and c["ebno"] >= 4.0:
+            assert np.mean(np.unpackbits(c["trace"][-1]) != c["bits"]) < 0.05, c["K"]
+
+
+def test_tcod_known_answer():
+    z = load("tcod_known.npz")
+    enc = oracle.tcod_encode(z["known_data"], 504)
+    np.testing.assert_array_equal(enc, z["ref_encoder_out"])
+    # the reference's fixture differs from the reference encoder only in the first tail bit
+    diff = np.nonzero(enc != z["known_data_encoded"])[0]
+    assert list(diff) == list(z["fixture_vs_encoder_diff"]) == [1512]
+
+
+def test_crc_and_cbsegm():
+    z = load("crc_cbsegm.npz")
+    polys = {"crc24a": oracle.CRC24A, "crc24b": oracle.CRC24B, "crc16": oracle.CRC16, "crc8": oracle.CRC8}
+    for i in range(int(z["nmsg"])):
+        m = z[f"msg{i}"]
+        for name, po in polys.items():
+            assert oracle.crc(m, 8 * m.size, po) == int(z[f"msg{i}_{name}"]), (i, name)
+    for t, row in zip(z["tbs"], z["cbsegm"]):
+        s = oracle.cbsegm(int(t))
+        assert [s[k] for k in ("C", "K1", "K2", "C1", "C2", "F")] == [int(v) for v in row], t
+
+
+def test_qpp_is_permutation_and_contention_free():
+    for K in oracle.cb_sizes():
+        pi = oracle.qpp(K).astype(np.int64)
+        assert np.array_equal(np.sort(pi), np.arange(K))
+        nsb = oracle.tdec_nsb(K)
+        if nsb:
+            L = K // nsb
+            w = np.arange(nsb)
+            for j in range(0, L, max(1, L // 7)):
+                assert len(set(pi[w * L + j] // L)) == nsb  # windows read distinct windows
