@@ -10,28 +10,18 @@
 
 namespace mi355 {
 
-// Packed lane-major layout of one window-mode code block (DESIGN.md "HBM layout"):
-//   u32 [NL = NSB/2 lanes][Lp steps]; low int16 = window 2l, high int16 = window 2l+1.
+// Wave-group interleaved layout (DESIGN.md "HBM layout"): G = 64/NL code blocks per group,
+//   u32 [group][Lp steps][64 lanes], lane q = cbg*NL + l; low int16 = window 2l, high = window 2l+1.
 struct TdecWinArgs {
-  const uint32_t* S;    // systematic
-  const uint32_t* P0;   // parity 1
-  const uint32_t* P1;   // parity 2 (interleaved order)
-  uint32_t*       A1;   // a-priori of DEC1 (natural order)
-  uint32_t*       E;    // DEC1 extrinsic -> DEC2 input (interleaved order)
-  uint32_t*       D;    // decision LLRs (natural order)
-  const int16_t*  T;    // 12 tail LLRs per code block (encoder order)
-  uint32_t*       ckpt; // [cb][l][nseg][8] beta checkpoints
-  const uint32_t* dstE; // [NL][Lp] (lo,hi) int16 offsets: natural -> interleaved position
-  const uint32_t* dstA; // [NL][Lp] (lo,hi) int16 offsets: interleaved -> natural position
+  const int16_t*  in;   // caller's decoder buffers (softbuffer layout), in_stride int16 apart
+  size_t          in_stride;
+  uint32_t*       A1;   // a-priori of DEC1 (natural order), wave-group interleaved
+  uint32_t*       E;    // DEC1 extrinsic -> DEC2 input (interleaved order), wave-group interleaved
+  uint32_t*       D;    // decision LLRs (natural order), wave-group interleaved
+  uint32_t*       ckpt; // [group][nseg][8][64] beta checkpoints
+  const uint32_t* dstE; // [L][NL] j' | wlo<<16 | whi<<24 : natural -> interleaved destination
+  const uint32_t* dstA; // [L][NL] same, interleaved -> natural
   int             ncb, L, Lp, nseg, n, write_d;
-};
-
-struct TdecPrepArgs {
-  const int16_t* in;  // softbuffer-layout inputs
-  size_t         stride;
-  uint32_t *     S, *P0, *P1;
-  int16_t*       T;
-  int            ncb, L, Lp;
 };
 
 struct TdecDecideArgs {
@@ -68,7 +58,6 @@ struct TdecGenDecideArgs {
   int             ncb, K, Kp;
 };
 
-hipError_t tdec_win_launch_prep(int nsb, const TdecPrepArgs& a, hipStream_t s);
 hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s);
 hipError_t tdec_win_launch_decide(int nsb, const TdecDecideArgs& a, hipStream_t s);
 hipError_t tdec_gen_launch_prep(const TdecGenPrepArgs& a, hipStream_t s);

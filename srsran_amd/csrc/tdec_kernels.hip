@@ -113,54 +113,80 @@ __device__ __forceinline__ void set_minf(v2s s[8])
 }
 
 // ---------------------------------------------------------------------------- window MAP kernel
+//
+// HBM layout ("wave-group interleaved"): code blocks are grouped G = 64/NL at a time so
+// that one wave owns one group; every array is u32 [group][step j (Lp)][64 lanes], lane q = cbg*NL + l
+// holding windows (2l, 2l+1) of code block cbg.  A wave's access to step j of any array is therefore
+// one contiguous 256-byte row, and -- because the QPP interleaver is contention-free for windows of
+// length L (pi(m) mod L depends on m mod L only) -- the 2*NL interleaved outputs of a code block at
+// step j all land in ONE destination row j' as well: the interleaver scatter stays inside a 256-byte
+// row per wave and store instruction.
+
+#define WG_AT(arr, j) (arr)[((size_t)grp * Lp + (j)) * 64 + q]
 
 template <int NSB, int SEG>
 __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
 {
   constexpr int NL = NSB / 2;
-  const int     g  = blockIdx.x * blockDim.x + threadIdx.x;
-  const int     cb = g / NL;
-  const int     l  = g % NL;
-  if (cb >= a.ncb) return;
+  constexpr int G  = 64 / NL;
+  const int     gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int     grp = gl >> 6, q = gl & 63;
+  const int     cbg = q / NL, l = q % NL;
+  if (grp * G + cbg >= a.ncb) return;
 
-  const int  L = a.L, Lp = a.Lp, K = L * NSB, nseg = a.nseg, n = a.n;
+  const int  L = a.L, Lp = a.Lp, nseg = a.nseg, n = a.n;
   const bool dec2   = n & 1;
   const bool has_ap = !dec2 && n > 0;
 
-  const size_t    cbase = (size_t)cb * NL * Lp;   // u32 units
-  const size_t    row   = cbase + (size_t)l * Lp;
-  const int       ln    = (l + 1 < NL) ? l + 1 : l;  // neighbour lanes (clamped; value unused)
-  const int       lp    = (l > 0) ? l - 1 : 0;
-  const uint32_t* X     = dec2 ? a.E : a.S;
-  const uint32_t* Y     = dec2 ? a.P1 : a.P0;
-  const uint32_t* AP    = a.A1;
-  const uint32_t* Xr    = X + row;
-  const uint32_t* Yr    = Y + row;
-  const uint32_t* Ar    = AP + row;
-  uint32_t*       ck    = a.ckpt + ((size_t)cb * NL + l) * nseg * 8;
+  // Inputs are read straight from the caller's softbuffer-layout buffers (rm_turbo.c:263-277): stream s
+  // of code block cb at u32 offset s*(K+32)/2, step j of lane l at j*NL + l -- a 32-byte row per code
+  // block and step.  DEC2's systematic input (e) and DEC1's a-priori (a1) live in the wave-group
+  // interleaved workspace.  Both are addressed as base[j*stride + lane offset], so a neighbour lane's
+  // value is always base[... + 1].
+  const int       cb   = grp * G + cbg;
+  const int       K    = L * NSB;
+  const uint32_t* in32 = (const uint32_t*)(a.in + (size_t)cb * a.in_stride);
+  const size_t    wg0  = (size_t)grp * Lp * 64 + q;
+  const uint32_t* X    = dec2 ? a.E + wg0 : in32 + l;
+  const int       xs   = dec2 ? 64 : NL;
+  const uint32_t* Y    = in32 + (dec2 ? (K + 32) : (K + 32) / 2) + l;
+  const uint32_t* AP   = a.A1 + wg0;
+  uint32_t*       ck   = a.ckpt + (size_t)grp * nseg * 8 * 64 + q;
 
   v2s st[8], nw[8];
 
   // ------------------------------------------------ backward pass: boundary (row L)
-  // warm-up: 40 steps over the first 40 steps of the NEXT window, from -INF (turbodecoder_win.h:566-631)
+  // warm-up over the first 40 steps of the NEXT window (lane q+1 holds windows 2l+2, 2l+3), from -INF
+  // (turbodecoder_win.h:566-631).  The neighbour value of lane NL-1 belongs to another code block and
+  // is discarded below (the last window's boundary comes from the tail trellis).
   set_minf(st);
-  {
-    const uint32_t* Xn = X + cbase + (size_t)ln * Lp;
-    const uint32_t* Yn = Y + cbase + (size_t)ln * Lp;
-    const uint32_t* An = AP + cbase + (size_t)ln * Lp;
-    for (int k = TDEC_WARMUP - 1; k >= 0; k--) {
-      v2s x = U(hi_lo(Xr[k], Xn[k]));
-      v2s y = U(hi_lo(Yr[k], Yn[k]));
-      if (has_ap) x = sadd(x, U(hi_lo(Ar[k], An[k])));
-      beta_step<true>(st, x, y, nw);
+#pragma unroll 1
+  for (int b = TDEC_WARMUP / 8 - 1; b >= 0; b--) {
+    uint32_t xo[8], xn[8], yo[8], yn[8], ao[8], an[8];
 #pragma unroll
-      for (int i = 0; i < 8; i++) st[i] = nw[i];
+    for (int i = 0; i < 8; i++) {
+      const int j = 8 * b + i;
+      xo[i]       = X[j * xs];
+      xn[i]       = X[j * xs + 1];
+      yo[i]       = Y[j * NL];
+      yn[i]       = Y[j * NL + 1];
+      ao[i]       = has_ap ? AP[j * 64] : 0u;
+      an[i]       = has_ap ? AP[j * 64 + 1] : 0u;
+    }
+#pragma unroll
+    for (int i = 7; i >= 0; i--) {
+      const int k = 8 * b + i;
+      v2s       x = U(hi_lo(xo[i], xn[i]));
+      if (has_ap) x = sadd(x, U(hi_lo(ao[i], an[i])));
+      beta_step<true>(st, x, U(hi_lo(yo[i], yn[i])), nw);
+#pragma unroll
+      for (int s = 0; s < 8; s++) st[s] = nw[s];
       if ((k & 1) == 0 && k != 0) normalize<true>(st);
     }
   }
   if (l == NL - 1) {
     // last window: tail trellis, wrapping arithmetic, no a-priori (turbodecoder_win.h:500-548)
-    const int16_t* T = a.T + (size_t)cb * 12 + (dec2 ? 6 : 0);
+    const int16_t* T = a.in + (size_t)cb * a.in_stride + 3 * (K + 32) + (dec2 ? 6 : 0);
     v2s            tr[8], tn[8];
     tr[0] = splat(0);
 #pragma unroll
@@ -175,56 +201,76 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
     for (int i = 0; i < 8; i++) st[i] = (v2s){st[i].x, tr[i].y};
   }
   // ckpt[nseg-1] = row L (not normalised)
-  {
-    uint4* c = (uint4*)(ck + (size_t)(nseg - 1) * 8);
-    c[0]     = make_uint4(W(st[0]), W(st[1]), W(st[2]), W(st[3]));
-    c[1]     = make_uint4(W(st[4]), W(st[5]), W(st[6]), W(st[7]));
-  }
+#pragma unroll
+  for (int s = 0; s < 8; s++) ck[((size_t)(nseg - 1) * 8 + s) * 64] = W(st[s]);
 
-  // ------------------------------------------------ backward pass: main, checkpoint every SEG rows
-  for (int c4 = (L - 1) >> 2; c4 >= 0; c4--) {
-    const uint4 xv = *(const uint4*)(Xr + 4 * c4);
-    const uint4 yv = *(const uint4*)(Yr + 4 * c4);
-    uint4       av = make_uint4(0, 0, 0, 0);
-    if (has_ap) av = *(const uint4*)(Ar + 4 * c4);
-    const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w};
-    const uint32_t ys[4] = {yv.x, yv.y, yv.z, yv.w};
-    const uint32_t as[4] = {av.x, av.y, av.z, av.w};
+  // ------------------------------------------------ backward pass: main, one checkpoint per segment
+  {
+    uint32_t cx[SEG], cy[SEG], ca[SEG];
+    auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap) {
 #pragma unroll
-    for (int i = 3; i >= 0; i--) {
-      const int k = 4 * c4 + i;
-      if (k < L) {
-        v2s x = U(xs[i]);
-        if (has_ap) x = sadd(x, U(as[i]));
-        beta_step<true>(st, x, U(ys[i]), nw);
+      for (int i = 0; i < SEG; i++) {
+        const int j = min(t * SEG + i, L - 1); // clamp the ragged last segment (values unused)
+        x[i]        = X[j * xs];
+        y[i]        = Y[j * NL];
+        ap[i]       = has_ap ? AP[j * 64] : 0u;
+      }
+    };
+    load(nseg - 1, cx, cy, ca);
+#pragma unroll 1
+    for (int t = nseg - 1; t >= 0; t--) {
+      uint32_t nx[SEG], ny[SEG], na[SEG];
+      if (t > 0) load(t - 1, nx, ny, na);
 #pragma unroll
-        for (int s = 0; s < 8; s++) st[s] = nw[s];
-        if (k % SEG == 0 && k != 0) {
-          uint4* c = (uint4*)(ck + (size_t)(k / SEG - 1) * 8);
-          c[0]     = make_uint4(W(st[0]), W(st[1]), W(st[2]), W(st[3]));
-          c[1]     = make_uint4(W(st[4]), W(st[5]), W(st[6]), W(st[7]));
+      for (int i = SEG - 1; i >= 0; i--) {
+        const int k = t * SEG + i;
+        if (k < L) {
+          v2s x = U(cx[i]);
+          if (has_ap) x = sadd(x, U(ca[i]));
+          beta_step<true>(st, x, U(cy[i]), nw);
+#pragma unroll
+          for (int s = 0; s < 8; s++) st[s] = nw[s];
+          if (i == 0 && t > 0) {
+#pragma unroll
+            for (int s = 0; s < 8; s++) ck[((size_t)(t - 1) * 8 + s) * 64] = W(st[s]);
+          }
+          if ((i & 1) == 0 && k != 0) normalize<true>(st);
         }
-        if ((k & 1) == 0 && k != 0) normalize<true>(st);
+      }
+#pragma unroll
+      for (int i = 0; i < SEG; i++) {
+        cx[i] = nx[i];
+        cy[i] = ny[i];
+        ca[i] = na[i];
       }
     }
   }
 
   // ------------------------------------------------ forward pass: boundary at the window start
-  // warm-up over the LAST 40 steps of the PREVIOUS window (turbodecoder_win.h:705-757)
+  // warm-up over the LAST 40 steps of the PREVIOUS window (lane q-1), turbodecoder_win.h:705-757
   set_minf(st);
-  {
-    const uint32_t* Xq = X + cbase + (size_t)lp * Lp;
-    const uint32_t* Yq = Y + cbase + (size_t)lp * Lp;
-    const uint32_t* Aq = AP + cbase + (size_t)lp * Lp;
-    for (int k = 0; k < TDEC_WARMUP; k++) {
-      const int j = L - TDEC_WARMUP + k;
-      v2s       x = U(hi_lo(Xq[j], Xr[j]));
-      v2s       y = U(hi_lo(Yq[j], Yr[j]));
-      if (has_ap) x = sadd(x, U(hi_lo(Aq[j], Ar[j])));
-      v2s c0[8], c1[8];
-      alpha_cands<true>(st, x, y, c0, c1);
+#pragma unroll 1
+  for (int b = 0; b < TDEC_WARMUP / 8; b++) {
+    uint32_t xo[8], xp[8], yo[8], yp[8], ao[8], ap_[8];
 #pragma unroll
-      for (int i = 0; i < 8; i++) st[i] = vmax(c0[i], c1[i]);
+    for (int i = 0; i < 8; i++) {
+      const int j = (L - TDEC_WARMUP) + 8 * b + i;
+      xo[i]       = X[j * xs];
+      xp[i]       = X[j * xs - 1];
+      yo[i]       = Y[j * NL];
+      yp[i]       = Y[j * NL - 1];
+      ao[i]       = has_ap ? AP[j * 64] : 0u;
+      ap_[i]      = has_ap ? AP[j * 64 - 1] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int k = 8 * b + i;
+      v2s       x = U(hi_lo(xp[i], xo[i]));
+      if (has_ap) x = sadd(x, U(hi_lo(ap_[i], ao[i])));
+      v2s c0[8], c1[8];
+      alpha_cands<true>(st, x, U(hi_lo(yp[i], yo[i])), c0, c1);
+#pragma unroll
+      for (int s = 0; s < 8; s++) st[s] = vmax(c0[s], c1[s]);
       if ((k & 1) == 0 && k != 0) normalize<true>(st);
     }
   }
@@ -236,42 +282,44 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
   }
 
   // ------------------------------------------------ forward pass: per segment, recompute beta then alpha
-  int16_t*        E16   = (int16_t*)(a.E + cbase);
-  int16_t*        A16   = (int16_t*)(a.A1 + cbase);
-  int16_t*        D16   = (int16_t*)(a.D + cbase);
-  const uint32_t* dstr  = (dec2 ? a.dstA : a.dstE) + (size_t)l * Lp;
-  const bool      wr_d  = a.write_d;
+  int16_t*        E16  = (int16_t*)a.E + (size_t)grp * Lp * 128;
+  int16_t*        A16  = (int16_t*)a.A1 + (size_t)grp * Lp * 128;
+  int16_t*        D16  = (int16_t*)a.D + (size_t)grp * Lp * 128;
+  const uint32_t* tab  = (dec2 ? a.dstA : a.dstE) + l;
+  const int       lane0 = cbg * NL; // first lane of this code block inside the 64-lane row
+  const bool      wr_d = a.write_d;
 
+  uint32_t cx[SEG], cy[SEG], ca[SEG], cd[SEG], cc[8];
+  auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap, uint32_t* d, uint32_t* c) {
+#pragma unroll
+    for (int i = 0; i < SEG; i++) {
+      const int j = min(t * SEG + i, L - 1); // clamp the ragged last segment (values unused)
+      x[i]        = X[j * xs];
+      y[i]        = Y[j * NL];
+      ap[i]       = has_ap ? AP[j * 64] : 0u;
+      d[i]        = tab[(size_t)j * NL];
+    }
+#pragma unroll
+    for (int s = 0; s < 8; s++) c[s] = ck[((size_t)t * 8 + s) * 64];
+  };
+  load(0, cx, cy, ca, cd, cc);
+
+#pragma unroll 1
   for (int t = 0; t < nseg; t++) {
     const int s0 = t * SEG;
     const int e  = (s0 + SEG < L) ? s0 + SEG : L;
+    uint32_t  nx[SEG], ny[SEG], na[SEG], nd[SEG], nc[8];
+    if (t + 1 < nseg) load(t + 1, nx, ny, na, nd, nc);
 
-    uint32_t xs[SEG], ys[SEG], as[SEG], ds[SEG];
-#pragma unroll
-    for (int q = 0; q < SEG / 4; q++) {
-      const uint4 xv = *(const uint4*)(Xr + s0 + 4 * q);
-      const uint4 yv = *(const uint4*)(Yr + s0 + 4 * q);
-      const uint4 dv = *(const uint4*)(dstr + s0 + 4 * q);
-      uint4       av = make_uint4(0, 0, 0, 0);
-      if (has_ap) av = *(const uint4*)(Ar + s0 + 4 * q);
-      xs[4 * q] = xv.x; xs[4 * q + 1] = xv.y; xs[4 * q + 2] = xv.z; xs[4 * q + 3] = xv.w;
-      ys[4 * q] = yv.x; ys[4 * q + 1] = yv.y; ys[4 * q + 2] = yv.z; ys[4 * q + 3] = yv.w;
-      ds[4 * q] = dv.x; ds[4 * q + 1] = dv.y; ds[4 * q + 2] = dv.z; ds[4 * q + 3] = dv.w;
-      as[4 * q] = av.x; as[4 * q + 1] = av.y; as[4 * q + 2] = av.z; as[4 * q + 3] = av.w;
-    }
     v2s xin[SEG];
 #pragma unroll
-    for (int i = 0; i < SEG; i++) xin[i] = has_ap ? sadd(U(xs[i]), U(as[i])) : U(xs[i]);
+    for (int i = 0; i < SEG; i++) xin[i] = has_ap ? sadd(U(cx[i]), U(ca[i])) : U(cx[i]);
 
     // beta rows s0+1 .. e from the checkpoint at row e
     v2s rows[SEG + 1][8];
     v2s cur[8];
-    {
-      const uint4* c  = (const uint4*)(ck + (size_t)t * 8);
-      const uint4  c0 = c[0], c1 = c[1];
-      rows[SEG][0] = U(c0.x); rows[SEG][1] = U(c0.y); rows[SEG][2] = U(c0.z); rows[SEG][3] = U(c0.w);
-      rows[SEG][4] = U(c1.x); rows[SEG][5] = U(c1.y); rows[SEG][6] = U(c1.z); rows[SEG][7] = U(c1.w);
-    }
+#pragma unroll
+    for (int s = 0; s < 8; s++) rows[SEG][s] = U(cc[s]);
 #pragma unroll
     for (int i = SEG; i >= 1; i--) {
       const int j = s0 + i;
@@ -284,7 +332,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
         for (int s = 0; s < 8; s++) cur[s] = rows[i][s];
         if ((j & 1) == 0 && j != L) normalize<true>(cur);
       } else if (j < e) {
-        beta_step<true>(cur, xin[i], U(ys[i]), rows[i]);
+        beta_step<true>(cur, xin[i], U(cy[i]), rows[i]);
 #pragma unroll
         for (int s = 0; s < 8; s++) cur[s] = rows[i][s];
         if ((j & 1) == 0) normalize<true>(cur);
@@ -297,7 +345,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
       const int j = s0 + i;
       if (j < e) {
         v2s c0[8], c1[8];
-        alpha_cands<true>(st, xin[i], U(ys[i]), c0, c1);
+        alpha_cands<true>(st, xin[i], U(cy[i]), c0, c1);
         v2s m0 = sadd(rows[i + 1][0], c0[0]);
         v2s m1 = sadd(rows[i + 1][0], c1[0]);
 #pragma unroll
@@ -310,97 +358,104 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
         for (int s = 0; s < 8; s++) st[s] = vmax(c0[s], c1[s]);
         if ((i & 1) == 0 && j != 0) normalize<true>(st);
 
-        const uint32_t dst = ds[i];
-        const int      dlo = dst & 0xffff, dhi = dst >> 16;
+        // destination row j' (same for every window) and the two destination windows
+        const uint32_t tb   = cd[i];
+        const int      jd   = tb & 0xffff;
+        const int      wlo  = (tb >> 16) & 0xff, whi = tb >> 24;
+        const size_t   rowd = (size_t)jd * 128 + lane0 * 2;
+        const size_t   olo  = rowd + (wlo >> 1) * 2 + (wlo & 1);
+        const size_t   ohi  = rowd + (whi >> 1) * 2 + (whi & 1);
         if (!dec2) {
           // e = ext1 - app1 (wrapping), turbodecoder_iter.h:118-120 of the next DEC2
-          const v2s ev = (n > 0) ? out - U(as[i]) : out;
-          E16[dlo]     = ev.x;
-          E16[dhi]     = ev.y;
-          if (wr_d) ((uint32_t*)a.D)[row + j] = W(out);
+          const v2s ev = (n > 0) ? out - U(ca[i]) : out;
+          E16[olo]     = ev.x;
+          E16[ohi]     = ev.y;
+          if (wr_d) WG_AT(a.D, j) = W(out);
         } else {
           // a1 = app1 - ext1 (wrapping) of the next DEC1, turbodecoder_iter.h:108-110
           const v2s av = out - xin[i];
-          A16[dlo]     = av.x;
-          A16[dhi]     = av.y;
+          A16[olo]     = av.x;
+          A16[ohi]     = av.y;
           if (wr_d) {
-            D16[dlo] = out.x;
-            D16[dhi] = out.y;
+            D16[olo] = out.x;
+            D16[ohi] = out.y;
           }
         }
       }
     }
+#pragma unroll
+    for (int i = 0; i < SEG; i++) {
+      cx[i] = nx[i];
+      cy[i] = ny[i];
+      ca[i] = na[i];
+      cd[i] = nd[i];
+    }
+#pragma unroll
+    for (int s = 0; s < 8; s++) cc[s] = nc[s];
   }
-  (void)K;
 }
 
 // ---------------------------------------------------------------------------- layout kernels
 
-// softbuffer layout (rm_turbo.c:263-277: stream s at s*(K+32), step j of window w at j*NSB + w,
-// tails at 3*(K+32)) -> packed lane-major arrays [cb][l][Lp] of (window 2l, window 2l+1) pairs.
+// decision bytes (turbodecoder_win.h:973-993): bit = LLR > 0, natural order, MSB first.
+// Fast path (L % 8 == 0, every K >= 1024 with L = K/16 multiple of 8, ...): one thread per (group row
+// block of 8 steps, lane) reads 8 consecutive rows of its lane (coalesced across the wave) and emits the
+// two bytes of its windows.
 template <int NSB>
-__global__ __launch_bounds__(256) void tdec_win_prep(TdecPrepArgs a)
+__global__ __launch_bounds__(256) void tdec_win_decide_rows(TdecDecideArgs a)
 {
-  constexpr int NL  = NSB / 2;
-  const size_t  g   = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t  per = (size_t)NL * a.Lp;
-  const size_t  cb  = g / per;
+  constexpr int NL = NSB / 2;
+  constexpr int G  = 64 / NL;
+  const size_t  g  = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int     q  = (int)(g & 63);
+  const size_t  r  = g >> 6;
+  const int     nb = a.L / 8;
+  const int     grp = (int)(r / nb), jb = (int)(r % nb);
+  const int     cbg = q / NL, l = q % NL;
+  const size_t  cb  = (size_t)grp * G + cbg;
   if (cb >= (size_t)a.ncb) return;
-  const int      r   = (int)(g % per);
-  const int      l   = r / a.Lp;
-  const int      j   = r % a.Lp;
-  const int      K   = a.L * NSB;
-  const int16_t* in  = a.in + cb * a.stride;
-  uint32_t       v[3] = {0, 0, 0};
-  if (j < a.L) {
+  const uint32_t* D  = a.D + ((size_t)grp * a.Lp + 8 * jb) * 64 + q;
+  uint32_t        lo = 0, hi = 0;
 #pragma unroll
-    for (int s = 0; s < 3; s++) v[s] = *(const uint32_t*)(in + s * (K + 32) + j * NSB + 2 * l);
+  for (int i = 0; i < 8; i++) {
+    const v2s v = U(D[(size_t)i * 64]);
+    lo |= (uint32_t)(v.x > 0) << (7 - i);
+    hi |= (uint32_t)(v.y > 0) << (7 - i);
   }
-  const size_t o = cb * per + r;
-  a.S[o]         = v[0];
-  a.P0[o]        = v[1];
-  a.P1[o]        = v[2];
-  if (r < 12) a.T[cb * 12 + r] = in[3 * (K + 32) + r];
+  uint8_t* o = a.out + cb * a.out_stride;
+  o[(2 * l) * nb + jb]     = (uint8_t)lo;
+  o[(2 * l + 1) * nb + jb] = (uint8_t)hi;
 }
 
-// decision bytes (turbodecoder_win.h:973-993): bit = LLR > 0, natural order, MSB first.
+// general path (any L): one thread per output byte
 template <int NSB>
 __global__ __launch_bounds__(256) void tdec_win_decide(TdecDecideArgs a)
 {
-  const size_t g    = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int    K    = a.L * NSB;
-  const int    nbyt = K / 8;
-  const size_t cb   = g / nbyt;
+  constexpr int NL   = NSB / 2;
+  constexpr int G    = 64 / NL;
+  const size_t  g    = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int     K    = a.L * NSB;
+  const int     nbyt = K / 8;
+  const size_t  cb   = g / nbyt;
   if (cb >= (size_t)a.ncb) return;
   const int      b   = (int)(g % nbyt);
-  const int16_t* D16 = (const int16_t*)(a.D + cb * (NSB / 2) * a.Lp);
+  const int      grp = (int)(cb / G), cbg = (int)(cb % G);
+  const int16_t* D16 = (const int16_t*)a.D + (size_t)grp * a.Lp * 128 + cbg * NL * 2;
   uint32_t       out = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const int nat = 8 * b + i, w = nat / a.L, j = nat % a.L;
-    out |= (uint32_t)(D16[((w >> 1) * a.Lp + j) * 2 + (w & 1)] > 0) << (7 - i);
+    out |= (uint32_t)(D16[(size_t)j * 128 + w] > 0) << (7 - i);
   }
   a.out[cb * a.out_stride + b] = (uint8_t)out;
 }
 
 // ---------------------------------------------------------------------------- launchers
 
-hipError_t tdec_win_launch_prep(int nsb, const TdecPrepArgs& a, hipStream_t s)
-{
-  const size_t total  = (size_t)a.ncb * (nsb / 2) * a.Lp;
-  const int    blocks = (int)((total + 255) / 256);
-  if (nsb == 16) {
-    hipLaunchKernelGGL(tdec_win_prep<16>, dim3(blocks), dim3(256), 0, s, a);
-  } else {
-    hipLaunchKernelGGL(tdec_win_prep<8>, dim3(blocks), dim3(256), 0, s, a);
-  }
-  return hipGetLastError();
-}
-
 hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s)
 {
-  const int lanes  = a.ncb * (nsb / 2);
-  const int blocks = (lanes + 255) / 256;
+  const int ngrp   = (a.ncb + (128 / nsb) - 1) / (128 / nsb);
+  const int blocks = (ngrp * 64 + 255) / 256;
   if (nsb == 16) {
     hipLaunchKernelGGL((tdec_win_halfit<16, TDEC_SEG>), dim3(blocks), dim3(256), 0, s, a);
   } else {
@@ -411,6 +466,18 @@ hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s)
 
 hipError_t tdec_win_launch_decide(int nsb, const TdecDecideArgs& a, hipStream_t s)
 {
+  if (a.L % 8 == 0) {
+    const int    G      = 128 / nsb;
+    const size_t ngrp   = (a.ncb + G - 1) / G;
+    const size_t total  = ngrp * (a.L / 8) * 64;
+    const int    blocks = (int)((total + 255) / 256);
+    if (nsb == 16) {
+      hipLaunchKernelGGL(tdec_win_decide_rows<16>, dim3(blocks), dim3(256), 0, s, a);
+    } else {
+      hipLaunchKernelGGL(tdec_win_decide_rows<8>, dim3(blocks), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+  }
   const size_t total  = (size_t)a.ncb * (a.L * nsb / 8);
   const int    blocks = (int)((total + 255) / 256);
   if (nsb == 16) {

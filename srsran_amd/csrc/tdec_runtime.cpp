@@ -47,7 +47,7 @@ struct KTables {
 };
 
 struct Geometry {
-  uint32_t K, nsb, L, Lp, nl, nseg; // window mode (nsb > 0)
+  uint32_t K, nsb, L, Lp, nl, nseg, ngrp; // window mode (nsb > 0)
   uint32_t npair, Kp;               // generic mode (nsb == 0)
 };
 
@@ -61,6 +61,7 @@ Geometry geometry(uint32_t K, uint32_t ncb)
     g.Lp   = round_up(g.L, TDEC_SEG);
     g.nl   = g.nsb / 2;
     g.nseg = (g.L + TDEC_SEG - 1) / TDEC_SEG;
+    g.ngrp = (ncb + (64 / g.nl) - 1) / (64 / g.nl);
   } else {
     g.npair = (ncb + 1) / 2;
     g.Kp    = round_up(K + 3, TDEC_SEG);
@@ -101,16 +102,16 @@ static int get_tables(mi355_tdec_batch_t* q, const Geometry& g, KTables** out)
   }
   KTables t;
   if (g.nsb) {
-    auto off = [&](uint32_t p) -> uint32_t {
-      uint32_t w = p / g.L, j = p % g.L;
-      return ((w >> 1) * g.Lp + j) * 2 + (w & 1);
-    };
-    std::vector<uint32_t> dE((size_t)g.nl * g.Lp, 0), dA((size_t)g.nl * g.Lp, 0);
-    for (uint32_t l = 0; l < g.nl; l++) {
-      for (uint32_t j = 0; j < g.L; j++) {
+    // per (step j, lane l): destination row j' (shared by every window, QPP contention-freeness)
+    // and the destination windows of this lane's two windows
+    std::vector<uint32_t> dE((size_t)g.L * g.nl, 0), dA((size_t)g.L * g.nl, 0);
+    for (uint32_t j = 0; j < g.L; j++) {
+      for (uint32_t l = 0; l < g.nl; l++) {
         uint32_t n0 = (2 * l) * g.L + j, n1 = (2 * l + 1) * g.L + j;
-        dE[(size_t)l * g.Lp + j] = off(inv[n0]) | (off(inv[n1]) << 16);
-        dA[(size_t)l * g.Lp + j] = off(pi[n0]) | (off(pi[n1]) << 16);
+        uint32_t e0 = inv[n0], e1 = inv[n1], a0 = pi[n0], a1 = pi[n1];
+        if (e0 % g.L != e1 % g.L || a0 % g.L != a1 % g.L) return MI355_ERROR; // not contention-free
+        dE[(size_t)j * g.nl + l] = (e0 % g.L) | ((e0 / g.L) << 16) | ((e1 / g.L) << 24);
+        dA[(size_t)j * g.nl + l] = (a0 % g.L) | ((a0 / g.L) << 16) | ((a1 / g.L) << 24);
       }
     }
     CHECK_HIP(hipMalloc(&t.dstE, dE.size() * 4));
@@ -131,8 +132,8 @@ static int get_tables(mi355_tdec_batch_t* q, const Geometry& g, KTables** out)
 static size_t ws_bytes(const Geometry& g, uint32_t n)
 {
   if (g.nsb) {
-    const size_t arr = (size_t)n * g.nl * g.Lp * 4;
-    return 6 * arr + round_up(n * 12 * 2, 256) + (size_t)n * g.nl * g.nseg * 32 + 6 * 256;
+    const size_t arr = (size_t)g.ngrp * g.Lp * 64 * 4;
+    return 3 * arr + (size_t)g.ngrp * g.nseg * 8 * 64 * 4 + 8 * 256;
   }
   const size_t arr = (size_t)g.npair * g.Kp * 4;
   return 6 * arr + (size_t)g.npair * 16 + (size_t)g.npair * g.nseg * 32 + 8 * 256;
@@ -258,20 +259,14 @@ int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
   };
 
   if (g.nsb) {
-    const size_t arr = (size_t)n * g.nl * g.Lp * 4;
-    auto*        S   = (uint32_t*)carve(arr);
-    auto*        P0  = (uint32_t*)carve(arr);
-    auto*        P1  = (uint32_t*)carve(arr);
+    const size_t arr = (size_t)g.ngrp * g.Lp * 64 * 4;
     auto*        A1  = (uint32_t*)carve(arr);
     auto*        E   = (uint32_t*)carve(arr);
     auto*        D   = (uint32_t*)carve(arr);
-    auto*        T   = (int16_t*)carve((size_t)n * 12 * 2);
-    auto*        CK  = (uint32_t*)carve((size_t)n * g.nl * g.nseg * 32);
+    auto*        CK  = (uint32_t*)carve((size_t)g.ngrp * g.nseg * 8 * 64 * 4);
 
-    TdecPrepArgs pa{d_in, in_stride, S, P0, P1, T, (int)n, (int)g.L, (int)g.Lp};
-    CHECK_HIP(tdec_win_launch_prep(g.nsb, pa, s));
     for (uint32_t h = 0; h < nhalf; h++) {
-      TdecWinArgs wa{S, P0, P1, A1, E, D, T, CK, t->dstE, t->dstA,
+      TdecWinArgs wa{d_in, in_stride, A1, E, D, CK, t->dstE, t->dstA,
                      (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == nhalf};
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (q->prof) {
