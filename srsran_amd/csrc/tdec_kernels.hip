@@ -27,6 +27,7 @@
 //                  de-interleaved (= app1, what the reference decides on).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "tdec_internal.h"
 
@@ -124,7 +125,11 @@ __device__ __forceinline__ void set_minf(v2s s[8])
 
 #define WG_AT(arr, j) (arr)[((size_t)grp * Lp + (j)) * 64 + q]
 
-template <int NSB, int SEG>
+// MODE: 0 = DEC1 without a-priori (n = 0), 1 = DEC1 with a-priori, 2 = DEC2.  A compile-time mode keeps
+// every load unconditional (a runtime "load or zero" select makes hipcc branch around each load and
+// wait for it, which serialises the memory pipeline).
+// DIAG (diagnostic builds only, selected by MI355_TDEC_DIAG): 1 = backward pass only, 2 = forward only
+template <int NSB, int SEG, int MODE, int DIAG = 0>
 __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
 {
   constexpr int NL = NSB / 2;
@@ -134,9 +139,9 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
   const int     cbg = q / NL, l = q % NL;
   if (grp * G + cbg >= a.ncb) return;
 
-  const int  L = a.L, Lp = a.Lp, nseg = a.nseg, n = a.n;
-  const bool dec2   = n & 1;
-  const bool has_ap = !dec2 && n > 0;
+  const int  L = a.L, Lp = a.Lp, nseg = a.nseg;
+  constexpr bool dec2   = MODE == 2;
+  constexpr bool has_ap = MODE == 1;
 
   // Inputs are read straight from the caller's softbuffer-layout buffers (rm_turbo.c:263-277): stream s
   // of code block cb at u32 offset s*(K+32)/2, step j of lane l at j*NL + l -- a 32-byte row per code
@@ -155,6 +160,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
 
   v2s st[8], nw[8];
 
+  if constexpr (DIAG != 2) {
   // ------------------------------------------------ backward pass: boundary (row L)
   // warm-up over the first 40 steps of the NEXT window (lane q+1 holds windows 2l+2, 2l+3), from -INF
   // (turbodecoder_win.h:566-631).  The neighbour value of lane NL-1 belongs to another code block and
@@ -162,7 +168,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
   set_minf(st);
 #pragma unroll 1
   for (int b = TDEC_WARMUP / 8 - 1; b >= 0; b--) {
-    uint32_t xo[8], xn[8], yo[8], yn[8], ao[8], an[8];
+    uint32_t xo[8], xn[8], yo[8], yn[8], ao[8] = {}, an[8] = {};
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = 8 * b + i;
@@ -170,14 +176,14 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
       xn[i]       = X[j * xs + 1];
       yo[i]       = Y[j * NL];
       yn[i]       = Y[j * NL + 1];
-      ao[i]       = has_ap ? AP[j * 64] : 0u;
-      an[i]       = has_ap ? AP[j * 64 + 1] : 0u;
+      if constexpr (has_ap) ao[i] = AP[j * 64];
+      if constexpr (has_ap) an[i] = AP[j * 64 + 1];
     }
 #pragma unroll
     for (int i = 7; i >= 0; i--) {
       const int k = 8 * b + i;
       v2s       x = U(hi_lo(xo[i], xn[i]));
-      if (has_ap) x = sadd(x, U(hi_lo(ao[i], an[i])));
+      if constexpr (has_ap) x = sadd(x, U(hi_lo(ao[i], an[i])));
       beta_step<true>(st, x, U(hi_lo(yo[i], yn[i])), nw);
 #pragma unroll
       for (int s = 0; s < 8; s++) st[s] = nw[s];
@@ -206,27 +212,30 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
 
   // ------------------------------------------------ backward pass: main, one checkpoint per segment
   {
-    uint32_t cx[SEG], cy[SEG], ca[SEG];
+    uint32_t cx[SEG], cy[SEG], ca[SEG] = {};
     auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap) {
 #pragma unroll
       for (int i = 0; i < SEG; i++) {
         const int j = min(t * SEG + i, L - 1); // clamp the ragged last segment (values unused)
         x[i]        = X[j * xs];
         y[i]        = Y[j * NL];
-        ap[i]       = has_ap ? AP[j * 64] : 0u;
+        if constexpr (has_ap) ap[i] = AP[j * 64];
       }
     };
+    // two segments in flight ahead of the one being consumed (registers are free in this pass)
+    uint32_t n1x[SEG], n1y[SEG], n1a[SEG] = {};
     load(nseg - 1, cx, cy, ca);
+    if (nseg > 1) load(nseg - 2, n1x, n1y, n1a);
 #pragma unroll 1
     for (int t = nseg - 1; t >= 0; t--) {
-      uint32_t nx[SEG], ny[SEG], na[SEG];
-      if (t > 0) load(t - 1, nx, ny, na);
+      uint32_t n2x[SEG], n2y[SEG], n2a[SEG] = {};
+      if (t > 1) load(t - 2, n2x, n2y, n2a);
 #pragma unroll
       for (int i = SEG - 1; i >= 0; i--) {
         const int k = t * SEG + i;
         if (k < L) {
           v2s x = U(cx[i]);
-          if (has_ap) x = sadd(x, U(ca[i]));
+          if constexpr (has_ap) x = sadd(x, U(ca[i]));
           beta_step<true>(st, x, U(cy[i]), nw);
 #pragma unroll
           for (int s = 0; s < 8; s++) st[s] = nw[s];
@@ -239,19 +248,23 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
       }
 #pragma unroll
       for (int i = 0; i < SEG; i++) {
-        cx[i] = nx[i];
-        cy[i] = ny[i];
-        ca[i] = na[i];
+        cx[i]  = n1x[i];
+        cy[i]  = n1y[i];
+        ca[i]  = n1a[i];
+        n1x[i] = n2x[i];
+        n1y[i] = n2y[i];
+        n1a[i] = n2a[i];
       }
     }
   }
-
+  } // DIAG != 2
+  if constexpr (DIAG == 1) return;
   // ------------------------------------------------ forward pass: boundary at the window start
   // warm-up over the LAST 40 steps of the PREVIOUS window (lane q-1), turbodecoder_win.h:705-757
   set_minf(st);
 #pragma unroll 1
   for (int b = 0; b < TDEC_WARMUP / 8; b++) {
-    uint32_t xo[8], xp[8], yo[8], yp[8], ao[8], ap_[8];
+    uint32_t xo[8], xp[8], yo[8], yp[8], ao[8] = {}, ap_[8] = {};
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = (L - TDEC_WARMUP) + 8 * b + i;
@@ -259,14 +272,14 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
       xp[i]       = X[j * xs - 1];
       yo[i]       = Y[j * NL];
       yp[i]       = Y[j * NL - 1];
-      ao[i]       = has_ap ? AP[j * 64] : 0u;
-      ap_[i]      = has_ap ? AP[j * 64 - 1] : 0u;
+      if constexpr (has_ap) ao[i] = AP[j * 64];
+      if constexpr (has_ap) ap_[i] = AP[j * 64 - 1];
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int k = 8 * b + i;
       v2s       x = U(hi_lo(xp[i], xo[i]));
-      if (has_ap) x = sadd(x, U(hi_lo(ap_[i], ao[i])));
+      if constexpr (has_ap) x = sadd(x, U(hi_lo(ap_[i], ao[i])));
       v2s c0[8], c1[8];
       alpha_cands<true>(st, x, U(hi_lo(yp[i], yo[i])), c0, c1);
 #pragma unroll
@@ -289,14 +302,14 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
   const int       lane0 = cbg * NL; // first lane of this code block inside the 64-lane row
   const bool      wr_d = a.write_d;
 
-  uint32_t cx[SEG], cy[SEG], ca[SEG], cd[SEG], cc[8];
+  uint32_t cx[SEG], cy[SEG], ca[SEG] = {}, cd[SEG], cc[8];
   auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap, uint32_t* d, uint32_t* c) {
 #pragma unroll
     for (int i = 0; i < SEG; i++) {
       const int j = min(t * SEG + i, L - 1); // clamp the ragged last segment (values unused)
       x[i]        = X[j * xs];
       y[i]        = Y[j * NL];
-      ap[i]       = has_ap ? AP[j * 64] : 0u;
+      if constexpr (has_ap) ap[i] = AP[j * 64];
       d[i]        = tab[(size_t)j * NL];
     }
 #pragma unroll
@@ -308,50 +321,68 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
   for (int t = 0; t < nseg; t++) {
     const int s0 = t * SEG;
     const int e  = (s0 + SEG < L) ? s0 + SEG : L;
-    uint32_t  nx[SEG], ny[SEG], na[SEG], nd[SEG], nc[8];
+    uint32_t  nx[SEG], ny[SEG], na[SEG] = {}, nd[SEG], nc[8];
     if (t + 1 < nseg) load(t + 1, nx, ny, na, nd, nc);
 
     v2s xin[SEG];
 #pragma unroll
-    for (int i = 0; i < SEG; i++) xin[i] = has_ap ? sadd(U(cx[i]), U(ca[i])) : U(cx[i]);
-
-    // beta rows s0+1 .. e from the checkpoint at row e
-    v2s rows[SEG + 1][8];
-    v2s cur[8];
-#pragma unroll
-    for (int s = 0; s < 8; s++) rows[SEG][s] = U(cc[s]);
-#pragma unroll
-    for (int i = SEG; i >= 1; i--) {
-      const int j = s0 + i;
-      if (j == e) {
-        if (i != SEG) {
-#pragma unroll
-          for (int s = 0; s < 8; s++) rows[i][s] = rows[SEG][s];
-        }
-#pragma unroll
-        for (int s = 0; s < 8; s++) cur[s] = rows[i][s];
-        if ((j & 1) == 0 && j != L) normalize<true>(cur);
-      } else if (j < e) {
-        beta_step<true>(cur, xin[i], U(cy[i]), rows[i]);
-#pragma unroll
-        for (int s = 0; s < 8; s++) cur[s] = rows[i][s];
-        if ((j & 1) == 0) normalize<true>(cur);
+    for (int i = 0; i < SEG; i++) {
+      if constexpr (has_ap) {
+        xin[i] = sadd(U(cx[i]), U(ca[i]));
+      } else {
+        xin[i] = U(cx[i]);
       }
     }
 
-    // alpha steps s0 .. e-1 with outputs
+    // Beta rows s0+1 .. e are rebuilt from the checkpoint (row e) in two halves so that only 4 rows
+    // are live at a time (the upper half is recomputed twice): phase A keeps rows 1..4 for alpha
+    // steps 0..3, phase B rows 5..8 for alpha steps 4..7.
+    static_assert(SEG == 8, "two-phase recompute assumes 8-row segments");
+    v2s ck8[8], cur[8], R[4][8];
 #pragma unroll
-    for (int i = 0; i < SEG; i++) {
-      const int j = s0 + i;
+    for (int s = 0; s < 8; s++) ck8[s] = U(cc[s]);
+    const bool ck_norm = (e & 1) == 0 && e != L;
+
+#pragma unroll
+    for (int ph = 0; ph < 2; ph++) {
+      const int lo = ph ? 5 : 1; // rows kept in this phase: lo .. lo+3
+#pragma unroll
+      for (int s = 0; s < 8; s++) cur[s] = ck8[s];
+      if (ck_norm) normalize<true>(cur);
+#pragma unroll
+      for (int i = SEG; i >= lo; i--) {
+        const int j = s0 + i;
+        if (j == e) {
+          if (i <= lo + 3) {
+#pragma unroll
+            for (int s = 0; s < 8; s++) R[i - lo][s] = ck8[s];
+          }
+        } else if (j < e) {
+          v2s row[8];
+          beta_step<true>(cur, xin[i], U(cy[i]), row);
+#pragma unroll
+          for (int s = 0; s < 8; s++) cur[s] = row[s];
+          if (i <= lo + 3) {
+#pragma unroll
+            for (int s = 0; s < 8; s++) R[i - lo][s] = row[s];
+          }
+          if ((j & 1) == 0) normalize<true>(cur);
+        }
+      }
+      // alpha steps lo-1 .. lo+2 with outputs
+#pragma unroll
+      for (int ii = 0; ii < 4; ii++) {
+        const int i = lo - 1 + ii;
+        const int j = s0 + i;
       if (j < e) {
         v2s c0[8], c1[8];
         alpha_cands<true>(st, xin[i], U(cy[i]), c0, c1);
-        v2s m0 = sadd(rows[i + 1][0], c0[0]);
-        v2s m1 = sadd(rows[i + 1][0], c1[0]);
+        v2s m0 = sadd(R[ii][0], c0[0]);
+        v2s m1 = sadd(R[ii][0], c1[0]);
 #pragma unroll
         for (int s = 1; s < 8; s++) {
-          m0 = vmax(m0, sadd(rows[i + 1][s], c0[s]));
-          m1 = vmax(m1, sadd(rows[i + 1][s], c1[s]));
+          m0 = vmax(m0, sadd(R[ii][s], c0[s]));
+          m1 = vmax(m1, sadd(R[ii][s], c1[s]));
         }
         const v2s out = ssub(m1, m0);
 #pragma unroll
@@ -365,9 +396,9 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
         const size_t   rowd = (size_t)jd * 128 + lane0 * 2;
         const size_t   olo  = rowd + (wlo >> 1) * 2 + (wlo & 1);
         const size_t   ohi  = rowd + (whi >> 1) * 2 + (whi & 1);
-        if (!dec2) {
+        if constexpr (!dec2) {
           // e = ext1 - app1 (wrapping), turbodecoder_iter.h:118-120 of the next DEC2
-          const v2s ev = (n > 0) ? out - U(ca[i]) : out;
+          const v2s ev = has_ap ? out - U(ca[i]) : out;
           E16[olo]     = ev.x;
           E16[ohi]     = ev.y;
           if (wr_d) WG_AT(a.D, j) = W(out);
@@ -382,6 +413,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
           }
         }
       }
+    }
     }
 #pragma unroll
     for (int i = 0; i < SEG; i++) {
@@ -452,14 +484,44 @@ __global__ __launch_bounds__(256) void tdec_win_decide(TdecDecideArgs a)
 
 // ---------------------------------------------------------------------------- launchers
 
+static int diag_mode()
+{
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("MI355_TDEC_DIAG");
+    m             = e ? atoi(e) : 0;
+  }
+  return m;
+}
+
+template <int NSB, int DIAG>
+static void launch_mode(int mode, int blocks, const TdecWinArgs& a, hipStream_t s)
+{
+  if (mode == 0) {
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 0, DIAG>), dim3(blocks), dim3(256), 0, s, a);
+  } else if (mode == 1) {
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 1, DIAG>), dim3(blocks), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 2, DIAG>), dim3(blocks), dim3(256), 0, s, a);
+  }
+}
+
 hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s)
 {
   const int ngrp   = (a.ncb + (128 / nsb) - 1) / (128 / nsb);
   const int blocks = (ngrp * 64 + 255) / 256;
+  const int mode   = (a.n & 1) ? 2 : (a.n > 0 ? 1 : 0);
+  const int dm     = diag_mode();
   if (nsb == 16) {
-    hipLaunchKernelGGL((tdec_win_halfit<16, TDEC_SEG>), dim3(blocks), dim3(256), 0, s, a);
+    if (dm == 1) {
+      launch_mode<16, 1>(mode, blocks, a, s);
+    } else if (dm == 2) {
+      launch_mode<16, 2>(mode, blocks, a, s);
+    } else {
+      launch_mode<16, 0>(mode, blocks, a, s);
+    }
   } else {
-    hipLaunchKernelGGL((tdec_win_halfit<8, TDEC_SEG>), dim3(blocks), dim3(256), 0, s, a);
+    launch_mode<8, 0>(mode, blocks, a, s);
   }
   return hipGetLastError();
 }
