@@ -175,9 +175,10 @@ def main():
     bytes_per_cb_halfit = 3.5 * 2 * K
     avg_launch_ms = kms / max(klaunch, 1)
     achieved = bytes_per_cb_halfit * ncb / (avg_launch_ms / 1e3) / 1e9
-    # VALU: lane-op count of the MAP kernel per CB-half-iteration, packed 2 windows per op
-    valu_ops_cb_halfit = float(os.environ.get("TDEC_VALU_OPS_PER_CB_HALFIT", "0")) or None
     pmc = load_pmc_traffic()
+    # VALU: wave-instructions of the MAP kernel per launch from SQ_INSTS_VALU (profiles/), one wave-
+    # instruction = 64 lanes x 2 packed int16 ops; peak = 1024 SIMDs x 1 wave-instruction / 2 clk.
+    valu_insts = (pmc or {}).get("valu_insts_per_launch")
 
     res = {
         "metric": "PDSCH decoded Mbps + code-blocks/sec, 20 MHz TM4 QAM256, 1/2/4/8 GPU",
@@ -202,10 +203,11 @@ def main():
                      "kernel": "tdec_win_halfit<16,8>", "avg_launch_ms": round(avg_launch_ms, 4),
                      "algorithmic_bytes_per_launch": int(bytes_per_cb_halfit * ncb)},
     }
-    if valu_ops_cb_halfit:
-        ops = valu_ops_cb_halfit * ncb / (avg_launch_ms / 1e3) / 1e12
-        res["roofline_valu"] = {"achieved": round(ops, 2), "peak": round(VALU_PEAK_TOPS, 1), "unit": "Tlane-op/s",
-                                "frac": round(ops / VALU_PEAK_TOPS, 4)}
+    if valu_insts and (pmc or {}).get("launch_ncb") == ncb:
+        rate = valu_insts * 64 / (avg_launch_ms / 1e3) / 1e12
+        res["roofline_valu"] = {"achieved": round(rate, 2), "peak": round(VALU_PEAK_TOPS, 1),
+                                "unit": "T lane-instr/s", "frac": round(rate / VALU_PEAK_TOPS, 4),
+                                "source": "SQ_INSTS_VALU from profiles/tdec_pmc_traffic.json"}
 
     if rank == 0 and world == 1 and not args.no_cpu:
         cb, cpu_out = cpu_baseline(pool[: min(args.pool, 256)], K, nh, args.cpu_seconds)

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile_tdec.sh run into profiles/<tag>_*.
+
+HBM bytes per MAP launch = FETCH_SIZE + WRITE_SIZE (KB units), with FETCH_SIZE corrected by a factor
+calibrated on this kernel's own access pattern: the loads-only diagnostic build (MI355_TDEC_DIAG=4)
+reads an exactly known byte count (MI355_MICROARCH.md "HBM": FETCH_SIZE under-reports wide streaming
+reads by 2x on gfx950 -- calibrate on a known byte count before trusting an absolute)."""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+TAG = sys.argv[1] if len(sys.argv) > 1 else "r01"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = os.path.join(ROOT, "gpurun_out", f"prof_{TAG}")
+OUTD = os.path.join(ROOT, "profiles")
+MAP = "tdec_win_halfit"
+NCB, K = 65536, 6144
+
+
+def counters(sub):
+    f = glob.glob(os.path.join(P, sub, "**", "*counter_collection.csv"), recursive=True)
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(f[0])):
+        agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    return agg
+
+
+def per_kernel(agg, counter, pat=MAP):
+    vals = [v for (k, c), vs in agg.items() if pat in k and c == counter for v in vs]
+    return sum(vals) / max(len(vals), 1), len(vals)
+
+
+def main():
+    os.makedirs(OUTD, exist_ok=True)
+    stats = glob.glob(os.path.join(P, "trace", "**", "*kernel_stats.csv"), recursive=True)[0]
+    shutil.copy(stats, os.path.join(OUTD, f"{TAG}_kernel_stats.csv"))
+    fetch, _ = per_kernel(counters("fetch"), "FETCH_SIZE")
+    write, _ = per_kernel(counters("write"), "WRITE_SIZE")
+    calib_fetch, _ = per_kernel(counters("calib"), "FETCH_SIZE")
+    # loads-only variant: the 8 launches of a step read S,P0 (n=0), E,P1 (DEC2) or S,A1,P0 (DEC1)
+    # twice?  No: the loads-only variant runs the backward pass only -> one read of each array.
+    known = NCB * 2 * K * (2 + 3 * 3 + 2 * 4) / 8  # avg over n=0..7 of arrays read once
+    factor = known / (calib_fetch * 1024) if calib_fetch else None
+    sq = counters("sq")
+    valu, _ = per_kernel(sq, "SQ_INSTS_VALU")
+    waves, _ = per_kernel(sq, "SQ_WAVES")
+    res = {
+        "tag": TAG, "kernel": MAP, "launch_ncb": NCB, "K": K,
+        "fetch_size_kb_per_launch": fetch, "write_size_kb_per_launch": write,
+        "fetch_calibration": {"known_bytes": known, "fetch_size_kb": calib_fetch, "factor": factor},
+        "bytes_per_launch": (fetch * 1024 * (factor or 1.0) + write * 1024),
+        "valu_insts_per_launch": valu, "waves_per_launch": waves,
+        "valu_lane_ops_per_cb_halfit": valu * 64 / NCB if valu else None,
+    }
+    json.dump(res, open(os.path.join(OUTD, "tdec_pmc_traffic.json"), "w"), indent=1)
+    json.dump(res, open(os.path.join(OUTD, f"{TAG}_pmc_summary.json"), "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
