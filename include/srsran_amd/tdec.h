@@ -54,6 +54,27 @@ int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
                              size_t              out_stride,
                              void*               stream);
 
+/* One half-iteration (0-based index half_idx) on the decoder's workspace, followed by the decision
+ * bytes: the building block of srslte_tdec_iteration() and of CRC early stopping
+ * (lib/src/phy/phch/sch.c:415-450).  half_idx > 0 continues the state left by the previous calls for the
+ * same (d_in, n, K); half_idx == 0 starts a new set of code blocks. */
+int mi355_tdec_batch_halfit_dev(mi355_tdec_batch_t* q,
+                                const int16_t*      d_in,
+                                size_t              in_stride,
+                                uint32_t            n,
+                                uint32_t            K,
+                                uint32_t            half_idx,
+                                uint8_t*            d_out,
+                                size_t              out_stride,
+                                void*               stream);
+
+/* Decoder implementation, as srslte_tdec_impl_type_t (turbodecoder_impl.h:28-38): AUTO (default) picks by
+ * K like the AVX2 build; GENERIC runs the generic decoder for every K on the LINEAR input layout
+ * (srslte_tdec_init_manual(GENERIC) + srslte_tdec_force_not_sb, turbodecoder_test -d 1). */
+#define MI355_TDEC_AUTO 0
+#define MI355_TDEC_GENERIC 1
+int mi355_tdec_batch_set_impl(mi355_tdec_batch_t* q, int impl);
+
 /* Host-buffer convenience wrapper: copy in, decode, copy out, synchronise. */
 int mi355_tdec_batch_run(mi355_tdec_batch_t* q,
                          const int16_t*      in,

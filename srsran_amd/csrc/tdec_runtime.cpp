@@ -51,11 +51,11 @@ struct Geometry {
   uint32_t npair, Kp;               // generic mode (nsb == 0)
 };
 
-Geometry geometry(uint32_t K, uint32_t ncb)
+Geometry geometry(uint32_t K, uint32_t ncb, int impl)
 {
   Geometry g{};
   g.K   = K;
-  g.nsb = mi355_tdec_autoimp_get_subblocks(K);
+  g.nsb = impl == MI355_TDEC_GENERIC ? 0 : mi355_tdec_autoimp_get_subblocks(K);
   if (g.nsb) {
     g.L    = K / g.nsb;
     g.Lp   = round_up(g.L, TDEC_SEG);
@@ -77,7 +77,9 @@ struct mi355_tdec_batch {
   hipStream_t                  own    = nullptr;
   char*                        ws     = nullptr;
   size_t                       ws_cap = 0;
-  std::map<uint32_t, KTables>  tables;
+  std::map<uint32_t, KTables>  tables;     // window-mode tables per K
+  std::map<uint32_t, KTables>  gtables;    // generic-mode tables per K
+  int                          impl = MI355_TDEC_AUTO;
   bool                         prof = false;
   std::vector<hipEvent_t>      ev;
   size_t                       ev_used = 0;
@@ -86,8 +88,9 @@ struct mi355_tdec_batch {
 
 static int get_tables(mi355_tdec_batch_t* q, const Geometry& g, KTables** out)
 {
-  auto it = q->tables.find(g.K);
-  if (it != q->tables.end()) {
+  auto& cache = g.nsb ? q->tables : q->gtables;
+  auto  it    = cache.find(g.K);
+  if (it != cache.end()) {
     *out = &it->second;
     return MI355_SUCCESS;
   }
@@ -124,7 +127,7 @@ static int get_tables(mi355_tdec_batch_t* q, const Geometry& g, KTables** out)
     CHECK_HIP(hipMalloc(&t.pi, 2 * K * 2));
     CHECK_HIP(hipMemcpy(t.pi, both.data(), 2 * K * 2, hipMemcpyHostToDevice));
   }
-  auto r = q->tables.emplace(K, t);
+  auto r = cache.emplace(K, t);
   *out   = &r.first->second;
   return MI355_SUCCESS;
 }
@@ -194,10 +197,12 @@ void mi355_tdec_batch_destroy(mi355_tdec_batch_t* q)
   if (!q) return;
   (void)hipSetDevice(q->device);
   (void)hipDeviceSynchronize();
-  for (auto& kv : q->tables) {
-    (void)hipFree(kv.second.dstE);
-    (void)hipFree(kv.second.dstA);
-    (void)hipFree(kv.second.pi);
+  for (auto* m : {&q->tables, &q->gtables}) {
+    for (auto& kv : *m) {
+      (void)hipFree(kv.second.dstE);
+      (void)hipFree(kv.second.dstA);
+      (void)hipFree(kv.second.pi);
+    }
   }
   for (auto e : q->ev) (void)hipEventDestroy(e);
   if (q->ws) (void)hipFree(q->ws);
@@ -226,18 +231,22 @@ int mi355_tdec_batch_kernel_stats(mi355_tdec_batch_t* q, double* ms, uint32_t* l
   return MI355_SUCCESS;
 }
 
-int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
-                             const int16_t*      d_in,
-                             size_t              in_stride,
-                             uint32_t            n,
-                             uint32_t            K,
-                             uint32_t            nhalf,
-                             uint8_t*            d_out,
-                             size_t              out_stride,
-                             void*               stream)
+// Launch half-iterations [h0, h1) on the workspace; decisions after h1-1 when `decide`.
+static int run_range(mi355_tdec_batch_t* q,
+                     const int16_t*      d_in,
+                     size_t              in_stride,
+                     uint32_t            n,
+                     uint32_t            K,
+                     uint32_t            h0,
+                     uint32_t            h1,
+                     uint8_t*            d_out,
+                     size_t              out_stride,
+                     void*               stream)
 {
-  if (!q || !d_in || !d_out || nhalf == 0 || cb_index(K) < 0) return MI355_ERROR_INVALID_INPUTS;
-  if (in_stride < 3 * (size_t)(K + 32) + 12 || (in_stride & 1) || out_stride < K / 8) {
+  if (!q || !d_in || !d_out || h1 <= h0 || cb_index(K) < 0) return MI355_ERROR_INVALID_INPUTS;
+  const bool generic = q->impl == MI355_TDEC_GENERIC || mi355_tdec_autoimp_get_subblocks(K) == 0;
+  const size_t need  = generic ? 3 * (size_t)K + 12 : 3 * (size_t)(K + 32) + 12;
+  if (in_stride < need || (in_stride & 1) || out_stride < K / 8) {
     return MI355_ERROR_INVALID_INPUTS;
   }
   if (n == 0) return MI355_SUCCESS;
@@ -245,11 +254,15 @@ int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
   CHECK_HIP(hipSetDevice(q->device));
   hipStream_t s = stream ? (hipStream_t)stream : q->own;
 
-  const Geometry g = geometry(K, n);
+  const Geometry g = geometry(K, n, q->impl);
   KTables*       t = nullptr;
   int            r = get_tables(q, g, &t);
   if (r) return r;
-  if ((r = ensure_ws(q, ws_bytes(g, n)))) return r;
+  if (h0 == 0) {
+    if ((r = ensure_ws(q, ws_bytes(g, n)))) return r;
+  } else if (ws_bytes(g, n) > q->ws_cap) {
+    return MI355_ERROR; // continuation without a workspace holding the earlier half-iterations
+  }
 
   char* p     = q->ws;
   auto  carve = [&](size_t bytes) {
@@ -265,9 +278,9 @@ int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
     auto*        D   = (uint32_t*)carve(arr);
     auto*        CK  = (uint32_t*)carve((size_t)g.ngrp * g.nseg * 8 * 64 * 4);
 
-    for (uint32_t h = 0; h < nhalf; h++) {
+    for (uint32_t h = h0; h < h1; h++) {
       TdecWinArgs wa{d_in, in_stride, A1, E, D, CK, t->dstE, t->dstA,
-                     (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == nhalf};
+                     (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == h1};
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (q->prof) {
         e0 = next_event(q);
@@ -289,11 +302,13 @@ int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
     auto*        D   = (uint32_t*)carve(arr);
     auto*        CK  = (uint32_t*)carve((size_t)g.npair * g.nseg * 32);
 
-    TdecGenPrepArgs pa{d_in, in_stride, S, P0, P1, E, (int)n, (int)g.npair, (int)K, (int)g.Kp};
-    CHECK_HIP(tdec_gen_launch_prep(pa, s));
-    for (uint32_t h = 0; h < nhalf; h++) {
+    if (h0 == 0) {
+      TdecGenPrepArgs pa{d_in, in_stride, S, P0, P1, E, (int)n, (int)g.npair, (int)K, (int)g.Kp};
+      CHECK_HIP(tdec_gen_launch_prep(pa, s));
+    }
+    for (uint32_t h = h0; h < h1; h++) {
       TdecGenArgs ga{S, P0, P1, A1, E, D, CK, t->pi,
-                     (int)g.npair, (int)K, (int)g.Kp, (int)g.nseg, (int)h, h + 1 == nhalf};
+                     (int)g.npair, (int)K, (int)g.Kp, (int)g.nseg, (int)h, h + 1 == h1};
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (q->prof) {
         e0 = next_event(q);
@@ -306,6 +321,40 @@ int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
     TdecGenDecideArgs da{D, d_out, out_stride, (int)n, (int)K, (int)g.Kp};
     CHECK_HIP(tdec_gen_launch_decide(da, s));
   }
+  return MI355_SUCCESS;
+}
+
+int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
+                             const int16_t*      d_in,
+                             size_t              in_stride,
+                             uint32_t            n,
+                             uint32_t            K,
+                             uint32_t            nhalf,
+                             uint8_t*            d_out,
+                             size_t              out_stride,
+                             void*               stream)
+{
+  if (nhalf == 0) return MI355_ERROR_INVALID_INPUTS;
+  return run_range(q, d_in, in_stride, n, K, 0, nhalf, d_out, out_stride, stream);
+}
+
+int mi355_tdec_batch_halfit_dev(mi355_tdec_batch_t* q,
+                                const int16_t*      d_in,
+                                size_t              in_stride,
+                                uint32_t            n,
+                                uint32_t            K,
+                                uint32_t            half_idx,
+                                uint8_t*            d_out,
+                                size_t              out_stride,
+                                void*               stream)
+{
+  return run_range(q, d_in, in_stride, n, K, half_idx, half_idx + 1, d_out, out_stride, stream);
+}
+
+int mi355_tdec_batch_set_impl(mi355_tdec_batch_t* q, int impl)
+{
+  if (!q || (impl != MI355_TDEC_AUTO && impl != MI355_TDEC_GENERIC)) return MI355_ERROR_INVALID_INPUTS;
+  q->impl = impl;
   return MI355_SUCCESS;
 }
 
