@@ -1,0 +1,71 @@
+/*
+ * include/srsran_amd/dlsch.h -- C ABI of the MI355X DL-SCH transport-block decoder.
+ *
+ * Replaces srslte_dlsch_decode / srslte_dlsch_decode2 (lib/src/phy/phch/sch.c:572-606 -> decode_tb
+ * :503-570 -> decode_tb_cb :363-488) for a BATCH of transport blocks (any mix of subframes / codewords):
+ * rate dematching into HARQ softbuffers, turbo decoding with CRC early stopping after every
+ * half-iteration, TB CRC.  Results are bit-exact with the reference for every transport block:
+ *   - per-CB LLR ranges use the reference's E/rp formulas including its cb_idx > C - gamma condition;
+ *   - CB i's decision bytes are written at data + i*rlen/8 (the payload needs tbs/8 + 6 bytes when C > 1,
+ *     tbs/8 + 3 when C == 1), the last CB keeps its CB-CRC bytes, the TB-CRC bytes are zeroed first;
+ *   - ret = 0 iff every CB CRC passed and CRC24A(payload) == the 3 parity bytes != 0 (sch.c:541-558),
+ *     -1 on CRC failure, -2 for invalid inputs (filler bits, too many CBs for the softbuffer);
+ *   - HARQ: softbuffers accumulate across calls (rv 0..3); CBs that passed before are skipped and restored.
+ *
+ * Softbuffers live in device memory (srslte_softbuffer_rx_t, softbuffer.h:37-60): a pool of nof_sb
+ * softbuffers of max_cb code blocks (18600 int16 + 768 data bytes + CRC flag each).
+ */
+#ifndef SRSRAN_AMD_DLSCH_H
+#define SRSRAN_AMD_DLSCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mi355_softbuffer_pool mi355_softbuffer_pool_t;
+
+int  mi355_softbuffer_pool_create(mi355_softbuffer_pool_t** p, uint32_t nof_sb, uint32_t max_cb, int device);
+void mi355_softbuffer_pool_destroy(mi355_softbuffer_pool_t* p);
+/* srslte_softbuffer_rx_reset / _reset_tbs / _reset_cb (softbuffer.c:128-154) on softbuffer `sb` */
+int mi355_softbuffer_reset(mi355_softbuffer_pool_t* p, uint32_t sb, void* stream);
+int mi355_softbuffer_reset_tbs(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t tbs, void* stream);
+int mi355_softbuffer_reset_cb(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t nof_cb, void* stream);
+int mi355_softbuffer_reset_all(mi355_softbuffer_pool_t* p, void* stream);
+
+typedef struct {
+  uint32_t tbs;         /* transport block size in bits (grant.tb[i].tbs) */
+  uint32_t nof_e_bits;  /* coded LLRs of the codeword (grant.tb[i].nof_bits) */
+  uint32_t Qm;          /* bits per symbol x layers of this codeword (sch.c:598-603: Qm * Nl) */
+  uint32_t rv;          /* redundancy version 0..3 */
+  uint32_t softbuffer;  /* softbuffer index in the pool */
+  uint64_t e_offset;    /* int16 offset of the codeword's LLRs in d_e_bits */
+  uint64_t data_offset; /* byte offset of the payload in d_data */
+} mi355_dlsch_tb_t;
+
+typedef struct mi355_dlsch mi355_dlsch_t;
+
+int  mi355_dlsch_create(mi355_dlsch_t** q, int device);
+void mi355_dlsch_destroy(mi355_dlsch_t* q);
+/* srslte_sch_set_max_noi (sch.c:222-225): half-iterations per CB, default 10 (SRSLTE_PDSCH_MAX_TDEC_ITERS) */
+int mi355_dlsch_set_max_iterations(mi355_dlsch_t* q, uint32_t max_iterations);
+
+/* Decode ntb transport blocks whose descrambled LLRs are in device memory.  Synchronous: returns after
+ * ret[] (host, one srslte return code per TB) and avg_iterations[] (host, nullable; q->avg_iterations of
+ * the reference: half-iterations per CB averaged over the TB) are filled. */
+int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
+                           mi355_softbuffer_pool_t* pool,
+                           const int16_t*           d_e_bits,
+                           const mi355_dlsch_tb_t*  tbs,
+                           uint32_t                 ntb,
+                           uint8_t*                 d_data,
+                           int32_t*                 ret,
+                           float*                   avg_iterations,
+                           void*                    stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

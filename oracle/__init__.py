@@ -58,6 +58,12 @@ def lib() -> C.CDLL:
         L.orc_crc.argtypes = [u8p, C.c_uint32, C.c_uint32, C.c_uint32]
         L.orc_cbsegm.argtypes = [C.c_uint32, u32p]
         L.orc_tdec_run_batch.argtypes = [i16p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u8p, C.c_int]
+        L.orc_rm_turbo_table.argtypes = [C.c_uint32, C.c_uint32, u16p]
+        L.orc_rm_turbo_rx.argtypes = [i16p, C.c_uint32, i16p, C.c_uint32, C.c_uint32]
+        L.orc_dlsch_decode_tb.argtypes = [i16p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                          i16p, u8p, u8p, u8p, C.POINTER(C.c_float)]
+        L.orc_rm_turbo_tx.argtypes = [u8p, C.c_uint32, C.c_uint32, C.c_uint32, u8p]
+        L.orc_dlsch_encode_tb.argtypes = [u8p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u8p]
         _LIB = L
     return _LIB
 
@@ -162,6 +168,65 @@ def cbsegm(tbs: int) -> dict:
     r = np.zeros(6, np.uint32)
     assert lib().orc_cbsegm(tbs, r) == 0
     return dict(zip(["C", "K1", "K2", "C1", "C2", "F"], [int(v) for v in r]))
+
+
+SOFTBUFFER_SIZE = 18600
+
+
+def rm_turbo_table(K: int, rv: int) -> np.ndarray:
+    t = np.zeros(3 * K + 12, np.uint16)
+    lib().orc_rm_turbo_table(K, rv, t)
+    return t
+
+
+def rm_turbo_rx(e: np.ndarray, K: int, rv: int, out: np.ndarray | None = None) -> np.ndarray:
+    """srslte_rm_turbo_rx_lut: accumulate (wrapping) into out (a SOFTBUFFER_SIZE int16 buffer)."""
+    if out is None:
+        out = np.zeros(SOFTBUFFER_SIZE, np.int16)
+    e = np.ascontiguousarray(e, np.int16)
+    assert lib().orc_rm_turbo_rx(e, e.size, out, K, rv) == 0
+    return out
+
+
+class Softbuffer:
+    """srslte_softbuffer_rx_t equivalent (softbuffer.h:37-43) for the oracle TB decoder."""
+
+    def __init__(self, max_cb: int = 32):
+        self.buf = np.zeros((max_cb, SOFTBUFFER_SIZE), np.int16)
+        self.cb_crc = np.zeros(max_cb, np.uint8)
+        self.data = np.zeros((max_cb, 768), np.uint8)
+
+    def reset(self):
+        self.buf[:] = 0
+        self.cb_crc[:] = 0
+        self.data[:] = 0
+
+
+def dlsch_decode_tb(e_bits: np.ndarray, tbs: int, Qm: int, rv: int, max_its: int, sb: Softbuffer):
+    """decode_tb (sch.c:503-570): returns (ret, data bytes, avg half-iterations)."""
+    e = np.ascontiguousarray(e_bits, np.int16)
+    data = np.zeros(tbs // 8 + 8, np.uint8)
+    its = C.c_float()
+    ret = lib().orc_dlsch_decode_tb(e, e.size, tbs, Qm, rv, max_its, sb.buf, sb.cb_crc, sb.data, data,
+                                    C.byref(its))
+    return ret, data, its.value
+
+
+def dlsch_encode_tb(payload_bits: np.ndarray, tbs: int, Qm: int, G: int, rv: int) -> np.ndarray:
+    """TB -> G coded bits (CRC24A, segmentation + CRC24B, turbo coding, rate matching)."""
+    e = np.zeros(G, np.uint8)
+    assert lib().orc_dlsch_encode_tb(np.ascontiguousarray(payload_bits, np.uint8), tbs, Qm, G, rv, e) == 0
+    return e
+
+
+def make_tb(rng: np.random.Generator, tbs: int, Qm: int, G: int, rv: int, snr_db: float, scale: float = 100.0):
+    """Random TB -> int16 LLRs of its G coded bits over BPSK/AWGN (positive = bit 1), plus payload bytes."""
+    bits = rng.integers(0, 2, tbs, dtype=np.uint8)
+    coded = dlsch_encode_tb(bits, tbs, Qm, G, rv)
+    sigma = 10 ** (-snr_db / 20)
+    y = np.where(coded.astype(bool), 1.0, -1.0) + sigma * rng.standard_normal(G)
+    llr = np.trunc(scale * y).clip(-32768, 32767).astype(np.int16)
+    return np.packbits(bits), llr
 
 
 # ------------------------------------------------------------------ test-vector synthesis

@@ -1,0 +1,82 @@
+// srsran_amd/csrc/dlsch_internal.h -- device argument blocks of the DL-SCH kernels (dlsch_kernels.hip)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SB_STRIDE 18600 // SOFTBUFFER_SIZE (softbuffer.h:50): int16 per code-block softbuffer
+#define SB_DATA 768     // bytes of decoded CB data kept per code block (softbuffer.c:146)
+
+namespace mi355 {
+
+struct CbDesc {      // one code block of one transport block
+  uint32_t tb, cb, C; // transport block index in the call, CB index, CBs in the TB
+  uint32_t rlen;      // K - 24 (C > 1) or K
+  uint32_t rp, n_e;   // offset / count of its LLRs in the TB's e_bits (sch.c:391-401)
+  uint32_t rv;
+  uint32_t slot;      // softbuffer code-block slot in the pool
+  uint64_t e_off;     // element offset of the TB's LLRs in the e_bits buffer
+  uint64_t data_off;  // byte offset of the TB payload in the data buffer
+};
+
+struct TbDesc {
+  uint32_t tbs, C, C1, K1, K2, slot0, invalid;
+  uint64_t data_off;
+};
+
+struct CrcTable {
+  uint32_t t[256];
+  uint32_t pw[24]; // x^(8*2^i) mod P
+  uint32_t poly;   // with the x^24 term
+};
+
+struct DlschRmArgs {
+  const CbDesc*   desc;
+  int             ncb;
+  uint32_t        N; // 3K+12
+  const uint16_t* table[4];
+  const int16_t*  e;
+  int16_t*        sb;
+  size_t          sb_stride;
+  const uint8_t*  sb_crc;
+};
+
+struct DlschCheckArgs {
+  const CbDesc*  desc;
+  int            ncb;
+  uint32_t       K, h, max_its;
+  const uint8_t* dec;
+  size_t         dec_stride;
+  uint8_t*       data;
+  uint8_t*       done;
+  uint32_t*      its;
+  uint8_t*        sb_crc;
+  const CrcTable* crc24a;
+  const CrcTable* crc24b;
+};
+
+struct DlschTbArgs {
+  const TbDesc* tb;
+  int           ntb;
+  uint8_t*      data;
+  uint8_t*      sb_crc;
+  uint8_t*      sb_data;
+  int32_t*        ret;
+  const CrcTable* crc24a;
+};
+
+struct DlschResetArgs {
+  int16_t* sb;
+  size_t   sb_stride;
+  uint8_t* sb_crc;
+  uint8_t* sb_data;
+  size_t   slot0, ncb;
+};
+
+hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s);
+hipError_t dlsch_launch_check(const DlschCheckArgs& a, hipStream_t s);
+hipError_t dlsch_launch_prologue(const DlschTbArgs& a, hipStream_t s);
+hipError_t dlsch_launch_epilogue(const DlschTbArgs& a, hipStream_t s);
+hipError_t dlsch_launch_reset(const DlschResetArgs& a, hipStream_t s);
+hipError_t dlsch_launch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc, int n, hipStream_t s);
+
+} // namespace mi355

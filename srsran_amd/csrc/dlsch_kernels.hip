@@ -1,0 +1,215 @@
+// srsran_amd/csrc/dlsch_kernels.hip -- DL-SCH transport-block decode kernels around the turbo decoder:
+// rate dematching into the HARQ softbuffers, per-code-block CRC early stopping, TB CRC.
+// Semantics follow lib/src/phy/phch/sch.c:363-570 (decode_tb_cb / decode_tb), see dlsch_runtime.cpp.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dlsch_internal.h"
+
+namespace mi355 {
+
+// ---------------------------------------------------------------------------- rate dematching
+// srslte_rm_turbo_rx_lut (rm_turbo.c:397-454, :717-822): out[deinter[i % N]] += in[i], wrapping int16.
+// The deinterleaver is a bijection on [0, N), so thread r owns destination deinter[r] and sums its
+// contributions i = r, r+N, r+2N, ... (wrapping addition is order independent) -- no atomics.
+__global__ __launch_bounds__(256) void dlsch_rm_rx(DlschRmArgs a)
+{
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int    b = (int)(g / a.N);
+  const int    r = (int)(g % a.N);
+  if (b >= a.ncb) return;
+  const CbDesc& d = a.desc[b];
+  if (a.sb_crc[d.slot]) return; // CB already decoded in an earlier transmission (sch.c:385)
+  const int16_t* e   = a.e + d.e_off + d.rp;
+  uint32_t       sum = 0;
+  bool           any = false;
+  for (uint32_t i = r; i < d.n_e; i += a.N) {
+    sum += (uint16_t)e[i];
+    any = true;
+  }
+  if (!any) return;
+  int16_t* sb = a.sb + (size_t)d.slot * a.sb_stride + a.table[d.rv][r];
+  *sb         = (int16_t)(uint16_t)((uint16_t)*sb + sum);
+}
+
+// ---------------------------------------------------------------------------- CRC helpers
+// CRC as crc.c:30-157: MSB first, zero init, no final xor; CRC(A||B) = CRC(A)*x^|B| + CRC(B) (mod P),
+// so a wave computes one CRC with every lane folding a contiguous chunk and scaling it by x^(8*bytes
+// after the chunk) (square-and-multiply with precomputed x^(8*2^i) mod P).
+
+__device__ __forceinline__ uint32_t gf2_mulmod24(uint32_t a, uint32_t b, uint32_t poly)
+{
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 23; i >= 0; i--) {
+    r <<= 1;
+    if (r & 0x1000000u) r ^= poly;
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r & 0xffffffu;
+}
+
+__device__ uint32_t wave_crc24(const uint8_t* bytes, uint32_t nbytes, const CrcTable& T)
+{
+  const int      lane  = threadIdx.x & 63;
+  const uint32_t chunk = (nbytes + 63) / 64;
+  const uint32_t b0    = min(nbytes, lane * chunk), b1 = min(nbytes, b0 + chunk);
+  uint32_t       crc   = 0;
+  for (uint32_t i = b0; i < b1; i++) crc = ((crc << 8) ^ T.t[((crc >> 16) & 0xff) ^ bytes[i]]) & 0xffffffu;
+  uint32_t after = nbytes - b1, sc = 1;
+  for (int i = 0; after; i++, after >>= 1) {
+    if (after & 1) sc = gf2_mulmod24(sc, T.pw[i], T.poly);
+  }
+  crc = gf2_mulmod24(crc, sc, T.poly);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
+  return crc;
+}
+
+// ---------------------------------------------------------------------------- per-CB early stop
+// After half-iteration h (sch.c:415-450): decision bytes -> CRC24B (C>1) or CRC24A over tbs+24 = K bits
+// (C==1); CRC ok => the CB is finished at this iteration.  Decision bytes of CB i land at i*rlen/8 of the
+// TB payload; only the last CB keeps its trailing CRC bytes (the earlier ones are overwritten by the
+// next CB in the reference's sequential loop, sch.c:422-424).
+__global__ __launch_bounds__(256) void dlsch_cb_check(DlschCheckArgs a)
+{
+  const int b    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (b >= a.ncb || a.done[b]) return;
+  const CbDesc&  d   = a.desc[b];
+  const uint8_t* dec = a.dec + (size_t)b * a.dec_stride;
+  const uint32_t crc = wave_crc24(dec, a.K / 8, d.C > 1 ? *a.crc24b : *a.crc24a);
+  const bool     ok  = crc == 0;
+  const bool     fin = ok || a.h + 1 == a.max_its;
+  if (!fin) return;
+  uint8_t*       dst = a.data + d.data_off + (size_t)d.cb * d.rlen / 8;
+  const uint32_t nb  = (d.cb + 1 == d.C) ? a.K / 8 : d.rlen / 8;
+  for (uint32_t i = lane; i < nb; i += 64) dst[i] = dec[i];
+  if (lane == 0) {
+    a.its[b] = a.h + 1;
+    if (ok) {
+      a.done[b]         = 1;
+      a.sb_crc[d.slot]  = 1;
+    } else {
+      a.done[b] = 2; // gave up: CRC error after max_iterations
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- TB prologue / epilogue
+
+// decode_tb (sch.c:532-535) zeroes the 3 TB-CRC bytes; decode_tb_cb (:476-484) restores the CBs that
+// passed in an earlier transmission from the softbuffer.
+__global__ __launch_bounds__(256) void dlsch_tb_prologue(DlschTbArgs a)
+{
+  const int t    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (t >= a.ntb) return;
+  const TbDesc& tb = a.tb[t];
+  if (tb.C == 0) return;
+  uint8_t* data = a.data + tb.data_off;
+  if (lane < 3) data[tb.tbs / 8 + lane] = 0;
+  for (uint32_t c = 0; c < tb.C; c++) {
+    const uint32_t slot = tb.slot0 + c;
+    if (!a.sb_crc[slot]) continue;
+    const uint32_t K    = c < tb.C1 ? tb.K1 : tb.K2;
+    const uint32_t rlen = tb.C == 1 ? K : K - 24;
+    const uint32_t o    = c * rlen / 8; // sch.c indexes with the CURRENT CB's rlen (cb_idx * rlen / 8)
+    for (uint32_t i = lane; i < rlen / 8; i += 64) data[o + i] = a.sb_data[(size_t)slot * 768 + i];
+  }
+}
+
+// sch.c:488-500 + decode_tb :537-559
+__global__ __launch_bounds__(256) void dlsch_tb_epilogue(DlschTbArgs a)
+{
+  const int t    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (t >= a.ntb) return;
+  const TbDesc& tb = a.tb[t];
+  if (tb.C == 0) {
+    if (lane == 0) a.ret[t] = tb.invalid ? -2 : 0;
+    return;
+  }
+  bool ok = true;
+  for (uint32_t c = 0; c < tb.C; c++) ok = ok && a.sb_crc[tb.slot0 + c];
+  uint8_t* data = a.data + tb.data_off;
+  if (!ok) {
+    for (uint32_t c = 0; c < tb.C; c++) {
+      const uint32_t slot = tb.slot0 + c;
+      if (!a.sb_crc[slot]) continue;
+      const uint32_t K    = c < tb.C1 ? tb.K1 : tb.K2;
+      const uint32_t rlen = tb.C == 1 ? K : K - 24;
+      for (uint32_t i = lane; i < rlen / 8; i += 64) a.sb_data[(size_t)slot * 768 + i] = data[c * rlen / 8 + i];
+    }
+    if (lane == 0) a.ret[t] = -1;
+    return;
+  }
+  const uint32_t par_rx = wave_crc24(data, tb.tbs / 8, *a.crc24a);
+  if (lane == 0) {
+    const uint32_t par_tx = ((uint32_t)data[tb.tbs / 8] << 16) | ((uint32_t)data[tb.tbs / 8 + 1] << 8) |
+                            (uint32_t)data[tb.tbs / 8 + 2];
+    a.ret[t] = (par_rx == par_tx && par_rx) ? 0 : -1;
+  }
+}
+
+// ---------------------------------------------------------------------------- softbuffer reset
+__global__ __launch_bounds__(256) void dlsch_sb_reset(DlschResetArgs a)
+{
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t per = (size_t)a.sb_stride / 2; // u32 words per CB buffer
+  const size_t cb  = g / per;
+  if (cb >= a.ncb) return;
+  const size_t slot = a.slot0 + cb;
+  ((uint32_t*)(a.sb + slot * a.sb_stride))[g % per] = 0;
+  if (g % per < 768 / 4) ((uint32_t*)(a.sb_data + slot * 768))[g % per] = 0;
+  if (g % per == 0) a.sb_crc[slot] = 0;
+}
+
+// CBs whose CRC passed in an earlier transmission start finished (sch.c:385)
+__global__ __launch_bounds__(256) void dlsch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc,
+                                                        int n)
+{
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < n) done[b] = sb_crc[slot[b]] ? 3 : 0;
+}
+
+hipError_t dlsch_launch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc, int n, hipStream_t s)
+{
+  hipLaunchKernelGGL(dlsch_init_done, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, done, slot, sb_crc, n);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- launchers
+hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s)
+{
+  const size_t total = (size_t)a.ncb * a.N;
+  hipLaunchKernelGGL(dlsch_rm_rx, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t dlsch_launch_check(const DlschCheckArgs& a, hipStream_t s)
+{
+  hipLaunchKernelGGL(dlsch_cb_check, dim3((unsigned)((a.ncb + 3) / 4)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t dlsch_launch_prologue(const DlschTbArgs& a, hipStream_t s)
+{
+  hipLaunchKernelGGL(dlsch_tb_prologue, dim3((unsigned)((a.ntb + 3) / 4)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t dlsch_launch_epilogue(const DlschTbArgs& a, hipStream_t s)
+{
+  hipLaunchKernelGGL(dlsch_tb_epilogue, dim3((unsigned)((a.ntb + 3) / 4)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t dlsch_launch_reset(const DlschResetArgs& a, hipStream_t s)
+{
+  const size_t total = a.ncb * (size_t)a.sb_stride / 2;
+  hipLaunchKernelGGL(dlsch_sb_reset, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+} // namespace mi355

@@ -1,0 +1,395 @@
+// srsran_amd/csrc/dlsch_runtime.cpp -- host runtime behind include/srsran_amd/dlsch.h.
+//
+// One call decodes a batch of transport blocks:
+//   prologue (TB-CRC bytes zeroed, CBs decoded in an earlier transmission restored)
+//   -> rate dematching of every code block into its softbuffer (one launch per K)
+//   -> for h in 0 .. max_its-1: MAP half-iteration (finished CBs skipped) -> decision bytes -> CRC check
+//   -> epilogue (TB CRC24A, softbuffer data of CRC-ok CBs saved when the TB fails).
+// Code blocks are grouped by K (one decoder workspace per K); within a group every CB advances one
+// half-iteration per launch, so CRC early stopping is a per-CB skip flag, not a per-CB loop.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <stdio.h>
+#include <string.h>
+#include <vector>
+
+#include "../../include/srsran_amd/dlsch.h"
+#include "../../include/srsran_amd/tdec.h"
+#include "dlsch_internal.h"
+#include "rm_tables.h"
+#include "tdec_internal.h"
+
+using namespace mi355;
+
+#define CHECK_HIP(x)                                                                                                   \
+  do {                                                                                                                 \
+    hipError_t e_ = (x);                                                                                               \
+    if (e_ != hipSuccess) {                                                                                            \
+      fprintf(stderr, "[srsran_amd] %s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));                 \
+      return MI355_ERROR;                                                                                              \
+    }                                                                                                                  \
+  } while (0)
+
+struct mi355_softbuffer_pool {
+  int      device = 0;
+  uint32_t nof_sb = 0, max_cb = 0;
+  int16_t* buf    = nullptr; // nof_sb * max_cb * SB_STRIDE
+  uint8_t* cb_crc = nullptr; // nof_sb * max_cb
+  uint8_t* data   = nullptr; // nof_sb * max_cb * SB_DATA
+};
+
+namespace {
+
+CrcTable make_crc_table(uint32_t poly)
+{
+  CrcTable t{};
+  t.poly = poly;
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i << 16;
+    for (int j = 0; j < 8; j++) c = (c & 0x800000) ? ((c << 1) ^ poly) & 0xffffff : (c << 1) & 0xffffff;
+    t.t[i] = c;
+  }
+  // x^(8*2^i) mod P: start from x^8, square repeatedly
+  auto mulmod = [&](uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+    for (int i = 23; i >= 0; i--) {
+      r <<= 1;
+      if (r & 0x1000000u) r ^= poly;
+      if ((b >> i) & 1u) r ^= a;
+    }
+    return r & 0xffffffu;
+  };
+  uint32_t p = 1u << 8;
+  for (int i = 0; i < 24; i++) {
+    t.pw[i] = p;
+    p       = mulmod(p, p);
+  }
+  return t;
+}
+
+struct Group {
+  uint32_t             K = 0;
+  std::vector<CbDesc>  cbs;
+  std::vector<uint32_t> slots;
+};
+
+} // namespace
+
+struct mi355_dlsch {
+  int                                    device = 0;
+  hipStream_t                            own    = nullptr;
+  uint32_t                               max_its = 10; // SRSLTE_PDSCH_MAX_TDEC_ITERS, sch.c:35
+  std::map<uint32_t, mi355_tdec_batch_t*> dec;         // one decoder workspace per K
+  std::map<uint64_t, uint16_t*>          rm;           // (K << 2 | rv) -> device table
+  CrcTable*                              crc = nullptr; // [0] CRC24A, [1] CRC24B
+  // per-call scratch
+  char*  scratch     = nullptr;
+  size_t scratch_cap = 0;
+  std::mutex mu;
+};
+
+static int rm_table(mi355_dlsch_t* q, uint32_t K, uint32_t rv, const uint16_t** out)
+{
+  const uint64_t key = ((uint64_t)K << 2) | rv;
+  auto           it  = q->rm.find(key);
+  if (it == q->rm.end()) {
+    std::vector<uint16_t> t = rm_rx_table(K, rv);
+    uint16_t*             d = nullptr;
+    CHECK_HIP(hipMalloc(&d, t.size() * 2));
+    CHECK_HIP(hipMemcpy(d, t.data(), t.size() * 2, hipMemcpyHostToDevice));
+    it = q->rm.emplace(key, d).first;
+  }
+  *out = it->second;
+  return MI355_SUCCESS;
+}
+
+static int scratch(mi355_dlsch_t* q, size_t bytes, char** p)
+{
+  if (bytes > q->scratch_cap) {
+    if (q->scratch) {
+      CHECK_HIP(hipDeviceSynchronize());
+      CHECK_HIP(hipFree(q->scratch));
+      q->scratch = nullptr;
+    }
+    size_t cap = bytes + bytes / 4 + 4096;
+    CHECK_HIP(hipMalloc(&q->scratch, cap));
+    q->scratch_cap = cap;
+  }
+  *p = q->scratch;
+  return MI355_SUCCESS;
+}
+
+extern "C" {
+
+int mi355_softbuffer_pool_create(mi355_softbuffer_pool_t** p, uint32_t nof_sb, uint32_t max_cb, int device)
+{
+  if (!p || !nof_sb || !max_cb) return MI355_ERROR_INVALID_INPUTS;
+  CHECK_HIP(hipSetDevice(device));
+  auto*        s  = new mi355_softbuffer_pool;
+  const size_t nc = (size_t)nof_sb * max_cb;
+  s->device       = device;
+  s->nof_sb       = nof_sb;
+  s->max_cb       = max_cb;
+  if (hipMalloc(&s->buf, nc * SB_STRIDE * 2) != hipSuccess || hipMalloc(&s->cb_crc, nc) != hipSuccess ||
+      hipMalloc(&s->data, nc * SB_DATA) != hipSuccess) {
+    mi355_softbuffer_pool_destroy(s);
+    return MI355_ERROR;
+  }
+  (void)hipMemset(s->buf, 0, nc * SB_STRIDE * 2);
+  (void)hipMemset(s->cb_crc, 0, nc);
+  (void)hipMemset(s->data, 0, nc * SB_DATA);
+  (void)hipDeviceSynchronize();
+  *p = s;
+  return MI355_SUCCESS;
+}
+
+void mi355_softbuffer_pool_destroy(mi355_softbuffer_pool_t* p)
+{
+  if (!p) return;
+  (void)hipFree(p->buf);
+  (void)hipFree(p->cb_crc);
+  (void)hipFree(p->data);
+  delete p;
+}
+
+int mi355_softbuffer_reset_cb(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t nof_cb, void* stream)
+{
+  if (!p || sb >= p->nof_sb) return MI355_ERROR_INVALID_INPUTS;
+  // softbuffer.c:134-154 clears nof_cb buffers/data and ALL cb_crc flags
+  CHECK_HIP(hipSetDevice(p->device));
+  hipStream_t    s  = (hipStream_t)stream;
+  const uint32_t nc = std::min(nof_cb, p->max_cb);
+  if (nc) {
+    DlschResetArgs a{p->buf, SB_STRIDE, p->cb_crc, p->data, (size_t)sb * p->max_cb, nc};
+    CHECK_HIP(dlsch_launch_reset(a, s));
+  }
+  CHECK_HIP(hipMemsetAsync(p->cb_crc + (size_t)sb * p->max_cb, 0, p->max_cb, s));
+  return MI355_SUCCESS;
+}
+
+int mi355_softbuffer_reset(mi355_softbuffer_pool_t* p, uint32_t sb, void* stream)
+{
+  return mi355_softbuffer_reset_cb(p, sb, p ? p->max_cb : 0, stream);
+}
+
+int mi355_softbuffer_reset_tbs(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t tbs, void* stream)
+{
+  return mi355_softbuffer_reset_cb(p, sb, (tbs + 24) / (6144 - 24) + 1, stream); // softbuffer.c:128-132
+}
+
+int mi355_softbuffer_reset_all(mi355_softbuffer_pool_t* p, void* stream)
+{
+  if (!p) return MI355_ERROR_INVALID_INPUTS;
+  for (uint32_t i = 0; i < p->nof_sb; i++) {
+    int r = mi355_softbuffer_reset(p, i, stream);
+    if (r) return r;
+  }
+  return MI355_SUCCESS;
+}
+
+int mi355_dlsch_create(mi355_dlsch_t** q, int device)
+{
+  if (!q) return MI355_ERROR_INVALID_INPUTS;
+  CHECK_HIP(hipSetDevice(device));
+  auto* d   = new mi355_dlsch;
+  d->device = device;
+  if (hipStreamCreateWithFlags(&d->own, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&d->crc, 2 * sizeof(CrcTable)) != hipSuccess) {
+    mi355_dlsch_destroy(d);
+    return MI355_ERROR;
+  }
+  const CrcTable t[2] = {make_crc_table(0x1864CFB), make_crc_table(0x1800063)}; // CRC24A, CRC24B (crc.h:40-41)
+  if (hipMemcpy(d->crc, t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess) {
+    mi355_dlsch_destroy(d);
+    return MI355_ERROR;
+  }
+  *q = d;
+  return MI355_SUCCESS;
+}
+
+void mi355_dlsch_destroy(mi355_dlsch_t* q)
+{
+  if (!q) return;
+  (void)hipSetDevice(q->device);
+  (void)hipDeviceSynchronize();
+  for (auto& kv : q->dec) mi355_tdec_batch_destroy(kv.second);
+  for (auto& kv : q->rm) (void)hipFree(kv.second);
+  (void)hipFree(q->crc);
+  (void)hipFree(q->scratch);
+  if (q->own) (void)hipStreamDestroy(q->own);
+  delete q;
+}
+
+int mi355_dlsch_set_max_iterations(mi355_dlsch_t* q, uint32_t max_iterations)
+{
+  if (!q || max_iterations == 0) return MI355_ERROR_INVALID_INPUTS;
+  q->max_its = max_iterations;
+  return MI355_SUCCESS;
+}
+
+int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
+                           mi355_softbuffer_pool_t* pool,
+                           const int16_t*           d_e_bits,
+                           const mi355_dlsch_tb_t*  tbs,
+                           uint32_t                 ntb,
+                           uint8_t*                 d_data,
+                           int32_t*                 ret,
+                           float*                   avg_iterations,
+                           void*                    stream)
+{
+  if (!q || !pool || !tbs || !ret || (ntb && (!d_e_bits || !d_data))) return MI355_ERROR_INVALID_INPUTS;
+  if (ntb == 0) return MI355_SUCCESS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t s = stream ? (hipStream_t)stream : q->own;
+
+  // ---------------------------------------------------------------- host planning (sch.c:363-401, 503-530)
+  std::vector<TbDesc>        tbd(ntb);
+  std::map<uint32_t, Group>  groups;
+  for (uint32_t t = 0; t < ntb; t++) {
+    const mi355_dlsch_tb_t& in = tbs[t];
+    TbDesc&                 d  = tbd[t];
+    d                          = TbDesc{in.tbs, 0, 0, 0, 0, 0, 0, in.data_offset};
+    CbSegm seg;
+    if (in.softbuffer >= pool->nof_sb || in.rv > 3 || in.Qm == 0 || cbsegm(in.tbs, &seg)) {
+      d.invalid = 1;
+      continue;
+    }
+    if (in.tbs == 0 || seg.C == 0) continue;                // nothing to decode: success
+    if (seg.F || seg.C > pool->max_cb) {                   // sch.c:517-527
+      d.invalid = 1;
+      continue;
+    }
+    d.C     = seg.C;
+    d.C1    = seg.C1;
+    d.K1    = seg.K1;
+    d.K2    = seg.K2;
+    d.slot0 = in.softbuffer * pool->max_cb;
+    const uint32_t Gp = in.nof_e_bits / in.Qm, gamma = Gp % seg.C, n_e = in.Qm * (Gp / seg.C);
+    for (uint32_t cb = 0; cb < seg.C; cb++) {
+      const uint32_t K = cb < seg.C1 ? seg.K1 : seg.K2; // sch.c:387
+      uint32_t       rp = cb * n_e, n_e2 = n_e;
+      if (cb > seg.C - gamma) { // sch.c:396-399 (note: '>', the reference's off-by-one)
+        n_e2 = n_e + in.Qm;
+        rp   = (seg.C - gamma) * n_e + (cb - (seg.C - gamma)) * n_e2;
+      }
+      Group& g = groups[K];
+      g.K      = K;
+      g.cbs.push_back(CbDesc{t, cb, seg.C, seg.C == 1 ? K : K - 24, rp, n_e2, in.rv, d.slot0 + cb, in.e_offset,
+                             in.data_offset});
+      g.slots.push_back(d.slot0 + cb);
+    }
+  }
+
+  // ---------------------------------------------------------------- device scratch
+  size_t total_cb = 0, dec_bytes = 0;
+  for (auto& kv : groups) {
+    total_cb += kv.second.cbs.size();
+    dec_bytes += kv.second.cbs.size() * (kv.first / 8);
+  }
+  auto rnd = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t need = rnd(ntb * sizeof(TbDesc)) + rnd(total_cb * sizeof(CbDesc)) + rnd(total_cb * 4) +
+                      rnd(total_cb) + rnd(total_cb * 4) + rnd(dec_bytes) + rnd(ntb * 4);
+  char* base = nullptr;
+  int   r    = scratch(q, need, &base);
+  if (r) return r;
+  char* p     = base;
+  auto  carve = [&](size_t b) {
+    char* c = p;
+    p += rnd(b);
+    return c;
+  };
+  auto*     d_tb    = (TbDesc*)carve(ntb * sizeof(TbDesc));
+  auto*     d_cb    = (CbDesc*)carve(total_cb * sizeof(CbDesc));
+  auto*     d_slot  = (uint32_t*)carve(total_cb * 4);
+  auto*     d_done  = (uint8_t*)carve(total_cb);
+  auto*     d_its   = (uint32_t*)carve(total_cb * 4);
+  auto*     d_dec   = (uint8_t*)carve(dec_bytes);
+  auto*     d_ret   = (int32_t*)carve(ntb * 4);
+
+  std::vector<CbDesc>   all_cb;
+  std::vector<uint32_t> all_slot;
+  all_cb.reserve(total_cb);
+  for (auto& kv : groups) {
+    all_cb.insert(all_cb.end(), kv.second.cbs.begin(), kv.second.cbs.end());
+    all_slot.insert(all_slot.end(), kv.second.slots.begin(), kv.second.slots.end());
+  }
+  CHECK_HIP(hipMemcpyAsync(d_tb, tbd.data(), ntb * sizeof(TbDesc), hipMemcpyHostToDevice, s));
+  if (total_cb) {
+    CHECK_HIP(hipMemcpyAsync(d_cb, all_cb.data(), total_cb * sizeof(CbDesc), hipMemcpyHostToDevice, s));
+    CHECK_HIP(hipMemcpyAsync(d_slot, all_slot.data(), total_cb * 4, hipMemcpyHostToDevice, s));
+    CHECK_HIP(hipMemsetAsync(d_its, 0, total_cb * 4, s));
+  }
+
+  DlschTbArgs ta{d_tb, (int)ntb, d_data, pool->cb_crc, pool->data, d_ret, &q->crc[0]};
+  CHECK_HIP(dlsch_launch_prologue(ta, s));
+
+  // ---------------------------------------------------------------- per-K groups
+  struct Live {
+    uint32_t            K, off, n;
+    uint8_t*            dec;
+    mi355_tdec_batch_t* td;
+  };
+  std::vector<Live> live;
+  size_t            off = 0, doff = 0;
+  for (auto& kv : groups) {
+    const uint32_t K = kv.first, n = (uint32_t)kv.second.cbs.size();
+    DlschRmArgs    ra{};
+    ra.desc = d_cb + off;
+    ra.ncb  = (int)n;
+    ra.N    = 3 * K + 12;
+    for (uint32_t rv = 0; rv < 4; rv++) {
+      bool used = false;
+      for (auto& c : kv.second.cbs) used |= c.rv == rv;
+      ra.table[rv] = nullptr;
+      if (used && (r = rm_table(q, K, rv, &ra.table[rv]))) return r;
+    }
+    ra.e         = d_e_bits;
+    ra.sb        = pool->buf;
+    ra.sb_stride = SB_STRIDE;
+    ra.sb_crc    = pool->cb_crc;
+    CHECK_HIP(dlsch_launch_rm(ra, s));
+    auto it = q->dec.find(K);
+    if (it == q->dec.end()) {
+      mi355_tdec_batch_t* td = nullptr;
+      if ((r = mi355_tdec_batch_create(&td, q->device))) return r;
+      it = q->dec.emplace(K, td).first;
+    }
+    live.push_back(Live{K, (uint32_t)off, n, d_dec + doff, it->second});
+    off += n;
+    doff += (size_t)n * (K / 8);
+  }
+  // CBs already decoded in an earlier transmission start as done (before the rate matcher adds into them
+  // this is the same flag it tested)
+  if (total_cb) CHECK_HIP(dlsch_launch_init_done(d_done, d_slot, pool->cb_crc, (int)total_cb, s));
+
+  for (uint32_t h = 0; h < q->max_its; h++) {
+    for (auto& lv : live) {
+      TdecRun rq{pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, lv.n, lv.K, h, h + 1, lv.dec, lv.K / 8, s};
+      if ((r = mi355_tdec_run_internal(lv.td, rq))) return r;
+      DlschCheckArgs ca{d_cb + lv.off, (int)lv.n, lv.K, h, q->max_its, lv.dec, lv.K / 8, d_data,
+                        d_done + lv.off, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1]};
+      CHECK_HIP(dlsch_launch_check(ca, s));
+    }
+  }
+  CHECK_HIP(dlsch_launch_epilogue(ta, s));
+
+  std::vector<uint32_t> its(total_cb);
+  CHECK_HIP(hipMemcpyAsync(ret, d_ret, ntb * 4, hipMemcpyDeviceToHost, s));
+  if (total_cb) CHECK_HIP(hipMemcpyAsync(its.data(), d_its, total_cb * 4, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipStreamSynchronize(s));
+  for (uint32_t t = 0; t < ntb; t++) {
+    if (tbd[t].invalid) ret[t] = MI355_ERROR_INVALID_INPUTS;
+  }
+  if (avg_iterations) {
+    std::vector<double> sum(ntb, 0.0);
+    for (size_t i = 0; i < total_cb; i++) sum[all_cb[i].tb] += its[i];
+    for (uint32_t t = 0; t < ntb; t++) avg_iterations[t] = tbd[t].C ? (float)(sum[t] / tbd[t].C) : 0.f;
+  }
+  return MI355_SUCCESS;
+}
+
+} // extern "C"

@@ -201,8 +201,8 @@ __global__ __launch_bounds__(256) void tdec_gen_prep(TdecGenPrepArgs a)
   if (p >= a.npair) return;
   const int      K    = a.K;
   const int      c0   = 2 * p, c1 = (2 * p + 1 < a.ncb) ? 2 * p + 1 : 2 * p;
-  const int16_t* in0  = a.in + (size_t)c0 * a.stride;
-  const int16_t* in1  = a.in + (size_t)c1 * a.stride;
+  const int16_t* in0  = a.in + (size_t)(a.in_idx ? a.in_idx[c0] : c0) * a.stride;
+  const int16_t* in1  = a.in + (size_t)(a.in_idx ? a.in_idx[c1] : c1) * a.stride;
   uint32_t       s = 0, p0 = 0, p1 = 0;
   auto           pk   = [](int16_t lo, int16_t hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); };
   const size_t   o    = (size_t)p * a.Kp + k;

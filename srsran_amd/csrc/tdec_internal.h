@@ -15,6 +15,8 @@ namespace mi355 {
 struct TdecWinArgs {
   const int16_t*  in;   // caller's decoder buffers (softbuffer layout), in_stride int16 apart
   size_t          in_stride;
+  const uint32_t* in_idx; // optional: buffer index of batch code block b (default b)
+  const uint8_t*  done;   // optional: code blocks already decoded (CRC early stop) are skipped
   uint32_t*       A1;   // a-priori of DEC1 (natural order), wave-group interleaved
   uint32_t*       E;    // DEC1 extrinsic -> DEC2 input (interleaved order), wave-group interleaved
   uint32_t*       D;    // decision LLRs (natural order), wave-group interleaved
@@ -45,8 +47,9 @@ struct TdecGenArgs {
 };
 
 struct TdecGenPrepArgs {
-  const int16_t* in;
-  size_t         stride;
+  const int16_t*  in;
+  size_t          stride;
+  const uint32_t* in_idx;
   uint32_t *     S, *P0, *P1, *E;
   int            ncb, npair, K, Kp;
 };
@@ -58,6 +61,18 @@ struct TdecGenDecideArgs {
   int             ncb, K, Kp;
 };
 
+// Host-side run request used by the batched API and by the DL-SCH decoder (dlsch_runtime.cpp).
+struct TdecRun {
+  const int16_t*  in;
+  size_t          in_stride;
+  const uint32_t* in_idx; // nullable
+  const uint8_t*  done;   // nullable
+  uint32_t        n, K, h0, h1;
+  uint8_t*        out;
+  size_t          out_stride;
+  hipStream_t     stream;
+};
+
 hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s);
 hipError_t tdec_win_launch_decide(int nsb, const TdecDecideArgs& a, hipStream_t s);
 hipError_t tdec_gen_launch_prep(const TdecGenPrepArgs& a, hipStream_t s);
@@ -65,3 +80,6 @@ hipError_t tdec_gen_launch_halfit(const TdecGenArgs& a, hipStream_t s);
 hipError_t tdec_gen_launch_decide(const TdecGenDecideArgs& a, hipStream_t s);
 
 } // namespace mi355
+
+struct mi355_tdec_batch;
+int mi355_tdec_run_internal(mi355_tdec_batch* q, const mi355::TdecRun& r);

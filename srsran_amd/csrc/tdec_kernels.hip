@@ -138,6 +138,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
   const int     grp = gl >> 6, q = gl & 63;
   const int     cbg = q / NL, l = q % NL;
   if (grp * G + cbg >= a.ncb) return;
+  if (a.done && a.done[grp * G + cbg]) return; // CRC early stop: this code block is finished
 
   const int  L = a.L, Lp = a.Lp, nseg = a.nseg;
   constexpr bool dec2   = MODE == 2;
@@ -150,7 +151,8 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
   // value is always base[... + 1].
   const int       cb   = grp * G + cbg;
   const int       K    = L * NSB;
-  const uint32_t* in32 = (const uint32_t*)(a.in + (size_t)cb * a.in_stride);
+  const size_t    bidx = a.in_idx ? a.in_idx[cb] : (size_t)cb;
+  const uint32_t* in32 = (const uint32_t*)(a.in + bidx * a.in_stride);
   const size_t    wg0  = (size_t)grp * Lp * 64 + q;
   const uint32_t* X    = dec2 ? a.E + wg0 : in32 + l;
   const int       xs   = dec2 ? 64 : NL;
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
   }
   if (l == NL - 1) {
     // last window: tail trellis, wrapping arithmetic, no a-priori (turbodecoder_win.h:500-548)
-    const int16_t* T = a.in + (size_t)cb * a.in_stride + 3 * (K + 32) + (dec2 ? 6 : 0);
+    const int16_t* T = a.in + bidx * a.in_stride + 3 * (K + 32) + (dec2 ? 6 : 0);
     v2s            tr[8], tn[8];
     tr[0] = splat(0);
 #pragma unroll

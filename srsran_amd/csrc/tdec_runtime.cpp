@@ -232,17 +232,15 @@ int mi355_tdec_batch_kernel_stats(mi355_tdec_batch_t* q, double* ms, uint32_t* l
 }
 
 // Launch half-iterations [h0, h1) on the workspace; decisions after h1-1 when `decide`.
-static int run_range(mi355_tdec_batch_t* q,
-                     const int16_t*      d_in,
-                     size_t              in_stride,
-                     uint32_t            n,
-                     uint32_t            K,
-                     uint32_t            h0,
-                     uint32_t            h1,
-                     uint8_t*            d_out,
-                     size_t              out_stride,
-                     void*               stream)
+} // extern "C"
+
+int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
 {
+  const int16_t* d_in = rq.in;
+  size_t in_stride = rq.in_stride;
+  uint32_t n = rq.n, K = rq.K, h0 = rq.h0, h1 = rq.h1;
+  uint8_t* d_out = rq.out;
+  size_t out_stride = rq.out_stride;
   if (!q || !d_in || !d_out || h1 <= h0 || cb_index(K) < 0) return MI355_ERROR_INVALID_INPUTS;
   const bool generic = q->impl == MI355_TDEC_GENERIC || mi355_tdec_autoimp_get_subblocks(K) == 0;
   const size_t need  = generic ? 3 * (size_t)K + 12 : 3 * (size_t)(K + 32) + 12;
@@ -252,7 +250,7 @@ static int run_range(mi355_tdec_batch_t* q,
   if (n == 0) return MI355_SUCCESS;
   std::lock_guard<std::mutex> lock(q->mu);
   CHECK_HIP(hipSetDevice(q->device));
-  hipStream_t s = stream ? (hipStream_t)stream : q->own;
+  hipStream_t s = rq.stream ? rq.stream : q->own;
 
   const Geometry g = geometry(K, n, q->impl);
   KTables*       t = nullptr;
@@ -279,7 +277,7 @@ static int run_range(mi355_tdec_batch_t* q,
     auto*        CK  = (uint32_t*)carve((size_t)g.ngrp * g.nseg * 8 * 64 * 4);
 
     for (uint32_t h = h0; h < h1; h++) {
-      TdecWinArgs wa{d_in, in_stride, A1, E, D, CK, t->dstE, t->dstA,
+      TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, A1, E, D, CK, t->dstE, t->dstA,
                      (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == h1};
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (q->prof) {
@@ -303,7 +301,7 @@ static int run_range(mi355_tdec_batch_t* q,
     auto*        CK  = (uint32_t*)carve((size_t)g.npair * g.nseg * 32);
 
     if (h0 == 0) {
-      TdecGenPrepArgs pa{d_in, in_stride, S, P0, P1, E, (int)n, (int)g.npair, (int)K, (int)g.Kp};
+      TdecGenPrepArgs pa{d_in, in_stride, rq.in_idx, S, P0, P1, E, (int)n, (int)g.npair, (int)K, (int)g.Kp};
       CHECK_HIP(tdec_gen_launch_prep(pa, s));
     }
     for (uint32_t h = h0; h < h1; h++) {
@@ -324,6 +322,8 @@ static int run_range(mi355_tdec_batch_t* q,
   return MI355_SUCCESS;
 }
 
+extern "C" {
+
 int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
                              const int16_t*      d_in,
                              size_t              in_stride,
@@ -335,7 +335,8 @@ int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
                              void*               stream)
 {
   if (nhalf == 0) return MI355_ERROR_INVALID_INPUTS;
-  return run_range(q, d_in, in_stride, n, K, 0, nhalf, d_out, out_stride, stream);
+  return mi355_tdec_run_internal(
+      q, TdecRun{d_in, in_stride, nullptr, nullptr, n, K, 0, nhalf, d_out, out_stride, (hipStream_t)stream});
 }
 
 int mi355_tdec_batch_halfit_dev(mi355_tdec_batch_t* q,
@@ -348,7 +349,8 @@ int mi355_tdec_batch_halfit_dev(mi355_tdec_batch_t* q,
                                 size_t              out_stride,
                                 void*               stream)
 {
-  return run_range(q, d_in, in_stride, n, K, half_idx, half_idx + 1, d_out, out_stride, stream);
+  return mi355_tdec_run_internal(q, TdecRun{d_in, in_stride, nullptr, nullptr, n, K, half_idx, half_idx + 1, d_out,
+                                            out_stride, (hipStream_t)stream});
 }
 
 int mi355_tdec_batch_set_impl(mi355_tdec_batch_t* q, int impl)

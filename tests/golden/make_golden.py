@@ -12,6 +12,8 @@ Contents
   tdec_generic.npz   GENERIC manual decoder + force_not_sb on linear input (turbodecoder_test -d 1).
   tcod_known.npz     the reference test's own known-answer vector (turbodecoder_test.h:69-125).
   crc_cbsegm.npz     CRC24A/24B/16/8 checksums and CB segmentation for a TBS sweep.
+  rm_turbo.npz       srslte_rm_turbo_rx_lut (AVX build): E LLRs -> decoder buffer, every rv, E below /
+                     at / above the circular buffer (wrap-around), plus HARQ accumulation rv0 + rv2.
 """
 from __future__ import annotations
 
@@ -124,6 +126,42 @@ def gen_crc_cbsegm(rng):
     print("crc_cbsegm.npz")
 
 
+def rm_init_softbuffer():
+    """Deterministic non-zero softbuffer content (same formula in tests/golden_io.py)."""
+    i = np.arange(oracle.SOFTBUFFER_SIZE, dtype=np.int64)
+    return ((i * 7919) % 60001 - 30000).astype(np.int16)
+
+
+def gen_rm(rng):
+    L = oracle.ref()
+    data = {}
+    cases = []
+    for K in (40, 104, 512, 816, 2048, 6144):
+        N = 3 * K + 12
+        for rv in range(4):
+            for E in ((N // 3, 2 * N + 17) if K < 2048 else (7200,) if rv else (7200, N + 501)):
+                cases.append((K, rv, E))
+    for ci, (K, rv, E) in enumerate(cases):
+        e = rng.integers(-20000, 20000, E).astype(np.int16)
+        out = rm_init_softbuffer()  # non-zero softbuffer: exercises the wrapping +=
+        assert L.ref_rm_turbo_rx(e.copy(), E, out, K, rv) == 0
+        blen = 3 * (K + 32) + 12
+        assert (out[blen:] == rm_init_softbuffer()[blen:]).all()
+        data[f"c{ci}_K"], data[f"c{ci}_rv"] = np.int32(K), np.int32(rv)
+        data[f"c{ci}_e"], data[f"c{ci}_out"] = e, out[:blen]
+    data["ncases"] = np.int32(len(cases))
+    # HARQ: rv 0 then rv 2 into a zeroed buffer, K = 5312 (SISO QPSK config: E = 10000)
+    K = 5312
+    e0 = rng.integers(-300, 300, 10000).astype(np.int16)
+    e2 = rng.integers(-300, 300, 10000).astype(np.int16)
+    acc = np.zeros(oracle.SOFTBUFFER_SIZE, np.int16)  # after srslte_softbuffer_rx_reset
+    L.ref_rm_turbo_rx(e0.copy(), e0.size, acc, K, 0)
+    L.ref_rm_turbo_rx(e2.copy(), e2.size, acc, K, 2)
+    data.update(harq_K=np.int32(K), harq_e0=e0, harq_e2=e2, harq_out=acc[: 3 * (K + 32) + 12])
+    np.savez_compressed(os.path.join(OUT, "rm_turbo.npz"), **data)
+    print("rm_turbo.npz:", len(cases), "cases")
+
+
 def main():
     oracle.build(ref=True)
     if not oracle.ref_available():
@@ -133,6 +171,7 @@ def main():
     gen_tdec_generic(rng)
     gen_tcod_known()
     gen_crc_cbsegm(rng)
+    gen_rm(np.random.default_rng(1212))
 
 
 if __name__ == "__main__":

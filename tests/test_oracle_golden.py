@@ -60,3 +60,19 @@ def test_qpp_is_permutation_and_contention_free():
             w = np.arange(nsb)
             for j in range(0, L, max(1, L // 7)):
                 assert len(set(pi[w * L + j] // L)) == nsb  # windows read distinct windows
+
+
+from golden_io import rm_cases, rm_harq, rm_init_softbuffer  # noqa: E402
+
+
+@pytest.mark.parametrize("case", rm_cases(), ids=lambda c: f"K{c['K']}-rv{c['rv']}-E{c['e'].size}")
+def test_oracle_rate_dematch_matches_reference(case):
+    out = oracle.rm_turbo_rx(case["e"], case["K"], case["rv"], rm_init_softbuffer())
+    np.testing.assert_array_equal(out[: case["out"].size], case["out"])
+
+
+def test_oracle_rate_dematch_harq_accumulation():
+    h = rm_harq()
+    acc = oracle.rm_turbo_rx(h["e0"], h["K"], 0)
+    oracle.rm_turbo_rx(h["e2"], h["K"], 2, acc)
+    np.testing.assert_array_equal(acc[: h["out"].size], h["out"])
