@@ -42,7 +42,7 @@ typedef struct {
   uint32_t rv;          /* redundancy version 0..3 */
   uint32_t softbuffer;  /* softbuffer index in the pool */
   uint64_t e_offset;    /* int16 offset of the codeword's LLRs in d_e_bits */
-  uint64_t data_offset; /* byte offset of the payload in d_data */
+  uint64_t data_offset; /* byte offset of the payload in d_data (d_data == NULL: absolute device address) */
 } mi355_dlsch_tb_t;
 
 typedef struct mi355_dlsch mi355_dlsch_t;

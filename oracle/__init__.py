@@ -64,6 +64,15 @@ def lib() -> C.CDLL:
                                           i16p, u8p, u8p, u8p, C.POINTER(C.c_float)]
         L.orc_rm_turbo_tx.argtypes = [u8p, C.c_uint32, C.c_uint32, C.c_uint32, u8p]
         L.orc_dlsch_encode_tb.argtypes = [u8p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u8p]
+        L.orc_sequence_lte.argtypes = [C.c_uint32, C.c_uint32, u8p]
+        L.orc_demod_soft_s.argtypes = [C.c_int, f32p, i16p, C.c_int]
+        L.orc_scramble_s.argtypes = [C.c_uint32, i16p, C.c_uint32]
+        L.orc_csi_correction_s.argtypes = [C.c_int, i16p, f32p, C.c_uint32]
+        L.orc_pdsch_re_map.restype = C.c_uint32
+        L.orc_pdsch_re_map.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_uint32,
+                                       C.c_uint32, u8p, C.c_uint32, C.c_uint32, u32p]
+        L.orc_predecode.argtypes = [f32p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
+                                    C.c_float, f32p, f32p, f32p]
         _LIB = L
     return _LIB
 
@@ -88,6 +97,7 @@ def ref() -> C.CDLL:
         L.ref_tdec_run_batch.argtypes = [i16p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u8p, C.c_int]
         L.ref_demod_soft_s.argtypes = [C.c_int, f32p, i16p, C.c_int]
         L.ref_scramble_s.argtypes = [C.c_uint32, i16p, C.c_int, C.c_int]
+        L.ref_predecoding.argtypes = [C.c_void_p] * 10 + [C.c_int] * 6 + [C.c_float, C.c_float, C.c_int]
         _REF = L
     return _REF
 
@@ -227,6 +237,96 @@ def make_tb(rng: np.random.Generator, tbs: int, Qm: int, G: int, rv: int, snr_db
     y = np.where(coded.astype(bool), 1.0, -1.0) + sigma * rng.standard_normal(G)
     llr = np.trunc(scale * y).clip(-32768, 32767).astype(np.int16)
     return np.packbits(bits), llr
+
+
+def sequence_lte(c_init: int, n: int) -> np.ndarray:
+    c = np.zeros(n, np.uint8)
+    lib().orc_sequence_lte(c_init, n, c)
+    return c
+
+
+def demod_soft_s(qm: int, symbols: np.ndarray) -> np.ndarray:
+    iq = np.ascontiguousarray(np.asarray(symbols, np.complex64).view(np.float32))
+    out = np.zeros(qm * (iq.size // 2), np.int16)
+    assert lib().orc_demod_soft_s(qm, iq, out, iq.size // 2) == 0
+    return out
+
+
+def scramble_s(c_init: int, llr: np.ndarray) -> np.ndarray:
+    out = np.array(llr, np.int16, copy=True)
+    lib().orc_scramble_s(c_init, out, out.size)
+    return out
+
+
+def csi_correction_s(qm: int, e: np.ndarray, csi: np.ndarray) -> np.ndarray:
+    out = np.array(e, np.int16, copy=True)
+    lib().orc_csi_correction_s(qm, out, np.ascontiguousarray(csi, np.float32), out.size)
+    return out
+
+
+def pdsch_re_map(nof_prb: int, nof_ports: int, cell_id: int, prb: np.ndarray, lstart: int, sf_idx: int,
+                 tdd: bool = False, cp_ext: bool = False, nof_symb_slot=(0, 0)) -> np.ndarray:
+    """Grid indices of the PDSCH REs in srslte_pdsch_get order (pdsch.c:136-228); prb: (2, nof_prb) bool."""
+    prb = np.ascontiguousarray(np.asarray(prb, np.uint8).reshape(2, nof_prb))
+    idx = np.zeros(14 * 12 * nof_prb, np.uint32)
+    n = lib().orc_pdsch_re_map(nof_prb, nof_ports, cell_id, int(tdd), int(cp_ext), nof_symb_slot[0],
+                               nof_symb_slot[1], prb, lstart, sf_idx, idx)
+    return idx[:n].copy()
+
+
+def predecode(y: np.ndarray, h: np.ndarray, nof_layers: int, cb: int, tx_scheme: int, scaling: float,
+              noise: float):
+    """orc_predecode: y (nof_rx, n) complex64, h (nof_ports, nof_rx, n) complex64 ->
+    (x (nof_layers, n_layer) complex64, csi (2, n) float32)."""
+    y = np.ascontiguousarray(y, np.complex64)
+    nof_rx, n = y.shape
+    nof_ports = h.shape[0]
+    hh = np.zeros((nof_ports, 2, n), np.complex64)
+    hh[:, :nof_rx] = h
+    x = np.zeros((max(nof_layers, 1), n), np.complex64)
+    csi = np.zeros((2, n), np.float32)
+    r = lib().orc_predecode(y.view(np.float32), hh.view(np.float32).reshape(-1), nof_rx, nof_ports, nof_layers,
+                            cb, n, tx_scheme, scaling, noise, x.view(np.float32).reshape(-1), csi[0], csi[1])
+    if r < 0:
+        raise ValueError("orc_predecode: invalid configuration")
+    nl = n // nof_ports if tx_scheme == 1 else n
+    return x[:, :nl].copy(), csi
+
+
+def _aligned(a: np.ndarray, align: int = 64) -> np.ndarray:
+    """Copy into an `align`-byte aligned buffer (the reference's SIMD kernels use aligned loads)."""
+    a = np.asarray(a)
+    raw = np.zeros(a.nbytes + align, np.uint8)
+    off = (-raw.ctypes.data) % align
+    out = raw[off:off + a.nbytes].view(a.dtype).reshape(a.shape)
+    out[...] = a
+    return out
+
+
+def ref_predecode(y: np.ndarray, h: np.ndarray, nof_layers: int, cb: int, tx_scheme: int, scaling: float,
+                  noise: float):
+    """The reference's srslte_predecoding_type (AVX2 build) through oracle/_ref, same layout as predecode()."""
+    y = np.ascontiguousarray(y, np.complex64)
+    nof_rx, n = y.shape
+    nof_ports = h.shape[0]
+    H = [[_aligned(h[p, r].astype(np.complex64)) if p < nof_ports and r < nof_rx else None
+          for r in range(2)] for p in range(2)]
+    x = [_aligned(np.zeros(n, np.complex64)) for _ in range(2)]
+    csi = [_aligned(np.zeros(n, np.float32)) for _ in range(2)]
+    ptr = lambda a: None if a is None else a.ctypes.data
+    ys = [_aligned(y[0]), _aligned(y[1]) if nof_rx > 1 else None]
+    r = ref().ref_predecoding(ptr(ys[0]), ptr(ys[1]), ptr(H[0][0]), ptr(H[0][1]), ptr(H[1][0]), ptr(H[1][1]),
+                              ptr(x[0]), ptr(x[1]), ptr(csi[0]), ptr(csi[1]), nof_rx, nof_ports, nof_layers, cb, n,
+                              tx_scheme, scaling, noise, 1)
+    if r < 0:
+        raise ValueError("ref_predecoding failed")
+    nl = n // nof_ports if tx_scheme == 1 else n
+    return np.stack(x)[:nof_layers, :nl].copy(), np.stack(csi)
+
+
+def pdsch_c_init(rnti: int, cw: int, sf: int, cell_id: int) -> int:
+    """srslte_sequence_pdsch (phch/sequences.c:61-64) with nslot = 2*sf."""
+    return (rnti << 14) + (cw << 13) + (sf << 9) + cell_id
 
 
 # ------------------------------------------------------------------ test-vector synthesis

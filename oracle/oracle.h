@@ -33,6 +33,17 @@ int  orc_dlsch_decode_tb(const int16_t* e_bits, uint32_t nof_e_bits, uint32_t tb
 void orc_rm_turbo_tx(const uint8_t* enc, uint32_t K, uint32_t rv, uint32_t E, uint8_t* out);
 int  orc_dlsch_encode_tb(const uint8_t* payload_bits, uint32_t tbs, uint32_t Qm, uint32_t G, uint32_t rv, uint8_t* e);
 
+/* per-codeword PDSCH stages (orc_pdsch.c) */
+void orc_sequence_lte(uint32_t c_init, uint32_t len, uint8_t* c);
+int  orc_demod_soft_s(int qm, const float* iq, int16_t* llr, int nsym);
+void orc_scramble_s(uint32_t c_init, int16_t* llr, uint32_t len);
+void orc_csi_correction_s(int qm, int16_t* e, const float* csi, uint32_t nof_bits);
+uint32_t orc_pdsch_re_map(uint32_t nof_prb, uint32_t nof_ports, uint32_t cell_id, int tdd, int cp_ext,
+                          uint32_t ns0, uint32_t ns1, const uint8_t* prb, uint32_t lstart_grant, uint32_t sf_idx,
+                          uint32_t* idx);
+int orc_predecode(const float* y, const float* h, int nof_rx, int nof_ports, int nof_layers, int cb, int n,
+                  int type, float scaling, float noise, float* x, float* csi0, float* csi1);
+
 /* multi-threaded batch driver used as the CPU baseline (orc_batch.c) */
 int orc_tdec_run_batch(const int16_t* bufs, uint32_t stride, uint32_t ncb, uint32_t K, uint32_t nhalf, uint8_t* out,
                        int nthreads);

@@ -184,13 +184,15 @@ static void crc_attach_bits(uint8_t* bits, uint32_t n, uint32_t poly)
 }
 
 /* Transport block -> G coded bits (36.212 5.3.2: CRC24A, segmentation with CRC24B, turbo coding, rate
- * matching with E_r = Qm*floor(G'/C) for r < C - gamma, else Qm*ceil(G'/C)).  Code block r uses
- * K1 for r < C1 like the receiver (sch.c:387).  Returns -2 if filler bits would be needed. */
+ * matching with E_r = Qm*floor(G'/C) for r < C - gamma, else Qm*ceil(G'/C)), as the reference transmitter
+ * encode_tb_off (sch.c:250-355): code block r uses K2 (the smaller size) for r < C2, K1 after.  (Its
+ * receiver uses K1 for r < C1, so TBS with mixed block sizes -- never produced by the 36.213 TBS tables --
+ * do not round-trip in the reference either.)  Returns -2 if filler bits would be needed. */
 int orc_dlsch_encode_tb(const uint8_t* payload_bits, uint32_t tbs, uint32_t Qm, uint32_t G, uint32_t rv, uint8_t* e)
 {
   uint32_t seg[6];
   if (orc_cbsegm(tbs, seg) || seg[5]) return -2;
-  const uint32_t C = seg[0], K1 = seg[1], K2 = seg[2], C1 = seg[3];
+  const uint32_t C = seg[0], K1 = seg[1], K2 = seg[2], C2 = seg[4];
   uint8_t*       tb = malloc(tbs + 24);
   memcpy(tb, payload_bits, tbs);
   crc_attach_bits(tb, tbs, 0x1864CFB);
@@ -199,7 +201,7 @@ int orc_dlsch_encode_tb(const uint8_t* payload_bits, uint32_t tbs, uint32_t Qm, 
   uint8_t*       cbb = malloc(6144);
   uint8_t*       enc = malloc(3 * 6144 + 12);
   for (uint32_t r = 0; r < C; r++) {
-    const uint32_t K = r < C1 ? K1 : K2;
+    const uint32_t K = r < C2 ? K2 : K1;
     if (C == 1) {
       memcpy(cbb, tb, K);
     } else {

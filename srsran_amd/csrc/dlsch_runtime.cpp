@@ -240,7 +240,7 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
                            float*                   avg_iterations,
                            void*                    stream)
 {
-  if (!q || !pool || !tbs || !ret || (ntb && (!d_e_bits || !d_data))) return MI355_ERROR_INVALID_INPUTS;
+  if (!q || !pool || !tbs || !ret || (ntb && !d_e_bits)) return MI355_ERROR_INVALID_INPUTS;
   if (ntb == 0) return MI355_SUCCESS;
   std::lock_guard<std::mutex> lock(q->mu);
   CHECK_HIP(hipSetDevice(q->device));

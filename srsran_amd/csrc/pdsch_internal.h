@@ -1,0 +1,44 @@
+// srsran_amd/csrc/pdsch_internal.h -- device-side descriptors of the PDSCH front-end (pdsch_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mi355 {
+
+constexpr uint32_t PDSCH_GOLD_MAX = 14u * 12u * 110u * 8u; // longest codeword: 100+ PRB x 14 symbols x 256QAM
+
+// One PDSCH decode job after host planning.
+struct PdschJobDev {
+  const float2*   y[2];    // received grids per rx antenna
+  const float2*   h[4][2]; // channel estimates [port][rx]
+  const uint16_t* map;     // grid index of each PDSCH RE, srslte_pdsch_get order
+  float2*         d[2];    // equalised + layer-demapped symbols per codeword (q->d)
+  float*          csi[2];  // CSI per codeword symbol (q->csi)
+  uint32_t*       cmax;    // [2] running max of csi[cw] (float bits, csi >= 0)
+  uint32_t        nof_re, nof_rx, nof_ports, nof_layers, scheme, cb;
+  uint32_t        row;       // 12 * nof_prb: grid index -> OFDM symbol l'
+  uint32_t        rhob_mask; // OFDM symbols l' scaled by 1/rho_b (apply_power_allocation, pdsch.c:589-607)
+  float           rhob_inv, scaling, noise;
+  uint32_t        units;     // kernel A work items
+};
+
+// One codeword (TB) symbol -> LLR job.
+struct PdschCwDev {
+  const float2* d;
+  const float*  csi;
+  const uint32_t* cmax;
+  int16_t*      e;
+  uint32_t      nof_re, nof_bits, qm, c_init, csi_enable;
+  uint32_t      pairs; // kernel B work items: symbol pairs
+};
+
+struct PdschBlk {
+  uint32_t job;  // job / codeword index
+  uint32_t unit; // first work item of the block
+};
+
+hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, const PdschBlk* blk, uint32_t nblk, hipStream_t s);
+hipError_t pdsch_launch_llr(const PdschCwDev* cws, const PdschBlk* blk, uint32_t nblk, const uint32_t* gold,
+                            hipStream_t s);
+
+} // namespace mi355

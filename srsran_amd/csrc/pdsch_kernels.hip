@@ -1,0 +1,418 @@
+// srsran_amd/csrc/pdsch_kernels.hip -- PDSCH symbol-level front-end for gfx950.
+//
+// Kernel A (pdsch_equalize): one work item = one RE (PORT0 / spatial multiplexing / CDD), one SFBC pair
+// (2-port diversity) or quad (4-port diversity).  Gathers the received symbols and channel estimates of its
+// REs through the extraction map (srslte_pdsch_get order, pdsch.c:136-228), applies rho_b
+// (apply_power_allocation, pdsch.c:575-611), equalises with the reference's exact formulas
+// (mimo/precoding.c, utils/mat.c -- cited per case below), writes the layer-demapped symbols d[cw] and CSI,
+// and folds the CSI maximum per codeword (csi_correction's srslte_vec_max_fi, pdsch.c:653).
+//
+// Kernel B (pdsch_llr): one work item = two consecutive symbols of a codeword (the granule of the
+// reference's SIMD lane quirks in csi_correction).  int16 soft demapping exactly as the AVX2 build
+// (demod_soft.c:896-919 with its SIMD-body / scalar-tail split), descrambling with the Gold sequence
+// c_init = (rnti<<14)+(cw<<13)+(sf<<9)+id read from a linear-mask table, CSI weighting (pdsch.c:660-741).
+//
+// Both kernels are pure streaming: HBM-bound, no LDS.  Integer conversions emulate x86 semantics
+// (cvttss2si/cvtps2dq: out-of-range -> INT32_MIN) so LLRs are bit-exact for bit-exact symbols.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pdsch_internal.h"
+
+namespace mi355 {
+
+namespace {
+
+struct cf {
+  float re, im;
+};
+__device__ __forceinline__ cf mk(float r, float i) { return cf{r, i}; }
+__device__ __forceinline__ cf operator+(cf a, cf b) { return mk(a.re + b.re, a.im + b.im); }
+__device__ __forceinline__ cf operator-(cf a, cf b) { return mk(a.re - b.re, a.im - b.im); }
+__device__ __forceinline__ cf operator*(cf a, cf b) { return mk(a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re); }
+__device__ __forceinline__ cf operator*(cf a, float s) { return mk(a.re * s, a.im * s); }
+__device__ __forceinline__ cf cj(cf a) { return mk(a.re, -a.im); }
+__device__ __forceinline__ cf mulj(cf a) { return mk(-a.im, a.re); }
+__device__ __forceinline__ float abs2(cf a) { return a.re * a.re + a.im * a.im; }
+__device__ __forceinline__ cf ld(const float2* p, uint32_t i)
+{
+  const float2 v = p[i];
+  return mk(v.x, v.y);
+}
+__device__ __forceinline__ void st(float2* p, uint32_t i, cf v) { p[i] = make_float2(v.re, v.im); }
+
+// srslte_mat_2x2_mmse_csi_gen (mat.c:63-110)
+__device__ __forceinline__ void mmse_2x2_csi(cf y0, cf y1, cf h00, cf h01, cf h10, cf h11, cf& x0, cf& x1,
+                                             float& csi0, float& csi1, float noise, float norm)
+{
+  const cf c00 = cj(h00), c01 = cj(h01), c10 = cj(h10), c11 = cj(h11);
+  const cf a00 = c00 * h00 + c10 * h10 + mk(noise, 0.f);
+  const cf a01 = c00 * h01 + c10 * h11;
+  const cf a10 = c01 * h00 + c11 * h10;
+  const cf a11 = c01 * h01 + c11 * h11 + mk(noise, 0.f);
+  const cf det = a00 * a11 - a01 * a10;
+  const float dd = abs2(det);
+  const cf    nm = mk(det.re / dd, -det.im / dd) * norm; // srslte_mat_cf_recip_gen
+  const cf b00 = a11 * nm, b01 = (a01 * -1.f) * nm, b10 = (a10 * -1.f) * nm, b11 = a00 * nm;
+  const cf w00 = b00 * c00 + b01 * c01;
+  const cf w01 = b00 * c10 + b01 * c11;
+  const cf w10 = b10 * c00 + b11 * c01;
+  const cf w11 = b10 * c10 + b11 * c11;
+  x0           = y0 * w00 + y1 * w01;
+  x1           = y0 * w10 + y1 * w11;
+  csi0         = 1.0f / b00.re;
+  csi1         = 1.0f / b11.re;
+}
+
+__device__ __forceinline__ void fold_max(uint32_t* m, float v)
+{
+  // csi >= 0: IEEE order == unsigned order of the bit patterns.  Reduce over the wave first.
+  uint32_t b = __float_as_uint(v);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(m, b);
+}
+
+} // namespace
+
+__global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restrict__ jobs,
+                                                      const PdschBlk* __restrict__ blk)
+{
+  const PdschBlk  bk = blk[blockIdx.x];
+  const PdschJobDev& J = jobs[bk.job];
+  const uint32_t  u  = bk.unit + threadIdx.x;
+  const bool      live = u < J.units;
+  float           m0 = 0.f, m1 = 0.f; // per-thread csi contribution for the max
+  if (live) {
+    const uint32_t nrx = J.nof_rx;
+    auto           Y   = [&](uint32_t r, uint32_t i) {
+      const uint32_t g = J.map[i];
+      cf             v = ld(J.y[r], g);
+      if ((J.rhob_mask >> (g / J.row)) & 1u) v = v * J.rhob_inv;
+      return v;
+    };
+    auto H = [&](uint32_t p, uint32_t r, uint32_t i) { return ld(J.h[p][r], J.map[i]); };
+    switch (J.scheme) {
+      case 0: { // srslte_predecoding_single_csi scalar formula (precoding.c:345-355)
+        const uint32_t i = u;
+        cf             r = mk(0.f, 0.f);
+        float          hh = 0.f;
+        for (uint32_t p = 0; p < nrx; p++) {
+          const cf h = H(0, p, i);
+          r          = r + Y(p, i) * cj(h);
+          hh += h.re * h.re + h.im * h.im;
+        }
+        const float c = hh + J.noise, nrm = 1.0f / J.scaling;
+        st(J.d[0], i, mk(r.re * nrm / c, r.im * nrm / c));
+        J.csi[0][i] = c;
+        m0          = c;
+        break;
+      }
+      case 1: {
+        if (J.nof_ports == 2) { // srslte_predecoding_diversity_csi 2 ports (precoding.c:686-716)
+          const uint32_t i = u; // pair
+          if (i < J.nof_re / 2) {
+            float hh = 0.f;
+            cf    x0 = mk(0.f, 0.f), x1 = mk(0.f, 0.f);
+            for (uint32_t p = 0; p < nrx; p++) {
+              const cf h00 = H(0, p, 2 * i), h01 = H(0, p, 2 * i + 1), h10 = H(1, p, 2 * i), h11 = H(1, p, 2 * i + 1);
+              hh += h00.re * h00.re + h00.im * h00.im + h11.re * h11.re + h11.im * h11.im;
+              const cf r0 = Y(p, 2 * i), r1 = Y(p, 2 * i + 1);
+              if (hh == 0.f) hh = 1e-4f;
+              x0 = x0 + (cj(h00) * r0 + h11 * cj(r1));
+              x1 = x1 + ((h10 * -1.f) * cj(r0) + cj(h01) * r1);
+            }
+            J.csi[0][2 * i] = J.csi[0][2 * i + 1] = hh;
+            m0                                   = hh;
+            const float s                        = hh * J.scaling;
+            // x / hh * M_SQRT2 evaluates in double in the reference
+            st(J.d[0], 2 * i, mk((float)((double)(x0.re / s) * 1.4142135623730951), (float)((double)(x0.im / s) * 1.4142135623730951)));
+            st(J.d[0], 2 * i + 1, mk((float)((double)(x1.re / s) * 1.4142135623730951), (float)((double)(x1.im / s) * 1.4142135623730951)));
+          } else {
+            for (uint32_t k = 2 * i; k < J.nof_re; k++) {
+              st(J.d[0], k, mk(0.f, 0.f));
+              J.csi[0][k] = 0.f;
+            }
+          }
+        } else { // 4 ports (precoding.c:717-776); REs past m_ap quads are left zero
+          const uint32_t i    = u;
+          const uint32_t m_ap = (J.nof_re % 4) ? ((J.nof_re - 2) / 4) : J.nof_re / 4;
+          if (i < m_ap) {
+            cf    xv[4] = {mk(0, 0), mk(0, 0), mk(0, 0), mk(0, 0)};
+            float a[4]  = {0.f, 0.f, 0.f, 0.f};
+            for (uint32_t p = 0; p < nrx; p++) {
+#pragma unroll
+              for (int hb = 0; hb < 2; hb++) {
+                const uint32_t k   = 4 * i + 2 * hb;
+                const cf       h00 = H(hb, p, k), h01 = H(hb + 2, p, k), h10 = H(hb, p, k + 1), h11 = H(hb + 2, p, k + 1);
+                a[2 * hb] += h00.re * h00.re + h00.im * h00.im + h11.re * h11.re + h11.im * h11.im;
+                a[2 * hb + 1] += h10.re * h10.re + h10.im * h10.im + h01.re * h01.re + h01.im * h01.im;
+                const cf r0 = Y(p, k), r1 = Y(p, k + 1);
+                xv[2 * hb]     = xv[2 * hb] + (cj(h00) * r0 + h11 * cj(r1));
+                xv[2 * hb + 1] = xv[2 * hb + 1] + ((h01 * -1.f) * cj(r0) + cj(h10) * r1);
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+              const float aq = a[q] * J.scaling;
+              const float c  = aq / (float)nrx;
+              J.csi[0][4 * i + q] = c;
+              m0                  = fmaxf(m0, c);
+              st(J.d[0], 4 * i + q,
+                 mk((float)((double)(xv[q].re / aq) * 1.4142135623730951), (float)((double)(xv[q].im / aq) * 1.4142135623730951)));
+            }
+          } else {
+            for (uint32_t k = 4 * i; k < min(J.nof_re, 4 * i + 4); k++) {
+              st(J.d[0], k, mk(0.f, 0.f));
+              J.csi[0][k] = 0.f;
+            }
+          }
+        }
+        break;
+      }
+      case 2: {
+        const uint32_t i = u;
+        if (J.nof_layers == 2) { // srslte_predecoding_multiplex_2x2_mmse_csi (precoding.c:1519-1548)
+          const float norm = J.cb == 0 ? 0x1.6a09e6p+0f / J.scaling : 2.0f / J.scaling;
+          cf          h00, h01, h10, h11;
+          const cf    g00 = H(0, 0, i), g01 = H(0, 1, i), g10 = H(1, 0, i), g11 = H(1, 1, i);
+          if (J.cb == 0) {
+            h00 = g00, h01 = g10, h10 = g01, h11 = g11;
+          } else if (J.cb == 1) {
+            h00 = g00 + g10, h01 = g00 - g10, h10 = g01 + g11, h11 = g01 - g11;
+          } else {
+            h00 = g00 + mulj(g10), h01 = g00 - mulj(g10), h10 = g01 + mulj(g11), h11 = g01 - mulj(g11);
+          }
+          cf    x0, x1;
+          float c0, c1;
+          mmse_2x2_csi(Y(0, i), Y(1, i), h00, h01, h10, h11, x0, x1, c0, c1, J.noise, norm);
+          st(J.d[0], i, x0);
+          st(J.d[1], i, x1);
+          J.csi[0][i] = c0;
+          J.csi[1][i] = c1;
+          m0          = c0;
+          m1          = c1;
+        } else { // srslte_predecoding_multiplex_2x1_mrc_csi (precoding.c:1786-1820)
+          const float norm = 0x1.6a09e6p+0f / J.scaling;
+          cf          h[2];
+#pragma unroll
+          for (int r = 0; r < 2; r++) {
+            const cf a = H(0, r, i), b = H(1, r, i);
+            h[r] = J.cb == 0 ? a + b : J.cb == 1 ? a - b : J.cb == 2 ? a + mulj(b) : a - mulj(b);
+          }
+          const float c  = h[0].re * h[0].re + h[0].im * h[0].im + h[1].re * h[1].re + h[1].im * h[1].im;
+          const float hh = norm / c;
+          st(J.d[0], i, (cj(h[0]) * Y(0, i) + cj(h[1]) * Y(1, i)) * hh);
+          const float cv = (float)((double)(c / norm) * 0.70710678118654752);
+          J.csi[0][i]    = cv;
+          m0             = cv;
+        }
+        break;
+      }
+      case 3: { // srslte_predecoding_ccd_2x2_mmse_csi (precoding.c:1111-1128)
+        const uint32_t i  = u;
+        const cf       s0 = H(0, 0, i), s1 = H(1, 0, i), t0 = H(0, 1, i), t1 = H(1, 1, i);
+        cf             h00, h01, h10, h11;
+        if ((i & 1u) == 0) {
+          h00 = s0 + s1, h10 = t0 + t1, h01 = s0 - s1, h11 = t0 - t1;
+        } else {
+          h00 = s0 - s1, h10 = t0 - t1, h01 = s0 + s1, h11 = t0 + t1;
+        }
+        cf    x0, x1;
+        float c0, c1;
+        mmse_2x2_csi(Y(0, i), Y(1, i), h00, h01, h10, h11, x0, x1, c0, c1, J.noise, 2.0f / J.scaling);
+        st(J.d[0], i, x0);
+        st(J.d[1], i, x1);
+        J.csi[0][i] = c0;
+        J.csi[1][i] = c1;
+        m0          = c0;
+        m1          = c1;
+        break;
+      }
+    }
+  }
+  fold_max(&J.cmax[0], m0);
+  if (J.nof_layers == 2 && J.scheme >= 2) fold_max(&J.cmax[1], m1);
+}
+
+// ---------------------------------------------------------------------------- LLRs
+
+namespace {
+
+__device__ __forceinline__ int32_t x86_cvt_i32(float r) // r already rounded; cvt*ps2dq out-of-range rule
+{
+  return (r >= -2147483648.0f && r < 2147483648.0f) ? (int32_t)r : INT32_MIN;
+}
+__device__ __forceinline__ int16_t sat16(int32_t v) { return (int16_t)max(-32768, min(32767, v)); }
+__device__ __forceinline__ int16_t f2s_trunc(float v) { return (int16_t)(uint16_t)(uint32_t)x86_cvt_i32(truncf(v)); }
+__device__ __forceinline__ int16_t abs16(int16_t v) { return (int16_t)(v < 0 ? (uint16_t)(-(int32_t)v) : (uint16_t)v); }
+__device__ __forceinline__ int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }
+
+// LLRs of symbol s (of n) for modulation order qm, as srslte_demod_soft_demodulate_s (AVX2 build)
+__device__ __forceinline__ void demod_symbol(uint32_t qm, cf x, uint32_t s, uint32_t n, int16_t* o)
+{
+  switch (qm) {
+    case 1: {
+      const float  t = -100.0f * (x.re + x.im);
+      const double v = (double)t * 0.70710678118654752440;
+      o[0]           = (int16_t)(uint16_t)(uint32_t)((v >= -2147483648.0 && v < 2147483648.0) ? (int32_t)v : INT32_MIN);
+      break;
+    }
+    case 2: { // srslte_vec_convert_fi: SIMD body (trunc + saturate) over the first n2 - n2 % 16 values
+      const float    sc   = -0x1.1ad7bcp+7f; // (float)(-100 * M_SQRT2)
+      const uint32_t body = 2 * n - (2 * n) % 16;
+      const float    a = x.re * sc, b = x.im * sc;
+      o[0] = 2 * s < body ? sat16(x86_cvt_i32(truncf(a))) : f2s_trunc(a);
+      o[1] = 2 * s + 1 < body ? sat16(x86_cvt_i32(truncf(b))) : f2s_trunc(b);
+      break;
+    }
+    case 4: {
+      if (s < n - n % 4) { // demod_16qam_lte_s_sse (demod_soft.c:273-322)
+        const int16_t a = sat16(x86_cvt_i32(rintf(x.re * -400.0f))), b = sat16(x86_cvt_i32(rintf(x.im * -400.0f)));
+        o[0] = a;
+        o[1] = b;
+        o[2] = wrap16(abs16(a) - 252);
+        o[3] = wrap16(abs16(b) - 252);
+      } else {
+        const int16_t yre = f2s_trunc(400.0f * x.re), yim = f2s_trunc(400.0f * x.im);
+        const float   off = 0x1.f9f6e4p+7f; // 2 * 400 / sqrtf(10)
+        o[0]              = (int16_t)-yre;
+        o[1]              = (int16_t)-yim;
+        o[2]              = f2s_trunc((float)abs((int)yre) - off);
+        o[3]              = f2s_trunc((float)abs((int)yim) - off);
+      }
+      break;
+    }
+    case 6: {
+      if (s < n - n % 4) { // demod_64qam_lte_s_sse (demod_soft.c:594-669)
+        const int16_t a = sat16(x86_cvt_i32(rintf(x.re * -700.0f))), b = sat16(x86_cvt_i32(rintf(x.im * -700.0f)));
+        const int16_t a1 = wrap16(abs16(a) - 432), b1 = wrap16(abs16(b) - 432);
+        o[0] = a;
+        o[1] = b;
+        o[2] = a1;
+        o[3] = b1;
+        o[4] = wrap16(abs16(a1) - 216);
+        o[5] = wrap16(abs16(b1) - 216);
+      } else {
+        const int16_t yre = f2s_trunc(700.0f * x.re), yim = f2s_trunc(700.0f * x.im);
+        o[0] = (int16_t)-yre;
+        o[1] = (int16_t)-yim;
+        o[2] = (int16_t)((int16_t)abs((int)yre) - 432);
+        o[3] = (int16_t)((int16_t)abs((int)yim) - 432);
+        o[4] = (int16_t)((int16_t)abs((int)o[2]) - 216);
+        o[5] = (int16_t)((int16_t)abs((int)o[3]) - 216);
+      }
+      break;
+    }
+    case 8: { // demod_256qam_lte_s (demod_soft.c:849-869)
+      float re = -x.re, im = -x.im;
+      const float k8 = 0x1.3a261cp-1f, k4 = 0x1.3a261cp-2f, k2 = 0x1.3a261cp-3f; // {8,4,2} / sqrtf(170)
+      o[0] = f2s_trunc(1000.0f * re);
+      o[1] = f2s_trunc(1000.0f * im);
+      re   = fabsf(re) - k8;
+      im   = fabsf(im) - k8;
+      o[2] = f2s_trunc(1000.0f * re);
+      o[3] = f2s_trunc(1000.0f * im);
+      re   = fabsf(re) - k4;
+      im   = fabsf(im) - k4;
+      o[4] = f2s_trunc(1000.0f * re);
+      o[5] = f2s_trunc(1000.0f * im);
+      re   = fabsf(re) - k2;
+      im   = fabsf(im) - k2;
+      o[6] = f2s_trunc(1000.0f * re);
+      o[7] = f2s_trunc(1000.0f * im);
+      break;
+    }
+  }
+}
+
+__device__ __forceinline__ int16_t mulhi16(int16_t a, int16_t b) { return (int16_t)(((int32_t)a * (int32_t)b) >> 16); }
+
+} // namespace
+
+__global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ cws, const PdschBlk* __restrict__ blk,
+                                                 const uint32_t* __restrict__ gold)
+{
+  const PdschBlk    bk = blk[blockIdx.x];
+  const PdschCwDev& C  = cws[bk.job];
+  const uint32_t    pr = bk.unit + threadIdx.x;
+  if (pr >= C.pairs) return;
+  const uint32_t qm = C.qm, n = C.nof_re;
+  const uint32_t s0 = 2 * pr, ns = min(2u, n - s0);
+  int16_t        o[16];
+  float          csi[2] = {0.f, 0.f};
+  for (uint32_t k = 0; k < ns; k++) {
+    demod_symbol(qm, ld(C.d, s0 + k), s0 + k, n, &o[k * qm]);
+    if (C.csi_enable) csi[k] = C.csi[s0 + k];
+  }
+  // descrambling: c(k) = x1(k+Nc) ^ <mask(k+Nc), c_init> (srslte_scrambling_s_offset, scrambling.c:43-47)
+  const uint32_t b0 = s0 * qm, nb = ns * qm;
+  for (uint32_t k = 0; k < nb; k++) {
+    const uint32_t g = gold[b0 + k];
+    const uint32_t c = (g >> 31) ^ (__popc(g & C.c_init & 0x7fffffffu) & 1u);
+    if (c) o[k] = (int16_t)(uint16_t)(-(int32_t)o[k]);
+  }
+  if (C.csi_enable) { // csi_correction (pdsch.c:628-741), SSE path
+    const uint32_t nsym   = C.nof_bits / qm;
+    const float    cmax   = nsym ? __uint_as_float(*C.cmax) : 1.0f;
+    const float    scale  = 32767.0f / cmax;
+    const bool     pair   = ns == 2;
+    auto           CV     = [&](float v) { return sat16(x86_cvt_i32(rintf(v * scale))); }; // _mm_cvtps_pi16
+    bool           body;
+    switch (qm) {
+      case 2: body = pair; break;
+      case 4: body = true; break;
+      case 6: body = pair; break;
+      case 8: body = true; break;
+      default: body = false; break;
+    }
+    if (body) {
+      if (qm == 2) { // _mm_blend_ps(csi1, csi2, 3): the pair's LLR lanes 0,1 take the second symbol's CSI
+        const int16_t c0 = CV(csi[0]), c1 = CV(csi[1]);
+        o[0] = mulhi16(o[0], c1);
+        o[1] = mulhi16(o[1], c1);
+        o[2] = mulhi16(o[2], c0);
+        o[3] = mulhi16(o[3], c0);
+      } else if (qm == 6) {
+        const int16_t c1 = CV(csi[0]), c3 = CV(csi[1]);
+#pragma unroll
+        for (int k = 0; k < 4; k++) o[k] = mulhi16(o[k], c1);
+        o[4] = mulhi16(o[4], c3);
+        o[5] = mulhi16(o[5], c3);
+        o[6] = mulhi16(o[6], c1);
+        o[7] = mulhi16(o[7], c1);
+#pragma unroll
+        for (int k = 8; k < 12; k++) o[k] = mulhi16(o[k], c3);
+      } else {
+        for (uint32_t k = 0; k < ns; k++) {
+          const int16_t c = CV(csi[k]);
+          for (uint32_t b = 0; b < qm; b++) o[k * qm + b] = mulhi16(o[k * qm + b], c);
+        }
+      }
+    } else {
+      for (uint32_t k = 0; k < ns; k++) {
+        const float c = csi[k] / cmax;
+        for (uint32_t b = 0; b < qm; b++) o[k * qm + b] = f2s_trunc((float)o[k * qm + b] * c);
+      }
+    }
+  }
+  int16_t* e = C.e + b0;
+  for (uint32_t k = 0; k < nb; k++) e[k] = o[k];
+}
+
+hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, const PdschBlk* blk, uint32_t nblk, hipStream_t s)
+{
+  if (!nblk) return hipSuccess;
+  hipLaunchKernelGGL(pdsch_equalize, dim3(nblk), dim3(256), 0, s, jobs, blk);
+  return hipGetLastError();
+}
+
+hipError_t pdsch_launch_llr(const PdschCwDev* cws, const PdschBlk* blk, uint32_t nblk, const uint32_t* gold,
+                            hipStream_t s)
+{
+  if (!nblk) return hipSuccess;
+  hipLaunchKernelGGL(pdsch_llr, dim3(nblk), dim3(256), 0, s, cws, blk, gold);
+  return hipGetLastError();
+}
+
+} // namespace mi355

@@ -1,0 +1,532 @@
+// srsran_amd/csrc/pdsch_runtime.cpp -- host runtime behind include/srsran_amd/pdsch.h.
+//
+// A batch of srslte_pdsch_decode calls (pdsch.c:907-1072) runs as
+//   kernel A (RE gather + rho_b + equaliser + layer demap + CSI max)   one launch for the whole batch
+//   kernel B (demapper + descrambler + CSI weighting)                  one launch for every codeword
+//   DL-SCH batch decode (dlsch_runtime.cpp)                            rate dematch, turbo, CRCs
+// The host only plans: extraction maps are built once per (grant allocation, cfi, subframe) and cached in
+// HBM, job / codeword descriptors and block tables are uploaded with one copy each.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+#include <vector>
+
+#include "../../include/srsran_amd/dlsch.h"
+#include "../../include/srsran_amd/pdsch.h"
+#include "../../include/srsran_amd/tdec.h"
+#include "pdsch_internal.h"
+
+using namespace mi355;
+
+#define CHECK_HIP(x)                                                                                                   \
+  do {                                                                                                                 \
+    hipError_t e_ = (x);                                                                                               \
+    if (e_ != hipSuccess) {                                                                                            \
+      fprintf(stderr, "[srsran_amd] %s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));                 \
+      return MI355_ERROR;                                                                                              \
+    }                                                                                                                  \
+  } while (0)
+
+namespace {
+
+// 36.213 Table 5.2-1 rho_B / rho_A (pdsch.c:44-46)
+const float kCellSpecificRatio[2][4] = {{1.0f / 1.0f, 4.0f / 5.0f, 3.0f / 5.0f, 2.0f / 5.0f},
+                                        {5.0f / 4.0f, 1.0f / 1.0f, 3.0f / 4.0f, 1.0f / 2.0f}};
+
+uint32_t nsymb_of(const mi355_cell_t& c) { return c.cp == MI355_CP_EXT ? 6 : 7; }
+
+// pdsch_cp_skip_symbol (pdsch.c:83-114)
+bool skip_symbol(const mi355_cell_t& c, const uint32_t ns[2], uint32_t sf, uint32_t s, uint32_t l, uint32_t n)
+{
+  if (!(n >= c.nof_prb / 2 - 3 && n < c.nof_prb / 2 + 3 + (c.nof_prb % 2))) return false;
+  if (c.frame_type == MI355_FDD) {
+    if (s == 0 && (sf == 0 || sf == 5) && l >= ns[s] - 2) return true;
+  } else {
+    if (s == 1 && (sf == 0 || sf == 5) && l >= ns[s] - 1) return true;
+    if (s == 0 && (sf == 1 || sf == 6) && l == 2) return true;
+  }
+  return s == 1 && sf == 0 && l < 4;
+}
+
+// The extraction order of srslte_pdsch_cp(get) (pdsch.c:136-228): per slot, per OFDM symbol from the first
+// non-control one, per allocated PRB; CRS REs skipped as prb_cp_ref does (prb_dl.c:46-74: `offset` REs, then
+// nof_intervals-1 times {skip 1, copy 12/nof_refs-1}, then {skip 1, copy interval-offset} if positive);
+// PSS/SSS/PBCH PRBs dropped except their outer halves for odd bandwidths.
+template <class Emit> uint32_t walk_map(const mi355_cell_t& c, const mi355_pdsch_grant_t& g, uint32_t cfi, uint32_t sf,
+                                        Emit emit)
+{
+  const uint32_t ns[2]    = {g.nof_symb_slot[0] ? g.nof_symb_slot[0] : nsymb_of(c),
+                             g.nof_symb_slot[1] ? g.nof_symb_slot[1] : nsymb_of(c)};
+  const uint32_t nof_refs = c.nof_ports == 1 ? 2 : 4;
+  const uint32_t lstart0  = cfi + (c.nof_prb < 10 ? 1 : 0); // SRSLTE_NOF_CTRL_SYMBOLS
+  const int      ri       = 12 / (int)nof_refs - 1;
+  uint32_t       k        = 0;
+  auto           cp_ref   = [&](uint32_t p, int off, int intervals) {
+    for (int i = 0; i < off; i++) emit(k++, p++);
+    for (int j = 0; j < intervals - 1; j++) {
+      p++;
+      for (int i = 0; i < ri; i++) emit(k++, p++);
+    }
+    if (ri - off > 0) {
+      p++;
+      for (int i = 0; i < ri - off; i++) emit(k++, p++);
+    }
+  };
+  for (uint32_t s = 0; s < 2; s++) {
+    for (uint32_t l = s == 0 ? lstart0 : 0; l < ns[s]; l++) {
+      const uint32_t nsymb_cp = nsymb_of(c);
+      const bool     has_crs  = (l == 1 && c.nof_ports == 4) || l == 0 || l == nsymb_cp - 3; // SRSLTE_SYMBOL_HAS_REF
+      const int      off      = !has_crs ? 0
+                                : c.nof_ports == 1 ? (int)(l == 0 ? c.id % 6 : (c.id + 3) % 6)
+                                                   : (int)(c.id % 3); // pdsch_cp_crs_offset
+      const uint32_t lp = l + s * ns[0];
+      for (uint32_t n = 0; n < c.nof_prb; n++) {
+        if (!g.prb_idx[s][n]) continue;
+        uint32_t p = (lp * c.nof_prb + n) * 12;
+        if (!skip_symbol(c, ns, sf, s, l, n)) {
+          if (has_crs) {
+            cp_ref(p, off, (int)nof_refs);
+          } else {
+            for (uint32_t i = 0; i < 12; i++) emit(k++, p + i);
+          }
+        } else if (c.nof_prb % 2) {
+          if (n == c.nof_prb / 2 - 3 || n == c.nof_prb / 2 + 3) {
+            if (n == c.nof_prb / 2 + 3) p += 6;
+            if (has_crs) {
+              cp_ref(p, off, (int)nof_refs / 2);
+            } else {
+              for (uint32_t i = 0; i < 6; i++) emit(k++, p + i);
+            }
+          }
+        }
+      }
+    }
+  }
+  return k;
+}
+
+// Gold sequence table (36.211 7.2, Nc = 1600): for sequence position k, bit 31 = x1(k + Nc) (x1 does not
+// depend on c_init) and bits 0..30 the GF(2) linear form of x2(k + Nc) over the bits of c_init, so
+// c(k) = bit31 ^ parity(mask & c_init).
+std::vector<uint32_t> gold_table(uint32_t len)
+{
+  std::vector<uint32_t> t(len);
+  uint32_t              x1 = 1, m[31];
+  for (int i = 0; i < 31; i++) m[i] = 1u << i;
+  for (uint32_t n = 0; n < 1600 + len; n++) {
+    if (n >= 1600) t[n - 1600] = ((x1 & 1u) << 31) | m[0];
+    const uint32_t f1 = ((x1 >> 3) ^ x1) & 1u;
+    const uint32_t f2 = m[3] ^ m[2] ^ m[1] ^ m[0];
+    x1                = (x1 >> 1) | (f1 << 30);
+    for (int i = 0; i < 30; i++) m[i] = m[i + 1];
+    m[30] = f2;
+  }
+  return t;
+}
+
+uint32_t mod_bits(uint32_t mod)
+{
+  switch (mod) {
+    case MI355_MOD_BPSK: return 1;
+    case MI355_MOD_QPSK: return 2;
+    case MI355_MOD_16QAM: return 4;
+    case MI355_MOD_64QAM: return 6;
+    case MI355_MOD_256QAM: return 8;
+  }
+  return 0;
+}
+
+struct JobPlan {
+  PdschJobDev dev{};
+  uint32_t    cw_of_tb[2]{};
+  size_t      d_off[2]{}, csi_off[2]{}, e_off[2]{}; // element offsets in the arenas
+  bool        decode[2]{};
+};
+
+} // namespace
+
+struct mi355_pdsch {
+  int                                  device = 0;
+  mi355_cell_t                         cell{};
+  uint32_t                             nof_rx = 1;
+  hipStream_t                          own    = nullptr;
+  mi355_dlsch_t*                       dlsch  = nullptr;
+  uint32_t                             max_its = 10; // SRSLTE_PDSCH_MAX_TDEC_ITERS
+  uint32_t*                            gold   = nullptr;
+  std::map<std::string, std::pair<uint16_t*, uint32_t>> maps; // extraction maps in HBM + RE count
+  char*                                scratch = nullptr;
+  size_t                               scratch_cap = 0;
+  std::vector<JobPlan>                 last; // plans of the last call (debug_stage)
+  float2*                              d_arena   = nullptr;
+  float*                               csi_arena = nullptr;
+  int16_t*                             e_arena   = nullptr;
+  std::mutex                           mu;
+};
+
+static int get_scratch(mi355_pdsch_t* q, size_t bytes, char** p)
+{
+  if (bytes > q->scratch_cap) {
+    if (q->scratch) {
+      CHECK_HIP(hipDeviceSynchronize());
+      CHECK_HIP(hipFree(q->scratch));
+      q->scratch = nullptr;
+    }
+    const size_t cap = bytes + bytes / 4 + 4096;
+    CHECK_HIP(hipMalloc(&q->scratch, cap));
+    q->scratch_cap = cap;
+  }
+  *p = q->scratch;
+  return MI355_SUCCESS;
+}
+
+static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi, uint32_t sf, const uint16_t** out,
+                   uint32_t* count)
+{
+  std::string key;
+  key.reserve(16 + 2 * q->cell.nof_prb);
+  const uint32_t hdr[4] = {cfi, sf, g.nof_symb_slot[0], g.nof_symb_slot[1]};
+  key.append((const char*)hdr, sizeof(hdr));
+  key.append((const char*)g.prb_idx[0], q->cell.nof_prb);
+  key.append((const char*)g.prb_idx[1], q->cell.nof_prb);
+  auto it = q->maps.find(key);
+  if (it == q->maps.end()) {
+    if (q->maps.size() >= 8192) { // bound the cache
+      CHECK_HIP(hipDeviceSynchronize());
+      for (auto& kv : q->maps) (void)hipFree(kv.second.first);
+      q->maps.clear();
+    }
+    std::vector<uint16_t> idx;
+    idx.reserve(14 * 12 * q->cell.nof_prb);
+    walk_map(q->cell, g, cfi, sf, [&](uint32_t, uint32_t p) { idx.push_back((uint16_t)p); });
+    uint16_t*      d = nullptr;
+    const uint32_t n = (uint32_t)idx.size();
+    CHECK_HIP(hipMalloc(&d, std::max<size_t>(n, 1) * sizeof(uint16_t)));
+    if (n) CHECK_HIP(hipMemcpy(d, idx.data(), n * 2, hipMemcpyHostToDevice));
+    it = q->maps.emplace(key, std::make_pair(d, n)).first;
+  }
+  *out   = it->second.first;
+  *count = it->second.second;
+  return MI355_SUCCESS;
+}
+
+// host planning of one job; returns <0 when srslte_pdsch_decode would fail before decoding
+static int plan_job(mi355_pdsch_t* q, const mi355_pdsch_job_t& j, const mi355_pdsch_res_t* res, JobPlan& P)
+{
+  const mi355_pdsch_cfg_t&   cfg = j.cfg;
+  const mi355_pdsch_grant_t& g   = cfg.grant;
+  const mi355_cell_t&        c   = q->cell;
+  PdschJobDev&               D   = P.dev;
+  if (j.sf.cfi < 1 || j.sf.cfi > 3 || g.nof_layers == 0 || g.nof_layers > 4 || g.nof_tb == 0 || g.nof_tb > 2 ||
+      g.nof_layers < g.nof_tb)
+    return MI355_ERROR_INVALID_INPUTS;
+  // equaliser configurations (precoding.c:1876-1938 with MMSE and csi)
+  const uint32_t sch = g.tx_scheme, L = g.nof_layers, np = c.nof_ports, nrx = q->nof_rx;
+  const uint32_t cb  = g.nof_tb == 1 ? g.pmi : g.pmi + 1;
+  bool           ok  = false;
+  switch (sch) {
+    case MI355_TXSCHEME_PORT0: ok = np == 1 && L == 1; break;
+    case MI355_TXSCHEME_DIVERSITY: ok = (np == 2 || np == 4) && L == np && g.nof_tb == 1; break;
+    case MI355_TXSCHEME_SPATIALMUX:
+      ok = np == 2 && nrx == 2 && L == g.nof_tb && ((L == 2 && cb <= 2) || (L == 1 && cb <= 3));
+      break;
+    case MI355_TXSCHEME_CDD: ok = np == 2 && nrx == 2 && L == 2 && g.nof_tb == 2; break;
+  }
+  if (!ok) return MI355_ERROR;
+  for (uint32_t r = 0; r < nrx; r++) {
+    if (!j.sf_symbols[r]) return MI355_ERROR_INVALID_INPUTS;
+    for (uint32_t p = 0; p < np; p++)
+      if (!j.ce[p][r]) return MI355_ERROR_INVALID_INPUTS;
+  }
+  uint32_t nre = 0;
+  int      rr  = get_map(q, g, j.sf.cfi, j.sf.tti % 10, &D.map, &nre);
+  if (rr) return rr;
+  if (nre != g.nof_re) return MI355_ERROR; // "Error expecting %d symbols but got %d" (pdsch.c:949-960)
+
+  // power allocation (pdsch.c:575-611, 926-932)
+  float scaling = 1.0f, rhob_inv = 1.0f;
+  uint32_t rmask = 0;
+  if (cfg.power_scale) {
+    if (cfg.p_b > 3) return MI355_ERROR_INVALID_INPUTS;
+    const float rho_a = (float)((double)powf(10.0f, cfg.p_a / 20.0f) * (np == 1 ? 1.0 : 1.4142135623730951));
+    const float rho_b = sqrtf(kCellSpecificRatio[np == 1 ? 0 : 1][cfg.p_b]);
+    if (rho_b != 0.0f && rho_b != 1.0f) {
+      rhob_inv          = 1.0f / rho_b;
+      const uint32_t ns = g.nof_symb_slot[0] ? g.nof_symb_slot[0] : nsymb_of(c);
+      for (uint32_t s = 0; s < 2; s++) {
+        rmask |= 1u << (s * ns + 0);
+        rmask |= 1u << (s * ns + (c.cp == MI355_CP_NORM ? 4 : 3));
+        if (np == 4) rmask |= 1u << (s * ns + 1);
+      }
+    }
+    if (rho_a != 0.0f && std::isnormal(rho_a)) scaling = rho_a;
+  }
+  for (uint32_t r = 0; r < nrx; r++) {
+    D.y[r] = (const float2*)j.sf_symbols[r];
+    for (uint32_t p = 0; p < np; p++) D.h[p][r] = (const float2*)j.ce[p][r];
+  }
+  D.nof_re     = nre;
+  D.nof_rx     = nrx;
+  D.nof_ports  = np;
+  D.nof_layers = L;
+  D.scheme     = sch;
+  D.cb         = cb;
+  D.row        = 12 * c.nof_prb;
+  D.rhob_mask  = rmask;
+  D.rhob_inv   = rhob_inv;
+  D.scaling    = scaling;
+  D.noise      = cfg.decoder_type == MI355_MIMO_DECODER_ZF ? 0.0f : j.noise_estimate;
+  D.units      = sch == MI355_TXSCHEME_DIVERSITY ? (np == 2 ? (nre + 1) / 2 : (nre + 3) / 4) : nre;
+  for (uint32_t t = 0; t < 2; t++) {
+    const mi355_ra_tb_t& tb = g.tb[t];
+    P.decode[t]             = tb.enabled && !(res && res[t].crc);
+    if (!P.decode[t]) continue;
+    P.cw_of_tb[t] = tb.cw_idx;
+    if (tb.cw_idx > 1 || mod_bits(tb.mod) == 0 || tb.nof_bits != nre * mod_bits(tb.mod) ||
+        tb.nof_bits > PDSCH_GOLD_MAX || cfg.softbuffer[t] == UINT32_MAX || !j.payload[t])
+      return MI355_ERROR_INVALID_INPUTS;
+  }
+  return MI355_SUCCESS;
+}
+
+// front-end over planned jobs; fills P.d_off/csi_off/e_off and runs kernels A and B on s
+static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::vector<JobPlan>& plans, hipStream_t s)
+{
+  const uint32_t njobs = (uint32_t)plans.size();
+  size_t         nd = 0, ne = 0;
+  std::vector<PdschCwDev> cws;
+  std::vector<PdschBlk>   blkA, blkB;
+  for (uint32_t i = 0; i < njobs; i++) {
+    JobPlan& P = plans[i];
+    for (uint32_t cw = 0; cw < 2; cw++) {
+      P.d_off[cw] = P.csi_off[cw] = nd;
+      nd += (P.dev.nof_re + 63) / 64 * 64;
+    }
+    for (uint32_t u = 0; u < P.dev.units; u += 256) blkA.push_back(PdschBlk{i, u});
+  }
+  for (uint32_t i = 0; i < njobs; i++) {
+    JobPlan& P = plans[i];
+    for (uint32_t t = 0; t < 2; t++) {
+      if (!P.decode[t]) continue;
+      const mi355_ra_tb_t& tb = jobs[i].cfg.grant.tb[t];
+      P.e_off[t]              = ne;
+      ne += (tb.nof_bits + 63) / 64 * 64;
+    }
+  }
+  // scratch: jobs | cws | blkA | blkB | cmax | d | csi | e
+  for (uint32_t i = 0; i < njobs; i++) {
+    for (uint32_t t = 0; t < 2; t++) {
+      if (!plans[i].decode[t]) continue;
+      PdschCwDev c{};
+      c.nof_re = plans[i].dev.nof_re;
+      const mi355_ra_tb_t& tb = jobs[i].cfg.grant.tb[t];
+      c.nof_bits              = tb.nof_bits;
+      c.qm                    = mod_bits(tb.mod);
+      c.c_init   = ((uint32_t)jobs[i].cfg.rnti << 14) + (tb.cw_idx << 13) + ((jobs[i].sf.tti % 10) << 9) + q->cell.id;
+      c.csi_enable = jobs[i].cfg.csi_enable ? 1u : 0u;
+      c.pairs      = (c.nof_re + 1) / 2;
+      const uint32_t ci = (uint32_t)cws.size();
+      for (uint32_t u = 0; u < c.pairs; u += 256) blkB.push_back(PdschBlk{ci, u});
+      cws.push_back(c);
+    }
+  }
+  auto         rnd  = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t need = rnd(njobs * sizeof(PdschJobDev)) + rnd(cws.size() * sizeof(PdschCwDev)) +
+                      rnd(blkA.size() * sizeof(PdschBlk)) + rnd(blkB.size() * sizeof(PdschBlk)) + rnd(njobs * 8) +
+                      rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2);
+  char* base = nullptr;
+  int   r    = get_scratch(q, need, &base);
+  if (r) return r;
+  char* p     = base;
+  auto  carve = [&](size_t b) {
+    char* c = p;
+    p += rnd(b);
+    return c;
+  };
+  auto* d_jobs = (PdschJobDev*)carve(njobs * sizeof(PdschJobDev));
+  auto* d_cws  = (PdschCwDev*)carve(cws.size() * sizeof(PdschCwDev));
+  auto* d_blkA = (PdschBlk*)carve(blkA.size() * sizeof(PdschBlk));
+  auto* d_blkB = (PdschBlk*)carve(blkB.size() * sizeof(PdschBlk));
+  auto* d_cmax = (uint32_t*)carve(njobs * 8);
+  q->d_arena   = (float2*)carve(nd * 8);
+  q->csi_arena = (float*)carve(nd * 4);
+  q->e_arena   = (int16_t*)carve(ne * 2);
+  std::vector<PdschJobDev> hj(njobs);
+  for (uint32_t i = 0; i < njobs; i++) {
+    JobPlan& P = plans[i];
+    P.dev.cmax = d_cmax + 2 * i;
+    for (uint32_t cw = 0; cw < 2; cw++) {
+      P.dev.d[cw]   = q->d_arena + P.d_off[cw];
+      P.dev.csi[cw] = q->csi_arena + P.csi_off[cw];
+    }
+    hj[i] = P.dev;
+  }
+  size_t ci = 0;
+  for (uint32_t i = 0; i < njobs; i++) {
+    for (uint32_t t = 0; t < 2; t++) {
+      if (!plans[i].decode[t]) continue;
+      const uint32_t cw = plans[i].cw_of_tb[t];
+      cws[ci].d         = plans[i].dev.d[cw];
+      cws[ci].csi       = plans[i].dev.csi[cw];
+      cws[ci].cmax      = plans[i].dev.cmax + cw;
+      cws[ci].e         = q->e_arena + plans[i].e_off[t];
+      ci++;
+    }
+  }
+  CHECK_HIP(hipMemcpyAsync(d_jobs, hj.data(), njobs * sizeof(PdschJobDev), hipMemcpyHostToDevice, s));
+  if (!cws.empty()) CHECK_HIP(hipMemcpyAsync(d_cws, cws.data(), cws.size() * sizeof(PdschCwDev), hipMemcpyHostToDevice, s));
+  if (!blkA.empty()) CHECK_HIP(hipMemcpyAsync(d_blkA, blkA.data(), blkA.size() * sizeof(PdschBlk), hipMemcpyHostToDevice, s));
+  if (!blkB.empty()) CHECK_HIP(hipMemcpyAsync(d_blkB, blkB.data(), blkB.size() * sizeof(PdschBlk), hipMemcpyHostToDevice, s));
+  CHECK_HIP(hipMemsetAsync(d_cmax, 0, njobs * 8, s));
+  CHECK_HIP(pdsch_launch_equalize(d_jobs, d_blkA, (uint32_t)blkA.size(), s));
+  CHECK_HIP(pdsch_launch_llr(d_cws, d_blkB, (uint32_t)blkB.size(), q->gold, s));
+  return MI355_SUCCESS;
+}
+
+extern "C" {
+
+uint32_t mi355_pdsch_re_map(const mi355_cell_t* cell, const mi355_pdsch_grant_t* grant, uint32_t cfi, uint32_t sf_idx,
+                            uint32_t* idx)
+{
+  if (!cell || !grant || cell->nof_prb == 0 || cell->nof_prb > MI355_MAX_PRB) return 0;
+  return walk_map(*cell, *grant, cfi, sf_idx % 10, [&](uint32_t k, uint32_t p) {
+    if (idx) idx[k] = p;
+  });
+}
+
+int mi355_pdsch_create(mi355_pdsch_t** q, const mi355_cell_t* cell, uint32_t nof_rx_antennas, int device)
+{
+  if (!q || !cell || cell->nof_prb == 0 || cell->nof_prb > MI355_MAX_PRB || nof_rx_antennas == 0 ||
+      nof_rx_antennas > MI355_MAX_RX_ANT || !(cell->nof_ports == 1 || cell->nof_ports == 2 || cell->nof_ports == 4))
+    return MI355_ERROR_INVALID_INPUTS;
+  CHECK_HIP(hipSetDevice(device));
+  auto* d   = new mi355_pdsch;
+  d->device = device;
+  d->cell   = *cell;
+  d->nof_rx = nof_rx_antennas;
+  const std::vector<uint32_t> g = gold_table(PDSCH_GOLD_MAX);
+  if (hipStreamCreateWithFlags(&d->own, hipStreamNonBlocking) != hipSuccess ||
+      mi355_dlsch_create(&d->dlsch, device) != MI355_SUCCESS ||
+      hipMalloc(&d->gold, g.size() * 4) != hipSuccess ||
+      hipMemcpy(d->gold, g.data(), g.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    mi355_pdsch_destroy(d);
+    return MI355_ERROR;
+  }
+  *q = d;
+  return MI355_SUCCESS;
+}
+
+void mi355_pdsch_destroy(mi355_pdsch_t* q)
+{
+  if (!q) return;
+  (void)hipSetDevice(q->device);
+  (void)hipDeviceSynchronize();
+  for (auto& kv : q->maps) (void)hipFree(kv.second.first);
+  (void)hipFree(q->gold);
+  (void)hipFree(q->scratch);
+  mi355_dlsch_destroy(q->dlsch);
+  if (q->own) (void)hipStreamDestroy(q->own);
+  delete q;
+}
+
+int mi355_pdsch_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, uint32_t njobs, void* stream)
+{
+  if (!q || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t          s = stream ? (hipStream_t)stream : q->own;
+  std::vector<JobPlan> plans(njobs);
+  for (uint32_t i = 0; i < njobs; i++) {
+    int r = plan_job(q, jobs[i], nullptr, plans[i]);
+    if (r) return r;
+  }
+  int r = run_frontend(q, jobs, plans, s);
+  if (r) return r;
+  CHECK_HIP(hipStreamSynchronize(s));
+  q->last = plans;
+  return MI355_SUCCESS;
+}
+
+int mi355_pdsch_debug_stage(mi355_pdsch_t* q, uint32_t job, uint32_t cw, const float** d, const float** csi,
+                            const int16_t** e)
+{
+  if (!q || job >= q->last.size() || cw > 1) return MI355_ERROR_INVALID_INPUTS;
+  const JobPlan& P = q->last[job];
+  if (d) *d = (const float*)(q->d_arena + P.d_off[cw]);
+  if (csi) *csi = q->csi_arena + P.csi_off[cw];
+  if (e) {
+    *e = nullptr;
+    for (uint32_t t = 0; t < 2; t++)
+      if (P.decode[t] && P.cw_of_tb[t] == cw) *e = q->e_arena + P.e_off[t];
+  }
+  return MI355_SUCCESS;
+}
+
+int mi355_pdsch_decode_batch(mi355_pdsch_t*           q,
+                             mi355_softbuffer_pool_t* pool,
+                             const mi355_pdsch_job_t* jobs,
+                             uint32_t                 njobs,
+                             mi355_pdsch_res_t*       res,
+                             void*                    stream)
+{
+  if (!q || !pool || !res || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t          s = stream ? (hipStream_t)stream : q->own;
+  std::vector<JobPlan> plans(njobs);
+  for (uint32_t i = 0; i < njobs; i++) {
+    int r = plan_job(q, jobs[i], &res[2 * i], plans[i]);
+    if (r) return r;
+  }
+  int r = run_frontend(q, jobs, plans, s);
+  if (r) return r;
+  q->last = plans;
+
+  // DL-SCH: one batch per max-iterations setting (srslte_sch_set_max_noi persists, pdsch.c:930-932)
+  std::map<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>> by_its; // its -> (job, tb)
+  std::map<uint32_t, std::vector<mi355_dlsch_tb_t>>              tbs;
+  for (uint32_t i = 0; i < njobs; i++) {
+    const mi355_pdsch_cfg_t& cfg = jobs[i].cfg;
+    if (cfg.max_nof_iterations) q->max_its = cfg.max_nof_iterations;
+    for (uint32_t t = 0; t < 2; t++) {
+      if (!plans[i].decode[t]) continue;
+      const mi355_ra_tb_t& tb = cfg.grant.tb[t];
+      const uint32_t       Nl = cfg.grant.nof_layers != cfg.grant.nof_tb ? 2 : 1; // sch.c:584-588
+      mi355_dlsch_tb_t     d{};
+      d.tbs         = (uint32_t)std::max(0, tb.tbs);
+      d.nof_e_bits  = tb.nof_bits;
+      d.Qm          = mod_bits(tb.mod) * Nl;
+      d.rv          = tb.rv;
+      d.softbuffer  = cfg.softbuffer[t];
+      d.e_offset    = plans[i].e_off[t];
+      d.data_offset = (uint64_t)(uintptr_t)jobs[i].payload[t]; // absolute (d_data == NULL)
+      by_its[q->max_its].push_back({i, t});
+      tbs[q->max_its].push_back(d);
+    }
+  }
+  for (auto& kv : tbs) {
+    const uint32_t         its = kv.first;
+    std::vector<int32_t>   ret(kv.second.size());
+    std::vector<float>     avg(kv.second.size());
+    if ((r = mi355_dlsch_set_max_iterations(q->dlsch, its))) return r;
+    r = mi355_dlsch_decode_dev(q->dlsch, pool, q->e_arena, kv.second.data(), (uint32_t)kv.second.size(), nullptr,
+                               ret.data(), avg.data(), s);
+    if (r) return r;
+    const auto& who = by_its[its];
+    for (size_t k = 0; k < who.size(); k++) {
+      mi355_pdsch_res_t& o = res[2 * who[k].first + who[k].second];
+      // srslte_pdsch_codeword_decode (pdsch.c:862-871)
+      o.crc                  = ret[k] == 0;
+      o.ret                  = ret[k] == MI355_ERROR_INVALID_INPUTS ? MI355_ERROR : MI355_SUCCESS;
+      o.avg_iterations_block = avg[k];
+    }
+  }
+  return MI355_SUCCESS;
+}
+
+} // extern "C"

@@ -14,6 +14,10 @@ Contents
   crc_cbsegm.npz     CRC24A/24B/16/8 checksums and CB segmentation for a TBS sweep.
   rm_turbo.npz       srslte_rm_turbo_rx_lut (AVX build): E LLRs -> decoder buffer, every rv, E below /
                      at / above the circular buffer (wrap-around), plus HARQ accumulation rv0 + rv2.
+  pdsch_stages.npz   srslte_demod_soft_demodulate_s for every modulation (SIMD bodies and scalar tails,
+                     saturating amplitudes), srslte_scrambling_s_offset (PDSCH c_init), and
+                     srslte_predecoding_type with CSI (AVX2 build, MMSE) for every scheme srslte_pdsch_decode
+                     uses -- the equaliser output is pinned within the reference's rcp tolerance.
 """
 from __future__ import annotations
 
@@ -162,6 +166,60 @@ def gen_rm(rng):
     print("rm_turbo.npz:", len(cases), "cases")
 
 
+def gen_pdsch_stages(rng):
+    R = oracle.ref()
+    data = {}
+    k = 0
+    for qm in (1, 2, 4, 6, 8):
+        for n in (1, 3, 4, 7, 16, 17, 100, 301):
+            for amp in (1.0, 60.0, 3e5):
+                sym = (amp * (rng.standard_normal(n) + 1j * rng.standard_normal(n)) / np.sqrt(2)).astype(np.complex64)
+                iq = np.ascontiguousarray(sym.view(np.float32))
+                out = np.zeros(qm * n, np.int16)
+                R.ref_demod_soft_s(qm, iq, out, n)
+                data[f"demod{k}_qm"] = np.int32(qm)
+                data[f"demod{k}_sym"] = sym
+                data[f"demod{k}_llr"] = out
+                k += 1
+    data["demod_n"] = np.int32(k)
+    k = 0
+    for (rnti, cw, sf, cid, n) in [(0x1234, 0, 3, 1, 1000), (0xffff, 1, 9, 503, 4097), (61, 0, 0, 0, 33),
+                                   (0x4601, 1, 5, 77, 20000)]:
+        c_init = oracle.pdsch_c_init(rnti, cw, sf, cid)
+        llr = rng.integers(-32768, 32768, n, dtype=np.int16)
+        llr[:4] = [-32768, 32767, 0, -1]
+        out = llr.copy()
+        R.ref_scramble_s(c_init, out, 0, n)
+        data[f"scr{k}_cinit"] = np.uint32(c_init)
+        data[f"scr{k}_in"] = llr
+        data[f"scr{k}_out"] = out
+        k += 1
+    data["scr_n"] = np.int32(k)
+    k = 0
+    # (scheme, ports, rx, layers, codebooks)
+    cfgs = [(0, 1, 1, 1, [0]), (0, 1, 2, 1, [0]), (1, 2, 1, 2, [0]), (1, 2, 2, 2, [0]), (2, 2, 2, 2, [0, 1, 2]),
+            (2, 2, 2, 1, [0, 1, 2, 3]), (3, 2, 2, 2, [0])]
+    for (scheme, ports, rx, layers, cbs) in cfgs:
+        for cb in cbs:
+            for n in (6, 258):
+                y = ((rng.standard_normal((rx, n)) + 1j * rng.standard_normal((rx, n))) / np.sqrt(2)).astype(
+                    np.complex64)
+                h = ((rng.standard_normal((ports, rx, n)) + 1j * rng.standard_normal((ports, rx, n))) /
+                     np.sqrt(2)).astype(np.complex64)
+                scaling, noise = 0.8, 0.03
+                x, csi = oracle.ref_predecode(y, h, layers, cb, scheme, scaling, noise)
+                data[f"pre{k}_cfg"] = np.array([scheme, ports, rx, layers, cb, n], np.int32)
+                data[f"pre{k}_sc"] = np.array([scaling, noise], np.float32)
+                data[f"pre{k}_y"] = y
+                data[f"pre{k}_h"] = h
+                data[f"pre{k}_x"] = x
+                data[f"pre{k}_csi"] = csi
+                k += 1
+    data["pre_n"] = np.int32(k)
+    np.savez_compressed(os.path.join(OUT, "pdsch_stages.npz"), **data)
+    print("pdsch_stages.npz:", data["demod_n"], "demod,", data["scr_n"], "scrambling,", k, "predecoding cases")
+
+
 def main():
     oracle.build(ref=True)
     if not oracle.ref_available():
@@ -172,6 +230,7 @@ def main():
     gen_tcod_known()
     gen_crc_cbsegm(rng)
     gen_rm(np.random.default_rng(1212))
+    gen_pdsch_stages(np.random.default_rng(3003))
 
 
 if __name__ == "__main__":
