@@ -2,12 +2,12 @@
 oracle's restatement of srslte_pdsch_decode (oracle/pdsch_chain.py over the oracle C stages, themselves
 pinned to the compiled reference by tests/golden/pdsch_stages.npz).
 
-Tolerances (north star: bit-exact decoded bits / CRCs, soft values within 1e-4):
-  * equalised symbols and CSI: |GPU - oracle| <= 2e-5 * |oracle| + 1e-6 (both evaluate the reference's exact
-    fp32 formulas; they differ only in FMA contraction / evaluation order);
-  * LLRs: bit-exact against the oracle demapper / descrambler / CSI weighting applied to the GPU's own
-    equalised symbols and CSI (the integer stages are exact), and within +-1 (fraction < 1e-3 differing)
-    against the full oracle chain (a symbol within 1 ulp of a truncation boundary can flip one LSB);
+Parity (north star: bit-exact decoded bits / CRCs, soft values within 1e-4):
+  * equalised symbols, CSI and LLRs: BIT-EXACT against the oracle.  Both evaluate the reference's exact
+    (non-SIMD) fp32 formulas operation by operation in the same order, with correctly rounded division and
+    no FMA contraction (-ffp-contract=off on both sides), so there is nothing left to differ.  (Against the
+    reference's own AVX2 build the equaliser differs by its rcp approximation, <= 1e-3 relative: pinned in
+    tests/test_pdsch_oracle.py.)
   * decoded payloads, CRC flags, iteration counts: identical to the oracle chain.
 """
 import numpy as np
@@ -52,20 +52,11 @@ def _stage_check(pd, k, cfg, sf, job=0):
     for cw in range(ncw):
         qm = cfg.qm[cw] if cw < cfg.nof_tb else 2
         d, csi, e = pd.stage(job, cw, nre, nre * qm if cw < cfg.nof_tb else None)
-        tol = 2e-5 * np.abs(d_o[cw]) + 1e-6
-        bad = np.abs(d - d_o[cw]) > tol
-        assert not bad.any(), (k, cw, int(bad.sum()), np.abs(d - d_o[cw])[bad][:4], d_o[cw][bad][:4])
-        ctol = 2e-5 * np.abs(csi_o[cw][:nre]) + 1e-6
-        assert (np.abs(csi - csi_o[cw][:nre]) <= ctol).all(), (k, cw)
+        bad = d.view(np.uint64) != d_o[cw].view(np.uint64)
+        assert not bad.any(), (k, cw, int(bad.sum()), (d - d_o[cw])[bad][:4], d_o[cw][bad][:4])
+        np.testing.assert_array_equal(csi.view(np.uint32), csi_o[cw][:nre].view(np.uint32), err_msg=f"csi {k} {cw}")
         if cw < cfg.nof_tb:
-            # integer stages exact on the GPU's own symbols
-            llr = oracle.demod_soft_s(qm, d)
-            llr = oracle.scramble_s(oracle.pdsch_c_init(cfg.rnti, cw, cfg.sf_idx, cfg.cell_id), llr[: nre * qm])
-            if cfg.csi_enable:
-                llr = oracle.csi_correction_s(qm, llr, csi)
-            np.testing.assert_array_equal(e, llr, err_msg=f"cfg {k} cw {cw}")
-            diff = np.abs(e.astype(np.int32) - e_o[cw].astype(np.int32))
-            assert diff.max() <= 1 and (diff > 0).mean() < 1e-3, (k, cw, diff.max(), (diff > 0).mean())
+            np.testing.assert_array_equal(e, e_o[cw], err_msg=f"cfg {k} cw {cw}")
 
 
 @pytest.mark.parametrize("k", range(len(CFGS)))
