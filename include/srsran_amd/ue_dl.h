@@ -1,0 +1,113 @@
+/*
+ * include/srsran_amd/ue_dl.h -- C ABI of the MI355X UE downlink front-end: OFDM demodulation and channel
+ * estimation for batches of subframes, and the srslte_ue_dl-level wrapper chaining them into the PDSCH
+ * receiver (pdsch.h).
+ *
+ *   mi355_ofdm_rx_batch          srslte_ofdm_rx_sf (lib/src/phy/dft/ofdm.c:458-471, :392-427): per slot, CP
+ *                                removal and an N-point forward DFT per OFDM symbol (no normalisation, as
+ *                                ue_dl.c:93 configures it), FFT-shift dropping DC: out[0:nre/2] =
+ *                                X[N-nre/2:N], out[nre/2:nre] = X[1:nre/2+1].
+ *   mi355_chest_dl_estimate_batch srslte_chest_dl_estimate_cfg (ch_estimation/chest_dl.c:985-1014) for normal
+ *                                FDD subframes: CRS LS estimates, RSRP/RSSI, REFS noise estimation, Gauss /
+ *                                triangle / no smoothing, AVERAGE estimator (merged pilots, linear interpolation,
+ *                                the same estimate on every OFDM symbol), srslte_chest_dl_res_t scalars.
+ *   mi355_ue_dl_*                srslte_ue_dl_init / set_cell / decode_fft_estimate / decode_pdsch
+ *                                (ue/ue_dl.c:75-140, :370-430, :486-520) over batches of subframes.
+ *
+ * Sample buffers are device pointers.  Numerics: the reference computes the DFT with FFTW (not vendored) and
+ * its estimator with SIMD float sums; both are reproduced within float tolerance.
+ */
+#ifndef SRSRAN_AMD_UE_DL_H
+#define SRSRAN_AMD_UE_DL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "pdsch.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* srslte_chest_filter_t, srslte_chest_dl_estimator_alg_t, srslte_chest_dl_noise_alg_t */
+enum { MI355_CHEST_FILTER_GAUSS = 0, MI355_CHEST_FILTER_TRIANGLE, MI355_CHEST_FILTER_NONE };
+enum { MI355_ESTIMATOR_ALG_AVERAGE = 0, MI355_ESTIMATOR_ALG_INTERPOLATE, MI355_ESTIMATOR_ALG_WIENER };
+enum { MI355_NOISE_ALG_REFS = 0, MI355_NOISE_ALG_PSS, MI355_NOISE_ALG_EMPTY };
+
+/* srslte_chest_dl_cfg_t (chest_dl.h:123-137) */
+typedef struct {
+  uint32_t estimator_alg;
+  uint32_t noise_alg;
+  uint32_t filter_type;
+  float    filter_coef[2];
+  uint32_t rsrp_neighbour;
+  uint32_t cfo_estimate_enable;
+  uint32_t sync_error_enable;
+} mi355_chest_dl_cfg_t;
+
+/* srslte_chest_dl_res_t scalars (chest_dl.h:50-68); ce pointers live in the job */
+typedef struct {
+  uint32_t nof_re;
+  float    noise_estimate;
+  float    noise_estimate_dbm;
+  float    snr_db;
+  float    snr_ant_port_db[MI355_MAX_PORTS][MI355_MAX_PORTS];
+  float    rsrp;
+  float    rsrp_dbm;
+  float    rsrp_neigh;
+  float    rsrp_port_dbm[MI355_MAX_PORTS];
+  float    rsrp_ant_port_dbm[MI355_MAX_PORTS][MI355_MAX_PORTS];
+  float    rsrq;
+  float    rsrq_db;
+  float    rsrq_ant_port_db[MI355_MAX_PORTS][MI355_MAX_PORTS];
+  float    rssi_dbm;
+  float    cfo;
+  float    sync_error;
+} mi355_chest_dl_res_t;
+
+/* One subframe of one UE: time-domain input per rx antenna (SRSLTE_SF_LEN(symbol_sz) complex samples), the
+ * resource grid it produces (nsymb*2 x 12*nof_prb complex, srslte_ue_dl_t.sf_symbols) and the channel
+ * estimates ce[port][rx] (same shape).  Device pointers. */
+typedef struct {
+  uint32_t     tti;
+  const float* in_buffer[MI355_MAX_RX_ANT];
+  float*       sf_symbols[MI355_MAX_RX_ANT];
+  float*       ce[MI355_MAX_PORTS][MI355_MAX_RX_ANT];
+} mi355_dl_sf_job_t;
+
+typedef struct mi355_ue_dl mi355_ue_dl_t;
+
+/* srslte_symbol_sz for nof_prb (standard LTE rates when use_standard_rates != 0), 0 if invalid */
+uint32_t mi355_symbol_sz(uint32_t nof_prb, int use_standard_rates);
+
+int  mi355_ue_dl_create(mi355_ue_dl_t** q, const mi355_cell_t* cell, uint32_t nof_rx_antennas, int device);
+void mi355_ue_dl_destroy(mi355_ue_dl_t* q);
+/* srslte_use_standard_symbol_size: switch the DFT size to the 3GPP rates (2048 for 100 PRB) */
+int mi355_ue_dl_set_standard_rates(mi355_ue_dl_t* q, int enable);
+
+/* OFDM demodulation of every job's rx antennas (in_buffer -> sf_symbols). */
+int mi355_ofdm_rx_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, void* stream);
+
+/* Channel estimation from sf_symbols into ce, res[njobs] filled on return (synchronous). */
+int mi355_chest_dl_estimate_batch(mi355_ue_dl_t*              q,
+                                  const mi355_dl_sf_job_t*    jobs,
+                                  uint32_t                    njobs,
+                                  const mi355_chest_dl_cfg_t* cfg,
+                                  mi355_chest_dl_res_t*       res,
+                                  void*                       stream);
+
+/* srslte_ue_dl_decode_fft_estimate for a batch: OFDM + channel estimation (synchronous). */
+int mi355_ue_dl_decode_fft_estimate_batch(mi355_ue_dl_t*              q,
+                                          const mi355_dl_sf_job_t*    jobs,
+                                          uint32_t                    njobs,
+                                          const mi355_chest_dl_cfg_t* cfg,
+                                          mi355_chest_dl_res_t*       res,
+                                          void*                       stream);
+
+/* The PDSCH receiver bound to this UE's cell (borrowed; valid until mi355_ue_dl_destroy). */
+mi355_pdsch_t* mi355_ue_dl_pdsch(mi355_ue_dl_t* q);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

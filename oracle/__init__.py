@@ -71,6 +71,9 @@ def lib() -> C.CDLL:
         L.orc_pdsch_re_map.restype = C.c_uint32
         L.orc_pdsch_re_map.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_uint32,
                                        C.c_uint32, u8p, C.c_uint32, C.c_uint32, u32p]
+        L.orc_crs_pilots.argtypes = [C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, f32p]
+        L.orc_chest_estimate_port.argtypes = [f32p, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, C.c_int,
+                                              C.c_float, C.c_float, C.c_int, f32p, f32p]
         L.orc_predecode.argtypes = [f32p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
                                     C.c_float, f32p, f32p, f32p]
         _LIB = L

@@ -1,0 +1,256 @@
+/*
+ * oracle/orc_chest.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Scalar restatement of the downlink channel estimator srslte_chest_dl_estimate_cfg for normal (non-MBSFN)
+ * FDD subframes (lib/src/phy/ch_estimation/chest_dl.c:985-1014 -> estimate_port :788-816 ->
+ * chest_interpolate_noise_est :621-728):
+ *   - cell-specific reference signals: srslte_refsignal_cs_set_cell (refsignal_dl.c:63-114), pilot
+ *     positions srslte_refsignal_cs_fidx / _nsymbol / _get_sf (:223-290);
+ *   - LS estimates rx * conj(crs), RSRP (average pilot power), RSSI (chest_dl_rssi :569-581);
+ *   - noise estimation SRSLTE_NOISE_ALG_REFS (estimate_noise_pilots :320-397, including its quirk that only
+ *     the LAST pilot symbol's residual power survives the loop);
+ *   - smoothing filter: Gauss (chest_common.c:70-88, auto sigma = noise * 200 when filter_coef[0] <= 0) or
+ *     triangle (:42-48) or none;
+ *   - SRSLTE_ESTIMATOR_ALG_AVERAGE: average_pilots (:530-567: interleave the pilot symbols, scale by
+ *     2/nsymbols) then srslte_conv_same_cf with its extrapolated edges (utils/convolution.c:183-220), then
+ *     interpolate_pilots' srslte_interp_linear_offset over the 3-spaced merged pilots (interp.c:259-285) and
+ *     copy to every OFDM symbol (chest_dl.c:488-494).
+ * chest_dl.c / refsignal_dl.c / interp.c / convolution.c include the generated srslte/version.h and are not
+ * compilable here: this file is pinned by restatement only ("parity unpinned" for a2).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle.h"
+
+typedef struct {
+  float re, im;
+} cf;
+static inline cf    cmk(float r, float i) { return (cf){r, i}; }
+static inline cf    cadd(cf a, cf b) { return cmk(a.re + b.re, a.im + b.im); }
+static inline cf    csub(cf a, cf b) { return cmk(a.re - b.re, a.im - b.im); }
+static inline cf    cscale(cf a, float s) { return cmk(a.re * s, a.im * s); }
+static inline cf    cprod_conj(cf a, cf b) { return cmk(a.re * b.re + a.im * b.im, a.im * b.re - a.re * b.im); }
+static inline float cpw(cf a) { return a.re * a.re + a.im * a.im; }
+
+#define MAXPRB 110
+
+static uint32_t crs_nof_symbols(uint32_t port) { return port < 2 ? 4 : 2; } /* FDD */
+static uint32_t crs_v(uint32_t port, uint32_t l)
+{
+  switch (port) {
+    case 0: return (l % 2) ? 3 : 0;
+    case 1: return (l % 2) ? 0 : 3;
+    case 2: return l == 0 ? 0 : 3;
+    default: return l == 0 ? 3 : 0;
+  }
+}
+static uint32_t crs_fidx(uint32_t id, uint32_t l, uint32_t port) { return (crs_v(port, l) + id % 6) % 6; }
+static uint32_t crs_nsymbol(uint32_t l, uint32_t nsymb, uint32_t port)
+{
+  if (port < 2) return (l % 2) ? (l / 2 + 1) * nsymb - 3 : (l / 2) * nsymb;
+  return 1 + l * nsymb;
+}
+
+/* pilots of port pair p (0: ports 0/1, 1: ports 2/3) for subframe sf: 2*nof_prb per reference symbol of
+ * the subframe, symbols in srslte_refsignal_cs_nsymbol order (refsignal_dl.c:86-110) */
+void orc_crs_pilots(uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t p, uint32_t sf, float* out)
+{
+  const uint32_t nsymb = cp_ext ? 6 : 7, Ncp = cp_ext ? 0 : 1;
+  uint8_t        c[4 * MAXPRB];
+  cf*            o = (cf*)out;
+  for (uint32_t ns = 2 * sf; ns < 2 * sf + 2; ns++) {
+    const uint32_t nsymbols = crs_nof_symbols(2 * p) / 2;
+    for (uint32_t l = 0; l < nsymbols; l++) {
+      const uint32_t lp     = crs_nsymbol(l, nsymb, 2 * p);
+      const uint32_t c_init = 1024 * (7 * (ns + 1) + lp + 1) * (2 * cell_id + 1) + 2 * cell_id + Ncp;
+      orc_sequence_lte(c_init, 4 * MAXPRB, c);
+      for (uint32_t i = 0; i < 2 * nof_prb; i++) {
+        const uint32_t idx = 2 * nof_prb * ((ns % 2) * nsymbols + l) + i, mp = i + MAXPRB - nof_prb;
+        o[idx] = cmk((float)((1 - 2 * (float)c[2 * mp]) * M_SQRT1_2), (float)((1 - 2 * (float)c[2 * mp + 1]) * M_SQRT1_2));
+      }
+    }
+  }
+}
+
+/* srslte_conv_same_cf with conv_same_extrapolates_extremes (convolution.c:183-220) */
+static void conv_same(const cf* in, const float* f, cf* out, uint32_t N, uint32_t M)
+{
+  cf first[16], last[16];
+  for (uint32_t i = 0; i < M + M / 2; i++) {
+    first[i] = i < M / 2 ? csub(cscale(in[1], (float)(2 + M / 2 - i)), cscale(in[0], (float)(1 + M / 2 - i)))
+                         : in[i - M / 2];
+    last[i]  = i >= M - 1 ? csub(cscale(in[N - 1], (float)(2 + i - M / 2)), cscale(in[N - 2], (float)(1 + i - M / 2)))
+                          : in[N - M + i + 1];
+  }
+  uint32_t i = 0;
+  for (; i < M / 2; i++) {
+    cf acc = cmk(0, 0);
+    for (uint32_t k = 0; k < M; k++) acc = cadd(acc, cscale(first[i + k], f[k]));
+    out[i] = acc;
+  }
+  for (; i < N - M / 2; i++) {
+    cf acc = cmk(0, 0);
+    for (uint32_t k = 0; k < M; k++) acc = cadd(acc, cscale(in[i - M / 2 + k], f[k]));
+    out[i] = acc;
+  }
+  for (uint32_t j = 0; i < N; i++, j++) {
+    cf acc = cmk(0, 0);
+    for (uint32_t k = 0; k < M; k++) acc = cadd(acc, cscale(last[j + k], f[k]));
+    out[i] = acc;
+  }
+}
+
+/* srslte_interp_linear_offset (interp.c:259-285) with M points per input interval */
+static void interp_linear_offset(const cf* in, cf* out, uint32_t len, uint32_t M, uint32_t off_st, uint32_t off_end)
+{
+  for (uint32_t j = 0; j < off_st; j++) {
+    const cf d = csub(in[1], in[0]);
+    out[off_st - j - 1] = csub(in[0], cmk((float)(j + 1) * d.re / (float)M, (float)(j + 1) * d.im / (float)M));
+  }
+  const float rM = (float)1 / M;
+  uint32_t    i;
+  for (i = 0; i < len - 1; i++) {
+    const cf d = cscale(csub(in[i + 1], in[i]), rM);
+    for (uint32_t j = 0; j < M; j++) out[i * M + j + off_st] = cadd(in[i], cscale(d, (float)j));
+  }
+  if (len > 1) {
+    const cf d = csub(in[len - 1], in[len - 2]);
+    for (uint32_t j = 0; j < off_end; j++)
+      out[i * M + j + off_st] = cadd(in[i], cmk((float)j * d.re / (float)M, (float)j * d.im / (float)M));
+  }
+}
+
+/* estimate_noise_pilots (chest_dl.c:320-397), normal subframe, nsymbols >= 2 */
+static float noise_refs(const cf* pe, uint32_t nsymbols, uint32_t nref, uint32_t fidx)
+{
+  const float weight = 1.0f;
+  cf*         buf    = malloc(sizeof(cf) * nref * 3);
+  const cf*   in2d[8] = {0};
+  cf*         first = buf + nref, *lastb = buf + 2 * nref, *tmp = buf;
+  for (uint32_t i = 0; i < nsymbols; i++) in2d[i + 1] = &pe[i * nref];
+  for (uint32_t k = 0; k < nref; k++) {
+    first[k] = nsymbols > 3 ? csub(cscale(in2d[2][k], 2.0f), in2d[4][k]) : cscale(in2d[2][k], 1.0f);
+    lastb[k] = nsymbols > 3 ? csub(cscale(in2d[nsymbols - 1][k], 2.0f), in2d[nsymbols - 3][k])
+                            : cscale(in2d[nsymbols - 1][k], 1.0f);
+  }
+  in2d[0]            = first;
+  in2d[nsymbols + 1] = lastb;
+  float    sum_power = 0;
+  uint32_t count     = 0;
+  for (uint32_t i = 1; i < nsymbols + 1; i++) {
+    const uint32_t off = ((fidx < 3) ^ (i & 1)) ? 0 : 1;
+    for (uint32_t k = 0; k < nref; k++) tmp[k] = cscale(in2d[i][k], weight);
+    for (int nb = -1; nb <= 1; nb += 2) {
+      const cf* a = in2d[i + nb];
+      for (uint32_t k = 0; k < nref - off; k++) tmp[k + off] = cadd(a[k], tmp[k + off]);
+      for (uint32_t k = 0; k < nref + off - 1; k++) tmp[k] = cadd(a[k + 1 - off], tmp[k]);
+      if (off) {
+        tmp[0] = cadd(tmp[0], csub(cscale(a[0], 2.0f), a[1]));
+      } else {
+        tmp[nref - 1] = cadd(tmp[nref - 1], csub(cscale(a[nref - 2], 2.0f), a[nref - 1]));
+      }
+    }
+    const float s = 1.0f / (weight + 4.0f);
+    float       p = 0;
+    for (uint32_t k = 0; k < nref; k++) {
+      tmp[k] = csub(in2d[i][k], cscale(tmp[k], s));
+      p += cpw(tmp[k]);
+    }
+    sum_power = p / (float)nref; /* srslte_vec_avg_power_cf; overwritten every symbol (reference quirk) */
+    count++;
+  }
+  free(buf);
+  return sum_power / (float)count * sqrtf(weight + 4.0f);
+}
+
+/* One (rx antenna, port) estimate_port call.  grid: nsymb*2 x 12*nof_prb cf.  cfg: filter_type (0 gauss,
+ * 1 triangle, 2 none), coef0/coef1 (filter_coef), estimator_alg (0 average).  ce: full grid output.
+ * out3: {noise_estimate, rsrp, rssi}.  Returns -1 for unsupported configurations. */
+int orc_chest_estimate_port(const float* grid_f, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf,
+                            uint32_t port, int filter_type, float coef0, float coef1, int estimator_alg,
+                            float* ce_f, float* out3)
+{
+  if (estimator_alg != 0) return -1;
+  const cf*      grid  = (const cf*)grid_f;
+  cf*            ce    = (cf*)ce_f;
+  const uint32_t nsymb = cp_ext ? 6 : 7, nre = 12 * nof_prb, nsym = crs_nof_symbols(port), nref = 2 * nof_prb;
+  const uint32_t np    = nsym * nref;
+  cf*            crs   = malloc(sizeof(cf) * 4 * nref);
+  cf*            rx    = malloc(sizeof(cf) * np);
+  cf*            pe    = malloc(sizeof(cf) * np);
+  cf*            avg   = malloc(sizeof(cf) * np);
+  cf*            smo   = malloc(sizeof(cf) * np);
+  orc_crs_pilots(nof_prb, cell_id, cp_ext, port / 2, sf, (float*)crs);
+  float rsrp = 0, rssi = 0;
+  for (uint32_t l = 0; l < nsym; l++) {
+    const uint32_t s = crs_nsymbol(l, nsymb, port), f = crs_fidx(cell_id, l, port);
+    for (uint32_t i = 0; i < nref; i++) {
+      rx[l * nref + i] = grid[s * nre + f + 6 * i];
+      pe[l * nref + i] = cprod_conj(rx[l * nref + i], crs[l * nref + i]);
+    }
+    float r = 0;
+    for (uint32_t k = 0; k < nre; k++) r += cpw(grid[s * nre + k]); /* Re(dot_prod_conj(x, x)) */
+    rssi += r;
+  }
+  for (uint32_t k = 0; k < np; k++) rsrp += cpw(rx[k]);
+  rsrp /= (float)np;
+  rssi /= (float)nsym;
+  const float noise = noise_refs(pe, nsym, nref, crs_fidx(cell_id, 0, port));
+
+  float    filt[16];
+  uint32_t flen = 0;
+  if (filter_type == 0) {
+    const uint32_t order = coef0 <= 0 ? 4 : (uint32_t)coef0;
+    const float    sd    = coef0 <= 0 ? noise * 200.0f : coef1;
+    flen                 = order + 1;
+    const int c          = (int)(flen - 1) / 2;
+    float     nrm        = 0;
+    for (int i = 0; i < (int)flen; i++) {
+      filt[i] = expf(-powf((float)(i - c), 2) / (2.0f * powf(sd, 2)));
+      nrm += filt[i];
+    }
+    for (uint32_t i = 0; i < flen; i++) filt[i] *= 1.0f / nrm;
+  } else if (filter_type == 1) {
+    filt[0] = filt[2] = coef0;
+    filt[1]           = 1 - 2 * coef0;
+    flen              = 3;
+  }
+
+  const cf* src = pe;
+  uint32_t  nr  = nref;
+  if (filter_type != 2) {
+    /* average_pilots: AVERAGE merges the pilot symbols (nsym > 1) */
+    const int first_lo = crs_fidx(cell_id, 0, port) < 3;
+    for (uint32_t i = 0; i < nref; i++) {
+      cf a = first_lo ? pe[i] : pe[nref + i], b = first_lo ? pe[nref + i] : pe[i];
+      for (uint32_t l = 2; l + 1 < nsym; l += 2) {
+        a = cadd(a, first_lo ? pe[l * nref + i] : pe[(l + 1) * nref + i]);
+        b = cadd(b, first_lo ? pe[(l + 1) * nref + i] : pe[l * nref + i]);
+      }
+      avg[2 * i]     = a;
+      avg[2 * i + 1] = b;
+    }
+    nr                = 2 * nref;
+    const float scale = 2.0f / (float)nsym;
+    for (uint32_t k = 0; k < nr; k++) avg[k] = cscale(avg[k], scale);
+    conv_same(avg, filt, smo, nr, flen);
+    src = smo;
+  }
+  /* interpolate_pilots, AVERAGE with nsymbols > 1: interp_lin_3 over 4*nof_prb merged pilots */
+  const uint32_t off = cell_id % 3;
+  interp_linear_offset(src, ce, 4 * nof_prb, 3, off, 3 - off);
+  for (uint32_t l = 1; l < 2 * nsymb; l++) memcpy(&ce[l * nre], ce, sizeof(cf) * nre);
+  out3[0] = noise;
+  out3[1] = rsrp;
+  out3[2] = rssi;
+  free(crs);
+  free(rx);
+  free(pe);
+  free(avg);
+  free(smo);
+  (void)nr;
+  return 0;
+}

@@ -1,0 +1,245 @@
+// srsran_amd/csrc/chest_kernels.hip -- downlink channel estimator (srslte_chest_dl_estimate_cfg,
+// lib/src/phy/ch_estimation/chest_dl.c:985-1014 -> estimate_port :788-816 -> chest_interpolate_noise_est
+// :621-728) for normal FDD subframes, AVERAGE estimator.
+//
+// One workgroup per (subframe, rx antenna, port).  The <= 880 pilots of the port are gathered from the
+// resource grid and LS-estimated against the CRS table into LDS; RSRP / RSSI / the REFS noise estimate are
+// block reductions; the pilot symbols are merged, smoothed (Gauss / triangle 3- or 5-tap filter with the
+// reference's extrapolated edges), linearly interpolated onto the 12*nof_prb subcarriers and the row is
+// streamed to every OFDM symbol of ce (the AVERAGE estimator's time-invariant estimate).  HBM traffic per
+// (rx, port): the 4 pilot rows read (RSSI), 14 ce rows written.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ue_dl_internal.h"
+
+namespace mi355 {
+
+namespace {
+
+constexpr uint32_t MAXPRB = 110;
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float  cpw(float2 a) { return a.x * a.x + a.y * a.y; }
+// srslte_vec_prod_conj_ccc: a * conj(b)
+__device__ __forceinline__ float2 cprod_conj(float2 a, float2 b)
+{
+  return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+
+__device__ __forceinline__ uint32_t crs_v(uint32_t port, uint32_t l)
+{
+  switch (port) {
+    case 0: return (l % 2) ? 3 : 0;
+    case 1: return (l % 2) ? 0 : 3;
+    case 2: return l == 0 ? 0 : 3;
+    default: return l == 0 ? 3 : 0;
+  }
+}
+__device__ __forceinline__ uint32_t crs_fidx(uint32_t id, uint32_t l, uint32_t port) { return (crs_v(port, l) + id % 6) % 6; }
+__device__ __forceinline__ uint32_t crs_nsymbol(uint32_t l, uint32_t nsymb, uint32_t port)
+{
+  if (port < 2) return (l % 2) ? (l / 2 + 1) * nsymb - 3 : (l / 2) * nsymb;
+  return 1 + l * nsymb;
+}
+
+template <int N> __device__ __forceinline__ void block_sum(float (&v)[N], float* red)
+{
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < N; k++) red[w * N + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; k++) v[k] = red[k] + red[N + k] + red[2 * N + k] + red[3 * N + k];
+}
+
+} // namespace
+
+__global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
+{
+  __shared__ float2 pe[4 * 2 * MAXPRB];
+  __shared__ float2 avg[4 * MAXPRB];
+  __shared__ float2 smo[4 * MAXPRB];
+  __shared__ float2 row[12 * MAXPRB];
+  __shared__ float  red[4 * 8];
+  __shared__ float  filt[16];
+  __shared__ uint32_t flen_s;
+
+  const ChestJob J    = a.jobs[blockIdx.x];
+  const uint32_t nprb = a.nof_prb, nre = 12 * nprb, nref = 2 * nprb, port = J.port;
+  const uint32_t nsym = port < 2 ? 4 : 2, np = nsym * nref;
+  const float2*  crs  = a.pilots + (size_t)((port / 2) * 10 + J.sf) * (4 * nref);
+  const float2*  g    = J.grid;
+
+  // 1. LS estimates and RSRP (srslte_refsignal_cs_get_sf + srslte_vec_prod_conj_ccc, estimate_port :793-806)
+  float acc[4] = {0.f, 0.f, 0.f, 0.f}; // rsrp, rssi, sum pe re, sum pe im
+  for (uint32_t k = threadIdx.x; k < np; k += blockDim.x) {
+    const uint32_t l = k / nref, i = k % nref;
+    const float2   x = g[crs_nsymbol(l, a.nsymb, port) * nre + crs_fidx(a.cell_id, l, port) + 6 * i];
+    acc[0] += cpw(x);
+    const float2 e = cprod_conj(x, crs[k]);
+    pe[k]          = e;
+    acc[2] += e.x;
+    acc[3] += e.y;
+  }
+  // RSSI over the reference symbols (chest_dl_rssi :569-581)
+  for (uint32_t k = threadIdx.x; k < nsym * nre; k += blockDim.x) {
+    const uint32_t l = k / nre;
+    acc[1] += cpw(g[crs_nsymbol(l, a.nsymb, port) * nre + k % nre]);
+  }
+  block_sum<4>(acc, red); // includes the barrier that publishes pe[]
+
+  // 2. REFS noise (estimate_noise_pilots :320-397): only the last pilot symbol's residual power survives
+  //    the reference's loop, divided by the symbol count and scaled by sqrt(5)
+  float nz[1] = {0.f};
+  {
+    const uint32_t fidx0 = crs_fidx(a.cell_id, 0, port);
+    const uint32_t off   = ((fidx0 < 3) ^ (nsym & 1)) ? 0 : 1;
+    const float2*  cen   = &pe[(nsym - 1) * nref];
+    const float2*  lo    = &pe[(nsym - 2) * nref];
+    for (uint32_t m = threadIdx.x; m < nref; m += blockDim.x) {
+      // in2d[nsym+1]: 2*pe[nsym-2] - pe[nsym-4] (4 symbols) or pe[nsym-2] (2 symbols)
+      auto hi = [&](uint32_t k) {
+        return nsym > 3 ? csub(cscale(pe[(nsym - 2) * nref + k], 2.0f), pe[(nsym - 4) * nref + k])
+                        : cscale(pe[(nsym - 2) * nref + k], 1.0f);
+      };
+      float2 t = cscale(cen[m], 1.0f);
+#pragma unroll
+      for (int nb = 0; nb < 2; nb++) {
+        auto A = [&](uint32_t k) { return nb == 0 ? lo[k] : hi(k); };
+        if (off == 0) {
+          t = cadd(A(m), t);
+          if (m < nref - 1) t = cadd(A(m + 1), t);
+          if (m == nref - 1) t = cadd(t, csub(cscale(A(nref - 2), 2.0f), A(nref - 1)));
+        } else {
+          if (m >= 1) t = cadd(A(m - 1), t);
+          t = cadd(A(m), t);
+          if (m == 0) t = cadd(t, csub(cscale(A(0), 2.0f), A(1)));
+        }
+      }
+      const float2 r = csub(cen[m], cscale(t, 1.0f / 5.0f));
+      nz[0] += cpw(r);
+    }
+    block_sum<1>(nz, red);
+  }
+  const float noise = nz[0] / (float)nref / (float)nsym * sqrtf(5.0f);
+
+  // 3. smoothing filter (chest_common.c:42-88)
+  if (threadIdx.x == 0) {
+    uint32_t flen = 0;
+    if (a.filter_type == 0) {
+      const uint32_t order = a.coef0 <= 0 ? 4u : (uint32_t)a.coef0;
+      const float    sd    = a.coef0 <= 0 ? noise * 200.0f : a.coef1;
+      flen                 = min(order + 1, 15u);
+      const int c          = (int)(flen - 1) / 2;
+      float     nrm        = 0.f;
+      for (int i = 0; i < (int)flen; i++) {
+        const float d = (float)(i - c);
+        filt[i]       = expf(-(d * d) / (2.0f * (sd * sd)));
+        nrm += filt[i];
+      }
+      const float in = 1.0f / nrm;
+      for (uint32_t i = 0; i < flen; i++) filt[i] *= in;
+    } else if (a.filter_type == 1) {
+      filt[0] = filt[2] = a.coef0;
+      filt[1]           = 1 - 2 * a.coef0;
+      flen              = 3;
+    }
+    flen_s = flen;
+  }
+  __syncthreads();
+  const uint32_t M = flen_s;
+
+  // 4. average_pilots (:530-567): merge the pilot symbols, scale 2/nsym, then srslte_conv_same_cf
+  const float2* src = pe;
+  if (a.filter_type != 2) {
+    const bool  first_lo = crs_fidx(a.cell_id, 0, port) < 3;
+    const float scale    = 2.0f / (float)nsym;
+    for (uint32_t i = threadIdx.x; i < nref; i += blockDim.x) {
+      float2 x = first_lo ? pe[i] : pe[nref + i], y = first_lo ? pe[nref + i] : pe[i];
+      for (uint32_t l = 2; l + 1 < nsym; l += 2) {
+        x = cadd(x, first_lo ? pe[l * nref + i] : pe[(l + 1) * nref + i]);
+        y = cadd(y, first_lo ? pe[(l + 1) * nref + i] : pe[l * nref + i]);
+      }
+      avg[2 * i]     = cscale(x, scale);
+      avg[2 * i + 1] = cscale(y, scale);
+    }
+    __syncthreads();
+    const uint32_t N = 2 * nref, h = M / 2;
+    for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+      float2 accv = make_float2(0.f, 0.f);
+      for (uint32_t k = 0; k < M; k++) {
+        float2   x;
+        const int idx = (int)i - (int)h + (int)k; // position in the extended sequence
+        if (i < h) {                              // first[i + k]
+          const uint32_t f = i + k;
+          x = f < h ? csub(cscale(avg[1], (float)(2 + h - f)), cscale(avg[0], (float)(1 + h - f))) : avg[f - h];
+        } else if (i >= N - h) { // last[j + k], j = i - (N - h)
+          const uint32_t f = i - (N - h) + k;
+          x = f >= M - 1 ? csub(cscale(avg[N - 1], (float)(2 + f - h)), cscale(avg[N - 2], (float)(1 + f - h)))
+                         : avg[N - M + f + 1];
+        } else {
+          x = avg[idx];
+        }
+        accv = cadd(accv, cscale(x, filt[k]));
+      }
+      smo[i] = accv;
+    }
+    __syncthreads();
+    src = smo;
+  }
+
+  // 5. interpolate_pilots (AVERAGE, nsymbols > 1): srslte_interp_linear_offset with M = 3 over 4*nof_prb
+  //    merged pilots starting at subcarrier id % 3, then the same estimate on every OFDM symbol
+  {
+    const uint32_t len = 4 * nprb, off_st = a.cell_id % 3, off_end = 3 - off_st;
+    const float    rM  = 1.0f / 3.0f;
+    for (uint32_t k = threadIdx.x; k < nre; k += blockDim.x) {
+      float2 v;
+      if (k < off_st) { // output[off_st - j - 1], j = off_st - 1 - k
+        const uint32_t j = off_st - 1 - k;
+        const float2   d = csub(src[1], src[0]);
+        v = csub(src[0], make_float2((float)(j + 1) * d.x / 3.0f, (float)(j + 1) * d.y / 3.0f));
+      } else if (k < off_st + 3 * (len - 1)) {
+        const uint32_t i = (k - off_st) / 3, j = (k - off_st) % 3;
+        const float2   d = cscale(csub(src[i + 1], src[i]), rM);
+        v                = cadd(src[i], cscale(d, (float)j));
+      } else {
+        const uint32_t j = k - off_st - 3 * (len - 1);
+        const float2   d = csub(src[len - 1], src[len - 2]);
+        v = cadd(src[len - 1], make_float2((float)j * d.x / 3.0f, (float)j * d.y / 3.0f));
+      }
+      row[k] = v;
+    }
+    (void)off_end;
+  }
+  __syncthreads();
+  const uint32_t nrows = 2 * a.nsymb;
+  for (uint32_t k = threadIdx.x; k < nrows * nre; k += blockDim.x) J.ce[k] = row[k % nre];
+  if (threadIdx.x == 0) {
+    J.out[0] = noise;
+    J.out[1] = acc[0] / (float)np;
+    J.out[2] = acc[1] / (float)nsym;
+    J.out[3] = acc[2];
+    J.out[4] = acc[3];
+  }
+}
+
+hipError_t chest_launch(const ChestArgs& a, uint32_t njobs, hipStream_t s)
+{
+  if (!njobs) return hipSuccess;
+  hipLaunchKernelGGL(chest_estimate, dim3(njobs), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+} // namespace mi355

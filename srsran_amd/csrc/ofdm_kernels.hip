@@ -1,0 +1,131 @@
+// srsran_amd/csrc/ofdm_kernels.hip -- OFDM demodulator (srslte_ofdm_rx_sf, lib/src/phy/dft/ofdm.c:392-471).
+//
+// One workgroup per (subframe x rx antenna, OFDM symbol): the N time samples after the cyclic prefix are
+// staged in LDS, transformed by an in-LDS Stockham autosort FFT (radix 8/4/2 stages plus one radix-3 stage
+// for the 3*2^k sizes of the non-standard LTE rates: 1536 = 3*8*8*8), and written FFT-shifted without DC:
+// out[k] = X[N - nre/2 + k] (k < nre/2), X[1 + k - nre/2] (k >= nre/2).  Forward DFT, no normalisation, as
+// FFTW's plan in ofdm.c with ue_dl.c:93's normalize = false.  Twiddles come from a table computed in double.
+// HBM traffic per symbol: N*8 B in, nre*8 B out; the LDS passes are the only other work.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ue_dl_internal.h"
+
+namespace mi355 {
+
+namespace {
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b)
+{
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); } // * (-i)
+
+__device__ __forceinline__ void dft2(float2& a, float2& b)
+{
+  const float2 t = a;
+  a              = cadd(t, b);
+  b              = csub(t, b);
+}
+
+__device__ __forceinline__ void dft4(float2* v)
+{
+  const float2 s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
+  const float2 s13 = cadd(v[1], v[3]), d13 = mul_mi(csub(v[1], v[3]));
+  v[0] = cadd(s02, s13);
+  v[2] = csub(s02, s13);
+  v[1] = cadd(d02, d13);
+  v[3] = csub(d02, d13);
+}
+
+__device__ __forceinline__ void dft8(float2* v)
+{
+  float2 e[4] = {v[0], v[2], v[4], v[6]}, o[4] = {v[1], v[3], v[5], v[7]};
+  dft4(e);
+  dft4(o);
+  const float c = 0.70710678118654752f;
+  o[1]          = make_float2(c * (o[1].x + o[1].y), c * (o[1].y - o[1].x));   // * exp(-i pi/4)
+  o[2]          = mul_mi(o[2]);                                               // * exp(-i pi/2)
+  o[3]          = make_float2(c * (o[3].y - o[3].x), -c * (o[3].x + o[3].y)); // * exp(-3i pi/4)
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    v[k]     = cadd(e[k], o[k]);
+    v[k + 4] = csub(e[k], o[k]);
+  }
+}
+
+__device__ __forceinline__ void dft3(float2* v)
+{
+  const float  s  = 0.86602540378443865f; // sin(2 pi / 3)
+  const float2 t  = cadd(v[1], v[2]);
+  const float2 d  = csub(v[1], v[2]);
+  const float2 m  = make_float2(v[0].x - 0.5f * t.x, v[0].y - 0.5f * t.y);
+  const float2 jd = make_float2(s * d.y, -s * d.x); // -i * sin * d
+  v[0]            = cadd(v[0], t);
+  v[1]            = cadd(m, jd);
+  v[2]            = csub(m, jd);
+}
+
+template <int R>
+__device__ __forceinline__ void stage(const float2* __restrict__ src, float2* __restrict__ dst, const float2* tw,
+                                      uint32_t N, uint32_t Ns)
+{
+  const uint32_t nb = N / R, tws = N / (Ns * R);
+  for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
+    const uint32_t k0 = j % Ns;
+    float2         v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      v[r] = src[j + r * nb];
+      if (r) v[r] = cmul(v[r], tw[(r * k0 * tws) % N]);
+    }
+    if constexpr (R == 2) dft2(v[0], v[1]);
+    if constexpr (R == 3) dft3(v);
+    if constexpr (R == 4) dft4(v);
+    if constexpr (R == 8) dft8(v);
+    const uint32_t d = (j / Ns) * Ns * R + k0;
+#pragma unroll
+    for (int r = 0; r < R; r++) dst[d + r * Ns] = v[r];
+  }
+}
+
+} // namespace
+
+__global__ __launch_bounds__(256) void ofdm_rx(OfdmArgs a)
+{
+  __shared__ float2 buf[2][OFDM_MAX_N];
+  const OfdmJob  J    = a.jobs[blockIdx.y];
+  const uint32_t sym  = blockIdx.x; // 0 .. 2*nsymb-1
+  const uint32_t slot = sym / a.nsymb, l = sym % a.nsymb;
+  const float2*  in   = J.in + (size_t)slot * a.slot_sz + a.cp0 + (size_t)l * (a.N + a.cp1);
+  const uint32_t N    = a.N;
+  for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) buf[0][i] = in[i];
+  __syncthreads();
+  uint32_t src = 0, Ns = 1;
+  for (uint32_t s = 0; s < a.nstages; s++) {
+    const uint32_t R = a.radix[s];
+    switch (R) {
+      case 2: stage<2>(buf[src], buf[src ^ 1], a.tw, N, Ns); break;
+      case 3: stage<3>(buf[src], buf[src ^ 1], a.tw, N, Ns); break;
+      case 4: stage<4>(buf[src], buf[src ^ 1], a.tw, N, Ns); break;
+      default: stage<8>(buf[src], buf[src ^ 1], a.tw, N, Ns); break;
+    }
+    __syncthreads();
+    src ^= 1;
+    Ns *= R;
+  }
+  float2*        out  = J.out + (size_t)sym * a.nre;
+  const uint32_t half = a.nre / 2;
+  for (uint32_t k = threadIdx.x; k < a.nre; k += blockDim.x) out[k] = buf[src][k < half ? N - half + k : 1 + k - half];
+}
+
+hipError_t ofdm_launch_rx(const OfdmArgs& a, uint32_t njobs, hipStream_t s)
+{
+  if (!njobs) return hipSuccess;
+  hipLaunchKernelGGL(ofdm_rx, dim3(2 * a.nsymb, njobs), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+} // namespace mi355

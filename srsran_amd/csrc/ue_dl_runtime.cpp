@@ -1,0 +1,391 @@
+// srsran_amd/csrc/ue_dl_runtime.cpp -- host runtime behind include/srsran_amd/ue_dl.h: OFDM demodulation and
+// channel estimation over batches of subframes, and the srslte_ue_dl-level object owning the PDSCH receiver.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <mutex>
+#include <stdio.h>
+#include <string.h>
+#include <vector>
+
+#include "../../include/srsran_amd/pdsch.h"
+#include "../../include/srsran_amd/tdec.h"
+#include "../../include/srsran_amd/ue_dl.h"
+#include "ue_dl_internal.h"
+
+using namespace mi355;
+
+#define CHECK_HIP(x)                                                                                                   \
+  do {                                                                                                                 \
+    hipError_t e_ = (x);                                                                                               \
+    if (e_ != hipSuccess) {                                                                                            \
+      fprintf(stderr, "[srsran_amd] %s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));                 \
+      return MI355_ERROR;                                                                                              \
+    }                                                                                                                  \
+  } while (0)
+
+namespace {
+
+constexpr uint32_t MAXPRB = 110;
+
+// srslte_symbol_sz / srslte_symbol_sz_power2 (common/phy_common.c:334-380)
+uint32_t symbol_sz(uint32_t nof_prb, bool std_rates)
+{
+  static const uint32_t lim[6] = {6, 15, 25, 50, 75, 110};
+  static const uint32_t ns[6]  = {128, 256, 384, 768, 1024, 1536};
+  static const uint32_t st[6]  = {128, 256, 512, 1024, 1536, 2048};
+  if (nof_prb == 0) return 0;
+  for (int i = 0; i < 6; i++)
+    if (nof_prb <= lim[i]) return std_rates ? st[i] : ns[i];
+  return 0;
+}
+
+uint32_t cp_len(uint32_t N, uint32_t c) { return (uint32_t)std::ceil((float)c * N / 2048.0f); } // SRSLTE_CP_LEN
+
+// radix plan: at most one radix-3 stage, then 8s, then a 4 or 2 remainder
+int radix_plan(uint32_t N, uint32_t* r)
+{
+  int n = 0;
+  if (N % 3 == 0) {
+    r[n++] = 3;
+    N /= 3;
+  }
+  while (N % 8 == 0 && N > 1) {
+    r[n++] = 8;
+    N /= 8;
+  }
+  if (N == 4 || N == 2) r[n++] = N, N = 1;
+  return N == 1 ? n : -1;
+}
+
+// 36.211 7.2 Gold sequence (sequence.c), c_init -> len bits
+void gold(uint32_t c_init, uint32_t len, std::vector<uint8_t>& c)
+{
+  c.resize(len);
+  uint32_t x1 = 1, x2 = c_init & 0x7fffffff;
+  for (uint32_t n = 0; n < 1600 + len; n++) {
+    if (n >= 1600) c[n - 1600] = (uint8_t)((x1 ^ x2) & 1u);
+    const uint32_t f1 = ((x1 >> 3) ^ x1) & 1u, f2 = ((x2 >> 3) ^ (x2 >> 2) ^ (x2 >> 1) ^ x2) & 1u;
+    x1 = (x1 >> 1) | (f1 << 30);
+    x2 = (x2 >> 1) | (f2 << 30);
+  }
+}
+
+uint32_t crs_nsymbol(uint32_t l, uint32_t nsymb, uint32_t port)
+{
+  if (port < 2) return (l % 2) ? (l / 2 + 1) * nsymb - 3 : (l / 2) * nsymb;
+  return 1 + l * nsymb;
+}
+
+// srslte_refsignal_cs_set_cell (refsignal_dl.c:63-114): pilots[pair][sf][4 * 2 * nof_prb]
+std::vector<float2> crs_table(const mi355_cell_t& c)
+{
+  const uint32_t nref = 2 * c.nof_prb, nsymb = c.cp == MI355_CP_EXT ? 6 : 7, Ncp = c.cp == MI355_CP_EXT ? 0 : 1;
+  std::vector<float2>  t(2 * 10 * 4 * nref, make_float2(0.f, 0.f));
+  std::vector<uint8_t> seq;
+  for (uint32_t ns = 0; ns < 20; ns++) {
+    for (uint32_t p = 0; p < 2; p++) {
+      const uint32_t nsymbols = (p == 0 ? 4 : 2) / 2;
+      for (uint32_t l = 0; l < nsymbols; l++) {
+        const uint32_t lp     = crs_nsymbol(l, nsymb, 2 * p);
+        const uint32_t c_init = 1024 * (7 * (ns + 1) + lp + 1) * (2 * c.id + 1) + 2 * c.id + Ncp;
+        gold(c_init, 4 * MAXPRB, seq);
+        for (uint32_t i = 0; i < nref; i++) {
+          const uint32_t idx = nref * ((ns % 2) * nsymbols + l) + i, mp = i + MAXPRB - c.nof_prb;
+          t[(p * 10 + ns / 2) * 4 * nref + idx] =
+              make_float2((float)((1 - 2 * (float)seq[2 * mp]) * M_SQRT1_2), (float)((1 - 2 * (float)seq[2 * mp + 1]) * M_SQRT1_2));
+        }
+      }
+    }
+  }
+  return t;
+}
+
+float to_db(float v) { return 10.0f * log10f(v); }
+float to_dbm(float v) { return to_db(v) + 30.0f; }
+
+} // namespace
+
+struct mi355_ue_dl {
+  int            device = 0;
+  mi355_cell_t   cell{};
+  uint32_t       nof_rx = 1;
+  bool           std_rates = false;
+  hipStream_t    own       = nullptr;
+  OfdmArgs       ofdm{};
+  float2*        tw     = nullptr;
+  float2*        pilots = nullptr;
+  mi355_pdsch_t* pdsch  = nullptr;
+  char*          scratch = nullptr;
+  size_t         scratch_cap = 0;
+  std::mutex     mu;
+};
+
+static int set_dft(mi355_ue_dl_t* q)
+{
+  const uint32_t N = symbol_sz(q->cell.nof_prb, q->std_rates);
+  OfdmArgs&      a = q->ofdm;
+  if (!N || N > OFDM_MAX_N) return MI355_ERROR_INVALID_INPUTS;
+  int ns = radix_plan(N, a.radix);
+  if (ns < 0) return MI355_ERROR;
+  a.nstages = (uint32_t)ns;
+  a.N       = N;
+  a.nre     = 12 * q->cell.nof_prb;
+  a.nsymb   = q->cell.cp == MI355_CP_EXT ? 6 : 7;
+  if (q->cell.cp == MI355_CP_EXT) {
+    a.cp0 = a.cp1 = cp_len(N, 512);
+  } else {
+    a.cp0 = cp_len(N, 160);
+    a.cp1 = cp_len(N, 144);
+  }
+  a.slot_sz = N * 15 / 2; // SRSLTE_SLOT_LEN
+  std::vector<float2> tw(N);
+  for (uint32_t m = 0; m < N; m++) {
+    const double ang = -2.0 * M_PI * (double)m / (double)N;
+    tw[m]            = make_float2((float)std::cos(ang), (float)std::sin(ang));
+  }
+  if (q->tw) CHECK_HIP(hipFree(q->tw));
+  CHECK_HIP(hipMalloc(&q->tw, N * sizeof(float2)));
+  CHECK_HIP(hipMemcpy(q->tw, tw.data(), N * sizeof(float2), hipMemcpyHostToDevice));
+  a.tw = q->tw;
+  return MI355_SUCCESS;
+}
+
+static int get_scratch(mi355_ue_dl_t* q, size_t bytes, char** p)
+{
+  if (bytes > q->scratch_cap) {
+    if (q->scratch) {
+      CHECK_HIP(hipDeviceSynchronize());
+      CHECK_HIP(hipFree(q->scratch));
+      q->scratch = nullptr;
+    }
+    const size_t cap = bytes + bytes / 4 + 4096;
+    CHECK_HIP(hipMalloc(&q->scratch, cap));
+    q->scratch_cap = cap;
+  }
+  *p = q->scratch;
+  return MI355_SUCCESS;
+}
+
+static int ofdm_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, hipStream_t s)
+{
+  std::vector<OfdmJob> oj;
+  oj.reserve((size_t)njobs * q->nof_rx);
+  for (uint32_t i = 0; i < njobs; i++) {
+    for (uint32_t r = 0; r < q->nof_rx; r++) {
+      if (!jobs[i].in_buffer[r] || !jobs[i].sf_symbols[r]) return MI355_ERROR_INVALID_INPUTS;
+      oj.push_back(OfdmJob{(const float2*)jobs[i].in_buffer[r], (float2*)jobs[i].sf_symbols[r]});
+    }
+  }
+  char* base = nullptr;
+  int   r    = get_scratch(q, oj.size() * sizeof(OfdmJob) + 256, &base);
+  if (r) return r;
+  CHECK_HIP(hipMemcpyAsync(base, oj.data(), oj.size() * sizeof(OfdmJob), hipMemcpyHostToDevice, s));
+  OfdmArgs a = q->ofdm;
+  a.jobs     = (const OfdmJob*)base;
+  // grid.y is limited to 65535: launch in chunks
+  for (size_t off = 0; off < oj.size(); off += 65535) {
+    a.jobs = (const OfdmJob*)base + off;
+    CHECK_HIP(ofdm_launch_rx(a, (uint32_t)std::min<size_t>(65535, oj.size() - off), s));
+  }
+  return MI355_SUCCESS;
+}
+
+// fill_res (chest_dl.c:944-972) from per (rx, port) noise / rsrp / rssi / sum(pe)
+static void fill_res(const mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const float* v, mi355_chest_dl_res_t* res)
+{
+  const uint32_t P = q->cell.nof_ports, R = q->nof_rx, nprb = q->cell.nof_prb;
+  float          noise[4][4] = {}, rsrp[4][4] = {}, rssi[4][4] = {}, rsrp_corr[4][4] = {};
+  const uint32_t npil[4] = {8 * nprb, 8 * nprb, 4 * nprb, 4 * nprb};
+  for (uint32_t a = 0; a < R; a++) {
+    for (uint32_t p = 0; p < P; p++) {
+      const float* o = &v[(a * P + p) * 5];
+      noise[a][p]    = o[0];
+      rsrp[a][p]     = o[1];
+      rssi[a][p]     = o[2];
+      if (cfg->rsrp_neighbour) { // estimate_port :797-800
+        const double e  = std::sqrt((double)(o[3] / npil[p]) * (o[3] / npil[p]) + (double)(o[4] / npil[p]) * (o[4] / npil[p]));
+        rsrp_corr[a][p] = (float)(e * e);
+      }
+    }
+  }
+  memset(res, 0, sizeof(*res));
+  res->nof_re = 2 * (q->cell.cp == MI355_CP_EXT ? 6 : 7) * 12 * nprb;
+  // get_noise
+  float n = 0;
+  for (uint32_t a = 0; a < R; a++) {
+    float acc = 0;
+    for (uint32_t p = 0; p < P; p++) acc += noise[a][p];
+    n += acc / P;
+  }
+  n /= R;
+  auto rsrp_port = [&](uint32_t port) {
+    float sum = 0;
+    for (uint32_t j = 0; j < R; j++) sum += rsrp[j][port];
+    return sum / R;
+  };
+  // get_rsrp: the reference iterates its "port" argument over the rx antenna count (chest_dl.c:897-905)
+  float rs = -1e9f;
+  for (uint32_t i = 0; i < R; i++) rs = std::max(rs, rsrp_port(i));
+  float neigh = -1e9f;
+  for (uint32_t i = 0; i < R; i++) {
+    float sum = 0;
+    for (uint32_t j = 0; j < P; j++) sum += rsrp_corr[i][j];
+    neigh = std::max(neigh, sum / P);
+  }
+  float rq = 0, ri = 0;
+  for (uint32_t a = 0; a < R; a++) {
+    rq += nprb * rsrp[a][0] / rssi[a][0];
+    ri += 4 * rssi[a][0] / nprb / 12;
+  }
+  rq /= R;
+  ri /= R;
+  res->noise_estimate     = n;
+  res->noise_estimate_dbm = to_dbm(n);
+  res->cfo                = 0.f;
+  res->rsrp               = rs;
+  res->rsrp_dbm           = to_dbm(rs);
+  res->rsrp_neigh         = neigh;
+  res->rsrq               = rq;
+  res->rsrq_db            = to_db(rq);
+  res->snr_db             = to_db(rs / n);
+  res->rssi_dbm           = to_dbm(ri);
+  res->sync_error         = 0.f;
+  for (uint32_t p = 0; p < P; p++) {
+    res->rsrp_port_dbm[p] = to_dbm(rsrp_port(p));
+    for (uint32_t a = 0; a < R; a++) {
+      res->snr_ant_port_db[a][p]   = to_db(rsrp[a][p] / noise[a][p]);
+      res->rsrp_ant_port_dbm[a][p] = to_dbm(rsrp[a][p]);
+      res->rsrq_ant_port_db[a][p]  = to_db(nprb * rsrp[a][p] / rssi[a][p]);
+    }
+  }
+}
+
+static int chest_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, const mi355_chest_dl_cfg_t* cfg,
+                     mi355_chest_dl_res_t* res, hipStream_t s)
+{
+  if (!cfg || !res) return MI355_ERROR_INVALID_INPUTS;
+  // supported: AVERAGE estimator, REFS noise, no CFO / sync-error correction (the srsUE and phy_dl_test setup)
+  if (cfg->estimator_alg != MI355_ESTIMATOR_ALG_AVERAGE || cfg->noise_alg != MI355_NOISE_ALG_REFS ||
+      cfg->cfo_estimate_enable || cfg->sync_error_enable || cfg->filter_type > MI355_CHEST_FILTER_NONE)
+    return MI355_ERROR;
+  const uint32_t        P = q->cell.nof_ports, R = q->nof_rx;
+  std::vector<ChestJob> cj;
+  cj.reserve((size_t)njobs * P * R);
+  const size_t nout = (size_t)njobs * P * R * 5;
+  char*        base = nullptr;
+  const size_t jb   = ((size_t)njobs * P * R * sizeof(ChestJob) + 255) / 256 * 256;
+  int          r    = get_scratch(q, jb + nout * 4 + 256, &base);
+  if (r) return r;
+  float* d_out = (float*)(base + jb);
+  for (uint32_t i = 0; i < njobs; i++) {
+    for (uint32_t a = 0; a < R; a++) {
+      for (uint32_t p = 0; p < P; p++) {
+        if (!jobs[i].sf_symbols[a] || !jobs[i].ce[p][a]) return MI355_ERROR_INVALID_INPUTS;
+        cj.push_back(ChestJob{(const float2*)jobs[i].sf_symbols[a], (float2*)jobs[i].ce[p][a],
+                              d_out + ((size_t)i * R * P + a * P + p) * 5, jobs[i].tti % 10, p});
+      }
+    }
+  }
+  CHECK_HIP(hipMemcpyAsync(base, cj.data(), cj.size() * sizeof(ChestJob), hipMemcpyHostToDevice, s));
+  ChestArgs ca{};
+  ca.jobs        = (const ChestJob*)base;
+  ca.pilots      = q->pilots;
+  ca.nof_prb     = q->cell.nof_prb;
+  ca.cell_id     = q->cell.id;
+  ca.nsymb       = q->cell.cp == MI355_CP_EXT ? 6 : 7;
+  ca.filter_type = cfg->filter_type;
+  ca.coef0       = cfg->filter_coef[0];
+  ca.coef1       = cfg->filter_coef[1];
+  CHECK_HIP(chest_launch(ca, (uint32_t)cj.size(), s));
+  std::vector<float> out(nout);
+  CHECK_HIP(hipMemcpyAsync(out.data(), d_out, nout * 4, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipStreamSynchronize(s));
+  for (uint32_t i = 0; i < njobs; i++) fill_res(q, cfg, &out[(size_t)i * R * P * 5], &res[i]);
+  return MI355_SUCCESS;
+}
+
+extern "C" {
+
+uint32_t mi355_symbol_sz(uint32_t nof_prb, int use_standard_rates) { return symbol_sz(nof_prb, use_standard_rates != 0); }
+
+int mi355_ue_dl_create(mi355_ue_dl_t** q, const mi355_cell_t* cell, uint32_t nof_rx_antennas, int device)
+{
+  if (!q || !cell || cell->nof_prb == 0 || cell->nof_prb > MI355_MAX_PRB || nof_rx_antennas == 0 ||
+      nof_rx_antennas > MI355_MAX_RX_ANT || !(cell->nof_ports == 1 || cell->nof_ports == 2 || cell->nof_ports == 4) ||
+      cell->frame_type != MI355_FDD)
+    return MI355_ERROR_INVALID_INPUTS;
+  CHECK_HIP(hipSetDevice(device));
+  auto* d   = new mi355_ue_dl;
+  d->device = device;
+  d->cell   = *cell;
+  d->nof_rx = nof_rx_antennas;
+  const std::vector<float2> pil = crs_table(*cell);
+  if (hipStreamCreateWithFlags(&d->own, hipStreamNonBlocking) != hipSuccess || set_dft(d) != MI355_SUCCESS ||
+      hipMalloc(&d->pilots, pil.size() * sizeof(float2)) != hipSuccess ||
+      hipMemcpy(d->pilots, pil.data(), pil.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+      mi355_pdsch_create(&d->pdsch, cell, nof_rx_antennas, device) != MI355_SUCCESS) {
+    mi355_ue_dl_destroy(d);
+    return MI355_ERROR;
+  }
+  *q = d;
+  return MI355_SUCCESS;
+}
+
+void mi355_ue_dl_destroy(mi355_ue_dl_t* q)
+{
+  if (!q) return;
+  (void)hipSetDevice(q->device);
+  (void)hipDeviceSynchronize();
+  (void)hipFree(q->tw);
+  (void)hipFree(q->pilots);
+  (void)hipFree(q->scratch);
+  mi355_pdsch_destroy(q->pdsch);
+  if (q->own) (void)hipStreamDestroy(q->own);
+  delete q;
+}
+
+int mi355_ue_dl_set_standard_rates(mi355_ue_dl_t* q, int enable)
+{
+  if (!q) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  q->std_rates = enable != 0;
+  return set_dft(q);
+}
+
+int mi355_ofdm_rx_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, void* stream)
+{
+  if (!q || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t s = stream ? (hipStream_t)stream : q->own;
+  int         r = ofdm_run(q, jobs, njobs, s);
+  if (r) return r;
+  CHECK_HIP(hipStreamSynchronize(s));
+  return MI355_SUCCESS;
+}
+
+int mi355_chest_dl_estimate_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs,
+                                  const mi355_chest_dl_cfg_t* cfg, mi355_chest_dl_res_t* res, void* stream)
+{
+  if (!q || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  return chest_run(q, jobs, njobs, cfg, res, stream ? (hipStream_t)stream : q->own);
+}
+
+int mi355_ue_dl_decode_fft_estimate_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs,
+                                          const mi355_chest_dl_cfg_t* cfg, mi355_chest_dl_res_t* res, void* stream)
+{
+  if (!q || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t s = stream ? (hipStream_t)stream : q->own;
+  int         r = ofdm_run(q, jobs, njobs, s);
+  if (r) return r;
+  return chest_run(q, jobs, njobs, cfg, res, s);
+}
+
+mi355_pdsch_t* mi355_ue_dl_pdsch(mi355_ue_dl_t* q) { return q ? q->pdsch : nullptr; }
+
+} // extern "C"
