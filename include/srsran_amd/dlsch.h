@@ -34,6 +34,10 @@ int mi355_softbuffer_reset(mi355_softbuffer_pool_t* p, uint32_t sb, void* stream
 int mi355_softbuffer_reset_tbs(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t tbs, void* stream);
 int mi355_softbuffer_reset_cb(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t nof_cb, void* stream);
 int mi355_softbuffer_reset_all(mi355_softbuffer_pool_t* p, void* stream);
+/* srslte_softbuffer_rx_reset on softbuffers [first, first + n) with one launch */
+int mi355_softbuffer_reset_range(mi355_softbuffer_pool_t* p, uint32_t first, uint32_t n, void* stream);
+/* device address of the pool's int16 code-block buffers (slot = sb * max_cb + cb, `stride` int16 apart) */
+int mi355_softbuffer_pool_buffer(mi355_softbuffer_pool_t* p, int16_t** buf, uint32_t* stride, uint32_t* max_cb);
 
 typedef struct {
   uint32_t tbs;         /* transport block size in bits (grant.tb[i].tbs) */
@@ -51,6 +55,9 @@ int  mi355_dlsch_create(mi355_dlsch_t** q, int device);
 void mi355_dlsch_destroy(mi355_dlsch_t* q);
 /* srslte_sch_set_max_noi (sch.c:222-225): half-iterations per CB, default 10 (SRSLTE_PDSCH_MAX_TDEC_ITERS) */
 int mi355_dlsch_set_max_iterations(mi355_dlsch_t* q, uint32_t max_iterations);
+/* HIP-event timing of the MAP half-iteration kernel launches of this decoder (all code-block sizes) */
+void mi355_dlsch_set_profiling(mi355_dlsch_t* q, int enable);
+int  mi355_dlsch_kernel_stats(mi355_dlsch_t* q, double* ms, uint32_t* launches);
 
 /* Decode ntb transport blocks whose descrambled LLRs are in device memory.  Synchronous: returns after
  * ret[] (host, one srslte return code per TB) and avg_iterations[] (host, nullable; q->avg_iterations of

@@ -123,6 +123,9 @@ int mi355_pdsch_decode_batch(mi355_pdsch_t*           q,
                              mi355_pdsch_res_t*       res,
                              void*                    stream);
 
+/* The DL-SCH decoder owned by this PDSCH receiver (borrowed: srslte_pdsch_t.dl_sch), e.g. for profiling. */
+mi355_dlsch_t* mi355_pdsch_dlsch(mi355_pdsch_t* q);
+
 /* Host-only helpers (no device needed):
  * the srslte_pdsch_get extraction order as grid indices (l' * 12 * nof_prb + k) for grant.prb_idx and
  * grant.nof_symb_slot (0 entries: the CP's symbol count).  Returns the number of REs; idx may be NULL. */

@@ -104,6 +104,20 @@ int mi355_ue_dl_decode_fft_estimate_batch(mi355_ue_dl_t*              q,
                                           mi355_chest_dl_res_t*       res,
                                           void*                       stream);
 
+/* srslte_ue_dl_decode_pdsch (ue/ue_dl.c:486-520) for a batch: the PDSCH of job i is read from sfjobs[i]'s grids
+ * and channel estimates with chest[i].noise_estimate, configured by sfs[i] / cfgs[i]; payloads[2*i + tb] are
+ * device buffers (tbs/8 + 6 bytes); res[2*i + tb] as mi355_pdsch_decode_batch. */
+int mi355_ue_dl_decode_pdsch_batch(mi355_ue_dl_t*              q,
+                                   mi355_softbuffer_pool_t*    pool,
+                                   const mi355_dl_sf_job_t*    sfjobs,
+                                   const mi355_dl_sf_cfg_t*    sfs,
+                                   const mi355_pdsch_cfg_t*    cfgs,
+                                   const mi355_chest_dl_res_t* chest,
+                                   uint8_t* const*             payloads,
+                                   uint32_t                    njobs,
+                                   mi355_pdsch_res_t*          res,
+                                   void*                       stream);
+
 /* The PDSCH receiver bound to this UE's cell (borrowed; valid until mi355_ue_dl_destroy). */
 mi355_pdsch_t* mi355_ue_dl_pdsch(mi355_ue_dl_t* q);
 

@@ -89,6 +89,7 @@ struct mi355_dlsch {
   char*  scratch     = nullptr;
   size_t scratch_cap = 0;
   std::mutex mu;
+  bool       prof = false;
 };
 
 static int rm_table(mi355_dlsch_t* q, uint32_t K, uint32_t rv, const uint16_t** out)
@@ -190,6 +191,25 @@ int mi355_softbuffer_reset_all(mi355_softbuffer_pool_t* p, void* stream)
   return MI355_SUCCESS;
 }
 
+int mi355_softbuffer_reset_range(mi355_softbuffer_pool_t* p, uint32_t first, uint32_t n, void* stream)
+{
+  if (!p || first + n > p->nof_sb) return MI355_ERROR_INVALID_INPUTS;
+  if (!n) return MI355_SUCCESS;
+  CHECK_HIP(hipSetDevice(p->device));
+  DlschResetArgs a{p->buf, SB_STRIDE, p->cb_crc, p->data, (size_t)first * p->max_cb, (size_t)n * p->max_cb};
+  CHECK_HIP(dlsch_launch_reset(a, (hipStream_t)stream));
+  return MI355_SUCCESS;
+}
+
+int mi355_softbuffer_pool_buffer(mi355_softbuffer_pool_t* p, int16_t** buf, uint32_t* stride, uint32_t* max_cb)
+{
+  if (!p) return MI355_ERROR_INVALID_INPUTS;
+  if (buf) *buf = p->buf;
+  if (stride) *stride = SB_STRIDE;
+  if (max_cb) *max_cb = p->max_cb;
+  return MI355_SUCCESS;
+}
+
 int mi355_dlsch_create(mi355_dlsch_t** q, int device)
 {
   if (!q) return MI355_ERROR_INVALID_INPUTS;
@@ -227,6 +247,31 @@ int mi355_dlsch_set_max_iterations(mi355_dlsch_t* q, uint32_t max_iterations)
 {
   if (!q || max_iterations == 0) return MI355_ERROR_INVALID_INPUTS;
   q->max_its = max_iterations;
+  return MI355_SUCCESS;
+}
+
+void mi355_dlsch_set_profiling(mi355_dlsch_t* q, int enable)
+{
+  if (!q) return;
+  q->prof = enable != 0;
+  for (auto& kv : q->dec) mi355_tdec_batch_set_profiling(kv.second, enable);
+}
+
+int mi355_dlsch_kernel_stats(mi355_dlsch_t* q, double* ms, uint32_t* launches)
+{
+  if (!q) return MI355_ERROR_INVALID_INPUTS;
+  double   tot = 0;
+  uint32_t n   = 0;
+  for (auto& kv : q->dec) {
+    double   m = 0;
+    uint32_t l = 0;
+    int      r = mi355_tdec_batch_kernel_stats(kv.second, &m, &l);
+    if (r) return r;
+    tot += m;
+    n += l;
+  }
+  if (ms) *ms = tot;
+  if (launches) *launches = n;
   return MI355_SUCCESS;
 }
 
@@ -356,6 +401,7 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
     if (it == q->dec.end()) {
       mi355_tdec_batch_t* td = nullptr;
       if ((r = mi355_tdec_batch_create(&td, q->device))) return r;
+      mi355_tdec_batch_set_profiling(td, q->prof);
       it = q->dec.emplace(K, td).first;
     }
     live.push_back(Live{K, (uint32_t)off, n, d_dec + doff, it->second});

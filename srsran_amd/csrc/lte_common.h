@@ -1,0 +1,71 @@
+// srsran_amd/csrc/lte_common.h -- host-side LTE helpers shared by the runtimes: the 36.211 7.2 Gold
+// sequence and the cell-specific reference signal table / positions (refsignal_dl.c:63-114, :214-290).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <stdint.h>
+#include <vector>
+
+#include "../../include/srsran_amd/pdsch.h"
+
+namespace mi355 {
+
+// c(n) for n < len from c_init (common/sequence.c)
+inline void gold_sequence(uint32_t c_init, uint32_t len, std::vector<uint8_t>& c)
+{
+  c.resize(len);
+  uint32_t x1 = 1, x2 = c_init & 0x7fffffff;
+  for (uint32_t n = 0; n < 1600 + len; n++) {
+    if (n >= 1600) c[n - 1600] = (uint8_t)((x1 ^ x2) & 1u);
+    const uint32_t f1 = ((x1 >> 3) ^ x1) & 1u, f2 = ((x2 >> 3) ^ (x2 >> 2) ^ (x2 >> 1) ^ x2) & 1u;
+    x1 = (x1 >> 1) | (f1 << 30);
+    x2 = (x2 >> 1) | (f2 << 30);
+  }
+}
+
+inline uint32_t crs_nsymbol(uint32_t l, uint32_t nsymb, uint32_t port)
+{
+  if (port < 2) return (l % 2) ? (l / 2 + 1) * nsymb - 3 : (l / 2) * nsymb;
+  return 1 + l * nsymb;
+}
+
+inline uint32_t crs_v(uint32_t port, uint32_t l)
+{
+  switch (port) {
+    case 0: return (l % 2) ? 3 : 0;
+    case 1: return (l % 2) ? 0 : 3;
+    case 2: return l == 0 ? 0 : 3;
+    default: return l == 0 ? 3 : 0;
+  }
+}
+
+inline uint32_t crs_fidx(uint32_t id, uint32_t l, uint32_t port) { return (crs_v(port, l) + id % 6) % 6; }
+
+// srslte_refsignal_cs_set_cell: pilots[pair][sf][4 * 2 * nof_prb] (pair 0: ports 0/1 over 4 symbols,
+// pair 1: ports 2/3 over 2 symbols)
+inline std::vector<float2> crs_table(const mi355_cell_t& c)
+{
+  const uint32_t       MAXPRB = 110;
+  const uint32_t       nref = 2 * c.nof_prb, nsymb = c.cp == MI355_CP_EXT ? 6 : 7, Ncp = c.cp == MI355_CP_EXT ? 0 : 1;
+  std::vector<float2>  t(2 * 10 * 4 * nref, make_float2(0.f, 0.f));
+  std::vector<uint8_t> seq;
+  for (uint32_t ns = 0; ns < 20; ns++) {
+    for (uint32_t p = 0; p < 2; p++) {
+      const uint32_t nsymbols = (p == 0 ? 4 : 2) / 2;
+      for (uint32_t l = 0; l < nsymbols; l++) {
+        const uint32_t lp     = crs_nsymbol(l, nsymb, 2 * p);
+        const uint32_t c_init = 1024 * (7 * (ns + 1) + lp + 1) * (2 * c.id + 1) + 2 * c.id + Ncp;
+        gold_sequence(c_init, 4 * MAXPRB, seq);
+        for (uint32_t i = 0; i < nref; i++) {
+          const uint32_t idx = nref * ((ns % 2) * nsymbols + l) + i, mp = i + MAXPRB - c.nof_prb;
+          t[(p * 10 + ns / 2) * 4 * nref + idx] = make_float2((float)((1 - 2 * (float)seq[2 * mp]) * M_SQRT1_2),
+                                                              (float)((1 - 2 * (float)seq[2 * mp + 1]) * M_SQRT1_2));
+        }
+      }
+    }
+  }
+  return t;
+}
+
+} // namespace mi355

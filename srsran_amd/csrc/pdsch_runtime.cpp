@@ -434,6 +434,8 @@ void mi355_pdsch_destroy(mi355_pdsch_t* q)
   delete q;
 }
 
+mi355_dlsch_t* mi355_pdsch_dlsch(mi355_pdsch_t* q) { return q ? q->dlsch : nullptr; }
+
 int mi355_pdsch_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, uint32_t njobs, void* stream)
 {
   if (!q || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;

@@ -11,6 +11,7 @@
 #include "../../include/srsran_amd/pdsch.h"
 #include "../../include/srsran_amd/tdec.h"
 #include "../../include/srsran_amd/ue_dl.h"
+#include "lte_common.h"
 #include "ue_dl_internal.h"
 
 using namespace mi355;
@@ -25,8 +26,6 @@ using namespace mi355;
   } while (0)
 
 namespace {
-
-constexpr uint32_t MAXPRB = 110;
 
 // srslte_symbol_sz / srslte_symbol_sz_power2 (common/phy_common.c:334-380)
 uint32_t symbol_sz(uint32_t nof_prb, bool std_rates)
@@ -56,49 +55,6 @@ int radix_plan(uint32_t N, uint32_t* r)
   }
   if (N == 4 || N == 2) r[n++] = N, N = 1;
   return N == 1 ? n : -1;
-}
-
-// 36.211 7.2 Gold sequence (sequence.c), c_init -> len bits
-void gold(uint32_t c_init, uint32_t len, std::vector<uint8_t>& c)
-{
-  c.resize(len);
-  uint32_t x1 = 1, x2 = c_init & 0x7fffffff;
-  for (uint32_t n = 0; n < 1600 + len; n++) {
-    if (n >= 1600) c[n - 1600] = (uint8_t)((x1 ^ x2) & 1u);
-    const uint32_t f1 = ((x1 >> 3) ^ x1) & 1u, f2 = ((x2 >> 3) ^ (x2 >> 2) ^ (x2 >> 1) ^ x2) & 1u;
-    x1 = (x1 >> 1) | (f1 << 30);
-    x2 = (x2 >> 1) | (f2 << 30);
-  }
-}
-
-uint32_t crs_nsymbol(uint32_t l, uint32_t nsymb, uint32_t port)
-{
-  if (port < 2) return (l % 2) ? (l / 2 + 1) * nsymb - 3 : (l / 2) * nsymb;
-  return 1 + l * nsymb;
-}
-
-// srslte_refsignal_cs_set_cell (refsignal_dl.c:63-114): pilots[pair][sf][4 * 2 * nof_prb]
-std::vector<float2> crs_table(const mi355_cell_t& c)
-{
-  const uint32_t nref = 2 * c.nof_prb, nsymb = c.cp == MI355_CP_EXT ? 6 : 7, Ncp = c.cp == MI355_CP_EXT ? 0 : 1;
-  std::vector<float2>  t(2 * 10 * 4 * nref, make_float2(0.f, 0.f));
-  std::vector<uint8_t> seq;
-  for (uint32_t ns = 0; ns < 20; ns++) {
-    for (uint32_t p = 0; p < 2; p++) {
-      const uint32_t nsymbols = (p == 0 ? 4 : 2) / 2;
-      for (uint32_t l = 0; l < nsymbols; l++) {
-        const uint32_t lp     = crs_nsymbol(l, nsymb, 2 * p);
-        const uint32_t c_init = 1024 * (7 * (ns + 1) + lp + 1) * (2 * c.id + 1) + 2 * c.id + Ncp;
-        gold(c_init, 4 * MAXPRB, seq);
-        for (uint32_t i = 0; i < nref; i++) {
-          const uint32_t idx = nref * ((ns % 2) * nsymbols + l) + i, mp = i + MAXPRB - c.nof_prb;
-          t[(p * 10 + ns / 2) * 4 * nref + idx] =
-              make_float2((float)((1 - 2 * (float)seq[2 * mp]) * M_SQRT1_2), (float)((1 - 2 * (float)seq[2 * mp + 1]) * M_SQRT1_2));
-        }
-      }
-    }
-  }
-  return t;
 }
 
 float to_db(float v) { return 10.0f * log10f(v); }
@@ -387,5 +343,29 @@ int mi355_ue_dl_decode_fft_estimate_batch(mi355_ue_dl_t* q, const mi355_dl_sf_jo
 }
 
 mi355_pdsch_t* mi355_ue_dl_pdsch(mi355_ue_dl_t* q) { return q ? q->pdsch : nullptr; }
+
+int mi355_ue_dl_decode_pdsch_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, const mi355_dl_sf_job_t* sfjobs,
+                                   const mi355_dl_sf_cfg_t* sfs, const mi355_pdsch_cfg_t* cfgs,
+                                   const mi355_chest_dl_res_t* chest, uint8_t* const* payloads, uint32_t njobs,
+                                   mi355_pdsch_res_t* res, void* stream)
+{
+  if (!q || !pool || !res || (njobs && (!sfjobs || !sfs || !cfgs || !chest || !payloads)))
+    return MI355_ERROR_INVALID_INPUTS;
+  std::vector<mi355_pdsch_job_t> jobs(njobs);
+  for (uint32_t i = 0; i < njobs; i++) {
+    mi355_pdsch_job_t& j = jobs[i];
+    memset(&j, 0, sizeof(j));
+    j.sf             = sfs[i];
+    j.cfg            = cfgs[i];
+    j.noise_estimate = chest[i].noise_estimate; // srslte_pdsch_decode(..., &q->chest_res, ...)
+    for (uint32_t r = 0; r < q->nof_rx; r++) {
+      j.sf_symbols[r] = sfjobs[i].sf_symbols[r];
+      for (uint32_t p = 0; p < q->cell.nof_ports; p++) j.ce[p][r] = sfjobs[i].ce[p][r];
+    }
+    j.payload[0] = payloads[2 * i];
+    j.payload[1] = payloads[2 * i + 1];
+  }
+  return mi355_pdsch_decode_batch(q->pdsch, pool, jobs.data(), njobs, res, stream);
+}
 
 } // extern "C"
