@@ -38,6 +38,9 @@ def main():
     os.makedirs(OUTD, exist_ok=True)
     stats = glob.glob(os.path.join(P, "trace", "**", "*kernel_stats.csv"), recursive=True)[0]
     shutil.copy(stats, os.path.join(OUTD, f"{TAG}_kernel_stats.csv"))
+    e2e = glob.glob(os.path.join(P, "e2e", "**", "*kernel_stats.csv"), recursive=True)
+    if e2e:
+        shutil.copy(e2e[0], os.path.join(OUTD, f"{TAG}_e2e_kernel_stats.csv"))
     fetch, _ = per_kernel(counters("fetch"), "FETCH_SIZE")
     write, _ = per_kernel(counters("write"), "WRITE_SIZE")
     calib_fetch, _ = per_kernel(counters("calib"), "FETCH_SIZE")
