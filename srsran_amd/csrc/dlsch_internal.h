@@ -29,15 +29,19 @@ struct CrcTable {
   uint32_t poly;   // with the x^24 term
 };
 
+constexpr uint16_t RM_NONE = 0xffff; // decoder-buffer position no circular-buffer bit maps to
+
 struct DlschRmArgs {
   const CbDesc*   desc;
   int             ncb;
-  uint32_t        N; // 3K+12
-  const uint16_t* table[4];
+  uint32_t        N;      // 3K+12 circular-buffer bits
+  uint32_t        buflen; // decoder buffer length 3(K+32)+12 (or 3K+12 linear)
+  const uint16_t* inv[4]; // [rv][decoder position] -> circular-buffer index or RM_NONE
   const int16_t*  e;
   int16_t*        sb;
   size_t          sb_stride;
   const uint8_t*  sb_crc;
+  uint8_t*        fresh;  // per slot: buffer logically zero (lazy srslte_softbuffer_rx_reset)
 };
 
 struct DlschCheckArgs {
@@ -48,6 +52,7 @@ struct DlschCheckArgs {
   size_t         dec_stride;
   uint8_t*       data;
   uint8_t*       done;
+  uint32_t*      remaining; // unfinished code blocks of the call
   uint32_t*      its;
   uint8_t*        sb_crc;
   const CrcTable* crc24a;
@@ -65,10 +70,8 @@ struct DlschTbArgs {
 };
 
 struct DlschResetArgs {
-  int16_t* sb;
-  size_t   sb_stride;
+  uint8_t* fresh;
   uint8_t* sb_crc;
-  uint8_t* sb_data;
   size_t   slot0, ncb;
 };
 
@@ -77,6 +80,7 @@ hipError_t dlsch_launch_check(const DlschCheckArgs& a, hipStream_t s);
 hipError_t dlsch_launch_prologue(const DlschTbArgs& a, hipStream_t s);
 hipError_t dlsch_launch_epilogue(const DlschTbArgs& a, hipStream_t s);
 hipError_t dlsch_launch_reset(const DlschResetArgs& a, hipStream_t s);
-hipError_t dlsch_launch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc, int n, hipStream_t s);
+hipError_t dlsch_launch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc, int n, uint32_t* remaining,
+                                  hipStream_t s);
 
 } // namespace mi355

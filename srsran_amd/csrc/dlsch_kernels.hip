@@ -10,26 +10,50 @@ namespace mi355 {
 
 // ---------------------------------------------------------------------------- rate dematching
 // srslte_rm_turbo_rx_lut (rm_turbo.c:397-454, :717-822): out[deinter[i % N]] += in[i], wrapping int16.
-// The deinterleaver is a bijection on [0, N), so thread r owns destination deinter[r] and sums its
-// contributions i = r, r+N, r+2N, ... (wrapping addition is order independent) -- no atomics.
-__global__ __launch_bounds__(256) void dlsch_rm_rx(DlschRmArgs a)
+// The deinterleaver is a bijection from the N circular-buffer bits onto decoder-buffer positions, so the
+// kernel walks the DECODER buffer in order (coalesced int16x2 read-modify-write) and gathers, for position
+// j with circular index r = inv[j], the LLRs r, r+N, r+2N, ... < n_e (wrapping addition is order
+// independent) -- no atomics, no scattered stores.  A slot marked fresh by the lazy reset is written whole
+// (sums or zeros) instead of read, which is srslte_softbuffer_rx_reset + the first accumulation in one pass.
+// One workgroup per code block: the CB's LLRs are folded modulo N into LDS (coalesced reads, wrap-around
+// sums for E > N), then the decoder buffer is written in order from LDS gathers.
+constexpr uint32_t RM_LDS = 3 * 6144 + 12; // N of the largest code block
+
+__global__ __launch_bounds__(512) void dlsch_rm_rx(DlschRmArgs a)
 {
-  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int    b = (int)(g / a.N);
-  const int    r = (int)(g % a.N);
-  if (b >= a.ncb) return;
-  const CbDesc& d = a.desc[b];
+  __shared__ uint16_t acc[RM_LDS + 4];
+  const CbDesc& d = a.desc[blockIdx.x];
   if (a.sb_crc[d.slot]) return; // CB already decoded in an earlier transmission (sch.c:385)
-  const int16_t* e   = a.e + d.e_off + d.rp;
-  uint32_t       sum = 0;
-  bool           any = false;
-  for (uint32_t i = r; i < d.n_e; i += a.N) {
-    sum += (uint16_t)e[i];
-    any = true;
+  const uint32_t  N = a.N, tid = threadIdx.x, nt = blockDim.x;
+  const int16_t*  e = a.e + d.e_off + d.rp;
+  const uint32_t  n_e = d.n_e, first = min(n_e, N);
+  // pass 0: the first wrap initialises (positions >= n_e get 0), later wraps accumulate
+  for (uint32_t r = tid; r < N; r += nt) acc[r] = r < first ? (uint16_t)e[r] : 0;
+  for (uint32_t base = N; base < n_e; base += N) {
+    __syncthreads();
+    for (uint32_t r = tid; r < N && base + r < n_e; r += nt) acc[r] = (uint16_t)(acc[r] + (uint16_t)e[base + r]);
   }
-  if (!any) return;
-  int16_t* sb = a.sb + (size_t)d.slot * a.sb_stride + a.table[d.rv][r];
-  *sb         = (int16_t)(uint16_t)((uint16_t)*sb + sum);
+  __syncthreads();
+  const bool      fresh = a.fresh[d.slot] != 0;
+  const uint16_t* inv   = a.inv[d.rv];
+  uint32_t*       sb    = (uint32_t*)(a.sb + (size_t)d.slot * a.sb_stride);
+  const uint32_t  pairs = a.buflen / 2;
+  for (uint32_t jp = tid; jp < pairs; jp += nt) {
+    const uint32_t iv = ((const uint32_t*)inv)[jp]; // inv is 4-byte aligned (buflen even)
+    const uint32_t r0 = iv & 0xffffu, r1 = iv >> 16;
+    const bool     h0 = r0 != RM_NONE && r0 < n_e, h1 = r1 != RM_NONE && r1 < n_e;
+    if (!fresh && !h0 && !h1) continue;
+    const uint32_t s0 = h0 ? acc[r0] : 0u, s1 = h1 ? acc[r1] : 0u;
+    const uint32_t v  = fresh ? 0u : sb[jp];
+    sb[jp]            = ((v + s0) & 0xffffu) | (((v >> 16) + s1) << 16);
+  }
+}
+
+// the slot's fresh flag is consumed once every block of the CB has run: a separate tiny pass
+__global__ __launch_bounds__(256) void dlsch_rm_consume(const CbDesc* desc, int ncb, uint8_t* fresh, const uint8_t* sb_crc)
+{
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < ncb && !sb_crc[desc[b].slot]) fresh[desc[b].slot] = 0;
 }
 
 // ---------------------------------------------------------------------------- CRC helpers
@@ -66,6 +90,27 @@ __device__ uint32_t wave_crc24(const uint8_t* bytes, uint32_t nbytes, const CrcT
   return crc;
 }
 
+// the same with a whole 256-thread workgroup (TB CRC over up to 12 KB)
+__device__ uint32_t block_crc24(const uint8_t* bytes, uint32_t nbytes, const CrcTable& T)
+{
+  __shared__ uint32_t part[4];
+  const uint32_t tid   = threadIdx.x;
+  const uint32_t chunk = (nbytes + 255) / 256;
+  const uint32_t b0 = min(nbytes, tid * chunk), b1 = min(nbytes, b0 + chunk);
+  uint32_t       crc = 0;
+  for (uint32_t i = b0; i < b1; i++) crc = ((crc << 8) ^ T.t[((crc >> 16) & 0xff) ^ bytes[i]]) & 0xffffffu;
+  uint32_t after = nbytes - b1, sc = 1;
+  for (int i = 0; after; i++, after >>= 1) {
+    if (after & 1) sc = gf2_mulmod24(sc, T.pw[i], T.poly);
+  }
+  crc = gf2_mulmod24(crc, sc, T.poly);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
+  if ((tid & 63) == 0) part[tid >> 6] = crc;
+  __syncthreads();
+  return part[0] ^ part[1] ^ part[2] ^ part[3];
+}
+
 // ---------------------------------------------------------------------------- per-CB early stop
 // After half-iteration h (sch.c:415-450): decision bytes -> CRC24B (C>1) or CRC24A over tbs+24 = K bits
 // (C==1); CRC ok => the CB is finished at this iteration.  Decision bytes of CB i land at i*rlen/8 of the
@@ -75,7 +120,7 @@ __global__ __launch_bounds__(256) void dlsch_cb_check(DlschCheckArgs a)
 {
   const int b    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  if (b >= a.ncb || a.done[b]) return;
+  if (b >= a.ncb || *a.remaining == 0 || a.done[b]) return;
   const CbDesc&  d   = a.desc[b];
   const uint8_t* dec = a.dec + (size_t)b * a.dec_stride;
   const uint32_t crc = wave_crc24(dec, a.K / 8, d.C > 1 ? *a.crc24b : *a.crc24a);
@@ -87,6 +132,7 @@ __global__ __launch_bounds__(256) void dlsch_cb_check(DlschCheckArgs a)
   for (uint32_t i = lane; i < nb; i += 64) dst[i] = dec[i];
   if (lane == 0) {
     a.its[b] = a.h + 1;
+    atomicSub(a.remaining, 1u);
     if (ok) {
       a.done[b]         = 1;
       a.sb_crc[d.slot]  = 1;
@@ -119,15 +165,15 @@ __global__ __launch_bounds__(256) void dlsch_tb_prologue(DlschTbArgs a)
   }
 }
 
-// sch.c:488-500 + decode_tb :537-559
+// sch.c:488-500 + decode_tb :537-559; one workgroup per TB
 __global__ __launch_bounds__(256) void dlsch_tb_epilogue(DlschTbArgs a)
 {
-  const int t    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
+  const int t   = blockIdx.x;
+  const int tid = threadIdx.x;
   if (t >= a.ntb) return;
   const TbDesc& tb = a.tb[t];
   if (tb.C == 0) {
-    if (lane == 0) a.ret[t] = tb.invalid ? -2 : 0;
+    if (tid == 0) a.ret[t] = tb.invalid ? -2 : 0;
     return;
   }
   bool ok = true;
@@ -139,13 +185,13 @@ __global__ __launch_bounds__(256) void dlsch_tb_epilogue(DlschTbArgs a)
       if (!a.sb_crc[slot]) continue;
       const uint32_t K    = c < tb.C1 ? tb.K1 : tb.K2;
       const uint32_t rlen = tb.C == 1 ? K : K - 24;
-      for (uint32_t i = lane; i < rlen / 8; i += 64) a.sb_data[(size_t)slot * 768 + i] = data[c * rlen / 8 + i];
+      for (uint32_t i = tid; i < rlen / 8; i += blockDim.x) a.sb_data[(size_t)slot * 768 + i] = data[c * rlen / 8 + i];
     }
-    if (lane == 0) a.ret[t] = -1;
+    if (tid == 0) a.ret[t] = -1;
     return;
   }
-  const uint32_t par_rx = wave_crc24(data, tb.tbs / 8, *a.crc24a);
-  if (lane == 0) {
+  const uint32_t par_rx = block_crc24(data, tb.tbs / 8, *a.crc24a);
+  if (tid == 0) {
     const uint32_t par_tx = ((uint32_t)data[tb.tbs / 8] << 16) | ((uint32_t)data[tb.tbs / 8 + 1] << 8) |
                             (uint32_t)data[tb.tbs / 8 + 2];
     a.ret[t] = (par_rx == par_tx && par_rx) ? 0 : -1;
@@ -153,37 +199,44 @@ __global__ __launch_bounds__(256) void dlsch_tb_epilogue(DlschTbArgs a)
 }
 
 // ---------------------------------------------------------------------------- softbuffer reset
+// srslte_softbuffer_rx_reset_cb (softbuffer.c:134-154), lazily: the code-block buffers are marked fresh (the
+// next rate dematching writes them whole) instead of being zeroed, and the CRC flags are cleared.  The saved
+// decoded bytes are only ever read for CBs whose CRC flag is set, so they need no clearing.
 __global__ __launch_bounds__(256) void dlsch_sb_reset(DlschResetArgs a)
 {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t per = (size_t)a.sb_stride / 2; // u32 words per CB buffer
-  const size_t cb  = g / per;
-  if (cb >= a.ncb) return;
-  const size_t slot = a.slot0 + cb;
-  ((uint32_t*)(a.sb + slot * a.sb_stride))[g % per] = 0;
-  if (g % per < 768 / 4) ((uint32_t*)(a.sb_data + slot * 768))[g % per] = 0;
-  if (g % per == 0) a.sb_crc[slot] = 0;
+  if (g >= a.ncb) return;
+  a.fresh[a.slot0 + g]  = 1;
+  a.sb_crc[a.slot0 + g] = 0;
 }
 
 // CBs whose CRC passed in an earlier transmission start finished (sch.c:385)
 __global__ __launch_bounds__(256) void dlsch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc,
-                                                        int n)
+                                                        int n, uint32_t* remaining)
 {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < n) done[b] = sb_crc[slot[b]] ? 3 : 0;
+  const int  b    = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool todo = b < n && !sb_crc[slot[b]];
+  if (b < n) done[b] = todo ? 0 : 3;
+  const uint64_t m = __ballot(todo);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(remaining, (uint32_t)__popcll(m));
 }
 
-hipError_t dlsch_launch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc, int n, hipStream_t s)
+hipError_t dlsch_launch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc, int n, uint32_t* remaining,
+                                  hipStream_t s)
 {
-  hipLaunchKernelGGL(dlsch_init_done, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, done, slot, sb_crc, n);
+  hipLaunchKernelGGL(dlsch_init_done, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, done, slot, sb_crc, n,
+                     remaining);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------- launchers
 hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s)
 {
-  const size_t total = (size_t)a.ncb * a.N;
-  hipLaunchKernelGGL(dlsch_rm_rx, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  if (a.ncb <= 0) return hipSuccess;
+  if (a.N > RM_LDS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dlsch_rm_rx, dim3((unsigned)a.ncb), dim3(512), 0, s, a);
+  hipLaunchKernelGGL(dlsch_rm_consume, dim3((unsigned)((a.ncb + 255) / 256)), dim3(256), 0, s, a.desc, a.ncb, a.fresh,
+                     a.sb_crc);
   return hipGetLastError();
 }
 
@@ -201,14 +254,15 @@ hipError_t dlsch_launch_prologue(const DlschTbArgs& a, hipStream_t s)
 
 hipError_t dlsch_launch_epilogue(const DlschTbArgs& a, hipStream_t s)
 {
-  hipLaunchKernelGGL(dlsch_tb_epilogue, dim3((unsigned)((a.ntb + 3) / 4)), dim3(256), 0, s, a);
+  if (a.ntb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dlsch_tb_epilogue, dim3((unsigned)a.ntb), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 hipError_t dlsch_launch_reset(const DlschResetArgs& a, hipStream_t s)
 {
-  const size_t total = a.ncb * (size_t)a.sb_stride / 2;
-  hipLaunchKernelGGL(dlsch_sb_reset, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  if (!a.ncb) return hipSuccess;
+  hipLaunchKernelGGL(dlsch_sb_reset, dim3((unsigned)((a.ncb + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -39,6 +39,7 @@ struct mi355_softbuffer_pool {
   int16_t* buf    = nullptr; // nof_sb * max_cb * SB_STRIDE
   uint8_t* cb_crc = nullptr; // nof_sb * max_cb
   uint8_t* data   = nullptr; // nof_sb * max_cb * SB_DATA
+  uint8_t* fresh  = nullptr; // nof_sb * max_cb: buffer logically zero (lazy reset)
 };
 
 namespace {
@@ -92,15 +93,20 @@ struct mi355_dlsch {
   bool       prof = false;
 };
 
+static uint32_t rm_buflen(uint32_t K) { return tdec_subblocks(K) ? 3 * (K + 32) + 12 : 3 * K + 12; }
+
+// inverse of the rate-dematching table: decoder-buffer position -> circular-buffer index (or RM_NONE)
 static int rm_table(mi355_dlsch_t* q, uint32_t K, uint32_t rv, const uint16_t** out)
 {
   const uint64_t key = ((uint64_t)K << 2) | rv;
   auto           it  = q->rm.find(key);
   if (it == q->rm.end()) {
-    std::vector<uint16_t> t = rm_rx_table(K, rv);
-    uint16_t*             d = nullptr;
-    CHECK_HIP(hipMalloc(&d, t.size() * 2));
-    CHECK_HIP(hipMemcpy(d, t.data(), t.size() * 2, hipMemcpyHostToDevice));
+    const std::vector<uint16_t> t = rm_rx_table(K, rv);
+    std::vector<uint16_t>       inv(rm_buflen(K) + 1, RM_NONE);
+    for (size_t r = 0; r < t.size(); r++) inv[t[r]] = (uint16_t)r;
+    uint16_t* d = nullptr;
+    CHECK_HIP(hipMalloc(&d, inv.size() * 2));
+    CHECK_HIP(hipMemcpy(d, inv.data(), inv.size() * 2, hipMemcpyHostToDevice));
     it = q->rm.emplace(key, d).first;
   }
   *out = it->second;
@@ -135,11 +141,11 @@ int mi355_softbuffer_pool_create(mi355_softbuffer_pool_t** p, uint32_t nof_sb, u
   s->nof_sb       = nof_sb;
   s->max_cb       = max_cb;
   if (hipMalloc(&s->buf, nc * SB_STRIDE * 2) != hipSuccess || hipMalloc(&s->cb_crc, nc) != hipSuccess ||
-      hipMalloc(&s->data, nc * SB_DATA) != hipSuccess) {
+      hipMalloc(&s->data, nc * SB_DATA) != hipSuccess || hipMalloc(&s->fresh, nc) != hipSuccess) {
     mi355_softbuffer_pool_destroy(s);
     return MI355_ERROR;
   }
-  (void)hipMemset(s->buf, 0, nc * SB_STRIDE * 2);
+  (void)hipMemset(s->fresh, 1, nc); // every buffer starts logically zero
   (void)hipMemset(s->cb_crc, 0, nc);
   (void)hipMemset(s->data, 0, nc * SB_DATA);
   (void)hipDeviceSynchronize();
@@ -153,6 +159,7 @@ void mi355_softbuffer_pool_destroy(mi355_softbuffer_pool_t* p)
   (void)hipFree(p->buf);
   (void)hipFree(p->cb_crc);
   (void)hipFree(p->data);
+  (void)hipFree(p->fresh);
   delete p;
 }
 
@@ -164,7 +171,7 @@ int mi355_softbuffer_reset_cb(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t 
   hipStream_t    s  = (hipStream_t)stream;
   const uint32_t nc = std::min(nof_cb, p->max_cb);
   if (nc) {
-    DlschResetArgs a{p->buf, SB_STRIDE, p->cb_crc, p->data, (size_t)sb * p->max_cb, nc};
+    DlschResetArgs a{p->fresh, p->cb_crc, (size_t)sb * p->max_cb, nc};
     CHECK_HIP(dlsch_launch_reset(a, s));
   }
   CHECK_HIP(hipMemsetAsync(p->cb_crc + (size_t)sb * p->max_cb, 0, p->max_cb, s));
@@ -196,7 +203,7 @@ int mi355_softbuffer_reset_range(mi355_softbuffer_pool_t* p, uint32_t first, uin
   if (!p || first + n > p->nof_sb) return MI355_ERROR_INVALID_INPUTS;
   if (!n) return MI355_SUCCESS;
   CHECK_HIP(hipSetDevice(p->device));
-  DlschResetArgs a{p->buf, SB_STRIDE, p->cb_crc, p->data, (size_t)first * p->max_cb, (size_t)n * p->max_cb};
+  DlschResetArgs a{p->fresh, p->cb_crc, (size_t)first * p->max_cb, (size_t)n * p->max_cb};
   CHECK_HIP(dlsch_launch_reset(a, (hipStream_t)stream));
   return MI355_SUCCESS;
 }
@@ -337,7 +344,7 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   }
   auto rnd = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t need = rnd(ntb * sizeof(TbDesc)) + rnd(total_cb * sizeof(CbDesc)) + rnd(total_cb * 4) +
-                      rnd(total_cb) + rnd(total_cb * 4) + rnd(dec_bytes) + rnd(ntb * 4);
+                      rnd(total_cb) + rnd(total_cb * 4) + rnd(dec_bytes) + rnd(ntb * 4) + rnd(4);
   char* base = nullptr;
   int   r    = scratch(q, need, &base);
   if (r) return r;
@@ -354,6 +361,7 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   auto*     d_its   = (uint32_t*)carve(total_cb * 4);
   auto*     d_dec   = (uint8_t*)carve(dec_bytes);
   auto*     d_ret   = (int32_t*)carve(ntb * 4);
+  auto*     d_rem   = (uint32_t*)carve(4);
 
   std::vector<CbDesc>   all_cb;
   std::vector<uint32_t> all_slot;
@@ -385,13 +393,15 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
     DlschRmArgs    ra{};
     ra.desc = d_cb + off;
     ra.ncb  = (int)n;
-    ra.N    = 3 * K + 12;
+    ra.N      = 3 * K + 12;
+    ra.buflen = rm_buflen(K);
     for (uint32_t rv = 0; rv < 4; rv++) {
       bool used = false;
       for (auto& c : kv.second.cbs) used |= c.rv == rv;
-      ra.table[rv] = nullptr;
-      if (used && (r = rm_table(q, K, rv, &ra.table[rv]))) return r;
+      ra.inv[rv] = nullptr;
+      if (used && (r = rm_table(q, K, rv, &ra.inv[rv]))) return r;
     }
+    ra.fresh     = pool->fresh;
     ra.e         = d_e_bits;
     ra.sb        = pool->buf;
     ra.sb_stride = SB_STRIDE;
@@ -410,14 +420,15 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   }
   // CBs already decoded in an earlier transmission start as done (before the rate matcher adds into them
   // this is the same flag it tested)
-  if (total_cb) CHECK_HIP(dlsch_launch_init_done(d_done, d_slot, pool->cb_crc, (int)total_cb, s));
+  CHECK_HIP(hipMemsetAsync(d_rem, 0, 4, s));
+  if (total_cb) CHECK_HIP(dlsch_launch_init_done(d_done, d_slot, pool->cb_crc, (int)total_cb, d_rem, s));
 
   for (uint32_t h = 0; h < q->max_its; h++) {
     for (auto& lv : live) {
-      TdecRun rq{pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, lv.n, lv.K, h, h + 1, lv.dec, lv.K / 8, s};
+      TdecRun rq{pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, d_rem, lv.n, lv.K, h, h + 1, lv.dec, lv.K / 8, s};
       if ((r = mi355_tdec_run_internal(lv.td, rq))) return r;
       DlschCheckArgs ca{d_cb + lv.off, (int)lv.n, lv.K, h, q->max_its, lv.dec, lv.K / 8, d_data,
-                        d_done + lv.off, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1]};
+                        d_done + lv.off, d_rem, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1]};
       CHECK_HIP(dlsch_launch_check(ca, s));
     }
   }

@@ -28,6 +28,7 @@ struct PdschCwDev {
   const float*  csi;
   const uint32_t* cmax;
   int16_t*      e;
+  const uint32_t* scr; // packed descrambling sequence of c_init (cached per c_init)
   uint32_t      nof_re, nof_bits, qm, c_init, csi_enable;
   uint32_t      pairs; // kernel B work items: symbol pairs
 };
@@ -38,7 +39,8 @@ struct PdschBlk {
 };
 
 hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, const PdschBlk* blk, uint32_t nblk, hipStream_t s);
-hipError_t pdsch_launch_llr(const PdschCwDev* cws, const PdschBlk* blk, uint32_t nblk, const uint32_t* gold,
-                            hipStream_t s);
+hipError_t pdsch_launch_scr_pack(const uint32_t* c_init, uint32_t* const* dst, uint32_t n, const uint32_t* gold,
+                                 uint32_t W, hipStream_t s);
+hipError_t pdsch_launch_llr(const PdschCwDev* cws, const PdschBlk* blk, uint32_t nblk, hipStream_t s);
 
 } // namespace mi355

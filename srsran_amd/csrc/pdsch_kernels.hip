@@ -249,7 +249,7 @@ __device__ __forceinline__ int16_t abs16(int16_t v) { return (int16_t)(v < 0 ? (
 __device__ __forceinline__ int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }
 
 // LLRs of symbol s (of n) for modulation order qm, as srslte_demod_soft_demodulate_s (AVX2 build)
-__device__ __forceinline__ void demod_symbol(uint32_t qm, cf x, uint32_t s, uint32_t n, int16_t* o)
+__device__ __forceinline__ void demod_symbol(const uint32_t qm, cf x, uint32_t s, uint32_t n, int16_t* o)
 {
   switch (qm) {
     case 1: {
@@ -330,50 +330,94 @@ __device__ __forceinline__ int16_t mulhi16(int16_t a, int16_t b) { return (int16
 
 } // namespace
 
-__global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ cws, const PdschBlk* __restrict__ blk,
-                                                 const uint32_t* __restrict__ gold)
+// Packed descrambling sequences for new c_init values (the UE's pregenerated per-RNTI sequences,
+// pdsch.c:516-559): word w of job j = gold[31][w] ^ XOR of gold[i][w] over the set bits i of c_init, from the
+// bit-plane table gold[i][w] (bit k of the word = coefficient of c_init bit i in x2(32w + k + Nc); plane 31
+// holds the x1 bits).  Plane-major, so the reads of a wave are coalesced.
+__global__ __launch_bounds__(256) void pdsch_scr_pack(const uint32_t* __restrict__ c_init, uint32_t* const* __restrict__ dst,
+                                                      const uint32_t* __restrict__ gold, uint32_t W)
 {
-  const PdschBlk    bk = blk[blockIdx.x];
-  const PdschCwDev& C  = cws[bk.job];
-  const uint32_t    pr = bk.unit + threadIdx.x;
-  if (pr >= C.pairs) return;
-  const uint32_t qm = C.qm, n = C.nof_re;
-  const uint32_t s0 = 2 * pr, ns = min(2u, n - s0);
-  int16_t        o[16];
-  float          csi[2] = {0.f, 0.f};
-  for (uint32_t k = 0; k < ns; k++) {
-    demod_symbol(qm, ld(C.d, s0 + k), s0 + k, n, &o[k * qm]);
-    if (C.csi_enable) csi[k] = C.csi[s0 + k];
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= W) return;
+  const uint32_t ci = c_init[blockIdx.y];
+  uint32_t       v  = gold[31 * (size_t)W + w];
+  uint32_t       m  = ci & 0x7fffffffu;
+  while (m) {
+    const int i = __ffs(m) - 1;
+    v ^= gold[(size_t)i * W + w];
+    m &= m - 1;
   }
-  // descrambling: c(k) = x1(k+Nc) ^ <mask(k+Nc), c_init> (srslte_scrambling_s_offset, scrambling.c:43-47)
-  const uint32_t b0 = s0 * qm, nb = ns * qm;
-  for (uint32_t k = 0; k < nb; k++) {
-    const uint32_t g = gold[b0 + k];
-    const uint32_t c = (g >> 31) ^ (__popc(g & C.c_init & 0x7fffffffu) & 1u);
-    if (c) o[k] = (int16_t)(uint16_t)(-(int32_t)o[k]);
-  }
-  if (C.csi_enable) { // csi_correction (pdsch.c:628-741), SSE path
-    const uint32_t nsym   = C.nof_bits / qm;
-    const float    cmax   = nsym ? __uint_as_float(*C.cmax) : 1.0f;
-    const float    scale  = 32767.0f / cmax;
-    const bool     pair   = ns == 2;
-    auto           CV     = [&](float v) { return sat16(x86_cvt_i32(rintf(v * scale))); }; // _mm_cvtps_pi16
-    bool           body;
-    switch (qm) {
-      case 2: body = pair; break;
-      case 4: body = true; break;
-      case 6: body = pair; break;
-      case 8: body = true; break;
-      default: body = false; break;
+  dst[blockIdx.y][w] = v;
+}
+
+template <int QM> __device__ __forceinline__ void store_llrs(int16_t* e, const int16_t (&o)[2 * QM], uint32_t nb)
+{
+  if (nb == 2 * QM) {
+    if constexpr ((2 * QM) % 8 == 0) { // 16-byte aligned groups (QM = 4, 8)
+#pragma unroll
+      for (int k = 0; k < 2 * QM; k += 8) {
+        uint4 v;
+        v.x = (uint16_t)o[k] | ((uint32_t)(uint16_t)o[k + 1] << 16);
+        v.y = (uint16_t)o[k + 2] | ((uint32_t)(uint16_t)o[k + 3] << 16);
+        v.z = (uint16_t)o[k + 4] | ((uint32_t)(uint16_t)o[k + 5] << 16);
+        v.w = (uint16_t)o[k + 6] | ((uint32_t)(uint16_t)o[k + 7] << 16);
+        *(uint4*)(e + k) = v;
+      }
+      return;
+    } else if constexpr ((2 * QM) % 4 == 0) { // 8-byte aligned groups (QM = 2, 6)
+#pragma unroll
+      for (int k = 0; k < 2 * QM; k += 4) {
+        uint2 v;
+        v.x = (uint16_t)o[k] | ((uint32_t)(uint16_t)o[k + 1] << 16);
+        v.y = (uint16_t)o[k + 2] | ((uint32_t)(uint16_t)o[k + 3] << 16);
+        *(uint2*)(e + k) = v;
+      }
+      return;
     }
+  }
+#pragma unroll
+  for (int k = 0; k < 2 * QM; k++)
+    if ((uint32_t)k < nb) e[k] = o[k];
+}
+
+template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, uint32_t pr)
+{
+  const uint32_t n  = C.nof_re;
+  const uint32_t s0 = 2 * pr, ns = min(2u, n - s0);
+  int16_t        o[2 * QM];
+  float          csi[2] = {0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if ((uint32_t)k < ns) {
+      demod_symbol(QM, ld(C.d, s0 + k), s0 + k, n, &o[k * QM]);
+      if (C.csi_enable) csi[k] = C.csi[s0 + k];
+    } else {
+#pragma unroll
+      for (int b = 0; b < QM; b++) o[k * QM + b] = 0;
+    }
+  }
+  // descrambling e = c ? -e : e (srslte_scrambling_s_offset, scrambling.c:43-47) with the packed sequence
+  const uint32_t b0 = s0 * QM, nb = ns * QM;
+  const uint32_t w0 = b0 >> 5, sh = b0 & 31;
+  const uint64_t bits = (uint64_t)C.scr[w0] | ((sh + 2 * QM > 32 && (b0 + 2 * QM - 1) / 32 < (C.nof_bits + 31) / 32)
+                                                  ? (uint64_t)C.scr[w0 + 1] << 32 : 0ull);
+#pragma unroll
+  for (int k = 0; k < 2 * QM; k++)
+    if ((bits >> (sh + k)) & 1ull) o[k] = (int16_t)(uint16_t)(-(int32_t)o[k]);
+  if (C.csi_enable) { // csi_correction (pdsch.c:628-741), SSE path
+    const uint32_t nsym  = C.nof_bits / QM;
+    const float    cmax  = nsym ? __uint_as_float(*C.cmax) : 1.0f;
+    const float    scale = 32767.0f / cmax;
+    auto           CV    = [&](float v) { return sat16(x86_cvt_i32(rintf(v * scale))); }; // _mm_cvtps_pi16
+    const bool     body  = (QM == 4 || QM == 8) || ((QM == 2 || QM == 6) && ns == 2);
     if (body) {
-      if (qm == 2) { // _mm_blend_ps(csi1, csi2, 3): the pair's LLR lanes 0,1 take the second symbol's CSI
+      if constexpr (QM == 2) { // _mm_blend_ps(csi1, csi2, 3): the pair's LLR lanes 0,1 take the 2nd symbol's CSI
         const int16_t c0 = CV(csi[0]), c1 = CV(csi[1]);
         o[0] = mulhi16(o[0], c1);
         o[1] = mulhi16(o[1], c1);
         o[2] = mulhi16(o[2], c0);
         o[3] = mulhi16(o[3], c0);
-      } else if (qm == 6) {
+      } else if constexpr (QM == 6) {
         const int16_t c1 = CV(csi[0]), c3 = CV(csi[1]);
 #pragma unroll
         for (int k = 0; k < 4; k++) o[k] = mulhi16(o[k], c1);
@@ -384,20 +428,38 @@ __global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ 
 #pragma unroll
         for (int k = 8; k < 12; k++) o[k] = mulhi16(o[k], c3);
       } else {
-        for (uint32_t k = 0; k < ns; k++) {
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
           const int16_t c = CV(csi[k]);
-          for (uint32_t b = 0; b < qm; b++) o[k * qm + b] = mulhi16(o[k * qm + b], c);
+#pragma unroll
+          for (int b = 0; b < QM; b++) o[k * QM + b] = mulhi16(o[k * QM + b], c);
         }
       }
     } else {
-      for (uint32_t k = 0; k < ns; k++) {
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
         const float c = csi[k] / cmax;
-        for (uint32_t b = 0; b < qm; b++) o[k * qm + b] = f2s_trunc((float)o[k * qm + b] * c);
+#pragma unroll
+        for (int b = 0; b < QM; b++) o[k * QM + b] = f2s_trunc((float)o[k * QM + b] * c);
       }
     }
   }
-  int16_t* e = C.e + b0;
-  for (uint32_t k = 0; k < nb; k++) e[k] = o[k];
+  store_llrs<QM>(C.e + b0, o, nb);
+}
+
+__global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ cws, const PdschBlk* __restrict__ blk)
+{
+  const PdschBlk    bk = blk[blockIdx.x];
+  const PdschCwDev& C  = cws[bk.job];
+  const uint32_t    pr = bk.unit + threadIdx.x;
+  if (pr >= C.pairs) return;
+  switch (C.qm) {
+    case 1: llr_pair<1>(C, pr); break;
+    case 2: llr_pair<2>(C, pr); break;
+    case 4: llr_pair<4>(C, pr); break;
+    case 6: llr_pair<6>(C, pr); break;
+    default: llr_pair<8>(C, pr); break;
+  }
 }
 
 hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, const PdschBlk* blk, uint32_t nblk, hipStream_t s)
@@ -407,11 +469,18 @@ hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, const PdschBlk* blk, u
   return hipGetLastError();
 }
 
-hipError_t pdsch_launch_llr(const PdschCwDev* cws, const PdschBlk* blk, uint32_t nblk, const uint32_t* gold,
-                            hipStream_t s)
+hipError_t pdsch_launch_scr_pack(const uint32_t* c_init, uint32_t* const* dst, uint32_t n, const uint32_t* gold,
+                                 uint32_t W, hipStream_t s)
+{
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(pdsch_scr_pack, dim3((W + 255) / 256, n), dim3(256), 0, s, c_init, dst, gold, W);
+  return hipGetLastError();
+}
+
+hipError_t pdsch_launch_llr(const PdschCwDev* cws, const PdschBlk* blk, uint32_t nblk, hipStream_t s)
 {
   if (!nblk) return hipSuccess;
-  hipLaunchKernelGGL(pdsch_llr, dim3(nblk), dim3(256), 0, s, cws, blk, gold);
+  hipLaunchKernelGGL(pdsch_llr, dim3(nblk), dim3(256), 0, s, cws, blk);
   return hipGetLastError();
 }
 

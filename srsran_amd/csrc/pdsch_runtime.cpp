@@ -111,16 +111,22 @@ template <class Emit> uint32_t walk_map(const mi355_cell_t& c, const mi355_pdsch
   return k;
 }
 
-// Gold sequence table (36.211 7.2, Nc = 1600): for sequence position k, bit 31 = x1(k + Nc) (x1 does not
-// depend on c_init) and bits 0..30 the GF(2) linear form of x2(k + Nc) over the bits of c_init, so
-// c(k) = bit31 ^ parity(mask & c_init).
+// Gold sequence table (36.211 7.2, Nc = 1600) in bit planes: x2(k + Nc) is a GF(2) linear form of the 31
+// bits of c_init (x1 does not depend on c_init), so for the 32 positions of word w, t[w][i] (i < 31) holds
+// bit j = coefficient of c_init bit i in x2(32w + j + Nc) and t[w][31] the x1 bits; the packed sequence word
+// is t[w][31] ^ XOR of t[w][i] over the set bits i of c_init.
 std::vector<uint32_t> gold_table(uint32_t len)
 {
-  std::vector<uint32_t> t(len);
+  const size_t          W = (len + 31) / 32;
+  std::vector<uint32_t> t(W * 32, 0u); // plane-major: t[i * W + w]
   uint32_t              x1 = 1, m[31];
   for (int i = 0; i < 31; i++) m[i] = 1u << i;
   for (uint32_t n = 0; n < 1600 + len; n++) {
-    if (n >= 1600) t[n - 1600] = ((x1 & 1u) << 31) | m[0];
+    if (n >= 1600) {
+      const uint32_t k = n - 1600, w = k / 32, j = k % 32;
+      for (int i = 0; i < 31; i++) t[(size_t)i * W + w] |= ((m[0] >> i) & 1u) << j;
+      t[31 * W + w] |= (x1 & 1u) << j;
+    }
     const uint32_t f1 = ((x1 >> 3) ^ x1) & 1u;
     const uint32_t f2 = m[3] ^ m[2] ^ m[1] ^ m[0];
     x1                = (x1 >> 1) | (f1 << 30);
@@ -160,6 +166,7 @@ struct mi355_pdsch {
   uint32_t                             max_its = 10; // SRSLTE_PDSCH_MAX_TDEC_ITERS
   uint32_t*                            gold   = nullptr;
   std::map<std::string, std::pair<uint16_t*, uint32_t>> maps; // extraction maps in HBM + RE count
+  std::map<uint32_t, uint32_t*>        scr;  // packed descrambling sequences per c_init (HBM)
   char*                                scratch = nullptr;
   size_t                               scratch_cap = 0;
   std::vector<JobPlan>                 last; // plans of the last call (debug_stage)
@@ -301,6 +308,13 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   size_t         nd = 0, ne = 0;
   std::vector<PdschCwDev> cws;
   std::vector<PdschBlk>   blkA, blkB;
+  std::vector<uint32_t>   new_ci;
+  std::vector<uint32_t*>  new_dst;
+  if (q->scr.size() > 4096) { // bound the sequence cache (~76 MB)
+    CHECK_HIP(hipStreamSynchronize(s));
+    for (auto& kv : q->scr) (void)hipFree(kv.second);
+    q->scr.clear();
+  }
   for (uint32_t i = 0; i < njobs; i++) {
     JobPlan& P = plans[i];
     for (uint32_t cw = 0; cw < 2; cw++) {
@@ -332,13 +346,22 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
       c.pairs      = (c.nof_re + 1) / 2;
       const uint32_t ci = (uint32_t)cws.size();
       for (uint32_t u = 0; u < c.pairs; u += 256) blkB.push_back(PdschBlk{ci, u});
+      auto it = q->scr.find(c.c_init);
+      if (it == q->scr.end()) {
+        uint32_t* d = nullptr;
+        CHECK_HIP(hipMalloc(&d, (PDSCH_GOLD_MAX / 32) * 4));
+        it = q->scr.emplace(c.c_init, d).first;
+        new_ci.push_back(c.c_init);
+        new_dst.push_back(d);
+      }
+      c.scr = it->second;
       cws.push_back(c);
     }
   }
   auto         rnd  = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t need = rnd(njobs * sizeof(PdschJobDev)) + rnd(cws.size() * sizeof(PdschCwDev)) +
                       rnd(blkA.size() * sizeof(PdschBlk)) + rnd(blkB.size() * sizeof(PdschBlk)) + rnd(njobs * 8) +
-                      rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2);
+                      rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2) + rnd(new_ci.size() * 12);
   char* base = nullptr;
   int   r    = get_scratch(q, need, &base);
   if (r) return r;
@@ -352,6 +375,8 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   auto* d_cws  = (PdschCwDev*)carve(cws.size() * sizeof(PdschCwDev));
   auto* d_blkA = (PdschBlk*)carve(blkA.size() * sizeof(PdschBlk));
   auto* d_blkB = (PdschBlk*)carve(blkB.size() * sizeof(PdschBlk));
+  auto* d_nci  = (uint32_t*)carve(new_ci.size() * 4);
+  auto* d_ndst = (uint32_t**)carve(new_ci.size() * 8);
   auto* d_cmax = (uint32_t*)carve(njobs * 8);
   q->d_arena   = (float2*)carve(nd * 8);
   q->csi_arena = (float*)carve(nd * 4);
@@ -382,9 +407,14 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   if (!cws.empty()) CHECK_HIP(hipMemcpyAsync(d_cws, cws.data(), cws.size() * sizeof(PdschCwDev), hipMemcpyHostToDevice, s));
   if (!blkA.empty()) CHECK_HIP(hipMemcpyAsync(d_blkA, blkA.data(), blkA.size() * sizeof(PdschBlk), hipMemcpyHostToDevice, s));
   if (!blkB.empty()) CHECK_HIP(hipMemcpyAsync(d_blkB, blkB.data(), blkB.size() * sizeof(PdschBlk), hipMemcpyHostToDevice, s));
+  if (!new_ci.empty()) {
+    CHECK_HIP(hipMemcpyAsync(d_nci, new_ci.data(), new_ci.size() * 4, hipMemcpyHostToDevice, s));
+    CHECK_HIP(hipMemcpyAsync(d_ndst, new_dst.data(), new_dst.size() * 8, hipMemcpyHostToDevice, s));
+  }
   CHECK_HIP(hipMemsetAsync(d_cmax, 0, njobs * 8, s));
   CHECK_HIP(pdsch_launch_equalize(d_jobs, d_blkA, (uint32_t)blkA.size(), s));
-  CHECK_HIP(pdsch_launch_llr(d_cws, d_blkB, (uint32_t)blkB.size(), q->gold, s));
+  CHECK_HIP(pdsch_launch_scr_pack(d_nci, d_ndst, (uint32_t)new_ci.size(), q->gold, PDSCH_GOLD_MAX / 32, s));
+  CHECK_HIP(pdsch_launch_llr(d_cws, d_blkB, (uint32_t)blkB.size(), s));
   return MI355_SUCCESS;
 }
 
@@ -427,6 +457,7 @@ void mi355_pdsch_destroy(mi355_pdsch_t* q)
   (void)hipSetDevice(q->device);
   (void)hipDeviceSynchronize();
   for (auto& kv : q->maps) (void)hipFree(kv.second.first);
+  for (auto& kv : q->scr) (void)hipFree(kv.second);
   (void)hipFree(q->gold);
   (void)hipFree(q->scratch);
   mi355_dlsch_destroy(q->dlsch);

@@ -17,6 +17,7 @@ struct TdecWinArgs {
   size_t          in_stride;
   const uint32_t* in_idx; // optional: buffer index of batch code block b (default b)
   const uint8_t*  done;   // optional: code blocks already decoded (CRC early stop) are skipped
+  const uint32_t* remaining; // optional: number of unfinished code blocks; 0 -> the launch is a no-op
   uint32_t*       A1;   // a-priori of DEC1 (natural order), wave-group interleaved
   uint32_t*       E;    // DEC1 extrinsic -> DEC2 input (interleaved order), wave-group interleaved
   uint32_t*       D;    // decision LLRs (natural order), wave-group interleaved
@@ -31,6 +32,8 @@ struct TdecDecideArgs {
   uint8_t*        out;
   size_t          out_stride;
   int             ncb, L, Lp;
+  const uint8_t*  done; // nullable: code blocks already finished (CRC early stop) are skipped
+  const uint32_t* remaining; // nullable
 };
 
 // generic (single-window, wrapping) decoder for K <= 400: two code blocks per lane
@@ -67,6 +70,7 @@ struct TdecRun {
   size_t          in_stride;
   const uint32_t* in_idx; // nullable
   const uint8_t*  done;   // nullable
+  const uint32_t* remaining; // nullable: unfinished code blocks (all launches no-ops at 0)
   uint32_t        n, K, h0, h1;
   uint8_t*        out;
   size_t          out_stride;

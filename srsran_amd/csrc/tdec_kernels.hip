@@ -138,6 +138,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
   const int     grp = gl >> 6, q = gl & 63;
   const int     cbg = q / NL, l = q % NL;
   if (grp * G + cbg >= a.ncb) return;
+  if (a.remaining && *a.remaining == 0) return;  // every code block of the batch has finished
   if (a.done && a.done[grp * G + cbg]) return; // CRC early stop: this code block is finished
 
   const int  L = a.L, Lp = a.Lp, nseg = a.nseg;
@@ -454,7 +455,7 @@ __global__ __launch_bounds__(256) void tdec_win_decide_rows(TdecDecideArgs a)
   const int     grp = (int)(r / nb), jb = (int)(r % nb);
   const int     cbg = q / NL, l = q % NL;
   const size_t  cb  = (size_t)grp * G + cbg;
-  if (cb >= (size_t)a.ncb) return;
+  if (cb >= (size_t)a.ncb || (a.remaining && *a.remaining == 0) || (a.done && a.done[cb])) return;
   const uint32_t* D  = a.D + ((size_t)grp * a.Lp + 8 * jb) * 64 + q;
   uint32_t        lo = 0, hi = 0;
 #pragma unroll
@@ -478,7 +479,7 @@ __global__ __launch_bounds__(256) void tdec_win_decide(TdecDecideArgs a)
   const int     K    = a.L * NSB;
   const int     nbyt = K / 8;
   const size_t  cb   = g / nbyt;
-  if (cb >= (size_t)a.ncb) return;
+  if (cb >= (size_t)a.ncb || (a.remaining && *a.remaining == 0) || (a.done && a.done[cb])) return;
   const int      b   = (int)(g % nbyt);
   const int      grp = (int)(cb / G), cbg = (int)(cb % G);
   const int16_t* D16 = (const int16_t*)a.D + (size_t)grp * a.Lp * 128 + cbg * NL * 2;

@@ -277,7 +277,7 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
     auto*        CK  = (uint32_t*)carve((size_t)g.ngrp * g.nseg * 8 * 64 * 4);
 
     for (uint32_t h = h0; h < h1; h++) {
-      TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, A1, E, D, CK, t->dstE, t->dstA,
+      TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, rq.remaining, A1, E, D, CK, t->dstE, t->dstA,
                      (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == h1};
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (q->prof) {
@@ -288,7 +288,7 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
       CHECK_HIP(tdec_win_launch_halfit(g.nsb, wa, s));
       if (q->prof && e1) (void)hipEventRecord(e1, s);
     }
-    TdecDecideArgs da{D, d_out, out_stride, (int)n, (int)g.L, (int)g.Lp};
+    TdecDecideArgs da{D, d_out, out_stride, (int)n, (int)g.L, (int)g.Lp, rq.done, rq.remaining};
     CHECK_HIP(tdec_win_launch_decide(g.nsb, da, s));
   } else {
     const size_t arr = (size_t)g.npair * g.Kp * 4;
@@ -336,7 +336,7 @@ int mi355_tdec_batch_run_dev(mi355_tdec_batch_t* q,
 {
   if (nhalf == 0) return MI355_ERROR_INVALID_INPUTS;
   return mi355_tdec_run_internal(
-      q, TdecRun{d_in, in_stride, nullptr, nullptr, n, K, 0, nhalf, d_out, out_stride, (hipStream_t)stream});
+      q, TdecRun{d_in, in_stride, nullptr, nullptr, nullptr, n, K, 0, nhalf, d_out, out_stride, (hipStream_t)stream});
 }
 
 int mi355_tdec_batch_halfit_dev(mi355_tdec_batch_t* q,
@@ -349,7 +349,7 @@ int mi355_tdec_batch_halfit_dev(mi355_tdec_batch_t* q,
                                 size_t              out_stride,
                                 void*               stream)
 {
-  return mi355_tdec_run_internal(q, TdecRun{d_in, in_stride, nullptr, nullptr, n, K, half_idx, half_idx + 1, d_out,
+  return mi355_tdec_run_internal(q, TdecRun{d_in, in_stride, nullptr, nullptr, nullptr, n, K, half_idx, half_idx + 1, d_out,
                                             out_stride, (hipStream_t)stream});
 }
 
