@@ -52,7 +52,8 @@ struct DlschCheckArgs {
   size_t         dec_stride;
   uint8_t*       data;
   uint8_t*       done;
-  uint32_t*      remaining; // unfinished code blocks of the call
+  const uint32_t* remaining; // running flag of this half-iteration (0: every code block finished)
+  uint32_t*      next;      // running flag of the next half-iteration
   uint32_t*      its;
   uint8_t*        sb_crc;
   const CrcTable* crc24a;

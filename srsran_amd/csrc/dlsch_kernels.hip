@@ -116,30 +116,47 @@ __device__ uint32_t block_crc24(const uint8_t* bytes, uint32_t nbytes, const Crc
 // (C==1); CRC ok => the CB is finished at this iteration.  Decision bytes of CB i land at i*rlen/8 of the
 // TB payload; only the last CB keeps its trailing CRC bytes (the earlier ones are overwritten by the
 // next CB in the reference's sequential loop, sch.c:422-424).
-__global__ __launch_bounds__(256) void dlsch_cb_check(DlschCheckArgs a)
+// "work remains" flags instead of a counter: running[h] != 0 iff some code block is unfinished before
+// half-iteration h.  Writers aggregate per workgroup and only store when the flag still reads 0 (L2-coherent
+// load), so the flag line is not hammered by thousands of stores.
+__device__ __forceinline__ void flag_set(uint32_t* f)
 {
+  if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(1024) void dlsch_cb_check(DlschCheckArgs a)
+{
+  __shared__ uint32_t unfinished;
+  if (threadIdx.x == 0) unfinished = 0;
+  __syncthreads();
   const int b    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  if (b >= a.ncb || *a.remaining == 0 || a.done[b]) return;
-  const CbDesc&  d   = a.desc[b];
-  const uint8_t* dec = a.dec + (size_t)b * a.dec_stride;
-  const uint32_t crc = wave_crc24(dec, a.K / 8, d.C > 1 ? *a.crc24b : *a.crc24a);
-  const bool     ok  = crc == 0;
-  const bool     fin = ok || a.h + 1 == a.max_its;
-  if (!fin) return;
-  uint8_t*       dst = a.data + d.data_off + (size_t)d.cb * d.rlen / 8;
-  const uint32_t nb  = (d.cb + 1 == d.C) ? a.K / 8 : d.rlen / 8;
-  for (uint32_t i = lane; i < nb; i += 64) dst[i] = dec[i];
-  if (lane == 0) {
-    a.its[b] = a.h + 1;
-    atomicSub(a.remaining, 1u);
-    if (ok) {
-      a.done[b]         = 1;
-      a.sb_crc[d.slot]  = 1;
+  if (b < a.ncb && *a.remaining != 0 && !a.done[b]) {
+    const CbDesc&  d   = a.desc[b];
+    const uint8_t* dec = a.dec + (size_t)b * a.dec_stride;
+    const uint32_t crc = wave_crc24(dec, a.K / 8, d.C > 1 ? *a.crc24b : *a.crc24a);
+    const bool     ok  = crc == 0;
+    const bool     fin = ok || a.h + 1 == a.max_its;
+    if (!fin) {
+      if (lane == 0) unfinished = 1;
     } else {
-      a.done[b] = 2; // gave up: CRC error after max_iterations
+      uint8_t*       dst = a.data + d.data_off + (size_t)d.cb * d.rlen / 8;
+      const uint32_t nb  = (d.cb + 1 == d.C) ? a.K / 8 : d.rlen / 8;
+      for (uint32_t i = lane; i < nb; i += 64) dst[i] = dec[i];
+      if (lane == 0) {
+        a.its[b] = a.h + 1;
+        if (ok) {
+          a.done[b]        = 1;
+          a.sb_crc[d.slot] = 1;
+        } else {
+          a.done[b] = 2; // gave up: CRC error after max_iterations
+        }
+      }
     }
   }
+  __syncthreads();
+  if (threadIdx.x == 0 && unfinished) flag_set(a.next);
 }
 
 // ---------------------------------------------------------------------------- TB prologue / epilogue
@@ -212,13 +229,17 @@ __global__ __launch_bounds__(256) void dlsch_sb_reset(DlschResetArgs a)
 
 // CBs whose CRC passed in an earlier transmission start finished (sch.c:385)
 __global__ __launch_bounds__(256) void dlsch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc,
-                                                        int n, uint32_t* remaining)
+                                                        int n, uint32_t* running)
 {
+  __shared__ uint32_t any;
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
   const int  b    = blockIdx.x * blockDim.x + threadIdx.x;
   const bool todo = b < n && !sb_crc[slot[b]];
   if (b < n) done[b] = todo ? 0 : 3;
-  const uint64_t m = __ballot(todo);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(remaining, (uint32_t)__popcll(m));
+  if (todo) any = 1;
+  __syncthreads();
+  if (threadIdx.x == 0 && any) flag_set(running);
 }
 
 hipError_t dlsch_launch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc, int n, uint32_t* remaining,
@@ -242,7 +263,7 @@ hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s)
 
 hipError_t dlsch_launch_check(const DlschCheckArgs& a, hipStream_t s)
 {
-  hipLaunchKernelGGL(dlsch_cb_check, dim3((unsigned)((a.ncb + 3) / 4)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(dlsch_cb_check, dim3((unsigned)((a.ncb + 15) / 16)), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 

@@ -344,7 +344,7 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   }
   auto rnd = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t need = rnd(ntb * sizeof(TbDesc)) + rnd(total_cb * sizeof(CbDesc)) + rnd(total_cb * 4) +
-                      rnd(total_cb) + rnd(total_cb * 4) + rnd(dec_bytes) + rnd(ntb * 4) + rnd(4);
+                      rnd(total_cb) + rnd(total_cb * 4) + rnd(dec_bytes) + rnd(ntb * 4) + rnd(4 * (q->max_its + 1));
   char* base = nullptr;
   int   r    = scratch(q, need, &base);
   if (r) return r;
@@ -361,7 +361,7 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   auto*     d_its   = (uint32_t*)carve(total_cb * 4);
   auto*     d_dec   = (uint8_t*)carve(dec_bytes);
   auto*     d_ret   = (int32_t*)carve(ntb * 4);
-  auto*     d_rem   = (uint32_t*)carve(4);
+  auto*     d_run   = (uint32_t*)carve(4 * (q->max_its + 1)); // running flags per half-iteration
 
   std::vector<CbDesc>   all_cb;
   std::vector<uint32_t> all_slot;
@@ -420,15 +420,15 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   }
   // CBs already decoded in an earlier transmission start as done (before the rate matcher adds into them
   // this is the same flag it tested)
-  CHECK_HIP(hipMemsetAsync(d_rem, 0, 4, s));
-  if (total_cb) CHECK_HIP(dlsch_launch_init_done(d_done, d_slot, pool->cb_crc, (int)total_cb, d_rem, s));
+  CHECK_HIP(hipMemsetAsync(d_run, 0, 4 * (q->max_its + 1), s));
+  if (total_cb) CHECK_HIP(dlsch_launch_init_done(d_done, d_slot, pool->cb_crc, (int)total_cb, d_run, s));
 
   for (uint32_t h = 0; h < q->max_its; h++) {
     for (auto& lv : live) {
-      TdecRun rq{pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, d_rem, lv.n, lv.K, h, h + 1, lv.dec, lv.K / 8, s};
+      TdecRun rq{pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, d_run + h, lv.n, lv.K, h, h + 1, lv.dec, lv.K / 8, s};
       if ((r = mi355_tdec_run_internal(lv.td, rq))) return r;
       DlschCheckArgs ca{d_cb + lv.off, (int)lv.n, lv.K, h, q->max_its, lv.dec, lv.K / 8, d_data,
-                        d_done + lv.off, d_rem, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1]};
+                        d_done + lv.off, d_run + h, d_run + h + 1, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1]};
       CHECK_HIP(dlsch_launch_check(ca, s));
     }
   }

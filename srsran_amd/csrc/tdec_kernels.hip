@@ -310,7 +310,8 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
   int16_t*        D16  = (int16_t*)a.D + (size_t)grp * Lp * 128;
   const uint32_t* tab  = (dec2 ? a.dstA : a.dstE) + l;
   const int       lane0 = cbg * NL; // first lane of this code block inside the 64-lane row
-  const bool      wr_d = a.write_d;
+  const bool      wr_bits = !dec2 && a.dec != nullptr; // fused decision bytes (DEC1: ext1 in natural order)
+  const bool      wr_d    = a.write_d && !wr_bits;
 
   uint32_t cx[SEG], cy[SEG], ca[SEG] = {}, cd[SEG], cc[8];
   auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap, uint32_t* d, uint32_t* c) {
@@ -332,6 +333,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
     const int s0 = t * SEG;
     const int e  = (s0 + SEG < L) ? s0 + SEG : L;
     uint32_t  nx[SEG], ny[SEG], na[SEG] = {}, nd[SEG], nc[8];
+    uint32_t  bits = 0; // decision bits of the segment: window 2l in bits 8..15, 2l+1 in 0..7 (MSB first)
     if (t + 1 < nseg) load(t + 1, nx, ny, na, nd, nc);
 
     v2s xin[SEG];
@@ -412,6 +414,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
           E16[olo]     = ev.x;
           E16[ohi]     = ev.y;
           if (wr_d) WG_AT(a.D, j) = W(out);
+          bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
         } else {
           // a1 = app1 - ext1 (wrapping) of the next DEC1, turbodecoder_iter.h:108-110
           const v2s av = out - xin[i];
@@ -424,6 +427,11 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
         }
       }
     }
+    }
+    if (wr_bits) { // turbodecoder_win.h:973-993: bit = LLR > 0, natural order, MSB first
+      uint8_t* o = a.dec + (size_t)cb * a.dec_stride + (size_t)(2 * l) * (L / 8) + t;
+      o[0]       = (uint8_t)(bits >> 8);
+      o[L / 8]   = (uint8_t)bits;
     }
 #pragma unroll
     for (int i = 0; i < SEG; i++) {

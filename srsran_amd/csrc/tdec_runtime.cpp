@@ -276,9 +276,13 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
     auto*        D   = (uint32_t*)carve(arr);
     auto*        CK  = (uint32_t*)carve((size_t)g.ngrp * g.nseg * 8 * 64 * 4);
 
+    // the last half-iteration is DEC1 (even index): its decisions (ext1, natural order) are packed into bytes by
+    // the MAP kernel itself when the windows are byte aligned, which saves the D array and the decide pass
+    const bool fuse = (h1 - 1) % 2 == 0 && g.L % 8 == 0;
     for (uint32_t h = h0; h < h1; h++) {
       TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, rq.remaining, A1, E, D, CK, t->dstE, t->dstA,
-                     (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == h1};
+                     (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == h1,
+                     (fuse && h + 1 == h1) ? d_out : nullptr, out_stride};
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (q->prof) {
         e0 = next_event(q);
@@ -288,8 +292,10 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
       CHECK_HIP(tdec_win_launch_halfit(g.nsb, wa, s));
       if (q->prof && e1) (void)hipEventRecord(e1, s);
     }
-    TdecDecideArgs da{D, d_out, out_stride, (int)n, (int)g.L, (int)g.Lp, rq.done, rq.remaining};
-    CHECK_HIP(tdec_win_launch_decide(g.nsb, da, s));
+    if (!fuse) {
+      TdecDecideArgs da{D, d_out, out_stride, (int)n, (int)g.L, (int)g.Lp, rq.done, rq.remaining};
+      CHECK_HIP(tdec_win_launch_decide(g.nsb, da, s));
+    }
   } else {
     const size_t arr = (size_t)g.npair * g.Kp * 4;
     auto*        S   = (uint32_t*)carve(arr);
