@@ -19,6 +19,7 @@
 #include "../../include/srsran_amd/dlsch.h"
 #include "../../include/srsran_amd/tdec.h"
 #include "dlsch_internal.h"
+#include "host_staging.h"
 #include "rm_tables.h"
 #include "tdec_internal.h"
 
@@ -91,6 +92,7 @@ struct mi355_dlsch {
   size_t scratch_cap = 0;
   std::mutex mu;
   bool       prof = false;
+  HostStaging stage;
 };
 
 static uint32_t rm_buflen(uint32_t K) { return tdec_subblocks(K) ? 3 * (K + 32) + 12 : 3 * K + 12; }
@@ -354,28 +356,32 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
     p += rnd(b);
     return c;
   };
+  // staged (one pinned upload): tb | cb | slot | its (zeros) | running flags (zeros)
   auto*     d_tb    = (TbDesc*)carve(ntb * sizeof(TbDesc));
   auto*     d_cb    = (CbDesc*)carve(total_cb * sizeof(CbDesc));
   auto*     d_slot  = (uint32_t*)carve(total_cb * 4);
-  auto*     d_done  = (uint8_t*)carve(total_cb);
   auto*     d_its   = (uint32_t*)carve(total_cb * 4);
+  auto*     d_run   = (uint32_t*)carve(4 * (q->max_its + 1)); // running flags per half-iteration
+  const size_t staged = (size_t)(p - base);
+  auto*     d_done  = (uint8_t*)carve(total_cb);
   auto*     d_dec   = (uint8_t*)carve(dec_bytes);
   auto*     d_ret   = (int32_t*)carve(ntb * 4);
-  auto*     d_run   = (uint32_t*)carve(4 * (q->max_its + 1)); // running flags per half-iteration
 
+  CHECK_HIP(q->stage.reserve(staged));
+  q->stage.put(tbd.data(), ntb * sizeof(TbDesc));
   std::vector<CbDesc>   all_cb;
   std::vector<uint32_t> all_slot;
   all_cb.reserve(total_cb);
+  all_slot.reserve(total_cb);
   for (auto& kv : groups) {
     all_cb.insert(all_cb.end(), kv.second.cbs.begin(), kv.second.cbs.end());
     all_slot.insert(all_slot.end(), kv.second.slots.begin(), kv.second.slots.end());
   }
-  CHECK_HIP(hipMemcpyAsync(d_tb, tbd.data(), ntb * sizeof(TbDesc), hipMemcpyHostToDevice, s));
-  if (total_cb) {
-    CHECK_HIP(hipMemcpyAsync(d_cb, all_cb.data(), total_cb * sizeof(CbDesc), hipMemcpyHostToDevice, s));
-    CHECK_HIP(hipMemcpyAsync(d_slot, all_slot.data(), total_cb * 4, hipMemcpyHostToDevice, s));
-    CHECK_HIP(hipMemsetAsync(d_its, 0, total_cb * 4, s));
-  }
+  q->stage.put(all_cb.data(), total_cb * sizeof(CbDesc));
+  q->stage.put(all_slot.data(), total_cb * 4);
+  q->stage.zeros(total_cb * 4);
+  q->stage.zeros(4 * (q->max_its + 1));
+  CHECK_HIP(hipMemcpyAsync(base, q->stage.host, q->stage.used, hipMemcpyHostToDevice, s));
 
   DlschTbArgs ta{d_tb, (int)ntb, d_data, pool->cb_crc, pool->data, d_ret, &q->crc[0]};
   CHECK_HIP(dlsch_launch_prologue(ta, s));
@@ -420,7 +426,6 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   }
   // CBs already decoded in an earlier transmission start as done (before the rate matcher adds into them
   // this is the same flag it tested)
-  CHECK_HIP(hipMemsetAsync(d_run, 0, 4 * (q->max_its + 1), s));
   if (total_cb) CHECK_HIP(dlsch_launch_init_done(d_done, d_slot, pool->cb_crc, (int)total_cb, d_run, s));
 
   for (uint32_t h = 0; h < q->max_its; h++) {

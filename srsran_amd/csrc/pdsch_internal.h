@@ -33,14 +33,11 @@ struct PdschCwDev {
   uint32_t      pairs; // kernel B work items: symbol pairs
 };
 
-struct PdschBlk {
-  uint32_t job;  // job / codeword index
-  uint32_t unit; // first work item of the block
-};
-
-hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, const PdschBlk* blk, uint32_t nblk, hipStream_t s);
+// Block b of a launch belongs to item i with start[i] <= b < start[i + 1] (prefix sums of blocks per item).
+hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, const uint32_t* start, uint32_t njobs, uint32_t nblk,
+                                 hipStream_t s);
 hipError_t pdsch_launch_scr_pack(const uint32_t* c_init, uint32_t* const* dst, uint32_t n, const uint32_t* gold,
                                  uint32_t W, hipStream_t s);
-hipError_t pdsch_launch_llr(const PdschCwDev* cws, const PdschBlk* blk, uint32_t nblk, hipStream_t s);
+hipError_t pdsch_launch_llr(const PdschCwDev* cws, const uint32_t* start, uint32_t ncw, uint32_t nblk, hipStream_t s);
 
 } // namespace mi355

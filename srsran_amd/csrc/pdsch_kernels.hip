@@ -73,14 +73,25 @@ __device__ __forceinline__ void fold_max(uint32_t* m, float v)
   if ((threadIdx.x & 63) == 0) atomicMax(m, b);
 }
 
+// item owning block b: the last i with start[i] <= b (start has n + 1 entries)
+__device__ __forceinline__ uint32_t owner(const uint32_t* start, uint32_t n, uint32_t b)
+{
+  uint32_t lo = 0, hi = n; // invariant: start[lo] <= b < start[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (start[mid] <= b) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
 } // namespace
 
 __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restrict__ jobs,
-                                                      const PdschBlk* __restrict__ blk)
+                                                      const uint32_t* __restrict__ start, uint32_t njobs)
 {
-  const PdschBlk  bk = blk[blockIdx.x];
-  const PdschJobDev& J = jobs[bk.job];
-  const uint32_t  u  = bk.unit + threadIdx.x;
+  const uint32_t     j  = owner(start, njobs, blockIdx.x);
+  const PdschJobDev& J  = jobs[j];
+  const uint32_t     u  = (blockIdx.x - start[j]) * 256 + threadIdx.x;
   const bool      live = u < J.units;
   float           m0 = 0.f, m1 = 0.f; // per-thread csi contribution for the max
   if (live) {
@@ -447,11 +458,12 @@ template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, 
   store_llrs<QM>(C.e + b0, o, nb);
 }
 
-__global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ cws, const PdschBlk* __restrict__ blk)
+__global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ cws, const uint32_t* __restrict__ start,
+                                                 uint32_t ncw)
 {
-  const PdschBlk    bk = blk[blockIdx.x];
-  const PdschCwDev& C  = cws[bk.job];
-  const uint32_t    pr = bk.unit + threadIdx.x;
+  const uint32_t    c  = owner(start, ncw, blockIdx.x);
+  const PdschCwDev& C  = cws[c];
+  const uint32_t    pr = (blockIdx.x - start[c]) * 256 + threadIdx.x;
   if (pr >= C.pairs) return;
   switch (C.qm) {
     case 1: llr_pair<1>(C, pr); break;
@@ -462,10 +474,11 @@ __global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ 
   }
 }
 
-hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, const PdschBlk* blk, uint32_t nblk, hipStream_t s)
+hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, const uint32_t* start, uint32_t njobs, uint32_t nblk,
+                                 hipStream_t s)
 {
   if (!nblk) return hipSuccess;
-  hipLaunchKernelGGL(pdsch_equalize, dim3(nblk), dim3(256), 0, s, jobs, blk);
+  hipLaunchKernelGGL(pdsch_equalize, dim3(nblk), dim3(256), 0, s, jobs, start, njobs);
   return hipGetLastError();
 }
 
@@ -477,10 +490,10 @@ hipError_t pdsch_launch_scr_pack(const uint32_t* c_init, uint32_t* const* dst, u
   return hipGetLastError();
 }
 
-hipError_t pdsch_launch_llr(const PdschCwDev* cws, const PdschBlk* blk, uint32_t nblk, hipStream_t s)
+hipError_t pdsch_launch_llr(const PdschCwDev* cws, const uint32_t* start, uint32_t ncw, uint32_t nblk, hipStream_t s)
 {
   if (!nblk) return hipSuccess;
-  hipLaunchKernelGGL(pdsch_llr, dim3(nblk), dim3(256), 0, s, cws, blk);
+  hipLaunchKernelGGL(pdsch_llr, dim3(nblk), dim3(256), 0, s, cws, start, ncw);
   return hipGetLastError();
 }
 

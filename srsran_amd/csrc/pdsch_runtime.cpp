@@ -20,6 +20,7 @@
 #include "../../include/srsran_amd/dlsch.h"
 #include "../../include/srsran_amd/pdsch.h"
 #include "../../include/srsran_amd/tdec.h"
+#include "host_staging.h"
 #include "pdsch_internal.h"
 
 using namespace mi355;
@@ -173,6 +174,7 @@ struct mi355_pdsch {
   float2*                              d_arena   = nullptr;
   float*                               csi_arena = nullptr;
   int16_t*                             e_arena   = nullptr;
+  HostStaging                          stage;
   std::mutex                           mu;
 };
 
@@ -307,7 +309,7 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   const uint32_t njobs = (uint32_t)plans.size();
   size_t         nd = 0, ne = 0;
   std::vector<PdschCwDev> cws;
-  std::vector<PdschBlk>   blkA, blkB;
+  std::vector<uint32_t>   startA(njobs + 1), startB;
   std::vector<uint32_t>   new_ci;
   std::vector<uint32_t*>  new_dst;
   if (q->scr.size() > 4096) { // bound the sequence cache (~76 MB)
@@ -315,37 +317,29 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
     for (auto& kv : q->scr) (void)hipFree(kv.second);
     q->scr.clear();
   }
+  uint32_t nblkA = 0, nblkB = 0;
   for (uint32_t i = 0; i < njobs; i++) {
     JobPlan& P = plans[i];
     for (uint32_t cw = 0; cw < 2; cw++) {
       P.d_off[cw] = P.csi_off[cw] = nd;
       nd += (P.dev.nof_re + 63) / 64 * 64;
     }
-    for (uint32_t u = 0; u < P.dev.units; u += 256) blkA.push_back(PdschBlk{i, u});
-  }
-  for (uint32_t i = 0; i < njobs; i++) {
-    JobPlan& P = plans[i];
+    startA[i] = nblkA;
+    nblkA += (P.dev.units + 255) / 256;
     for (uint32_t t = 0; t < 2; t++) {
       if (!P.decode[t]) continue;
       const mi355_ra_tb_t& tb = jobs[i].cfg.grant.tb[t];
       P.e_off[t]              = ne;
       ne += (tb.nof_bits + 63) / 64 * 64;
-    }
-  }
-  // scratch: jobs | cws | blkA | blkB | cmax | d | csi | e
-  for (uint32_t i = 0; i < njobs; i++) {
-    for (uint32_t t = 0; t < 2; t++) {
-      if (!plans[i].decode[t]) continue;
       PdschCwDev c{};
-      c.nof_re = plans[i].dev.nof_re;
-      const mi355_ra_tb_t& tb = jobs[i].cfg.grant.tb[t];
-      c.nof_bits              = tb.nof_bits;
-      c.qm                    = mod_bits(tb.mod);
-      c.c_init   = ((uint32_t)jobs[i].cfg.rnti << 14) + (tb.cw_idx << 13) + ((jobs[i].sf.tti % 10) << 9) + q->cell.id;
+      c.nof_re     = P.dev.nof_re;
+      c.nof_bits   = tb.nof_bits;
+      c.qm         = mod_bits(tb.mod);
+      c.c_init     = ((uint32_t)jobs[i].cfg.rnti << 14) + (tb.cw_idx << 13) + ((jobs[i].sf.tti % 10) << 9) + q->cell.id;
       c.csi_enable = jobs[i].cfg.csi_enable ? 1u : 0u;
       c.pairs      = (c.nof_re + 1) / 2;
-      const uint32_t ci = (uint32_t)cws.size();
-      for (uint32_t u = 0; u < c.pairs; u += 256) blkB.push_back(PdschBlk{ci, u});
+      startB.push_back(nblkB);
+      nblkB += (c.pairs + 255) / 256;
       auto it = q->scr.find(c.c_init);
       if (it == q->scr.end()) {
         uint32_t* d = nullptr;
@@ -358,29 +352,28 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
       cws.push_back(c);
     }
   }
+  startA[njobs] = nblkA;
+  startB.push_back(nblkB);
+  const size_t ncw = cws.size();
+  // device scratch: [staged descriptors | d | csi | e]; the staged part mirrors the pinned host buffer
+  const size_t staged = staged_size(njobs * sizeof(PdschJobDev)) + staged_size(ncw * sizeof(PdschCwDev)) +
+                        staged_size(startA.size() * 4) + staged_size(startB.size() * 4) +
+                        staged_size(new_ci.size() * 4) + staged_size(new_ci.size() * 8) + staged_size(njobs * 8);
   auto         rnd  = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t need = rnd(njobs * sizeof(PdschJobDev)) + rnd(cws.size() * sizeof(PdschCwDev)) +
-                      rnd(blkA.size() * sizeof(PdschBlk)) + rnd(blkB.size() * sizeof(PdschBlk)) + rnd(njobs * 8) +
-                      rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2) + rnd(new_ci.size() * 12);
+  const size_t need = staged + rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2);
   char* base = nullptr;
   int   r    = get_scratch(q, need, &base);
   if (r) return r;
-  char* p     = base;
-  auto  carve = [&](size_t b) {
-    char* c = p;
-    p += rnd(b);
-    return c;
-  };
-  auto* d_jobs = (PdschJobDev*)carve(njobs * sizeof(PdschJobDev));
-  auto* d_cws  = (PdschCwDev*)carve(cws.size() * sizeof(PdschCwDev));
-  auto* d_blkA = (PdschBlk*)carve(blkA.size() * sizeof(PdschBlk));
-  auto* d_blkB = (PdschBlk*)carve(blkB.size() * sizeof(PdschBlk));
-  auto* d_nci  = (uint32_t*)carve(new_ci.size() * 4);
-  auto* d_ndst = (uint32_t**)carve(new_ci.size() * 8);
-  auto* d_cmax = (uint32_t*)carve(njobs * 8);
-  q->d_arena   = (float2*)carve(nd * 8);
-  q->csi_arena = (float*)carve(nd * 4);
-  q->e_arena   = (int16_t*)carve(ne * 2);
+  q->d_arena   = (float2*)(base + staged);
+  q->csi_arena = (float*)(base + staged + rnd(nd * 8));
+  q->e_arena   = (int16_t*)(base + staged + rnd(nd * 8) + rnd(nd * 4));
+  CHECK_HIP(q->stage.reserve(staged));
+  // offsets are known up front: jobs | cws | startA | startB | nci | ndst | cmax
+  const size_t o_jobs = 0, o_cws = o_jobs + staged_size(njobs * sizeof(PdschJobDev));
+  const size_t o_sa = o_cws + staged_size(ncw * sizeof(PdschCwDev)), o_sb = o_sa + staged_size(startA.size() * 4);
+  const size_t o_nci = o_sb + staged_size(startB.size() * 4), o_ndst = o_nci + staged_size(new_ci.size() * 4);
+  const size_t o_cmax = o_ndst + staged_size(new_ci.size() * 8);
+  uint32_t*    d_cmax = (uint32_t*)(base + o_cmax);
   std::vector<PdschJobDev> hj(njobs);
   for (uint32_t i = 0; i < njobs; i++) {
     JobPlan& P = plans[i];
@@ -403,18 +396,18 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
       ci++;
     }
   }
-  CHECK_HIP(hipMemcpyAsync(d_jobs, hj.data(), njobs * sizeof(PdschJobDev), hipMemcpyHostToDevice, s));
-  if (!cws.empty()) CHECK_HIP(hipMemcpyAsync(d_cws, cws.data(), cws.size() * sizeof(PdschCwDev), hipMemcpyHostToDevice, s));
-  if (!blkA.empty()) CHECK_HIP(hipMemcpyAsync(d_blkA, blkA.data(), blkA.size() * sizeof(PdschBlk), hipMemcpyHostToDevice, s));
-  if (!blkB.empty()) CHECK_HIP(hipMemcpyAsync(d_blkB, blkB.data(), blkB.size() * sizeof(PdschBlk), hipMemcpyHostToDevice, s));
-  if (!new_ci.empty()) {
-    CHECK_HIP(hipMemcpyAsync(d_nci, new_ci.data(), new_ci.size() * 4, hipMemcpyHostToDevice, s));
-    CHECK_HIP(hipMemcpyAsync(d_ndst, new_dst.data(), new_dst.size() * 8, hipMemcpyHostToDevice, s));
-  }
-  CHECK_HIP(hipMemsetAsync(d_cmax, 0, njobs * 8, s));
-  CHECK_HIP(pdsch_launch_equalize(d_jobs, d_blkA, (uint32_t)blkA.size(), s));
-  CHECK_HIP(pdsch_launch_scr_pack(d_nci, d_ndst, (uint32_t)new_ci.size(), q->gold, PDSCH_GOLD_MAX / 32, s));
-  CHECK_HIP(pdsch_launch_llr(d_cws, d_blkB, (uint32_t)blkB.size(), s));
+  q->stage.put(hj.data(), njobs * sizeof(PdschJobDev));
+  q->stage.put(cws.data(), ncw * sizeof(PdschCwDev));
+  q->stage.put(startA.data(), startA.size() * 4);
+  q->stage.put(startB.data(), startB.size() * 4);
+  q->stage.put(new_ci.data(), new_ci.size() * 4);
+  q->stage.put(new_dst.data(), new_dst.size() * 8);
+  q->stage.zeros(njobs * 8);
+  CHECK_HIP(hipMemcpyAsync(base, q->stage.host, q->stage.used, hipMemcpyHostToDevice, s));
+  CHECK_HIP(pdsch_launch_equalize((const PdschJobDev*)(base + o_jobs), (const uint32_t*)(base + o_sa), njobs, nblkA, s));
+  CHECK_HIP(pdsch_launch_scr_pack((const uint32_t*)(base + o_nci), (uint32_t* const*)(base + o_ndst),
+                                  (uint32_t)new_ci.size(), q->gold, PDSCH_GOLD_MAX / 32, s));
+  CHECK_HIP(pdsch_launch_llr((const PdschCwDev*)(base + o_cws), (const uint32_t*)(base + o_sb), (uint32_t)ncw, nblkB, s));
   return MI355_SUCCESS;
 }
 

@@ -130,7 +130,7 @@ __device__ __forceinline__ void set_minf(v2s s[8])
 // wait for it, which serialises the memory pipeline).
 // DIAG (diagnostic builds only, selected by MI355_TDEC_DIAG): 1 = backward pass only, 2 = forward only
 template <int NSB, int SEG, int MODE, int DIAG = 0>
-__global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tdec_win_halfit(TdecWinArgs a)
 {
   constexpr int NL = NSB / 2;
   constexpr int G  = 64 / NL;
@@ -327,6 +327,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
     for (int s = 0; s < 8; s++) c[s] = ck[((size_t)t * 8 + s) * 64];
   };
   load(0, cx, cy, ca, cd, cc);
+  uint32_t dbits = 0; // decision bits of the previous (even) segment, bits 16..31
 
 #pragma unroll 1
   for (int t = 0; t < nseg; t++) {
@@ -334,6 +335,7 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
     const int e  = (s0 + SEG < L) ? s0 + SEG : L;
     uint32_t  nx[SEG], ny[SEG], na[SEG] = {}, nd[SEG], nc[8];
     uint32_t  bits = 0; // decision bits of the segment: window 2l in bits 8..15, 2l+1 in 0..7 (MSB first)
+    if (wr_bits && (t & 1)) bits = dbits;
     if (t + 1 < nseg) load(t + 1, nx, ny, na, nd, nc);
 
     v2s xin[SEG];
@@ -429,9 +431,20 @@ __global__ __launch_bounds__(256) void tdec_win_halfit(TdecWinArgs a)
     }
     }
     if (wr_bits) { // turbodecoder_win.h:973-993: bit = LLR > 0, natural order, MSB first
-      uint8_t* o = a.dec + (size_t)cb * a.dec_stride + (size_t)(2 * l) * (L / 8) + t;
-      o[0]       = (uint8_t)(bits >> 8);
-      o[L / 8]   = (uint8_t)bits;
+      // two segments per store: bytes t-1, t of each window as one 16-bit word (the segment of an odd t
+      // lands in the high byte); a trailing even segment is stored alone
+      if ((t & 1) || t + 1 == nseg) {
+        uint8_t* o = a.dec + (size_t)cb * a.dec_stride + (size_t)(2 * l) * (L / 8) + (t & ~1);
+        if (t & 1) {
+          *(uint16_t*)o           = (uint16_t)(((bits >> 8) & 0xffu) << 8 | ((bits >> 24) & 0xffu));
+          *(uint16_t*)(o + L / 8) = (uint16_t)((bits & 0xffu) << 8 | ((bits >> 16) & 0xffu));
+        } else {
+          o[0]     = (uint8_t)(bits >> 8);
+          o[L / 8] = (uint8_t)bits;
+        }
+      } else {
+        dbits = bits << 16; // keep segment t (even) in the upper half for the next segment's store
+      }
     }
 #pragma unroll
     for (int i = 0; i < SEG; i++) {
