@@ -226,29 +226,31 @@ class Tm4Batch:
             self.pays[2 * i + 1] = self.d_pay.ptr + (2 * i + 1) * self.plen
         from srsran_amd.ue_dl import ChestRes, _declare
         self.L = _declare()
-        self.L.mi355_ue_dl_decode_pdsch_batch.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(DlSfJob),
-                                                           C.POINTER(P.DlSfCfg), C.POINTER(P.PdschCfg),
-                                                           C.POINTER(ChestRes), C.POINTER(C.c_void_p), C.c_uint32,
-                                                           C.POINTER(P.PdschRes), C.c_void_p]
         self.L.mi355_softbuffer_reset_range.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
         self.chest = (ChestRes * B)()
         self.res = (P.PdschRes * (2 * B))()
 
     def step(self, stages=None):
+        """One batch: new-TB softbuffer reset + mi355_ue_dl_decode_batch (OFDM, estimation, PDSCH, DL-SCH).
+        With `stages`, the two-call form (decode_fft_estimate, then decode_pdsch) is timed per stage instead."""
         from srsran_amd import check, lib
         t0 = time.perf_counter()
         check(self.L.mi355_softbuffer_reset_range(self.pool.h, 0, 2 * self.B, None), "softbuffer_reset_range")
+        C.memset(self.res, 0, C.sizeof(self.res))
+        if stages is None:
+            check(self.L.mi355_ue_dl_decode_batch(self.ue.h, self.pool.h, self.jobs, self.sfs, self.cfgs,
+                                                  C.byref(self.chest_cfg), self.chest, self.pays, self.B, self.res,
+                                                  None), "ue_dl_decode_batch")
+            return
         check(self.L.mi355_ue_dl_decode_fft_estimate_batch(self.ue.h, self.jobs, self.B, C.byref(self.chest_cfg),
                                                            self.chest, None), "decode_fft_estimate")
         t1 = time.perf_counter()
-        C.memset(self.res, 0, C.sizeof(self.res))
         check(self.L.mi355_ue_dl_decode_pdsch_batch(self.ue.h, self.pool.h, self.jobs, self.sfs, self.cfgs,
                                                     self.chest, self.pays, self.B, self.res, None), "decode_pdsch")
-        if stages is not None:
-            lib().mi355_device_sync()
-            t2 = time.perf_counter()
-            stages["reset_fft_chest_ms"] = stages.get("reset_fft_chest_ms", 0) + (t1 - t0) * 1e3
-            stages["pdsch_decode_ms"] = stages.get("pdsch_decode_ms", 0) + (t2 - t1) * 1e3
+        lib().mi355_device_sync()
+        t2 = time.perf_counter()
+        stages["reset_fft_chest_ms"] = stages.get("reset_fft_chest_ms", 0) + (t1 - t0) * 1e3
+        stages["pdsch_decode_ms"] = stages.get("pdsch_decode_ms", 0) + (t2 - t1) * 1e3
 
     def check_payloads(self):
         """All TBs CRC-ok and every payload equal to what the encoder was given."""

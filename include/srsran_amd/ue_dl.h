@@ -118,6 +118,21 @@ int mi355_ue_dl_decode_pdsch_batch(mi355_ue_dl_t*              q,
                                    mi355_pdsch_res_t*          res,
                                    void*                       stream);
 
+/* decode_fft_estimate + decode_pdsch in one call: the noise estimate stays on the device and the PDSCH jobs
+ * are planned while the GPU demodulates, so there is no host round trip between the stages.  chest[i] and
+ * res[2*i + tb] are filled on return; same semantics as the two calls in sequence. */
+int mi355_ue_dl_decode_batch(mi355_ue_dl_t*              q,
+                             mi355_softbuffer_pool_t*    pool,
+                             const mi355_dl_sf_job_t*    sfjobs,
+                             const mi355_dl_sf_cfg_t*    sfs,
+                             const mi355_pdsch_cfg_t*    cfgs,
+                             const mi355_chest_dl_cfg_t* chest_cfg,
+                             mi355_chest_dl_res_t*       chest,
+                             uint8_t* const*             payloads,
+                             uint32_t                    njobs,
+                             mi355_pdsch_res_t*          res,
+                             void*                       stream);
+
 /* The PDSCH receiver bound to this UE's cell (borrowed; valid until mi355_ue_dl_destroy). */
 mi355_pdsch_t* mi355_ue_dl_pdsch(mi355_ue_dl_t* q);
 

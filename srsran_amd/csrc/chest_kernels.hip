@@ -235,6 +235,27 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
   }
 }
 
+__global__ __launch_bounds__(256) void chest_noise(const float* out, uint32_t R, uint32_t P, uint32_t njobs,
+                                                   float* noise)
+{
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= njobs) return;
+  float n = 0.f;
+  for (uint32_t a = 0; a < R; a++) {
+    float acc = 0.f;
+    for (uint32_t p = 0; p < P; p++) acc += out[(((size_t)i * R + a) * P + p) * 5];
+    n += acc / (float)P;
+  }
+  noise[i] = n / (float)R;
+}
+
+hipError_t chest_launch_noise(const float* out, uint32_t R, uint32_t P, uint32_t njobs, float* noise, hipStream_t s)
+{
+  if (!njobs) return hipSuccess;
+  hipLaunchKernelGGL(chest_noise, dim3((njobs + 255) / 256), dim3(256), 0, s, out, R, P, njobs, noise);
+  return hipGetLastError();
+}
+
 hipError_t chest_launch(const ChestArgs& a, uint32_t njobs, hipStream_t s)
 {
   if (!njobs) return hipSuccess;

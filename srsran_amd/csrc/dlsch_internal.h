@@ -58,6 +58,7 @@ struct DlschCheckArgs {
   uint8_t*        sb_crc;
   const CrcTable* crc24a;
   const CrcTable* crc24b;
+  const uint32_t* scale; // [CRC24A | CRC24B][64 lanes]: x^(8 * bytes after the lane's chunk) mod P for K/8 bytes
 };
 
 struct DlschTbArgs {

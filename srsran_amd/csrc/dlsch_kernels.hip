@@ -27,8 +27,18 @@ __global__ __launch_bounds__(512) void dlsch_rm_rx(DlschRmArgs a)
   const uint32_t  N = a.N, tid = threadIdx.x, nt = blockDim.x;
   const int16_t*  e = a.e + d.e_off + d.rp;
   const uint32_t  n_e = d.n_e, first = min(n_e, N);
-  // pass 0: the first wrap initialises (positions >= n_e get 0), later wraps accumulate
-  for (uint32_t r = tid; r < N; r += nt) acc[r] = r < first ? (uint16_t)e[r] : 0;
+  // pass 0: the first wrap initialises (positions >= n_e get 0), later wraps accumulate; 4 loads in flight
+  for (uint32_t r = tid; r < N; r += 4 * nt) {
+    uint16_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t rr = r + k * nt;
+      v[k]              = rr < first ? (uint16_t)e[rr] : (uint16_t)0;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (r + k * nt < N) acc[r + k * nt] = v[k];
+  }
   for (uint32_t base = N; base < n_e; base += N) {
     __syncthreads();
     for (uint32_t r = tid; r < N && base + r < n_e; r += nt) acc[r] = (uint16_t)(acc[r] + (uint16_t)e[base + r]);
@@ -38,14 +48,23 @@ __global__ __launch_bounds__(512) void dlsch_rm_rx(DlschRmArgs a)
   const uint16_t* inv   = a.inv[d.rv];
   uint32_t*       sb    = (uint32_t*)(a.sb + (size_t)d.slot * a.sb_stride);
   const uint32_t  pairs = a.buflen / 2;
-  for (uint32_t jp = tid; jp < pairs; jp += nt) {
-    const uint32_t iv = ((const uint32_t*)inv)[jp]; // inv is 4-byte aligned (buflen even)
-    const uint32_t r0 = iv & 0xffffu, r1 = iv >> 16;
-    const bool     h0 = r0 != RM_NONE && r0 < n_e, h1 = r1 != RM_NONE && r1 < n_e;
-    if (!fresh && !h0 && !h1) continue;
-    const uint32_t s0 = h0 ? acc[r0] : 0u, s1 = h1 ? acc[r1] : 0u;
-    const uint32_t v  = fresh ? 0u : sb[jp];
-    sb[jp]            = ((v + s0) & 0xffffu) | (((v >> 16) + s1) << 16);
+  for (uint32_t j0 = tid; j0 < pairs; j0 += 2 * nt) {
+    uint32_t iv[2], old[2] = {0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 2; k++) { // inv is 4-byte aligned (buflen even)
+      const uint32_t jp = j0 + k * nt;
+      iv[k]             = jp < pairs ? ((const uint32_t*)inv)[jp] : 0xffffffffu;
+      if (!fresh && jp < pairs) old[k] = sb[jp];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const uint32_t jp = j0 + k * nt;
+      const uint32_t r0 = iv[k] & 0xffffu, r1 = iv[k] >> 16;
+      const bool     h0 = r0 != RM_NONE && r0 < n_e, h1 = r1 != RM_NONE && r1 < n_e;
+      if (jp >= pairs || (!fresh && !h0 && !h1)) continue;
+      const uint32_t s0 = h0 ? acc[r0] : 0u, s1 = h1 ? acc[r1] : 0u;
+      sb[jp]            = ((old[k] + s0) & 0xffffu) | (((old[k] >> 16) + s1) << 16);
+    }
   }
 }
 
@@ -85,6 +104,21 @@ __device__ uint32_t wave_crc24(const uint8_t* bytes, uint32_t nbytes, const CrcT
     if (after & 1) sc = gf2_mulmod24(sc, T.pw[i], T.poly);
   }
   crc = gf2_mulmod24(crc, sc, T.poly);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
+  return crc;
+}
+
+// wave CRC with the per-lane scale factors x^(8*after) precomputed for this byte count (scale[lane])
+__device__ __forceinline__ uint32_t wave_crc24_scaled(const uint8_t* bytes, uint32_t nbytes, const CrcTable& T,
+                                                      const uint32_t* scale)
+{
+  const int      lane  = threadIdx.x & 63;
+  const uint32_t chunk = (nbytes + 63) / 64;
+  const uint32_t b0    = min(nbytes, lane * chunk), b1 = min(nbytes, b0 + chunk);
+  uint32_t       crc   = 0;
+  for (uint32_t i = b0; i < b1; i++) crc = ((crc << 8) ^ T.t[((crc >> 16) & 0xff) ^ bytes[i]]) & 0xffffffu;
+  crc = gf2_mulmod24(crc, scale[lane], T.poly);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
   return crc;
@@ -135,7 +169,7 @@ __global__ __launch_bounds__(1024) void dlsch_cb_check(DlschCheckArgs a)
   if (b < a.ncb && *a.remaining != 0 && !a.done[b]) {
     const CbDesc&  d   = a.desc[b];
     const uint8_t* dec = a.dec + (size_t)b * a.dec_stride;
-    const uint32_t crc = wave_crc24(dec, a.K / 8, d.C > 1 ? *a.crc24b : *a.crc24a);
+    const uint32_t crc = wave_crc24_scaled(dec, a.K / 8, d.C > 1 ? *a.crc24b : *a.crc24a, a.scale + (d.C > 1 ? 64 : 0));
     const bool     ok  = crc == 0;
     const bool     fin = ok || a.h + 1 == a.max_its;
     if (!fin) {

@@ -86,6 +86,7 @@ struct mi355_dlsch {
   uint32_t                               max_its = 10; // SRSLTE_PDSCH_MAX_TDEC_ITERS, sch.c:35
   std::map<uint32_t, mi355_tdec_batch_t*> dec;         // one decoder workspace per K
   std::map<uint64_t, uint16_t*>          rm;           // (K << 2 | rv) -> device table
+  std::map<uint32_t, uint32_t*>          scales;       // K -> per-lane CRC scale factors
   CrcTable*                              crc = nullptr; // [0] CRC24A, [1] CRC24B
   // per-call scratch
   char*  scratch     = nullptr;
@@ -110,6 +111,45 @@ static int rm_table(mi355_dlsch_t* q, uint32_t K, uint32_t rv, const uint16_t** 
     CHECK_HIP(hipMalloc(&d, inv.size() * 2));
     CHECK_HIP(hipMemcpy(d, inv.data(), inv.size() * 2, hipMemcpyHostToDevice));
     it = q->rm.emplace(key, d).first;
+  }
+  *out = it->second;
+  return MI355_SUCCESS;
+}
+
+static uint32_t gf2_mulmod24_host(uint32_t a, uint32_t b, uint32_t poly)
+{
+  uint32_t r = 0;
+  for (int i = 23; i >= 0; i--) {
+    r <<= 1;
+    if (r & 0x1000000u) r ^= poly;
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r & 0xffffffu;
+}
+
+// per-lane CRC chunk scale factors for the decision bytes of K (wave_crc24_scaled), both polynomials
+static int crc_scales(mi355_dlsch_t* q, uint32_t K, const uint32_t** out)
+{
+  auto it = q->scales.find(K);
+  if (it == q->scales.end()) {
+    std::vector<uint32_t> t(128);
+    const uint32_t        nbytes = K / 8, chunk = (nbytes + 63) / 64;
+    const uint32_t        polys[2] = {0x1864CFB, 0x1800063};
+    for (int pi = 0; pi < 2; pi++) {
+      for (uint32_t lane = 0; lane < 64; lane++) {
+        const uint32_t b0 = std::min(nbytes, lane * chunk), b1 = std::min(nbytes, b0 + chunk);
+        uint32_t       sc = 1, x8 = 1u << 8; // x^(8 * 2^i)
+        for (uint32_t after = nbytes - b1; after; after >>= 1) {
+          if (after & 1) sc = gf2_mulmod24_host(sc, x8, polys[pi]);
+          x8 = gf2_mulmod24_host(x8, x8, polys[pi]);
+        }
+        t[pi * 64 + lane] = sc;
+      }
+    }
+    uint32_t* d = nullptr;
+    CHECK_HIP(hipMalloc(&d, t.size() * 4));
+    CHECK_HIP(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    it = q->scales.emplace(K, d).first;
   }
   *out = it->second;
   return MI355_SUCCESS;
@@ -246,6 +286,7 @@ void mi355_dlsch_destroy(mi355_dlsch_t* q)
   (void)hipDeviceSynchronize();
   for (auto& kv : q->dec) mi355_tdec_batch_destroy(kv.second);
   for (auto& kv : q->rm) (void)hipFree(kv.second);
+  for (auto& kv : q->scales) (void)hipFree(kv.second);
   (void)hipFree(q->crc);
   (void)hipFree(q->scratch);
   if (q->own) (void)hipStreamDestroy(q->own);
@@ -391,6 +432,7 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
     uint32_t            K, off, n;
     uint8_t*            dec;
     mi355_tdec_batch_t* td;
+    const uint32_t*     scale;
   };
   std::vector<Live> live;
   size_t            off = 0, doff = 0;
@@ -420,7 +462,9 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
       mi355_tdec_batch_set_profiling(td, q->prof);
       it = q->dec.emplace(K, td).first;
     }
-    live.push_back(Live{K, (uint32_t)off, n, d_dec + doff, it->second});
+    const uint32_t* sc = nullptr;
+    if ((r = crc_scales(q, K, &sc))) return r;
+    live.push_back(Live{K, (uint32_t)off, n, d_dec + doff, it->second, sc});
     off += n;
     doff += (size_t)n * (K / 8);
   }
@@ -433,7 +477,8 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
       TdecRun rq{pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, d_run + h, lv.n, lv.K, h, h + 1, lv.dec, lv.K / 8, s};
       if ((r = mi355_tdec_run_internal(lv.td, rq))) return r;
       DlschCheckArgs ca{d_cb + lv.off, (int)lv.n, lv.K, h, q->max_its, lv.dec, lv.K / 8, d_data,
-                        d_done + lv.off, d_run + h, d_run + h + 1, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1]};
+                        d_done + lv.off, d_run + h, d_run + h + 1, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1],
+                        lv.scale};
       CHECK_HIP(dlsch_launch_check(ca, s));
     }
   }

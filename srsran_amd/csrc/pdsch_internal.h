@@ -19,6 +19,7 @@ struct PdschJobDev {
   uint32_t        row;       // 12 * nof_prb: grid index -> OFDM symbol l'
   uint32_t        rhob_mask; // OFDM symbols l' scaled by 1/rho_b (apply_power_allocation, pdsch.c:589-607)
   float           rhob_inv, scaling, noise;
+  const float*    noise_dev; // nullable: noise estimate produced on the device (chest), used instead of noise
   uint32_t        units;     // kernel A work items
 };
 

@@ -94,6 +94,7 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
   const uint32_t     u  = (blockIdx.x - start[j]) * 256 + threadIdx.x;
   const bool      live = u < J.units;
   float           m0 = 0.f, m1 = 0.f; // per-thread csi contribution for the max
+  const float     noise = J.noise_dev ? *J.noise_dev : J.noise;
   if (live) {
     const uint32_t nrx = J.nof_rx;
     auto           Y   = [&](uint32_t r, uint32_t i) {
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
           r          = r + Y(p, i) * cj(h);
           hh += h.re * h.re + h.im * h.im;
         }
-        const float c = hh + J.noise, nrm = 1.0f / J.scaling;
+        const float c = hh + noise, nrm = 1.0f / J.scaling;
         st(J.d[0], i, mk(r.re * nrm / c, r.im * nrm / c));
         J.csi[0][i] = c;
         m0          = c;
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
           }
           cf    x0, x1;
           float c0, c1;
-          mmse_2x2_csi(Y(0, i), Y(1, i), h00, h01, h10, h11, x0, x1, c0, c1, J.noise, norm);
+          mmse_2x2_csi(Y(0, i), Y(1, i), h00, h01, h10, h11, x0, x1, c0, c1, noise, norm);
           st(J.d[0], i, x0);
           st(J.d[1], i, x1);
           J.csi[0][i] = c0;
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
         }
         cf    x0, x1;
         float c0, c1;
-        mmse_2x2_csi(Y(0, i), Y(1, i), h00, h01, h10, h11, x0, x1, c0, c1, J.noise, 2.0f / J.scaling);
+        mmse_2x2_csi(Y(0, i), Y(1, i), h00, h01, h10, h11, x0, x1, c0, c1, noise, 2.0f / J.scaling);
         st(J.d[0], i, x0);
         st(J.d[1], i, x1);
         J.csi[0][i] = c0;

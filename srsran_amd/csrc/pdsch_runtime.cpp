@@ -22,6 +22,7 @@
 #include "../../include/srsran_amd/tdec.h"
 #include "host_staging.h"
 #include "pdsch_internal.h"
+#include "runtime_internal.h"
 
 using namespace mi355;
 
@@ -500,6 +501,14 @@ int mi355_pdsch_decode_batch(mi355_pdsch_t*           q,
                              mi355_pdsch_res_t*       res,
                              void*                    stream)
 {
+  return mi355::pdsch_decode_batch_dev_noise(q, pool, jobs, njobs, res, stream, nullptr);
+}
+
+} // extern "C"
+
+int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi355_pdsch_job_t* jobs,
+                                        uint32_t njobs, mi355_pdsch_res_t* res, void* stream, const float* d_noise)
+{
   if (!q || !pool || !res || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;
   std::lock_guard<std::mutex> lock(q->mu);
   CHECK_HIP(hipSetDevice(q->device));
@@ -508,6 +517,8 @@ int mi355_pdsch_decode_batch(mi355_pdsch_t*           q,
   for (uint32_t i = 0; i < njobs; i++) {
     int r = plan_job(q, jobs[i], &res[2 * i], plans[i]);
     if (r) return r;
+    // noise estimate left in device memory by the channel estimator (ZF ignores it, pdsch.c:934)
+    if (d_noise && jobs[i].cfg.decoder_type != MI355_MIMO_DECODER_ZF) plans[i].dev.noise_dev = d_noise + i;
   }
   int r = run_frontend(q, jobs, plans, s);
   if (r) return r;
@@ -555,4 +566,4 @@ int mi355_pdsch_decode_batch(mi355_pdsch_t*           q,
   return MI355_SUCCESS;
 }
 
-} // extern "C"
+

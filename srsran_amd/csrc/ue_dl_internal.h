@@ -37,5 +37,7 @@ struct ChestArgs {
 
 hipError_t ofdm_launch_rx(const OfdmArgs& a, uint32_t njobs, hipStream_t s);
 hipError_t chest_launch(const ChestArgs& a, uint32_t njobs, hipStream_t s);
+// get_noise (chest_dl.c:847-857) per job from the [job][rx][port][5] estimator outputs
+hipError_t chest_launch_noise(const float* out, uint32_t R, uint32_t P, uint32_t njobs, float* noise, hipStream_t s);
 
 } // namespace mi355

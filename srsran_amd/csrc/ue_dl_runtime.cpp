@@ -12,6 +12,7 @@
 #include "../../include/srsran_amd/tdec.h"
 #include "../../include/srsran_amd/ue_dl.h"
 #include "lte_common.h"
+#include "runtime_internal.h"
 #include "ue_dl_internal.h"
 
 using namespace mi355;
@@ -123,7 +124,8 @@ static int get_scratch(mi355_ue_dl_t* q, size_t bytes, char** p)
   return MI355_SUCCESS;
 }
 
-static int ofdm_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, hipStream_t s)
+static int ofdm_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, hipStream_t s,
+                    size_t* used = nullptr)
 {
   std::vector<OfdmJob> oj;
   oj.reserve((size_t)njobs * q->nof_rx);
@@ -144,6 +146,7 @@ static int ofdm_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t nj
     a.jobs = (const OfdmJob*)base + off;
     CHECK_HIP(ofdm_launch_rx(a, (uint32_t)std::min<size_t>(65535, oj.size() - off), s));
   }
+  if (used) *used = (oj.size() * sizeof(OfdmJob) + 255) / 256 * 256;
   return MI355_SUCCESS;
 }
 
@@ -217,23 +220,35 @@ static void fill_res(const mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, co
   }
 }
 
-static int chest_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, const mi355_chest_dl_cfg_t* cfg,
-                     mi355_chest_dl_res_t* res, hipStream_t s)
+static int chest_check_cfg(const mi355_chest_dl_cfg_t* cfg)
 {
-  if (!cfg || !res) return MI355_ERROR_INVALID_INPUTS;
+  if (!cfg) return MI355_ERROR_INVALID_INPUTS;
   // supported: AVERAGE estimator, REFS noise, no CFO / sync-error correction (the srsUE and phy_dl_test setup)
   if (cfg->estimator_alg != MI355_ESTIMATOR_ALG_AVERAGE || cfg->noise_alg != MI355_NOISE_ALG_REFS ||
       cfg->cfo_estimate_enable || cfg->sync_error_enable || cfg->filter_type > MI355_CHEST_FILTER_NONE)
     return MI355_ERROR;
+  return MI355_SUCCESS;
+}
+
+// launches the estimator (and, when d_noise is wanted, the per-job noise average of get_noise) without
+// synchronising; the scratch region starts after `offset` bytes (the OFDM job table may live before it)
+static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs,
+                             const mi355_chest_dl_cfg_t* cfg, hipStream_t s, size_t offset, float** d_out_p,
+                             float** d_noise_p)
+{
+  int r = chest_check_cfg(cfg);
+  if (r) return r;
   const uint32_t        P = q->cell.nof_ports, R = q->nof_rx;
   std::vector<ChestJob> cj;
   cj.reserve((size_t)njobs * P * R);
   const size_t nout = (size_t)njobs * P * R * 5;
   char*        base = nullptr;
   const size_t jb   = ((size_t)njobs * P * R * sizeof(ChestJob) + 255) / 256 * 256;
-  int          r    = get_scratch(q, jb + nout * 4 + 256, &base);
-  if (r) return r;
-  float* d_out = (float*)(base + jb);
+  const size_t ob   = (nout * 4 + 255) / 256 * 256;
+  if ((r = get_scratch(q, offset + jb + ob + (size_t)njobs * 4 + 256, &base))) return r;
+  base += offset;
+  float* d_out   = (float*)(base + jb);
+  float* d_noise = (float*)(base + jb + ob);
   for (uint32_t i = 0; i < njobs; i++) {
     for (uint32_t a = 0; a < R; a++) {
       for (uint32_t p = 0; p < P; p++) {
@@ -254,11 +269,32 @@ static int chest_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t n
   ca.coef0       = cfg->filter_coef[0];
   ca.coef1       = cfg->filter_coef[1];
   CHECK_HIP(chest_launch(ca, (uint32_t)cj.size(), s));
+  if (d_noise_p) CHECK_HIP(chest_launch_noise(d_out, R, P, njobs, d_noise, s));
+  *d_out_p = d_out;
+  if (d_noise_p) *d_noise_p = d_noise;
+  return MI355_SUCCESS;
+}
+
+static int chest_finish(mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const float* d_out, uint32_t njobs,
+                        mi355_chest_dl_res_t* res, hipStream_t s)
+{
+  const uint32_t     P = q->cell.nof_ports, R = q->nof_rx;
+  const size_t       nout = (size_t)njobs * P * R * 5;
   std::vector<float> out(nout);
   CHECK_HIP(hipMemcpyAsync(out.data(), d_out, nout * 4, hipMemcpyDeviceToHost, s));
   CHECK_HIP(hipStreamSynchronize(s));
   for (uint32_t i = 0; i < njobs; i++) fill_res(q, cfg, &out[(size_t)i * R * P * 5], &res[i]);
   return MI355_SUCCESS;
+}
+
+static int chest_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, const mi355_chest_dl_cfg_t* cfg,
+                     mi355_chest_dl_res_t* res, hipStream_t s, size_t offset = 0)
+{
+  if (!res) return MI355_ERROR_INVALID_INPUTS;
+  float* d_out = nullptr;
+  int    r     = chest_launch_only(q, jobs, njobs, cfg, s, offset, &d_out, nullptr);
+  if (r) return r;
+  return chest_finish(q, cfg, d_out, njobs, res, s);
 }
 
 extern "C" {
@@ -337,12 +373,46 @@ int mi355_ue_dl_decode_fft_estimate_batch(mi355_ue_dl_t* q, const mi355_dl_sf_jo
   std::lock_guard<std::mutex> lock(q->mu);
   CHECK_HIP(hipSetDevice(q->device));
   hipStream_t s = stream ? (hipStream_t)stream : q->own;
-  int         r = ofdm_run(q, jobs, njobs, s);
+  size_t      used = 0;
+  int         r    = ofdm_run(q, jobs, njobs, s, &used);
   if (r) return r;
-  return chest_run(q, jobs, njobs, cfg, res, s);
+  return chest_run(q, jobs, njobs, cfg, res, s, used);
 }
 
 mi355_pdsch_t* mi355_ue_dl_pdsch(mi355_ue_dl_t* q) { return q ? q->pdsch : nullptr; }
+
+int mi355_ue_dl_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, const mi355_dl_sf_job_t* sfjobs,
+                             const mi355_dl_sf_cfg_t* sfs, const mi355_pdsch_cfg_t* cfgs,
+                             const mi355_chest_dl_cfg_t* chest_cfg, mi355_chest_dl_res_t* chest,
+                             uint8_t* const* payloads, uint32_t njobs, mi355_pdsch_res_t* res, void* stream)
+{
+  if (!q || !pool || !res || !chest || (njobs && (!sfjobs || !sfs || !cfgs || !payloads)))
+    return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t s    = stream ? (hipStream_t)stream : q->own;
+  size_t      used = 0;
+  int         r    = ofdm_run(q, sfjobs, njobs, s, &used);
+  if (r) return r;
+  float *d_out = nullptr, *d_noise = nullptr;
+  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise))) return r;
+  // the PDSCH jobs are planned on the host while the GPU demodulates and estimates
+  std::vector<mi355_pdsch_job_t> jobs(njobs);
+  for (uint32_t i = 0; i < njobs; i++) {
+    mi355_pdsch_job_t& j = jobs[i];
+    memset(&j, 0, sizeof(j));
+    j.sf  = sfs[i];
+    j.cfg = cfgs[i];
+    for (uint32_t a = 0; a < q->nof_rx; a++) {
+      j.sf_symbols[a] = sfjobs[i].sf_symbols[a];
+      for (uint32_t p = 0; p < q->cell.nof_ports; p++) j.ce[p][a] = sfjobs[i].ce[p][a];
+    }
+    j.payload[0] = payloads[2 * i];
+    j.payload[1] = payloads[2 * i + 1];
+  }
+  if ((r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), njobs, res, s, d_noise))) return r;
+  return chest_finish(q, chest_cfg, d_out, njobs, chest, s);
+}
 
 int mi355_ue_dl_decode_pdsch_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, const mi355_dl_sf_job_t* sfjobs,
                                    const mi355_dl_sf_cfg_t* sfs, const mi355_pdsch_cfg_t* cfgs,

@@ -60,6 +60,12 @@ def _declare():
                                                         C.POINTER(ChestRes), vp]
     L.mi355_ue_dl_pdsch.restype = vp
     L.mi355_ue_dl_pdsch.argtypes = [vp]
+    from .pdsch import DlSfCfg, PdschCfg, PdschRes
+    L.mi355_ue_dl_decode_pdsch_batch.argtypes = [vp, vp, C.POINTER(DlSfJob), C.POINTER(DlSfCfg), C.POINTER(PdschCfg),
+                                                 C.POINTER(ChestRes), C.POINTER(vp), u32, C.POINTER(PdschRes), vp]
+    L.mi355_ue_dl_decode_batch.argtypes = [vp, vp, C.POINTER(DlSfJob), C.POINTER(DlSfCfg), C.POINTER(PdschCfg),
+                                           C.POINTER(ChestCfg), C.POINTER(ChestRes), C.POINTER(vp), u32,
+                                           C.POINTER(PdschRes), vp]
     L._ue_dl_declared = True
     return L
 
@@ -99,6 +105,28 @@ class UeDl:
         check(self.L.mi355_ue_dl_decode_fft_estimate_batch(self.h, arr, len(jobs), C.byref(cfg), res, None),
               "decode_fft_estimate")
         return res
+
+    def decode_pdsch(self, pool, jobs, sfs, cfgs, chest, payloads):
+        """mi355_ue_dl_decode_pdsch_batch; payloads: 2 device pointers per job."""
+        from .pdsch import DlSfCfg, PdschCfg, PdschRes
+        n = len(jobs)
+        res = (PdschRes * (2 * n))()
+        pays = (C.c_void_p * (2 * n))(*payloads)
+        check(self.L.mi355_ue_dl_decode_pdsch_batch(self.h, pool.h, (DlSfJob * n)(*jobs), (DlSfCfg * n)(*sfs),
+                                                    (PdschCfg * n)(*cfgs), chest, pays, n, res, None), "decode_pdsch")
+        return res
+
+    def decode(self, pool, jobs, sfs, cfgs, cfg: ChestCfg, payloads):
+        """mi355_ue_dl_decode_batch (fft + estimate + PDSCH in one call): returns (chest res, PDSCH res)."""
+        from .pdsch import DlSfCfg, PdschCfg, PdschRes
+        n = len(jobs)
+        res = (PdschRes * (2 * n))()
+        chest = (ChestRes * n)()
+        pays = (C.c_void_p * (2 * n))(*payloads)
+        check(self.L.mi355_ue_dl_decode_batch(self.h, pool.h, (DlSfJob * n)(*jobs), (DlSfCfg * n)(*sfs),
+                                              (PdschCfg * n)(*cfgs), C.byref(cfg), chest, pays, n, res, None),
+              "ue_dl_decode_batch")
+        return chest, res
 
     def close(self):
         if getattr(self, "h", None):

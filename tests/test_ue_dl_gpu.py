@@ -130,3 +130,42 @@ def test_ue_dl_end_to_end():
             e_g = ue.pdsch.stage(0, t, nre, nre * cfg.qm[t])[2]
             diff = np.abs(e_g.astype(np.int32) - e_o[t].astype(np.int32))
             assert diff.max() <= 2 and (diff > 0).mean() < 1e-3, (k, t, diff.max(), (diff > 0).mean())
+
+
+def test_fused_decode_matches_two_step():
+    """mi355_ue_dl_decode_batch (noise kept on the device, no host round trip) == decode_fft_estimate followed
+    by decode_pdsch: same chest results, CRCs, payloads and LLRs, over a batch mixing subframes."""
+    rng = np.random.default_rng(5)
+    cfg0 = E2E[1]
+    subs = []
+    for sf in (1, 4, 0):
+        cfg = pc.Cfg(**{**cfg0.__dict__, "sf_idx": sf})
+        iq, payload, _h, _s2 = uc.synth_iq(cfg, rng, snr_db=34, channel="cross")
+        subs.append((cfg, iq, payload))
+    outs = []
+    for fused in (False, True):
+        ue = UeDl(cell_of(cfg0), 2)
+        ds = [DevIqSubframe(c, iq, softbuffers=(2 * k, 2 * k + 1)) for k, (c, iq, _) in enumerate(subs)]
+        pool = SoftbufferPool(6, max_cb=16)
+        jobs = [d.sfjob for d in ds]
+        sfs = [d.job.sf for d in ds]
+        cfgs = [d.job.cfg for d in ds]
+        pays = [p for d in ds for p in (d.job.payload[0], d.job.payload[1])]
+        if fused:
+            chest, res = ue.decode(pool, jobs, sfs, cfgs, default_chest_cfg(), pays)
+        else:
+            chest = ue.fft_estimate(jobs, default_chest_cfg())
+            res = ue.decode_pdsch(pool, jobs, sfs, cfgs, chest, pays)
+        nre = ds[0].job.cfg.grant.nof_re
+        e = [ue.pdsch.stage(k, t, ds[k].job.cfg.grant.nof_re, ds[k].job.cfg.grant.nof_re * 8)[2]
+             for k in range(3) for t in range(2)]
+        outs.append(([chest[k].noise_estimate for k in range(3)], [(r.crc, r.avg_iterations_block) for r in res],
+                     [d.payload_bytes(t)[: 97896 // 8] for d in ds for t in range(2)], e))
+        for k, (c, _, payload) in enumerate(subs):
+            for t in range(2):
+                assert res[2 * k + t].crc
+                np.testing.assert_array_equal(ds[k].payload_bytes(t)[: 97896 // 8], payload[t])
+    assert outs[0][0] == outs[1][0]
+    assert outs[0][1] == outs[1][1]
+    for a, b in zip(outs[0][3], outs[1][3]):
+        np.testing.assert_array_equal(a, b)
