@@ -20,6 +20,9 @@ struct CbDesc {      // one code block of one transport block
 
 struct TbDesc {
   uint32_t tbs, C, C1, K1, K2, slot0, invalid;
+  uint32_t Qm, nof_e_bits, rv;
+  uint32_t cb_base[2]; // index of the TB's first K1 / K2 code block in the call's (K-grouped) CB arrays
+  uint64_t e_off;      // element offset of the TB's LLRs in the e_bits buffer
   uint64_t data_off;
 };
 
@@ -69,6 +72,13 @@ struct DlschTbArgs {
   uint8_t*      sb_data;
   int32_t*        ret;
   const CrcTable* crc24a;
+  // code-block arrays of the call, expanded by the prologue from the TB descriptors
+  CbDesc*   desc;
+  uint32_t* slot;
+  uint32_t* its;
+  uint8_t*  done;
+  uint32_t* running; // running flag of half-iteration 0
+  float*    avg;     // per TB: mean half-iterations over its code blocks (epilogue)
 };
 
 struct DlschResetArgs {
@@ -82,7 +92,5 @@ hipError_t dlsch_launch_check(const DlschCheckArgs& a, hipStream_t s);
 hipError_t dlsch_launch_prologue(const DlschTbArgs& a, hipStream_t s);
 hipError_t dlsch_launch_epilogue(const DlschTbArgs& a, hipStream_t s);
 hipError_t dlsch_launch_reset(const DlschResetArgs& a, hipStream_t s);
-hipError_t dlsch_launch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc, int n, uint32_t* remaining,
-                                  hipStream_t s);
 
 } // namespace mi355

@@ -195,25 +195,53 @@ __global__ __launch_bounds__(1024) void dlsch_cb_check(DlschCheckArgs a)
 
 // ---------------------------------------------------------------------------- TB prologue / epilogue
 
-// decode_tb (sch.c:532-535) zeroes the 3 TB-CRC bytes; decode_tb_cb (:476-484) restores the CBs that
-// passed in an earlier transmission from the softbuffer.
+// One wave per TB.  Expands the TB into its code-block descriptors (sch.c:391-401 rp / n_e with the reference's
+// '>' quirk; K1 for cb < C1, sch.c:387), marks CBs decoded in an earlier transmission as done (sch.c:385) and
+// restores their bytes from the softbuffer (decode_tb_cb :476-484), zeroes the 3 TB-CRC bytes (decode_tb
+// :532-535) and raises the half-iteration-0 running flag when any CB is left to decode.
 __global__ __launch_bounds__(256) void dlsch_tb_prologue(DlschTbArgs a)
 {
+  __shared__ uint32_t todo_any;
+  if (threadIdx.x == 0) todo_any = 0;
+  __syncthreads();
   const int t    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  if (t >= a.ntb) return;
-  const TbDesc& tb = a.tb[t];
-  if (tb.C == 0) return;
-  uint8_t* data = a.data + tb.data_off;
-  if (lane < 3) data[tb.tbs / 8 + lane] = 0;
-  for (uint32_t c = 0; c < tb.C; c++) {
-    const uint32_t slot = tb.slot0 + c;
-    if (!a.sb_crc[slot]) continue;
-    const uint32_t K    = c < tb.C1 ? tb.K1 : tb.K2;
-    const uint32_t rlen = tb.C == 1 ? K : K - 24;
-    const uint32_t o    = c * rlen / 8; // sch.c indexes with the CURRENT CB's rlen (cb_idx * rlen / 8)
-    for (uint32_t i = lane; i < rlen / 8; i += 64) data[o + i] = a.sb_data[(size_t)slot * 768 + i];
+  if (t < a.ntb && a.tb[t].C != 0) {
+    const TbDesc&  tb    = a.tb[t];
+    const uint32_t Gp    = tb.nof_e_bits / tb.Qm, gamma = Gp % tb.C, n_e = tb.Qm * (Gp / tb.C);
+    uint8_t*       data  = a.data + tb.data_off;
+    bool           todo  = false;
+    if (lane < 3) data[tb.tbs / 8 + lane] = 0;
+    for (uint32_t c = lane; c < tb.C; c += 64) {
+      const uint32_t K    = c < tb.C1 ? tb.K1 : tb.K2;
+      const uint32_t rlen = tb.C == 1 ? K : K - 24;
+      uint32_t       rp = c * n_e, n_e2 = n_e;
+      if (c > tb.C - gamma) {
+        n_e2 = n_e + tb.Qm;
+        rp   = (tb.C - gamma) * n_e + (c - (tb.C - gamma)) * n_e2;
+      }
+      const uint32_t g    = c < tb.C1 ? tb.cb_base[0] + c : tb.cb_base[1] + (c - tb.C1);
+      const uint32_t slot = tb.slot0 + c;
+      a.desc[g]           = CbDesc{(uint32_t)t, c, tb.C, rlen, rp, n_e2, tb.rv, slot, tb.e_off, tb.data_off};
+      a.slot[g]           = slot;
+      a.its[g]            = 0;
+      const bool prior    = a.sb_crc[slot] != 0;
+      a.done[g]           = prior ? 3 : 0;
+      todo |= !prior;
+    }
+    if (todo) todo_any = 1;
+    // restore CBs that passed before (sch.c indexes with the CURRENT CB's rlen: cb_idx * rlen / 8)
+    for (uint32_t c = 0; c < tb.C; c++) {
+      const uint32_t slot = tb.slot0 + c;
+      if (!a.sb_crc[slot]) continue;
+      const uint32_t K    = c < tb.C1 ? tb.K1 : tb.K2;
+      const uint32_t rlen = tb.C == 1 ? K : K - 24;
+      const uint32_t o    = c * rlen / 8;
+      for (uint32_t i = lane; i < rlen / 8; i += 64) data[o + i] = a.sb_data[(size_t)slot * 768 + i];
+    }
   }
+  __syncthreads();
+  if (threadIdx.x == 0 && todo_any) flag_set(a.running);
 }
 
 // sch.c:488-500 + decode_tb :537-559; one workgroup per TB
@@ -223,6 +251,11 @@ __global__ __launch_bounds__(256) void dlsch_tb_epilogue(DlschTbArgs a)
   const int tid = threadIdx.x;
   if (t >= a.ntb) return;
   const TbDesc& tb = a.tb[t];
+  if (tid == 0) { // srslte_pdsch_res_t.avg_iterations_block (sch.c:451-453): mean over the TB's code blocks
+    double sum = 0.0;
+    for (uint32_t c = 0; c < tb.C; c++) sum += a.its[c < tb.C1 ? tb.cb_base[0] + c : tb.cb_base[1] + (c - tb.C1)];
+    a.avg[t] = tb.C ? (float)(sum / tb.C) : 0.f;
+  }
   if (tb.C == 0) {
     if (tid == 0) a.ret[t] = tb.invalid ? -2 : 0;
     return;
@@ -261,30 +294,6 @@ __global__ __launch_bounds__(256) void dlsch_sb_reset(DlschResetArgs a)
   a.sb_crc[a.slot0 + g] = 0;
 }
 
-// CBs whose CRC passed in an earlier transmission start finished (sch.c:385)
-__global__ __launch_bounds__(256) void dlsch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc,
-                                                        int n, uint32_t* running)
-{
-  __shared__ uint32_t any;
-  if (threadIdx.x == 0) any = 0;
-  __syncthreads();
-  const int  b    = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool todo = b < n && !sb_crc[slot[b]];
-  if (b < n) done[b] = todo ? 0 : 3;
-  if (todo) any = 1;
-  __syncthreads();
-  if (threadIdx.x == 0 && any) flag_set(running);
-}
-
-hipError_t dlsch_launch_init_done(uint8_t* done, const uint32_t* slot, const uint8_t* sb_crc, int n, uint32_t* remaining,
-                                  hipStream_t s)
-{
-  hipLaunchKernelGGL(dlsch_init_done, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, done, slot, sb_crc, n,
-                     remaining);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------- launchers
 hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s)
 {
   if (a.ncb <= 0) return hipSuccess;

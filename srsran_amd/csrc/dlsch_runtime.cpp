@@ -72,12 +72,6 @@ CrcTable make_crc_table(uint32_t poly)
   return t;
 }
 
-struct Group {
-  uint32_t             K = 0;
-  std::vector<CbDesc>  cbs;
-  std::vector<uint32_t> slots;
-};
-
 } // namespace
 
 struct mi355_dlsch {
@@ -94,6 +88,7 @@ struct mi355_dlsch {
   std::mutex mu;
   bool       prof = false;
   HostStaging stage;
+  HostStaging back; // pinned read-back of ret | avg
 };
 
 static uint32_t rm_buflen(uint32_t K) { return tdec_subblocks(K) ? 3 * (K + 32) + 12 : 3 * K + 12; }
@@ -342,14 +337,33 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   hipStream_t s = stream ? (hipStream_t)stream : q->own;
 
   // ---------------------------------------------------------------- host planning (sch.c:363-401, 503-530)
-  std::vector<TbDesc>        tbd(ntb);
-  std::map<uint32_t, Group>  groups;
+  // Per TB only: segmentation and the TB's place in the K-grouped code-block arrays; the code-block
+  // descriptors themselves are expanded on the device by the prologue.
+  std::vector<TbDesc>                        tbd(ntb);
+  std::vector<std::pair<uint32_t, uint32_t>> kcount; // (K, code blocks) in first-seen order; few distinct K
+  std::vector<uint32_t>                      rvmask; // per group: redundancy versions present
+  auto group_of = [&](uint32_t K) {
+    for (uint32_t i = 0; i < kcount.size(); i++)
+      if (kcount[i].first == K) return i;
+    kcount.push_back({K, 0u});
+    rvmask.push_back(0u);
+    return (uint32_t)kcount.size() - 1;
+  };
+  std::vector<uint8_t> grp(2 * ntb, 0);
+  uint32_t             seg_tbs = UINT32_MAX;
+  CbSegm               seg{};
+  int                  seg_err = 0;
   for (uint32_t t = 0; t < ntb; t++) {
     const mi355_dlsch_tb_t& in = tbs[t];
     TbDesc&                 d  = tbd[t];
-    d                          = TbDesc{in.tbs, 0, 0, 0, 0, 0, 0, in.data_offset};
-    CbSegm seg;
-    if (in.softbuffer >= pool->nof_sb || in.rv > 3 || in.Qm == 0 || cbsegm(in.tbs, &seg)) {
+    d                          = TbDesc{};
+    d.tbs                      = in.tbs;
+    d.data_off                 = in.data_offset;
+    if (in.tbs != seg_tbs) {
+      seg_err = cbsegm(in.tbs, &seg);
+      seg_tbs = in.tbs;
+    }
+    if (in.softbuffer >= pool->nof_sb || in.rv > 3 || in.Qm == 0 || seg_err) {
       d.invalid = 1;
       continue;
     }
@@ -358,36 +372,47 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
       d.invalid = 1;
       continue;
     }
-    d.C     = seg.C;
-    d.C1    = seg.C1;
-    d.K1    = seg.K1;
-    d.K2    = seg.K2;
-    d.slot0 = in.softbuffer * pool->max_cb;
-    const uint32_t Gp = in.nof_e_bits / in.Qm, gamma = Gp % seg.C, n_e = in.Qm * (Gp / seg.C);
-    for (uint32_t cb = 0; cb < seg.C; cb++) {
-      const uint32_t K = cb < seg.C1 ? seg.K1 : seg.K2; // sch.c:387
-      uint32_t       rp = cb * n_e, n_e2 = n_e;
-      if (cb > seg.C - gamma) { // sch.c:396-399 (note: '>', the reference's off-by-one)
-        n_e2 = n_e + in.Qm;
-        rp   = (seg.C - gamma) * n_e + (cb - (seg.C - gamma)) * n_e2;
-      }
-      Group& g = groups[K];
-      g.K      = K;
-      g.cbs.push_back(CbDesc{t, cb, seg.C, seg.C == 1 ? K : K - 24, rp, n_e2, in.rv, d.slot0 + cb, in.e_offset,
-                             in.data_offset});
-      g.slots.push_back(d.slot0 + cb);
+    d.C          = seg.C;
+    d.C1         = seg.C1;
+    d.K1         = seg.K1;
+    d.K2         = seg.K2;
+    d.slot0      = in.softbuffer * pool->max_cb;
+    d.Qm         = in.Qm;
+    d.nof_e_bits = in.nof_e_bits;
+    d.rv         = in.rv;
+    d.e_off      = in.e_offset;
+    if (seg.C1) {
+      const uint32_t g = group_of(seg.K1);
+      grp[2 * t]       = (uint8_t)g;
+      d.cb_base[0]     = kcount[g].second;
+      kcount[g].second += seg.C1;
+      rvmask[g] |= 1u << in.rv;
     }
+    if (seg.C > seg.C1) {
+      const uint32_t g = group_of(seg.K2);
+      grp[2 * t + 1]   = (uint8_t)g;
+      d.cb_base[1]     = kcount[g].second;
+      kcount[g].second += seg.C - seg.C1;
+      rvmask[g] |= 1u << in.rv;
+    }
+  }
+  std::vector<uint32_t> goff(kcount.size());
+  size_t                total_cb = 0, dec_bytes = 0;
+  for (size_t g = 0; g < kcount.size(); g++) {
+    goff[g] = (uint32_t)total_cb;
+    total_cb += kcount[g].second;
+    dec_bytes += (size_t)kcount[g].second * (kcount[g].first / 8);
+  }
+  for (uint32_t t = 0; t < ntb; t++) {
+    if (!tbd[t].C) continue;
+    tbd[t].cb_base[0] += goff[grp[2 * t]];
+    tbd[t].cb_base[1] += goff[grp[2 * t + 1]];
   }
 
   // ---------------------------------------------------------------- device scratch
-  size_t total_cb = 0, dec_bytes = 0;
-  for (auto& kv : groups) {
-    total_cb += kv.second.cbs.size();
-    dec_bytes += kv.second.cbs.size() * (kv.first / 8);
-  }
   auto rnd = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t need = rnd(ntb * sizeof(TbDesc)) + rnd(total_cb * sizeof(CbDesc)) + rnd(total_cb * 4) +
-                      rnd(total_cb) + rnd(total_cb * 4) + rnd(dec_bytes) + rnd(ntb * 4) + rnd(4 * (q->max_its + 1));
+  const size_t need = rnd(ntb * sizeof(TbDesc)) + rnd(4 * (q->max_its + 1)) + rnd(total_cb * sizeof(CbDesc)) +
+                      3 * rnd(total_cb * 4) + rnd(total_cb) + rnd(dec_bytes) + 2 * rnd(ntb * 4);
   char* base = nullptr;
   int   r    = scratch(q, need, &base);
   if (r) return r;
@@ -397,34 +422,25 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
     p += rnd(b);
     return c;
   };
-  // staged (one pinned upload): tb | cb | slot | its (zeros) | running flags (zeros)
-  auto*     d_tb    = (TbDesc*)carve(ntb * sizeof(TbDesc));
-  auto*     d_cb    = (CbDesc*)carve(total_cb * sizeof(CbDesc));
-  auto*     d_slot  = (uint32_t*)carve(total_cb * 4);
-  auto*     d_its   = (uint32_t*)carve(total_cb * 4);
-  auto*     d_run   = (uint32_t*)carve(4 * (q->max_its + 1)); // running flags per half-iteration
-  const size_t staged = (size_t)(p - base);
-  auto*     d_done  = (uint8_t*)carve(total_cb);
-  auto*     d_dec   = (uint8_t*)carve(dec_bytes);
-  auto*     d_ret   = (int32_t*)carve(ntb * 4);
+  // staged (one pinned upload): tb | running flags (zeros)
+  auto*        d_tb    = (TbDesc*)carve(ntb * sizeof(TbDesc));
+  auto*        d_run   = (uint32_t*)carve(4 * (q->max_its + 1)); // running flags per half-iteration
+  const size_t staged  = (size_t)(p - base);
+  auto*        d_cb    = (CbDesc*)carve(total_cb * sizeof(CbDesc));
+  auto*        d_slot  = (uint32_t*)carve(total_cb * 4);
+  auto*        d_its   = (uint32_t*)carve(total_cb * 4);
+  auto*        d_done  = (uint8_t*)carve(total_cb);
+  auto*        d_dec   = (uint8_t*)carve(dec_bytes);
+  auto*        d_ret   = (int32_t*)carve(ntb * 4); // ret | avg read back with one copy
+  auto*        d_avg   = (float*)carve(ntb * 4);
 
   CHECK_HIP(q->stage.reserve(staged));
   q->stage.put(tbd.data(), ntb * sizeof(TbDesc));
-  std::vector<CbDesc>   all_cb;
-  std::vector<uint32_t> all_slot;
-  all_cb.reserve(total_cb);
-  all_slot.reserve(total_cb);
-  for (auto& kv : groups) {
-    all_cb.insert(all_cb.end(), kv.second.cbs.begin(), kv.second.cbs.end());
-    all_slot.insert(all_slot.end(), kv.second.slots.begin(), kv.second.slots.end());
-  }
-  q->stage.put(all_cb.data(), total_cb * sizeof(CbDesc));
-  q->stage.put(all_slot.data(), total_cb * 4);
-  q->stage.zeros(total_cb * 4);
   q->stage.zeros(4 * (q->max_its + 1));
   CHECK_HIP(hipMemcpyAsync(base, q->stage.host, q->stage.used, hipMemcpyHostToDevice, s));
 
-  DlschTbArgs ta{d_tb, (int)ntb, d_data, pool->cb_crc, pool->data, d_ret, &q->crc[0]};
+  DlschTbArgs ta{d_tb,  (int)ntb, d_data, pool->cb_crc, pool->data, d_ret, &q->crc[0],
+                 d_cb,  d_slot,   d_its,  d_done,       d_run,      d_avg};
   CHECK_HIP(dlsch_launch_prologue(ta, s));
 
   // ---------------------------------------------------------------- per-K groups
@@ -436,18 +452,16 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   };
   std::vector<Live> live;
   size_t            off = 0, doff = 0;
-  for (auto& kv : groups) {
-    const uint32_t K = kv.first, n = (uint32_t)kv.second.cbs.size();
+  for (size_t gi = 0; gi < kcount.size(); gi++) {
+    const uint32_t K = kcount[gi].first, n = kcount[gi].second;
     DlschRmArgs    ra{};
     ra.desc = d_cb + off;
     ra.ncb  = (int)n;
     ra.N      = 3 * K + 12;
     ra.buflen = rm_buflen(K);
     for (uint32_t rv = 0; rv < 4; rv++) {
-      bool used = false;
-      for (auto& c : kv.second.cbs) used |= c.rv == rv;
       ra.inv[rv] = nullptr;
-      if (used && (r = rm_table(q, K, rv, &ra.inv[rv]))) return r;
+      if (((rvmask[gi] >> rv) & 1u) && (r = rm_table(q, K, rv, &ra.inv[rv]))) return r;
     }
     ra.fresh     = pool->fresh;
     ra.e         = d_e_bits;
@@ -468,9 +482,6 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
     off += n;
     doff += (size_t)n * (K / 8);
   }
-  // CBs already decoded in an earlier transmission start as done (before the rate matcher adds into them
-  // this is the same flag it tested)
-  if (total_cb) CHECK_HIP(dlsch_launch_init_done(d_done, d_slot, pool->cb_crc, (int)total_cb, d_run, s));
 
   for (uint32_t h = 0; h < q->max_its; h++) {
     for (auto& lv : live) {
@@ -484,18 +495,14 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   }
   CHECK_HIP(dlsch_launch_epilogue(ta, s));
 
-  std::vector<uint32_t> its(total_cb);
-  CHECK_HIP(hipMemcpyAsync(ret, d_ret, ntb * 4, hipMemcpyDeviceToHost, s));
-  if (total_cb) CHECK_HIP(hipMemcpyAsync(its.data(), d_its, total_cb * 4, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(q->back.reserve(rnd(ntb * 4) + ntb * 4));
+  CHECK_HIP(hipMemcpyAsync(q->back.host, d_ret, rnd(ntb * 4) + ntb * 4, hipMemcpyDeviceToHost, s));
   CHECK_HIP(hipStreamSynchronize(s));
+  memcpy(ret, q->back.host, ntb * 4);
   for (uint32_t t = 0; t < ntb; t++) {
     if (tbd[t].invalid) ret[t] = MI355_ERROR_INVALID_INPUTS;
   }
-  if (avg_iterations) {
-    std::vector<double> sum(ntb, 0.0);
-    for (size_t i = 0; i < total_cb; i++) sum[all_cb[i].tb] += its[i];
-    for (uint32_t t = 0; t < ntb; t++) avg_iterations[t] = tbd[t].C ? (float)(sum[t] / tbd[t].C) : 0.f;
-  }
+  if (avg_iterations) memcpy(avg_iterations, q->back.host + rnd(ntb * 4), ntb * 4);
   return MI355_SUCCESS;
 }
 

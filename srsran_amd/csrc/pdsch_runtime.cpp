@@ -168,6 +168,9 @@ struct mi355_pdsch {
   uint32_t                             max_its = 10; // SRSLTE_PDSCH_MAX_TDEC_ITERS
   uint32_t*                            gold   = nullptr;
   std::map<std::string, std::pair<uint16_t*, uint32_t>> maps; // extraction maps in HBM + RE count
+  const uint16_t*                      last_map = nullptr; // the previous lookup (key below)
+  uint32_t                             last_map_n = 0, last_map_hdr[4]{};
+  uint8_t                              last_map_prb[2][MI355_MAX_PRB]{};
   std::map<uint32_t, uint32_t*>        scr;  // packed descrambling sequences per c_init (HBM)
   char*                                scratch = nullptr;
   size_t                               scratch_cap = 0;
@@ -198,6 +201,15 @@ static int get_scratch(mi355_pdsch_t* q, size_t bytes, char** p)
 static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi, uint32_t sf, const uint16_t** out,
                    uint32_t* count)
 {
+  // consecutive jobs of a batch usually share the allocation: compare with the previous lookup first
+  const uint32_t np = q->cell.nof_prb;
+  if (q->last_map && q->last_map_hdr[0] == cfi && q->last_map_hdr[1] == sf && q->last_map_hdr[2] == g.nof_symb_slot[0] &&
+      q->last_map_hdr[3] == g.nof_symb_slot[1] && !memcmp(q->last_map_prb[0], g.prb_idx[0], np) &&
+      !memcmp(q->last_map_prb[1], g.prb_idx[1], np)) {
+    *out   = q->last_map;
+    *count = q->last_map_n;
+    return MI355_SUCCESS;
+  }
   std::string key;
   key.reserve(16 + 2 * q->cell.nof_prb);
   const uint32_t hdr[4] = {cfi, sf, g.nof_symb_slot[0], g.nof_symb_slot[1]};
@@ -210,6 +222,7 @@ static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi,
       CHECK_HIP(hipDeviceSynchronize());
       for (auto& kv : q->maps) (void)hipFree(kv.second.first);
       q->maps.clear();
+      q->last_map = nullptr;
     }
     std::vector<uint16_t> idx;
     idx.reserve(14 * 12 * q->cell.nof_prb);
@@ -222,6 +235,12 @@ static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi,
   }
   *out   = it->second.first;
   *count = it->second.second;
+  q->last_map       = it->second.first;
+  q->last_map_n     = it->second.second;
+  const uint32_t h[4] = {cfi, sf, g.nof_symb_slot[0], g.nof_symb_slot[1]};
+  memcpy(q->last_map_hdr, h, sizeof(h));
+  memcpy(q->last_map_prb[0], g.prb_idx[0], np);
+  memcpy(q->last_map_prb[1], g.prb_idx[1], np);
   return MI355_SUCCESS;
 }
 
@@ -318,7 +337,11 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
     for (auto& kv : q->scr) (void)hipFree(kv.second);
     q->scr.clear();
   }
-  uint32_t nblkA = 0, nblkB = 0;
+  uint32_t  nblkA = 0, nblkB = 0;
+  uint32_t  last_ci  = 0;
+  const uint32_t* last_scr = nullptr;
+  cws.reserve(2 * njobs);
+  startB.reserve(2 * njobs + 1);
   for (uint32_t i = 0; i < njobs; i++) {
     JobPlan& P = plans[i];
     for (uint32_t cw = 0; cw < 2; cw++) {
@@ -341,15 +364,21 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
       c.pairs      = (c.nof_re + 1) / 2;
       startB.push_back(nblkB);
       nblkB += (c.pairs + 255) / 256;
-      auto it = q->scr.find(c.c_init);
-      if (it == q->scr.end()) {
-        uint32_t* d = nullptr;
-        CHECK_HIP(hipMalloc(&d, (PDSCH_GOLD_MAX / 32) * 4));
-        it = q->scr.emplace(c.c_init, d).first;
-        new_ci.push_back(c.c_init);
-        new_dst.push_back(d);
+      if (c.c_init == last_ci && last_scr) {
+        c.scr = last_scr;
+      } else {
+        auto it = q->scr.find(c.c_init);
+        if (it == q->scr.end()) {
+          uint32_t* d = nullptr;
+          CHECK_HIP(hipMalloc(&d, (PDSCH_GOLD_MAX / 32) * 4));
+          it = q->scr.emplace(c.c_init, d).first;
+          new_ci.push_back(c.c_init);
+          new_dst.push_back(d);
+        }
+        c.scr   = it->second;
+        last_ci = c.c_init;
+        last_scr = c.scr;
       }
-      c.scr = it->second;
       cws.push_back(c);
     }
   }
@@ -522,7 +551,8 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
   }
   int r = run_frontend(q, jobs, plans, s);
   if (r) return r;
-  q->last = plans;
+  q->last.swap(plans);
+  const std::vector<JobPlan>& plan = q->last;
 
   // DL-SCH: one batch per max-iterations setting (srslte_sch_set_max_noi persists, pdsch.c:930-932)
   std::map<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>> by_its; // its -> (job, tb)
@@ -531,7 +561,7 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
     const mi355_pdsch_cfg_t& cfg = jobs[i].cfg;
     if (cfg.max_nof_iterations) q->max_its = cfg.max_nof_iterations;
     for (uint32_t t = 0; t < 2; t++) {
-      if (!plans[i].decode[t]) continue;
+      if (!plan[i].decode[t]) continue;
       const mi355_ra_tb_t& tb = cfg.grant.tb[t];
       const uint32_t       Nl = cfg.grant.nof_layers != cfg.grant.nof_tb ? 2 : 1; // sch.c:584-588
       mi355_dlsch_tb_t     d{};
@@ -540,7 +570,7 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
       d.Qm          = mod_bits(tb.mod) * Nl;
       d.rv          = tb.rv;
       d.softbuffer  = cfg.softbuffer[t];
-      d.e_offset    = plans[i].e_off[t];
+      d.e_offset    = plan[i].e_off[t];
       d.data_offset = (uint64_t)(uintptr_t)jobs[i].payload[t]; // absolute (d_data == NULL)
       by_its[q->max_its].push_back({i, t});
       tbs[q->max_its].push_back(d);

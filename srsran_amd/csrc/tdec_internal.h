@@ -25,7 +25,7 @@ struct TdecWinArgs {
   const uint32_t* dstE; // [L][NL] j' | wlo<<16 | whi<<24 : natural -> interleaved destination
   const uint32_t* dstA; // [L][NL] same, interleaved -> natural
   int             ncb, L, Lp, nseg, n, write_d;
-  uint8_t*        dec;  // optional (DEC1, L % 8 == 0): decision bytes written directly, D not written
+  uint8_t*        dec;  // optional (L % 8 == 0): decision bytes written directly, D not written
   size_t          dec_stride;
 };
 

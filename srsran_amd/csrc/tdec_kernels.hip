@@ -311,7 +311,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   const uint32_t* tab  = (dec2 ? a.dstA : a.dstE) + l;
   const int       lane0 = cbg * NL; // first lane of this code block inside the 64-lane row
   const bool      wr_bits = !dec2 && a.dec != nullptr; // fused decision bytes (DEC1: ext1 in natural order)
-  const bool      wr_d    = a.write_d && !wr_bits;
+  const bool      wr_bm   = dec2 && a.dec != nullptr;  // fused decision bytes (DEC2: app1 de-interleaved)
+  const bool      wr_d    = a.write_d && !wr_bits && !wr_bm;
+  // DEC2 decisions land at scattered natural positions (row j' of windows wlo/whi), so they are collected
+  // as a bitmap of the code block in LDS (K/8 bytes, byte order of the output) and stored at the end
+  constexpr int BMW = NSB == 16 ? 192 : 25; // u32 words per code block (K <= 6144 / K <= 800)
+  uint32_t*     bm  = nullptr;
+  if constexpr (dec2) {
+    __shared__ uint32_t bm_lds[4 * G * BMW];
+    bm = bm_lds + ((threadIdx.x >> 6) * G + cbg) * BMW;
+    if (wr_bm) {
+      for (int w = l; w < K / 32; w += NL) bm[w] = 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
 
   uint32_t cx[SEG], cy[SEG], ca[SEG] = {}, cd[SEG], cc[8];
   auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap, uint32_t* d, uint32_t* c) {
@@ -422,6 +436,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
           const v2s av = out - xin[i];
           A16[olo]     = av.x;
           A16[ohi]     = av.y;
+          if (wr_bm) { // natural bit w*L + j': byte w*L/8 + j'/8, bit 7 - j'%8 (turbodecoder_win.h:973-993)
+            const uint32_t blo = wlo * (L / 8) + (jd >> 3), bhi = whi * (L / 8) + (jd >> 3);
+            const uint32_t sh  = 7 - (jd & 7);
+            atomicOr(&bm[blo >> 2], (uint32_t)(out.x > 0) << (((blo & 3) << 3) + sh));
+            atomicOr(&bm[bhi >> 2], (uint32_t)(out.y > 0) << (((bhi & 3) << 3) + sh));
+          }
           if (wr_d) {
             D16[olo] = out.x;
             D16[ohi] = out.y;
@@ -455,6 +475,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
     }
 #pragma unroll
     for (int s = 0; s < 8; s++) cc[s] = nc[s];
+  }
+  if constexpr (dec2) {
+    if (wr_bm) { // the code block's K/8 decision bytes, 8-byte stores by its NL lanes
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      uint2* o = (uint2*)(a.dec + (size_t)cb * a.dec_stride);
+      for (int w = l; w < K / 64; w += NL) o[w] = make_uint2(bm[2 * w], bm[2 * w + 1]);
+    }
   }
 }
 

@@ -276,9 +276,10 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
     auto*        D   = (uint32_t*)carve(arr);
     auto*        CK  = (uint32_t*)carve((size_t)g.ngrp * g.nseg * 8 * 64 * 4);
 
-    // the last half-iteration is DEC1 (even index): its decisions (ext1, natural order) are packed into bytes by
-    // the MAP kernel itself when the windows are byte aligned, which saves the D array and the decide pass
-    const bool fuse = (h1 - 1) % 2 == 0 && g.L % 8 == 0;
+    // the decisions of the last half-iteration are packed into bytes by the MAP kernel itself when the windows
+    // are byte aligned (DEC1: in registers, natural order; DEC2: an LDS bitmap), which saves the D array and
+    // the decide pass
+    const bool fuse = g.L % 8 == 0 && out_stride % 8 == 0 && (uintptr_t)d_out % 8 == 0;
     for (uint32_t h = h0; h < h1; h++) {
       TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, rq.remaining, A1, E, D, CK, t->dstE, t->dstA,
                      (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == h1,
