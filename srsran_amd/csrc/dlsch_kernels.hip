@@ -17,54 +17,82 @@ namespace mi355 {
 // (sums or zeros) instead of read, which is srslte_softbuffer_rx_reset + the first accumulation in one pass.
 // One workgroup per code block: the CB's LLRs are folded modulo N into LDS (coalesced reads, wrap-around
 // sums for E > N), then the decoder buffer is written in order from LDS gathers.
-constexpr uint32_t RM_LDS = 3 * 6144 + 12; // N of the largest code block
+constexpr uint32_t RM_LDS     = 3 * 6144 + 12; // N of the largest code block
+constexpr uint32_t RM_THREADS = 1024;
+constexpr int      RM_IT      = (3 * (6144 + 32) + 12 + 2 * RM_THREADS - 1) / (2 * RM_THREADS); // buffer pairs per thread
+constexpr int      RM_E_IT    = (RM_LDS + 2 * RM_THREADS - 1) / (2 * RM_THREADS);             // LLR pairs per thread
 
-__global__ __launch_bounds__(512) void dlsch_rm_rx(DlschRmArgs a)
+__device__ __forceinline__ uint32_t add_pairs(uint32_t a, uint32_t b) // two wrapping int16 additions
 {
-  __shared__ uint16_t acc[RM_LDS + 4];
-  const CbDesc& d = a.desc[blockIdx.x];
+  return ((a + b) & 0xffffu) | (((a >> 16) + (b >> 16)) << 16);
+}
+
+// Every load of a thread is issued up front (inverse table, LLRs, old softbuffer words: fully unrolled,
+// independent of one another), so a block pays the memory latency about twice instead of once per
+// loop trip.  Qm is even, so n_e, rp and N are even and the LLRs are handled as int16 pairs.
+__global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
+{
+  __shared__ uint32_t acc32[RM_LDS / 2 + 2];
+  const uint16_t* acc = (const uint16_t*)acc32;
+  const CbDesc&   d   = a.desc[blockIdx.x];
   if (a.sb_crc[d.slot]) return; // CB already decoded in an earlier transmission (sch.c:385)
-  const uint32_t  N = a.N, tid = threadIdx.x, nt = blockDim.x;
-  const int16_t*  e = a.e + d.e_off + d.rp;
-  const uint32_t  n_e = d.n_e, first = min(n_e, N);
-  // pass 0: the first wrap initialises (positions >= n_e get 0), later wraps accumulate; 4 loads in flight
-  for (uint32_t r = tid; r < N; r += 4 * nt) {
-    uint16_t v[4];
+  const uint32_t  N = a.N, tid = threadIdx.x;
+  const uint32_t  n_e = d.n_e, first2 = min(n_e, N) / 2, N2 = N / 2;
+  const uint32_t* inv32 = (const uint32_t*)a.inv[d.rv]; // 4-byte aligned (buflen even)
+  const uint32_t  pairs = a.buflen / 2;
+  const bool      fresh = a.fresh[d.slot] != 0;
+  uint32_t*       sb    = (uint32_t*)(a.sb + (size_t)d.slot * a.sb_stride);
+
+  uint32_t iv[RM_IT];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t rr = r + k * nt;
-      v[k]              = rr < first ? (uint16_t)e[rr] : (uint16_t)0;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (r + k * nt < N) acc[r + k * nt] = v[k];
+  for (int k = 0; k < RM_IT; k++) {
+    const uint32_t jp = tid + k * RM_THREADS;
+    iv[k]             = jp < pairs ? inv32[jp] : 0xffffffffu;
   }
+  // pass 0: the first wrap initialises (positions >= n_e get 0)
+  const int16_t* e   = a.e + d.e_off + d.rp;
+  const bool     al4 = ((uintptr_t)e & 3) == 0;
+  uint32_t       ev[RM_E_IT];
+#pragma unroll
+  for (int k = 0; k < RM_E_IT; k++) {
+    const uint32_t r2 = tid + k * RM_THREADS;
+    if (r2 < first2) {
+      ev[k] = al4 ? ((const uint32_t*)e)[r2]
+                  : ((uint32_t)(uint16_t)e[2 * r2] | ((uint32_t)(uint16_t)e[2 * r2 + 1] << 16));
+    } else {
+      ev[k] = 0;
+    }
+  }
+  uint32_t old[RM_IT];
+#pragma unroll
+  for (int k = 0; k < RM_IT; k++) {
+    const uint32_t jp = tid + k * RM_THREADS;
+    old[k]            = (!fresh && jp < pairs) ? sb[jp] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < RM_E_IT; k++) {
+    const uint32_t r2 = tid + k * RM_THREADS;
+    if (r2 < N2) acc32[r2] = ev[k];
+  }
+  // later wraps (E > N) accumulate
   for (uint32_t base = N; base < n_e; base += N) {
     __syncthreads();
-    for (uint32_t r = tid; r < N && base + r < n_e; r += nt) acc[r] = (uint16_t)(acc[r] + (uint16_t)e[base + r]);
+    const uint32_t lim2 = min(N, n_e - base) / 2;
+    for (uint32_t r2 = tid; r2 < lim2; r2 += RM_THREADS) {
+      const uint32_t v = al4 ? ((const uint32_t*)(e + base))[r2]
+                             : ((uint32_t)(uint16_t)e[base + 2 * r2] | ((uint32_t)(uint16_t)e[base + 2 * r2 + 1] << 16));
+      acc32[r2] = add_pairs(acc32[r2], v);
+    }
   }
   __syncthreads();
-  const bool      fresh = a.fresh[d.slot] != 0;
-  const uint16_t* inv   = a.inv[d.rv];
-  uint32_t*       sb    = (uint32_t*)(a.sb + (size_t)d.slot * a.sb_stride);
-  const uint32_t  pairs = a.buflen / 2;
-  for (uint32_t j0 = tid; j0 < pairs; j0 += 2 * nt) {
-    uint32_t iv[2], old[2] = {0u, 0u};
 #pragma unroll
-    for (int k = 0; k < 2; k++) { // inv is 4-byte aligned (buflen even)
-      const uint32_t jp = j0 + k * nt;
-      iv[k]             = jp < pairs ? ((const uint32_t*)inv)[jp] : 0xffffffffu;
-      if (!fresh && jp < pairs) old[k] = sb[jp];
-    }
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const uint32_t jp = j0 + k * nt;
-      const uint32_t r0 = iv[k] & 0xffffu, r1 = iv[k] >> 16;
-      const bool     h0 = r0 != RM_NONE && r0 < n_e, h1 = r1 != RM_NONE && r1 < n_e;
-      if (jp >= pairs || (!fresh && !h0 && !h1)) continue;
-      const uint32_t s0 = h0 ? acc[r0] : 0u, s1 = h1 ? acc[r1] : 0u;
-      sb[jp]            = ((old[k] + s0) & 0xffffu) | (((old[k] >> 16) + s1) << 16);
-    }
+  for (int k = 0; k < RM_IT; k++) {
+    const uint32_t jp = tid + k * RM_THREADS;
+    const uint32_t r0 = iv[k] & 0xffffu, r1 = iv[k] >> 16;
+    const bool     h0 = r0 != RM_NONE && r0 < n_e, h1 = r1 != RM_NONE && r1 < n_e;
+    if (jp >= pairs || (!fresh && !h0 && !h1)) continue;
+    const uint32_t s0 = h0 ? acc[r0] : 0u, s1 = h1 ? acc[r1] : 0u;
+    sb[jp]            = add_pairs(old[k], s0 | (s1 << 16));
   }
 }
 
@@ -298,7 +326,7 @@ hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s)
 {
   if (a.ncb <= 0) return hipSuccess;
   if (a.N > RM_LDS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dlsch_rm_rx, dim3((unsigned)a.ncb), dim3(512), 0, s, a);
+  hipLaunchKernelGGL(dlsch_rm_rx, dim3((unsigned)a.ncb), dim3(RM_THREADS), 0, s, a);
   hipLaunchKernelGGL(dlsch_rm_consume, dim3((unsigned)((a.ncb + 255) / 256)), dim3(256), 0, s, a.desc, a.ncb, a.fresh,
                      a.sb_crc);
   return hipGetLastError();

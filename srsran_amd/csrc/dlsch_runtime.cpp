@@ -437,7 +437,7 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   CHECK_HIP(q->stage.reserve(staged));
   q->stage.put(tbd.data(), ntb * sizeof(TbDesc));
   q->stage.zeros(4 * (q->max_its + 1));
-  CHECK_HIP(hipMemcpyAsync(base, q->stage.host, q->stage.used, hipMemcpyHostToDevice, s));
+  CHECK_HIP(q->stage.upload(base, s));
 
   DlschTbArgs ta{d_tb,  (int)ntb, d_data, pool->cb_crc, pool->data, d_ret, &q->crc[0],
                  d_cb,  d_slot,   d_its,  d_done,       d_run,      d_avg};

@@ -1,7 +1,7 @@
 // srsran_amd/csrc/host_staging.h -- pinned host staging for the per-call descriptor uploads.  Descriptors are
 // packed into one page-locked buffer and sent with a single asynchronous copy (pageable copies are staged
-// synchronously by the runtime and dominate the host side of a batch call).  Calls are synchronous, so the
-// buffer is free again when the next call starts.
+// synchronously by the runtime and dominate the host side of a batch call).  The buffer is refilled only
+// after the previous upload from it has completed (event), so asynchronous callers are safe too.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -11,15 +11,25 @@
 namespace mi355 {
 
 struct HostStaging {
-  char*  host = nullptr;
-  size_t cap = 0, used = 0;
+  char*      host = nullptr;
+  size_t     cap = 0, used = 0;
+  hipEvent_t ev      = nullptr; // recorded after the last upload from this buffer
+  bool       pending = false;
 
   ~HostStaging()
   {
+    if (pending) (void)hipEventSynchronize(ev);
+    if (ev) (void)hipEventDestroy(ev);
     if (host) (void)hipHostFree(host);
   }
+  // start a new fill; waits for the previous upload from this buffer if it may still be in flight
   hipError_t reserve(size_t bytes)
   {
+    if (pending) {
+      pending      = false;
+      hipError_t e = hipEventSynchronize(ev);
+      if (e != hipSuccess) return e;
+    }
     used = 0;
     if (bytes <= cap) return hipSuccess;
     if (host) (void)hipHostFree(host);
@@ -44,6 +54,24 @@ struct HostStaging {
     if (n) memset(host + off, 0, n);
     used += (n + 255) / 256 * 256;
     return off;
+  }
+  // direct fill: pointer to the next n-byte slot
+  void* slot(size_t n)
+  {
+    void* p = host + used;
+    used += (n + 255) / 256 * 256;
+    return p;
+  }
+  // one asynchronous copy of everything put so far to dst on stream s
+  hipError_t upload(void* dst, hipStream_t s)
+  {
+    if (!used) return hipSuccess;
+    hipError_t e = hipMemcpyAsync(dst, host, used, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ev, s)) != hipSuccess) return e;
+    pending = true;
+    return hipSuccess;
   }
 };
 

@@ -34,11 +34,10 @@ struct PdschCwDev {
   uint32_t      pairs; // kernel B work items: symbol pairs
 };
 
-// Block b of a launch belongs to item i with start[i] <= b < start[i + 1] (prefix sums of blocks per item).
-hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, const uint32_t* start, uint32_t njobs, uint32_t nblk,
-                                 hipStream_t s);
+// 2-D grids: blockIdx.y = job / codeword, blockIdx.x over the largest one's work items.
+hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, uint32_t njobs, uint32_t max_units, hipStream_t s);
 hipError_t pdsch_launch_scr_pack(const uint32_t* c_init, uint32_t* const* dst, uint32_t n, const uint32_t* gold,
                                  uint32_t W, hipStream_t s);
-hipError_t pdsch_launch_llr(const PdschCwDev* cws, const uint32_t* start, uint32_t ncw, uint32_t nblk, hipStream_t s);
+hipError_t pdsch_launch_llr(const PdschCwDev* cws, uint32_t ncw, uint32_t max_pairs, hipStream_t s);
 
 } // namespace mi355

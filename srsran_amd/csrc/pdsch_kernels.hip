@@ -15,6 +15,8 @@
 // Both kernels are pure streaming: HBM-bound, no LDS.  Integer conversions emulate x86 semantics
 // (cvttss2si/cvtps2dq: out-of-range -> INT32_MIN) so LLRs are bit-exact for bit-exact symbols.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "pdsch_internal.h"
@@ -34,12 +36,21 @@ __device__ __forceinline__ cf operator*(cf a, float s) { return mk(a.re * s, a.i
 __device__ __forceinline__ cf cj(cf a) { return mk(a.re, -a.im); }
 __device__ __forceinline__ cf mulj(cf a) { return mk(-a.im, a.re); }
 __device__ __forceinline__ float abs2(cf a) { return a.re * a.re + a.im * a.im; }
-__device__ __forceinline__ cf ld(const float2* p, uint32_t i)
+// Pointers read from descriptors in memory are generic (flat) to the compiler; the kernels cast them to
+// the global address space so loads/stores are global_* (flat ones also count against lgkmcnt and serialise
+// with the scalar descriptor loads).
+#define GLB __attribute__((address_space(1)))
+typedef float    vf2 __attribute__((ext_vector_type(2)));
+typedef float    vf4 __attribute__((ext_vector_type(4)));
+typedef uint32_t vu2 __attribute__((ext_vector_type(2)));
+typedef uint32_t vu4 __attribute__((ext_vector_type(4)));
+template <class T> __device__ __forceinline__ GLB T* gptr(T* p) { return (GLB T*)p; }
+__device__ __forceinline__ cf ld(const GLB float2* p, uint32_t i)
 {
-  const float2 v = p[i];
+  const vf2 v = *(const GLB vf2*)(p + i);
   return mk(v.x, v.y);
 }
-__device__ __forceinline__ void st(float2* p, uint32_t i, cf v) { p[i] = make_float2(v.re, v.im); }
+__device__ __forceinline__ void st(GLB float2* p, uint32_t i, cf v) { *(GLB vf2*)(p + i) = (vf2){v.re, v.im}; }
 
 // srslte_mat_2x2_mmse_csi_gen (mat.c:63-110)
 __device__ __forceinline__ void mmse_2x2_csi(cf y0, cf y1, cf h00, cf h01, cf h10, cf h11, cf& x0, cf& x1,
@@ -70,40 +81,34 @@ __device__ __forceinline__ void fold_max(uint32_t* m, float v)
   uint32_t b = __float_as_uint(v);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(m, b);
-}
-
-// item owning block b: the last i with start[i] <= b (start has n + 1 entries)
-__device__ __forceinline__ uint32_t owner(const uint32_t* start, uint32_t n, uint32_t b)
-{
-  uint32_t lo = 0, hi = n; // invariant: start[lo] <= b < start[hi]
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (start[mid] <= b) lo = mid; else hi = mid;
-  }
-  return lo;
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_max(gptr(m), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 } // namespace
 
-__global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restrict__ jobs,
-                                                      const uint32_t* __restrict__ start, uint32_t njobs)
+// grid (blocks of the largest job, jobs): blockIdx.y is the job, blocks past a smaller job's work exit
+__global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restrict__ jobs)
 {
-  const uint32_t     j  = owner(start, njobs, blockIdx.x);
-  const PdschJobDev& J  = jobs[j];
-  const uint32_t     u  = (blockIdx.x - start[j]) * 256 + threadIdx.x;
-  const bool      live = u < J.units;
+  const PdschJobDev& J = jobs[blockIdx.y];
+  if (blockIdx.x * 256 >= J.units) return;
+  const uint32_t u    = blockIdx.x * 256 + threadIdx.x;
+  const bool     live = u < J.units;
   float           m0 = 0.f, m1 = 0.f; // per-thread csi contribution for the max
-  const float     noise = J.noise_dev ? *J.noise_dev : J.noise;
+  const float     noise = J.noise_dev ? *gptr(J.noise_dev) : J.noise;
+  const GLB uint16_t* map  = gptr(J.map);
+  GLB float2*         d0   = gptr(J.d[0]);
+  GLB float2*         d1   = gptr(J.d[1]);
+  GLB float*          csi0 = gptr(J.csi[0]);
+  GLB float*          csi1 = gptr(J.csi[1]);
   if (live) {
     const uint32_t nrx = J.nof_rx;
     auto           Y   = [&](uint32_t r, uint32_t i) {
-      const uint32_t g = J.map[i];
-      cf             v = ld(J.y[r], g);
+      const uint32_t g = map[i];
+      cf             v = ld(gptr(J.y[r]), g);
       if ((J.rhob_mask >> (g / J.row)) & 1u) v = v * J.rhob_inv;
       return v;
     };
-    auto H = [&](uint32_t p, uint32_t r, uint32_t i) { return ld(J.h[p][r], J.map[i]); };
+    auto H = [&](uint32_t p, uint32_t r, uint32_t i) { return ld(gptr(J.h[p][r]), map[i]); };
     switch (J.scheme) {
       case 0: { // srslte_predecoding_single_csi scalar formula (precoding.c:345-355)
         const uint32_t i = u;
@@ -115,8 +120,8 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
           hh += h.re * h.re + h.im * h.im;
         }
         const float c = hh + noise, nrm = 1.0f / J.scaling;
-        st(J.d[0], i, mk(r.re * nrm / c, r.im * nrm / c));
-        J.csi[0][i] = c;
+        st(d0, i, mk(r.re * nrm / c, r.im * nrm / c));
+        csi0[i] = c;
         m0          = c;
         break;
       }
@@ -134,16 +139,16 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
               x0 = x0 + (cj(h00) * r0 + h11 * cj(r1));
               x1 = x1 + ((h10 * -1.f) * cj(r0) + cj(h01) * r1);
             }
-            J.csi[0][2 * i] = J.csi[0][2 * i + 1] = hh;
+            csi0[2 * i] = csi0[2 * i + 1] = hh;
             m0                                   = hh;
             const float s                        = hh * J.scaling;
             // x / hh * M_SQRT2 evaluates in double in the reference
-            st(J.d[0], 2 * i, mk((float)((double)(x0.re / s) * 1.4142135623730951), (float)((double)(x0.im / s) * 1.4142135623730951)));
-            st(J.d[0], 2 * i + 1, mk((float)((double)(x1.re / s) * 1.4142135623730951), (float)((double)(x1.im / s) * 1.4142135623730951)));
+            st(d0, 2 * i, mk((float)((double)(x0.re / s) * 1.4142135623730951), (float)((double)(x0.im / s) * 1.4142135623730951)));
+            st(d0, 2 * i + 1, mk((float)((double)(x1.re / s) * 1.4142135623730951), (float)((double)(x1.im / s) * 1.4142135623730951)));
           } else {
             for (uint32_t k = 2 * i; k < J.nof_re; k++) {
-              st(J.d[0], k, mk(0.f, 0.f));
-              J.csi[0][k] = 0.f;
+              st(d0, k, mk(0.f, 0.f));
+              csi0[k] = 0.f;
             }
           }
         } else { // 4 ports (precoding.c:717-776); REs past m_ap quads are left zero
@@ -168,15 +173,15 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
             for (int q = 0; q < 4; q++) {
               const float aq = a[q] * J.scaling;
               const float c  = aq / (float)nrx;
-              J.csi[0][4 * i + q] = c;
+              csi0[4 * i + q] = c;
               m0                  = fmaxf(m0, c);
-              st(J.d[0], 4 * i + q,
+              st(d0, 4 * i + q,
                  mk((float)((double)(xv[q].re / aq) * 1.4142135623730951), (float)((double)(xv[q].im / aq) * 1.4142135623730951)));
             }
           } else {
             for (uint32_t k = 4 * i; k < min(J.nof_re, 4 * i + 4); k++) {
-              st(J.d[0], k, mk(0.f, 0.f));
-              J.csi[0][k] = 0.f;
+              st(d0, k, mk(0.f, 0.f));
+              csi0[k] = 0.f;
             }
           }
         }
@@ -198,10 +203,10 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
           cf    x0, x1;
           float c0, c1;
           mmse_2x2_csi(Y(0, i), Y(1, i), h00, h01, h10, h11, x0, x1, c0, c1, noise, norm);
-          st(J.d[0], i, x0);
-          st(J.d[1], i, x1);
-          J.csi[0][i] = c0;
-          J.csi[1][i] = c1;
+          st(d0, i, x0);
+          st(d1, i, x1);
+          csi0[i] = c0;
+          csi1[i] = c1;
           m0          = c0;
           m1          = c1;
         } else { // srslte_predecoding_multiplex_2x1_mrc_csi (precoding.c:1786-1820)
@@ -214,9 +219,9 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
           }
           const float c  = h[0].re * h[0].re + h[0].im * h[0].im + h[1].re * h[1].re + h[1].im * h[1].im;
           const float hh = norm / c;
-          st(J.d[0], i, (cj(h[0]) * Y(0, i) + cj(h[1]) * Y(1, i)) * hh);
+          st(d0, i, (cj(h[0]) * Y(0, i) + cj(h[1]) * Y(1, i)) * hh);
           const float cv = (float)((double)(c / norm) * 0.70710678118654752);
-          J.csi[0][i]    = cv;
+          csi0[i]    = cv;
           m0             = cv;
         }
         break;
@@ -233,10 +238,10 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
         cf    x0, x1;
         float c0, c1;
         mmse_2x2_csi(Y(0, i), Y(1, i), h00, h01, h10, h11, x0, x1, c0, c1, noise, 2.0f / J.scaling);
-        st(J.d[0], i, x0);
-        st(J.d[1], i, x1);
-        J.csi[0][i] = c0;
-        J.csi[1][i] = c1;
+        st(d0, i, x0);
+        st(d1, i, x1);
+        csi0[i] = c0;
+        csi1[i] = c1;
         m0          = c0;
         m1          = c1;
         break;
@@ -359,30 +364,30 @@ __global__ __launch_bounds__(256) void pdsch_scr_pack(const uint32_t* __restrict
     v ^= gold[(size_t)i * W + w];
     m &= m - 1;
   }
-  dst[blockIdx.y][w] = v;
+  gptr(dst[blockIdx.y])[w] = v;
 }
 
-template <int QM> __device__ __forceinline__ void store_llrs(int16_t* e, const int16_t (&o)[2 * QM], uint32_t nb)
+template <int QM> __device__ __forceinline__ void store_llrs(GLB int16_t* e, const int16_t (&o)[2 * QM], uint32_t nb)
 {
   if (nb == 2 * QM) {
     if constexpr ((2 * QM) % 8 == 0) { // 16-byte aligned groups (QM = 4, 8)
 #pragma unroll
       for (int k = 0; k < 2 * QM; k += 8) {
-        uint4 v;
+        vu4 v;
         v.x = (uint16_t)o[k] | ((uint32_t)(uint16_t)o[k + 1] << 16);
         v.y = (uint16_t)o[k + 2] | ((uint32_t)(uint16_t)o[k + 3] << 16);
         v.z = (uint16_t)o[k + 4] | ((uint32_t)(uint16_t)o[k + 5] << 16);
         v.w = (uint16_t)o[k + 6] | ((uint32_t)(uint16_t)o[k + 7] << 16);
-        *(uint4*)(e + k) = v;
+        *(GLB vu4*)(e + k) = v;
       }
       return;
     } else if constexpr ((2 * QM) % 4 == 0) { // 8-byte aligned groups (QM = 2, 6)
 #pragma unroll
       for (int k = 0; k < 2 * QM; k += 4) {
-        uint2 v;
+        vu2 v;
         v.x = (uint16_t)o[k] | ((uint32_t)(uint16_t)o[k + 1] << 16);
         v.y = (uint16_t)o[k + 2] | ((uint32_t)(uint16_t)o[k + 3] << 16);
-        *(uint2*)(e + k) = v;
+        *(GLB vu2*)(e + k) = v;
       }
       return;
     }
@@ -398,11 +403,24 @@ template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, 
   const uint32_t s0 = 2 * pr, ns = min(2u, n - s0);
   int16_t        o[2 * QM];
   float          csi[2] = {0.f, 0.f};
+  cf             x[2]   = {mk(0.f, 0.f), mk(0.f, 0.f)};
+  if (ns == 2) { // the pair as one 16-byte load (d is 64-element aligned per codeword, s0 even)
+    const vf4 v = *(const GLB vf4*)(gptr(C.d) + s0);
+    x[0]           = mk(v.x, v.y);
+    x[1]           = mk(v.z, v.w);
+    if (C.csi_enable) {
+      const vf2 c = *(const GLB vf2*)(gptr(C.csi) + s0);
+      csi[0] = c.x;
+      csi[1] = c.y;
+    }
+  } else {
+    x[0] = ld(gptr(C.d), s0);
+    if (C.csi_enable) csi[0] = gptr(C.csi)[s0];
+  }
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     if ((uint32_t)k < ns) {
-      demod_symbol(QM, ld(C.d, s0 + k), s0 + k, n, &o[k * QM]);
-      if (C.csi_enable) csi[k] = C.csi[s0 + k];
+      demod_symbol(QM, x[k], s0 + k, n, &o[k * QM]);
     } else {
 #pragma unroll
       for (int b = 0; b < QM; b++) o[k * QM + b] = 0;
@@ -411,14 +429,15 @@ template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, 
   // descrambling e = c ? -e : e (srslte_scrambling_s_offset, scrambling.c:43-47) with the packed sequence
   const uint32_t b0 = s0 * QM, nb = ns * QM;
   const uint32_t w0 = b0 >> 5, sh = b0 & 31;
-  const uint64_t bits = (uint64_t)C.scr[w0] | ((sh + 2 * QM > 32 && (b0 + 2 * QM - 1) / 32 < (C.nof_bits + 31) / 32)
-                                                  ? (uint64_t)C.scr[w0 + 1] << 32 : 0ull);
+  const GLB uint32_t* scr = gptr(C.scr);
+  const uint64_t bits = (uint64_t)scr[w0] | ((sh + 2 * QM > 32 && (b0 + 2 * QM - 1) / 32 < (C.nof_bits + 31) / 32)
+                                                ? (uint64_t)scr[w0 + 1] << 32 : 0ull);
 #pragma unroll
   for (int k = 0; k < 2 * QM; k++)
     if ((bits >> (sh + k)) & 1ull) o[k] = (int16_t)(uint16_t)(-(int32_t)o[k]);
   if (C.csi_enable) { // csi_correction (pdsch.c:628-741), SSE path
     const uint32_t nsym  = C.nof_bits / QM;
-    const float    cmax  = nsym ? __uint_as_float(*C.cmax) : 1.0f;
+    const float    cmax  = nsym ? __uint_as_float(*gptr(C.cmax)) : 1.0f;
     const float    scale = 32767.0f / cmax;
     auto           CV    = [&](float v) { return sat16(x86_cvt_i32(rintf(v * scale))); }; // _mm_cvtps_pi16
     const bool     body  = (QM == 4 || QM == 8) || ((QM == 2 || QM == 6) && ns == 2);
@@ -456,15 +475,13 @@ template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, 
       }
     }
   }
-  store_llrs<QM>(C.e + b0, o, nb);
+  store_llrs<QM>(gptr(C.e) + b0, o, nb);
 }
 
-__global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ cws, const uint32_t* __restrict__ start,
-                                                 uint32_t ncw)
+__global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ cws)
 {
-  const uint32_t    c  = owner(start, ncw, blockIdx.x);
-  const PdschCwDev& C  = cws[c];
-  const uint32_t    pr = (blockIdx.x - start[c]) * 256 + threadIdx.x;
+  const PdschCwDev& C  = cws[blockIdx.y];
+  const uint32_t    pr = blockIdx.x * 256 + threadIdx.x;
   if (pr >= C.pairs) return;
   switch (C.qm) {
     case 1: llr_pair<1>(C, pr); break;
@@ -475,11 +492,12 @@ __global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ 
   }
 }
 
-hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, const uint32_t* start, uint32_t njobs, uint32_t nblk,
-                                 hipStream_t s)
+hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, uint32_t njobs, uint32_t max_units, hipStream_t s)
 {
+  const uint32_t nblk = (max_units + 255) / 256;
   if (!nblk) return hipSuccess;
-  hipLaunchKernelGGL(pdsch_equalize, dim3(nblk), dim3(256), 0, s, jobs, start, njobs);
+  for (uint32_t j0 = 0; j0 < njobs; j0 += 65535) // grid.y <= 65535
+    hipLaunchKernelGGL(pdsch_equalize, dim3(nblk, std::min(65535u, njobs - j0)), dim3(256), 0, s, jobs + j0);
   return hipGetLastError();
 }
 
@@ -491,10 +509,12 @@ hipError_t pdsch_launch_scr_pack(const uint32_t* c_init, uint32_t* const* dst, u
   return hipGetLastError();
 }
 
-hipError_t pdsch_launch_llr(const PdschCwDev* cws, const uint32_t* start, uint32_t ncw, uint32_t nblk, hipStream_t s)
+hipError_t pdsch_launch_llr(const PdschCwDev* cws, uint32_t ncw, uint32_t max_pairs, hipStream_t s)
 {
+  const uint32_t nblk = (max_pairs + 255) / 256;
   if (!nblk) return hipSuccess;
-  hipLaunchKernelGGL(pdsch_llr, dim3(nblk), dim3(256), 0, s, cws, start, ncw);
+  for (uint32_t c0 = 0; c0 < ncw; c0 += 65535)
+    hipLaunchKernelGGL(pdsch_llr, dim3(nblk, std::min(65535u, ncw - c0)), dim3(256), 0, s, cws + c0);
   return hipGetLastError();
 }
 

@@ -329,7 +329,6 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   const uint32_t njobs = (uint32_t)plans.size();
   size_t         nd = 0, ne = 0;
   std::vector<PdschCwDev> cws;
-  std::vector<uint32_t>   startA(njobs + 1), startB;
   std::vector<uint32_t>   new_ci;
   std::vector<uint32_t*>  new_dst;
   if (q->scr.size() > 4096) { // bound the sequence cache (~76 MB)
@@ -337,19 +336,17 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
     for (auto& kv : q->scr) (void)hipFree(kv.second);
     q->scr.clear();
   }
-  uint32_t  nblkA = 0, nblkB = 0;
+  uint32_t  max_units = 0, max_pairs = 0;
   uint32_t  last_ci  = 0;
   const uint32_t* last_scr = nullptr;
   cws.reserve(2 * njobs);
-  startB.reserve(2 * njobs + 1);
   for (uint32_t i = 0; i < njobs; i++) {
     JobPlan& P = plans[i];
     for (uint32_t cw = 0; cw < 2; cw++) {
       P.d_off[cw] = P.csi_off[cw] = nd;
       nd += (P.dev.nof_re + 63) / 64 * 64;
     }
-    startA[i] = nblkA;
-    nblkA += (P.dev.units + 255) / 256;
+    max_units = std::max(max_units, P.dev.units);
     for (uint32_t t = 0; t < 2; t++) {
       if (!P.decode[t]) continue;
       const mi355_ra_tb_t& tb = jobs[i].cfg.grant.tb[t];
@@ -362,8 +359,7 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
       c.c_init     = ((uint32_t)jobs[i].cfg.rnti << 14) + (tb.cw_idx << 13) + ((jobs[i].sf.tti % 10) << 9) + q->cell.id;
       c.csi_enable = jobs[i].cfg.csi_enable ? 1u : 0u;
       c.pairs      = (c.nof_re + 1) / 2;
-      startB.push_back(nblkB);
-      nblkB += (c.pairs + 255) / 256;
+      max_pairs = std::max(max_pairs, c.pairs);
       if (c.c_init == last_ci && last_scr) {
         c.scr = last_scr;
       } else {
@@ -382,12 +378,9 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
       cws.push_back(c);
     }
   }
-  startA[njobs] = nblkA;
-  startB.push_back(nblkB);
   const size_t ncw = cws.size();
   // device scratch: [staged descriptors | d | csi | e]; the staged part mirrors the pinned host buffer
   const size_t staged = staged_size(njobs * sizeof(PdschJobDev)) + staged_size(ncw * sizeof(PdschCwDev)) +
-                        staged_size(startA.size() * 4) + staged_size(startB.size() * 4) +
                         staged_size(new_ci.size() * 4) + staged_size(new_ci.size() * 8) + staged_size(njobs * 8);
   auto         rnd  = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t need = staged + rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2);
@@ -398,10 +391,9 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   q->csi_arena = (float*)(base + staged + rnd(nd * 8));
   q->e_arena   = (int16_t*)(base + staged + rnd(nd * 8) + rnd(nd * 4));
   CHECK_HIP(q->stage.reserve(staged));
-  // offsets are known up front: jobs | cws | startA | startB | nci | ndst | cmax
+  // offsets are known up front: jobs | cws | nci | ndst | cmax
   const size_t o_jobs = 0, o_cws = o_jobs + staged_size(njobs * sizeof(PdschJobDev));
-  const size_t o_sa = o_cws + staged_size(ncw * sizeof(PdschCwDev)), o_sb = o_sa + staged_size(startA.size() * 4);
-  const size_t o_nci = o_sb + staged_size(startB.size() * 4), o_ndst = o_nci + staged_size(new_ci.size() * 4);
+  const size_t o_nci = o_cws + staged_size(ncw * sizeof(PdschCwDev)), o_ndst = o_nci + staged_size(new_ci.size() * 4);
   const size_t o_cmax = o_ndst + staged_size(new_ci.size() * 8);
   uint32_t*    d_cmax = (uint32_t*)(base + o_cmax);
   std::vector<PdschJobDev> hj(njobs);
@@ -428,16 +420,14 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   }
   q->stage.put(hj.data(), njobs * sizeof(PdschJobDev));
   q->stage.put(cws.data(), ncw * sizeof(PdschCwDev));
-  q->stage.put(startA.data(), startA.size() * 4);
-  q->stage.put(startB.data(), startB.size() * 4);
   q->stage.put(new_ci.data(), new_ci.size() * 4);
   q->stage.put(new_dst.data(), new_dst.size() * 8);
   q->stage.zeros(njobs * 8);
-  CHECK_HIP(hipMemcpyAsync(base, q->stage.host, q->stage.used, hipMemcpyHostToDevice, s));
-  CHECK_HIP(pdsch_launch_equalize((const PdschJobDev*)(base + o_jobs), (const uint32_t*)(base + o_sa), njobs, nblkA, s));
+  CHECK_HIP(q->stage.upload(base, s));
+  CHECK_HIP(pdsch_launch_equalize((const PdschJobDev*)(base + o_jobs), njobs, max_units, s));
   CHECK_HIP(pdsch_launch_scr_pack((const uint32_t*)(base + o_nci), (uint32_t* const*)(base + o_ndst),
                                   (uint32_t)new_ci.size(), q->gold, PDSCH_GOLD_MAX / 32, s));
-  CHECK_HIP(pdsch_launch_llr((const PdschCwDev*)(base + o_cws), (const uint32_t*)(base + o_sb), (uint32_t)ncw, nblkB, s));
+  CHECK_HIP(pdsch_launch_llr((const PdschCwDev*)(base + o_cws), (uint32_t)ncw, max_pairs, s));
   return MI355_SUCCESS;
 }
 

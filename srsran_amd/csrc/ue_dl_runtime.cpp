@@ -13,6 +13,7 @@
 #include "../../include/srsran_amd/ue_dl.h"
 #include "lte_common.h"
 #include "runtime_internal.h"
+#include "host_staging.h"
 #include "ue_dl_internal.h"
 
 using namespace mi355;
@@ -75,6 +76,7 @@ struct mi355_ue_dl {
   mi355_pdsch_t* pdsch  = nullptr;
   char*          scratch = nullptr;
   size_t         scratch_cap = 0;
+  HostStaging    st_ofdm, st_chest, back; // pinned descriptor uploads / estimator read-back
   std::mutex     mu;
 };
 
@@ -127,26 +129,27 @@ static int get_scratch(mi355_ue_dl_t* q, size_t bytes, char** p)
 static int ofdm_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, hipStream_t s,
                     size_t* used = nullptr)
 {
-  std::vector<OfdmJob> oj;
-  oj.reserve((size_t)njobs * q->nof_rx);
+  const size_t nj = (size_t)njobs * q->nof_rx;
+  CHECK_HIP(q->st_ofdm.reserve(nj * sizeof(OfdmJob)));
+  auto* oj = (OfdmJob*)q->st_ofdm.slot(nj * sizeof(OfdmJob));
   for (uint32_t i = 0; i < njobs; i++) {
     for (uint32_t r = 0; r < q->nof_rx; r++) {
       if (!jobs[i].in_buffer[r] || !jobs[i].sf_symbols[r]) return MI355_ERROR_INVALID_INPUTS;
-      oj.push_back(OfdmJob{(const float2*)jobs[i].in_buffer[r], (float2*)jobs[i].sf_symbols[r]});
+      oj[(size_t)i * q->nof_rx + r] = OfdmJob{(const float2*)jobs[i].in_buffer[r], (float2*)jobs[i].sf_symbols[r]};
     }
   }
   char* base = nullptr;
-  int   r    = get_scratch(q, oj.size() * sizeof(OfdmJob) + 256, &base);
+  int   r    = get_scratch(q, nj * sizeof(OfdmJob) + 256, &base);
   if (r) return r;
-  CHECK_HIP(hipMemcpyAsync(base, oj.data(), oj.size() * sizeof(OfdmJob), hipMemcpyHostToDevice, s));
+  CHECK_HIP(q->st_ofdm.upload(base, s));
   OfdmArgs a = q->ofdm;
   a.jobs     = (const OfdmJob*)base;
   // grid.y is limited to 65535: launch in chunks
-  for (size_t off = 0; off < oj.size(); off += 65535) {
+  for (size_t off = 0; off < nj; off += 65535) {
     a.jobs = (const OfdmJob*)base + off;
-    CHECK_HIP(ofdm_launch_rx(a, (uint32_t)std::min<size_t>(65535, oj.size() - off), s));
+    CHECK_HIP(ofdm_launch_rx(a, (uint32_t)std::min<size_t>(65535, nj - off), s));
   }
-  if (used) *used = (oj.size() * sizeof(OfdmJob) + 255) / 256 * 256;
+  if (used) *used = (nj * sizeof(OfdmJob) + 255) / 256 * 256;
   return MI355_SUCCESS;
 }
 
@@ -238,9 +241,11 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
 {
   int r = chest_check_cfg(cfg);
   if (r) return r;
-  const uint32_t        P = q->cell.nof_ports, R = q->nof_rx;
-  std::vector<ChestJob> cj;
-  cj.reserve((size_t)njobs * P * R);
+  const uint32_t P = q->cell.nof_ports, R = q->nof_rx;
+  const size_t   ncj = (size_t)njobs * P * R;
+  CHECK_HIP(q->st_chest.reserve(ncj * sizeof(ChestJob)));
+  auto*  cj = (ChestJob*)q->st_chest.slot(ncj * sizeof(ChestJob));
+  size_t k  = 0;
   const size_t nout = (size_t)njobs * P * R * 5;
   char*        base = nullptr;
   const size_t jb   = ((size_t)njobs * P * R * sizeof(ChestJob) + 255) / 256 * 256;
@@ -253,12 +258,12 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
     for (uint32_t a = 0; a < R; a++) {
       for (uint32_t p = 0; p < P; p++) {
         if (!jobs[i].sf_symbols[a] || !jobs[i].ce[p][a]) return MI355_ERROR_INVALID_INPUTS;
-        cj.push_back(ChestJob{(const float2*)jobs[i].sf_symbols[a], (float2*)jobs[i].ce[p][a],
-                              d_out + ((size_t)i * R * P + a * P + p) * 5, jobs[i].tti % 10, p});
+        cj[k++] = ChestJob{(const float2*)jobs[i].sf_symbols[a], (float2*)jobs[i].ce[p][a],
+                           d_out + ((size_t)i * R * P + a * P + p) * 5, jobs[i].tti % 10, p};
       }
     }
   }
-  CHECK_HIP(hipMemcpyAsync(base, cj.data(), cj.size() * sizeof(ChestJob), hipMemcpyHostToDevice, s));
+  CHECK_HIP(q->st_chest.upload(base, s));
   ChestArgs ca{};
   ca.jobs        = (const ChestJob*)base;
   ca.pilots      = q->pilots;
@@ -268,7 +273,7 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
   ca.filter_type = cfg->filter_type;
   ca.coef0       = cfg->filter_coef[0];
   ca.coef1       = cfg->filter_coef[1];
-  CHECK_HIP(chest_launch(ca, (uint32_t)cj.size(), s));
+  CHECK_HIP(chest_launch(ca, (uint32_t)ncj, s));
   if (d_noise_p) CHECK_HIP(chest_launch_noise(d_out, R, P, njobs, d_noise, s));
   *d_out_p = d_out;
   if (d_noise_p) *d_noise_p = d_noise;
@@ -280,8 +285,9 @@ static int chest_finish(mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const
 {
   const uint32_t     P = q->cell.nof_ports, R = q->nof_rx;
   const size_t       nout = (size_t)njobs * P * R * 5;
-  std::vector<float> out(nout);
-  CHECK_HIP(hipMemcpyAsync(out.data(), d_out, nout * 4, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(q->back.reserve(nout * 4));
+  const float* out = (const float*)q->back.host;
+  CHECK_HIP(hipMemcpyAsync(q->back.host, d_out, nout * 4, hipMemcpyDeviceToHost, s));
   CHECK_HIP(hipStreamSynchronize(s));
   for (uint32_t i = 0; i < njobs; i++) fill_res(q, cfg, &out[(size_t)i * R * P * 5], &res[i]);
   return MI355_SUCCESS;
