@@ -120,47 +120,43 @@ __device__ __forceinline__ uint32_t gf2_mulmod24(uint32_t a, uint32_t b, uint32_
   return r & 0xffffffu;
 }
 
-__device__ uint32_t wave_crc24(const uint8_t* bytes, uint32_t nbytes, const CrcTable& T)
+// byte-serial CRC of n bytes (table in LDS); the bytes are loaded 16 at a time, independently of the fold
+__device__ __forceinline__ uint32_t crc24_bytes(const uint8_t* p, uint32_t n, const uint32_t* tl)
 {
-  const int      lane  = threadIdx.x & 63;
-  const uint32_t chunk = (nbytes + 63) / 64;
-  const uint32_t b0    = min(nbytes, lane * chunk), b1 = min(nbytes, b0 + chunk);
-  uint32_t       crc   = 0;
-  for (uint32_t i = b0; i < b1; i++) crc = ((crc << 8) ^ T.t[((crc >> 16) & 0xff) ^ bytes[i]]) & 0xffffffu;
-  uint32_t after = nbytes - b1, sc = 1;
-  for (int i = 0; after; i++, after >>= 1) {
-    if (after & 1) sc = gf2_mulmod24(sc, T.pw[i], T.poly);
-  }
-  crc = gf2_mulmod24(crc, sc, T.poly);
+  uint32_t crc = 0;
+  for (uint32_t i = 0; i < n; i += 16) {
+    uint8_t v[16];
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
+    for (int k = 0; k < 16; k++) v[k] = i + k < n ? p[i + k] : 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      if (i + k < n) crc = ((crc << 8) ^ tl[((crc >> 16) & 0xff) ^ v[k]]) & 0xffffffu;
+  }
   return crc;
 }
 
 // wave CRC with the per-lane scale factors x^(8*after) precomputed for this byte count (scale[lane])
-__device__ __forceinline__ uint32_t wave_crc24_scaled(const uint8_t* bytes, uint32_t nbytes, const CrcTable& T,
-                                                      const uint32_t* scale)
+__device__ __forceinline__ uint32_t wave_crc24_scaled(const uint8_t* bytes, uint32_t nbytes, const uint32_t* tl,
+                                                      uint32_t poly, const uint32_t* scale)
 {
   const int      lane  = threadIdx.x & 63;
   const uint32_t chunk = (nbytes + 63) / 64;
   const uint32_t b0    = min(nbytes, lane * chunk), b1 = min(nbytes, b0 + chunk);
-  uint32_t       crc   = 0;
-  for (uint32_t i = b0; i < b1; i++) crc = ((crc << 8) ^ T.t[((crc >> 16) & 0xff) ^ bytes[i]]) & 0xffffffu;
-  crc = gf2_mulmod24(crc, scale[lane], T.poly);
+  uint32_t       crc   = crc24_bytes(bytes + b0, b1 - b0, tl);
+  crc                  = gf2_mulmod24(crc, scale[lane], poly);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
   return crc;
 }
 
-// the same with a whole 256-thread workgroup (TB CRC over up to 12 KB)
-__device__ uint32_t block_crc24(const uint8_t* bytes, uint32_t nbytes, const CrcTable& T)
+// the same with a whole 256-thread workgroup (TB CRC over up to 49 KB), scale factors by square-and-multiply
+__device__ uint32_t block_crc24(const uint8_t* bytes, uint32_t nbytes, const uint32_t* tl, const CrcTable& T)
 {
   __shared__ uint32_t part[4];
   const uint32_t tid   = threadIdx.x;
   const uint32_t chunk = (nbytes + 255) / 256;
   const uint32_t b0 = min(nbytes, tid * chunk), b1 = min(nbytes, b0 + chunk);
-  uint32_t       crc = 0;
-  for (uint32_t i = b0; i < b1; i++) crc = ((crc << 8) ^ T.t[((crc >> 16) & 0xff) ^ bytes[i]]) & 0xffffffu;
+  uint32_t       crc = crc24_bytes(bytes + b0, b1 - b0, tl);
   uint32_t after = nbytes - b1, sc = 1;
   for (int i = 0; after; i++, after >>= 1) {
     if (after & 1) sc = gf2_mulmod24(sc, T.pw[i], T.poly);
@@ -190,14 +186,18 @@ __device__ __forceinline__ void flag_set(uint32_t* f)
 __global__ __launch_bounds__(1024) void dlsch_cb_check(DlschCheckArgs a)
 {
   __shared__ uint32_t unfinished;
+  __shared__ uint32_t tl[2][256]; // CRC24A | CRC24B tables
   if (threadIdx.x == 0) unfinished = 0;
+  if (a.ncb && *a.remaining == 0) return; // uniform: every code block has finished
+  if (threadIdx.x < 512) tl[threadIdx.x >> 8][threadIdx.x & 255] = (threadIdx.x < 256 ? a.crc24a : a.crc24b)->t[threadIdx.x & 255];
   __syncthreads();
   const int b    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (b < a.ncb && *a.remaining != 0 && !a.done[b]) {
     const CbDesc&  d   = a.desc[b];
     const uint8_t* dec = a.dec + (size_t)b * a.dec_stride;
-    const uint32_t crc = wave_crc24_scaled(dec, a.K / 8, d.C > 1 ? *a.crc24b : *a.crc24a, a.scale + (d.C > 1 ? 64 : 0));
+    const uint32_t crc = wave_crc24_scaled(dec, a.K / 8, tl[d.C > 1 ? 1 : 0], d.C > 1 ? a.crc24b->poly : a.crc24a->poly,
+                                           a.scale + (d.C > 1 ? 64 : 0));
     const bool     ok  = crc == 0;
     const bool     fin = ok || a.h + 1 == a.max_its;
     if (!fin) {
@@ -278,6 +278,9 @@ __global__ __launch_bounds__(256) void dlsch_tb_epilogue(DlschTbArgs a)
   const int t   = blockIdx.x;
   const int tid = threadIdx.x;
   if (t >= a.ntb) return;
+  __shared__ uint32_t tl[256];
+  tl[tid] = a.crc24a->t[tid]; // blockDim == 256
+  __syncthreads();
   const TbDesc& tb = a.tb[t];
   if (tid == 0) { // srslte_pdsch_res_t.avg_iterations_block (sch.c:451-453): mean over the TB's code blocks
     double sum = 0.0;
@@ -289,7 +292,7 @@ __global__ __launch_bounds__(256) void dlsch_tb_epilogue(DlschTbArgs a)
     return;
   }
   bool ok = true;
-  for (uint32_t c = 0; c < tb.C; c++) ok = ok && a.sb_crc[tb.slot0 + c];
+  for (uint32_t c = 0; c < tb.C; c++) ok &= a.sb_crc[tb.slot0 + c] != 0; // independent loads
   uint8_t* data = a.data + tb.data_off;
   if (!ok) {
     for (uint32_t c = 0; c < tb.C; c++) {
@@ -302,7 +305,7 @@ __global__ __launch_bounds__(256) void dlsch_tb_epilogue(DlschTbArgs a)
     if (tid == 0) a.ret[t] = -1;
     return;
   }
-  const uint32_t par_rx = block_crc24(data, tb.tbs / 8, *a.crc24a);
+  const uint32_t par_rx = block_crc24(data, tb.tbs / 8, tl, *a.crc24a);
   if (tid == 0) {
     const uint32_t par_tx = ((uint32_t)data[tb.tbs / 8] << 16) | ((uint32_t)data[tb.tbs / 8 + 1] << 8) |
                             (uint32_t)data[tb.tbs / 8 + 2];

@@ -75,6 +75,9 @@ __device__ __forceinline__ void mmse_2x2_csi(cf y0, cf y1, cf h00, cf h01, cf h1
   csi1         = 1.0f / b11.re;
 }
 
+// max in the unsigned order of the bit patterns (the order fold_max reduces in; IEEE order for csi >= 0)
+__device__ __forceinline__ float bmax(float a, float b) { return __uint_as_float(max(__float_as_uint(a), __float_as_uint(b))); }
+
 __device__ __forceinline__ void fold_max(uint32_t* m, float v)
 {
   // csi >= 0: IEEE order == unsigned order of the bit patterns.  Reduce over the wave first.
@@ -86,21 +89,15 @@ __device__ __forceinline__ void fold_max(uint32_t* m, float v)
 
 } // namespace
 
-// grid (blocks of the largest job, jobs): blockIdx.y is the job, blocks past a smaller job's work exit
-__global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restrict__ jobs)
+// One work item of any scheme (the reference formulas per case); m0/m1 fold the CSI maxima.
+__device__ __forceinline__ void eq_one(const PdschJobDev& J, uint32_t u, float noise, float& m0, float& m1)
 {
-  const PdschJobDev& J = jobs[blockIdx.y];
-  if (blockIdx.x * 256 >= J.units) return;
-  const uint32_t u    = blockIdx.x * 256 + threadIdx.x;
-  const bool     live = u < J.units;
-  float           m0 = 0.f, m1 = 0.f; // per-thread csi contribution for the max
-  const float     noise = J.noise_dev ? *gptr(J.noise_dev) : J.noise;
   const GLB uint16_t* map  = gptr(J.map);
   GLB float2*         d0   = gptr(J.d[0]);
   GLB float2*         d1   = gptr(J.d[1]);
   GLB float*          csi0 = gptr(J.csi[0]);
   GLB float*          csi1 = gptr(J.csi[1]);
-  if (live) {
+  {
     const uint32_t nrx = J.nof_rx;
     auto           Y   = [&](uint32_t r, uint32_t i) {
       const uint32_t g = map[i];
@@ -122,7 +119,7 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
         const float c = hh + noise, nrm = 1.0f / J.scaling;
         st(d0, i, mk(r.re * nrm / c, r.im * nrm / c));
         csi0[i] = c;
-        m0          = c;
+        m0          = bmax(m0, c);
         break;
       }
       case 1: {
@@ -140,7 +137,7 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
               x1 = x1 + ((h10 * -1.f) * cj(r0) + cj(h01) * r1);
             }
             csi0[2 * i] = csi0[2 * i + 1] = hh;
-            m0                                   = hh;
+            m0                                   = bmax(m0, hh);
             const float s                        = hh * J.scaling;
             // x / hh * M_SQRT2 evaluates in double in the reference
             st(d0, 2 * i, mk((float)((double)(x0.re / s) * 1.4142135623730951), (float)((double)(x0.im / s) * 1.4142135623730951)));
@@ -174,7 +171,7 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
               const float aq = a[q] * J.scaling;
               const float c  = aq / (float)nrx;
               csi0[4 * i + q] = c;
-              m0                  = fmaxf(m0, c);
+              m0                  = bmax(m0, c);
               st(d0, 4 * i + q,
                  mk((float)((double)(xv[q].re / aq) * 1.4142135623730951), (float)((double)(xv[q].im / aq) * 1.4142135623730951)));
             }
@@ -207,8 +204,8 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
           st(d1, i, x1);
           csi0[i] = c0;
           csi1[i] = c1;
-          m0          = c0;
-          m1          = c1;
+          m0          = bmax(m0, c0);
+          m1          = bmax(m1, c1);
         } else { // srslte_predecoding_multiplex_2x1_mrc_csi (precoding.c:1786-1820)
           const float norm = 0x1.6a09e6p+0f / J.scaling;
           cf          h[2];
@@ -222,7 +219,7 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
           st(d0, i, (cj(h[0]) * Y(0, i) + cj(h[1]) * Y(1, i)) * hh);
           const float cv = (float)((double)(c / norm) * 0.70710678118654752);
           csi0[i]    = cv;
-          m0             = cv;
+          m0             = bmax(m0, cv);
         }
         break;
       }
@@ -242,9 +239,132 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
         st(d1, i, x1);
         csi0[i] = c0;
         csi1[i] = c1;
-        m0          = c0;
-        m1          = c1;
+        m0          = bmax(m0, c0);
+        m1          = bmax(m1, c1);
         break;
+      }
+    }
+  }
+}
+
+
+constexpr int EQ_U = 4; // work items per thread: all their gathers are issued before any arithmetic
+
+// The received symbol of grid index g with rho_b applied (apply_power_allocation, pdsch.c:589-607)
+__device__ __forceinline__ cf y_at(const PdschJobDev& J, uint32_t r, uint32_t g)
+{
+  cf v = ld(gptr(J.y[r]), g);
+  if (J.rhob_mask && ((J.rhob_mask >> (g / J.row)) & 1u)) v = v * J.rhob_inv;
+  return v;
+}
+
+// grid (blocks of the largest job, jobs): blockIdx.y is the job, blocks past a smaller job's work exit.
+// Single-RE schemes (port 0, spatial multiplexing, CDD) gather the symbols and channel estimates of EQ_U REs
+// first and then equalise them (memory-level parallelism); SFBC pairs/quads go through eq_one.
+__global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restrict__ jobs)
+{
+  const PdschJobDev& J    = jobs[blockIdx.y];
+  const uint32_t     base = blockIdx.x * 256 * EQ_U + threadIdx.x;
+  if (blockIdx.x * 256 * EQ_U >= J.units) return;
+  const float noise = J.noise_dev ? *gptr(J.noise_dev) : J.noise;
+  float       m0 = 0.f, m1 = 0.f; // per-thread csi contributions for the maxima
+  if (J.scheme == 1) {
+#pragma unroll 1
+    for (int k = 0; k < EQ_U; k++)
+      if (base + k * 256 < J.units) eq_one(J, base + k * 256, noise, m0, m1);
+  } else {
+    const GLB uint16_t* map = gptr(J.map);
+    const uint32_t      nrx = J.nof_rx;
+    cf                  Y[EQ_U][2], H[EQ_U][4]; // H: [p * 2 + r] (port 0: [r])
+    uint32_t            g[EQ_U];
+#pragma unroll
+    for (int k = 0; k < EQ_U; k++) g[k] = base + k * 256 < J.units ? map[base + k * 256] : 0u;
+#pragma unroll
+    for (int k = 0; k < EQ_U; k++) {
+      const bool lv = base + k * 256 < J.units;
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        const bool rr = lv && (uint32_t)r < nrx;
+        Y[k][r]       = rr ? y_at(J, r, g[k]) : mk(0.f, 0.f);
+#pragma unroll
+        for (int p = 0; p < 2; p++)
+          H[k][p * 2 + r] = (rr && (p == 0 || J.scheme != 0)) ? ld(gptr(J.h[p][r]), g[k]) : mk(0.f, 0.f);
+      }
+    }
+    GLB float2* d0   = gptr(J.d[0]);
+    GLB float2* d1   = gptr(J.d[1]);
+    GLB float*  csi0 = gptr(J.csi[0]);
+    GLB float*  csi1 = gptr(J.csi[1]);
+#pragma unroll
+    for (int k = 0; k < EQ_U; k++) {
+      const uint32_t i = base + k * 256;
+      if (i >= J.units) continue;
+      if (J.scheme == 0) { // srslte_predecoding_single_csi scalar formula (precoding.c:345-355)
+        cf    r  = mk(0.f, 0.f);
+        float hh = 0.f;
+#pragma unroll
+        for (int p = 0; p < 2; p++) {
+          if ((uint32_t)p < nrx) {
+            const cf h = H[k][p];
+            r          = r + Y[k][p] * cj(h);
+            hh += h.re * h.re + h.im * h.im;
+          }
+        }
+        const float c = hh + noise, nrm = 1.0f / J.scaling;
+        st(d0, i, mk(r.re * nrm / c, r.im * nrm / c));
+        csi0[i] = c;
+        m0      = bmax(m0, c);
+      } else if (J.scheme == 2 && J.nof_layers == 2) { // multiplex_2x2_mmse_csi (precoding.c:1519-1548)
+        const float norm = J.cb == 0 ? 0x1.6a09e6p+0f / J.scaling : 2.0f / J.scaling;
+        const cf    g00 = H[k][0], g01 = H[k][1], g10 = H[k][2], g11 = H[k][3];
+        cf          h00, h01, h10, h11;
+        if (J.cb == 0) {
+          h00 = g00, h01 = g10, h10 = g01, h11 = g11;
+        } else if (J.cb == 1) {
+          h00 = g00 + g10, h01 = g00 - g10, h10 = g01 + g11, h11 = g01 - g11;
+        } else {
+          h00 = g00 + mulj(g10), h01 = g00 - mulj(g10), h10 = g01 + mulj(g11), h11 = g01 - mulj(g11);
+        }
+        cf    x0, x1;
+        float c0, c1;
+        mmse_2x2_csi(Y[k][0], Y[k][1], h00, h01, h10, h11, x0, x1, c0, c1, noise, norm);
+        st(d0, i, x0);
+        st(d1, i, x1);
+        csi0[i] = c0;
+        csi1[i] = c1;
+        m0      = bmax(m0, c0);
+        m1      = bmax(m1, c1);
+      } else if (J.scheme == 2) { // multiplex_2x1_mrc_csi (precoding.c:1786-1820)
+        const float norm = 0x1.6a09e6p+0f / J.scaling;
+        cf          h[2];
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+          const cf a = H[k][r], b = H[k][2 + r];
+          h[r] = J.cb == 0 ? a + b : J.cb == 1 ? a - b : J.cb == 2 ? a + mulj(b) : a - mulj(b);
+        }
+        const float c  = h[0].re * h[0].re + h[0].im * h[0].im + h[1].re * h[1].re + h[1].im * h[1].im;
+        const float hh = norm / c;
+        st(d0, i, (cj(h[0]) * Y[k][0] + cj(h[1]) * Y[k][1]) * hh);
+        const float cv = (float)((double)(c / norm) * 0.70710678118654752);
+        csi0[i]        = cv;
+        m0             = bmax(m0, cv);
+      } else { // ccd_2x2_mmse_csi (precoding.c:1111-1128)
+        const cf s0 = H[k][0], s1 = H[k][2], t0 = H[k][1], t1 = H[k][3];
+        cf       h00, h01, h10, h11;
+        if ((i & 1u) == 0) {
+          h00 = s0 + s1, h10 = t0 + t1, h01 = s0 - s1, h11 = t0 - t1;
+        } else {
+          h00 = s0 - s1, h10 = t0 - t1, h01 = s0 + s1, h11 = t0 + t1;
+        }
+        cf    x0, x1;
+        float c0, c1;
+        mmse_2x2_csi(Y[k][0], Y[k][1], h00, h01, h10, h11, x0, x1, c0, c1, noise, 2.0f / J.scaling);
+        st(d0, i, x0);
+        st(d1, i, x1);
+        csi0[i] = c0;
+        csi1[i] = c1;
+        m0      = bmax(m0, c0);
+        m1      = bmax(m1, c1);
       }
     }
   }
@@ -494,7 +614,7 @@ __global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ 
 
 hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, uint32_t njobs, uint32_t max_units, hipStream_t s)
 {
-  const uint32_t nblk = (max_units + 255) / 256;
+  const uint32_t nblk = (max_units + 256 * EQ_U - 1) / (256 * EQ_U);
   if (!nblk) return hipSuccess;
   for (uint32_t j0 = 0; j0 < njobs; j0 += 65535) // grid.y <= 65535
     hipLaunchKernelGGL(pdsch_equalize, dim3(nblk, std::min(65535u, njobs - j0)), dim3(256), 0, s, jobs + j0);
