@@ -121,10 +121,125 @@ __global__ __launch_bounds__(256) void ofdm_rx(OfdmArgs a)
   for (uint32_t k = threadIdx.x; k < a.nre; k += blockDim.x) out[k] = buf[src][k < half ? N - half + k : 1 + k - half];
 }
 
+// ---------------------------------------------------------------------------- size-specialised kernels
+// The LTE symbol sizes with a compile-time radix plan: index arithmetic folds to constants, the twiddle
+// table is staged in LDS together with the first stage's inputs (all loads issued up front), stage 0 reads
+// its inputs straight from HBM and the last stage writes the FFT-shifted subcarriers straight to HBM, so a
+// symbol makes (stages - 1) LDS round trips.  Stages run in place: every thread reads all of its inputs,
+// the workgroup synchronises, then writes.
+
+template <uint32_t R> __device__ __forceinline__ void dft(float2* v)
+{
+  if constexpr (R == 2) dft2(v[0], v[1]);
+  if constexpr (R == 3) dft3(v);
+  if constexpr (R == 4) dft4(v);
+  if constexpr (R == 8) dft8(v);
+}
+
+template <uint32_t N, uint32_t Ns, uint32_t R, bool LAST>
+__device__ __forceinline__ void stage_c(float2* buf, const float2* tw, float2* out, uint32_t half)
+{
+  constexpr uint32_t nb = N / R, M = (nb + 255) / 256, tws = N / (Ns * R);
+  float2             v[M][R];
+#pragma unroll
+  for (uint32_t m = 0; m < M; m++) {
+    const uint32_t j = threadIdx.x + 256 * m;
+    if (j < nb) {
+      const uint32_t k0 = j % Ns;
+#pragma unroll
+      for (uint32_t r = 0; r < R; r++) {
+        v[m][r] = buf[j + r * nb];
+        if (r) v[m][r] = cmul(v[m][r], tw[r * k0 * tws]); // r*k0*tws < N
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t m = 0; m < M; m++) {
+    const uint32_t j = threadIdx.x + 256 * m;
+    if (j < nb) {
+      const uint32_t k0 = j % Ns;
+      dft<R>(v[m]);
+      const uint32_t d = (j / Ns) * Ns * R + k0;
+#pragma unroll
+      for (uint32_t r = 0; r < R; r++) {
+        if constexpr (LAST) { // X[x] -> subcarrier k (ofdm.c:446-452 / ofdm_rx_slot's fft_shift without DC)
+          const uint32_t x = d + r * Ns;
+          if (x >= N - half) {
+            out[x - (N - half)] = v[m][r];
+          } else if (x >= 1 && x <= half) {
+            out[x - 1 + half] = v[m][r];
+          }
+        } else {
+          buf[d + r * Ns] = v[m][r];
+        }
+      }
+    }
+  }
+  if constexpr (!LAST) __syncthreads();
+}
+
+template <uint32_t N, uint32_t R0, uint32_t R1, uint32_t R2, uint32_t R3>
+__global__ __launch_bounds__(256) void ofdm_rx_n(OfdmArgs a)
+{
+  __shared__ float2 buf[N], tw[N];
+  const OfdmJob  J    = a.jobs[blockIdx.y];
+  const uint32_t sym  = blockIdx.x; // 0 .. 2*nsymb-1
+  const uint32_t slot = sym / a.nsymb, l = sym % a.nsymb;
+  const float2*  in   = J.in + (size_t)slot * a.slot_sz + a.cp0 + (size_t)l * (N + a.cp1);
+  constexpr uint32_t nb = N / R0, M = (nb + 255) / 256, MT = (N + 255) / 256;
+  float2             v[M][R0], t[MT];
+#pragma unroll
+  for (uint32_t m = 0; m < M; m++) {
+    const uint32_t j = threadIdx.x + 256 * m;
+#pragma unroll
+    for (uint32_t r = 0; r < R0; r++)
+      if (j < nb) v[m][r] = in[j + r * nb];
+  }
+#pragma unroll
+  for (uint32_t m = 0; m < MT; m++)
+    if (threadIdx.x + 256 * m < N) t[m] = a.tw[threadIdx.x + 256 * m];
+#pragma unroll
+  for (uint32_t m = 0; m < MT; m++)
+    if (threadIdx.x + 256 * m < N) tw[threadIdx.x + 256 * m] = t[m];
+  // stage 0 (Ns = 1: no twiddles), outputs j*R0 + r
+#pragma unroll
+  for (uint32_t m = 0; m < M; m++) {
+    const uint32_t j = threadIdx.x + 256 * m;
+    if (j < nb) {
+      dft<R0>(v[m]);
+#pragma unroll
+      for (uint32_t r = 0; r < R0; r++) buf[j * R0 + r] = v[m][r];
+    }
+  }
+  __syncthreads();
+  float2*        out  = J.out + (size_t)sym * a.nre;
+  const uint32_t half = a.nre / 2;
+  if constexpr (R3 == 1) {
+    stage_c<N, R0, R1, false>(buf, tw, out, half);
+    stage_c<N, R0 * R1, R2, true>(buf, tw, out, half);
+  } else {
+    stage_c<N, R0, R1, false>(buf, tw, out, half);
+    stage_c<N, R0 * R1, R2, false>(buf, tw, out, half);
+    stage_c<N, R0 * R1 * R2, R3, true>(buf, tw, out, half);
+  }
+}
+
 hipError_t ofdm_launch_rx(const OfdmArgs& a, uint32_t njobs, hipStream_t s)
 {
   if (!njobs) return hipSuccess;
-  hipLaunchKernelGGL(ofdm_rx, dim3(2 * a.nsymb, njobs), dim3(256), 0, s, a);
+  const dim3 g(2 * a.nsymb, njobs), b(256);
+  switch (a.N) { // plans of radix_plan (ue_dl_runtime.cpp)
+    case 128: hipLaunchKernelGGL((ofdm_rx_n<128, 8, 8, 2, 1>), g, b, 0, s, a); break;
+    case 256: hipLaunchKernelGGL((ofdm_rx_n<256, 8, 8, 4, 1>), g, b, 0, s, a); break;
+    case 384: hipLaunchKernelGGL((ofdm_rx_n<384, 3, 8, 8, 2>), g, b, 0, s, a); break;
+    case 512: hipLaunchKernelGGL((ofdm_rx_n<512, 8, 8, 8, 1>), g, b, 0, s, a); break;
+    case 768: hipLaunchKernelGGL((ofdm_rx_n<768, 3, 8, 8, 4>), g, b, 0, s, a); break;
+    case 1024: hipLaunchKernelGGL((ofdm_rx_n<1024, 8, 8, 8, 2>), g, b, 0, s, a); break;
+    case 1536: hipLaunchKernelGGL((ofdm_rx_n<1536, 3, 8, 8, 8>), g, b, 0, s, a); break;
+    case 2048: hipLaunchKernelGGL((ofdm_rx_n<2048, 8, 8, 8, 4>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL(ofdm_rx, g, b, 0, s, a); break;
+  }
   return hipGetLastError();
 }
 
