@@ -13,13 +13,15 @@ namespace mi355 {
 struct HostStaging {
   char*      host = nullptr;
   size_t     cap = 0, used = 0;
-  hipEvent_t ev      = nullptr; // recorded after the last upload from this buffer
-  bool       pending = false;
+  hipEvent_t  ev      = nullptr; // recorded after the last upload from this buffer
+  hipStream_t cs      = nullptr; // copy stream: uploads overlap the compute stream's earlier work
+  bool        pending = false;
 
   ~HostStaging()
   {
     if (pending) (void)hipEventSynchronize(ev);
     if (ev) (void)hipEventDestroy(ev);
+    if (cs) (void)hipStreamDestroy(cs);
     if (host) (void)hipHostFree(host);
   }
   // start a new fill; waits for the previous upload from this buffer if it may still be in flight
@@ -62,16 +64,19 @@ struct HostStaging {
     used += (n + 255) / 256 * 256;
     return p;
   }
-  // one asynchronous copy of everything put so far to dst on stream s
+  // one asynchronous copy of everything put so far to dst, ordered before the work enqueued on s after this
+  // call.  The copy runs on the staging's own stream, so it does not wait behind s's earlier kernels (the
+  // destination must not be in use by them: callers upload into per-call descriptor space).
   hipError_t upload(void* dst, hipStream_t s)
   {
     if (!used) return hipSuccess;
-    hipError_t e = hipMemcpyAsync(dst, host, used, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    if (!cs && (e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking)) != hipSuccess) return e;
     if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventRecord(ev, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(dst, host, used, hipMemcpyHostToDevice, cs)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ev, cs)) != hipSuccess) return e;
     pending = true;
-    return hipSuccess;
+    return hipStreamWaitEvent(s, ev, 0);
   }
 };
 
