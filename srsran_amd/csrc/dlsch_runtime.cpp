@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <stdlib.h>
 #include <map>
 #include <mutex>
 #include <stdio.h>
@@ -21,6 +23,7 @@
 #include "dlsch_internal.h"
 #include "host_staging.h"
 #include "rm_tables.h"
+#include "runtime_internal.h"
 #include "tdec_internal.h"
 
 using namespace mi355;
@@ -330,9 +333,21 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
                            float*                   avg_iterations,
                            void*                    stream)
 {
+  return mi355::dlsch_decode_dev_hook(q, pool, d_e_bits, tbs, ntb, d_data, ret, avg_iterations, stream, mi355::WaitHook{});
+}
+
+} // extern "C"
+
+int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const int16_t* d_e_bits,
+                                 const mi355_dlsch_tb_t* tbs, uint32_t ntb, uint8_t* d_data, int32_t* ret,
+                                 float* avg_iterations, void* stream, mi355::WaitHook hook)
+{
   if (!q || !pool || !tbs || !ret || (ntb && !d_e_bits)) return MI355_ERROR_INVALID_INPUTS;
   if (ntb == 0) return MI355_SUCCESS;
   std::lock_guard<std::mutex> lock(q->mu);
+  static const bool prof = getenv("MI355_HOST_PROF") != nullptr;
+  auto              now  = [] { return std::chrono::steady_clock::now(); };
+  const auto        t0   = now();
   CHECK_HIP(hipSetDevice(q->device));
   hipStream_t s = stream ? (hipStream_t)stream : q->own;
 
@@ -495,6 +510,8 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   }
   CHECK_HIP(dlsch_launch_epilogue(ta, s));
 
+  const auto t1 = now();
+  if (hook.fn) hook.fn(hook.ctx);
   CHECK_HIP(q->back.reserve(rnd(ntb * 4) + ntb * 4));
   CHECK_HIP(hipMemcpyAsync(q->back.host, d_ret, rnd(ntb * 4) + ntb * 4, hipMemcpyDeviceToHost, s));
   CHECK_HIP(hipStreamSynchronize(s));
@@ -503,7 +520,9 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
     if (tbd[t].invalid) ret[t] = MI355_ERROR_INVALID_INPUTS;
   }
   if (avg_iterations) memcpy(avg_iterations, q->back.host + rnd(ntb * 4), ntb * 4);
+  if (prof) {
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    fprintf(stderr, "[mi355 host] dlsch_decode_dev: plan+launch %.1f us, wait+readback %.1f us\n", us(t0, t1), us(t1, now()));
+  }
   return MI355_SUCCESS;
 }
-
-} // extern "C"

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <stdlib.h>
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -526,10 +528,14 @@ int mi355_pdsch_decode_batch(mi355_pdsch_t*           q,
 } // extern "C"
 
 int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi355_pdsch_job_t* jobs,
-                                        uint32_t njobs, mi355_pdsch_res_t* res, void* stream, const float* d_noise)
+                                        uint32_t njobs, mi355_pdsch_res_t* res, void* stream, const float* d_noise,
+                                        WaitHook hook)
 {
   if (!q || !pool || !res || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;
   std::lock_guard<std::mutex> lock(q->mu);
+  static const bool prof = getenv("MI355_HOST_PROF") != nullptr;
+  auto              now  = [] { return std::chrono::steady_clock::now(); };
+  const auto        t0   = now();
   CHECK_HIP(hipSetDevice(q->device));
   hipStream_t          s = stream ? (hipStream_t)stream : q->own;
   std::vector<JobPlan> plans(njobs);
@@ -539,8 +545,13 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
     // noise estimate left in device memory by the channel estimator (ZF ignores it, pdsch.c:934)
     if (d_noise && jobs[i].cfg.decoder_type != MI355_MIMO_DECODER_ZF) plans[i].dev.noise_dev = d_noise + i;
   }
+  const auto t1 = now();
   int r = run_frontend(q, jobs, plans, s);
   if (r) return r;
+  if (prof) {
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    fprintf(stderr, "[mi355 host] pdsch: plan %.1f us, frontend launch %.1f us\n", us(t0, t1), us(t1, now()));
+  }
   q->last.swap(plans);
   const std::vector<JobPlan>& plan = q->last;
 
@@ -571,8 +582,9 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
     std::vector<int32_t>   ret(kv.second.size());
     std::vector<float>     avg(kv.second.size());
     if ((r = mi355_dlsch_set_max_iterations(q->dlsch, its))) return r;
-    r = mi355_dlsch_decode_dev(q->dlsch, pool, q->e_arena, kv.second.data(), (uint32_t)kv.second.size(), nullptr,
-                               ret.data(), avg.data(), s);
+    r = dlsch_decode_dev_hook(q->dlsch, pool, q->e_arena, kv.second.data(), (uint32_t)kv.second.size(), nullptr,
+                              ret.data(), avg.data(), s, hook);
+    hook = WaitHook{}; // once
     if (r) return r;
     const auto& who = by_its[its];
     for (size_t k = 0; k < who.size(); k++) {

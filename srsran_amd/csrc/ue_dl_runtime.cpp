@@ -2,7 +2,9 @@
 // channel estimation over batches of subframes, and the srslte_ue_dl-level object owning the PDSCH receiver.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
+#include <stdlib.h>
 #include <mutex>
 #include <stdio.h>
 #include <string.h>
@@ -77,6 +79,8 @@ struct mi355_ue_dl {
   char*          scratch = nullptr;
   size_t         scratch_cap = 0;
   HostStaging    st_ofdm, st_chest, back; // pinned descriptor uploads / estimator read-back
+  hipStream_t    side     = nullptr;       // estimator read-back + fill_res overlapping the PDSCH decode
+  hipEvent_t     ev_chest = nullptr;
   std::mutex     mu;
 };
 
@@ -293,6 +297,40 @@ static int chest_finish(mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const
   return MI355_SUCCESS;
 }
 
+// chest_finish overlapped with the decode: the read-back runs on the side stream once the estimator has
+// finished, and fill_res runs on the calling thread as the DL-SCH's wait hook (after every decode kernel is
+// enqueued, before the final wait).
+struct ChestFill {
+  const mi355_ue_dl_t*        q;
+  const mi355_chest_dl_cfg_t* cfg;
+  const float*                out;
+  uint32_t                    njobs;
+  mi355_chest_dl_res_t*       res;
+  bool                        done;
+};
+
+static void chest_fill_cb(void* p)
+{
+  const ChestFill* f = (const ChestFill*)p;
+  if (hipStreamSynchronize(f->q->side) != hipSuccess) return; // the read-back has landed
+  const uint32_t   k = f->q->cell.nof_ports * f->q->nof_rx * 5;
+  for (uint32_t i = 0; i < f->njobs; i++) fill_res(f->q, f->cfg, &f->out[(size_t)i * k], &f->res[i]);
+  ((ChestFill*)p)->done = true;
+}
+
+static int chest_finish_async(mi355_ue_dl_t* q, ChestFill* f, const float* d_out, hipStream_t s)
+{
+  if (!q->side) CHECK_HIP(hipStreamCreateWithFlags(&q->side, hipStreamNonBlocking));
+  if (!q->ev_chest) CHECK_HIP(hipEventCreateWithFlags(&q->ev_chest, hipEventDisableTiming));
+  const size_t nout = (size_t)f->njobs * q->cell.nof_ports * q->nof_rx * 5;
+  CHECK_HIP(q->back.reserve(nout * 4));
+  f->out = (const float*)q->back.host;
+  CHECK_HIP(hipEventRecord(q->ev_chest, s));
+  CHECK_HIP(hipStreamWaitEvent(q->side, q->ev_chest, 0));
+  CHECK_HIP(hipMemcpyAsync(q->back.host, d_out, nout * 4, hipMemcpyDeviceToHost, q->side));
+  return MI355_SUCCESS;
+}
+
 static int chest_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, const mi355_chest_dl_cfg_t* cfg,
                      mi355_chest_dl_res_t* res, hipStream_t s, size_t offset = 0)
 {
@@ -340,6 +378,8 @@ void mi355_ue_dl_destroy(mi355_ue_dl_t* q)
   (void)hipFree(q->scratch);
   mi355_pdsch_destroy(q->pdsch);
   if (q->own) (void)hipStreamDestroy(q->own);
+  if (q->side) (void)hipStreamDestroy(q->side);
+  if (q->ev_chest) (void)hipEventDestroy(q->ev_chest);
   delete q;
 }
 
@@ -395,6 +435,9 @@ int mi355_ue_dl_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, co
   if (!q || !pool || !res || !chest || (njobs && (!sfjobs || !sfs || !cfgs || !payloads)))
     return MI355_ERROR_INVALID_INPUTS;
   std::lock_guard<std::mutex> lock(q->mu);
+  static const bool prof = getenv("MI355_HOST_PROF") != nullptr; // host-side phase timing to stderr
+  auto              now  = [] { return std::chrono::steady_clock::now(); };
+  const auto        t0   = now();
   CHECK_HIP(hipSetDevice(q->device));
   hipStream_t s    = stream ? (hipStream_t)stream : q->own;
   size_t      used = 0;
@@ -416,8 +459,21 @@ int mi355_ue_dl_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, co
     j.payload[0] = payloads[2 * i];
     j.payload[1] = payloads[2 * i + 1];
   }
-  if ((r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), njobs, res, s, d_noise))) return r;
-  return chest_finish(q, chest_cfg, d_out, njobs, chest, s);
+  ChestFill fill{q, chest_cfg, nullptr, njobs, chest, false};
+  if ((r = chest_finish_async(q, &fill, d_out, s))) return r;
+  const auto t1 = now();
+  r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), njobs, res, s, d_noise, WaitHook{chest_fill_cb, &fill});
+  const auto t2 = now();
+  CHECK_HIP(hipStreamSynchronize(q->side));
+  if (r) return r;
+  if (!fill.done) chest_fill_cb(&fill); // no DL-SCH work in the batch: the hook did not run
+  if (prof) {
+    const auto t3 = now();
+    auto       us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    fprintf(stderr, "[mi355 host] ue_dl_decode_batch: launch ofdm/chest + jobs %.1f us, pdsch+dlsch (incl. sync) %.1f us, "
+                    "chest fill wait %.1f us\n", us(t0, t1), us(t1, t2), us(t2, t3));
+  }
+  return r;
 }
 
 int mi355_ue_dl_decode_pdsch_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, const mi355_dl_sf_job_t* sfjobs,
