@@ -19,80 +19,108 @@ namespace mi355 {
 // sums for E > N), then the decoder buffer is written in order from LDS gathers.
 constexpr uint32_t RM_LDS     = 3 * 6144 + 12; // N of the largest code block
 constexpr uint32_t RM_THREADS = 1024;
-constexpr int      RM_IT      = (3 * (6144 + 32) + 12 + 2 * RM_THREADS - 1) / (2 * RM_THREADS); // buffer pairs per thread
-constexpr int      RM_E_IT    = (RM_LDS + 2 * RM_THREADS - 1) / (2 * RM_THREADS);             // LLR pairs per thread
+constexpr int      RM_Q       = (3 * (6144 + 32) + 12 + 8 * RM_THREADS - 1) / (8 * RM_THREADS); // buffer quads per thread
+constexpr int      RM_EQ      = (RM_LDS + 8 * RM_THREADS - 1) / (8 * RM_THREADS);             // LLR quads per thread
 
 __device__ __forceinline__ uint32_t add_pairs(uint32_t a, uint32_t b) // two wrapping int16 additions
 {
   return ((a + b) & 0xffffu) | (((a >> 16) + (b >> 16)) << 16);
 }
 
+// u32 pairs 4q .. 4q+3 of p (pairs >= lim read as `fill`): one 16-byte load when whole and aligned
+__device__ __forceinline__ uint4 ld_quad(const uint32_t* p, uint32_t q, uint32_t lim, bool al16, uint32_t fill)
+{
+  const uint32_t i = 4 * q;
+  if (al16 && i + 3 < lim) return *(const uint4*)(p + i);
+  return make_uint4(i < lim ? p[i] : fill, i + 1 < lim ? p[i + 1] : fill, i + 2 < lim ? p[i + 2] : fill,
+                    i + 3 < lim ? p[i + 3] : fill);
+}
+
+// LLR pair r2 of e (int16 pairs; e 4-byte aligned or not)
+__device__ __forceinline__ uint32_t ld_llr_pair(const int16_t* e, uint32_t r2, bool al4)
+{
+  return al4 ? ((const uint32_t*)e)[r2] : ((uint32_t)(uint16_t)e[2 * r2] | ((uint32_t)(uint16_t)e[2 * r2 + 1] << 16));
+}
+
 // Every load of a thread is issued up front (inverse table, LLRs, old softbuffer words: fully unrolled,
-// independent of one another), so a block pays the memory latency about twice instead of once per
-// loop trip.  Qm is even, so n_e, rp and N are even and the LLRs are handled as int16 pairs.
+// independent of one another, 16 bytes per lane), so a block pays the memory latency about twice instead of
+// once per loop trip; the decoder buffer is written with 16-byte stores.  Qm is even, so n_e, rp and N are
+// even and the LLRs are handled as int16 pairs.
 __global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
 {
-  __shared__ uint32_t acc32[RM_LDS / 2 + 2];
+  __shared__ __attribute__((aligned(16))) uint32_t acc32[RM_LDS / 2 + 4];
   const uint16_t* acc = (const uint16_t*)acc32;
   const CbDesc&   d   = a.desc[blockIdx.x];
   if (a.sb_crc[d.slot]) return; // CB already decoded in an earlier transmission (sch.c:385)
   const uint32_t  N = a.N, tid = threadIdx.x;
   const uint32_t  n_e = d.n_e, first2 = min(n_e, N) / 2, N2 = N / 2;
-  const uint32_t* inv32 = (const uint32_t*)a.inv[d.rv]; // 4-byte aligned (buflen even)
+  const uint32_t* inv32 = (const uint32_t*)a.inv[d.rv]; // hipMalloc'd: 16-byte aligned
   const uint32_t  pairs = a.buflen / 2;
   const bool      fresh = a.fresh[d.slot] != 0;
   uint32_t*       sb    = (uint32_t*)(a.sb + (size_t)d.slot * a.sb_stride);
+  const bool      sb16  = ((uintptr_t)sb & 15) == 0;
+  const int16_t*  e     = a.e + d.e_off + d.rp;
+  const bool      e4    = ((uintptr_t)e & 3) == 0, e16 = ((uintptr_t)e & 15) == 0;
 
-  uint32_t iv[RM_IT];
+  uint4 iv[RM_Q], old[RM_Q], ev[RM_EQ];
 #pragma unroll
-  for (int k = 0; k < RM_IT; k++) {
-    const uint32_t jp = tid + k * RM_THREADS;
-    iv[k]             = jp < pairs ? inv32[jp] : 0xffffffffu;
-  }
+  for (int k = 0; k < RM_Q; k++) iv[k] = ld_quad(inv32, tid + k * RM_THREADS, pairs, true, 0xffffffffu);
   // pass 0: the first wrap initialises (positions >= n_e get 0)
-  const int16_t* e   = a.e + d.e_off + d.rp;
-  const bool     al4 = ((uintptr_t)e & 3) == 0;
-  uint32_t       ev[RM_E_IT];
 #pragma unroll
-  for (int k = 0; k < RM_E_IT; k++) {
-    const uint32_t r2 = tid + k * RM_THREADS;
-    if (r2 < first2) {
-      ev[k] = al4 ? ((const uint32_t*)e)[r2]
-                  : ((uint32_t)(uint16_t)e[2 * r2] | ((uint32_t)(uint16_t)e[2 * r2 + 1] << 16));
+  for (int k = 0; k < RM_EQ; k++) {
+    const uint32_t q = tid + k * RM_THREADS;
+    if (e16) {
+      ev[k] = ld_quad((const uint32_t*)e, q, first2, true, 0u);
     } else {
-      ev[k] = 0;
+      ev[k] = make_uint4(4 * q < first2 ? ld_llr_pair(e, 4 * q, e4) : 0u, 4 * q + 1 < first2 ? ld_llr_pair(e, 4 * q + 1, e4) : 0u,
+                         4 * q + 2 < first2 ? ld_llr_pair(e, 4 * q + 2, e4) : 0u,
+                         4 * q + 3 < first2 ? ld_llr_pair(e, 4 * q + 3, e4) : 0u);
     }
   }
-  uint32_t old[RM_IT];
 #pragma unroll
-  for (int k = 0; k < RM_IT; k++) {
-    const uint32_t jp = tid + k * RM_THREADS;
-    old[k]            = (!fresh && jp < pairs) ? sb[jp] : 0u;
-  }
+  for (int k = 0; k < RM_Q; k++)
+    old[k] = fresh ? make_uint4(0u, 0u, 0u, 0u) : ld_quad(sb, tid + k * RM_THREADS, pairs, sb16, 0u);
 #pragma unroll
-  for (int k = 0; k < RM_E_IT; k++) {
-    const uint32_t r2 = tid + k * RM_THREADS;
-    if (r2 < N2) acc32[r2] = ev[k];
+  for (int k = 0; k < RM_EQ; k++) {
+    const uint32_t i = 4 * (tid + k * RM_THREADS);
+    if (i + 3 < N2) {
+      *(uint4*)&acc32[i] = ev[k];
+    } else {
+      if (i < N2) acc32[i] = ev[k].x;
+      if (i + 1 < N2) acc32[i + 1] = ev[k].y;
+      if (i + 2 < N2) acc32[i + 2] = ev[k].z;
+    }
   }
   // later wraps (E > N) accumulate
   for (uint32_t base = N; base < n_e; base += N) {
     __syncthreads();
     const uint32_t lim2 = min(N, n_e - base) / 2;
-    for (uint32_t r2 = tid; r2 < lim2; r2 += RM_THREADS) {
-      const uint32_t v = al4 ? ((const uint32_t*)(e + base))[r2]
-                             : ((uint32_t)(uint16_t)e[base + 2 * r2] | ((uint32_t)(uint16_t)e[base + 2 * r2 + 1] << 16));
-      acc32[r2] = add_pairs(acc32[r2], v);
-    }
+    for (uint32_t r2 = tid; r2 < lim2; r2 += RM_THREADS) acc32[r2] = add_pairs(acc32[r2], ld_llr_pair(e + base, r2, e4));
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < RM_IT; k++) {
-    const uint32_t jp = tid + k * RM_THREADS;
-    const uint32_t r0 = iv[k] & 0xffffu, r1 = iv[k] >> 16;
-    const bool     h0 = r0 != RM_NONE && r0 < n_e, h1 = r1 != RM_NONE && r1 < n_e;
-    if (jp >= pairs || (!fresh && !h0 && !h1)) continue;
-    const uint32_t s0 = h0 ? acc[r0] : 0u, s1 = h1 ? acc[r1] : 0u;
-    sb[jp]            = add_pairs(old[k], s0 | (s1 << 16));
+  for (int k = 0; k < RM_Q; k++) {
+    const uint32_t q = tid + k * RM_THREADS, i = 4 * q;
+    if (i >= pairs) continue;
+    const uint32_t w[4] = {iv[k].x, iv[k].y, iv[k].z, iv[k].w};
+    const uint32_t o[4] = {old[k].x, old[k].y, old[k].z, old[k].w};
+    uint32_t       v[4];
+    bool           any = fresh;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t r0 = w[c] & 0xffffu, r1 = w[c] >> 16;
+      const bool     h0 = r0 != RM_NONE && r0 < n_e, h1 = r1 != RM_NONE && r1 < n_e;
+      any |= h0 || h1;
+      v[c] = add_pairs(o[c], (h0 ? acc[r0] : 0u) | ((h1 ? acc[r1] : 0u) << 16));
+    }
+    if (!any) continue; // nothing to add to an old buffer
+    if (sb16 && i + 3 < pairs) {
+      *(uint4*)(sb + i) = make_uint4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        if (i + c < pairs) sb[i + c] = v[c];
+    }
   }
 }
 

@@ -5,6 +5,8 @@
 
 namespace mi355 {
 
+constexpr uint32_t EQ_BLOCK_ITEMS = 1024; // equaliser work items per workgroup (256 threads x 4)
+
 constexpr uint32_t PDSCH_GOLD_MAX = 14u * 12u * 110u * 8u; // longest codeword: 100+ PRB x 14 symbols x 256QAM
 
 // One PDSCH decode job after host planning.
@@ -12,22 +14,30 @@ struct PdschJobDev {
   const float2*   y[2];    // received grids per rx antenna
   const float2*   h[4][2]; // channel estimates [port][rx]
   const uint16_t* map;     // grid index of each PDSCH RE, srslte_pdsch_get order
+  const uint16_t* imap;    // RE index of grid index g0 + t (0xffff: not a PDSCH RE)
+  uint32_t        g0;      // first grid index of the allocation
   float2*         d[2];    // equalised + layer-demapped symbols per codeword (q->d)
   float*          csi[2];  // CSI per codeword symbol (q->csi)
-  uint32_t*       cmax;    // [2] running max of csi[cw] (float bits, csi >= 0)
+  uint32_t*       cmax;    // [2][cmax_stride]: per-block maxima of csi[cw] (float bits, csi >= 0)
+  uint32_t        cmax_stride;
   uint32_t        nof_re, nof_rx, nof_ports, nof_layers, scheme, cb;
   uint32_t        row;       // 12 * nof_prb: grid index -> OFDM symbol l'
+  uint32_t        row_magic; // floor(2^32 / row) + 1: l' = umulhi(g, row_magic), exact for g < 2^16
+  uint32_t        h_invariant; // channel estimates identical in every OFDM symbol (AVERAGE estimator output):
+                               // read them from the first symbol's row, which stays in cache
   uint32_t        rhob_mask; // OFDM symbols l' scaled by 1/rho_b (apply_power_allocation, pdsch.c:589-607)
   float           rhob_inv, scaling, noise;
   const float*    noise_dev; // nullable: noise estimate produced on the device (chest), used instead of noise
-  uint32_t        units;     // kernel A work items
+  uint32_t        units;     // kernel A work items: grid positions g0 + u (single-RE schemes), SFBC pairs / quads
 };
 
 // One codeword (TB) symbol -> LLR job.
 struct PdschCwDev {
   const float2* d;
   const float*  csi;
-  const uint32_t* cmax;
+  const uint32_t* cmax;   // the job's per-block csi maxima of this codeword (nparts of them)
+  uint32_t        nparts;
+  uint32_t*       cmax_final; // their maximum (pdsch_cmax_reduce)
   int16_t*      e;
   const uint32_t* scr; // packed descrambling sequence of c_init (cached per c_init)
   uint32_t      nof_re, nof_bits, qm, c_init, csi_enable;

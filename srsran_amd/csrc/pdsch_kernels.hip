@@ -78,14 +78,6 @@ __device__ __forceinline__ void mmse_2x2_csi(cf y0, cf y1, cf h00, cf h01, cf h1
 // max in the unsigned order of the bit patterns (the order fold_max reduces in; IEEE order for csi >= 0)
 __device__ __forceinline__ float bmax(float a, float b) { return __uint_as_float(max(__float_as_uint(a), __float_as_uint(b))); }
 
-__device__ __forceinline__ void fold_max(uint32_t* m, float v)
-{
-  // csi >= 0: IEEE order == unsigned order of the bit patterns.  Reduce over the wave first.
-  uint32_t b = __float_as_uint(v);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_max(gptr(m), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 } // namespace
 
@@ -102,7 +94,7 @@ __device__ __forceinline__ void eq_one(const PdschJobDev& J, uint32_t u, float n
     auto           Y   = [&](uint32_t r, uint32_t i) {
       const uint32_t g = map[i];
       cf             v = ld(gptr(J.y[r]), g);
-      if ((J.rhob_mask >> (g / J.row)) & 1u) v = v * J.rhob_inv;
+      if ((J.rhob_mask >> __umulhi(g, J.row_magic)) & 1u) v = v * J.rhob_inv;
       return v;
     };
     auto H = [&](uint32_t p, uint32_t r, uint32_t i) { return ld(gptr(J.h[p][r]), map[i]); };
@@ -248,13 +240,13 @@ __device__ __forceinline__ void eq_one(const PdschJobDev& J, uint32_t u, float n
 }
 
 
-constexpr int EQ_U = 4; // work items per thread: all their gathers are issued before any arithmetic
+constexpr int EQ_U = EQ_BLOCK_ITEMS / 256; // work items per thread: all their gathers are issued before any arithmetic
 
 // The received symbol of grid index g with rho_b applied (apply_power_allocation, pdsch.c:589-607)
 __device__ __forceinline__ cf y_at(const PdschJobDev& J, uint32_t r, uint32_t g)
 {
   cf v = ld(gptr(J.y[r]), g);
-  if (J.rhob_mask && ((J.rhob_mask >> (g / J.row)) & 1u)) v = v * J.rhob_inv;
+  if (J.rhob_mask && ((J.rhob_mask >> __umulhi(g, J.row_magic)) & 1u)) v = v * J.rhob_inv;
   return v;
 }
 
@@ -273,23 +265,38 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
     for (int k = 0; k < EQ_U; k++)
       if (base + k * 256 < J.units) eq_one(J, base + k * 256, noise, m0, m1);
   } else {
-    const GLB uint16_t* map = gptr(J.map);
-    const uint32_t      nrx = J.nof_rx;
-    cf                  Y[EQ_U][2], H[EQ_U][4]; // H: [p * 2 + r] (port 0: [r])
-    uint32_t            g[EQ_U];
+    // grid-driven: work item u is grid position g0 + u; its RE index comes from the inverse map, loaded in
+    // parallel with the symbols.  Every load is unconditional (out-of-span items and absent antennas read a
+    // valid address whose value is discarded) and rho_b is a multiplier chosen from g, so the compiler issues
+    // all gathers before the first wait.
+    const uint32_t      nrx = J.nof_rx, units = J.units, g0 = J.g0, row = J.row, magic = J.row_magic;
+    const uint32_t      rmask = J.rhob_mask;
+    const float         rinv  = J.rhob_inv;
+    const bool          hinv  = J.h_invariant != 0;
+    const GLB uint16_t* imap  = gptr(J.imap);
+    const GLB float2*   yp[2] = {gptr(J.y[0]), gptr(nrx > 1 ? J.y[1] : J.y[0])};
+    const GLB float2*   hp[4]; // [p * 2 + r]
 #pragma unroll
-    for (int k = 0; k < EQ_U; k++) g[k] = base + k * 256 < J.units ? map[base + k * 256] : 0u;
+    for (int p = 0; p < 2; p++)
+#pragma unroll
+      for (int r = 0; r < 2; r++)
+        hp[p * 2 + r] = gptr(J.h[(p == 0 || J.scheme != 0) ? p : 0][(uint32_t)r < nrx ? r : 0]);
+    cf       Y[EQ_U][2], H[EQ_U][4];
+    uint32_t re[EQ_U];
 #pragma unroll
     for (int k = 0; k < EQ_U; k++) {
-      const bool lv = base + k * 256 < J.units;
+      const bool     lv = base + k * 256 < units;
+      const uint32_t u  = lv ? base + k * 256 : 0u;
+      const uint32_t g  = g0 + u;
+      const uint32_t l  = __umulhi(g, magic); // OFDM symbol of g
+      const uint32_t gh = hinv ? g - l * row : g;
+      re[k]             = imap[u];
+      if (!lv) re[k] = 0xffffu;
+      const float sc = ((rmask >> l) & 1u) ? rinv : 1.0f; // x * 1.0f is exact
 #pragma unroll
-      for (int r = 0; r < 2; r++) {
-        const bool rr = lv && (uint32_t)r < nrx;
-        Y[k][r]       = rr ? y_at(J, r, g[k]) : mk(0.f, 0.f);
+      for (int r = 0; r < 2; r++) Y[k][r] = ld(yp[r], g) * sc;
 #pragma unroll
-        for (int p = 0; p < 2; p++)
-          H[k][p * 2 + r] = (rr && (p == 0 || J.scheme != 0)) ? ld(gptr(J.h[p][r]), g[k]) : mk(0.f, 0.f);
-      }
+      for (int q = 0; q < 4; q++) H[k][q] = ld(hp[q], gh);
     }
     GLB float2* d0   = gptr(J.d[0]);
     GLB float2* d1   = gptr(J.d[1]);
@@ -297,8 +304,8 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
     GLB float*  csi1 = gptr(J.csi[1]);
 #pragma unroll
     for (int k = 0; k < EQ_U; k++) {
-      const uint32_t i = base + k * 256;
-      if (i >= J.units) continue;
+      const uint32_t i = re[k];
+      if (i == 0xffffu) continue; // past the span, or a grid position that is not a PDSCH RE
       if (J.scheme == 0) { // srslte_predecoding_single_csi scalar formula (precoding.c:345-355)
         cf    r  = mk(0.f, 0.f);
         float hh = 0.f;
@@ -368,8 +375,26 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
       }
     }
   }
-  fold_max(&J.cmax[0], m0);
-  if (J.nof_layers == 2 && J.scheme >= 2) fold_max(&J.cmax[1], m1);
+  // per-block csi maxima (csi_correction's srslte_vec_max_fi, pdsch.c:653) for the LLR kernel: wave reduction,
+  // then one store per block and codeword (no atomics)
+  __shared__ uint32_t red[2][4];
+  uint32_t            b0 = __float_as_uint(m0), b1 = __float_as_uint(m1);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    b0 = max(b0, (uint32_t)__shfl_xor((int)b0, o, 64));
+    b1 = max(b1, (uint32_t)__shfl_xor((int)b1, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = b0;
+    red[1][threadIdx.x >> 6] = b1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    GLB uint32_t* cm = gptr(J.cmax);
+    cm[blockIdx.x]   = max(max(red[0][0], red[0][1]), max(red[0][2], red[0][3]));
+    if (J.nof_layers == 2 && J.scheme >= 2)
+      cm[J.cmax_stride + blockIdx.x] = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
+  }
 }
 
 // ---------------------------------------------------------------------------- LLRs
@@ -517,7 +542,7 @@ template <int QM> __device__ __forceinline__ void store_llrs(GLB int16_t* e, con
     if ((uint32_t)k < nb) e[k] = o[k];
 }
 
-template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, uint32_t pr)
+template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, uint32_t pr, uint32_t cmax_bits)
 {
   const uint32_t n  = C.nof_re;
   const uint32_t s0 = 2 * pr, ns = min(2u, n - s0);
@@ -557,7 +582,7 @@ template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, 
     if ((bits >> (sh + k)) & 1ull) o[k] = (int16_t)(uint16_t)(-(int32_t)o[k]);
   if (C.csi_enable) { // csi_correction (pdsch.c:628-741), SSE path
     const uint32_t nsym  = C.nof_bits / QM;
-    const float    cmax  = nsym ? __uint_as_float(*gptr(C.cmax)) : 1.0f;
+    const float    cmax  = nsym ? __uint_as_float(cmax_bits) : 1.0f;
     const float    scale = 32767.0f / cmax;
     auto           CV    = [&](float v) { return sat16(x86_cvt_i32(rintf(v * scale))); }; // _mm_cvtps_pi16
     const bool     body  = (QM == 4 || QM == 8) || ((QM == 2 || QM == 6) && ns == 2);
@@ -603,13 +628,25 @@ __global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ 
   const PdschCwDev& C  = cws[blockIdx.y];
   const uint32_t    pr = blockIdx.x * 256 + threadIdx.x;
   if (pr >= C.pairs) return;
+  const uint32_t cm = C.csi_enable ? *gptr(C.cmax_final) : 0u;
   switch (C.qm) {
-    case 1: llr_pair<1>(C, pr); break;
-    case 2: llr_pair<2>(C, pr); break;
-    case 4: llr_pair<4>(C, pr); break;
-    case 6: llr_pair<6>(C, pr); break;
-    default: llr_pair<8>(C, pr); break;
+    case 1: llr_pair<1>(C, pr, cm); break;
+    case 2: llr_pair<2>(C, pr, cm); break;
+    case 4: llr_pair<4>(C, pr, cm); break;
+    case 6: llr_pair<6>(C, pr, cm); break;
+    default: llr_pair<8>(C, pr, cm); break;
   }
+}
+
+// the codeword's csi maximum from the equaliser's per-block maxima
+__global__ __launch_bounds__(256) void pdsch_cmax_reduce(const PdschCwDev* __restrict__ cws, uint32_t ncw)
+{
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= ncw) return;
+  const PdschCwDev& C = cws[c];
+  uint32_t          b = 0;
+  for (uint32_t k = 0; k < C.nparts; k++) b = max(b, gptr(C.cmax)[k]);
+  *gptr(C.cmax_final) = b;
 }
 
 hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, uint32_t njobs, uint32_t max_units, hipStream_t s)
@@ -633,6 +670,7 @@ hipError_t pdsch_launch_llr(const PdschCwDev* cws, uint32_t ncw, uint32_t max_pa
 {
   const uint32_t nblk = (max_pairs + 255) / 256;
   if (!nblk) return hipSuccess;
+  hipLaunchKernelGGL(pdsch_cmax_reduce, dim3((ncw + 255) / 256), dim3(256), 0, s, cws, ncw);
   for (uint32_t c0 = 0; c0 < ncw; c0 += 65535)
     hipLaunchKernelGGL(pdsch_llr, dim3(nblk, std::min(65535u, ncw - c0)), dim3(256), 0, s, cws + c0);
   return hipGetLastError();

@@ -152,6 +152,14 @@ uint32_t mod_bits(uint32_t mod)
   return 0;
 }
 
+// RE extraction map of one (allocation, cfi, subframe): d = [RE index -> grid index (n) | pad | grid index
+// g0 + t -> RE index or 0xffff (g1 - g0)], the inverse letting the single-RE equalisers walk the grid
+struct MapEntry {
+  uint16_t* d = nullptr;
+  uint32_t  n = 0, g0 = 0, g1 = 0;
+  const uint16_t* inv() const { return d + ((n + 1) & ~1u); }
+};
+
 struct JobPlan {
   PdschJobDev dev{};
   uint32_t    cw_of_tb[2]{};
@@ -169,9 +177,9 @@ struct mi355_pdsch {
   mi355_dlsch_t*                       dlsch  = nullptr;
   uint32_t                             max_its = 10; // SRSLTE_PDSCH_MAX_TDEC_ITERS
   uint32_t*                            gold   = nullptr;
-  std::map<std::string, std::pair<uint16_t*, uint32_t>> maps; // extraction maps in HBM + RE count
-  const uint16_t*                      last_map = nullptr; // the previous lookup (key below)
-  uint32_t                             last_map_n = 0, last_map_hdr[4]{};
+  std::map<std::string, MapEntry>      maps; // extraction maps in HBM
+  MapEntry                             last_map{};   // the previous lookup (key below)
+  uint32_t                             last_map_hdr[4]{};
   uint8_t                              last_map_prb[2][MI355_MAX_PRB]{};
   std::map<uint32_t, uint32_t*>        scr;  // packed descrambling sequences per c_init (HBM)
   char*                                scratch = nullptr;
@@ -200,16 +208,14 @@ static int get_scratch(mi355_pdsch_t* q, size_t bytes, char** p)
   return MI355_SUCCESS;
 }
 
-static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi, uint32_t sf, const uint16_t** out,
-                   uint32_t* count)
+static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi, uint32_t sf, MapEntry* out)
 {
   // consecutive jobs of a batch usually share the allocation: compare with the previous lookup first
   const uint32_t np = q->cell.nof_prb;
-  if (q->last_map && q->last_map_hdr[0] == cfi && q->last_map_hdr[1] == sf && q->last_map_hdr[2] == g.nof_symb_slot[0] &&
+  if (q->last_map.d && q->last_map_hdr[0] == cfi && q->last_map_hdr[1] == sf && q->last_map_hdr[2] == g.nof_symb_slot[0] &&
       q->last_map_hdr[3] == g.nof_symb_slot[1] && !memcmp(q->last_map_prb[0], g.prb_idx[0], np) &&
       !memcmp(q->last_map_prb[1], g.prb_idx[1], np)) {
-    *out   = q->last_map;
-    *count = q->last_map_n;
+    *out = q->last_map;
     return MI355_SUCCESS;
   }
   std::string key;
@@ -222,23 +228,28 @@ static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi,
   if (it == q->maps.end()) {
     if (q->maps.size() >= 8192) { // bound the cache
       CHECK_HIP(hipDeviceSynchronize());
-      for (auto& kv : q->maps) (void)hipFree(kv.second.first);
+      for (auto& kv : q->maps) (void)hipFree(kv.second.d);
       q->maps.clear();
-      q->last_map = nullptr;
+      q->last_map = MapEntry{};
     }
     std::vector<uint16_t> idx;
     idx.reserve(14 * 12 * q->cell.nof_prb);
     walk_map(q->cell, g, cfi, sf, [&](uint32_t, uint32_t p) { idx.push_back((uint16_t)p); });
-    uint16_t*      d = nullptr;
-    const uint32_t n = (uint32_t)idx.size();
-    CHECK_HIP(hipMalloc(&d, std::max<size_t>(n, 1) * sizeof(uint16_t)));
-    if (n) CHECK_HIP(hipMemcpy(d, idx.data(), n * 2, hipMemcpyHostToDevice));
-    it = q->maps.emplace(key, std::make_pair(d, n)).first;
+    MapEntry e;
+    e.n = (uint32_t)idx.size();
+    if (e.n) {
+      e.g0 = *std::min_element(idx.begin(), idx.end());
+      e.g1 = *std::max_element(idx.begin(), idx.end()) + 1u;
+    }
+    std::vector<uint16_t> all(((e.n + 1) & ~1u) + (e.g1 - e.g0), 0xffff);
+    std::copy(idx.begin(), idx.end(), all.begin());
+    for (uint32_t i = 0; i < e.n; i++) all[((e.n + 1) & ~1u) + idx[i] - e.g0] = (uint16_t)i;
+    CHECK_HIP(hipMalloc(&e.d, std::max<size_t>(all.size(), 1) * sizeof(uint16_t)));
+    if (!all.empty()) CHECK_HIP(hipMemcpy(e.d, all.data(), all.size() * 2, hipMemcpyHostToDevice));
+    it = q->maps.emplace(key, e).first;
   }
-  *out   = it->second.first;
-  *count = it->second.second;
-  q->last_map       = it->second.first;
-  q->last_map_n     = it->second.second;
+  *out        = it->second;
+  q->last_map = it->second;
   const uint32_t h[4] = {cfi, sf, g.nof_symb_slot[0], g.nof_symb_slot[1]};
   memcpy(q->last_map_hdr, h, sizeof(h));
   memcpy(q->last_map_prb[0], g.prb_idx[0], np);
@@ -274,9 +285,13 @@ static int plan_job(mi355_pdsch_t* q, const mi355_pdsch_job_t& j, const mi355_pd
     for (uint32_t p = 0; p < np; p++)
       if (!j.ce[p][r]) return MI355_ERROR_INVALID_INPUTS;
   }
-  uint32_t nre = 0;
-  int      rr  = get_map(q, g, j.sf.cfi, j.sf.tti % 10, &D.map, &nre);
+  MapEntry me;
+  int      rr = get_map(q, g, j.sf.cfi, j.sf.tti % 10, &me);
   if (rr) return rr;
+  const uint32_t nre = me.n;
+  D.map              = me.d;
+  D.imap             = me.inv();
+  D.g0               = me.g0;
   if (nre != g.nof_re) return MI355_ERROR; // "Error expecting %d symbols but got %d" (pdsch.c:949-960)
 
   // power allocation (pdsch.c:575-611, 926-932)
@@ -308,11 +323,13 @@ static int plan_job(mi355_pdsch_t* q, const mi355_pdsch_job_t& j, const mi355_pd
   D.scheme     = sch;
   D.cb         = cb;
   D.row        = 12 * c.nof_prb;
+  D.row_magic  = (uint32_t)((1ull << 32) / D.row + 1);
   D.rhob_mask  = rmask;
   D.rhob_inv   = rhob_inv;
   D.scaling    = scaling;
   D.noise      = cfg.decoder_type == MI355_MIMO_DECODER_ZF ? 0.0f : j.noise_estimate;
-  D.units      = sch == MI355_TXSCHEME_DIVERSITY ? (np == 2 ? (nre + 1) / 2 : (nre + 3) / 4) : nre;
+  // single-RE schemes walk the grid span of the allocation (inverse map), SFBC the RE pairs / quads
+  D.units      = sch == MI355_TXSCHEME_DIVERSITY ? (np == 2 ? (nre + 1) / 2 : (nre + 3) / 4) : me.g1 - me.g0;
   for (uint32_t t = 0; t < 2; t++) {
     const mi355_ra_tb_t& tb = g.tb[t];
     P.decode[t]             = tb.enabled && !(res && res[t].crc);
@@ -383,9 +400,11 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   const size_t ncw = cws.size();
   // device scratch: [staged descriptors | d | csi | e]; the staged part mirrors the pinned host buffer
   const size_t staged = staged_size(njobs * sizeof(PdschJobDev)) + staged_size(ncw * sizeof(PdschCwDev)) +
-                        staged_size(new_ci.size() * 4) + staged_size(new_ci.size() * 8) + staged_size(njobs * 8);
-  auto         rnd  = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t need = staged + rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2);
+                        staged_size(new_ci.size() * 4) + staged_size(new_ci.size() * 8);
+  auto           rnd    = [](size_t b) { return (b + 255) / 256 * 256; };
+  const uint32_t nparts = (max_units + EQ_BLOCK_ITEMS - 1) / EQ_BLOCK_ITEMS; // equaliser blocks per job
+  const size_t   need   = staged + rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2) + rnd((size_t)njobs * 2 * nparts * 4) +
+                        rnd(ncw * 4);
   char* base = nullptr;
   int   r    = get_scratch(q, need, &base);
   if (r) return r;
@@ -393,15 +412,17 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   q->csi_arena = (float*)(base + staged + rnd(nd * 8));
   q->e_arena   = (int16_t*)(base + staged + rnd(nd * 8) + rnd(nd * 4));
   CHECK_HIP(q->stage.reserve(staged));
-  // offsets are known up front: jobs | cws | nci | ndst | cmax
+  // offsets are known up front: jobs | cws | nci | ndst; the per-block csi maxima follow the arenas (written by
+  // every equaliser block that has work, read by the LLR kernel: no initialisation)
   const size_t o_jobs = 0, o_cws = o_jobs + staged_size(njobs * sizeof(PdschJobDev));
   const size_t o_nci = o_cws + staged_size(ncw * sizeof(PdschCwDev)), o_ndst = o_nci + staged_size(new_ci.size() * 4);
-  const size_t o_cmax = o_ndst + staged_size(new_ci.size() * 8);
-  uint32_t*    d_cmax = (uint32_t*)(base + o_cmax);
+  uint32_t*    d_cmax = (uint32_t*)(base + staged + rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2));
+  uint32_t*    d_cfin = d_cmax + rnd((size_t)njobs * 2 * nparts * 4) / 4;
   std::vector<PdschJobDev> hj(njobs);
   for (uint32_t i = 0; i < njobs; i++) {
     JobPlan& P = plans[i];
-    P.dev.cmax = d_cmax + 2 * i;
+    P.dev.cmax        = d_cmax + (size_t)2 * nparts * i;
+    P.dev.cmax_stride = nparts;
     for (uint32_t cw = 0; cw < 2; cw++) {
       P.dev.d[cw]   = q->d_arena + P.d_off[cw];
       P.dev.csi[cw] = q->csi_arena + P.csi_off[cw];
@@ -415,7 +436,9 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
       const uint32_t cw = plans[i].cw_of_tb[t];
       cws[ci].d         = plans[i].dev.d[cw];
       cws[ci].csi       = plans[i].dev.csi[cw];
-      cws[ci].cmax      = plans[i].dev.cmax + cw;
+      cws[ci].cmax      = plans[i].dev.cmax + (size_t)cw * nparts;
+      cws[ci].nparts    = (plans[i].dev.units + EQ_BLOCK_ITEMS - 1) / EQ_BLOCK_ITEMS;
+      cws[ci].cmax_final = d_cfin + ci;
       cws[ci].e         = q->e_arena + plans[i].e_off[t];
       ci++;
     }
@@ -424,7 +447,6 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   q->stage.put(cws.data(), ncw * sizeof(PdschCwDev));
   q->stage.put(new_ci.data(), new_ci.size() * 4);
   q->stage.put(new_dst.data(), new_dst.size() * 8);
-  q->stage.zeros(njobs * 8);
   CHECK_HIP(q->stage.upload(base, s));
   CHECK_HIP(pdsch_launch_equalize((const PdschJobDev*)(base + o_jobs), njobs, max_units, s));
   CHECK_HIP(pdsch_launch_scr_pack((const uint32_t*)(base + o_nci), (uint32_t* const*)(base + o_ndst),
@@ -471,7 +493,7 @@ void mi355_pdsch_destroy(mi355_pdsch_t* q)
   if (!q) return;
   (void)hipSetDevice(q->device);
   (void)hipDeviceSynchronize();
-  for (auto& kv : q->maps) (void)hipFree(kv.second.first);
+  for (auto& kv : q->maps) (void)hipFree(kv.second.d);
   for (auto& kv : q->scr) (void)hipFree(kv.second);
   (void)hipFree(q->gold);
   (void)hipFree(q->scratch);
@@ -529,7 +551,7 @@ int mi355_pdsch_decode_batch(mi355_pdsch_t*           q,
 
 int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi355_pdsch_job_t* jobs,
                                         uint32_t njobs, mi355_pdsch_res_t* res, void* stream, const float* d_noise,
-                                        WaitHook hook)
+                                        WaitHook hook, bool ce_invariant)
 {
   if (!q || !pool || !res || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;
   std::lock_guard<std::mutex> lock(q->mu);
@@ -544,6 +566,7 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
     if (r) return r;
     // noise estimate left in device memory by the channel estimator (ZF ignores it, pdsch.c:934)
     if (d_noise && jobs[i].cfg.decoder_type != MI355_MIMO_DECODER_ZF) plans[i].dev.noise_dev = d_noise + i;
+    plans[i].dev.h_invariant = ce_invariant ? 1u : 0u;
   }
   const auto t1 = now();
   int r = run_frontend(q, jobs, plans, s);

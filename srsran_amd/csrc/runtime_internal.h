@@ -18,9 +18,11 @@ int dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const
 
 // mi355_pdsch_decode_batch with the MMSE noise estimate of job i read from device memory d_noise[i] (written
 // by the channel estimator of the same stream), so no host round trip is needed between estimation and
-// equalisation.  d_noise == nullptr: the jobs' noise_estimate fields.
+// equalisation.  d_noise == nullptr: the jobs' noise_estimate fields.  ce_invariant: the channel estimates
+// were just written by this library's estimator, whose every OFDM symbol row is the same (AVERAGE estimator,
+// chest_dl.c average_pilots + interpolation), so the equaliser may read them from the first row.
 int pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi355_pdsch_job_t* jobs,
                                  uint32_t njobs, mi355_pdsch_res_t* res, void* stream, const float* d_noise,
-                                 WaitHook hook = WaitHook{});
+                                 WaitHook hook = WaitHook{}, bool ce_invariant = false);
 
 } // namespace mi355

@@ -462,7 +462,8 @@ int mi355_ue_dl_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, co
   ChestFill fill{q, chest_cfg, nullptr, njobs, chest, false};
   if ((r = chest_finish_async(q, &fill, d_out, s))) return r;
   const auto t1 = now();
-  r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), njobs, res, s, d_noise, WaitHook{chest_fill_cb, &fill});
+  r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), njobs, res, s, d_noise, WaitHook{chest_fill_cb, &fill},
+                                   true);
   const auto t2 = now();
   CHECK_HIP(hipStreamSynchronize(q->side));
   if (r) return r;
