@@ -129,7 +129,9 @@ __device__ __forceinline__ void set_minf(v2s s[8])
 // every load unconditional (a runtime "load or zero" select makes hipcc branch around each load and
 // wait for it, which serialises the memory pipeline).
 // DIAG (diagnostic builds only, selected by MI355_TDEC_DIAG): 1 = backward pass only, 2 = forward only
-template <int NSB, int SEG, int MODE, int DIAG = 0>
+// FULL: L % SEG == 0 (every K whose window length is a multiple of 8, e.g. K = 6144): no ragged last segment,
+// so every segment-bound test folds at compile time and the unrolled steps stay one basic block.
+template <int NSB, int SEG, int MODE, int DIAG = 0, bool FULL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tdec_win_halfit(TdecWinArgs a)
 {
   constexpr int NL = NSB / 2;
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
     auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap) {
 #pragma unroll
       for (int i = 0; i < SEG; i++) {
-        const int j = min(t * SEG + i, L - 1); // clamp the ragged last segment (values unused)
+        const int j = FULL ? t * SEG + i : min(t * SEG + i, L - 1); // clamp the ragged last segment
         x[i]        = X[j * xs];
         y[i]        = Y[j * NL];
         if constexpr (has_ap) ap[i] = AP[j * 64];
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
 #pragma unroll
       for (int i = SEG - 1; i >= 0; i--) {
         const int k = t * SEG + i;
-        if (k < L) {
+        if (FULL || k < L) {
           v2s x = U(cx[i]);
           if constexpr (has_ap) x = sadd(x, U(ca[i]));
           if constexpr (DIAG == 4) {
@@ -331,7 +333,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap, uint32_t* d, uint32_t* c) {
 #pragma unroll
     for (int i = 0; i < SEG; i++) {
-      const int j = min(t * SEG + i, L - 1); // clamp the ragged last segment (values unused)
+      const int j = FULL ? t * SEG + i : min(t * SEG + i, L - 1); // clamp the ragged last segment
       x[i]        = X[j * xs];
       y[i]        = Y[j * NL];
       if constexpr (has_ap) ap[i] = AP[j * 64];
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
 #pragma unroll 1
   for (int t = 0; t < nseg; t++) {
     const int s0 = t * SEG;
-    const int e  = (s0 + SEG < L) ? s0 + SEG : L;
+    const int e  = FULL ? s0 + SEG : ((s0 + SEG < L) ? s0 + SEG : L);
     uint32_t  nx[SEG], ny[SEG], na[SEG] = {}, nd[SEG], nc[8];
     uint32_t  bits = 0; // decision bits of the segment: window 2l in bits 8..15, 2l+1 in 0..7 (MSB first)
     if (wr_bits && (t & 1)) bits = dbits;
@@ -380,12 +382,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
 #pragma unroll
       for (int i = SEG; i >= lo; i--) {
         const int j = s0 + i;
-        if (j == e) {
+        if (FULL ? i == SEG : j == e) {
           if (i <= lo + 3) {
 #pragma unroll
             for (int s = 0; s < 8; s++) R[i - lo][s] = ck8[s];
           }
-        } else if (j < e) {
+        } else if (FULL ? i < SEG : j < e) {
           v2s row[8];
           beta_step<true>(cur, xin[i], U(cy[i]), row);
 #pragma unroll
@@ -402,7 +404,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
       for (int ii = 0; ii < 4; ii++) {
         const int i = lo - 1 + ii;
         const int j = s0 + i;
-      if (j < e) {
+      if (FULL ? i < SEG : j < e) {
         v2s c0[8], c1[8];
         alpha_cands<true>(st, xin[i], U(cy[i]), c0, c1);
         v2s m0 = sadd(R[ii][0], c0[0]);
@@ -554,15 +556,15 @@ static int diag_mode()
   return m;
 }
 
-template <int NSB, int DIAG>
+template <int NSB, int DIAG, bool FULL = false>
 static void launch_mode(int mode, int blocks, const TdecWinArgs& a, hipStream_t s)
 {
   if (mode == 0) {
-    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 0, DIAG>), dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 0, DIAG, FULL>), dim3(blocks), dim3(256), 0, s, a);
   } else if (mode == 1) {
-    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 1, DIAG>), dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 1, DIAG, FULL>), dim3(blocks), dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 2, DIAG>), dim3(blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 2, DIAG, FULL>), dim3(blocks), dim3(256), 0, s, a);
   }
 }
 
@@ -581,9 +583,13 @@ hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s)
       launch_mode<16, 4>(mode, blocks, a, s);
     } else if (dm == 2) {
       launch_mode<16, 2>(mode, blocks, a, s);
+    } else if (a.L % TDEC_SEG == 0) {
+      launch_mode<16, 0, true>(mode, blocks, a, s);
     } else {
       launch_mode<16, 0>(mode, blocks, a, s);
     }
+  } else if (a.L % TDEC_SEG == 0) {
+    launch_mode<8, 0, true>(mode, blocks, a, s);
   } else {
     launch_mode<8, 0>(mode, blocks, a, s);
   }
