@@ -29,6 +29,14 @@ struct PdschJobDev {
   float           rhob_inv, scaling, noise;
   const float*    noise_dev; // nullable: noise estimate produced on the device (chest), used instead of noise
   uint32_t        units;     // kernel A work items: grid positions g0 + u (single-RE schemes), SFBC pairs / quads
+  // fused path (pdsch_csimax_cols + pdsch_eq_llr): single-RE schemes whose csi depends on the subcarrier only
+  // (port 0, spatial multiplexing 2x2 MMSE / 2x1 MRC) with row-invariant channel estimates.  The symbols and
+  // csi are never stored: the LLRs of each RE pair are produced where the pair is equalised.
+  uint32_t                 fused;
+  uint32_t                 fused_key; // modulation orders of the layers' codewords: qm0 * 16 + qm1 (0: none)
+  const uint16_t*          cols;  // distinct subcarriers of the PDSCH REs (csi maximum over them)
+  uint32_t                 ncols;
+  const struct PdschCwDev* cw[2]; // codeword (TB) descriptor fed by layer 0 / 1, null when not decoded
 };
 
 // One codeword (TB) symbol -> LLR job.
@@ -42,6 +50,7 @@ struct PdschCwDev {
   const uint32_t* scr; // packed descrambling sequence of c_init (cached per c_init)
   uint32_t      nof_re, nof_bits, qm, c_init, csi_enable;
   uint32_t      pairs; // kernel B work items: symbol pairs
+  uint32_t      fused; // produced by pdsch_eq_llr (pdsch_llr / pdsch_cmax_reduce skip it)
 };
 
 // 2-D grids: blockIdx.y = job / codeword, blockIdx.x over the largest one's work items.
@@ -49,5 +58,8 @@ hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, uint32_t njobs, uint32
 hipError_t pdsch_launch_scr_pack(const uint32_t* c_init, uint32_t* const* dst, uint32_t n, const uint32_t* gold,
                                  uint32_t W, hipStream_t s);
 hipError_t pdsch_launch_llr(const PdschCwDev* cws, uint32_t ncw, uint32_t max_pairs, hipStream_t s);
+// fused equaliser + LLR for the jobs flagged fused (others return at once)
+hipError_t pdsch_launch_fused(const PdschJobDev* jobs, uint32_t njobs, uint32_t max_pairs, const uint32_t* keys,
+                              uint32_t nkeys, hipStream_t s);
 
 } // namespace mi355

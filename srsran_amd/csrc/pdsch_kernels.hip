@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
 {
   const PdschJobDev& J    = jobs[blockIdx.y];
   const uint32_t     base = blockIdx.x * 256 * EQ_U + threadIdx.x;
-  if (blockIdx.x * 256 * EQ_U >= J.units) return;
+  if (J.fused || blockIdx.x * 256 * EQ_U >= J.units) return;
   const float noise = J.noise_dev ? *gptr(J.noise_dev) : J.noise;
   float       m0 = 0.f, m1 = 0.f; // per-thread csi contributions for the maxima
   if (J.scheme == 1) {
@@ -542,26 +542,14 @@ template <int QM> __device__ __forceinline__ void store_llrs(GLB int16_t* e, con
     if ((uint32_t)k < nb) e[k] = o[k];
 }
 
-template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, uint32_t pr, uint32_t cmax_bits)
+// LLRs of symbol pair pr (symbols 2pr, 2pr+1; ns of them exist) of codeword C from the symbols and csi
+template <int QM>
+__device__ __forceinline__ void llr_syms(const PdschCwDev& C, uint32_t pr, uint32_t ns, const cf (&x)[2],
+                                         const float (&csi)[2], uint32_t cmax_bits)
 {
   const uint32_t n  = C.nof_re;
-  const uint32_t s0 = 2 * pr, ns = min(2u, n - s0);
+  const uint32_t s0 = 2 * pr;
   int16_t        o[2 * QM];
-  float          csi[2] = {0.f, 0.f};
-  cf             x[2]   = {mk(0.f, 0.f), mk(0.f, 0.f)};
-  if (ns == 2) { // the pair as one 16-byte load (d is 64-element aligned per codeword, s0 even)
-    const vf4 v = *(const GLB vf4*)(gptr(C.d) + s0);
-    x[0]           = mk(v.x, v.y);
-    x[1]           = mk(v.z, v.w);
-    if (C.csi_enable) {
-      const vf2 c = *(const GLB vf2*)(gptr(C.csi) + s0);
-      csi[0] = c.x;
-      csi[1] = c.y;
-    }
-  } else {
-    x[0] = ld(gptr(C.d), s0);
-    if (C.csi_enable) csi[0] = gptr(C.csi)[s0];
-  }
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     if ((uint32_t)k < ns) {
@@ -623,11 +611,32 @@ template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, 
   store_llrs<QM>(gptr(C.e) + b0, o, nb);
 }
 
+template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, uint32_t pr, uint32_t cmax_bits)
+{
+  const uint32_t s0 = 2 * pr, ns = min(2u, C.nof_re - s0);
+  float          csi[2] = {0.f, 0.f};
+  cf             x[2]   = {mk(0.f, 0.f), mk(0.f, 0.f)};
+  if (ns == 2) { // the pair as one 16-byte load (d is 64-element aligned per codeword, s0 even)
+    const vf4 v = *(const GLB vf4*)(gptr(C.d) + s0);
+    x[0]        = mk(v.x, v.y);
+    x[1]        = mk(v.z, v.w);
+    if (C.csi_enable) {
+      const vf2 c = *(const GLB vf2*)(gptr(C.csi) + s0);
+      csi[0]      = c.x;
+      csi[1]      = c.y;
+    }
+  } else {
+    x[0] = ld(gptr(C.d), s0);
+    if (C.csi_enable) csi[0] = gptr(C.csi)[s0];
+  }
+  llr_syms<QM>(C, pr, ns, x, csi, cmax_bits);
+}
+
 __global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ cws)
 {
   const PdschCwDev& C  = cws[blockIdx.y];
   const uint32_t    pr = blockIdx.x * 256 + threadIdx.x;
-  if (pr >= C.pairs) return;
+  if (C.fused || pr >= C.pairs) return;
   const uint32_t cm = C.csi_enable ? *gptr(C.cmax_final) : 0u;
   switch (C.qm) {
     case 1: llr_pair<1>(C, pr, cm); break;
@@ -644,9 +653,239 @@ __global__ __launch_bounds__(256) void pdsch_cmax_reduce(const PdschCwDev* __res
   const uint32_t c = blockIdx.x * 256 + threadIdx.x;
   if (c >= ncw) return;
   const PdschCwDev& C = cws[c];
+  if (C.fused) return;
   uint32_t          b = 0;
   for (uint32_t k = 0; k < C.nparts; k++) b = max(b, gptr(C.cmax)[k]);
   *gptr(C.cmax_final) = b;
+}
+
+// ---------------------------------------------------------------------------- fused equaliser + LLR
+// csi of the single-RE schemes depends on the channel estimate and the noise only, so with row-invariant
+// estimates it is a function of the subcarrier: the codeword maxima (csi_correction's srslte_vec_max_fi,
+// pdsch.c:653) are taken over the PDSCH subcarriers before any symbol is equalised.  One workgroup per job.
+__device__ __forceinline__ void csi_of(const PdschJobDev& J, const cf (&H)[4], float noise, float& c0, float& c1)
+{
+  if (J.scheme == 0) { // precoding.c:345-355
+    float hh = 0.f;
+#pragma unroll
+    for (int p = 0; p < 2; p++)
+      if ((uint32_t)p < J.nof_rx) hh += H[p].re * H[p].re + H[p].im * H[p].im;
+    c0 = hh + noise;
+    c1 = 0.f;
+  } else if (J.nof_layers == 2) { // precoding.c:1519-1548
+    const float norm = J.cb == 0 ? 0x1.6a09e6p+0f / J.scaling : 2.0f / J.scaling;
+    const cf    g00 = H[0], g01 = H[1], g10 = H[2], g11 = H[3];
+    cf          h00, h01, h10, h11;
+    if (J.cb == 0) {
+      h00 = g00, h01 = g10, h10 = g01, h11 = g11;
+    } else if (J.cb == 1) {
+      h00 = g00 + g10, h01 = g00 - g10, h10 = g01 + g11, h11 = g01 - g11;
+    } else {
+      h00 = g00 + mulj(g10), h01 = g00 - mulj(g10), h10 = g01 + mulj(g11), h11 = g01 - mulj(g11);
+    }
+    cf x0, x1;
+    mmse_2x2_csi(mk(0.f, 0.f), mk(0.f, 0.f), h00, h01, h10, h11, x0, x1, c0, c1, noise, norm);
+  } else { // precoding.c:1786-1820
+    const float norm = 0x1.6a09e6p+0f / J.scaling;
+    cf          h[2];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const cf a = H[r], b = H[2 + r];
+      h[r] = J.cb == 0 ? a + b : J.cb == 1 ? a - b : J.cb == 2 ? a + mulj(b) : a - mulj(b);
+    }
+    const float c = h[0].re * h[0].re + h[0].im * h[0].im + h[1].re * h[1].re + h[1].im * h[1].im;
+    c0            = (float)((double)(c / norm) * 0.70710678118654752);
+    c1            = 0.f;
+  }
+}
+
+__device__ __forceinline__ void h_ptrs(const PdschJobDev& J, const GLB float2* (&hp)[4])
+{
+#pragma unroll
+  for (int p = 0; p < 2; p++)
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+      hp[p * 2 + r] = gptr(J.h[(p == 0 || J.scheme != 0) ? p : 0][(uint32_t)r < J.nof_rx ? r : 0]);
+}
+
+__global__ __launch_bounds__(256) void pdsch_csimax_cols(const PdschJobDev* __restrict__ jobs)
+{
+  const PdschJobDev& J = jobs[blockIdx.x];
+  if (!J.fused) return;
+  const float       noise = J.noise_dev ? *gptr(J.noise_dev) : J.noise;
+  const GLB float2* hp[4];
+  h_ptrs(J, hp);
+  uint32_t b0 = 0, b1 = 0;
+  for (uint32_t c = threadIdx.x; c < J.ncols; c += 256) {
+    const uint32_t k = gptr(J.cols)[c]; // row 0 holds every symbol's estimate
+    cf             H[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) H[q] = ld(hp[q], k);
+    float c0, c1;
+    csi_of(J, H, noise, c0, c1);
+    b0 = max(b0, __float_as_uint(c0));
+    b1 = max(b1, __float_as_uint(c1));
+  }
+  __shared__ uint32_t red[2][4];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    b0 = max(b0, (uint32_t)__shfl_xor((int)b0, o, 64));
+    b1 = max(b1, (uint32_t)__shfl_xor((int)b1, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = b0;
+    red[1][threadIdx.x >> 6] = b1;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const uint32_t l = threadIdx.x;
+    if (J.cw[l]) *gptr(J.cw[l]->cmax_final) = max(max(red[l][0], red[l][1]), max(red[l][2], red[l][3]));
+  }
+}
+
+constexpr int FU_P = 2; // RE pairs per thread
+
+// grid (pair blocks of the largest job, jobs): work item = RE pair (2pr, 2pr+1), the granule of the LLR kernel.
+// One instantiation per (layer-0, layer-1) modulation order pair present in the batch (0: layer not decoded);
+// blocks of jobs with another pair return at once.
+template <int QM0, int QM1>
+__global__ __launch_bounds__(256) void pdsch_eq_llr(const PdschJobDev* __restrict__ jobs)
+{
+  const PdschJobDev& J     = jobs[blockIdx.y];
+  const uint32_t     pairs = (J.nof_re + 1) / 2;
+  const uint32_t     base  = blockIdx.x * 256 * FU_P + threadIdx.x;
+  if (!J.fused || J.fused_key != (uint32_t)(QM0 * 16 + QM1) || blockIdx.x * 256 * FU_P >= pairs) return;
+  // the codeword descriptors and csi maxima, once per block
+  __shared__ PdschCwDev cwd[2];
+  __shared__ uint32_t   cmb[2];
+  if (threadIdx.x < 2 && J.cw[threadIdx.x]) {
+    cwd[threadIdx.x] = *J.cw[threadIdx.x];
+    cmb[threadIdx.x] = cwd[threadIdx.x].csi_enable ? *gptr(cwd[threadIdx.x].cmax_final) : 0u;
+  }
+  __syncthreads();
+  const float         noise = J.noise_dev ? *gptr(J.noise_dev) : J.noise;
+  const uint32_t      row = J.row, magic = J.row_magic, rmask = J.rhob_mask;
+  const float         rinv = J.rhob_inv;
+  const GLB uint32_t* map2 = (const GLB uint32_t*)gptr(J.map); // two grid indices per pair (map is 4-byte aligned)
+  const GLB float2*   yp[2] = {gptr(J.y[0]), gptr(J.nof_rx > 1 ? J.y[1] : J.y[0])};
+  const GLB float2*   hp[4];
+  h_ptrs(J, hp);
+  uint32_t m[FU_P];
+#pragma unroll
+  for (int k = 0; k < FU_P; k++) m[k] = map2[base + k * 256 < pairs ? base + k * 256 : 0];
+  cf Y[FU_P][2][2], H[FU_P][2][4]; // [pair][RE][...]
+#pragma unroll
+  for (int k = 0; k < FU_P; k++) {
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const uint32_t g  = e ? (m[k] >> 16) : (m[k] & 0xffffu);
+      const uint32_t gc = g < 14 * row ? g : 0u; // the odd tail's second index is padding
+      const uint32_t l  = __umulhi(gc, magic);
+      const float    sc = ((rmask >> l) & 1u) ? rinv : 1.0f; // x * 1.0f is exact
+#pragma unroll
+      for (int r = 0; r < 2; r++) Y[k][e][r] = ld(yp[r], gc) * sc;
+#pragma unroll
+      for (int q = 0; q < 4; q++) H[k][e][q] = ld(hp[q], gc - l * row);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < FU_P; k++) {
+    const uint32_t pr = base + k * 256;
+    if (pr >= pairs) continue;
+    const uint32_t ns = min(2u, J.nof_re - 2 * pr);
+    cf             xs[2][2]; // [layer][RE]
+    float          cs[2][2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const cf(&h)[4] = H[k][e];
+      const cf(&y)[2] = Y[k][e];
+      if (J.scheme == 0) { // precoding.c:345-355
+        cf    r  = mk(0.f, 0.f);
+        float hh = 0.f;
+#pragma unroll
+        for (int p = 0; p < 2; p++) {
+          if ((uint32_t)p < J.nof_rx) {
+            r = r + y[p] * cj(h[p]);
+            hh += h[p].re * h[p].re + h[p].im * h[p].im;
+          }
+        }
+        const float c = hh + noise, nrm = 1.0f / J.scaling;
+        xs[0][e]      = mk(r.re * nrm / c, r.im * nrm / c);
+        cs[0][e]      = c;
+        xs[1][e]      = mk(0.f, 0.f);
+        cs[1][e]      = 0.f;
+      } else if (J.nof_layers == 2) { // precoding.c:1519-1548
+        const float norm = J.cb == 0 ? 0x1.6a09e6p+0f / J.scaling : 2.0f / J.scaling;
+        cf          h00, h01, h10, h11;
+        if (J.cb == 0) {
+          h00 = h[0], h01 = h[2], h10 = h[1], h11 = h[3];
+        } else if (J.cb == 1) {
+          h00 = h[0] + h[2], h01 = h[0] - h[2], h10 = h[1] + h[3], h11 = h[1] - h[3];
+        } else {
+          h00 = h[0] + mulj(h[2]), h01 = h[0] - mulj(h[2]), h10 = h[1] + mulj(h[3]), h11 = h[1] - mulj(h[3]);
+        }
+        mmse_2x2_csi(y[0], y[1], h00, h01, h10, h11, xs[0][e], xs[1][e], cs[0][e], cs[1][e], noise, norm);
+      } else { // precoding.c:1786-1820
+        const float norm = 0x1.6a09e6p+0f / J.scaling;
+        cf          hv[2];
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+          const cf a = h[r], b = h[2 + r];
+          hv[r] = J.cb == 0 ? a + b : J.cb == 1 ? a - b : J.cb == 2 ? a + mulj(b) : a - mulj(b);
+        }
+        const float c  = hv[0].re * hv[0].re + hv[0].im * hv[0].im + hv[1].re * hv[1].re + hv[1].im * hv[1].im;
+        const float hh = norm / c;
+        xs[0][e]       = (cj(hv[0]) * y[0] + cj(hv[1]) * y[1]) * hh;
+        cs[0][e]       = (float)((double)(c / norm) * 0.70710678118654752);
+        xs[1][e]       = mk(0.f, 0.f);
+        cs[1][e]       = 0.f;
+      }
+    }
+    if constexpr (QM0 != 0) {
+      const cf    x[2]   = {xs[0][0], xs[0][1]};
+      const float csi[2] = {cs[0][0], cs[0][1]};
+      llr_syms<QM0>(cwd[0], pr, ns, x, csi, cmb[0]);
+    }
+    if constexpr (QM1 != 0) {
+      const cf    x[2]   = {xs[1][0], xs[1][1]};
+      const float csi[2] = {cs[1][0], cs[1][1]};
+      llr_syms<QM1>(cwd[1], pr, ns, x, csi, cmb[1]);
+    }
+  }
+}
+
+template <int QM0>
+static void launch_eq_llr_1(uint32_t qm1, const dim3& g, const PdschJobDev* jobs, hipStream_t s)
+{
+  switch (qm1) {
+    case 0: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 0>), g, dim3(256), 0, s, jobs); break;
+    case 2: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 2>), g, dim3(256), 0, s, jobs); break;
+    case 4: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 4>), g, dim3(256), 0, s, jobs); break;
+    case 6: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 6>), g, dim3(256), 0, s, jobs); break;
+    default: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 8>), g, dim3(256), 0, s, jobs); break;
+  }
+}
+
+hipError_t pdsch_launch_fused(const PdschJobDev* jobs, uint32_t njobs, uint32_t max_pairs, const uint32_t* keys,
+                              uint32_t nkeys, hipStream_t s)
+{
+  const uint32_t nblk = (max_pairs + 256 * FU_P - 1) / (256 * FU_P);
+  if (!njobs || !nblk) return hipSuccess;
+  hipLaunchKernelGGL(pdsch_csimax_cols, dim3(njobs), dim3(256), 0, s, jobs);
+  for (uint32_t k = 0; k < nkeys; k++) {
+    const uint32_t q0 = keys[k] >> 4, q1 = keys[k] & 15;
+    for (uint32_t j0 = 0; j0 < njobs; j0 += 65535) {
+      const dim3 g(nblk, std::min(65535u, njobs - j0));
+      switch (q0) {
+        case 0: launch_eq_llr_1<0>(q1, g, jobs + j0, s); break;
+        case 2: launch_eq_llr_1<2>(q1, g, jobs + j0, s); break;
+        case 4: launch_eq_llr_1<4>(q1, g, jobs + j0, s); break;
+        case 6: launch_eq_llr_1<6>(q1, g, jobs + j0, s); break;
+        default: launch_eq_llr_1<8>(q1, g, jobs + j0, s); break;
+      }
+    }
+  }
+  return hipGetLastError();
 }
 
 hipError_t pdsch_launch_equalize(const PdschJobDev* jobs, uint32_t njobs, uint32_t max_units, hipStream_t s)

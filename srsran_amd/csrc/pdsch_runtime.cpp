@@ -156,8 +156,9 @@ uint32_t mod_bits(uint32_t mod)
 // g0 + t -> RE index or 0xffff (g1 - g0)], the inverse letting the single-RE equalisers walk the grid
 struct MapEntry {
   uint16_t* d = nullptr;
-  uint32_t  n = 0, g0 = 0, g1 = 0;
+  uint32_t  n = 0, g0 = 0, g1 = 0, ncols = 0;
   const uint16_t* inv() const { return d + ((n + 1) & ~1u); }
+  const uint16_t* cols() const { return inv() + (g1 - g0); } // distinct subcarriers of the REs
 };
 
 struct JobPlan {
@@ -241,9 +242,17 @@ static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi,
       e.g0 = *std::min_element(idx.begin(), idx.end());
       e.g1 = *std::max_element(idx.begin(), idx.end()) + 1u;
     }
-    std::vector<uint16_t> all(((e.n + 1) & ~1u) + (e.g1 - e.g0), 0xffff);
+    const uint32_t        row = 12 * q->cell.nof_prb;
+    std::vector<uint8_t>  used(row, 0);
+    for (uint16_t gi : idx) used[gi % row] = 1;
+    std::vector<uint16_t> cols;
+    for (uint32_t k = 0; k < row; k++)
+      if (used[k]) cols.push_back((uint16_t)k);
+    e.ncols = (uint32_t)cols.size();
+    std::vector<uint16_t> all(((e.n + 1) & ~1u) + (e.g1 - e.g0) + e.ncols, 0xffff);
     std::copy(idx.begin(), idx.end(), all.begin());
     for (uint32_t i = 0; i < e.n; i++) all[((e.n + 1) & ~1u) + idx[i] - e.g0] = (uint16_t)i;
+    std::copy(cols.begin(), cols.end(), all.begin() + ((e.n + 1) & ~1u) + (e.g1 - e.g0));
     CHECK_HIP(hipMalloc(&e.d, std::max<size_t>(all.size(), 1) * sizeof(uint16_t)));
     if (!all.empty()) CHECK_HIP(hipMemcpy(e.d, all.data(), all.size() * 2, hipMemcpyHostToDevice));
     it = q->maps.emplace(key, e).first;
@@ -292,6 +301,8 @@ static int plan_job(mi355_pdsch_t* q, const mi355_pdsch_job_t& j, const mi355_pd
   D.map              = me.d;
   D.imap             = me.inv();
   D.g0               = me.g0;
+  D.cols             = me.cols();
+  D.ncols            = me.ncols;
   if (nre != g.nof_re) return MI355_ERROR; // "Error expecting %d symbols but got %d" (pdsch.c:949-960)
 
   // power allocation (pdsch.c:575-611, 926-932)
@@ -355,7 +366,7 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
     for (auto& kv : q->scr) (void)hipFree(kv.second);
     q->scr.clear();
   }
-  uint32_t  max_units = 0, max_pairs = 0;
+  uint32_t  max_units = 0, max_pairs = 0, max_fpairs = 0;
   uint32_t  last_ci  = 0;
   const uint32_t* last_scr = nullptr;
   cws.reserve(2 * njobs);
@@ -365,7 +376,11 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
       P.d_off[cw] = P.csi_off[cw] = nd;
       nd += (P.dev.nof_re + 63) / 64 * 64;
     }
-    max_units = std::max(max_units, P.dev.units);
+    if (P.dev.fused) {
+      max_fpairs = std::max(max_fpairs, (P.dev.nof_re + 1) / 2);
+    } else {
+      max_units = std::max(max_units, P.dev.units);
+    }
     for (uint32_t t = 0; t < 2; t++) {
       if (!P.decode[t]) continue;
       const mi355_ra_tb_t& tb = jobs[i].cfg.grant.tb[t];
@@ -378,7 +393,8 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
       c.c_init     = ((uint32_t)jobs[i].cfg.rnti << 14) + (tb.cw_idx << 13) + ((jobs[i].sf.tti % 10) << 9) + q->cell.id;
       c.csi_enable = jobs[i].cfg.csi_enable ? 1u : 0u;
       c.pairs      = (c.nof_re + 1) / 2;
-      max_pairs = std::max(max_pairs, c.pairs);
+      c.fused      = P.dev.fused;
+      if (!c.fused) max_pairs = std::max(max_pairs, c.pairs);
       if (c.c_init == last_ci && last_scr) {
         c.scr = last_scr;
       } else {
@@ -419,6 +435,24 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   uint32_t*    d_cmax = (uint32_t*)(base + staged + rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2));
   uint32_t*    d_cfin = d_cmax + rnd((size_t)njobs * 2 * nparts * 4) / 4;
   std::vector<PdschJobDev> hj(njobs);
+  const PdschCwDev*        d_cws = (const PdschCwDev*)(base + o_cws);
+  std::vector<uint32_t>    fkeys; // (qm0, qm1) pairs of the fused jobs: one kernel instantiation each
+  {
+    size_t k = 0;
+    for (uint32_t i = 0; i < njobs; i++) {
+      plans[i].dev.cw[0] = plans[i].dev.cw[1] = nullptr;
+      uint32_t qm[2]     = {0, 0};
+      for (uint32_t t = 0; t < 2; t++) {
+        if (!plans[i].decode[t]) continue;
+        plans[i].dev.cw[plans[i].cw_of_tb[t] & 1] = d_cws + k; // the layer (codeword) feeding this TB
+        qm[plans[i].cw_of_tb[t] & 1]              = cws[k].qm;
+        k++;
+      }
+      plans[i].dev.fused_key = qm[0] * 16 + qm[1];
+      if (plans[i].dev.fused && std::find(fkeys.begin(), fkeys.end(), plans[i].dev.fused_key) == fkeys.end())
+        fkeys.push_back(plans[i].dev.fused_key);
+    }
+  }
   for (uint32_t i = 0; i < njobs; i++) {
     JobPlan& P = plans[i];
     P.dev.cmax        = d_cmax + (size_t)2 * nparts * i;
@@ -451,6 +485,8 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   CHECK_HIP(pdsch_launch_equalize((const PdschJobDev*)(base + o_jobs), njobs, max_units, s));
   CHECK_HIP(pdsch_launch_scr_pack((const uint32_t*)(base + o_nci), (uint32_t* const*)(base + o_ndst),
                                   (uint32_t)new_ci.size(), q->gold, PDSCH_GOLD_MAX / 32, s));
+  CHECK_HIP(pdsch_launch_fused((const PdschJobDev*)(base + o_jobs), njobs, max_fpairs, fkeys.data(),
+                               (uint32_t)fkeys.size(), s));
   CHECK_HIP(pdsch_launch_llr((const PdschCwDev*)(base + o_cws), (uint32_t)ncw, max_pairs, s));
   return MI355_SUCCESS;
 }
@@ -567,6 +603,9 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
     // noise estimate left in device memory by the channel estimator (ZF ignores it, pdsch.c:934)
     if (d_noise && jobs[i].cfg.decoder_type != MI355_MIMO_DECODER_ZF) plans[i].dev.noise_dev = d_noise + i;
     plans[i].dev.h_invariant = ce_invariant ? 1u : 0u;
+    // csi depends on the subcarrier only for these schemes (CDD alternates its precoder per RE, SFBC pairs REs)
+    plans[i].dev.fused = ce_invariant && (plans[i].dev.scheme == MI355_TXSCHEME_PORT0 ||
+                                          plans[i].dev.scheme == MI355_TXSCHEME_SPATIALMUX) ? 1u : 0u;
   }
   const auto t1 = now();
   int r = run_frontend(q, jobs, plans, s);

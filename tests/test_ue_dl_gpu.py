@@ -132,20 +132,36 @@ def test_ue_dl_end_to_end():
             assert diff.max() <= 2 and (diff > 0).mean() < 1e-3, (k, t, diff.max(), (diff > 0).mean())
 
 
-def test_fused_decode_matches_two_step():
-    """mi355_ue_dl_decode_batch (noise kept on the device, no host round trip) == decode_fft_estimate followed
-    by decode_pdsch: same chest results, CRCs, payloads and LLRs, over a batch mixing subframes."""
-    rng = np.random.default_rng(5)
-    cfg0 = E2E[1]
+FUSED = [  # (cfg, sf indices): the fused call's equaliser+LLR path (port 0, SM) and its two-kernel path (SFBC, CDD)
+    (E2E[1], (1, 4, 0)),
+    (pc.Cfg(nof_prb=50, nof_ports=1, nof_rx=2, cell_id=3, cfi=2, sf_idx=0, scheme=0, nof_layers=1, qm=[6],
+            tbs=[pc.valid_tbs(18000)], csi_enable=True), (2, 5, 7)),
+    (pc.Cfg(nof_prb=25, nof_ports=2, nof_rx=2, cell_id=9, cfi=1, sf_idx=0, scheme=2, nof_layers=1, qm=[4],
+            tbs=[pc.valid_tbs(5000)], pmi=2, csi_enable=True), (3, 6, 9)),
+    (pc.Cfg(nof_prb=50, nof_ports=2, nof_rx=2, cell_id=5, cfi=3, sf_idx=0, scheme=3, nof_layers=2, qm=[6, 6],
+            tbs=[20616, 20616], csi_enable=True), (1, 2, 8)),
+    (pc.Cfg(nof_prb=25, nof_ports=2, nof_rx=2, cell_id=7, cfi=2, sf_idx=0, scheme=1, nof_layers=2, qm=[4],
+            tbs=[4968], csi_enable=True), (0, 4, 5)),
+]
+
+
+@pytest.mark.parametrize("k", range(len(FUSED)))
+def test_fused_decode_matches_two_step(k):
+    """mi355_ue_dl_decode_batch (noise kept on the device, channel estimates read from their first row, the
+    equaliser and LLR fused for port 0 / spatial multiplexing) == decode_fft_estimate followed by decode_pdsch:
+    same chest results, CRCs, payloads and LLRs, over a batch mixing subframes."""
+    rng = np.random.default_rng(5 + k)
+    cfg0, sfl = FUSED[k]
     subs = []
-    for sf in (1, 4, 0):
+    for sf in sfl:
         cfg = pc.Cfg(**{**cfg0.__dict__, "sf_idx": sf})
         iq, payload, _h, _s2 = uc.synth_iq(cfg, rng, snr_db=34, channel="cross")
         subs.append((cfg, iq, payload))
+    ntb = cfg0.nof_tb
     outs = []
     for fused in (False, True):
-        ue = UeDl(cell_of(cfg0), 2)
-        ds = [DevIqSubframe(c, iq, softbuffers=(2 * k, 2 * k + 1)) for k, (c, iq, _) in enumerate(subs)]
+        ue = UeDl(cell_of(cfg0), cfg0.nof_rx)
+        ds = [DevIqSubframe(c, iq, softbuffers=(2 * j, 2 * j + 1)) for j, (c, iq, _) in enumerate(subs)]
         pool = SoftbufferPool(6, max_cb=16)
         jobs = [d.sfjob for d in ds]
         sfs = [d.job.sf for d in ds]
@@ -156,16 +172,15 @@ def test_fused_decode_matches_two_step():
         else:
             chest = ue.fft_estimate(jobs, default_chest_cfg())
             res = ue.decode_pdsch(pool, jobs, sfs, cfgs, chest, pays)
-        nre = ds[0].job.cfg.grant.nof_re
-        e = [ue.pdsch.stage(k, t, ds[k].job.cfg.grant.nof_re, ds[k].job.cfg.grant.nof_re * 8)[2]
-             for k in range(3) for t in range(2)]
-        outs.append(([chest[k].noise_estimate for k in range(3)], [(r.crc, r.avg_iterations_block) for r in res],
-                     [d.payload_bytes(t)[: 97896 // 8] for d in ds for t in range(2)], e))
-        for k, (c, _, payload) in enumerate(subs):
-            for t in range(2):
-                assert res[2 * k + t].crc
-                np.testing.assert_array_equal(ds[k].payload_bytes(t)[: 97896 // 8], payload[t])
+        e = [ue.pdsch.stage(j, t, ds[j].job.cfg.grant.nof_re, ds[j].job.cfg.grant.nof_re * cfg0.qm[t])[2]
+             for j in range(3) for t in range(ntb)]
+        outs.append(([chest[j].noise_estimate for j in range(3)], [(r.crc, r.avg_iterations_block) for r in res],
+                     e))
+        for j, (c, _, payload) in enumerate(subs):
+            for t in range(ntb):
+                assert res[2 * j + t].crc, (k, fused, j, t)
+                np.testing.assert_array_equal(ds[j].payload_bytes(t)[: c.tbs[t] // 8], payload[t])
     assert outs[0][0] == outs[1][0]
     assert outs[0][1] == outs[1][1]
-    for a, b in zip(outs[0][3], outs[1][3]):
+    for a, b in zip(outs[0][2], outs[1][2]):
         np.testing.assert_array_equal(a, b)
