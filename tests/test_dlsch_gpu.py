@@ -14,7 +14,9 @@ pytestmark = pytest.mark.gpu
 # gamma != 0 cases, 16-window and 8-window and generic single-CB sizes
 CASES = [(15840, 2, 30000, 3.0), (97896, 8, 115200, 9.0), (97896, 8, 115200, 5.5), (30576, 6, 36300, 4.5),
          (1000, 2, 3010, 1.0), (456, 2, 1500, 0.5), (40, 2, 200, -1.0), (6120, 4, 14402, 2.0),
-         (75376, 6, 86400, 5.0), (2600, 2, 7800, 0.0)]
+         (75376, 6, 86400, 5.0), (2600, 2, 7800, 0.0),
+         # E several times the circular buffer (rate-dematching wrap-around sums): the SIB sizes of the real signal
+         (144, 2, 1080, 0.0), (256, 2, 1080, -2.0), (40, 2, 600, -3.0)]
 
 
 def _oracle(llrs, cases, rvs, max_its, sbs):

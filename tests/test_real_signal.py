@@ -1,0 +1,117 @@
+"""Real-signal known answer: the reference's own test vector lib/src/phy/phch/test/signal.1.92M.amar.dat
+(a recorded 1.4 MHz eNodeB, cell id 1, 6 PRB, 1 port, CFI 3 -- CMakeLists.txt:440, pdsch_pdcch_file_test)
+carries two SI-RNTI transmissions (subframe 5: SIB1, 144 bits, rv 0; subframe 2: 256 bits, rv 3).  Their grants
+come from tests/golden/real_signal_sib.json (found by tools/find_sib_grant.py: the PDCCH that signals them is
+outside this framework's scope, so every allocation / rv / TBS was tried and the 24-bit TB CRC selected).
+
+A CRC24A pass on a real, noisy, over-the-air-style recording pins the whole receive chain end to end -- OFDM
+demodulation, CRS estimation, equalisation, demapping, descrambling, rate dematching (with 2x wrap-around
+sums), the generic turbo decoder (K <= 400) and both CRCs -- independently of the restatement: the CPU
+oracle chain and the GPU product must both recover the same bytes.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import pdsch_chain as pc
+from oracle import ue_dl_chain as uc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FIX = json.load(open(os.path.join(HERE, "golden", "real_signal_sib.json")))
+IQ = np.fromfile(os.path.join(HERE, "golden", "signal_1.92M_amar.c64"), np.complex64)
+NPRB, CELL, CFI, RNTI = FIX["cell"]["nof_prb"], FIX["cell"]["id"], FIX["cfi"], FIX["rnti"]
+SF_LEN = 15 * uc.symbol_sz(NPRB)
+
+
+def _cfg(s):
+    prb = np.zeros((2, NPRB), np.uint8)
+    prb[:, s["prb_start"]:s["prb_start"] + s["nof_prb"]] = 1
+    return pc.Cfg(nof_prb=NPRB, nof_ports=1, cell_id=CELL, nof_rx=1, cfi=CFI, sf_idx=s["sf"], rnti=RNTI, scheme=0,
+                  nof_layers=1, qm=[2], tbs=[s["tbs"]], rv=[s["rv"], 0], prb=prb)
+
+
+def _oracle_chain(s):
+    iq = IQ[s["sf"] * SF_LEN:(s["sf"] + 1) * SF_LEN]
+    grid = uc.ofdm_rx_sf(iq, NPRB)[None, :]
+    ce, res = uc.chest_estimate(grid, NPRB, 1, CELL, s["sf"])
+    cfg = _cfg(s)
+    _d, _c, e = pc.rx_front(cfg, grid, ce, res["noise_estimate"])
+    ret, data, its = pc.rx_decode(cfg, [e[0]], [oracle.Softbuffer(1)])[0]
+    return ret, np.asarray(data, np.uint8), e[0], res
+
+
+def test_signal_fixture_shape():
+    assert IQ.size == 10 * SF_LEN  # one radio frame of 1.92 Msps
+    assert [s["sf"] for s in FIX["subframes"]] == [2, 5]
+
+
+@pytest.mark.parametrize("k", range(len(FIX["subframes"])))
+def test_oracle_chain_decodes_real_signal(k):
+    s = FIX["subframes"][k]
+    ret, data, _e, _res = _oracle_chain(s)
+    assert ret == 0
+    assert data[: s["tbs"] // 8].tobytes().hex() == s["payload_hex"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", [False, True])
+def test_product_decodes_real_signal(fused):
+    """Both SI transmissions through the GPU chain (two-step and fused ue_dl calls): CRC ok, the fixture's
+    bytes, LLRs within +-1 of the oracle chain (the estimator's float noise estimate may differ in the last
+    ulp), noise estimate within 1e-5 relative."""
+    from srsran_amd import lib
+    from srsran_amd import pdsch as P
+    from srsran_amd.dlsch import SoftbufferPool
+    from srsran_amd.tdec import DeviceBuffer
+    from srsran_amd.ue_dl import DlSfJob, UeDl, default_chest_cfg
+
+    cell = P.make_cell(NPRB, 1, CELL)
+    ue = UeDl(cell, 1)
+    G = 14 * 12 * NPRB
+    subs = FIX["subframes"]
+    n = len(subs)
+    d_iq = DeviceBuffer(n * SF_LEN * 8)
+    d_grid, d_ce, d_pay = DeviceBuffer(n * G * 8), DeviceBuffer(n * G * 8), DeviceBuffer(n * 2 * 64)
+    sfjobs, jobs = [], []
+    for i, s in enumerate(subs):
+        iq = np.ascontiguousarray(IQ[s["sf"] * SF_LEN:(s["sf"] + 1) * SF_LEN])
+        lib().mi355_memcpy_h2d(d_iq.ptr + i * SF_LEN * 8, iq.ctypes.data, iq.nbytes)
+        j = DlSfJob()
+        j.tti = s["sf"]
+        j.in_buffer[0] = d_iq.ptr + i * SF_LEN * 8
+        j.sf_symbols[0] = d_grid.ptr + i * G * 8
+        j.ce[0][0] = d_ce.ptr + i * G * 8
+        sfjobs.append(j)
+        job = P.PdschJob()
+        job.sf.tti, job.sf.cfi = s["sf"], CFI
+        job.cfg.grant = P.make_grant(cell, _cfg(s).prb_mask(), CFI, s["sf"], P.TXSCHEME_PORT0, 1,
+                                     [dict(qm=2, tbs=s["tbs"], rv=s["rv"], cw_idx=0)])
+        job.cfg.rnti = RNTI
+        job.cfg.decoder_type = P.MIMO_DECODER_MMSE
+        job.cfg.softbuffer[0], job.cfg.softbuffer[1] = 2 * i, 2 * i + 1
+        job.sf_symbols[0] = j.sf_symbols[0]
+        job.ce[0][0] = j.ce[0][0]
+        job.payload[0] = d_pay.ptr + 2 * i * 64
+        job.payload[1] = d_pay.ptr + (2 * i + 1) * 64
+        jobs.append(job)
+    pool = SoftbufferPool(2 * n, max_cb=1)
+    pays = [p for jb in jobs for p in (jb.payload[0], jb.payload[1])]
+    if fused:
+        chest, res = ue.decode(pool, sfjobs, [jb.sf for jb in jobs], [jb.cfg for jb in jobs], default_chest_cfg(),
+                               pays)
+    else:
+        chest = ue.fft_estimate(sfjobs, default_chest_cfg())
+        res = ue.decode_pdsch(pool, sfjobs, [jb.sf for jb in jobs], [jb.cfg for jb in jobs], chest, pays)
+    host = np.zeros(n * 2 * 64, np.uint8)
+    d_pay.download(host)
+    for i, s in enumerate(subs):
+        assert res[2 * i].crc and res[2 * i].ret == 0, (fused, s)
+        assert host[2 * i * 64: 2 * i * 64 + s["tbs"] // 8].tobytes().hex() == s["payload_hex"]
+        _ret, _data, e_o, res_o = _oracle_chain(s)
+        assert abs(chest[i].noise_estimate - res_o["noise_estimate"]) <= 1e-5 * res_o["noise_estimate"]
+        nre = jobs[i].cfg.grant.nof_re
+        e_g = ue.pdsch.stage(i, 0, nre, 2 * nre)[2]
+        assert np.abs(e_g.astype(np.int32) - e_o.astype(np.int32)).max() <= 1
