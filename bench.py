@@ -39,6 +39,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # lane-ops/s: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz
+# the MAP kernel's instructions are packed int16 (v_pk_add_i16 clamp / v_pk_max_i16), which issue at half that
+# rate on gfx950: tools/microbench/valu_rate.hip measured 0.555 wave-instr/ns/SIMD (profiles/r01c_valu_rate.txt)
+VALU_PK_I16_TOPS = 0.555 * 64 * 1024 / 1e3
 METRIC = "PDSCH decoded Mbps + code-blocks/sec, 20 MHz TM4 QAM256, 1/2/4/8 GPU"
 
 
@@ -119,7 +122,9 @@ def tdec_roofline(ms, launches, ncb, K):
     if pmc.get("valu_insts_per_launch") and pmc.get("launch_ncb") == ncb:
         rate = pmc["valu_insts_per_launch"] * 64 / (avg / 1e3) / 1e12
         valu = {"achieved": round(rate, 2), "peak": round(VALU_PEAK_TOPS, 1), "unit": "T lane-instr/s",
-                "frac": round(rate / VALU_PEAK_TOPS, 4), "source": "SQ_INSTS_VALU, profiles/tdec_pmc_traffic.json"}
+                "frac": round(rate / VALU_PEAK_TOPS, 4), "peak_packed_i16": round(VALU_PK_I16_TOPS, 1),
+                "frac_packed_i16": round(rate / VALU_PK_I16_TOPS, 4),
+                "source": "SQ_INSTS_VALU, profiles/tdec_pmc_traffic.json; packed-int16 issue rate measured"}
     return roof, valu
 
 
