@@ -21,6 +21,7 @@ constexpr uint32_t RM_LDS     = 3 * 6144 + 12; // N of the largest code block
 constexpr uint32_t RM_THREADS = 1024;
 constexpr int      RM_Q       = (3 * (6144 + 32) + 12 + 8 * RM_THREADS - 1) / (8 * RM_THREADS); // buffer quads per thread
 constexpr int      RM_EQ      = (RM_LDS + 8 * RM_THREADS - 1) / (8 * RM_THREADS);             // LLR quads per thread
+constexpr int      RM_CPB     = 1;                                                              // code blocks per workgroup
 
 __device__ __forceinline__ uint32_t add_pairs(uint32_t a, uint32_t b) // two wrapping int16 additions
 {
@@ -49,77 +50,89 @@ __device__ __forceinline__ uint32_t ld_llr_pair(const int16_t* e, uint32_t r2, b
 __global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
 {
   __shared__ __attribute__((aligned(16))) uint32_t acc32[RM_LDS / 2 + 4];
-  const uint16_t* acc = (const uint16_t*)acc32;
-  const CbDesc&   d   = a.desc[blockIdx.x];
-  if (a.sb_crc[d.slot]) return; // CB already decoded in an earlier transmission (sch.c:385)
-  const uint32_t  N = a.N, tid = threadIdx.x;
-  const uint32_t  n_e = d.n_e, first2 = min(n_e, N) / 2, N2 = N / 2;
-  const uint32_t* inv32 = (const uint32_t*)a.inv[d.rv]; // hipMalloc'd: 16-byte aligned
+  const uint16_t* acc   = (const uint16_t*)acc32;
+  const uint32_t  N     = a.N, tid = threadIdx.x, N2 = N / 2;
   const uint32_t  pairs = a.buflen / 2;
-  const bool      fresh = a.fresh[d.slot] != 0;
-  uint32_t*       sb    = (uint32_t*)(a.sb + (size_t)d.slot * a.sb_stride);
-  const bool      sb16  = ((uintptr_t)sb & 15) == 0;
-  const int16_t*  e     = a.e + d.e_off + d.rp;
-  const bool      e4    = ((uintptr_t)e & 3) == 0, e16 = ((uintptr_t)e & 15) == 0;
-
-  uint4 iv[RM_Q], old[RM_Q], ev[RM_EQ];
+  uint4           iv[RM_Q];
+  uint32_t        iv_rv = 0xffffffffu;
+  // RM_CPB consecutive code blocks per workgroup (usually one TB, one rv): the inverse table is loaded once
+  for (int c = 0; c < RM_CPB; c++) {
+    const int b = blockIdx.x * RM_CPB + c;
+    if (b >= a.ncb) break;
+    const CbDesc& d = a.desc[b];
+    if (a.sb_crc[d.slot]) continue; // CB already decoded in an earlier transmission (sch.c:385)
+    const uint32_t n_e = d.n_e, first2 = min(n_e, N) / 2;
+    const bool     fresh = a.fresh[d.slot] != 0;
+    uint32_t*      sb    = (uint32_t*)(a.sb + (size_t)d.slot * a.sb_stride);
+    const bool     sb16  = ((uintptr_t)sb & 15) == 0;
+    const int16_t* e     = a.e + d.e_off + d.rp;
+    const bool     e4    = ((uintptr_t)e & 3) == 0, e16 = ((uintptr_t)e & 15) == 0;
+    if (d.rv != iv_rv) {
+      const uint32_t* inv32 = (const uint32_t*)a.inv[d.rv]; // hipMalloc'd: 16-byte aligned
 #pragma unroll
-  for (int k = 0; k < RM_Q; k++) iv[k] = ld_quad(inv32, tid + k * RM_THREADS, pairs, true, 0xffffffffu);
-  // pass 0: the first wrap initialises (positions >= n_e get 0)
-#pragma unroll
-  for (int k = 0; k < RM_EQ; k++) {
-    const uint32_t q = tid + k * RM_THREADS;
-    if (e16) {
-      ev[k] = ld_quad((const uint32_t*)e, q, first2, true, 0u);
-    } else {
-      ev[k] = make_uint4(4 * q < first2 ? ld_llr_pair(e, 4 * q, e4) : 0u, 4 * q + 1 < first2 ? ld_llr_pair(e, 4 * q + 1, e4) : 0u,
-                         4 * q + 2 < first2 ? ld_llr_pair(e, 4 * q + 2, e4) : 0u,
-                         4 * q + 3 < first2 ? ld_llr_pair(e, 4 * q + 3, e4) : 0u);
+      for (int k = 0; k < RM_Q; k++) iv[k] = ld_quad(inv32, tid + k * RM_THREADS, pairs, true, 0xffffffffu);
+      iv_rv = d.rv;
     }
-  }
+    uint4 old[RM_Q], ev[RM_EQ];
+    // pass 0: the first wrap initialises (positions >= n_e get 0)
 #pragma unroll
-  for (int k = 0; k < RM_Q; k++)
-    old[k] = fresh ? make_uint4(0u, 0u, 0u, 0u) : ld_quad(sb, tid + k * RM_THREADS, pairs, sb16, 0u);
-#pragma unroll
-  for (int k = 0; k < RM_EQ; k++) {
-    const uint32_t i = 4 * (tid + k * RM_THREADS);
-    if (i + 3 < N2) {
-      *(uint4*)&acc32[i] = ev[k];
-    } else {
-      if (i < N2) acc32[i] = ev[k].x;
-      if (i + 1 < N2) acc32[i + 1] = ev[k].y;
-      if (i + 2 < N2) acc32[i + 2] = ev[k].z;
+    for (int k = 0; k < RM_EQ; k++) {
+      const uint32_t q = tid + k * RM_THREADS;
+      if (e16) {
+        ev[k] = ld_quad((const uint32_t*)e, q, first2, true, 0u);
+      } else {
+        ev[k] = make_uint4(4 * q < first2 ? ld_llr_pair(e, 4 * q, e4) : 0u,
+                           4 * q + 1 < first2 ? ld_llr_pair(e, 4 * q + 1, e4) : 0u,
+                           4 * q + 2 < first2 ? ld_llr_pair(e, 4 * q + 2, e4) : 0u,
+                           4 * q + 3 < first2 ? ld_llr_pair(e, 4 * q + 3, e4) : 0u);
+      }
     }
-  }
-  // later wraps (E > N) accumulate
-  for (uint32_t base = N; base < n_e; base += N) {
+#pragma unroll
+    for (int k = 0; k < RM_Q; k++)
+      old[k] = fresh ? make_uint4(0u, 0u, 0u, 0u) : ld_quad(sb, tid + k * RM_THREADS, pairs, sb16, 0u);
+    __syncthreads(); // the previous code block's gathers from acc are complete
+#pragma unroll
+    for (int k = 0; k < RM_EQ; k++) {
+      const uint32_t i = 4 * (tid + k * RM_THREADS);
+      if (i + 3 < N2) {
+        *(uint4*)&acc32[i] = ev[k];
+      } else {
+        if (i < N2) acc32[i] = ev[k].x;
+        if (i + 1 < N2) acc32[i + 1] = ev[k].y;
+        if (i + 2 < N2) acc32[i + 2] = ev[k].z;
+      }
+    }
+    // later wraps (E > N) accumulate
+    for (uint32_t base = N; base < n_e; base += N) {
+      __syncthreads();
+      const uint32_t lim2 = min(N, n_e - base) / 2;
+      for (uint32_t r2 = tid; r2 < lim2; r2 += RM_THREADS)
+        acc32[r2] = add_pairs(acc32[r2], ld_llr_pair(e + base, r2, e4));
+    }
     __syncthreads();
-    const uint32_t lim2 = min(N, n_e - base) / 2;
-    for (uint32_t r2 = tid; r2 < lim2; r2 += RM_THREADS) acc32[r2] = add_pairs(acc32[r2], ld_llr_pair(e + base, r2, e4));
-  }
-  __syncthreads();
 #pragma unroll
-  for (int k = 0; k < RM_Q; k++) {
-    const uint32_t q = tid + k * RM_THREADS, i = 4 * q;
-    if (i >= pairs) continue;
-    const uint32_t w[4] = {iv[k].x, iv[k].y, iv[k].z, iv[k].w};
-    const uint32_t o[4] = {old[k].x, old[k].y, old[k].z, old[k].w};
-    uint32_t       v[4];
-    bool           any = fresh;
+    for (int k = 0; k < RM_Q; k++) {
+      const uint32_t q = tid + k * RM_THREADS, i = 4 * q;
+      if (i >= pairs) continue;
+      const uint32_t w[4] = {iv[k].x, iv[k].y, iv[k].z, iv[k].w};
+      const uint32_t o[4] = {old[k].x, old[k].y, old[k].z, old[k].w};
+      uint32_t       v[4];
+      bool           any = fresh;
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const uint32_t r0 = w[c] & 0xffffu, r1 = w[c] >> 16;
-      const bool     h0 = r0 != RM_NONE && r0 < n_e, h1 = r1 != RM_NONE && r1 < n_e;
-      any |= h0 || h1;
-      v[c] = add_pairs(o[c], (h0 ? acc[r0] : 0u) | ((h1 ? acc[r1] : 0u) << 16));
-    }
-    if (!any) continue; // nothing to add to an old buffer
-    if (sb16 && i + 3 < pairs) {
-      *(uint4*)(sb + i) = make_uint4(v[0], v[1], v[2], v[3]);
-    } else {
+      for (int cc = 0; cc < 4; cc++) {
+        const uint32_t r0 = w[cc] & 0xffffu, r1 = w[cc] >> 16;
+        const bool     h0 = r0 != RM_NONE && r0 < n_e, h1 = r1 != RM_NONE && r1 < n_e;
+        any |= h0 || h1;
+        v[cc] = add_pairs(o[cc], (h0 ? acc[r0] : 0u) | ((h1 ? acc[r1] : 0u) << 16));
+      }
+      if (!any) continue; // nothing to add to an old buffer
+      if (sb16 && i + 3 < pairs) {
+        *(uint4*)(sb + i) = make_uint4(v[0], v[1], v[2], v[3]);
+      } else {
 #pragma unroll
-      for (int c = 0; c < 4; c++)
-        if (i + c < pairs) sb[i + c] = v[c];
+        for (int cc = 0; cc < 4; cc++)
+          if (i + cc < pairs) sb[i + cc] = v[cc];
+      }
     }
   }
 }
@@ -357,7 +370,7 @@ hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s)
 {
   if (a.ncb <= 0) return hipSuccess;
   if (a.N > RM_LDS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dlsch_rm_rx, dim3((unsigned)a.ncb), dim3(RM_THREADS), 0, s, a);
+  hipLaunchKernelGGL(dlsch_rm_rx, dim3((unsigned)((a.ncb + RM_CPB - 1) / RM_CPB)), dim3(RM_THREADS), 0, s, a);
   hipLaunchKernelGGL(dlsch_rm_consume, dim3((unsigned)((a.ncb + 255) / 256)), dim3(256), 0, s, a.desc, a.ncb, a.fresh,
                      a.sb_crc);
   return hipGetLastError();
