@@ -65,7 +65,14 @@ def parse():
     return ap.parse_args()
 
 
+def dist_backend() -> str:
+    """RCCL ("nccl") on the GPU node; BENCH_DIST_BACKEND=gloo runs the same plumbing on CPU (tests/test_dist.py)."""
+    return os.environ.get("BENCH_DIST_BACKEND", "nccl")
+
+
 def dist_setup():
+    """One process per GPU (torch.distributed.run): the ranks share nothing but the timing barrier and the
+    max-over-ranks reduction -- subframes are independent, so there is no data-path collective."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -74,26 +81,51 @@ def dist_setup():
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        if dist_backend() == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(dist_backend(), rank=rank, world_size=world)
         pg = dist
     return world, rank, local, pg
 
 
 def barrier(pg, local):
     if pg is not None:
-        import torch
-        pg.barrier(device_ids=[local])
-        torch.cuda.synchronize(local)
+        if dist_backend() == "nccl":
+            import torch
+            pg.barrier(device_ids=[local])
+            torch.cuda.synchronize(local)
+        else:
+            pg.barrier()
 
 
 def max_over_ranks(pg, local, v: float) -> float:
     if pg is None:
         return v
     import torch
-    t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{local}")
+    dev = f"cuda:{local}" if dist_backend() == "nccl" else "cpu"
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
     pg.all_reduce(t, op=pg.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(pg, local, v: float) -> float:
+    if pg is None:
+        return v
+    import torch
+    dev = f"cuda:{local}" if dist_backend() == "nccl" else "cpu"
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    pg.all_reduce(t, op=pg.ReduceOp.SUM)
+    return float(t.item())
+
+
+def shard_seed(rank: int) -> int:
+    """Each rank synthesises its own subframes (weak scaling: per-GPU work fixed as N grows)."""
+    return 4242 + rank
+
+
+def whole_job_rate(world: int, units_per_rank: int, steps: int, dt_max: float) -> float:
+    """Units of all ranks over the slowest rank's time (value = whole-job aggregate)."""
+    return world * units_per_rank * steps / dt_max
 
 
 def load_pmc():
@@ -346,7 +378,7 @@ def run_pdsch(args, world, rank, local, pg):
     from srsran_amd.tdec import DeviceBuffer, TdecBatch
     cell = tm4_setup()
     B = args.subframes
-    b = Tm4Batch(cell, B, min(args.distinct, B), args.snr, seed=4242 + rank, device=local)
+    b = Tm4Batch(cell, B, min(args.distinct, B), args.snr, seed=shard_seed(rank), device=local)
     for _ in range(args.warmup):
         b.step()
     lib().mi355_device_sync()
@@ -391,7 +423,8 @@ def run_pdsch(args, world, rank, local, pg):
         roof, valu = tdec_roofline(kms, kl, ncb, 6144)
 
     subframes = world * B * args.steps
-    mbps = subframes * 2 * 97896 / dt / 1e6 * (ok_last / (2 * B))
+    ok_all = int(sum_over_ranks(pg, local, ok_last))  # CRC-ok TBs of the last step, all ranks
+    mbps = whole_job_rate(world, B * 2 * 97896, args.steps, dt) / 1e6 * (ok_all / (2 * B * world))
     res = {
         "metric": METRIC, "value": round(mbps, 1), "unit": "Mbps", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
@@ -403,7 +436,7 @@ def run_pdsch(args, world, rank, local, pg):
                    "parallelism": f"dp{world}"},
         "code_blocks_per_s": round(world * 32 * B * args.steps / dt, 1),
         "subframes_per_s": round(subframes / dt, 1),
-        "crc_ok_tbs": f"{ok_last}/{2 * B}", "avg_half_iterations": round(its, 3),
+        "crc_ok_tbs": f"{ok_all}/{2 * B * world}", "avg_half_iterations": round(its, 3),
         "stage_ms": {k: round(v, 3) for k, v in stages.items()},
         "roofline": roof,
     }
