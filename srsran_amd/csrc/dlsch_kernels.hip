@@ -127,7 +127,8 @@ __global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
       }
       if (!any) continue; // nothing to add to an old buffer
       if (sb16 && i + 3 < pairs) {
-        *(uint4*)(sb + i) = make_uint4(v[0], v[1], v[2], v[3]);
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store((u4v){v[0], v[1], v[2], v[3]}, (u4v*)(sb + i));
       } else {
 #pragma unroll
         for (int cc = 0; cc < 4; cc++)
