@@ -137,7 +137,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   constexpr int NL = NSB / 2;
   constexpr int G  = 64 / NL;
   const int     gl = blockIdx.x * blockDim.x + threadIdx.x;
-  const int     grp = gl >> 6, q = gl & 63;
+  // the wave's group index is wave-uniform: readfirstlane keeps it (and every per-group base pointer) in SGPRs,
+  // so stores address as SGPR base + 32-bit lane offset instead of per-lane 64-bit arithmetic
+  const int     grp = __builtin_amdgcn_readfirstlane(gl >> 6), q = gl & 63;
   const int     cbg = q / NL, l = q % NL;
   if (grp * G + cbg >= a.ncb) return;
   if (a.remaining && *a.remaining == 0) return;  // every code block of the batch has finished
