@@ -12,7 +12,8 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libsrsran_amd.so")
+# MI355_LIB: an alternative in-tree build of the same library (A/B timing of kernel variants on one box)
+LIB_PATH = os.environ.get("MI355_LIB") or os.path.join(HERE, "lib", "libsrsran_amd.so")
 _LIB: C.CDLL | None = None
 
 

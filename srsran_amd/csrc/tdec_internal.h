@@ -22,7 +22,7 @@ struct TdecWinArgs {
   uint32_t*       E;    // DEC1 extrinsic -> DEC2 input (interleaved order), wave-group interleaved
   uint32_t*       D;    // decision LLRs (natural order), wave-group interleaved
   uint32_t*       ckpt; // [group][nseg][8][64] beta checkpoints
-  const uint32_t* dstE; // [L][NL] j' | wlo<<16 | whi<<24 : natural -> interleaved destination
+  const uint32_t* dstE; // [L][NL] (j'*128 + wlo) | (j'*128 + whi) << 16: natural -> interleaved destination
   const uint32_t* dstA; // [L][NL] same, interleaved -> natural
   int             ncb, L, Lp, nseg, n, write_d;
   uint8_t*        dec;  // optional (L % 8 == 0): decision bytes written directly, D not written

@@ -421,13 +421,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
         for (int s = 0; s < 8; s++) st[s] = vmax(c0[s], c1[s]);
         if ((i & 1) == 0 && j != 0) normalize<true>(st);
 
-        // destination row j' (same for every window) and the two destination windows
-        const uint32_t tb   = cd[i];
-        const int      jd   = tb & 0xffff;
-        const int      wlo  = (tb >> 16) & 0xff, whi = tb >> 24;
-        const size_t   rowd = (size_t)jd * 128 + lane0 * 2;
-        const size_t   olo  = rowd + (wlo >> 1) * 2 + (wlo & 1);
-        const size_t   ohi  = rowd + (whi >> 1) * 2 + (whi & 1);
+        // destinations: j'*128 + window of this lane's two outputs (j' shared by every window of the CB)
+        const uint32_t tb  = cd[i];
+        const uint32_t olo = (tb & 0xffffu) + lane0 * 2, ohi = (tb >> 16) + lane0 * 2;
         if constexpr (!dec2) {
           // e = ext1 - app1 (wrapping), turbodecoder_iter.h:118-120 of the next DEC2
           const v2s ev = has_ap ? out - U(ca[i]) : out;
@@ -441,6 +437,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
           A16[olo]     = av.x;
           A16[ohi]     = av.y;
           if (wr_bm) { // natural bit w*L + j': byte w*L/8 + j'/8, bit 7 - j'%8 (turbodecoder_win.h:973-993)
+            const uint32_t jd = (tb & 0xffffu) >> 7, wlo = tb & 15u, whi = (tb >> 16) & 15u;
             const uint32_t blo = wlo * (L / 8) + (jd >> 3), bhi = whi * (L / 8) + (jd >> 3);
             const uint32_t sh  = 7 - (jd & 7);
             atomicOr(&bm[blo >> 2], (uint32_t)(out.x > 0) << (((blo & 3) << 3) + sh));

@@ -113,8 +113,9 @@ static int get_tables(mi355_tdec_batch_t* q, const Geometry& g, KTables** out)
         uint32_t n0 = (2 * l) * g.L + j, n1 = (2 * l + 1) * g.L + j;
         uint32_t e0 = inv[n0], e1 = inv[n1], a0 = pi[n0], a1 = pi[n1];
         if (e0 % g.L != e1 % g.L || a0 % g.L != a1 % g.L) return MI355_ERROR; // not contention-free
-        dE[(size_t)j * g.nl + l] = (e0 % g.L) | ((e0 / g.L) << 16) | ((e1 / g.L) << 24);
-        dA[(size_t)j * g.nl + l] = (a0 % g.L) | ((a0 / g.L) << 16) | ((a1 / g.L) << 24);
+        // int16 offsets inside the wave group's row block: row j' (128 int16 per row) + window
+        dE[(size_t)j * g.nl + l] = ((e0 % g.L) * 128 + e0 / g.L) | (((e1 % g.L) * 128 + e1 / g.L) << 16);
+        dA[(size_t)j * g.nl + l] = ((a0 % g.L) * 128 + a0 / g.L) | (((a1 % g.L) * 128 + a1 / g.L) << 16);
       }
     }
     CHECK_HIP(hipMalloc(&t.dstE, dE.size() * 4));
