@@ -48,6 +48,8 @@ typedef struct {
   uint32_t id;
   uint32_t cp;         /* MI355_CP_NORM / MI355_CP_EXT */
   uint32_t frame_type; /* MI355_FDD / MI355_TDD */
+  uint32_t phich_length;    /* MI355_PHICH_NORM / _EXT (pdcch.h); only the control-channel REG map reads it */
+  uint32_t phich_resources; /* MI355_PHICH_R_1_6 ... _R_2 */
 } mi355_cell_t;
 
 typedef struct {

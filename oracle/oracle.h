@@ -52,6 +52,27 @@ int orc_predecode(const float* y, const float* h, int nof_rx, int nof_ports, int
 int orc_tdec_run_batch(const int16_t* bufs, uint32_t stride, uint32_t ncb, uint32_t K, uint32_t nhalf, uint8_t* out,
                        int nthreads);
 
+/* downlink control channels (orc_pdcch.c) */
+int      orc_regs_init(uint32_t nof_prb, uint32_t nof_ports, uint32_t cell_id, uint32_t cp_ext, uint32_t phich_res,
+                       uint32_t phich_ext, uint32_t phich_mi, uint32_t* pcfich_re, uint32_t* pdcch_re, uint32_t nregs_max,
+                       uint32_t* pdcch_nregs, uint32_t* phich_re);
+void     orc_ctrl_equalize(const float* y, const float* h, int nof_rx, int nof_ports, int n, float noise, float* d);
+int      orc_pcfich_decode(const float* grid, const float* ce, int nof_rx, int nof_ports, int grid_len,
+                           const uint32_t* pcfich_re, uint32_t cell_id, uint32_t sf_idx, float noise, float* corr,
+                           float* llr_out);
+int      orc_pdcch_llr(const float* grid, const float* ce, int nof_rx, int nof_ports, int grid_len, const uint32_t* re,
+                       uint32_t nregs, uint32_t cell_id, uint32_t sf_idx, float noise, float* llr);
+uint32_t orc_pdcch_ue_locations(uint32_t nof_cce, uint32_t sf_idx, uint32_t rnti, uint32_t* L, uint32_t* ncce);
+uint32_t orc_pdcch_common_locations(uint32_t nof_cce, uint32_t* L, uint32_t* ncce);
+void     orc_rm_conv_rx(const float* in, uint32_t E, float* out, uint32_t out_len);
+void     orc_rm_conv_tx(const uint8_t* in, uint32_t in_len, uint8_t* out, uint32_t E);
+void     orc_conv_encode_tb(const uint8_t* in, uint32_t F, uint8_t* out);
+void     orc_viterbi_quant(const float* x, uint32_t len, uint16_t* out);
+int      orc_viterbi37_tb_decode_us(const uint16_t* sym, uint32_t F, uint8_t* data);
+uint32_t orc_crc16_bits(const uint8_t* bits, uint32_t n);
+int      orc_pdcch_decode_candidate(const float* llr, uint32_t E, uint32_t nof_bits, uint8_t* payload, uint16_t* crc_rem);
+void     orc_pdcch_encode(const uint8_t* payload, uint32_t nof_bits, uint32_t rnti, uint32_t E, uint8_t* e);
+
 #ifdef __cplusplus
 }
 #endif

@@ -181,8 +181,9 @@ def channel_freq(rng: np.random.Generator, nof_ports: int, nof_rx: int, nof_prb:
 
 
 def synth_iq(cfg: pc.Cfg, rng: np.random.Generator, snr_db: float = 30.0, payload_bits=None, max_delay: int = 6,
-             channel: str = "taps"):
+             channel: str = "taps", ctrl=None):
     """channel: "taps" (random taps up to max_delay samples) or "cross" (phy_dl_test's flat 2x2 [[1,1],[1,-1]]).
+    ctrl: optional callable(tx) writing the control region (PCFICH / PDCCH) into the (ports, grid) tx grids.
     Returns (iq (nof_rx, N*15) complex64, payload bytes per TB, true per-subcarrier channel, noise var)."""
     idx = pdsch_re_map(cfg.nof_prb, cfg.nof_ports, cfg.cell_id, cfg.prb_mask(), cfg.lstart, cfg.sf_idx)
     nre = 12 * cfg.nof_prb
@@ -200,6 +201,8 @@ def synth_iq(cfg: pc.Cfg, rng: np.random.Generator, snr_db: float = 30.0, payloa
     tx = np.zeros((cfg.nof_ports, G), np.complex64)
     tx[:, idx] = pc.precode(d, cfg)
     crs_put(tx, cfg.nof_prb, cfg.cell_id, cfg.nof_ports, cfg.sf_idx)
+    if ctrl is not None:
+        ctrl(tx)
     if channel == "cross":
         w = np.array([[1, 1], [1, -1]], np.complex64)[: cfg.nof_ports, : cfg.nof_rx]
         h = np.repeat(w[:, :, None], nre, axis=2).astype(np.complex64)

@@ -1,0 +1,152 @@
+// srsran_amd/csrc/pdcch_runtime.cpp -- host runtime of the control-channel stage: the cell's REG map and
+// scrambling sequences resident in HBM, per-call descriptor upload, the two kernels (PCFICH + PDCCH LLRs, blind
+// candidate decoding), one read-back of the CFIs and candidate results, and the host replay of the UE's
+// sequential blind search (ue_dl.c:450-730).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <stdio.h>
+#include <string.h>
+#include <vector>
+
+#include "host_staging.h"
+#include "lte_common.h"
+#include "pdcch_internal.h"
+#include "pdcch_runtime.h"
+
+#define CHECK_HIP(x)                                                                                                   \
+  do {                                                                                                                 \
+    hipError_t e_ = (x);                                                                                               \
+    if (e_ != hipSuccess) {                                                                                            \
+      fprintf(stderr, "[srsran_amd] %s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));                 \
+      return MI355_ERROR;                                                                                              \
+    }                                                                                                                  \
+  } while (0)
+
+namespace mi355 {
+
+CtrlState::~CtrlState()
+{
+  (void)hipFree(d_tab);
+  (void)hipFree(d_buf);
+  delete st;
+  delete back;
+}
+
+int CtrlState::init(const mi355_cell_t& c, uint32_t nrx)
+{
+  cell   = c;
+  nof_rx = nrx;
+  if (!regs_build(cell, 1, regs)) return MI355_ERROR;
+  // table layout: pcfich_re[16] | pdcch_re[3][PDCCH_MAX_REGS*4] | pcfich_seq[10] | pdcch_seq[10][seq_words]
+  seq_words = (8 * regs.nregs[2] + 31) / 32;
+  std::vector<uint32_t> tab(16 + 3 * PDCCH_MAX_REGS * 4 + 10 + 10 * seq_words, 0u);
+  memcpy(tab.data(), regs.pcfich, sizeof(regs.pcfich));
+  for (uint32_t cfi = 0; cfi < 3; cfi++)
+    std::copy(regs.pdcch[cfi].begin(), regs.pdcch[cfi].end(), tab.begin() + 16 + cfi * PDCCH_MAX_REGS * 4);
+  std::vector<uint8_t> c0;
+  for (uint32_t sf = 0; sf < 10; sf++) {
+    gold_sequence((sf + 1) * (2 * cell.id + 1) * 512 + cell.id, 32, c0); // sequences.c:39-42
+    uint32_t w = 0;
+    for (uint32_t j = 0; j < 32; j++) w |= (uint32_t)c0[j] << j;
+    tab[16 + 3 * PDCCH_MAX_REGS * 4 + sf] = w;
+    gold_sequence(sf * 512 + cell.id, 32 * seq_words, c0); // sequences.c:55-58
+    for (uint32_t j = 0; j < 32 * seq_words; j++)
+      tab[16 + 3 * PDCCH_MAX_REGS * 4 + 10 + sf * seq_words + j / 32] |= (uint32_t)c0[j] << (j % 32);
+  }
+  CHECK_HIP(hipMalloc(&d_tab, tab.size() * 4));
+  CHECK_HIP(hipMemcpy(d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+  st   = new HostStaging;
+  back = new HostStaging;
+  return MI355_SUCCESS;
+}
+
+int CtrlState::run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, const float* d_noise,
+                   const uint16_t* rntis, const mi355_ue_dl_cfg_t* cfgs, uint32_t n, hipStream_t s,
+                   mi355_ctrl_res_t* res, mi355_dci_msg_t* msgs)
+{
+  if (!n) return MI355_SUCCESS;
+  const uint32_t stride = (8 * regs.nregs[2] + 63) / 64 * 64; // LLRs per subframe (CFI 3 worst case)
+  const size_t   b_jobs = staged_size((size_t)n * sizeof(CtrlJob)), b_blind = staged_size((size_t)n * sizeof(BlindJob));
+  const size_t   b_llr = staged_size((size_t)n * stride * 4), b_cfi = staged_size((size_t)n * 4);
+  const size_t   b_corr = staged_size((size_t)n * 12);
+  const size_t   b_cand = staged_size((size_t)n * PDCCH_SLOTS * PDCCH_FMTS * sizeof(DciCand));
+  const size_t   need   = b_jobs + b_blind + b_llr + b_cfi + b_corr + b_cand;
+  if (need > cap) {
+    if (d_buf) {
+      CHECK_HIP(hipStreamSynchronize(s));
+      CHECK_HIP(hipFree(d_buf));
+      d_buf = nullptr;
+    }
+    cap = need + need / 4;
+    CHECK_HIP(hipMalloc(&d_buf, cap));
+  }
+  char* base = d_buf;
+  CHECK_HIP(st->reserve(b_jobs + b_blind));
+  auto* cj = (CtrlJob*)st->slot((size_t)n * sizeof(CtrlJob));
+  auto* bj = (BlindJob*)st->slot((size_t)n * sizeof(BlindJob));
+  for (uint32_t i = 0; i < n; i++) {
+    CtrlJob& J = cj[i];
+    memset(&J, 0, sizeof(J));
+    for (uint32_t r = 0; r < nof_rx; r++) {
+      if (!sfjobs[i].sf_symbols[r]) return MI355_ERROR_INVALID_INPUTS;
+      J.grid[r] = (const float2*)sfjobs[i].sf_symbols[r];
+      for (uint32_t p = 0; p < cell.nof_ports; p++) {
+        if (!sfjobs[i].ce[p][r]) return MI355_ERROR_INVALID_INPUTS;
+        J.ce[p][r] = (const float2*)sfjobs[i].ce[p][r];
+      }
+    }
+    J.d_noise = d_noise ? d_noise + i : nullptr;
+    J.noise   = host_noise ? host_noise[i] : 0.f;
+    J.sf_idx  = sfjobs[i].tti % 10;
+    bj[i]     = blind_plan(cell, J.sf_idx, rntis[i], cfgs[i]);
+  }
+  CHECK_HIP(st->upload(base, s));
+  float*    d_llr  = (float*)(base + b_jobs + b_blind);
+  uint32_t* d_cfi  = (uint32_t*)(base + b_jobs + b_blind + b_llr);
+  float*    d_corr = (float*)(base + b_jobs + b_blind + b_llr + b_cfi);
+  DciCand*  d_cand = (DciCand*)(base + b_jobs + b_blind + b_llr + b_cfi + b_corr);
+  CtrlArgs  a{};
+  a.jobs       = (const CtrlJob*)base;
+  a.pcfich_re  = d_tab;
+  a.pdcch_re   = d_tab + 16;
+  a.pcfich_seq = d_tab + 16 + 3 * PDCCH_MAX_REGS * 4;
+  a.pdcch_seq  = a.pcfich_seq + 10;
+  a.seq_words  = seq_words;
+  for (int c = 0; c < 3; c++) a.nregs[c] = regs.nregs[c];
+  a.nof_rx     = nof_rx;
+  a.nof_ports  = cell.nof_ports;
+  a.llr        = d_llr;
+  a.llr_stride = stride;
+  a.cfi        = d_cfi;
+  a.corr       = d_corr;
+  CHECK_HIP(ctrl_launch_llr(a, n, s));
+  BlindArgs b{};
+  b.jobs       = (const BlindJob*)(base + b_jobs);
+  b.llr        = d_llr;
+  b.llr_stride = stride;
+  b.cfi        = d_cfi;
+  for (int c = 0; c < 3; c++) b.ncce[c] = regs.nregs[c] / 9;
+  b.out = d_cand;
+  CHECK_HIP(ctrl_launch_blind(b, n, s));
+  last_n = n, last_stride = stride, last_llr = d_llr, last_cand = d_cand;
+  // one read-back: cfi | corr | candidates (contiguous in the arena)
+  const size_t nback = b_cfi + b_corr + (size_t)n * PDCCH_SLOTS * PDCCH_FMTS * sizeof(DciCand);
+  CHECK_HIP(back->reserve(nback));
+  CHECK_HIP(hipMemcpyAsync(back->host, d_cfi, nback, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipStreamSynchronize(s));
+  const uint32_t* h_cfi  = (const uint32_t*)back->host;
+  const float*    h_corr = (const float*)(back->host + b_cfi);
+  const DciCand*  h_cand = (const DciCand*)(back->host + b_cfi + b_corr);
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t cfi = h_cfi[i];
+    res[i].cfi         = cfi;
+    res[i].cfi_corr    = std::max({0.f, h_corr[3 * i], h_corr[3 * i + 1], h_corr[3 * i + 2]});
+    res[i].nof_cce     = regs.nregs[cfi - 1] / 9;
+    res[i].nof_dci     = blind_search_replay(cell, res[i].nof_cce, sfjobs[i].tti % 10, rntis[i], cfgs[i],
+                                         h_cand + (size_t)i * PDCCH_SLOTS * PDCCH_FMTS, msgs + (size_t)i * MI355_MAX_DCI_MSG);
+  }
+  return MI355_SUCCESS;
+}
+
+} // namespace mi355

@@ -1,0 +1,33 @@
+// srsran_amd/csrc/pdcch_runtime.h -- the control-channel stage owned by a mi355_ue_dl_t (pdcch_runtime.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "pdcch_internal.h"
+
+namespace mi355 {
+
+struct HostStaging;
+
+struct CtrlState {
+  mi355_cell_t cell{};
+  uint32_t     nof_rx    = 1;
+  RegMap       regs;
+  uint32_t*    d_tab     = nullptr; // REG map + scrambling words, resident
+  uint32_t     seq_words = 0;
+  char*        d_buf     = nullptr; // per-call arena: descriptors | LLRs | CFIs | correlations | candidates
+  size_t       cap       = 0;
+  HostStaging* st        = nullptr;
+  HostStaging* back      = nullptr;
+  uint32_t     last_n = 0, last_stride = 0; // the previous call's arena layout (inspection accessors)
+  float*       last_llr  = nullptr;
+  DciCand*     last_cand = nullptr;
+
+  ~CtrlState();
+  int init(const mi355_cell_t& c, uint32_t nof_rx);
+  // PCFICH + PDCCH LLRs + blind decoding of n subframes on s, then the blind-search replay (synchronous).
+  // Noise per subframe from host_noise[i] or, when host_noise is null, from device memory d_noise[i].
+  int run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, const float* d_noise, const uint16_t* rntis,
+          const mi355_ue_dl_cfg_t* cfgs, uint32_t n, hipStream_t s, mi355_ctrl_res_t* res, mi355_dci_msg_t* msgs);
+};
+
+} // namespace mi355

@@ -10,12 +10,14 @@
 #include <string.h>
 #include <vector>
 
+#include "../../include/srsran_amd/pdcch.h"
 #include "../../include/srsran_amd/pdsch.h"
 #include "../../include/srsran_amd/tdec.h"
 #include "../../include/srsran_amd/ue_dl.h"
 #include "lte_common.h"
 #include "runtime_internal.h"
 #include "host_staging.h"
+#include "pdcch_runtime.h"
 #include "ue_dl_internal.h"
 
 using namespace mi355;
@@ -81,6 +83,7 @@ struct mi355_ue_dl {
   HostStaging    st_ofdm, st_chest, back; // pinned descriptor uploads / estimator read-back
   hipStream_t    side     = nullptr;       // estimator read-back + fill_res overlapping the PDSCH decode
   hipEvent_t     ev_chest = nullptr;
+  CtrlState*     ctrl     = nullptr;       // PCFICH / PDCCH stage, built on first use
   std::mutex     mu;
 };
 
@@ -380,6 +383,7 @@ void mi355_ue_dl_destroy(mi355_ue_dl_t* q)
   if (q->own) (void)hipStreamDestroy(q->own);
   if (q->side) (void)hipStreamDestroy(q->side);
   if (q->ev_chest) (void)hipEventDestroy(q->ev_chest);
+  delete q->ctrl;
   delete q;
 }
 
@@ -499,6 +503,154 @@ int mi355_ue_dl_decode_pdsch_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* po
     j.payload[1] = payloads[2 * i + 1];
   }
   return mi355_pdsch_decode_batch(q->pdsch, pool, jobs.data(), njobs, res, stream);
+}
+
+static int ctrl_ready(mi355_ue_dl_t* q)
+{
+  if (q->ctrl) return MI355_SUCCESS;
+  auto* c = new CtrlState;
+  int   r = c->init(q->cell, q->nof_rx);
+  if (r) {
+    delete c;
+    return r;
+  }
+  q->ctrl = c;
+  return MI355_SUCCESS;
+}
+
+// search results -> srslte_dci_dl_t (srslte_dci_msg_unpack_pdsch with the UE's DCI configuration, ue_dl.c:722-728)
+static int unpack_all(mi355_ue_dl_t* q, const mi355_dl_sf_cfg_t* sfs, const mi355_ue_dl_cfg_t* cfgs, uint32_t n,
+                      mi355_ctrl_res_t* ctrl, std::vector<mi355_dci_msg_t>& msgs, mi355_dci_dl_t* dci)
+{
+  for (uint32_t i = 0; i < n; i++) {
+    for (int k = 0; k < ctrl[i].nof_dci; k++) {
+      mi355_dci_msg_t& m = msgs[(size_t)i * MI355_MAX_DCI_MSG + k];
+      if (mi355_dci_msg_unpack_pdsch(&q->cell, &sfs[i], &cfgs[i].dci, &m, &dci[(size_t)i * MI355_MAX_DCI_MSG + k]))
+        ctrl[i].nof_dci = -1; // "Error unpacking DL DCI" (ue_dl.c:724-727)
+      if (ctrl[i].nof_dci < 0) break;
+    }
+  }
+  return MI355_SUCCESS;
+}
+
+int mi355_ue_dl_find_dl_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* sfjobs, mi355_dl_sf_cfg_t* sfs,
+                                  const mi355_ue_dl_cfg_t* cfgs, const uint16_t* rntis,
+                                  const mi355_chest_dl_res_t* chest, uint32_t njobs, mi355_ctrl_res_t* ctrl,
+                                  mi355_dci_dl_t* dci, void* stream)
+{
+  if (!q || (njobs && (!sfjobs || !sfs || !cfgs || !rntis || !chest || !ctrl || !dci))) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  int r = ctrl_ready(q);
+  if (r) return r;
+  std::vector<float>           noise(njobs);
+  std::vector<mi355_dci_msg_t> msgs((size_t)njobs * MI355_MAX_DCI_MSG);
+  for (uint32_t i = 0; i < njobs; i++) noise[i] = chest[i].noise_estimate;
+  if ((r = q->ctrl->run(sfjobs, noise.data(), nullptr, rntis, cfgs, njobs, stream ? (hipStream_t)stream : q->own, ctrl,
+                        msgs.data())))
+    return r;
+  for (uint32_t i = 0; i < njobs; i++) sfs[i].cfi = ctrl[i].cfi;
+  return unpack_all(q, sfs, cfgs, njobs, ctrl, msgs, dci);
+}
+
+int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, const mi355_dl_sf_job_t* sfjobs,
+                                      mi355_dl_sf_cfg_t* sfs, const mi355_ue_dl_cfg_t* ue_cfgs, mi355_pdsch_cfg_t* cfgs,
+                                      const mi355_chest_dl_cfg_t* chest_cfg, mi355_chest_dl_res_t* chest,
+                                      uint8_t* const* payloads, uint32_t njobs, mi355_ctrl_res_t* ctrl,
+                                      mi355_dci_dl_t* dci, mi355_pdsch_res_t* res, void* stream)
+{
+  if (!q || !pool || !res || !chest || !ctrl || !dci ||
+      (njobs && (!sfjobs || !sfs || !ue_cfgs || !cfgs || !payloads || !chest_cfg)))
+    return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t s = stream ? (hipStream_t)stream : q->own;
+  int         r = ctrl_ready(q);
+  if (r) return r;
+  // srslte_ue_dl_decode_fft_estimate: OFDM + estimation; the noise estimate stays on the device for the control
+  // channels, the host fills srslte_chest_dl_res_t while the control kernels run
+  size_t used = 0;
+  if ((r = ofdm_run(q, sfjobs, njobs, s, &used))) return r;
+  float *d_out = nullptr, *d_noise = nullptr;
+  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise))) return r;
+  ChestFill fill{q, chest_cfg, nullptr, njobs, chest, false};
+  if ((r = chest_finish_async(q, &fill, d_out, s))) return r;
+  std::vector<uint16_t>        rntis(njobs);
+  std::vector<mi355_dci_msg_t> msgs((size_t)njobs * MI355_MAX_DCI_MSG);
+  for (uint32_t i = 0; i < njobs; i++) rntis[i] = cfgs[i].rnti;
+  r = q->ctrl->run(sfjobs, nullptr, d_noise, rntis.data(), ue_cfgs, njobs, s, ctrl, msgs.data());
+  chest_fill_cb(&fill);
+  if (r) return r;
+  for (uint32_t i = 0; i < njobs; i++) sfs[i].cfi = ctrl[i].cfi;
+  if ((r = unpack_all(q, sfs, ue_cfgs, njobs, ctrl, msgs, dci))) return r;
+  // DCI -> grant, RV from the SFN for format 1C, softbuffer reset (ue_dl.c:1494-1535)
+  std::vector<mi355_pdsch_job_t> jobs;
+  std::vector<uint32_t>          which;
+  for (uint32_t i = 0; i < njobs; i++) {
+    if (ctrl[i].nof_dci != 1) continue; // the reference decodes only when exactly one DCI was found
+    const mi355_dci_dl_t& d = dci[(size_t)i * MI355_MAX_DCI_MSG];
+    if (mi355_ra_dl_dci_to_grant(&q->cell, &sfs[i], ue_cfgs[i].tm, ue_cfgs[i].use_tbs_index_alt, &d, &cfgs[i].grant)) {
+      ctrl[i].nof_dci = -1; // "Error unpacking DCI"
+      continue;
+    }
+    for (int tb = 0; tb < MI355_MAX_CODEWORDS; tb++) {
+      mi355_ra_tb_t& t = cfgs[i].grant.tb[tb];
+      if (!t.enabled) continue;
+      if ((int32_t)t.rv < 0) {
+        const uint32_t k = ((sfs[i].tti / 10) / 2) % 4;
+        t.rv             = ((uint32_t)ceilf(1.5f * k)) % 4;
+      }
+      if ((r = mi355_softbuffer_reset_tbs(pool, cfgs[i].softbuffer[tb], (uint32_t)t.tbs, s))) return r;
+    }
+    mi355_pdsch_job_t j;
+    memset(&j, 0, sizeof(j));
+    j.sf             = sfs[i];
+    j.cfg            = cfgs[i];
+    j.noise_estimate = chest[i].noise_estimate;
+    for (uint32_t a = 0; a < q->nof_rx; a++) {
+      j.sf_symbols[a] = sfjobs[i].sf_symbols[a];
+      for (uint32_t p = 0; p < q->cell.nof_ports; p++) j.ce[p][a] = sfjobs[i].ce[p][a];
+    }
+    j.payload[0] = payloads[2 * i];
+    j.payload[1] = payloads[2 * i + 1];
+    for (int tb = 0; tb < 2; tb++) res[2 * i + tb].crc = 0;
+    jobs.push_back(j);
+    which.push_back(i);
+  }
+  if (jobs.empty()) return MI355_SUCCESS;
+  std::vector<mi355_pdsch_res_t> sub(2 * jobs.size());
+  for (size_t k = 0; k < jobs.size(); k++) sub[2 * k] = res[2 * which[k]], sub[2 * k + 1] = res[2 * which[k] + 1];
+  r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), (uint32_t)jobs.size(), sub.data(), s, nullptr,
+                                   WaitHook{}, true);
+  for (size_t k = 0; k < jobs.size(); k++) res[2 * which[k]] = sub[2 * k], res[2 * which[k] + 1] = sub[2 * k + 1];
+  return r;
+}
+
+int mi355_ue_dl_ctrl_llr(mi355_ue_dl_t* q, uint32_t i, float* llr, uint32_t max_llr)
+{
+  if (!q || !q->ctrl || i >= q->ctrl->last_n || !llr) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  uint32_t cfi = 0;
+  CHECK_HIP(hipDeviceSynchronize());
+  // the CFI array follows the LLRs in the arena (pdcch_runtime.cpp)
+  const char* cfi_base = (const char*)(q->ctrl->last_llr) + staged_size((size_t)q->ctrl->last_n * q->ctrl->last_stride * 4);
+  CHECK_HIP(hipMemcpy(&cfi, cfi_base + 4 * i, 4, hipMemcpyDeviceToHost));
+  if (cfi < 1 || cfi > 3) return MI355_ERROR;
+  const uint32_t n = std::min(8 * q->ctrl->regs.nregs[cfi - 1], max_llr);
+  CHECK_HIP(hipMemcpy(llr, q->ctrl->last_llr + (size_t)i * q->ctrl->last_stride, n * 4, hipMemcpyDeviceToHost));
+  return (int)n;
+}
+
+int mi355_ue_dl_ctrl_candidates(mi355_ue_dl_t* q, uint32_t i, uint32_t* out, uint32_t max_words)
+{
+  if (!q || !q->ctrl || i >= q->ctrl->last_n || !out) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  const uint32_t words = std::min<uint32_t>(PDCCH_SLOTS * PDCCH_FMTS * sizeof(DciCand) / 4, max_words);
+  CHECK_HIP(hipDeviceSynchronize());
+  CHECK_HIP(hipMemcpy(out, q->ctrl->last_cand + (size_t)i * PDCCH_SLOTS * PDCCH_FMTS, words * 4, hipMemcpyDeviceToHost));
+  return (int)words;
 }
 
 } // extern "C"

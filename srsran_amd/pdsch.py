@@ -23,7 +23,7 @@ MIMO_DECODER_ZF, MIMO_DECODER_MMSE = 0, 1
 
 class Cell(C.Structure):
     _fields_ = [("nof_prb", C.c_uint32), ("nof_ports", C.c_uint32), ("id", C.c_uint32), ("cp", C.c_uint32),
-                ("frame_type", C.c_uint32)]
+                ("frame_type", C.c_uint32), ("phich_length", C.c_uint32), ("phich_resources", C.c_uint32)]
 
 
 class DlSfCfg(C.Structure):
@@ -72,8 +72,10 @@ def _declare():
     return L
 
 
-def make_cell(nof_prb: int, nof_ports: int = 1, cell_id: int = 0, cp: int = 0, frame_type: int = 0) -> Cell:
-    return Cell(nof_prb, nof_ports, cell_id, cp, frame_type)
+def make_cell(nof_prb: int, nof_ports: int = 1, cell_id: int = 0, cp: int = 0, frame_type: int = 0,
+              phich_length: int = 0, phich_resources: int = 0) -> Cell:
+    """srslte_cell_t; phich_resources 0 R1/6, 1 R1/2, 2 R1, 3 R2 (only the control-channel REG map reads it)."""
+    return Cell(nof_prb, nof_ports, cell_id, cp, frame_type, phich_length, phich_resources)
 
 
 def re_map(cell: Cell, grant: PdschGrant, cfi: int, sf_idx: int) -> np.ndarray:

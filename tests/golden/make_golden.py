@@ -14,6 +14,11 @@ Contents
   crc_cbsegm.npz     CRC24A/24B/16/8 checksums and CB segmentation for a TBS sweep.
   rm_turbo.npz       srslte_rm_turbo_rx_lut (AVX build): E LLRs -> decoder buffer, every rv, E below /
                      at / above the circular buffer (wrap-around), plus HARQ accumulation rv0 + rv2.
+  pdcch.npz          downlink control channels: REG maps (srslte_regs_init_opts: PCFICH / PHICH / per-CFI PDCCH),
+                     UE / common search spaces, CRC16, the tail-biting Viterbi decoder on u16 symbols
+                     (srslte_viterbi_decode_us, AVX2 16-bit build), srslte_pdcch_dci_decode on noisy LLRs,
+                     srslte_pdcch_dci_encode, and srslte_pcfich_decode / srslte_pdcch_extract_llr on synthetic
+                     control regions (1 / 2 / 4 ports, 1 / 2 rx).  ``make_golden.py pdcch`` regenerates only this.
   pdsch_stages.npz   srslte_demod_soft_demodulate_s for every modulation (SIMD bodies and scalar tails,
                      saturating amplitudes), srslte_scrambling_s_offset (PDSCH c_init), and
                      srslte_predecoding_type with CSI (AVX2 build, MMSE) for every scheme srslte_pdsch_decode
@@ -220,10 +225,127 @@ def gen_pdsch_stages(rng):
     print("pdsch_stages.npz:", data["demod_n"], "demod,", data["scr_n"], "scrambling,", k, "predecoding cases")
 
 
+def gen_pdcch(rng):
+    import ctypes as C
+
+    from oracle import pdcch_chain as P
+    R = P._ref()
+    data = {}
+    cells = [(6, 1, 1, 2), (15, 2, 0, 0), (25, 2, 3, 1), (50, 4, 7, 3), (75, 1, 301, 2), (100, 2, 1, 0),
+             (100, 4, 503, 1), (100, 1, 77, 2)]
+    for k, (nprb, ports, cid, res) in enumerate(cells):
+        rg = P.regs(nprb, ports, cid, res, use_ref=True)
+        data[f"regs{k}_cell"] = np.array([nprb, ports, cid, res], np.int32)
+        data[f"regs{k}_pcfich"] = rg.pcfich
+        data[f"regs{k}_nregs"] = rg.nregs
+        for c in range(3):
+            data[f"regs{k}_pdcch{c}"] = rg.pdcch[c]
+        data[f"regs{k}_phich"] = rg.phich
+    data["regs_n"] = np.int32(len(cells))
+    locs = []
+    for ncce in (1, 2, 5, 8, 17, 21, 43, 86, 88):
+        for sf in range(10):
+            for rnti in (0x1234, 0x000B, 0xFFF3, 0x4601):
+                u = P.ue_locations(ncce, sf, rnti, use_ref=True)
+                locs.append([ncce, sf, rnti, len(u)] + [v for lv in u for v in lv] + [0] * (32 - 2 * len(u)))
+        c = P.common_locations(ncce, use_ref=True)
+        locs.append([ncce, 0, 0xFFFF, len(c)] + [v for lv in c for v in lv] + [0] * (32 - 2 * len(c)))
+    data["locations"] = np.array(locs, np.int32)
+    k = 0
+    for n in (1, 7, 8, 15, 16, 27, 43, 57, 61, 128):
+        for _ in range(2):
+            b = rng.integers(0, 2, n, dtype=np.uint8)
+            data[f"crc{k}_bits"] = b
+            data[f"crc{k}_crc"] = np.uint32(R.ref_crc16(b, n))
+            k += 1
+    data["crc_n"] = np.int32(k)
+    k = 0
+    for F in (28, 37, 43, 57, 60, 72, 144):
+        for kind in ("noisy", "rand", "edge"):
+            if kind == "rand":
+                sym = rng.integers(0, 65536, 3 * F, dtype=np.uint16)
+            elif kind == "edge":
+                sym = rng.choice(np.array([0, 1, 32767, 32768, 65534, 65535], np.uint16), 3 * F)
+            else:
+                bits = rng.integers(0, 2, F, dtype=np.uint8)
+                coded = np.zeros(3 * F, np.uint8)
+                P._lib().orc_conv_encode_tb(bits, F, coded)
+                sym = np.clip(32767.5 + (1 - 2 * coded.astype(np.float64)) * 700 + rng.normal(0, 600, 3 * F), 0,
+                              65535).astype(np.uint16)
+            out = np.zeros(F, np.uint8)
+            R.ref_viterbi_decode_us(sym, F, out)
+            data[f"vit{k}_sym"] = sym
+            data[f"vit{k}_bits"] = out
+            k += 1
+    data["vit_n"] = np.int32(k)
+    k = 0
+    for nb in (8, 21, 27, 31, 43, 57, 61):
+        for L in range(4):
+            E = 72 << L
+            bits = rng.integers(0, 2, nb, dtype=np.uint8)
+            e = np.zeros(E, np.uint8)
+            R.ref_pdcch_dci_encode(bits.copy(), nb, 0x1234, E, e)
+            data[f"enc{k}_bits"] = bits
+            data[f"enc{k}_e"] = e
+            for snr in (0.4, 1.0, 2.5):
+                llr = ((1 - 2 * e.astype(np.float32)) * snr + rng.normal(0, 1, E)).astype(np.float32)
+                pay = np.zeros(nb + 16, np.uint8)
+                crc = R.ref_pdcch_dci_decode(llr, E, nb, pay)
+                data[f"dec{k}_{snr}_llr"] = llr
+                data[f"dec{k}_{snr}_out"] = pay
+                data[f"dec{k}_{snr}_crc"] = np.int32(crc)
+            k += 1
+    data["enc_n"] = np.int32(k)
+    k = 0
+    for (nprb, ports, nrx, cid, sf, cfi, snr) in [(6, 1, 1, 1, 0, 1, 30), (6, 2, 2, 4, 5, 3, 10),
+                                                  (25, 2, 2, 3, 3, 2, 20), (50, 1, 2, 7, 9, 3, 15),
+                                                  (100, 2, 2, 1, 1, 1, 25), (100, 4, 2, 5, 7, 3, 18),
+                                                  (15, 4, 1, 0, 2, 2, 12), (100, 1, 1, 77, 4, 2, 3)]:
+        rg = P.regs(nprb, ports, cid, 0)
+        glen = 14 * 12 * nprb
+        tx = np.zeros((ports, glen), np.complex64)
+        msgs = []
+        nb = P.dci_sizeof(P.FORMAT1A, nprb, ports)
+        if rg.nof_cce(cfi) >= 4:
+            b = rng.integers(0, 2, nb, dtype=np.uint8)
+            b[0] = 1
+            msgs.append(dict(bits=b, rnti=0xFFFF, L=2, ncce=0))
+        P.ctrl_tx(tx, rg, cid, ports, sf, cfi, msgs)
+        h = ((rng.normal(size=(ports, nrx, glen)) + 1j * rng.normal(size=(ports, nrx, glen))) / np.sqrt(2)).astype(
+            np.complex64)
+        y = np.einsum("prg,pg->rg", h, tx).astype(np.complex64)
+        sd = 10 ** (-snr / 20) / np.sqrt(2)
+        y += (sd * (rng.normal(size=y.shape) + 1j * rng.normal(size=y.shape))).astype(np.complex64)
+        noise = np.float32(2 * sd * sd)
+        corr = C.c_float()
+        cf = R.ref_pcfich_decode(y.view(np.float32).ravel(), h.view(np.float32).ravel(), nrx, nprb, ports, cid, sf,
+                                 noise, C.byref(corr))
+        llr = np.zeros(8 * int(rg.nregs[cf - 1]), np.float32)
+        R.ref_pdcch_llr(y.view(np.float32).ravel(), h.view(np.float32).ravel(), nrx, nprb, ports, cid, cf, sf, noise,
+                        llr)
+        ctrl = 4 * 12 * nprb  # only the first 4 OFDM symbols are stored (the control region)
+        data[f"sf{k}_cfg"] = np.array([nprb, ports, nrx, cid, sf, cfi], np.int32)
+        data[f"sf{k}_y"] = y[:, :ctrl].copy()
+        data[f"sf{k}_h"] = h[:, :, :ctrl].copy()
+        data[f"sf{k}_noise"] = noise
+        data[f"sf{k}_cfi"] = np.int32(cf)
+        data[f"sf{k}_corr"] = np.float32(corr.value)
+        data[f"sf{k}_llr"] = llr
+        data[f"sf{k}_msg"] = msgs[0]["bits"] if msgs else np.zeros(0, np.uint8)
+        k += 1
+    data["sf_n"] = np.int32(k)
+    np.savez_compressed(os.path.join(OUT, "pdcch.npz"), **data)
+    print("pdcch.npz:", len(cells), "REG maps,", len(locs), "search spaces,", data["vit_n"], "Viterbi,",
+          data["enc_n"], "DCI encode/decode,", k, "control regions")
+
+
 def main():
     oracle.build(ref=True)
     if not oracle.ref_available():
         sys.exit("oracle/_ref/libsrslte_ref.so is not available (needs /root/reference)")
+    if sys.argv[1:] == ["pdcch"]:
+        gen_pdcch(np.random.default_rng(4004))
+        return
     rng = np.random.default_rng(20201010)
     gen_tdec_auto(rng)
     gen_tdec_generic(rng)
@@ -231,6 +353,7 @@ def main():
     gen_crc_cbsegm(rng)
     gen_rm(np.random.default_rng(1212))
     gen_pdsch_stages(np.random.default_rng(3003))
+    gen_pdcch(np.random.default_rng(4004))
 
 
 if __name__ == "__main__":

@@ -43,6 +43,38 @@ def _oracle_chain(s):
     return ret, np.asarray(data, np.uint8), e[0], res
 
 
+def _oracle_ctrl(sf):
+    """PCFICH + PDCCH blind search for SI-RNTI on one subframe of the recording (cell: PHICH normal, Ng = 1 as
+    pdsch_pdcch_file_test.c:32-41 configures it)."""
+    from oracle import pdcch_chain as pd
+    iq = IQ[sf * SF_LEN:(sf + 1) * SF_LEN]
+    grid = uc.ofdm_rx_sf(iq, NPRB)[None, :]
+    ce, res = uc.chest_estimate(grid, NPRB, 1, CELL, sf)
+    rg = pd.regs(NPRB, 1, CELL, 2)
+    cfi, _corr, _ = pd.pcfich_decode(grid, ce, rg, CELL, sf, res["noise_estimate"])
+    llr = pd.pdcch_llr(grid, ce, rg, cfi, CELL, sf, res["noise_estimate"])
+    return cfi, pd.find_dl_dci(llr, rg.nof_cce(cfi), sf, RNTI, NPRB, 1)
+
+
+def test_oracle_control_channels_find_the_si_grants():
+    """The whole control chain on the recording, as pdsch_pdcch_file_test runs it (srslte_ue_dl_find_and_decode over
+    subframes 0..9): CFI 3 from the PCFICH in every subframe, and an SI-RNTI DCI (format 1A) exactly in subframes
+    2 and 5, whose grants are the ones the TB CRC selected independently (the fixture)."""
+    from oracle import pdcch_chain as pd
+    by_sf = {s["sf"]: s for s in FIX["subframes"]}
+    for sf in range(10):
+        cfi, found = _oracle_ctrl(sf)
+        assert cfi == CFI
+        if sf not in by_sf:
+            assert found == []
+            continue
+        s = by_sf[sf]
+        assert len(found) == 1 and found[0]["format"] == pd.FORMAT1A
+        g = pd.dci_to_grant(found[0]["dci"], NPRB, 1, 0)
+        assert int(g["prb"][0].argmax()) == s["prb_start"] and g["nof_prb"] == s["nof_prb"]
+        assert g["tbs"][0] == s["tbs"] and g["rv"][0] == s["rv"]
+
+
 def test_signal_fixture_shape():
     assert IQ.size == 10 * SF_LEN  # one radio frame of 1.92 Msps
     assert [s["sf"] for s in FIX["subframes"]] == [2, 5]
@@ -115,3 +147,56 @@ def test_product_decodes_real_signal(fused):
         nre = jobs[i].cfg.grant.nof_re
         e_g = ue.pdsch.stage(i, 0, nre, 2 * nre)[2]
         assert np.abs(e_g.astype(np.int32) - e_o.astype(np.int32)).max() <= 1
+
+
+@pytest.mark.gpu
+def test_product_find_and_decode_real_signal():
+    """srslte_ue_dl_find_and_decode on all ten subframes of the recording in one GPU batch: PCFICH CFI 3 everywhere,
+    the SI-RNTI DCIs found in subframes 2 and 5 only, their grants derived from the DCI, both SI payloads decoded
+    with the CRC passing -- the reference test pdsch_pdcch_file_test's known answer, end to end."""
+    from srsran_amd import lib
+    from srsran_amd import pdcch as D
+    from srsran_amd import pdsch as P
+    from srsran_amd.dlsch import SoftbufferPool
+    from srsran_amd.tdec import DeviceBuffer
+    from srsran_amd.ue_dl import DlSfJob, UeDl, default_chest_cfg
+
+    cell = P.make_cell(NPRB, 1, CELL, phich_resources=2)
+    ue = UeDl(cell, 1)
+    G = 14 * 12 * NPRB
+    n = 10
+    d_iq = DeviceBuffer(n * SF_LEN * 8)
+    d_grid, d_ce, d_pay = DeviceBuffer(n * G * 8), DeviceBuffer(n * G * 8), DeviceBuffer(n * 2 * 64)
+    jobs, cfgs = [], []
+    for sf in range(n):
+        iq = np.ascontiguousarray(IQ[sf * SF_LEN:(sf + 1) * SF_LEN])
+        lib().mi355_memcpy_h2d(d_iq.ptr + sf * SF_LEN * 8, iq.ctypes.data, iq.nbytes)
+        j = DlSfJob()
+        j.tti = sf
+        j.in_buffer[0] = d_iq.ptr + sf * SF_LEN * 8
+        j.sf_symbols[0] = d_grid.ptr + sf * G * 8
+        j.ce[0][0] = d_ce.ptr + sf * G * 8
+        jobs.append(j)
+        c = P.PdschCfg()
+        c.rnti, c.decoder_type = RNTI, P.MIMO_DECODER_MMSE
+        c.softbuffer[0], c.softbuffer[1] = 2 * sf, 2 * sf + 1
+        cfgs.append(c)
+    pool = SoftbufferPool(2 * n, max_cb=1)
+    pays = [d_pay.ptr + k * 64 for k in range(2 * n)]
+    sfs, chest, ctrl, dcis, res, got = D.find_and_decode(ue, pool, jobs, [D.UeDlCfg()] * n, cfgs, default_chest_cfg(),
+                                                        pays)
+    host = np.zeros(n * 2 * 64, np.uint8)
+    d_pay.download(host)
+    by_sf = {s["sf"]: s for s in FIX["subframes"]}
+    for sf in range(n):
+        assert sfs[sf].cfi == CFI and ctrl[sf].cfi == CFI
+        if sf not in by_sf:
+            assert ctrl[sf].nof_dci == 0
+            continue
+        s = by_sf[sf]
+        assert ctrl[sf].nof_dci == 1 and dcis[sf][0].format == D.FORMAT1A
+        g = got[sf].grant
+        assert g.nof_prb == s["nof_prb"] and g.tb[0].tbs == s["tbs"] and g.tb[0].rv == s["rv"]
+        assert res[2 * sf].crc and res[2 * sf].ret == 0
+        assert host[2 * sf * 64: 2 * sf * 64 + s["tbs"] // 8].tobytes().hex() == s["payload_hex"]
+    ue.close()
