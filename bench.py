@@ -16,6 +16,8 @@ phy_dl_test's crossed 2x2 channel [[1,1],[1,-1]] + AWGN (40 dB) -> IFFT + CP; D 
 
     python bench.py [--gpus N --steps K --warmup W]            # N > 1: launched by torch.distributed.run
     python bench.py --workload tdec                            # configs[1]: batched turbo decode only
+    python bench.py --workload ue_dl                           # + PCFICH / PDCCH blind search -> DCI -> grant
+                                                               #   (phy_dl_test.c:194-247 work_ue per subframe)
 
 Multi-GPU: weak scaling -- every rank decodes its own B subframes (independent subframes shard with no
 data-path collective); ranks only meet at the timing barriers and the max-over-ranks reduction.
@@ -50,7 +52,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["pdsch", "tdec"], default="pdsch")
+    ap.add_argument("--workload", choices=["pdsch", "ue_dl", "tdec"], default="pdsch",
+                    help="pdsch: known grants (decode_batch); ue_dl: phy_dl_test's work_ue with the PCFICH / PDCCH "
+                         "blind search deriving every grant (find_and_decode); tdec: configs[1]")
     ap.add_argument("--subframes", type=int, default=2048, help="TM4 subframes per GPU per step")
     ap.add_argument("--distinct", type=int, default=20, help="distinct synthetic subframes tiled over the batch")
     ap.add_argument("--snr", type=float, default=40.0)
@@ -182,8 +186,26 @@ def tm4_cfg(P, cell, sf_idx, rnti=0x1234, softbuffers=(0, 1)):
     return cfg
 
 
-def synth_tm4(cell, D, snr_db, seed):
-    """D distinct subframes as time-domain I/Q (D, 2 rx, 15*N) + payloads, via the product encoder."""
+def tm4_dci_msg(cell, sf_idx, rnti=0x1234):
+    """The TM4 grant of tm4_cfg as a DCI format 2 (type-0 allocation of every RBG, MCS 27 on both TBs with the
+    256QAM table, precoding information 0) at the UE's first aggregation-level-4 candidate (CFI 1)."""
+    from srsran_amd import pdcch as D
+    d = D.DciDl()
+    d.rnti, d.format, d.alloc_type = rnti, D.FORMAT2, D.ALLOC_TYPE0
+    d.type0_alloc.rbg_bitmask = (1 << 25) - 1  # 100 PRB: 25 RBGs of 4
+    for t in range(2):
+        d.tb[t].mcs_idx, d.tb[t].rv, d.tb[t].ndi = 27, 0, 1
+    d.tb[1].cw_idx = 1
+    m = D.pack(cell, d, sf_idx)
+    locs = D.ue_locations(D.nof_cce(cell, 1), sf_idx, rnti)
+    L, n = next(lv for lv in locs if lv[0] == 2)
+    m.location, m.rnti = D.DciLocation(L, n), rnti
+    return m
+
+
+def synth_tm4(cell, D, snr_db, seed, ctrl=False):
+    """D distinct subframes as time-domain I/Q (D, 2 rx, 15*N) + payloads, via the product encoder (with ctrl: the
+    PCFICH (CFI 1) and the subframe's DCI on the PDCCH too)."""
     from srsran_amd import enb_dl
     from srsran_amd import pdsch as P
     from srsran_amd.ue_dl import symbol_sz
@@ -202,6 +224,9 @@ def synth_tm4(cell, D, snr_db, seed):
         grids = np.zeros((2, 14 * nre), np.complex64)
         enb_dl.pdsch_encode(cell, P.DlSfCfg(sf, 1), cfg, pl, grids)
         enb_dl.put_refs(cell, sf, grids)
+        if ctrl:
+            from srsran_amd import pdcch as Dc
+            Dc.encode_ctrl_host(cell, sf, 1, [tm4_dci_msg(cell, sf)], grids)
         # phy_dl_test crossed channel: rx0 = p0 + p1, rx1 = p0 - p1, plus AWGN per RE
         y = np.stack([grids[0] + grids[1], grids[0] - grids[1]]).reshape(2, 14, nre)
         y = y + sigma * (rng.standard_normal(y.shape) + 1j * rng.standard_normal(y.shape))
@@ -222,14 +247,15 @@ def synth_tm4(cell, D, snr_db, seed):
 class Tm4Batch:
     """B subframes resident in HBM with their grids, channel estimates, softbuffers and payload buffers."""
 
-    def __init__(self, cell, B, D, snr, seed, device):
+    def __init__(self, cell, B, D, snr, seed, device, ctrl=False):
         from srsran_amd import lib
         from srsran_amd import pdsch as P
         from srsran_amd.dlsch import SoftbufferPool
         from srsran_amd.tdec import DeviceBuffer
         from srsran_amd.ue_dl import DlSfJob, UeDl, default_chest_cfg
         self.P, self.B, self.D = P, B, D
-        self.iq_host, self.payloads = synth_tm4(cell, D, snr, seed)
+        self.ctrl = ctrl
+        self.iq_host, self.payloads = synth_tm4(cell, D, snr, seed, ctrl)
         sf_len = self.iq_host.shape[2]
         G = 14 * 12 * cell.nof_prb
         self.G = G
@@ -273,12 +299,28 @@ class Tm4Batch:
         self.L.mi355_softbuffer_reset_range.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
         self.chest = (ChestRes * B)()
         self.res = (P.PdschRes * (2 * B))()
+        if ctrl:
+            from srsran_amd import pdcch as Dc
+            self.Lc = Dc._declare()
+            u = Dc.UeDlCfg()
+            u.tm, u.use_tbs_index_alt = Dc.TM4, 1
+            self.ue_cfgs = (Dc.UeDlCfg * B)(*([u] * B))
+            self.ctrl_res = (Dc.CtrlRes * B)()
+            self.dci = (Dc.DciDl * (B * Dc.MAX_DCI_MSG))()
 
     def step(self, stages=None):
         """One batch: new-TB softbuffer reset + mi355_ue_dl_decode_batch (OFDM, estimation, PDSCH, DL-SCH).
         With `stages`, the two-call form (decode_fft_estimate, then decode_pdsch) is timed per stage instead."""
         from srsran_amd import check, lib
         t0 = time.perf_counter()
+        if self.ctrl:
+            # find_and_decode resets each TB's softbuffer itself (ue_dl.c:1522-1529)
+            C.memset(self.res, 0, C.sizeof(self.res))
+            check(self.Lc.mi355_ue_dl_find_and_decode_batch(self.ue.h, self.pool.h, self.jobs, self.sfs, self.ue_cfgs,
+                                                            self.cfgs, C.byref(self.chest_cfg), self.chest, self.pays,
+                                                            self.B, self.ctrl_res, self.dci, self.res, None),
+                  "ue_dl_find_and_decode_batch")
+            return
         check(self.L.mi355_softbuffer_reset_range(self.pool.h, 0, 2 * self.B, None), "softbuffer_reset_range")
         C.memset(self.res, 0, C.sizeof(self.res))
         if stages is None:
@@ -297,7 +339,8 @@ class Tm4Batch:
         stages["pdsch_decode_ms"] = stages.get("pdsch_decode_ms", 0) + (t2 - t1) * 1e3
 
     def check_payloads(self):
-        """All TBs CRC-ok and every payload equal to what the encoder was given."""
+        """All TBs CRC-ok and every payload equal to what the encoder was given (and, with the control channels,
+        exactly one DCI found per subframe)."""
         host = np.zeros(self.B * 2 * self.plen, np.uint8)
         self.d_pay.download(host)
         host = host.reshape(self.B, 2, self.plen)
@@ -305,7 +348,8 @@ class Tm4Batch:
         for i in range(self.B):
             for t in range(2):
                 r = self.res[2 * i + t]
-                if r.crc and np.array_equal(host[i, t, : 97896 // 8], self.payloads[i % self.D][t]):
+                dci_ok = not self.ctrl or self.ctrl_res[i].nof_dci == 1
+                if dci_ok and r.crc and np.array_equal(host[i, t, : 97896 // 8], self.payloads[i % self.D][t]):
                     ok += 1
         its = float(np.mean([self.res[k].avg_iterations_block for k in range(2 * self.B)]))
         return ok, its
@@ -378,7 +422,8 @@ def run_pdsch(args, world, rank, local, pg):
     from srsran_amd.tdec import DeviceBuffer, TdecBatch
     cell = tm4_setup()
     B = args.subframes
-    b = Tm4Batch(cell, B, min(args.distinct, B), args.snr, seed=shard_seed(rank), device=local)
+    ctrl = args.workload == "ue_dl"
+    b = Tm4Batch(cell, B, min(args.distinct, B), args.snr, seed=shard_seed(rank), device=local, ctrl=ctrl)
     for _ in range(args.warmup):
         b.step()
     lib().mi355_device_sync()
@@ -399,7 +444,7 @@ def run_pdsch(args, world, rank, local, pg):
     roof, valu = None, None
     if args.no_roofline:
         kms = None
-    else:
+    elif not ctrl:
         b.step(stages)
     # dominant kernel: the MAP half-iteration over this batch's 32*B code blocks (the softbuffers hold the
     # rate-dematched LLRs of the last step), 8 half-iterations without early stop, HIP events on its stream
@@ -431,7 +476,9 @@ def run_pdsch(args, world, rank, local, pg):
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32+int16", "data": "synthetic",
         "config": {"workload": f"srslte_ue_dl chain from time-domain I/Q: {B} subframes/GPU/step, 20 MHz (100 PRB), "
                                "TM4 2x2 spatial multiplexing, 2 codewords QAM256 TBS 97896 (C=16, K=6144), "
-                               "MMSE+CSI, max 10 half-its with CRC early stop, 40 dB crossed 2x2 channel",
+                               "MMSE+CSI, max 10 half-its with CRC early stop, 40 dB crossed 2x2 channel" +
+                               ("; grants from the PCFICH/PDCCH blind search (DCI format 2 per subframe, "
+                                "find_and_decode = phy_dl_test work_ue)" if ctrl else ""),
                    "subframes_per_gpu": B, "code_blocks_per_gpu": 32 * B, "distinct_subframes": b.D,
                    "parallelism": f"dp{world}"},
         "code_blocks_per_s": round(world * 32 * B * args.steps / dt, 1),
@@ -547,7 +594,7 @@ def run_tdec(args, world, rank, local, pg):
 def main():
     args = parse()
     world, rank, local, pg = dist_setup()
-    res = run_pdsch(args, world, rank, local, pg) if args.workload == "pdsch" else run_tdec(args, world, rank, local, pg)
+    res = run_tdec(args, world, rank, local, pg) if args.workload == "tdec" else run_pdsch(args, world, rank, local, pg)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if pg is not None:

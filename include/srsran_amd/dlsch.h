@@ -36,6 +36,10 @@ int mi355_softbuffer_reset_cb(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t 
 int mi355_softbuffer_reset_all(mi355_softbuffer_pool_t* p, void* stream);
 /* srslte_softbuffer_rx_reset on softbuffers [first, first + n) with one launch */
 int mi355_softbuffer_reset_range(mi355_softbuffer_pool_t* p, uint32_t first, uint32_t n, void* stream);
+/* srslte_softbuffer_rx_reset_tbs (softbuffer.c:128-154) for n softbuffers in one launch: sbs[i] reset for a TB of
+ * tbs[i] bits (its code blocks' buffers logically zeroed, every CB CRC flag cleared) */
+int mi355_softbuffer_reset_tbs_batch(mi355_softbuffer_pool_t* p, const uint32_t* sbs, const uint32_t* tbs, uint32_t n,
+                                     void* stream);
 /* device address of the pool's int16 code-block buffers (slot = sb * max_cb + cb, `stride` int16 apart) */
 int mi355_softbuffer_pool_buffer(mi355_softbuffer_pool_t* p, int16_t** buf, uint32_t* stride, uint32_t* max_cb);
 

@@ -88,6 +88,9 @@ struct DlschResetArgs {
 };
 
 hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s);
+// srslte_softbuffer_rx_reset_tbs for a list of softbuffers: list[i] = {softbuffer, code blocks to reset}
+hipError_t dlsch_launch_reset_list(const uint2* list, uint32_t n, uint32_t max_cb, uint8_t* fresh, uint8_t* cb_crc,
+                                   hipStream_t s);
 hipError_t dlsch_launch_check(const DlschCheckArgs& a, hipStream_t s);
 hipError_t dlsch_launch_prologue(const DlschTbArgs& a, hipStream_t s);
 hipError_t dlsch_launch_epilogue(const DlschTbArgs& a, hipStream_t s);

@@ -367,6 +367,29 @@ __global__ __launch_bounds__(256) void dlsch_sb_reset(DlschResetArgs a)
   a.sb_crc[a.slot0 + g] = 0;
 }
 
+// one thread per (list entry, code block): lazy buffer reset for the TB's code blocks, every CB CRC flag cleared
+__global__ __launch_bounds__(256) void dlsch_sb_reset_list(const uint2* list, uint32_t n, uint32_t max_cb, uint8_t* fresh,
+                                                           uint8_t* cb_crc)
+{
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (size_t)n * max_cb) return;
+  const uint2    e  = list[g / max_cb];
+  const uint32_t cb = (uint32_t)(g % max_cb);
+  const size_t   k  = (size_t)e.x * max_cb + cb;
+  if (cb < e.y) fresh[k] = 1;
+  cb_crc[k] = 0;
+}
+
+hipError_t dlsch_launch_reset_list(const uint2* list, uint32_t n, uint32_t max_cb, uint8_t* fresh, uint8_t* cb_crc,
+                                   hipStream_t s)
+{
+  const size_t t = (size_t)n * max_cb;
+  if (!t) return hipSuccess;
+  hipLaunchKernelGGL(dlsch_sb_reset_list, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, s, list, n, max_cb, fresh,
+                     cb_crc);
+  return hipGetLastError();
+}
+
 hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s)
 {
   if (a.ncb <= 0) return hipSuccess;

@@ -44,6 +44,9 @@ struct mi355_softbuffer_pool {
   uint8_t* cb_crc = nullptr; // nof_sb * max_cb
   uint8_t* data   = nullptr; // nof_sb * max_cb * SB_DATA
   uint8_t* fresh  = nullptr; // nof_sb * max_cb: buffer logically zero (lazy reset)
+  uint2*   d_list = nullptr; // batched reset list {softbuffer, code blocks to reset}
+  uint32_t list_cap = 0;
+  mi355::HostStaging st_list;
 };
 
 namespace {
@@ -200,6 +203,7 @@ void mi355_softbuffer_pool_destroy(mi355_softbuffer_pool_t* p)
   (void)hipFree(p->cb_crc);
   (void)hipFree(p->data);
   (void)hipFree(p->fresh);
+  (void)hipFree(p->d_list);
   delete p;
 }
 
@@ -226,6 +230,32 @@ int mi355_softbuffer_reset(mi355_softbuffer_pool_t* p, uint32_t sb, void* stream
 int mi355_softbuffer_reset_tbs(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t tbs, void* stream)
 {
   return mi355_softbuffer_reset_cb(p, sb, (tbs + 24) / (6144 - 24) + 1, stream); // softbuffer.c:128-132
+}
+
+int mi355_softbuffer_reset_tbs_batch(mi355_softbuffer_pool_t* p, const uint32_t* sbs, const uint32_t* tbs, uint32_t n,
+                                     void* stream)
+{
+  if (!p || (n && (!sbs || !tbs))) return MI355_ERROR_INVALID_INPUTS;
+  if (!n) return MI355_SUCCESS;
+  CHECK_HIP(hipSetDevice(p->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (n > p->list_cap) {
+    if (p->d_list) {
+      CHECK_HIP(hipStreamSynchronize(s));
+      CHECK_HIP(hipFree(p->d_list));
+    }
+    p->list_cap = n + n / 2 + 64;
+    CHECK_HIP(hipMalloc(&p->d_list, p->list_cap * sizeof(uint2)));
+  }
+  CHECK_HIP(p->st_list.reserve(n * sizeof(uint2)));
+  auto* l = (uint2*)p->st_list.slot(n * sizeof(uint2));
+  for (uint32_t i = 0; i < n; i++) {
+    if (sbs[i] >= p->nof_sb) return MI355_ERROR_INVALID_INPUTS;
+    l[i] = make_uint2(sbs[i], std::min((tbs[i] + 24) / (6144 - 24) + 1, p->max_cb)); // softbuffer.c:128-132
+  }
+  CHECK_HIP(p->st_list.upload(p->d_list, s));
+  CHECK_HIP(dlsch_launch_reset_list(p->d_list, n, p->max_cb, p->fresh, p->cb_crc, s));
+  return MI355_SUCCESS;
 }
 
 int mi355_softbuffer_reset_all(mi355_softbuffer_pool_t* p, void* stream)

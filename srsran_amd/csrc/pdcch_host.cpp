@@ -205,6 +205,47 @@ void precode_diversity(const std::vector<float2>& d, uint32_t ports, std::vector
   }
 }
 
+// REs of one PRB in one slot of a normal FDD subframe (ra_re_x_prb, ra_dl.c:46-174): the control region, PBCH and
+// synchronisation signals in the six middle PRBs of subframes 0 / 5, and the cell-specific reference signals
+uint32_t re_x_prb(const mi355_cell_t& c, uint32_t sf_idx, uint32_t cfi, uint32_t slot, uint32_t prb)
+{
+  const bool     ext   = c.cp == MI355_CP_EXT;
+  const uint32_t nsym  = ext ? 6 : 7;
+  const uint32_t nctrl = cfi + (c.nof_prb < 10 ? 1 : 0); // SRSLTE_NOF_CTRL_SYMBOLS
+  uint32_t       re    = (slot == 0 ? nsym - nctrl : nsym) * NRE;
+  bool           refs  = true;
+  const uint32_t lo = c.nof_prb / 2 - 3, hi = c.nof_prb / 2 + 3 + (c.nof_prb % 2);
+  if ((sf_idx == 0 || sf_idx == 5) && prb >= lo && prb < hi) {
+    if (sf_idx == 0) {
+      if (slot == 0) {
+        re = (nsym - nctrl - 2) * NRE;
+      } else if (ext) {
+        re   = (nsym - 4) * NRE;
+        refs = false;
+      } else {
+        re = (nsym - 4) * NRE + 2 * c.nof_ports;
+      }
+    } else if (slot == 0) {
+      re = (nsym - nctrl - 2) * NRE;
+    }
+    if ((c.nof_prb % 2) && (prb == c.nof_prb / 2 - 3 || prb == c.nof_prb / 2 + 3)) {
+      if (slot == 0) {
+        re += 2 * NRE / 2;
+      } else if (sf_idx == 0) {
+        re += 4 * NRE / 2 - c.nof_ports;
+        if (ext) re -= c.nof_ports > 2 ? 2 : c.nof_ports;
+      }
+    }
+  }
+  if (refs) {
+    if (c.nof_ports <= 2)
+      re -= 2 * (slot + 1) * c.nof_ports;
+    else
+      re -= slot == 1 ? 12 : (nctrl == 1 ? 8 : 4);
+  }
+  return re;
+}
+
 } // namespace
 
 // ---------------------------------------------------------------------------------------- REG map
@@ -368,8 +409,8 @@ BlindJob blind_plan(const mi355_cell_t& cell, uint32_t sf_idx, uint16_t rnti, co
 }
 
 // dci_blind_search (ue_dl.c:450-550) per search space, as find_dl_dci_type_* call it (ue_dl.c:644-692)
-int blind_search_replay(const mi355_cell_t& cell, uint32_t nof_cce, uint32_t sf_idx, uint16_t rnti,
-                        const mi355_ue_dl_cfg_t& cfg, const DciCand* cand, mi355_dci_msg_t* msgs)
+int blind_search_replay(const mi355_cell_t& cell, uint32_t nof_cce, uint16_t rnti, const mi355_ue_dl_cfg_t& cfg,
+                        const BlindJob& j, const DciCand* cand, mi355_dci_msg_t* msgs)
 {
   if (!rnti) return 0;
   std::vector<mi355_dci_location_t> allocated;
@@ -426,10 +467,8 @@ int blind_search_replay(const mi355_cell_t& cell, uint32_t nof_cce, uint32_t sf_
   };
   if (common_search_only(rnti)) {
     const uint32_t f[2] = {MI355_DCI_FORMAT1A, MI355_DCI_FORMAT1C};
-    const BlindJob j    = blind_plan(cell, sf_idx, rnti, cfg);
     search(1, com, ncom, f, 2, j.nbits[1]);
   } else {
-    const BlindJob       j = blind_plan(cell, sf_idx, rnti, cfg);
     mi355_dci_location_t ue[MI355_MAX_CANDIDATES_UE];
     const uint32_t       nue  = ue_locations(nof_cce, j.Yk, ue);
     const uint32_t       f[2] = {MI355_DCI_FORMAT1A, cfg.tm < 8 ? kUeFormats[cfg.tm] : MI355_DCI_FORMAT1};
@@ -839,8 +878,20 @@ int mi355_ra_dl_dci_to_grant(const mi355_cell_t* cell, const mi355_dl_sf_cfg_t* 
   }
   // REs / bits (srslte_ra_dl_compute_nof_re, ra_dl.c:421-446)
   g->nof_symb_slot[0] = g->nof_symb_slot[1] = cell->cp == MI355_CP_EXT ? 6 : 7;
-  std::vector<uint32_t> idx(14 * 12 * nprb);
-  g->nof_re = mi355_pdsch_re_map(cell, g, sf->cfi, sf->tti % 10, idx.data());
+  g->nof_re = 0; // srslte_ra_dl_grant_nof_re (ra_dl.c:666-679)
+  // every PRB outside the middle seven carries the same count per slot: count those, evaluate the middle ones
+  const uint32_t sfi = sf->tti % 10, lo = nprb / 2 - 3, hi = nprb / 2 + 4;
+  for (uint32_t s = 0; s < 2; s++) {
+    uint32_t plain = 0;
+    for (uint32_t k = 0; k < nprb; k++) {
+      if (!g->prb_idx[s][k]) continue;
+      if (k >= lo && k < hi)
+        g->nof_re += re_x_prb(*cell, sfi, sf->cfi, s, k);
+      else
+        plain++;
+    }
+    if (plain) g->nof_re += plain * re_x_prb(*cell, sfi, sf->cfi, s, lo > 0 ? 0 : hi);
+  }
   static const uint32_t qm[5] = {1, 2, 4, 6, 8};
   for (int i = 0; i < 2; i++)
     if (en[i]) g->tb[i].nof_bits = g->nof_re * qm[g->tb[i].mod];

@@ -81,8 +81,8 @@ uint32_t ue_search_hash(uint16_t rnti, uint32_t sf_idx);
 
 // The reference's sequential blind search (ue_dl.c:450-730) over the decoded candidates of one subframe:
 // fills msgs (<= MI355_MAX_DCI_MSG) and returns their number.
-int blind_search_replay(const mi355_cell_t& cell, uint32_t nof_cce, uint32_t sf_idx, uint16_t rnti,
-                        const mi355_ue_dl_cfg_t& cfg, const DciCand* cand, mi355_dci_msg_t* msgs);
+int blind_search_replay(const mi355_cell_t& cell, uint32_t nof_cce, uint16_t rnti, const mi355_ue_dl_cfg_t& cfg,
+                        const BlindJob& plan, const DciCand* cand, mi355_dci_msg_t* msgs);
 // per-job search plan (spaces, payload sizes) for the device
 BlindJob blind_plan(const mi355_cell_t& cell, uint32_t sf_idx, uint16_t rnti, const mi355_ue_dl_cfg_t& cfg);
 

@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void pdcch_blind(BlindArgs a)
   const uint32_t     slot = (gw / PDCCH_FMTS) % PDCCH_SLOTS, fmt = gw % PDCCH_FMTS;
   WaveLds&           S    = lds[wv];
   DciCand*           out  = a.out + gw;
-  const BlindJob     bj   = a.jobs[job];
+  const BlindJob&    bj   = a.jobs[job]; // read in place (a private copy indexed by space / fmt would go to scratch)
   const uint32_t     space = slot < MI355_MAX_CANDIDATES_UE ? 0u : 1u;
   const uint32_t     cidx  = space ? slot - MI355_MAX_CANDIDATES_UE : slot;
   const uint32_t     nbits = bj.nbits[space][fmt];
@@ -246,20 +246,15 @@ __global__ __launch_bounds__(256) void pdcch_blind(BlindArgs a)
   bool     have = false;
   if (((bj.spaces >> space) & 1u) && nbits) {
     if (space == 0) {
-      const uint32_t per_level[4] = {6, 6, 2, 2};
-      uint32_t       lv[MI355_MAX_CANDIDATES_UE], nv[MI355_MAX_CANDIDATES_UE];
+      // pdcch.c:230-290 without the candidate list: within a level, candidate i repeats an earlier one exactly when
+      // i >= N / L (the modulo wraps), and candidates of different levels never coincide, so level l contributes
+      // min(6/6/2/2, N / L) candidates in order
       for (uint32_t l = 0; l < 4 && !have; l++) {
-        const uint32_t LL = 1u << l;
-        if (ntot < LL) continue;
-        for (uint32_t i = 0; i < per_level[l] && !have; i++) {
-          const uint32_t c  = LL * ((bj.Yk + i) % (ntot / LL));
-          bool           ok = k < MI355_MAX_CANDIDATES_UE && c + LL <= ntot;
-          for (uint32_t j = 0; j < k && ok; j++) ok = !(lv[j] == l && nv[j] == c);
-          if (ok) {
-            if (k == cidx) have = true, L = l, ncce = c;
-            lv[k] = l, nv[k] = c, k++;
-          }
+        const uint32_t LL = 1u << l, m = ntot / LL, cnt = min(l < 2 ? 6u : 2u, m);
+        if (cidx < k + cnt) {
+          have = true, L = l, ncce = LL * ((bj.Yk + (cidx - k)) % m);
         }
+        k += cnt;
       }
     } else {
       for (uint32_t l = 2; l <= 3 && !have; l++) {
@@ -369,13 +364,16 @@ __global__ __launch_bounds__(256) void pdcch_blind(BlindArgs a)
       if (fb) crc ^= 0x1021u;
     }
     for (uint32_t i = 0; i < 16; i++) p = (p << 1) | S.bits[nbits + i];
-    uint32_t w[4] = {0, 0, 0, 0};
-    for (uint32_t i = 0; i < nbits; i++) w[i >> 5] |= (uint32_t)S.bits[i] << (31 - (i & 31));
     out->status  = 2;
     out->crc_rem = p ^ crc;
     out->L       = L;
     out->ncce    = ncce;
-    for (int q = 0; q < 4; q++) out->bits[q] = w[q];
+    for (uint32_t q = 0; q < 4; q++) {
+      uint32_t w = 0;
+      for (uint32_t b = 0; b < 32; b++)
+        if (32 * q + b < nbits) w |= (uint32_t)S.bits[32 * q + b] << (31 - b);
+      out->bits[q] = w;
+    }
   }
 }
 

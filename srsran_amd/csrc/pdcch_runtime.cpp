@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 #include <vector>
@@ -82,6 +84,7 @@ int CtrlState::run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, con
     CHECK_HIP(hipMalloc(&d_buf, cap));
   }
   char* base = d_buf;
+  plan_of.resize(n);
   CHECK_HIP(st->reserve(b_jobs + b_blind));
   auto* cj = (CtrlJob*)st->slot((size_t)n * sizeof(CtrlJob));
   auto* bj = (BlindJob*)st->slot((size_t)n * sizeof(BlindJob));
@@ -99,7 +102,19 @@ int CtrlState::run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, con
     J.d_noise = d_noise ? d_noise + i : nullptr;
     J.noise   = host_noise ? host_noise[i] : 0.f;
     J.sf_idx  = sfjobs[i].tti % 10;
-    bj[i]     = blind_plan(cell, J.sf_idx, rntis[i], cfgs[i]);
+    // the plan depends on the RNTI, the subframe and the UE's DCI configuration only
+    const mi355_ue_dl_cfg_t& u   = cfgs[i];
+    const uint64_t           key = (uint64_t)rntis[i] | (uint64_t)J.sf_idx << 16 | (uint64_t)(u.tm & 15) << 20 |
+                         (uint64_t)(u.dci_common_ss != 0) << 24 | (uint64_t)(u.dci.multiple_csi_request_enabled != 0) << 25 |
+                         (uint64_t)(u.dci.cif_enabled != 0) << 26 | (uint64_t)(u.dci.srs_request_enabled != 0) << 27 |
+                         (uint64_t)(u.dci.is_not_ue_ss != 0) << 28;
+    auto it = plans.find(key);
+    if (it == plans.end()) {
+      if (plans.size() >= 65536) plans.clear(); // bounded: many RNTIs x 10 subframes
+      it = plans.emplace(key, blind_plan(cell, J.sf_idx, rntis[i], u)).first;
+    }
+    bj[i]      = it->second;
+    plan_of[i] = it->second;
   }
   CHECK_HIP(st->upload(base, s));
   float*    d_llr  = (float*)(base + b_jobs + b_blind);
@@ -135,6 +150,8 @@ int CtrlState::run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, con
   CHECK_HIP(back->reserve(nback));
   CHECK_HIP(hipMemcpyAsync(back->host, d_cfi, nback, hipMemcpyDeviceToHost, s));
   CHECK_HIP(hipStreamSynchronize(s));
+  static const bool prof = getenv("MI355_HOST_PROF") != nullptr;
+  const auto        tr0  = std::chrono::steady_clock::now();
   const uint32_t* h_cfi  = (const uint32_t*)back->host;
   const float*    h_corr = (const float*)(back->host + b_cfi);
   const DciCand*  h_cand = (const DciCand*)(back->host + b_cfi + b_corr);
@@ -143,9 +160,12 @@ int CtrlState::run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, con
     res[i].cfi         = cfi;
     res[i].cfi_corr    = std::max({0.f, h_corr[3 * i], h_corr[3 * i + 1], h_corr[3 * i + 2]});
     res[i].nof_cce     = regs.nregs[cfi - 1] / 9;
-    res[i].nof_dci     = blind_search_replay(cell, res[i].nof_cce, sfjobs[i].tti % 10, rntis[i], cfgs[i],
+    res[i].nof_dci     = blind_search_replay(cell, res[i].nof_cce, rntis[i], cfgs[i], plan_of[i],
                                          h_cand + (size_t)i * PDCCH_SLOTS * PDCCH_FMTS, msgs + (size_t)i * MI355_MAX_DCI_MSG);
   }
+  if (prof)
+    fprintf(stderr, "[mi355 host] control stage: blind-search replay %.1f us for %u subframes\n",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tr0).count(), n);
   return MI355_SUCCESS;
 }
 

@@ -2,6 +2,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <unordered_map>
+#include <vector>
+
 #include "pdcch_internal.h"
 
 namespace mi355 {
@@ -21,6 +24,8 @@ struct CtrlState {
   uint32_t     last_n = 0, last_stride = 0; // the previous call's arena layout (inspection accessors)
   float*       last_llr  = nullptr;
   DciCand*     last_cand = nullptr;
+  std::unordered_map<uint64_t, BlindJob> plans; // search plan per (rnti, subframe, UE configuration)
+  std::vector<BlindJob>                  plan_of; // this call's plan per subframe
 
   ~CtrlState();
   int init(const mi355_cell_t& c, uint32_t nof_rx);

@@ -563,6 +563,9 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
       (njobs && (!sfjobs || !sfs || !ue_cfgs || !cfgs || !payloads || !chest_cfg)))
     return MI355_ERROR_INVALID_INPUTS;
   std::lock_guard<std::mutex> lock(q->mu);
+  static const bool prof = getenv("MI355_HOST_PROF") != nullptr;
+  auto              now  = [] { return std::chrono::steady_clock::now(); };
+  const auto        t0   = now();
   CHECK_HIP(hipSetDevice(q->device));
   hipStream_t s = stream ? (hipStream_t)stream : q->own;
   int         r = ctrl_ready(q);
@@ -578,14 +581,18 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   std::vector<uint16_t>        rntis(njobs);
   std::vector<mi355_dci_msg_t> msgs((size_t)njobs * MI355_MAX_DCI_MSG);
   for (uint32_t i = 0; i < njobs; i++) rntis[i] = cfgs[i].rnti;
+  const auto t1 = now();
   r = q->ctrl->run(sfjobs, nullptr, d_noise, rntis.data(), ue_cfgs, njobs, s, ctrl, msgs.data());
-  chest_fill_cb(&fill);
-  if (r) return r;
+  const auto t2 = now();
+  if (r) {
+    chest_fill_cb(&fill);
+    return r;
+  }
   for (uint32_t i = 0; i < njobs; i++) sfs[i].cfi = ctrl[i].cfi;
   if ((r = unpack_all(q, sfs, ue_cfgs, njobs, ctrl, msgs, dci))) return r;
   // DCI -> grant, RV from the SFN for format 1C, softbuffer reset (ue_dl.c:1494-1535)
   std::vector<mi355_pdsch_job_t> jobs;
-  std::vector<uint32_t>          which;
+  std::vector<uint32_t>          which, rs_sb, rs_tbs;
   for (uint32_t i = 0; i < njobs; i++) {
     if (ctrl[i].nof_dci != 1) continue; // the reference decodes only when exactly one DCI was found
     const mi355_dci_dl_t& d = dci[(size_t)i * MI355_MAX_DCI_MSG];
@@ -600,13 +607,13 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
         const uint32_t k = ((sfs[i].tti / 10) / 2) % 4;
         t.rv             = ((uint32_t)ceilf(1.5f * k)) % 4;
       }
-      if ((r = mi355_softbuffer_reset_tbs(pool, cfgs[i].softbuffer[tb], (uint32_t)t.tbs, s))) return r;
+      rs_sb.push_back(cfgs[i].softbuffer[tb]);
+      rs_tbs.push_back((uint32_t)t.tbs);
     }
     mi355_pdsch_job_t j;
     memset(&j, 0, sizeof(j));
     j.sf             = sfs[i];
     j.cfg            = cfgs[i];
-    j.noise_estimate = chest[i].noise_estimate;
     for (uint32_t a = 0; a < q->nof_rx; a++) {
       j.sf_symbols[a] = sfjobs[i].sf_symbols[a];
       for (uint32_t p = 0; p < q->cell.nof_ports; p++) j.ce[p][a] = sfjobs[i].ce[p][a];
@@ -617,12 +624,31 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
     jobs.push_back(j);
     which.push_back(i);
   }
+  const auto t3 = now();
+  // every subframe decodes (the usual case): the equaliser reads the device noise estimates and srslte_chest_dl_res_t
+  // is filled on the host while the DL-SCH runs; otherwise the host values are needed first
+  const bool all = jobs.size() == njobs;
+  if (!all) {
+    chest_fill_cb(&fill);
+    for (size_t k = 0; k < jobs.size(); k++) jobs[k].noise_estimate = chest[which[k]].noise_estimate;
+  }
   if (jobs.empty()) return MI355_SUCCESS;
+  if ((r = mi355_softbuffer_reset_tbs_batch(pool, rs_sb.data(), rs_tbs.data(), (uint32_t)rs_sb.size(), s))) return r;
   std::vector<mi355_pdsch_res_t> sub(2 * jobs.size());
   for (size_t k = 0; k < jobs.size(); k++) sub[2 * k] = res[2 * which[k]], sub[2 * k + 1] = res[2 * which[k] + 1];
-  r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), (uint32_t)jobs.size(), sub.data(), s, nullptr,
-                                   WaitHook{}, true);
+  r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), (uint32_t)jobs.size(), sub.data(), s,
+                                   all ? d_noise : nullptr, all ? WaitHook{chest_fill_cb, &fill} : WaitHook{}, true);
+  if (all) {
+    CHECK_HIP(hipStreamSynchronize(q->side));
+    if (!fill.done) chest_fill_cb(&fill);
+  }
   for (size_t k = 0; k < jobs.size(); k++) res[2 * which[k]] = sub[2 * k], res[2 * which[k] + 1] = sub[2 * k + 1];
+  if (prof) {
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    fprintf(stderr, "[mi355 host] find_and_decode: launch ofdm/chest %.1f us, control stage (incl. sync + replay) "
+                    "%.1f us, fill/unpack/grants %.1f us, pdsch+dlsch %.1f us\n", us(t0, t1), us(t1, t2), us(t2, t3),
+            us(t3, now()));
+  }
   return r;
 }
 
