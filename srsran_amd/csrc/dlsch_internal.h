@@ -32,6 +32,8 @@ struct CrcTable {
   uint32_t poly;   // with the x^24 term
 };
 
+CrcTable make_crc_table(uint32_t poly); // host: byte table + x^(8*2^i) mod P (dlsch_runtime.cpp)
+
 constexpr uint16_t RM_NONE = 0xffff; // decoder-buffer position no circular-buffer bit maps to
 
 struct DlschRmArgs {

@@ -49,9 +49,7 @@ struct mi355_softbuffer_pool {
   mi355::HostStaging st_list;
 };
 
-namespace {
-
-CrcTable make_crc_table(uint32_t poly)
+CrcTable mi355::make_crc_table(uint32_t poly)
 {
   CrcTable t{};
   t.poly = poly;
@@ -77,8 +75,6 @@ CrcTable make_crc_table(uint32_t poly)
   }
   return t;
 }
-
-} // namespace
 
 struct mi355_dlsch {
   int                                    device = 0;

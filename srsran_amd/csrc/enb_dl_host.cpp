@@ -13,10 +13,39 @@
 
 #include "../../include/srsran_amd/enb_dl.h"
 #include "../../include/srsran_amd/tdec.h"
+#include "enb_dl_internal.h"
 #include "lte_common.h"
 #include "rm_tables.h"
 
 using namespace mi355;
+
+// circular-buffer bit selection: natural encoder index (3m+s, tails at 3K..3K+11) of each transmitted bit
+std::vector<uint16_t> mi355::rm_tx_table(uint32_t K, uint32_t rv)
+{
+  static const int NC = 32;
+  auto colperm = [](int c) { return ((c & 1) << 4) | ((c & 2) << 2) | (c & 4) | ((c & 8) >> 2) | ((c & 16) >> 4); };
+  const int D = (int)K + 4, R = (D + NC - 1) / NC, KP = R * NC, ND = KP - D, Ncb = 3 * KP;
+  const int k0 = R * (2 * (int)ceilf((float)Ncb / (float)(8 * R)) * (int)rv + 2);
+  std::vector<uint16_t> t(3 * (size_t)D);
+  int                   k = 0;
+  for (int j = 0; k < 3 * D; j++) {
+    const int p = (k0 + j) % Ncb;
+    int       s, y;
+    if (p < KP) {
+      s = 0;
+      y = colperm(p / R) + NC * (p % R);
+    } else if (((p - KP) & 1) == 0) {
+      s = 1;
+      y = colperm(((p - KP) / 2) / R) + NC * (((p - KP) / 2) % R);
+    } else {
+      const int q = (p - KP - 1) / 2;
+      s           = 2;
+      y           = (colperm(q / R) + NC * (q % R) + 1) % KP;
+    }
+    if (y >= ND) t[k++] = (uint16_t)(3 * (y - ND) + s);
+  }
+  return t;
+}
 
 namespace {
 
@@ -71,34 +100,6 @@ void turbo_encode(const uint8_t* c, uint32_t K, uint8_t* out)
       *t++             = (uint8_t)step(s, x);
     }
   }
-}
-
-// circular-buffer bit selection: natural encoder index (3m+s, tails at 3K..3K+11) of each transmitted bit
-std::vector<uint16_t> rm_tx_table(uint32_t K, uint32_t rv)
-{
-  static const int NC = 32;
-  auto colperm = [](int c) { return ((c & 1) << 4) | ((c & 2) << 2) | (c & 4) | ((c & 8) >> 2) | ((c & 16) >> 4); };
-  const int D = (int)K + 4, R = (D + NC - 1) / NC, KP = R * NC, ND = KP - D, Ncb = 3 * KP;
-  const int k0 = R * (2 * (int)ceilf((float)Ncb / (float)(8 * R)) * (int)rv + 2);
-  std::vector<uint16_t> t(3 * (size_t)D);
-  int                   k = 0;
-  for (int j = 0; k < 3 * D; j++) {
-    const int p = (k0 + j) % Ncb;
-    int       s, y;
-    if (p < KP) {
-      s = 0;
-      y = colperm(p / R) + NC * (p % R);
-    } else if (((p - KP) & 1) == 0) {
-      s = 1;
-      y = colperm(((p - KP) / 2) / R) + NC * (((p - KP) / 2) % R);
-    } else {
-      const int q = (p - KP - 1) / 2;
-      s           = 2;
-      y           = (colperm(q / R) + NC * (q % R) + 1) % KP;
-    }
-    if (y >= ND) t[k++] = (uint16_t)(3 * (y - ND) + s);
-  }
-  return t;
 }
 
 uint32_t mod_bits(uint32_t mod)

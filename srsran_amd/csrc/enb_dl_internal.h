@@ -1,0 +1,69 @@
+// srsran_amd/csrc/enb_dl_internal.h -- device descriptors of the eNodeB-side generator kernels
+// (enb_dl_kernels.hip) and the host helpers the GPU runtime shares with the host encoder (enb_dl_host.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "dlsch_internal.h"
+
+namespace mi355 {
+
+// circular-buffer bit selection of srslte_rm_turbo_tx_lut for (K, rv): encoder index (3m+s, tails at 3K..3K+11)
+// of the k-th transmitted bit, k < 3K+12 (enb_dl_host.cpp)
+std::vector<uint16_t> rm_tx_table(uint32_t K, uint32_t rv);
+
+struct EnbTbDev {        // one transport block: CRC24A of its payload (encode_tb_off, sch.c:282-287)
+  const uint8_t* data;   // tbs/8 payload bytes
+  uint8_t*       crc;    // 3 bytes out (MSB first)
+  uint32_t       nbytes; // tbs/8
+};
+
+struct EnbCbDev {         // one code block (encode_tb_off's loop body, sch.c:300-350)
+  const uint8_t*  data;   // TB payload
+  const uint8_t*  tbcrc;  // the TB's 3 CRC bytes (EnbTbDev.crc)
+  const uint16_t* txt;    // rm_tx_table(K, rv)
+  uint8_t*        e;      // codeword bits, one byte per bit
+  uint32_t        tb_bytes;
+  uint32_t        rp8;    // first byte of the block's data in payload || TB CRC
+  uint32_t        rlen;   // data bits (K - 24 when C > 1, else K)
+  uint32_t        K, cbcrc; // cbcrc: attach CRC24B (C > 1)
+  uint32_t        f1, f2;   // QPP interleaver (tc_interl_lte.c:39-67)
+  uint32_t        E, wp, nbits; // transmitted bits, first bit in the codeword, codeword length (guard)
+};
+
+struct EnbMapDev {        // one PDSCH job: codeword bits -> symbols -> layers -> ports -> grid
+  const uint16_t* map;    // RE -> grid index (srslte_pdsch_put order)
+  const uint8_t*  e[2];   // codeword bits (by cw_idx)
+  const uint32_t* scr[2]; // packed scrambling sequence of the codeword's c_init
+  float2*         grid[4];
+  uint32_t        nre, units; // units: REs (port 0 / spatial multiplexing / CDD) or RE pairs (SFBC)
+  uint32_t        qm[2];
+  uint32_t        scheme, nports, nlayers, cb;
+  float           r2, n16, n64, n256; // 1/sqrt(2), 1/sqrt(10), 1/sqrt(42), 1/sqrt(170) as the host encoder rounds them
+};
+
+struct EnbChanJob {
+  const float2* tx[4];
+  float2*       rx[2];
+};
+
+struct EnbChanMat {
+  float2 h[2][4]; // [rx][port]
+};
+
+struct EnbCrsJob {
+  float2*  grid[4];
+  uint32_t sf;
+};
+
+hipError_t enb_launch_tb_crc(const EnbTbDev* tb, uint32_t ntb, const CrcTable* crc24a, hipStream_t s);
+hipError_t enb_launch_cb_encode(const EnbCbDev* cb, uint32_t ncb, const CrcTable* crc24b, hipStream_t s);
+hipError_t enb_launch_map(const EnbMapDev* jobs, uint32_t njobs, uint32_t max_units, hipStream_t s);
+hipError_t enb_launch_crs(const EnbCrsJob* jobs, uint32_t njobs, const float2* pilots, uint32_t nof_prb,
+                          uint32_t nof_ports, uint32_t cell_id, uint32_t nsymb, hipStream_t s);
+hipError_t enb_launch_channel(const EnbChanJob* jobs, uint32_t njobs, uint32_t nof_re, uint32_t nports, uint32_t nrx,
+                              const EnbChanMat& H, float sigma, uint64_t seed, hipStream_t s);
+
+} // namespace mi355

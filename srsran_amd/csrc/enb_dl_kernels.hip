@@ -1,0 +1,356 @@
+// srsran_amd/csrc/enb_dl_kernels.hip -- eNodeB-side PDSCH generator kernels: the transmit
+// chain of srslte_pdsch_encode (pdsch.c:1133-1225) / srslte_dlsch_encode2 (sch.c:250-355) for a batch of
+// subframes, plus the CRS and a test channel.  Bit / symbol semantics are the host encoder's
+// (enb_dl_host.cpp), which the parity tests pin against the oracle transmitter.
+//
+//   enb_tb_crc     WG per TB: CRC24A of the payload (byte table in LDS, chunked CRC combine).
+//   enb_cb_encode  WG per code block: block bytes (payload || TB CRC) -> CRC24B -> bits in LDS -> QPP
+//                  interleave -> both 8-state RSCs as a wave each -> rate matching into codeword bits.
+//   enb_map        thread per RE (RE pair for SFBC): scrambling + 36.211 7.1 modulation + layer mapping +
+//                  precoding + RE mapping.
+//   enb_crs        thread per pilot: srslte_refsignal_cs_put_sf.
+//   enb_channel    thread per RE: channel matrix + AWGN (test channel).
+//
+// The recursive systematic convolutional encoder (36.212 5.1.3.2.1; turbocoder.c:76-186) is a linear recursion
+// over GF(2)^3, s' = A s + b u, so a wave encodes a K-bit block in parallel: lane l runs its chunk of
+// Lc = ceil(K/64) steps from the zero state (end state e_l), a Hillis-Steele scan with the constant multiplier
+// A^Lc (squared per level) turns the e_l into every chunk's true start state, and each lane re-runs its chunk
+// from there, emitting the parity bits.  The lane holding the last step appends the trellis termination.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc_device.h"
+#include "enb_dl_internal.h"
+
+namespace mi355 {
+
+namespace {
+
+// ---------------------------------------------------------------------------- RSC encoder (g0 = 13, g1 = 15)
+// state bits r0 r1 r2 (bit 0..2); feedback 1 + D^2 + D^3, parity 1 + D + D^3
+__device__ __forceinline__ uint32_t rsc_step(uint32_t& s, uint32_t in)
+{
+  const uint32_t r0 = s & 1u, r1 = (s >> 1) & 1u, r2 = (s >> 2) & 1u;
+  const uint32_t fb = in ^ r1 ^ r2;
+  const uint32_t z  = fb ^ r0 ^ r2;
+  s                 = fb | (r0 << 1) | (r1 << 2);
+  return z;
+}
+
+// 3x3 GF(2) matrices as three 3-bit columns (column i at bits 3i..3i+2)
+__device__ __forceinline__ uint32_t gf2_mv(uint32_t M, uint32_t x)
+{
+  return ((x & 1u) ? (M & 7u) : 0u) ^ ((x & 2u) ? ((M >> 3) & 7u) : 0u) ^ ((x & 4u) ? ((M >> 6) & 7u) : 0u);
+}
+__device__ __forceinline__ uint32_t gf2_mm(uint32_t P, uint32_t Q)
+{
+  return gf2_mv(P, Q & 7u) | (gf2_mv(P, (Q >> 3) & 7u) << 3) | (gf2_mv(P, (Q >> 6) & 7u) << 6);
+}
+// zero-input transition A: r0' = r1 ^ r2, r1' = r0, r2' = r1
+constexpr uint32_t RSC_A = 2u | (5u << 3) | (1u << 6);
+constexpr uint32_t GF2_I = 1u | (2u << 3) | (4u << 6);
+
+__device__ __forceinline__ uint32_t gf2_pow(uint32_t M, uint32_t n)
+{
+  uint32_t R = GF2_I;
+  while (n) {
+    if (n & 1u) R = gf2_mm(R, M);
+    M = gf2_mm(M, M);
+    n >>= 1;
+  }
+  return R;
+}
+
+// ---------------------------------------------------------------------------- modulation (36.211 7.1)
+// the host encoder's formulas operation by operation (this file is built with -ffp-contract=off)
+__device__ __forceinline__ float2 modulate(const uint32_t* b, uint32_t qm, const EnbMapDev& J)
+{
+  auto s = [&](int k) { return 1.0f - 2.0f * (float)b[k]; };
+  switch (qm) {
+    case 1: return make_float2(s(0) * J.r2, s(0) * J.r2);
+    case 2: return make_float2(s(0) * J.r2, s(1) * J.r2);
+    case 4: return make_float2(s(0) * (2 - s(2)) * J.n16, s(1) * (2 - s(3)) * J.n16);
+    case 6: return make_float2(s(0) * (4 - s(2) * (2 - s(4))) * J.n64, s(1) * (4 - s(3) * (2 - s(5))) * J.n64);
+    default:
+      return make_float2(s(0) * (8 - s(2) * (4 - s(4) * (2 - s(6)))) * J.n256,
+                         s(1) * (8 - s(3) * (4 - s(5) * (2 - s(7)))) * J.n256);
+  }
+}
+
+// scrambled bits of symbol m of codeword cw, then the symbol
+__device__ __forceinline__ float2 cw_symbol(const EnbMapDev& J, uint32_t cw, uint32_t m)
+{
+  const uint32_t  qm = J.qm[cw];
+  const uint8_t*  e  = J.e[cw];
+  const uint32_t* c  = J.scr[cw];
+  uint32_t        b[8];
+  const uint32_t  j0 = m * qm;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; k++) {
+    if (k < qm) {
+      const uint32_t j = j0 + k;
+      b[k]             = (uint32_t)e[j] ^ ((c[j >> 5] >> (j & 31u)) & 1u);
+    }
+  }
+  return modulate(b, qm, J);
+}
+
+__device__ __forceinline__ uint32_t crs_nsymbol_d(uint32_t l, uint32_t nsymb, uint32_t port)
+{
+  if (port < 2) return (l % 2) ? (l / 2 + 1) * nsymb - 3 : (l / 2) * nsymb;
+  return 1 + l * nsymb;
+}
+
+__device__ __forceinline__ uint32_t crs_fidx_d(uint32_t id, uint32_t l, uint32_t port)
+{
+  uint32_t v;
+  switch (port) {
+    case 0: v = (l % 2) ? 3 : 0; break;
+    case 1: v = (l % 2) ? 0 : 3; break;
+    case 2: v = l == 0 ? 0 : 3; break;
+    default: v = l == 0 ? 3 : 0; break;
+  }
+  return (v + id % 6) % 6;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z)
+{
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+} // namespace
+
+// ---------------------------------------------------------------------------- TB CRC24A
+__global__ __launch_bounds__(256) void enb_tb_crc(const EnbTbDev* __restrict__ tbs, const CrcTable* __restrict__ T)
+{
+  __shared__ uint32_t tl[256];
+  tl[threadIdx.x]    = T->t[threadIdx.x];
+  const EnbTbDev tb  = tbs[blockIdx.x];
+  __syncthreads();
+  const uint32_t crc = block_crc24(tb.data, tb.nbytes, tl, *T);
+  if (threadIdx.x < 3) tb.crc[threadIdx.x] = (uint8_t)(crc >> (16 - 8 * threadIdx.x));
+}
+
+// ---------------------------------------------------------------------------- code-block encoder
+constexpr uint32_t ENB_KMAX = 6144;
+
+__global__ __launch_bounds__(256) void enb_cb_encode(const EnbCbDev* __restrict__ cbs, const CrcTable* __restrict__ T)
+{
+  __shared__ uint8_t  cbb[ENB_KMAX / 8 + 4];
+  __shared__ uint8_t  ci[ENB_KMAX];            // QPP-interleaved block bits
+  __shared__ uint8_t  d[3 * ENB_KMAX + 12 + 4]; // encoder output, x z z' per step then the tails
+  __shared__ uint32_t tl[256];
+  const EnbCbDev J   = cbs[blockIdx.x];
+  const uint32_t tid = threadIdx.x, K = J.K;
+  tl[tid]            = T->t[tid];
+  // block bytes: rlen is a multiple of 8 and every block starts on a byte of payload || TB CRC
+  for (uint32_t i = tid; i < J.rlen / 8; i += 256) {
+    const uint32_t b = J.rp8 + i;
+    cbb[i]           = b < J.tb_bytes ? J.data[b] : J.tbcrc[b - J.tb_bytes];
+  }
+  __syncthreads();
+  if (J.cbcrc) { // CRC24B over the block's data (sch.c:316-323)
+    const uint32_t crc = block_crc24(cbb, J.rlen / 8, tl, *T);
+    if (tid < 3) cbb[J.rlen / 8 + tid] = (uint8_t)(crc >> (16 - 8 * tid));
+    __syncthreads();
+  }
+  for (uint32_t i = tid; i < K; i += 256) d[3 * i] = (cbb[i >> 3] >> (7 - (i & 7u))) & 1u;
+  __syncthreads();
+  for (uint32_t i = tid; i < K; i += 256) {
+    const uint32_t pi = (uint32_t)(((uint64_t)i * ((uint64_t)J.f1 + (uint64_t)J.f2 * i)) % K);
+    ci[i]             = d[3 * pi];
+  }
+  __syncthreads();
+  const uint32_t w = tid >> 6, lane = tid & 63u;
+  if (w < 2) { // wave 0: constituent encoder 1 (natural order), wave 1: encoder 2 (interleaved)
+    const uint32_t Lc = (K + 63) / 64;
+    const uint32_t i0 = min(K, lane * Lc), i1 = min(K, i0 + Lc);
+    auto           in = [&](uint32_t i) -> uint32_t { return w == 0 ? d[3 * i] : ci[i]; };
+    uint32_t       s  = 0;
+    for (uint32_t i = i0; i < i1; i++) rsc_step(s, in(i));
+    uint32_t x = s, M = gf2_pow(RSC_A, Lc);
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x ^= gf2_mv(M, y);
+      M = gf2_mm(M, M);
+    }
+    uint32_t st = __shfl_up(x, 1, 64);
+    if (lane == 0) st = 0;
+    for (uint32_t i = i0; i < i1; i++) d[3 * i + 1 + w] = (uint8_t)rsc_step(st, in(i));
+    if (i0 < K && i1 == K) { // trellis termination, tails in encoder order x z x z x z (per encoder)
+      uint8_t* t = d + 3 * K + 6 * w;
+      for (int j = 0; j < 3; j++) {
+        const uint32_t xb = ((st >> 1) ^ (st >> 2)) & 1u;
+        t[2 * j]          = (uint8_t)xb;
+        t[2 * j + 1]      = (uint8_t)rsc_step(st, xb);
+      }
+    }
+  }
+  __syncthreads();
+  // rate matching: bit k of the block = circular-buffer bit (k0 + k) mod N without dummies
+  const uint32_t N = 3 * K + 12;
+  for (uint32_t k = tid; k < J.E; k += 256) {
+    const uint32_t j = J.wp + k;
+    if (j < J.nbits) J.e[j] = d[J.txt[k % N]];
+  }
+}
+
+// ---------------------------------------------------------------------------- symbols -> grid
+__global__ __launch_bounds__(256) void enb_map(const EnbMapDev* __restrict__ jobs)
+{
+  const EnbMapDev& J = jobs[blockIdx.y];
+  const uint32_t   u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= J.units) return;
+  const uint16_t* map = J.map;
+  const float     r2  = J.r2;
+  switch (J.scheme) {
+    case 0: { // port 0
+      const float2 x            = cw_symbol(J, 0, u);
+      J.grid[0][map[u]]         = x;
+      break;
+    }
+    case 1: { // srslte_layermap_diversity + srslte_precoding_diversity, 2 ports (Alamouti over RE pairs)
+      const float2 x0 = cw_symbol(J, 0, 2 * u), x1 = cw_symbol(J, 0, 2 * u + 1);
+      const uint32_t g0 = map[2 * u], g1 = map[2 * u + 1];
+      J.grid[0][g0] = make_float2(x0.x * r2, x0.y * r2);
+      J.grid[1][g0] = make_float2(-x1.x * r2, x1.y * r2);
+      J.grid[0][g1] = make_float2(x1.x * r2, x1.y * r2);
+      J.grid[1][g1] = make_float2(x0.x * r2, -x0.y * r2);
+      break;
+    }
+    default: { // spatial multiplexing (codebooks) / large-delay CDD, 2 ports
+      const uint32_t g = map[u];
+      float2         y0, y1;
+      if (J.nlayers == 1) {
+        const float2 x = cw_symbol(J, 0, u);
+        y0             = make_float2(x.x * r2, x.y * r2);
+        switch (J.cb) {
+          case 0: y1 = make_float2(x.x * r2, x.y * r2); break;
+          case 1: y1 = make_float2(-x.x * r2, -x.y * r2); break;
+          case 2: y1 = make_float2(-x.y * r2, x.x * r2); break;
+          default: y1 = make_float2(x.y * r2, -x.x * r2); break;
+        }
+      } else {
+        const float2 x0 = cw_symbol(J, 0, u), x1 = cw_symbol(J, 1, u);
+        const float2 sm = make_float2((x0.x + x1.x) * 0.5f, (x0.y + x1.y) * 0.5f);
+        const float2 df = make_float2((x0.x - x1.x) * 0.5f, (x0.y - x1.y) * 0.5f);
+        if (J.scheme == 3) { // CDD
+          y0 = sm;
+          y1 = (u & 1u) ? make_float2(-df.x, -df.y) : df;
+        } else if (J.cb == 0) {
+          y0 = make_float2(x0.x * r2, x0.y * r2);
+          y1 = make_float2(x1.x * r2, x1.y * r2);
+        } else if (J.cb == 1) {
+          y0 = sm;
+          y1 = df;
+        } else {
+          y0 = sm;
+          y1 = make_float2(-df.y, df.x);
+        }
+      }
+      J.grid[0][g] = y0;
+      J.grid[1][g] = y1;
+      break;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- CRS
+__global__ __launch_bounds__(256) void enb_crs(const EnbCrsJob* __restrict__ jobs, const float2* __restrict__ pilots,
+                                               uint32_t nof_prb, uint32_t cell_id, uint32_t nsymb)
+{
+  const EnbCrsJob& J    = jobs[blockIdx.z];
+  const uint32_t   p    = blockIdx.y;
+  const uint32_t   nref = 2 * nof_prb, nre = 12 * nof_prb, nsym = p < 2 ? 4 : 2;
+  const uint32_t   t    = blockIdx.x * 256 + threadIdx.x;
+  if (t >= nsym * nref) return;
+  const uint32_t l = t / nref, i = t % nref;
+  const uint32_t s = crs_nsymbol_d(l, nsymb, p), f = crs_fidx_d(cell_id, l, p);
+  J.grid[p][s * nre + f + 6 * i] = pilots[((p / 2) * 10 + J.sf) * 4 * nref + l * nref + i];
+}
+
+// ---------------------------------------------------------------------------- test channel
+__global__ __launch_bounds__(256) void enb_channel(const EnbChanJob* __restrict__ jobs, uint32_t nof_re, uint32_t nports,
+                                                   uint32_t nrx, EnbChanMat H, float sigma, uint64_t seed)
+{
+  const EnbChanJob& J = jobs[blockIdx.y];
+  const uint32_t    k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= nof_re) return;
+  float2 x[4];
+  for (uint32_t p = 0; p < nports; p++) x[p] = J.tx[p][k];
+  for (uint32_t r = 0; r < nrx; r++) {
+    float2 y = make_float2(0.f, 0.f);
+    for (uint32_t p = 0; p < nports; p++) {
+      const float2 h = H.h[r][p];
+      y.x += h.x * x[p].x - h.y * x[p].y;
+      y.y += h.x * x[p].y + h.y * x[p].x;
+    }
+    if (sigma > 0.f) {
+      const uint64_t z  = splitmix64(seed ^ splitmix64(((uint64_t)blockIdx.y << 32) | ((uint64_t)r << 28) | k));
+      const float    u1 = ((float)(uint32_t)(z >> 40) + 1.0f) * (1.0f / 16777216.0f); // (0, 1]
+      const float    u2 = (float)(uint32_t)((z >> 16) & 0xffffffu) * (1.0f / 16777216.0f);
+      const float    rad = sqrtf(-2.0f * logf(u1));
+      float          sn, cs;
+      sincosf(6.283185307179586f * u2, &sn, &cs);
+      y.x += sigma * rad * cs;
+      y.y += sigma * rad * sn;
+    }
+    J.rx[r][k] = y;
+  }
+}
+
+// ---------------------------------------------------------------------------- launchers
+hipError_t enb_launch_tb_crc(const EnbTbDev* tb, uint32_t ntb, const CrcTable* crc24a, hipStream_t s)
+{
+  if (!ntb) return hipSuccess;
+  hipLaunchKernelGGL(enb_tb_crc, dim3(ntb), dim3(256), 0, s, tb, crc24a);
+  return hipGetLastError();
+}
+
+hipError_t enb_launch_cb_encode(const EnbCbDev* cb, uint32_t ncb, const CrcTable* crc24b, hipStream_t s)
+{
+  if (!ncb) return hipSuccess;
+  hipLaunchKernelGGL(enb_cb_encode, dim3(ncb), dim3(256), 0, s, cb, crc24b);
+  return hipGetLastError();
+}
+
+hipError_t enb_launch_map(const EnbMapDev* jobs, uint32_t njobs, uint32_t max_units, hipStream_t s)
+{
+  if (!njobs || !max_units) return hipSuccess;
+  for (uint32_t j0 = 0; j0 < njobs; j0 += 65535) { // grid.y limit
+    const uint32_t n = njobs - j0 < 65535 ? njobs - j0 : 65535;
+    hipLaunchKernelGGL(enb_map, dim3((max_units + 255) / 256, n), dim3(256), 0, s, jobs + j0);
+  }
+  return hipGetLastError();
+}
+
+hipError_t enb_launch_crs(const EnbCrsJob* jobs, uint32_t njobs, const float2* pilots, uint32_t nof_prb,
+                          uint32_t nof_ports, uint32_t cell_id, uint32_t nsymb, hipStream_t s)
+{
+  if (!njobs) return hipSuccess;
+  for (uint32_t j0 = 0; j0 < njobs; j0 += 65535) {
+    const uint32_t n = njobs - j0 < 65535 ? njobs - j0 : 65535;
+    hipLaunchKernelGGL(enb_crs, dim3((4 * 2 * nof_prb + 255) / 256, nof_ports, n), dim3(256), 0, s, jobs + j0,
+                       pilots, nof_prb, cell_id, nsymb);
+  }
+  return hipGetLastError();
+}
+
+hipError_t enb_launch_channel(const EnbChanJob* jobs, uint32_t njobs, uint32_t nof_re, uint32_t nports, uint32_t nrx,
+                              const EnbChanMat& H, float sigma, uint64_t seed, hipStream_t s)
+{
+  if (!njobs) return hipSuccess;
+  for (uint32_t j0 = 0; j0 < njobs; j0 += 65535) {
+    const uint32_t n = njobs - j0 < 65535 ? njobs - j0 : 65535;
+    // the job index in the noise key is global (j0 + blockIdx.y): fold j0 into the seed's key space
+    hipLaunchKernelGGL(enb_channel, dim3((nof_re + 255) / 256, n), dim3(256), 0, s, jobs + j0, nof_re, nports, nrx, H,
+                       sigma, seed + (uint64_t)j0 * 0x100000001ull);
+  }
+  return hipGetLastError();
+}
+
+} // namespace mi355

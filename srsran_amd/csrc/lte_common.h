@@ -24,6 +24,31 @@ inline void gold_sequence(uint32_t c_init, uint32_t len, std::vector<uint8_t>& c
   }
 }
 
+// Gold sequence table (36.211 7.2, Nc = 1600) in bit planes: x2(k + Nc) is a GF(2) linear form of the 31
+// bits of c_init (x1 does not depend on c_init), so for the 32 positions of word w, t[w][i] (i < 31) holds
+// bit j = coefficient of c_init bit i in x2(32w + j + Nc) and t[w][31] the x1 bits; the packed sequence word
+// is t[w][31] ^ XOR of t[w][i] over the set bits i of c_init.
+inline std::vector<uint32_t> gold_table(uint32_t len)
+{
+  const size_t          W = (len + 31) / 32;
+  std::vector<uint32_t> t(W * 32, 0u); // plane-major: t[i * W + w]
+  uint32_t              x1 = 1, m[31];
+  for (int i = 0; i < 31; i++) m[i] = 1u << i;
+  for (uint32_t n = 0; n < 1600 + len; n++) {
+    if (n >= 1600) {
+      const uint32_t k = n - 1600, w = k / 32, j = k % 32;
+      for (int i = 0; i < 31; i++) t[(size_t)i * W + w] |= ((m[0] >> i) & 1u) << j;
+      t[31 * W + w] |= (x1 & 1u) << j;
+    }
+    const uint32_t f1 = ((x1 >> 3) ^ x1) & 1u;
+    const uint32_t f2 = m[3] ^ m[2] ^ m[1] ^ m[0];
+    x1                = (x1 >> 1) | (f1 << 30);
+    for (int i = 0; i < 30; i++) m[i] = m[i + 1];
+    m[30] = f2;
+  }
+  return t;
+}
+
 inline uint32_t crs_nsymbol(uint32_t l, uint32_t nsymb, uint32_t port)
 {
   if (port < 2) return (l % 2) ? (l / 2 + 1) * nsymb - 3 : (l / 2) * nsymb;

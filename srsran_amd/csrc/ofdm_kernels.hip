@@ -225,6 +225,59 @@ __global__ __launch_bounds__(256) void ofdm_rx_n(OfdmArgs a)
   }
 }
 
+// ---------------------------------------------------------------------------- modulator
+// srslte_ofdm_tx_sf / ofdm_tx_slot (ofdm.c:492-541, 567-581): per OFDM symbol, subcarriers k >= nre/2 go to bin
+// 1 + k - nre/2 and k < nre/2 to bin N - nre/2 + k (DC and guards zero), backward DFT without 1/N (FFTW's
+// BACKWARD plan with normalize = false, enb_dl.c:57), cyclic prefix copied from the symbol's tail, then
+// srslte_enb_dl_gen_signal's scale (enb_dl.c:427-444).  The backward DFT is the forward one conjugated on
+// both sides: x = conj(DFT(conj(X))).  One workgroup per (grid, OFDM symbol), runtime radix plan.
+__global__ __launch_bounds__(256) void ofdm_tx(OfdmArgs a, float scale)
+{
+  __shared__ float2 buf[2][OFDM_MAX_N];
+  const OfdmJob  J    = a.jobs[blockIdx.y];
+  const uint32_t sym  = blockIdx.x;
+  const uint32_t slot = sym / a.nsymb, l = sym % a.nsymb;
+  const uint32_t N = a.N, half = a.nre / 2;
+  for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) buf[0][i] = make_float2(0.f, 0.f);
+  __syncthreads();
+  const float2* in = J.in + (size_t)sym * a.nre;
+  for (uint32_t k = threadIdx.x; k < a.nre; k += blockDim.x) {
+    const float2 v                                  = in[k];
+    buf[0][k < half ? N - half + k : 1 + k - half] = make_float2(v.x, -v.y);
+  }
+  __syncthreads();
+  uint32_t src = 0, Ns = 1;
+  for (uint32_t st = 0; st < a.nstages; st++) {
+    const uint32_t R = a.radix[st];
+    switch (R) {
+      case 2: stage<2>(buf[src], buf[src ^ 1], a.tw, N, Ns); break;
+      case 3: stage<3>(buf[src], buf[src ^ 1], a.tw, N, Ns); break;
+      case 4: stage<4>(buf[src], buf[src ^ 1], a.tw, N, Ns); break;
+      default: stage<8>(buf[src], buf[src ^ 1], a.tw, N, Ns); break;
+    }
+    __syncthreads();
+    src ^= 1;
+    Ns *= R;
+  }
+  const uint32_t cp  = l == 0 ? a.cp0 : a.cp1;
+  float2*        out = J.out + (size_t)slot * a.slot_sz + (l == 0 ? 0u : a.cp0 + N + (l - 1) * (N + a.cp1));
+  for (uint32_t n = threadIdx.x; n < N + cp; n += blockDim.x) {
+    const float2 v = buf[src][n < cp ? N - cp + n : n - cp];
+    out[n]         = make_float2(v.x * scale, -v.y * scale);
+  }
+}
+
+hipError_t ofdm_launch_tx(const OfdmArgs& a, float scale, uint32_t njobs, hipStream_t s)
+{
+  for (uint32_t j0 = 0; j0 < njobs; j0 += 65535) {
+    OfdmArgs       b = a;
+    const uint32_t n = njobs - j0 < 65535 ? njobs - j0 : 65535;
+    b.jobs           = a.jobs + j0;
+    hipLaunchKernelGGL(ofdm_tx, dim3(2 * a.nsymb, n), dim3(256), 0, s, b, scale);
+  }
+  return hipGetLastError();
+}
+
 hipError_t ofdm_launch_rx(const OfdmArgs& a, uint32_t njobs, hipStream_t s)
 {
   if (!njobs) return hipSuccess;

@@ -410,7 +410,10 @@ void mi355_dev_free(void* p)
 
 int mi355_memcpy_h2d(void* dst, const void* src, size_t bytes)
 {
+  // a pageable-source hipMemcpy may return once the data is staged, before the DMA lands; the library's own
+  // streams are non-blocking (not ordered after the null stream), so complete it before returning
   CHECK_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  CHECK_HIP(hipStreamSynchronize(nullptr));
   return MI355_SUCCESS;
 }
 
@@ -423,6 +426,7 @@ int mi355_memcpy_d2h(void* dst, const void* src, size_t bytes)
 int mi355_memset_dev(void* dst, int value, size_t bytes)
 {
   CHECK_HIP(hipMemset(dst, value, bytes));
+  CHECK_HIP(hipStreamSynchronize(nullptr));
   return MI355_SUCCESS;
 }
 

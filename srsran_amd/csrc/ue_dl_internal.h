@@ -3,10 +3,42 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cmath>
+
 namespace mi355 {
 
 constexpr uint32_t OFDM_MAX_N      = 2048;
 constexpr uint32_t OFDM_MAX_STAGES = 8;
+
+// srslte_symbol_sz / srslte_symbol_sz_power2 (common/phy_common.c:334-380)
+inline uint32_t symbol_sz(uint32_t nof_prb, bool std_rates)
+{
+  static const uint32_t lim[6] = {6, 15, 25, 50, 75, 110};
+  static const uint32_t ns[6]  = {128, 256, 384, 768, 1024, 1536};
+  static const uint32_t st[6]  = {128, 256, 512, 1024, 1536, 2048};
+  if (nof_prb == 0) return 0;
+  for (int i = 0; i < 6; i++)
+    if (nof_prb <= lim[i]) return std_rates ? st[i] : ns[i];
+  return 0;
+}
+
+inline uint32_t cp_len(uint32_t N, uint32_t c) { return (uint32_t)std::ceil((float)c * N / 2048.0f); } // SRSLTE_CP_LEN
+
+// radix plan: at most one radix-3 stage, then 8s, then a 4 or 2 remainder
+inline int radix_plan(uint32_t N, uint32_t* r)
+{
+  int n = 0;
+  if (N % 3 == 0) {
+    r[n++] = 3;
+    N /= 3;
+  }
+  while (N % 8 == 0 && N > 1) {
+    r[n++] = 8;
+    N /= 8;
+  }
+  if (N == 4 || N == 2) r[n++] = N, N = 1;
+  return N == 1 ? n : -1;
+}
 
 struct OfdmJob {
   const float2* in;  // time-domain subframe of one rx antenna
@@ -36,6 +68,8 @@ struct ChestArgs {
 };
 
 hipError_t ofdm_launch_rx(const OfdmArgs& a, uint32_t njobs, hipStream_t s);
+// srslte_ofdm_tx_sf + the srslte_enb_dl_gen_signal scale; jobs: in = grid, out = time-domain subframe
+hipError_t ofdm_launch_tx(const OfdmArgs& a, float scale, uint32_t njobs, hipStream_t s);
 hipError_t chest_launch(const ChestArgs& a, uint32_t njobs, hipStream_t s);
 // get_noise (chest_dl.c:847-857) per job from the [job][rx][port][5] estimator outputs
 hipError_t chest_launch_noise(const float* out, uint32_t R, uint32_t P, uint32_t njobs, float* noise, hipStream_t s);

@@ -33,36 +33,6 @@ using namespace mi355;
 
 namespace {
 
-// srslte_symbol_sz / srslte_symbol_sz_power2 (common/phy_common.c:334-380)
-uint32_t symbol_sz(uint32_t nof_prb, bool std_rates)
-{
-  static const uint32_t lim[6] = {6, 15, 25, 50, 75, 110};
-  static const uint32_t ns[6]  = {128, 256, 384, 768, 1024, 1536};
-  static const uint32_t st[6]  = {128, 256, 512, 1024, 1536, 2048};
-  if (nof_prb == 0) return 0;
-  for (int i = 0; i < 6; i++)
-    if (nof_prb <= lim[i]) return std_rates ? st[i] : ns[i];
-  return 0;
-}
-
-uint32_t cp_len(uint32_t N, uint32_t c) { return (uint32_t)std::ceil((float)c * N / 2048.0f); } // SRSLTE_CP_LEN
-
-// radix plan: at most one radix-3 stage, then 8s, then a 4 or 2 remainder
-int radix_plan(uint32_t N, uint32_t* r)
-{
-  int n = 0;
-  if (N % 3 == 0) {
-    r[n++] = 3;
-    N /= 3;
-  }
-  while (N % 8 == 0 && N > 1) {
-    r[n++] = 8;
-    N /= 8;
-  }
-  if (N == 4 || N == 2) r[n++] = N, N = 1;
-  return N == 1 ? n : -1;
-}
-
 float to_db(float v) { return 10.0f * log10f(v); }
 float to_dbm(float v) { return to_db(v) + 30.0f; }
 

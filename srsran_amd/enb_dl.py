@@ -44,3 +44,70 @@ def put_refs(cell: Cell, tti: int, grids: np.ndarray) -> None:
     for p in range(grids.shape[0]):
         g[p] = grids[p].ctypes.data
     check(L.mi355_refsignal_cs_put_sf_host(C.byref(cell), tti, g), "refsignal_cs_put_sf_host")
+
+
+class EnbPdschJob(C.Structure):
+    """mi355_enb_dl_pdsch_job_t: one srslte_enb_dl_put_pdsch call (device payloads and port grids)."""
+    _fields_ = [("sf", DlSfCfg), ("cfg", PdschCfg), ("data", C.c_void_p * 2), ("sf_symbols", C.c_void_p * 4)]
+
+
+def _declare_gpu():
+    L = _declare()
+    if getattr(L, "_enb_gpu_declared", False):
+        return L
+    vp, u32, i32 = C.c_void_p, C.c_uint32, C.c_int
+    L.mi355_enb_dl_create.argtypes = [C.POINTER(vp), C.POINTER(Cell), i32]
+    L.mi355_enb_dl_destroy.argtypes = [vp]
+    L.mi355_enb_dl_put_pdsch_batch.argtypes = [vp, C.POINTER(EnbPdschJob), u32, vp]
+    L.mi355_enb_dl_put_refs_batch.argtypes = [vp, C.POINTER(u32), C.POINTER(vp), u32, vp]
+    L.mi355_enb_dl_gen_signal_batch.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), u32, vp]
+    L.mi355_channel_grid_batch.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), u32, u32, C.POINTER(C.c_float),
+                                           C.c_float, C.c_uint64, vp]
+    L._enb_gpu_declared = True
+    return L
+
+
+class EnbDl:
+    """srslte_enb_dl_t's PDSCH / CRS / IFFT path on one MI355X (mi355_enb_dl_*).  Pointer arguments are device
+    addresses (ints, e.g. torch tensor data_ptr()); stream None: synchronous, else asynchronous on that HIP stream."""
+
+    def __init__(self, cell: Cell, device: int = 0):
+        self.L = _declare_gpu()
+        h = C.c_void_p()
+        check(self.L.mi355_enb_dl_create(C.byref(h), C.byref(cell), device), "enb_dl_create")
+        self.h, self.cell, self.device = h, cell, device
+
+    def put_pdsch(self, jobs: list[EnbPdschJob], stream=None):
+        n = len(jobs)
+        check(self.L.mi355_enb_dl_put_pdsch_batch(self.h, (EnbPdschJob * n)(*jobs), n, stream), "enb_dl_put_pdsch")
+
+    def put_refs(self, ttis: list[int], grids: list[int], stream=None):
+        n = len(ttis)
+        check(self.L.mi355_enb_dl_put_refs_batch(self.h, (C.c_uint32 * n)(*ttis), (C.c_void_p * len(grids))(*grids),
+                                                 n, stream), "enb_dl_put_refs")
+
+    def gen_signal(self, grids: list[int], out: list[int], stream=None):
+        n = len(grids)
+        check(self.L.mi355_enb_dl_gen_signal_batch(self.h, (C.c_void_p * n)(*grids), (C.c_void_p * n)(*out), n,
+                                                   stream), "enb_dl_gen_signal")
+
+    def channel(self, tx: list[int], rx: list[int], nof_rx: int, H: np.ndarray, sigma: float, seed: int,
+                stream=None):
+        """rx grids (nof_rx per job) = H (nof_rx x nof_ports complex) . tx grids (nof_ports per job) + AWGN."""
+        n = len(rx) // nof_rx
+        h = np.ascontiguousarray(np.asarray(H, np.complex64)).view(np.float32).ravel()
+        hf = (C.c_float * len(h))(*h.tolist())
+        check(self.L.mi355_channel_grid_batch(self.h, (C.c_void_p * len(tx))(*tx), (C.c_void_p * len(rx))(*rx), n,
+                                              nof_rx, hf, float(sigma), int(seed) & (2**64 - 1), stream),
+              "channel_grid")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.mi355_enb_dl_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
