@@ -10,9 +10,10 @@ time-domain I/Q already resident in HBM:
     softbuffer reset (new TBs) -> OFDM demodulation (2 x 14 x 1536-pt DFT) -> CRS channel estimation
     (AVERAGE, Gauss, REFS noise) -> RE extraction + MMSE + demap + descramble + CSI -> rate dematching ->
     turbo decoding with per-CB CRC early stop -> TB CRC.
-Synthetic data: random payloads -> the product's eNodeB-side encoder (include/srsran_amd/enb_dl.h) ->
-phy_dl_test's crossed 2x2 channel [[1,1],[1,-1]] + AWGN (40 dB) -> IFFT + CP; D distinct subframes
-(sf_idx cycling 0..9) tiled over the batch.
+Synthetic data (generated before the timed region): random payloads -> the product's GPU eNodeB generator
+(include/srsran_amd/enb_dl.h: DL-SCH encode, QAM256, TM4 precoding, CRS) -> phy_dl_test's crossed 2x2 channel
+[[1,1],[1,-1]] + AWGN (40 dB) -> IFFT + CP; every subframe of the batch distinct (sf_idx cycling 0..9), seeded
+per rank.  --gen host: D distinct subframes from the host encoder tiled over the batch (the earlier data).
 
     python bench.py [--gpus N --steps K --warmup W]            # N > 1: launched by torch.distributed.run
     python bench.py --workload tdec                            # configs[1]: batched turbo decode only
@@ -56,7 +57,10 @@ def parse():
                     help="pdsch: known grants (decode_batch); ue_dl: phy_dl_test's work_ue with the PCFICH / PDCCH "
                          "blind search deriving every grant (find_and_decode); tdec: configs[1]")
     ap.add_argument("--subframes", type=int, default=2048, help="TM4 subframes per GPU per step")
-    ap.add_argument("--distinct", type=int, default=20, help="distinct synthetic subframes tiled over the batch")
+    ap.add_argument("--gen", choices=["device", "host"], default="device",
+                    help="device: every subframe of the batch distinct, synthesised by the product's GPU eNodeB "
+                         "generator (mi355_enb_dl_*); host: --distinct subframes from the host encoder, tiled")
+    ap.add_argument("--distinct", type=int, default=20, help="--gen host: distinct synthetic subframes tiled")
     ap.add_argument("--snr", type=float, default=40.0)
     ap.add_argument("--ncb", type=int, default=65536, help="tdec workload: code blocks per GPU per step")
     ap.add_argument("--K", type=int, default=6144)
@@ -244,10 +248,67 @@ def synth_tm4(cell, D, snr_db, seed, ctrl=False):
     return iq, payloads
 
 
+def synth_tm4_device(cell, B, snr_db, seed, device, ctrl, d_iq, sf_len, chunk=256):
+    """B distinct subframes straight into d_iq (B x 2 rx x sf_len complex) with the product's GPU eNodeB generator:
+    random payloads -> mi355_enb_dl_put_pdsch_batch (TB/CB CRC, turbo coding, rate matching, scrambling, QAM256,
+    TM4 precoding, RE map) + put_refs (CRS) [+ the host-encoded PCFICH/PDCCH row of the subframe index, CFI 1] ->
+    phy_dl_test's crossed 2x2 channel + AWGN (mi355_channel_grid_batch) -> gen_signal (IFFT + CP).  Returns the
+    payloads (B, 2, tbs/8)."""
+    from srsran_amd import enb_dl, lib
+    from srsran_amd import pdsch as P
+    from srsran_amd.tdec import DeviceBuffer
+    rng = np.random.default_rng(seed)
+    G, nre, nb = 14 * 12 * cell.nof_prb, 12 * cell.nof_prb, 97896 // 8
+    payloads = rng.integers(0, 256, (B, 2, nb), dtype=np.uint8)
+    d_pl = DeviceBuffer(payloads.nbytes, device).upload(payloads)
+    enb = enb_dl.EnbDl(cell, device)
+    chunk = min(chunk, B)
+    d_tx = DeviceBuffer(chunk * 2 * G * 8, device)
+    d_rx = DeviceBuffer(chunk * 2 * G * 8, device)
+    cfg_sf = {sf: tm4_cfg(P, cell, sf) for sf in range(10)}
+    rows = None
+    if ctrl:  # symbol 0 (CFI 1) of each port: CRS + PCFICH + the subframe's DCI on the PDCCH
+        from srsran_amd import pdcch as Dc
+        rows = {}
+        for sf in range(10):
+            g = np.zeros((2, G), np.complex64)
+            enb_dl.put_refs(cell, sf, g)
+            Dc.encode_ctrl_host(cell, sf, 1, [tm4_dci_msg(cell, sf)], g)
+            rows[sf] = np.ascontiguousarray(g[:, :nre])
+    H = np.array([[1, 1], [1, -1]], np.complex64)
+    sigma = math.sqrt(10 ** (-snr_db / 10) / 2)
+    for c0 in range(0, B, chunk):
+        n = min(chunk, B - c0)
+        lib().mi355_memset_dev(d_tx.ptr, 0, n * 2 * G * 8)
+        jobs = []
+        tx = [d_tx.ptr + (k * 2 + p) * G * 8 for k in range(n) for p in range(2)]
+        rx = [d_rx.ptr + (k * 2 + r) * G * 8 for k in range(n) for r in range(2)]
+        for k in range(n):
+            i, sf = c0 + k, (c0 + k) % 10
+            j = enb_dl.EnbPdschJob()
+            j.sf.tti, j.sf.cfi = sf, 1
+            j.cfg = cfg_sf[sf]
+            for t in range(2):
+                j.data[t] = d_pl.ptr + (i * 2 + t) * nb
+            for p in range(2):
+                j.sf_symbols[p] = tx[2 * k + p]
+            jobs.append(j)
+        enb.put_pdsch(jobs)
+        enb.put_refs([(c0 + k) % 10 for k in range(n)], tx)
+        if ctrl:
+            for k in range(n):
+                for p in range(2):
+                    lib().mi355_memcpy_h2d(tx[2 * k + p], rows[(c0 + k) % 10][p].ctypes.data, nre * 8)
+        enb.channel(tx, rx, 2, H, sigma, seed * 1000003 + c0)
+        enb.gen_signal(rx, [d_iq.ptr + ((c0 + k) * 2 + r) * sf_len * 8 for k in range(n) for r in range(2)])
+    enb.close()
+    return payloads
+
+
 class Tm4Batch:
     """B subframes resident in HBM with their grids, channel estimates, softbuffers and payload buffers."""
 
-    def __init__(self, cell, B, D, snr, seed, device, ctrl=False):
+    def __init__(self, cell, B, D, snr, seed, device, ctrl=False, gen="host"):
         from srsran_amd import lib
         from srsran_amd import pdsch as P
         from srsran_amd.dlsch import SoftbufferPool
@@ -255,18 +316,25 @@ class Tm4Batch:
         from srsran_amd.ue_dl import DlSfJob, UeDl, default_chest_cfg
         self.P, self.B, self.D = P, B, D
         self.ctrl = ctrl
-        self.iq_host, self.payloads = synth_tm4(cell, D, snr, seed, ctrl)
-        sf_len = self.iq_host.shape[2]
+        from srsran_amd.ue_dl import symbol_sz
+        sf_len = 15 * symbol_sz(cell.nof_prb)
         G = 14 * 12 * cell.nof_prb
         self.G = G
         self.plen = 97896 // 8 + 16
-        # every subframe gets its own I/Q buffers (the D distinct contents tiled), so the OFDM stage streams
-        # B distinct inputs from HBM instead of re-reading D cached ones
+        # every subframe gets its own I/Q buffers, so the OFDM stage streams B inputs from HBM
         self.d_iq = DeviceBuffer(B * 2 * sf_len * 8, device)
-        iq = np.ascontiguousarray(self.iq_host, np.complex64)
-        for i in range(B):
-            lib().mi355_memcpy_h2d(C.c_void_p(self.d_iq.ptr + i * 2 * sf_len * 8), iq[i % D].ctypes.data,
-                                   C.c_size_t(2 * sf_len * 8))
+        if gen == "device":  # all B subframes distinct, synthesised on the GPU
+            self.D = D = B
+            self.payloads = synth_tm4_device(cell, B, snr, seed, device, ctrl, self.d_iq, sf_len)
+            S = min(B, 10)  # the CPU baseline's sample
+            self.iq_host = np.zeros((S, 2, sf_len), np.complex64)
+            self.d_iq.download(self.iq_host)
+        else:  # D distinct host-encoded subframes tiled over the batch
+            self.iq_host, self.payloads = synth_tm4(cell, D, snr, seed, ctrl)
+            iq = np.ascontiguousarray(self.iq_host, np.complex64)
+            for i in range(B):
+                lib().mi355_memcpy_h2d(C.c_void_p(self.d_iq.ptr + i * 2 * sf_len * 8), iq[i % D].ctypes.data,
+                                       C.c_size_t(2 * sf_len * 8))
         self.d_grid = DeviceBuffer(B * 2 * G * 8, device)
         self.d_ce = DeviceBuffer(B * 4 * G * 8, device)
         self.d_pay = DeviceBuffer(B * 2 * self.plen, device)
@@ -423,7 +491,8 @@ def run_pdsch(args, world, rank, local, pg):
     cell = tm4_setup()
     B = args.subframes
     ctrl = args.workload == "ue_dl"
-    b = Tm4Batch(cell, B, min(args.distinct, B), args.snr, seed=shard_seed(rank), device=local, ctrl=ctrl)
+    b = Tm4Batch(cell, B, min(args.distinct, B), args.snr, seed=shard_seed(rank), device=local, ctrl=ctrl,
+                 gen=args.gen)
     for _ in range(args.warmup):
         b.step()
     lib().mi355_device_sync()
@@ -476,7 +545,9 @@ def run_pdsch(args, world, rank, local, pg):
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32+int16", "data": "synthetic",
         "config": {"workload": f"srslte_ue_dl chain from time-domain I/Q: {B} subframes/GPU/step, 20 MHz (100 PRB), "
                                "TM4 2x2 spatial multiplexing, 2 codewords QAM256 TBS 97896 (C=16, K=6144), "
-                               "MMSE+CSI, max 10 half-its with CRC early stop, 40 dB crossed 2x2 channel" +
+                               "MMSE+CSI, max 10 half-its with CRC early stop, 40 dB crossed 2x2 channel, " +
+                               ("every subframe distinct (GPU eNodeB generator)" if args.gen == "device" else
+                                f"{b.D} distinct host-encoded subframes tiled") +
                                ("; grants from the PCFICH/PDCCH blind search (DCI format 2 per subframe, "
                                 "find_and_decode = phy_dl_test work_ue)" if ctrl else ""),
                    "subframes_per_gpu": B, "code_blocks_per_gpu": 32 * B, "distinct_subframes": b.D,
