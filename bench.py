@@ -53,9 +53,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["pdsch", "ue_dl", "tdec"], default="pdsch",
+    ap.add_argument("--workload", choices=["pdsch", "ue_dl", "tdec", "enb"], default="pdsch",
                     help="pdsch: known grants (decode_batch); ue_dl: phy_dl_test's work_ue with the PCFICH / PDCCH "
-                         "blind search deriving every grant (find_and_decode); tdec: configs[1]")
+                         "blind search deriving every grant (find_and_decode); tdec: configs[1]; enb: the GPU "
+                         "eNodeB generator (encode side, SURVEY 8f row 2)")
     ap.add_argument("--subframes", type=int, default=2048, help="TM4 subframes per GPU per step")
     ap.add_argument("--gen", choices=["device", "host"], default="device",
                     help="device: every subframe of the batch distinct, synthesised by the product's GPU eNodeB "
@@ -662,10 +663,134 @@ def run_tdec(args, world, rank, local, pg):
     return res
 
 
+# ====================================================================================== eNodeB generator (8f row 2)
+
+def run_enb(args, world, rank, local, pg):
+    """The GPU eNodeB generator on the TM4 batch: payloads resident in HBM -> put_pdsch (DL-SCH encode, QAM256,
+    precoding, RE map) -> put_refs -> crossed 2x2 channel + AWGN -> gen_signal (IFFT + CP), B subframes per step.
+    Parity: the last step's I/Q decodes through the product's UE chain with every payload (checked after timing)."""
+    from srsran_amd import enb_dl, lib
+    from srsran_amd import pdsch as P
+    from srsran_amd.tdec import DeviceBuffer
+    from srsran_amd.ue_dl import symbol_sz
+    cell = tm4_setup()
+    B = args.subframes
+    G, N, nb = 14 * 12 * cell.nof_prb, symbol_sz(cell.nof_prb), 97896 // 8
+    sf_len = 15 * N
+    rng = np.random.default_rng(shard_seed(rank))
+    payloads = rng.integers(0, 256, (B, 2, nb), dtype=np.uint8)
+    d_pl = DeviceBuffer(payloads.nbytes, local).upload(payloads)
+    d_tx = DeviceBuffer(B * 2 * G * 8, local)
+    d_rx = DeviceBuffer(B * 2 * G * 8, local)
+    d_iq = DeviceBuffer(B * 2 * sf_len * 8, local)
+    lib().mi355_memset_dev(d_tx.ptr, 0, B * 2 * G * 8)
+    enb = enb_dl.EnbDl(cell, local)
+    cfg_sf = {sf: tm4_cfg(P, cell, sf) for sf in range(10)}
+    tx = [d_tx.ptr + (i * 2 + p) * G * 8 for i in range(B) for p in range(2)]
+    rx = [d_rx.ptr + (i * 2 + r) * G * 8 for i in range(B) for r in range(2)]
+    iq = [d_iq.ptr + (i * 2 + r) * sf_len * 8 for i in range(B) for r in range(2)]
+    jobs = []
+    for i in range(B):
+        j = enb_dl.EnbPdschJob()
+        j.sf.tti, j.sf.cfi = i % 10, 1
+        j.cfg = cfg_sf[i % 10]
+        for t in range(2):
+            j.data[t] = d_pl.ptr + (i * 2 + t) * nb
+        for p in range(2):
+            j.sf_symbols[p] = tx[2 * i + p]
+        jobs.append(j)
+    ttis = (C.c_uint32 * B)(*[i % 10 for i in range(B)])
+    jobs = (enb_dl.EnbPdschJob * B)(*jobs)
+    tx, rx, iq = [(C.c_void_p * len(v))(*v) for v in (tx, rx, iq)]
+    H = np.array([[1, 1], [1, -1]], np.complex64)
+    sigma = math.sqrt(10 ** (-args.snr / 10) / 2)
+
+    def step(k):
+        enb.put_pdsch(jobs)
+        enb.put_refs(ttis, tx)
+        enb.channel(tx, rx, 2, H, sigma, 1000003 * shard_seed(rank) + k)
+        enb.gen_signal(rx, iq)
+
+    for k in range(args.warmup):
+        step(k)
+    lib().mi355_device_sync()
+    barrier(pg, local)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    lib().mi355_device_sync()
+    barrier(pg, local)
+    dt = max_over_ranks(pg, local, time.perf_counter() - t0)
+    # parity: decode the last step's I/Q with the product's UE chain
+    ok = decode_check(cell, B, d_iq, payloads, local)
+    ok_all = int(sum_over_ranks(pg, local, ok))
+    mbps = whole_job_rate(world, B * 2 * 97896, args.steps, dt) / 1e6
+    # algorithmic HBM bytes per subframe of the chain (DESIGN.md 5): payload in, codeword bits out + in, PDSCH and
+    # CRS REs out, channel grids in + out, IFFT grids in + I/Q out
+    nre_pdsch = 2 * 14400
+    per_sf = 2 * nb + 2 * 2 * 115200 + 2 * nre_pdsch * 8 + 2 * 800 * 8 + 2 * 2 * G * 8 + 2 * G * 8 + 2 * sf_len * 8
+    ach = B * per_sf * args.steps / dt / 1e9
+    res = {
+        "metric": "PDSCH encoded Mbps (GPU eNodeB generator), 20 MHz TM4 QAM256", "value": round(mbps, 1),
+        "unit": "Mbps", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8+fp32", "data": "synthetic",
+        "config": {"workload": f"srslte_enb_dl put_pdsch + put_refs + crossed 2x2 channel + gen_signal for {B} TM4 "
+                               "QAM256 subframes/GPU/step (2 x TBS 97896, 32 CBs of K=6144 each), payloads in HBM",
+                   "subframes_per_gpu": B, "parallelism": f"dp{world}"},
+        "subframes_per_s": round(world * B * args.steps / dt, 1),
+        "decoded_back_ok_tbs": f"{ok_all}/{2 * B * world}",
+        "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(ach / 8000.0, 4), "traffic": None, "kernel": "whole generator chain",
+                     "algorithmic_bytes_per_subframe": per_sf},
+    }
+    return res
+
+
+def decode_check(cell, B, d_iq, payloads, device):
+    """CRC-ok TBs with the right payload when the I/Q in d_iq (B x 2 x sf_len) goes through mi355_ue_dl_decode_batch."""
+    from srsran_amd import pdsch as P
+    from srsran_amd.dlsch import SoftbufferPool
+    from srsran_amd.tdec import DeviceBuffer
+    from srsran_amd.ue_dl import DlSfJob, UeDl, default_chest_cfg, symbol_sz
+    G, sf_len, plen = 14 * 12 * cell.nof_prb, 15 * symbol_sz(cell.nof_prb), 97896 // 8 + 16
+    ue = UeDl(cell, 2, device)
+    d_grid = DeviceBuffer(B * 2 * G * 8, device)
+    d_ce = DeviceBuffer(B * 4 * G * 8, device)
+    d_pay = DeviceBuffer(B * 2 * plen, device)
+    pool = SoftbufferPool(2 * B, max_cb=16, device=device)
+    jobs, sfs, cfgs = (DlSfJob * B)(), (P.DlSfCfg * B)(), (P.PdschCfg * B)()
+    pays = (C.c_void_p * (2 * B))()
+    for i in range(B):
+        j = jobs[i]
+        j.tti = i % 10
+        for r in range(2):
+            j.in_buffer[r] = d_iq.ptr + (i * 2 + r) * sf_len * 8
+            j.sf_symbols[r] = d_grid.ptr + (i * 2 + r) * G * 8
+            for p in range(2):
+                j.ce[p][r] = d_ce.ptr + (i * 4 + p * 2 + r) * G * 8
+        sfs[i] = P.DlSfCfg(i % 10, 1)
+        cfgs[i] = tm4_cfg(P, cell, i % 10, softbuffers=(2 * i, 2 * i + 1))
+        pays[2 * i], pays[2 * i + 1] = d_pay.ptr + 2 * i * plen, d_pay.ptr + (2 * i + 1) * plen
+    chest, res = ue.decode(pool, list(jobs), list(sfs), list(cfgs), default_chest_cfg(), list(pays))
+    host = d_pay.download(np.zeros(B * 2 * plen, np.uint8)).reshape(B, 2, plen)
+    ok = 0
+    for i in range(B):
+        for t in range(2):
+            if res[2 * i + t].crc and np.array_equal(host[i, t, : 97896 // 8], payloads[i, t]):
+                ok += 1
+    return ok
+
+
 def main():
     args = parse()
     world, rank, local, pg = dist_setup()
-    res = run_tdec(args, world, rank, local, pg) if args.workload == "tdec" else run_pdsch(args, world, rank, local, pg)
+    if args.workload == "tdec":
+        res = run_tdec(args, world, rank, local, pg)
+    elif args.workload == "enb":
+        res = run_enb(args, world, rank, local, pg)
+    else:
+        res = run_pdsch(args, world, rank, local, pg)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if pg is not None:

@@ -23,13 +23,13 @@ struct EnbTbDev {        // one transport block: CRC24A of its payload (encode_t
 struct EnbCbDev {         // one code block (encode_tb_off's loop body, sch.c:300-350)
   const uint8_t*  data;   // TB payload
   const uint8_t*  tbcrc;  // the TB's 3 CRC bytes (EnbTbDev.crc)
-  const uint16_t* txt;    // rm_tx_table(K, rv)
+  const uint16_t* txt;    // rm_tx_table(K, rv) as (stream << 14 | position): stream 0..2 = x z z', 3 = tails
+  const uint16_t* qpp;    // QPP interleaver of K: pi(i) = (f1 i + f2 i^2) mod K (tc_interl_lte.c:72-109)
   uint8_t*        e;      // codeword bits, one byte per bit
   uint32_t        tb_bytes;
   uint32_t        rp8;    // first byte of the block's data in payload || TB CRC
   uint32_t        rlen;   // data bits (K - 24 when C > 1, else K)
   uint32_t        K, cbcrc; // cbcrc: attach CRC24B (C > 1)
-  uint32_t        f1, f2;   // QPP interleaver (tc_interl_lte.c:39-67)
   uint32_t        E, wp, nbits; // transmitted bits, first bit in the codeword, codeword length (guard)
 };
 

@@ -4,8 +4,8 @@
 // (enb_dl_host.cpp), which the parity tests pin against the oracle transmitter.
 //
 //   enb_tb_crc     WG per TB: CRC24A of the payload (byte table in LDS, chunked CRC combine).
-//   enb_cb_encode  WG per code block: block bytes (payload || TB CRC) -> CRC24B -> bits in LDS -> QPP
-//                  interleave -> both 8-state RSCs as a wave each -> rate matching into codeword bits.
+//   enb_cb_encode  WG per code block: block bytes (payload || TB CRC) -> CRC24B -> QPP interleave (packed)
+//                  -> both 8-state RSCs as a wave each, a byte per step -> rate matching into codeword bits.
 //   enb_map        thread per RE (RE pair for SFBC): scrambling + 36.211 7.1 modulation + layer mapping +
 //                  precoding + RE mapping.
 //   enb_crs        thread per pilot: srslte_refsignal_cs_put_sf.
@@ -13,9 +13,9 @@
 //
 // The recursive systematic convolutional encoder (36.212 5.1.3.2.1; turbocoder.c:76-186) is a linear recursion
 // over GF(2)^3, s' = A s + b u, so a wave encodes a K-bit block in parallel: lane l runs its chunk of
-// Lc = ceil(K/64) steps from the zero state (end state e_l), a Hillis-Steele scan with the constant multiplier
-// A^Lc (squared per level) turns the e_l into every chunk's true start state, and each lane re-runs its chunk
-// from there, emitting the parity bits.  The lane holding the last step appends the trellis termination.
+// Lb = ceil(K/512) bytes from the zero state (end state e_l), a Hillis-Steele scan with the constant multiplier
+// A^(8 Lb) (squared per level) turns the e_l into every chunk's true start state, and each lane re-runs its
+// chunk from there, emitting the parity bytes.  The lane holding the last step appends the trellis termination.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -137,65 +137,109 @@ __global__ __launch_bounds__(256) void enb_tb_crc(const EnbTbDev* __restrict__ t
 // ---------------------------------------------------------------------------- code-block encoder
 constexpr uint32_t ENB_KMAX = 6144;
 
+// Streams in LDS, packed MSB first as the block bytes: systematic (the block itself), parity 1, parity 2, plus
+// the 12 tail bits.  The encoders step a byte at a time through T[s][x] = (state after the 8 input bits x from
+// state s) << 8 | (their 8 parity bits), built per workgroup.
 __global__ __launch_bounds__(256) void enb_cb_encode(const EnbCbDev* __restrict__ cbs, const CrcTable* __restrict__ T)
 {
-  __shared__ uint8_t  cbb[ENB_KMAX / 8 + 4];
-  __shared__ uint8_t  ci[ENB_KMAX];            // QPP-interleaved block bits
-  __shared__ uint8_t  d[3 * ENB_KMAX + 12 + 4]; // encoder output, x z z' per step then the tails
+  __shared__ uint8_t  sys[ENB_KMAX / 8 + 4];
+  __shared__ uint8_t  il[ENB_KMAX / 8];   // QPP-interleaved block, packed
+  __shared__ uint8_t  par[2][ENB_KMAX / 8];
+  __shared__ uint8_t  tail[12];
+  __shared__ uint16_t trel[8 * 256];
   __shared__ uint32_t tl[256];
   const EnbCbDev J   = cbs[blockIdx.x];
-  const uint32_t tid = threadIdx.x, K = J.K;
+  const uint32_t tid = threadIdx.x, K = J.K, KB = K / 8;
   tl[tid]            = T->t[tid];
+#pragma unroll
+  for (uint32_t r = 0; r < 8; r++) { // trellis table entry (s, x) = tid + 256 r
+    const uint32_t e = tid + 256 * r, x = e & 255u;
+    uint32_t       st = e >> 8, z = 0;
+#pragma unroll
+    for (int b = 7; b >= 0; b--) z = (z << 1) | rsc_step(st, (x >> b) & 1u);
+    trel[e] = (uint16_t)((st << 8) | z);
+  }
   // block bytes: rlen is a multiple of 8 and every block starts on a byte of payload || TB CRC
   for (uint32_t i = tid; i < J.rlen / 8; i += 256) {
     const uint32_t b = J.rp8 + i;
-    cbb[i]           = b < J.tb_bytes ? J.data[b] : J.tbcrc[b - J.tb_bytes];
+    sys[i]           = b < J.tb_bytes ? J.data[b] : J.tbcrc[b - J.tb_bytes];
   }
   __syncthreads();
   if (J.cbcrc) { // CRC24B over the block's data (sch.c:316-323)
-    const uint32_t crc = block_crc24(cbb, J.rlen / 8, tl, *T);
-    if (tid < 3) cbb[J.rlen / 8 + tid] = (uint8_t)(crc >> (16 - 8 * tid));
+    const uint32_t crc = block_crc24(sys, J.rlen / 8, tl, *T);
+    if (tid < 3) sys[J.rlen / 8 + tid] = (uint8_t)(crc >> (16 - 8 * tid));
     __syncthreads();
   }
-  for (uint32_t i = tid; i < K; i += 256) d[3 * i] = (cbb[i >> 3] >> (7 - (i & 7u))) & 1u;
-  __syncthreads();
-  for (uint32_t i = tid; i < K; i += 256) {
-    const uint32_t pi = (uint32_t)(((uint64_t)i * ((uint64_t)J.f1 + (uint64_t)J.f2 * i)) % K);
-    ci[i]             = d[3 * pi];
+  for (uint32_t j = tid; j < KB; j += 256) { // interleaved byte j: bits pi(8j) .. pi(8j+7)
+    const uint4 q = *(const uint4*)(J.qpp + 8 * j); // 16-byte aligned (tables are allocated per K)
+    const uint32_t p[8] = {q.x & 0xffffu, q.x >> 16, q.y & 0xffffu, q.y >> 16, q.z & 0xffffu, q.z >> 16,
+                           q.w & 0xffffu, q.w >> 16};
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; b++) v = (v << 1) | ((sys[p[b] >> 3] >> (7 - (p[b] & 7u))) & 1u);
+    il[j] = (uint8_t)v;
   }
   __syncthreads();
   const uint32_t w = tid >> 6, lane = tid & 63u;
   if (w < 2) { // wave 0: constituent encoder 1 (natural order), wave 1: encoder 2 (interleaved)
-    const uint32_t Lc = (K + 63) / 64;
-    const uint32_t i0 = min(K, lane * Lc), i1 = min(K, i0 + Lc);
-    auto           in = [&](uint32_t i) -> uint32_t { return w == 0 ? d[3 * i] : ci[i]; };
-    uint32_t       s  = 0;
-    for (uint32_t i = i0; i < i1; i++) rsc_step(s, in(i));
-    uint32_t x = s, M = gf2_pow(RSC_A, Lc);
+    const uint8_t* in = w == 0 ? sys : il;
+    uint8_t*       pa = par[w];
+    const uint32_t Lb = (KB + 63) / 64; // bytes per lane
+    const uint32_t b0 = min(KB, lane * Lb), b1 = min(KB, b0 + Lb);
+    uint32_t       st = 0;
+    for (uint32_t b = b0; b < b1; b++) st = trel[(st << 8) | in[b]] >> 8;
+    uint32_t x = st, M = gf2_pow(RSC_A, 8 * Lb);
 #pragma unroll
     for (uint32_t o = 1; o < 64; o <<= 1) {
       const uint32_t y = __shfl_up(x, o, 64);
       if (lane >= o) x ^= gf2_mv(M, y);
       M = gf2_mm(M, M);
     }
-    uint32_t st = __shfl_up(x, 1, 64);
+    st = __shfl_up(x, 1, 64);
     if (lane == 0) st = 0;
-    for (uint32_t i = i0; i < i1; i++) d[3 * i + 1 + w] = (uint8_t)rsc_step(st, in(i));
-    if (i0 < K && i1 == K) { // trellis termination, tails in encoder order x z x z x z (per encoder)
-      uint8_t* t = d + 3 * K + 6 * w;
+    for (uint32_t b = b0; b < b1; b++) {
+      const uint32_t t = trel[(st << 8) | in[b]];
+      pa[b]            = (uint8_t)t;
+      st               = t >> 8;
+    }
+    if (b0 < KB && b1 == KB) { // trellis termination, tails in encoder order x z x z x z (per encoder)
       for (int j = 0; j < 3; j++) {
-        const uint32_t xb = ((st >> 1) ^ (st >> 2)) & 1u;
-        t[2 * j]          = (uint8_t)xb;
-        t[2 * j + 1]      = (uint8_t)rsc_step(st, xb);
+        const uint32_t xb    = ((st >> 1) ^ (st >> 2)) & 1u;
+        tail[6 * w + 2 * j]     = (uint8_t)xb;
+        tail[6 * w + 2 * j + 1] = (uint8_t)rsc_step(st, xb);
       }
     }
   }
   __syncthreads();
-  // rate matching: bit k of the block = circular-buffer bit (k0 + k) mod N without dummies
+  // rate matching: bit k of the block = circular-buffer bit (k0 + k) mod N without dummies; the device table
+  // holds (stream << 14 | position) per circular-buffer bit.  A thread emits 4 consecutive bits as one 32-bit
+  // store when the block starts on a 4-byte boundary (Qm' multiple of 4).
   const uint32_t N = 3 * K + 12;
-  for (uint32_t k = tid; k < J.E; k += 256) {
-    const uint32_t j = J.wp + k;
-    if (j < J.nbits) J.e[j] = d[J.txt[k % N]];
+  const uint32_t E = min(J.E, J.nbits > J.wp ? J.nbits - J.wp : 0u);
+  auto           bit_at = [&](uint32_t kk) -> uint32_t {
+    const uint32_t t = J.txt[kk], m = t & 0x3fffu, sn = t >> 14;
+    if (sn == 3) return tail[m];
+    const uint8_t* src = sn == 0 ? sys : par[sn - 1];
+    return (src[m >> 3] >> (7 - (m & 7u))) & 1u;
+  };
+  if ((J.wp & 3u) == 0) {
+    uint32_t* e4 = (uint32_t*)(J.e + J.wp);
+    for (uint32_t k4 = 4 * tid; k4 < E; k4 += 1024) {
+      uint32_t kk = k4 % N, v = 0;
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++) {
+        const uint32_t bit = k4 + b < E ? bit_at(kk) : 0u;
+        v |= bit << (8 * b);
+        if (++kk == N) kk = 0;
+      }
+      if (k4 + 4 <= E) {
+        e4[k4 / 4] = v;
+      } else {
+        for (uint32_t b = 0; k4 + b < E; b++) J.e[J.wp + k4 + b] = (uint8_t)(v >> (8 * b));
+      }
+    }
+  } else {
+    for (uint32_t k = tid; k < E; k += 256) J.e[J.wp + k] = (uint8_t)bit_at(k % N);
   }
 }
 

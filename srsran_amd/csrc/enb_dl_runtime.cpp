@@ -67,6 +67,7 @@ struct mi355_enb_dl {
   OfdmArgs                         ofdm{};
   std::map<uint32_t, uint32_t*>    scr;  // packed scrambling sequences per c_init
   std::map<uint32_t, uint16_t*>    txt;  // (K << 2 | rv) -> rate-matching selection table
+  std::map<uint32_t, uint16_t*>    qpp;  // K -> QPP interleaver table
   std::map<std::string, MapRef>    maps; // RE maps
   char*                            scratch     = nullptr;
   size_t                           scratch_cap = 0;
@@ -107,11 +108,31 @@ static int get_txt(mi355_enb_dl_t* q, uint32_t K, uint32_t rv, const uint16_t** 
   const uint32_t key = (K << 2) | (rv & 3u);
   auto           it  = q->txt.find(key);
   if (it == q->txt.end()) {
-    const std::vector<uint16_t> t = rm_tx_table(K, rv & 3u);
-    uint16_t*                   d = nullptr;
+    std::vector<uint16_t> t = rm_tx_table(K, rv & 3u);
+    for (auto& v : t) // encoder index 3m + s (tails 3K + j) -> stream << 14 | position
+      v = v < 3 * K ? (uint16_t)(((v % 3u) << 14) | (v / 3u)) : (uint16_t)((3u << 14) | (v - 3 * K));
+    uint16_t* d = nullptr;
     CHECK_HIP(hipMalloc(&d, t.size() * 2));
     CHECK_HIP(hipMemcpy(d, t.data(), t.size() * 2, hipMemcpyHostToDevice));
     it = q->txt.emplace(key, d).first;
+  }
+  *out = it->second;
+  return MI355_SUCCESS;
+}
+
+static int get_qpp(mi355_enb_dl_t* q, uint32_t K, const uint16_t** out)
+{
+  auto it = q->qpp.find(K);
+  if (it == q->qpp.end()) {
+    const int ki = lte_cb_index_eq(K);
+    if (ki < 0) return MI355_ERROR_INVALID_INPUTS;
+    const uint64_t        f1 = lte_qpp_table[ki][1], f2 = lte_qpp_table[ki][2];
+    std::vector<uint16_t> t(K);
+    for (uint64_t i = 0; i < K; i++) t[i] = (uint16_t)((f1 * i + f2 * i % K * i) % K);
+    uint16_t* d = nullptr;
+    CHECK_HIP(hipMalloc(&d, K * 2)); // hipMalloc alignment >= 256 B: the kernel reads 8 entries per 16-byte load
+    CHECK_HIP(hipMemcpy(d, t.data(), K * 2, hipMemcpyHostToDevice));
+    it = q->qpp.emplace(K, d).first;
   }
   *out = it->second;
   return MI355_SUCCESS;
@@ -204,6 +225,7 @@ void mi355_enb_dl_destroy(mi355_enb_dl_t* q)
   (void)hipDeviceSynchronize();
   for (auto& kv : q->scr) (void)hipFree(kv.second);
   for (auto& kv : q->txt) (void)hipFree(kv.second);
+  for (auto& kv : q->qpp) (void)hipFree(kv.second);
   for (auto& kv : q->maps) (void)hipFree(kv.second.d);
   if (q->crc) (void)hipFree(q->crc);
   if (q->gold) (void)hipFree(q->gold);
@@ -305,8 +327,6 @@ int mi355_enb_dl_put_pdsch_batch(mi355_enb_dl_t* q, const mi355_enb_dl_pdsch_job
         const uint32_t K    = c < sg.C2 ? sg.K2 : sg.K1;
         const uint32_t rlen = sg.C > 1 ? K - 24 : K;
         const uint32_t E    = (c + gamma + 1 <= sg.C) ? Qme * (Gp / sg.C) : Qme * ((Gp + sg.C - 1) / sg.C);
-        const int      ki   = lte_cb_index_eq(K);
-        if (ki < 0) return MI355_ERROR_INVALID_INPUTS;
         EnbCbDev cb{};
         cb.data     = J.data[t];
         cb.tb_bytes = (uint32_t)tb.tbs / 8;
@@ -314,12 +334,10 @@ int mi355_enb_dl_put_pdsch_batch(mi355_enb_dl_t* q, const mi355_enb_dl_pdsch_job
         cb.rlen     = rlen;
         cb.K        = K;
         cb.cbcrc    = sg.C > 1;
-        cb.f1       = lte_qpp_table[ki][1];
-        cb.f2       = lte_qpp_table[ki][2];
         cb.E        = E;
         cb.wp       = wp;
         cb.nbits    = tb.nof_bits;
-        if (get_txt(q, K, tb.rv, &cb.txt)) return MI355_ERROR;
+        if (get_txt(q, K, tb.rv, &cb.txt) || get_qpp(q, K, &cb.qpp)) return MI355_ERROR_INVALID_INPUTS;
         cbs.push_back(cb);
         rp += rlen;
         wp += E;

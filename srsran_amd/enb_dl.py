@@ -67,6 +67,10 @@ def _declare_gpu():
     return L
 
 
+def _arr(t, v):
+    return v if isinstance(v, C.Array) else (t * len(v))(*v)
+
+
 class EnbDl:
     """srslte_enb_dl_t's PDSCH / CRS / IFFT path on one MI355X (mi355_enb_dl_*).  Pointer arguments are device
     addresses (ints, e.g. torch tensor data_ptr()); stream None: synchronous, else asynchronous on that HIP stream."""
@@ -77,29 +81,26 @@ class EnbDl:
         check(self.L.mi355_enb_dl_create(C.byref(h), C.byref(cell), device), "enb_dl_create")
         self.h, self.cell, self.device = h, cell, device
 
-    def put_pdsch(self, jobs: list[EnbPdschJob], stream=None):
-        n = len(jobs)
-        check(self.L.mi355_enb_dl_put_pdsch_batch(self.h, (EnbPdschJob * n)(*jobs), n, stream), "enb_dl_put_pdsch")
+    # every list argument may also be a prebuilt ctypes array of the same element type (no per-call conversion)
+    def put_pdsch(self, jobs, stream=None):
+        check(self.L.mi355_enb_dl_put_pdsch_batch(self.h, _arr(EnbPdschJob, jobs), len(jobs), stream),
+              "enb_dl_put_pdsch")
 
-    def put_refs(self, ttis: list[int], grids: list[int], stream=None):
-        n = len(ttis)
-        check(self.L.mi355_enb_dl_put_refs_batch(self.h, (C.c_uint32 * n)(*ttis), (C.c_void_p * len(grids))(*grids),
-                                                 n, stream), "enb_dl_put_refs")
+    def put_refs(self, ttis, grids, stream=None):
+        check(self.L.mi355_enb_dl_put_refs_batch(self.h, _arr(C.c_uint32, ttis), _arr(C.c_void_p, grids), len(ttis),
+                                                 stream), "enb_dl_put_refs")
 
-    def gen_signal(self, grids: list[int], out: list[int], stream=None):
-        n = len(grids)
-        check(self.L.mi355_enb_dl_gen_signal_batch(self.h, (C.c_void_p * n)(*grids), (C.c_void_p * n)(*out), n,
+    def gen_signal(self, grids, out, stream=None):
+        check(self.L.mi355_enb_dl_gen_signal_batch(self.h, _arr(C.c_void_p, grids), _arr(C.c_void_p, out), len(grids),
                                                    stream), "enb_dl_gen_signal")
 
-    def channel(self, tx: list[int], rx: list[int], nof_rx: int, H: np.ndarray, sigma: float, seed: int,
-                stream=None):
+    def channel(self, tx, rx, nof_rx: int, H: np.ndarray, sigma: float, seed: int, stream=None):
         """rx grids (nof_rx per job) = H (nof_rx x nof_ports complex) . tx grids (nof_ports per job) + AWGN."""
         n = len(rx) // nof_rx
         h = np.ascontiguousarray(np.asarray(H, np.complex64)).view(np.float32).ravel()
         hf = (C.c_float * len(h))(*h.tolist())
-        check(self.L.mi355_channel_grid_batch(self.h, (C.c_void_p * len(tx))(*tx), (C.c_void_p * len(rx))(*rx), n,
-                                              nof_rx, hf, float(sigma), int(seed) & (2**64 - 1), stream),
-              "channel_grid")
+        check(self.L.mi355_channel_grid_batch(self.h, _arr(C.c_void_p, tx), _arr(C.c_void_p, rx), n, nof_rx, hf,
+                                              float(sigma), int(seed) & (2**64 - 1), stream), "channel_grid")
 
     def close(self):
         if getattr(self, "h", None):
