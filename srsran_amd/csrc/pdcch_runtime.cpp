@@ -14,6 +14,7 @@
 #include "host_staging.h"
 #include "lte_common.h"
 #include "pdcch_internal.h"
+#include "host_parallel.h"
 #include "pdcch_runtime.h"
 
 #define CHECK_HIP(x)                                                                                                   \
@@ -155,14 +156,17 @@ int CtrlState::run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, con
   const uint32_t* h_cfi  = (const uint32_t*)back->host;
   const float*    h_corr = (const float*)(back->host + b_cfi);
   const DciCand*  h_cand = (const DciCand*)(back->host + b_cfi + b_corr);
-  for (uint32_t i = 0; i < n; i++) {
-    const uint32_t cfi = h_cfi[i];
-    res[i].cfi         = cfi;
-    res[i].cfi_corr    = std::max({0.f, h_corr[3 * i], h_corr[3 * i + 1], h_corr[3 * i + 2]});
-    res[i].nof_cce     = regs.nregs[cfi - 1] / 9;
-    res[i].nof_dci     = blind_search_replay(cell, res[i].nof_cce, rntis[i], cfgs[i], plan_of[i],
-                                         h_cand + (size_t)i * PDCCH_SLOTS * PDCCH_FMTS, msgs + (size_t)i * MI355_MAX_DCI_MSG);
-  }
+  host_parallel_for(n, 128, [&](uint32_t b, uint32_t e) { // subframes are independent
+    for (uint32_t i = b; i < e; i++) {
+      const uint32_t cfi = h_cfi[i];
+      res[i].cfi         = cfi;
+      res[i].cfi_corr    = std::max({0.f, h_corr[3 * i], h_corr[3 * i + 1], h_corr[3 * i + 2]});
+      res[i].nof_cce     = regs.nregs[cfi - 1] / 9;
+      res[i].nof_dci     = blind_search_replay(cell, res[i].nof_cce, rntis[i], cfgs[i], plan_of[i],
+                                           h_cand + (size_t)i * PDCCH_SLOTS * PDCCH_FMTS,
+                                           msgs + (size_t)i * MI355_MAX_DCI_MSG);
+    }
+  });
   if (prof)
     fprintf(stderr, "[mi355 host] control stage: blind-search replay %.1f us for %u subframes\n",
             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tr0).count(), n);

@@ -16,6 +16,7 @@
 #include "../../include/srsran_amd/ue_dl.h"
 #include "lte_common.h"
 #include "runtime_internal.h"
+#include "host_parallel.h"
 #include "host_staging.h"
 #include "pdcch_runtime.h"
 #include "ue_dl_internal.h"
@@ -492,14 +493,16 @@ static int ctrl_ready(mi355_ue_dl_t* q)
 static int unpack_all(mi355_ue_dl_t* q, const mi355_dl_sf_cfg_t* sfs, const mi355_ue_dl_cfg_t* cfgs, uint32_t n,
                       mi355_ctrl_res_t* ctrl, std::vector<mi355_dci_msg_t>& msgs, mi355_dci_dl_t* dci)
 {
-  for (uint32_t i = 0; i < n; i++) {
-    for (int k = 0; k < ctrl[i].nof_dci; k++) {
-      mi355_dci_msg_t& m = msgs[(size_t)i * MI355_MAX_DCI_MSG + k];
-      if (mi355_dci_msg_unpack_pdsch(&q->cell, &sfs[i], &cfgs[i].dci, &m, &dci[(size_t)i * MI355_MAX_DCI_MSG + k]))
-        ctrl[i].nof_dci = -1; // "Error unpacking DL DCI" (ue_dl.c:724-727)
-      if (ctrl[i].nof_dci < 0) break;
+  host_parallel_for(n, 128, [&](uint32_t b, uint32_t e) {
+    for (uint32_t i = b; i < e; i++) {
+      for (int k = 0; k < ctrl[i].nof_dci; k++) {
+        mi355_dci_msg_t& m = msgs[(size_t)i * MI355_MAX_DCI_MSG + k];
+        if (mi355_dci_msg_unpack_pdsch(&q->cell, &sfs[i], &cfgs[i].dci, &m, &dci[(size_t)i * MI355_MAX_DCI_MSG + k]))
+          ctrl[i].nof_dci = -1; // "Error unpacking DL DCI" (ue_dl.c:724-727)
+        if (ctrl[i].nof_dci < 0) break;
+      }
     }
-  }
+  });
   return MI355_SUCCESS;
 }
 
@@ -563,20 +566,28 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   // DCI -> grant, RV from the SFN for format 1C, softbuffer reset (ue_dl.c:1494-1535)
   std::vector<mi355_pdsch_job_t> jobs;
   std::vector<uint32_t>          which, rs_sb, rs_tbs;
-  for (uint32_t i = 0; i < njobs; i++) {
-    if (ctrl[i].nof_dci != 1) continue; // the reference decodes only when exactly one DCI was found
-    const mi355_dci_dl_t& d = dci[(size_t)i * MI355_MAX_DCI_MSG];
-    if (mi355_ra_dl_dci_to_grant(&q->cell, &sfs[i], ue_cfgs[i].tm, ue_cfgs[i].use_tbs_index_alt, &d, &cfgs[i].grant)) {
-      ctrl[i].nof_dci = -1; // "Error unpacking DCI"
-      continue;
-    }
-    for (int tb = 0; tb < MI355_MAX_CODEWORDS; tb++) {
-      mi355_ra_tb_t& t = cfgs[i].grant.tb[tb];
-      if (!t.enabled) continue;
-      if ((int32_t)t.rv < 0) {
-        const uint32_t k = ((sfs[i].tti / 10) / 2) % 4;
-        t.rv             = ((uint32_t)ceilf(1.5f * k)) % 4;
+  host_parallel_for(njobs, 128, [&](uint32_t b, uint32_t e) { // grants: independent per subframe
+    for (uint32_t i = b; i < e; i++) {
+      if (ctrl[i].nof_dci != 1) continue; // the reference decodes only when exactly one DCI was found
+      const mi355_dci_dl_t& d = dci[(size_t)i * MI355_MAX_DCI_MSG];
+      if (mi355_ra_dl_dci_to_grant(&q->cell, &sfs[i], ue_cfgs[i].tm, ue_cfgs[i].use_tbs_index_alt, &d, &cfgs[i].grant)) {
+        ctrl[i].nof_dci = -1; // "Error unpacking DCI"
+        continue;
       }
+      for (int tb = 0; tb < MI355_MAX_CODEWORDS; tb++) {
+        mi355_ra_tb_t& t = cfgs[i].grant.tb[tb];
+        if (t.enabled && (int32_t)t.rv < 0) {
+          const uint32_t k = ((sfs[i].tti / 10) / 2) % 4;
+          t.rv             = ((uint32_t)ceilf(1.5f * k)) % 4;
+        }
+      }
+    }
+  });
+  for (uint32_t i = 0; i < njobs; i++) {
+    if (ctrl[i].nof_dci != 1) continue;
+    for (int tb = 0; tb < MI355_MAX_CODEWORDS; tb++) {
+      const mi355_ra_tb_t& t = cfgs[i].grant.tb[tb];
+      if (!t.enabled) continue;
       rs_sb.push_back(cfgs[i].softbuffer[tb]);
       rs_tbs.push_back((uint32_t)t.tbs);
     }
