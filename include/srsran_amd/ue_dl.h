@@ -10,7 +10,9 @@
  *   mi355_chest_dl_estimate_batch srslte_chest_dl_estimate_cfg (ch_estimation/chest_dl.c:985-1014) for normal
  *                                FDD subframes: CRS LS estimates, RSRP/RSSI, REFS noise estimation, Gauss /
  *                                triangle / no smoothing, AVERAGE estimator (merged pilots, linear interpolation,
- *                                the same estimate on every OFDM symbol), srslte_chest_dl_res_t scalars.
+ *                                the same estimate on every OFDM symbol) or INTERPOLATE (each pilot symbol
+ *                                smoothed and interpolated in frequency, then linearly in time, :430-531),
+ *                                srslte_chest_dl_res_t scalars.
  *   mi355_ue_dl_*                srslte_ue_dl_init / set_cell / decode_fft_estimate / decode_pdsch
  *                                (ue/ue_dl.c:75-140, :370-430, :486-520) over batches of subframes.
  *

@@ -123,6 +123,22 @@ static void interp_linear_offset(const cf* in, cf* out, uint32_t len, uint32_t M
   }
 }
 
+/* srslte_interp_linear_vector3 (interp.c:158-188), to the right: between[0] = (start ? start : in0) + d,
+ * between[j] = between[j - 1] + d with d = (in1 - in0) * (1 / in1_in0_d), rows of nre elements */
+static void interp_vec(const cf* in0, const cf* in1, const cf* start, cf* between, uint32_t dd, uint32_t M, uint32_t nre)
+{
+  const float r = (float)1 / dd;
+  for (uint32_t k = 0; k < nre; k++) {
+    const cf d   = cscale(csub(in1[k], in0[k]), r);
+    cf       v   = cadd(start ? start[k] : in0[k], d);
+    between[k]   = v;
+    for (uint32_t i = 0; i + 1 < M; i++) {
+      v                          = cadd(v, d);
+      between[(i + 1) * nre + k] = v;
+    }
+  }
+}
+
 /* estimate_noise_pilots (chest_dl.c:320-397), normal subframe, nsymbols >= 2 */
 static float noise_refs(const cf* pe, uint32_t nsymbols, uint32_t nref, uint32_t fidx)
 {
@@ -167,13 +183,15 @@ static float noise_refs(const cf* pe, uint32_t nsymbols, uint32_t nref, uint32_t
 }
 
 /* One (rx antenna, port) estimate_port call.  grid: nsymb*2 x 12*nof_prb cf.  cfg: filter_type (0 gauss,
- * 1 triangle, 2 none), coef0/coef1 (filter_coef), estimator_alg (0 average).  ce: full grid output.
- * out3: {noise_estimate, rsrp, rssi}.  Returns -1 for unsupported configurations. */
+ * 1 triangle, 2 none), coef0/coef1 (filter_coef), estimator_alg (0 average, 1 interpolate).  ce: full grid
+ * output (INTERPOLATE with 2 pilot symbols -- ports 2, 3 -- copies the buffer's row 0, which it never writes,
+ * over every other row: chest_dl.c:490-494 as the reference runs it).  out3: {noise_estimate, rsrp, rssi}.
+ * Returns -1 for unsupported configurations. */
 int orc_chest_estimate_port(const float* grid_f, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf,
                             uint32_t port, int filter_type, float coef0, float coef1, int estimator_alg,
                             float* ce_f, float* out3)
 {
-  if (estimator_alg != 0) return -1;
+  if (estimator_alg != 0 && estimator_alg != 1) return -1;
   const cf*      grid  = (const cf*)grid_f;
   cf*            ce    = (cf*)ce_f;
   const uint32_t nsymb = cp_ext ? 6 : 7, nre = 12 * nof_prb, nsym = crs_nof_symbols(port), nref = 2 * nof_prb;
@@ -221,6 +239,45 @@ int orc_chest_estimate_port(const float* grid_f, uint32_t nof_prb, uint32_t cell
 
   const cf* src = pe;
   uint32_t  nr  = nref;
+  if (estimator_alg == 1) {
+    /* INTERPOLATE: average_pilots smooths every pilot symbol on its own (no time averaging, :549-567),
+     * interpolate_pilots interpolates each in frequency into its OFDM symbol (interp_lin, M = 6, :451-488), then
+     * linearly in time between the pilot symbols (:496-531) */
+    if (filter_type != 2) {
+      for (uint32_t l = 0; l < nsym; l++) conv_same(&pe[l * nref], filt, &smo[l * nref], nref, flen);
+      src = smo;
+    }
+    if (nsym < 3) {
+      for (uint32_t l = 1; l < 2 * nsymb; l++) memcpy(&ce[l * nre], ce, sizeof(cf) * nre);
+    } else {
+      for (uint32_t l = 0; l < nsym; l++) {
+        const uint32_t f = crs_fidx(cell_id, l, port);
+        interp_linear_offset(&src[l * nref], &ce[crs_nsymbol(l, nsymb, port) * nre], nref, 6, f, 6 - f);
+      }
+#define CE(i) (&ce[(i)*nre])
+      if (!cp_ext) {
+        interp_vec(CE(0), CE(4), NULL, CE(1), 4, 3, nre);
+        interp_vec(CE(4), CE(7), NULL, CE(5), 3, 2, nre);
+        interp_vec(CE(7), CE(11), NULL, CE(8), 4, 3, nre);
+        interp_vec(CE(7), CE(11), CE(11), CE(12), 4, 2, nre);
+      } else {
+        interp_vec(CE(0), CE(3), NULL, CE(1), 3, 2, nre);
+        interp_vec(CE(3), CE(6), NULL, CE(4), 3, 2, nre);
+        interp_vec(CE(6), CE(9), NULL, CE(7), 3, 2, nre);
+        interp_vec(CE(6), CE(9), CE(9), CE(10), 3, 2, nre);
+      }
+#undef CE
+    }
+    out3[0] = noise;
+    out3[1] = rsrp;
+    out3[2] = rssi;
+    free(crs);
+    free(rx);
+    free(pe);
+    free(avg);
+    free(smo);
+    return 0;
+  }
   if (filter_type != 2) {
     /* average_pilots: AVERAGE merges the pilot symbols (nsym > 1) */
     const int first_lo = crs_fidx(cell_id, 0, port) < 3;

@@ -111,8 +111,11 @@ def crs_put(tx: np.ndarray, nof_prb: int, cell_id: int, nof_ports: int, sf: int,
 
 
 def chest_estimate(grids: np.ndarray, nof_prb: int, nof_ports: int, cell_id: int, sf: int, filter_type: int = 0,
-                   coef=(4.0, 1.0), cp_ext: bool = False, rsrp_neighbour: bool = False):
-    """grids: (nof_rx, grid).  Returns ce (nof_ports, nof_rx, grid) and the srslte_chest_dl_res_t scalars."""
+                   coef=(4.0, 1.0), cp_ext: bool = False, rsrp_neighbour: bool = False, alg: int = 0,
+                   ce_init: np.ndarray | None = None):
+    """grids: (nof_rx, grid).  alg: 0 AVERAGE, 1 INTERPOLATE.  ce_init: (nof_ports, nof_rx, grid) initial content of
+    the estimate buffers (INTERPOLATE on ports 2, 3 copies their row 0).  Returns ce (nof_ports, nof_rx, grid) and
+    the srslte_chest_dl_res_t scalars."""
     R = grids.shape[0]
     G = grids.shape[1]
     ce = np.zeros((nof_ports, R, G), np.complex64)
@@ -120,10 +123,10 @@ def chest_estimate(grids: np.ndarray, nof_prb: int, nof_ports: int, cell_id: int
     for a in range(R):
         g = np.ascontiguousarray(grids[a], np.complex64)
         for p in range(nof_ports):
-            out = np.zeros(G, np.complex64)
+            out = np.zeros(G, np.complex64) if ce_init is None else np.array(ce_init[p, a], np.complex64)
             o3 = np.zeros(3, np.float32)
             r = lib().orc_chest_estimate_port(g.view(np.float32), nof_prb, cell_id, int(cp_ext), sf, p, filter_type,
-                                              float(coef[0]), float(coef[1]), 0, out.view(np.float32), o3)
+                                              float(coef[0]), float(coef[1]), alg, out.view(np.float32), o3)
             assert r == 0
             ce[p, a] = out
             vals[a, p] = o3

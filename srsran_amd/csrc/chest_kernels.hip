@@ -63,13 +63,68 @@ template <int N> __device__ __forceinline__ void block_sum(float (&v)[N], float*
   for (int k = 0; k < N; k++) v[k] = red[k] + red[N + k] + red[2 * N + k] + red[3 * N + k];
 }
 
+// srslte_interp_linear_offset (interp.c:259-285) output k: M points per input interval, off_st extrapolated
+// before the first input, the rest after the last
+__device__ __forceinline__ float2 interp_at(const float2* src, uint32_t len, uint32_t M, uint32_t off_st, uint32_t k)
+{
+  const float fM = (float)M;
+  if (k < off_st) {
+    const uint32_t j = off_st - 1 - k;
+    const float2   d = csub(src[1], src[0]);
+    return csub(src[0], make_float2((float)(j + 1) * d.x / fM, (float)(j + 1) * d.y / fM));
+  }
+  if (k < off_st + M * (len - 1)) {
+    const uint32_t i = (k - off_st) / M, j = (k - off_st) % M;
+    const float2   d = cscale(csub(src[i + 1], src[i]), 1.0f / fM);
+    return cadd(src[i], cscale(d, (float)j));
+  }
+  const uint32_t j = k - off_st - M * (len - 1);
+  const float2   d = csub(src[len - 1], src[len - 2]);
+  return cadd(src[len - 1], make_float2((float)j * d.x / fM, (float)j * d.y / fM));
+}
+
+// srslte_conv_same_cf with extrapolated extremes (convolution.c:183-220), output i of an N-sample input
+__device__ __forceinline__ float2 conv_same_at(const float2* in, uint32_t N, uint32_t i, const float* filt, uint32_t M)
+{
+  const uint32_t h    = M / 2;
+  float2         accv = make_float2(0.f, 0.f);
+  for (uint32_t k = 0; k < M; k++) {
+    float2 x;
+    if (i < h) { // first[i + k]
+      const uint32_t f = i + k;
+      x = f < h ? csub(cscale(in[1], (float)(2 + h - f)), cscale(in[0], (float)(1 + h - f))) : in[f - h];
+    } else if (i >= N - h) { // last[j + k], j = i - (N - h)
+      const uint32_t f = i - (N - h) + k;
+      x = f >= M - 1 ? csub(cscale(in[N - 1], (float)(2 + f - h)), cscale(in[N - 2], (float)(1 + f - h)))
+                     : in[N - M + f + 1];
+    } else {
+      x = in[(int)i - (int)h + (int)k];
+    }
+    accv = cadd(accv, cscale(x, filt[k]));
+  }
+  return accv;
+}
+
+// srslte_interp_linear_vector3 to the right (interp.c:158-188) at one subcarrier: rows[0 .. M) of `between`
+__device__ __forceinline__ void interp_rows(float2 in0, float2 in1, float2 start, uint32_t dd, uint32_t M, float2* out,
+                                            uint32_t row0, uint32_t nre)
+{
+  const float2 d = cscale(csub(in1, in0), (float)1 / (float)dd);
+  float2       v = cadd(start, d);
+  out[(size_t)row0 * nre] = v;
+  for (uint32_t i = 1; i < M; i++) {
+    v                              = cadd(v, d);
+    out[(size_t)(row0 + i) * nre]  = v;
+  }
+}
+
 } // namespace
 
 __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
 {
   __shared__ float2 pe[4 * 2 * MAXPRB];
   __shared__ float2 avg[4 * MAXPRB];
-  __shared__ float2 smo[4 * MAXPRB];
+  __shared__ float2 smo[8 * MAXPRB]; // AVERAGE: 2 nref merged; INTERPOLATE: nsym x nref
   __shared__ float2 row[12 * MAXPRB];
   __shared__ float  red[4 * 8];
   __shared__ float  filt[16];
@@ -159,6 +214,55 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
   }
   __syncthreads();
   const uint32_t M = flen_s;
+
+  if (a.alg == 1) {
+    // INTERPOLATE: average_pilots smooths each pilot symbol on its own (:549-567), interpolate_pilots
+    // interpolates each in frequency into its OFDM symbol (interp_lin, M = 6, :451-488) and linearly in time
+    // between pilot symbols (:496-531).  Thread per subcarrier: the pilot rows' values, then every row.
+    const float2* s4 = pe;
+    if (a.filter_type != 2) {
+      for (uint32_t t = threadIdx.x; t < nsym * nref; t += blockDim.x)
+        smo[t] = conv_same_at(&pe[(t / nref) * nref], nref, t % nref, filt, M);
+      __syncthreads();
+      s4 = smo;
+    }
+    const uint32_t nrows = 2 * a.nsymb;
+    float2*        ce    = J.ce;
+    for (uint32_t k = threadIdx.x; k < nre; k += blockDim.x) {
+      if (nsym < 3) { // :490-494 copies row 0 -- which nothing wrote for ports 2, 3 -- over every row
+        const float2 v = ce[k];
+        for (uint32_t r = 1; r < nrows; r++) ce[(size_t)r * nre + k] = v;
+        continue;
+      }
+      float2 P[4];
+#pragma unroll
+      for (uint32_t l = 0; l < 4; l++) {
+        const uint32_t f = crs_fidx(a.cell_id, l, port);
+        P[l]             = interp_at(&s4[l * nref], nref, 6, f, k);
+        ce[(size_t)crs_nsymbol(l, a.nsymb, port) * nre + k] = P[l];
+      }
+      float2* o = ce + k;
+      if (a.nsymb == 7) { // pilot rows 0, 4, 7, 11
+        interp_rows(P[0], P[1], P[0], 4, 3, o, 1, nre);
+        interp_rows(P[1], P[2], P[1], 3, 2, o, 5, nre);
+        interp_rows(P[2], P[3], P[2], 4, 3, o, 8, nre);
+        interp_rows(P[2], P[3], P[3], 4, 2, o, 12, nre);
+      } else { // extended CP: pilot rows 0, 3, 6, 9
+        interp_rows(P[0], P[1], P[0], 3, 2, o, 1, nre);
+        interp_rows(P[1], P[2], P[1], 3, 2, o, 4, nre);
+        interp_rows(P[2], P[3], P[2], 3, 2, o, 7, nre);
+        interp_rows(P[2], P[3], P[3], 3, 2, o, 10, nre);
+      }
+    }
+    if (threadIdx.x == 0) {
+      J.out[0] = noise;
+      J.out[1] = acc[0] / (float)np;
+      J.out[2] = acc[1] / (float)nsym;
+      J.out[3] = acc[2];
+      J.out[4] = acc[3];
+    }
+    return;
+  }
 
   // 4. average_pilots (:530-567): merge the pilot symbols, scale 2/nsym, then srslte_conv_same_cf
   const float2* src = pe;

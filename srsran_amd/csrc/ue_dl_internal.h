@@ -65,6 +65,7 @@ struct ChestArgs {
   const float2*   pilots; // [pair][sf][4 * 2 * nof_prb]
   uint32_t        nof_prb, cell_id, nsymb, filter_type;
   float           coef0, coef1;
+  uint32_t        alg; // srslte_chest_dl_estimator_alg_t: 0 AVERAGE, 1 INTERPOLATE
 };
 
 hipError_t ofdm_launch_rx(const OfdmArgs& a, uint32_t njobs, hipStream_t s);

@@ -205,7 +205,8 @@ static int chest_check_cfg(const mi355_chest_dl_cfg_t* cfg)
 {
   if (!cfg) return MI355_ERROR_INVALID_INPUTS;
   // supported: AVERAGE estimator, REFS noise, no CFO / sync-error correction (the srsUE and phy_dl_test setup)
-  if (cfg->estimator_alg != MI355_ESTIMATOR_ALG_AVERAGE || cfg->noise_alg != MI355_NOISE_ALG_REFS ||
+  if ((cfg->estimator_alg != MI355_ESTIMATOR_ALG_AVERAGE && cfg->estimator_alg != MI355_ESTIMATOR_ALG_INTERPOLATE) ||
+      cfg->noise_alg != MI355_NOISE_ALG_REFS ||
       cfg->cfo_estimate_enable || cfg->sync_error_enable || cfg->filter_type > MI355_CHEST_FILTER_NONE)
     return MI355_ERROR;
   return MI355_SUCCESS;
@@ -249,6 +250,7 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
   ca.cell_id     = q->cell.id;
   ca.nsymb       = q->cell.cp == MI355_CP_EXT ? 6 : 7;
   ca.filter_type = cfg->filter_type;
+  ca.alg         = cfg->estimator_alg;
   ca.coef0       = cfg->filter_coef[0];
   ca.coef1       = cfg->filter_coef[1];
   CHECK_HIP(chest_launch(ca, (uint32_t)ncj, s));
@@ -437,8 +439,9 @@ int mi355_ue_dl_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, co
   ChestFill fill{q, chest_cfg, nullptr, njobs, chest, false};
   if ((r = chest_finish_async(q, &fill, d_out, s))) return r;
   const auto t1 = now();
+  // the AVERAGE estimator writes the same estimate into every OFDM symbol: the equaliser may read row 0 only
   r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), njobs, res, s, d_noise, WaitHook{chest_fill_cb, &fill},
-                                   true);
+                                   chest_cfg->estimator_alg == MI355_ESTIMATOR_ALG_AVERAGE);
   const auto t2 = now();
   CHECK_HIP(hipStreamSynchronize(q->side));
   if (r) return r;
@@ -618,7 +621,8 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   std::vector<mi355_pdsch_res_t> sub(2 * jobs.size());
   for (size_t k = 0; k < jobs.size(); k++) sub[2 * k] = res[2 * which[k]], sub[2 * k + 1] = res[2 * which[k] + 1];
   r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), (uint32_t)jobs.size(), sub.data(), s,
-                                   all ? d_noise : nullptr, all ? WaitHook{chest_fill_cb, &fill} : WaitHook{}, true);
+                                   all ? d_noise : nullptr, all ? WaitHook{chest_fill_cb, &fill} : WaitHook{},
+                                   chest_cfg->estimator_alg == MI355_ESTIMATOR_ALG_AVERAGE);
   if (all) {
     CHECK_HIP(hipStreamSynchronize(q->side));
     if (!fill.done) chest_fill_cb(&fill);

@@ -184,3 +184,68 @@ def test_fused_decode_matches_two_step(k):
     assert outs[0][1] == outs[1][1]
     for a, b in zip(outs[0][2], outs[1][2]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("k", range(len(CHEST)))
+def test_chest_interpolate_matches_oracle(k):
+    """srslte_chest_dl_estimate with SRSLTE_ESTIMATOR_ALG_INTERPOLATE (chest_dl.c:430-531): per-symbol smoothing,
+    frequency interpolation of each pilot symbol, linear time interpolation (ports 0/1); ports 2/3 reproduce the
+    reference copying the never-written row 0 of the estimate buffer over the others (random initial content)."""
+    nof_prb, ports, cid, nrx, sf, ft, coef = CHEST[k]
+    rng = np.random.default_rng(400 + k)
+    G = 14 * 12 * nof_prb
+    nre = 12 * nof_prb
+    tx = np.zeros((ports, G), np.complex64)
+    uc.crs_put(tx, nof_prb, cid, ports, sf)
+    h = uc.channel_freq(rng, ports, nrx, nof_prb)
+    grids = np.zeros((nrx, G), np.complex64)
+    for r in range(nrx):
+        # a time-varying channel: the estimate rows differ
+        tv = (1 + 0.05 * np.arange(14))[:, None]
+        y = sum(tx[p].reshape(14, nre) * h[p, r][None, :] * tv for p in range(ports))
+        y = y + 0.02 * (rng.standard_normal(y.shape) + 1j * rng.standard_normal(y.shape))
+        grids[r] = y.reshape(-1)
+    init = (rng.standard_normal((ports, nrx, G)) + 1j * rng.standard_normal((ports, nrx, G))).astype(np.complex64)
+    ce_o, res_o = uc.chest_estimate(grids, nof_prb, ports, cid, sf, ft, coef, alg=1, ce_init=init)
+    ue = UeDl(P.make_cell(nof_prb, ports, cid), nrx)
+    gb = [DeviceBuffer(G * 8).upload(grids[r]) for r in range(nrx)]
+    cb = [[DeviceBuffer(G * 8).upload(init[p, r]) for r in range(nrx)] for p in range(ports)]
+    j = DlSfJob()
+    j.tti = sf
+    for r in range(nrx):
+        j.sf_symbols[r] = gb[r].ptr
+        for p in range(ports):
+            j.ce[p][r] = cb[p][r].ptr
+    cfg = default_chest_cfg(ft, coef)
+    cfg.estimator_alg = 1
+    res = ue.chest([j], cfg)[0]
+    for p in range(ports):
+        for r in range(nrx):
+            got = cb[p][r].download(np.zeros(G, np.complex64))
+            rms = np.sqrt(np.mean(np.abs(ce_o[p, r]) ** 2))
+            err = np.abs(got - ce_o[p, r]).max() / rms
+            assert err < 2e-5, (k, p, r, err)
+            if ports == 4 and p >= 2:
+                assert np.array_equal(got.reshape(14, nre)[5], init[p, r][:nre])
+    assert abs(res.noise_estimate - res_o["noise_estimate"]) <= 1e-3 * res_o["noise_estimate"]
+    assert abs(res.rsrp - res_o["rsrp"]) <= 1e-4 * res_o["rsrp"]
+
+
+def test_ue_dl_decode_interpolate():
+    """mi355_ue_dl_decode_batch with the INTERPOLATE estimator on a time-varying channel (no fused equaliser: the
+    estimate rows differ): every TB decodes with its payload."""
+    from srsran_amd.dlsch import SoftbufferPool
+    rng = np.random.default_rng(91)
+    for k, cfg in enumerate([E2E[0], E2E[1], E2E[3]]):
+        # 40 dB: per-symbol estimates are not averaged over the 4 pilot symbols, and QAM256 at 32 dB on this
+        # channel fails the CRC in the oracle chain with either estimator
+        iq, payload, _h, _s2 = uc.synth_iq(cfg, rng, snr_db=40, max_delay=3)
+        ue = UeDl(cell_of(cfg), cfg.nof_rx)
+        ds = DevIqSubframe(cfg, iq)
+        ccfg = default_chest_cfg()
+        ccfg.estimator_alg = 1
+        pool = SoftbufferPool(2, max_cb=32)
+        _, res = ue.decode(pool, [ds.sfjob], [ds.job.sf], [ds.job.cfg], ccfg, [ds.job.payload[0], ds.job.payload[1]])
+        for t in range(cfg.nof_tb):
+            assert res[t].ret == 0 and res[t].crc, (k, t)
+            np.testing.assert_array_equal(ds.payload_bytes(t)[: cfg.tbs[t] // 8], payload[t])
