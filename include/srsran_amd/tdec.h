@@ -103,6 +103,27 @@ int   mi355_memset_dev(void* dst, int value, size_t bytes);
 int   mi355_device_sync(void);
 int   mi355_device_count(void);
 
+/* ------------------------------------------------------------------------------------------------ 8-bit path
+ * srslte_tdec_run_all_8bit / srslte_tdec_iteration_8bit (turbodecoder.c:552-575) in AUTO mode for a batch of code
+ * blocks of one K that has an 8-bit window decoder in the AVX2 build: 32 windows for K % 32 == 0 && K > 2048,
+ * 16 for K % 16 == 0 && K > 800 (srslte_tdec_autoimp_get_subblocks_8bit).  (The reference runs the other K on a
+ * 16-bit decoder over a conversion of only the first 3K+12 input bytes, which for 400 < K <= 800 leaves the
+ * windowed layout's tail region unconverted; those K are rejected here.)  in: device buffers in the layout
+ * srslte_rm_turbo_rx_lut_8bit writes ([syst K | 32 | p0 K | 32 | p1 K | 32 | 12 tails], window-ordered),
+ * in_stride bytes apart, MUTATED (tails copied into the pads, as the reference does); out: decision bytes after
+ * the last half-iteration; trace (optional, device): ncb x nhalf x K/8 decision bytes after every half-iteration.
+ * stream NULL: synchronous on the decoder's own stream. */
+typedef struct mi355_tdec8 mi355_tdec8_t;
+int      mi355_tdec8_create(mi355_tdec8_t** q, int device);
+void     mi355_tdec8_destroy(mi355_tdec8_t* q);
+uint32_t mi355_tdec_autoimp_get_subblocks_8bit(uint32_t long_cb);
+int      mi355_tdec8_run_dev(mi355_tdec8_t* q, int8_t* in, size_t in_stride, uint32_t ncb, uint32_t K, uint32_t nhalf,
+                             uint8_t* out, size_t out_stride, uint8_t* trace, void* stream);
+/* srslte_rm_turbo_rx_lut_8bit (rm_turbo.c:456-495) for ncb code blocks of one (K, rv): out[deinter[i % N]] += e[i],
+ * wrapping int8 (HARQ combining), in the 8-bit decoder layout of K. */
+int mi355_rm_turbo_rx_8bit_dev(mi355_tdec8_t* q, const int8_t* e, size_t e_stride, uint32_t E, int8_t* out,
+                               size_t out_stride, uint32_t ncb, uint32_t K, uint32_t rv, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

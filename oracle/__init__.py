@@ -97,6 +97,12 @@ def ref() -> C.CDLL:
         L.ref_crc_byte.argtypes = [C.c_uint32, C.c_int, u8p, C.c_int]
         L.ref_cbsegm.argtypes = [C.c_uint32, u32p]
         L.ref_rm_turbo_rx.argtypes = [i16p, C.c_uint32, i16p, C.c_uint32, C.c_uint32]
+        i8p = np.ctypeslib.ndpointer(np.int8, flags="C_CONTIGUOUS")
+        L.ref_tdec8_new.restype = C.c_void_p
+        L.ref_tdec8_new.argtypes = [C.c_uint32]
+        L.ref_tdec8_free.argtypes = [C.c_void_p]
+        L.ref_tdec8_run.argtypes = [C.c_void_p, i8p, C.c_uint32, C.c_uint32, u8p, C.c_void_p]
+        L.ref_rm_turbo_rx_8bit.argtypes = [i8p, C.c_uint32, i8p, C.c_uint32, C.c_uint32]
         L.ref_tdec_run_batch.argtypes = [i16p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u8p, C.c_int]
         L.ref_demod_soft_s.argtypes = [C.c_int, f32p, i16p, C.c_int]
         L.ref_scramble_s.argtypes = [C.c_uint32, i16p, C.c_int, C.c_int]

@@ -57,6 +57,29 @@ static srslte_tdec_16bit_impl_t ref_avx16_impl = {tdec_winavx16_init,
 #include "srslte/phy/fec/turbodecoder_iter.h"
 #undef LLR_IS_16BIT
 
+/* the 8-bit window decoders of the AVX2 build (turbodecoder.c:81-97) and the 8-bit iteration template */
+#define WINIMP_IS_SSE8
+#include "srslte/phy/fec/turbodecoder_win.h"
+#undef WINIMP_IS_SSE8
+static srslte_tdec_8bit_impl_t ref_sse8_impl = {tdec_winsse8_init,
+                                                tdec_winsse8_free,
+                                                tdec_winsse8_dec,
+                                                tdec_winsse8_extract_input,
+                                                tdec_winsse8_decision_byte};
+
+#define WINIMP_IS_AVX8
+#include "srslte/phy/fec/turbodecoder_win.h"
+#undef WINIMP_IS_AVX8
+static srslte_tdec_8bit_impl_t ref_avx8_impl = {tdec_winavx8_init,
+                                                tdec_winavx8_free,
+                                                tdec_winavx8_dec,
+                                                tdec_winavx8_extract_input,
+                                                tdec_winavx8_decision_byte};
+
+#define LLR_IS_8BIT
+#include "srslte/phy/fec/turbodecoder_iter.h"
+#undef LLR_IS_8BIT
+
 /* indices in dec16[] as in turbodecoder.c:112-118 (AVX2 build) */
 #define H_GEN 0
 #define H_SSEWIN 1
@@ -154,6 +177,97 @@ int ref_tdec_run(void* hh, int16_t* buf, uint32_t K, uint32_t nhalf, uint8_t* ou
   memcpy(buf, abuf, blen * sizeof(int16_t));
   free(abuf);
   return 0;
+}
+
+/* --------------------------------------------------------------- 8-bit decoder */
+/* srslte_tdec_iteration_8bit / run_all_8bit in AUTO mode for the K that have an 8-bit window decoder
+ * (turbodecoder.c:410-440: 32 windows for K % 32 == 0 && K > 2048, 16 for K % 16 == 0 && K > 800); the other
+ * K fall back to a 16-bit decoder on converted input (:458-483) and are not covered here (-2). */
+#define H8_SSEWIN 0
+#define H8_AVXWIN 1
+
+void* ref_tdec8_new(uint32_t max_K)
+{
+  srslte_tdec_t* h    = calloc(1, sizeof(srslte_tdec_t));
+  uint32_t       len  = max_K + SRSLTE_TCOD_TOTALTAIL;
+  h->max_long_cb      = max_K;
+  h->dec_type         = SRSLTE_TDEC_AUTO;
+  h->current_llr_type = SRSLTE_TDEC_8;
+  h->app1             = srslte_vec_i16_malloc(len);
+  h->app2             = srslte_vec_i16_malloc(len);
+  h->ext1             = srslte_vec_i16_malloc(len);
+  h->ext2             = srslte_vec_i16_malloc(len);
+  h->syst0            = srslte_vec_i16_malloc(len);
+  h->parity0          = srslte_vec_i16_malloc(len);
+  h->parity1          = srslte_vec_i16_malloc(len);
+  h->input_conv       = srslte_vec_i16_malloc(len * 3 + 32 * 3);
+  h->dec8[H8_SSEWIN]  = &ref_sse8_impl;
+  h->dec8[H8_AVXWIN]  = &ref_avx8_impl;
+  for (int td = 0; td < 2; td++) h->nof_blocks8[td] = h->dec8[td]->tdec_init(&h->dec8_hdlr[td], max_K);
+  for (int s = 0; s < 4; s++) {
+    for (int i = 0; i < SRSLTE_NOF_TC_CB_SIZES; i++) {
+      srslte_tc_interl_init(&h->interleaver[s][i], srslte_cbsegm_cbsize(i));
+      srslte_tc_interl_LTE_gen_interl(&h->interleaver[s][i], srslte_cbsegm_cbsize(i), s ? (8 << (s - 1)) : 1);
+    }
+  }
+  h->current_cbidx = -1;
+  return h;
+}
+
+void ref_tdec8_free(void* hh)
+{
+  srslte_tdec_t* h = hh;
+  free(h->app1); free(h->app2); free(h->ext1); free(h->ext2);
+  free(h->syst0); free(h->parity0); free(h->parity1); free(h->input_conv);
+  for (int td = 0; td < 2; td++) h->dec8[td]->tdec_free(h->dec8_hdlr[td]);
+  for (int s = 0; s < 4; s++)
+    for (int i = 0; i < SRSLTE_NOF_TC_CB_SIZES; i++) srslte_tc_interl_free(&h->interleaver[s][i]);
+  free(h);
+}
+
+/* buf: the 8-bit sub-block layout [syst K | 32 | p0 K | 32 | p1 K | 32 | 12 tails] (what rm_turbo_rx_lut_8bit
+ * writes); decision bytes after every half-iteration into trace (nhalf x K/8) when non-NULL. */
+int ref_tdec8_run(void* hh, int8_t* buf, uint32_t K, uint32_t nhalf, uint8_t* out, uint8_t* trace)
+{
+  srslte_tdec_t* h = hh;
+  if (K > h->max_long_cb) return -1;
+  uint32_t nsb = 0;
+  if (K % 32 == 0 && K > 2048) {
+    h->current_dec = H8_AVXWIN;
+    nsb            = 32;
+  } else if (K % 16 == 0 && K > 800) {
+    h->current_dec = H8_SSEWIN;
+    nsb            = 16;
+  } else {
+    return -2;
+  }
+  h->n_iter            = 0;
+  h->current_long_cb   = K;
+  h->current_cbidx     = srslte_cbsegm_cbindex(K);
+  h->current_llr_type  = SRSLTE_TDEC_8;
+  h->current_inter_idx = inter_idx((int)nsb);
+  if (h->current_cbidx < 0) return -1;
+  uint32_t blen = 3 * (K + 32) + 12;
+  int8_t*  abuf = srslte_vec_malloc(blen + 64);
+  memcpy(abuf, buf, blen);
+  do {
+    run_tdec_iteration_8bit(h, abuf);
+    if (trace) {
+      h->dec8[h->current_dec]->tdec_decision_byte(!(h->n_iter % 2) ? (int8_t*)h->app1 : (int8_t*)h->ext1,
+                                                  &trace[(size_t)(h->n_iter - 1) * (K / 8)], K);
+    }
+  } while ((uint32_t)h->n_iter < nhalf);
+  h->dec8[h->current_dec]->tdec_decision_byte(!(h->n_iter % 2) ? (int8_t*)h->app1 : (int8_t*)h->ext1, out, K);
+  memcpy(buf, abuf, blen);
+  free(abuf);
+  return 0;
+}
+
+/* rate dematching into the 8-bit decoder buffer (srslte_rm_turbo_rx_lut_8bit, rm_turbo.c:456-495) */
+int ref_rm_turbo_rx_8bit(int8_t* in, uint32_t in_len, int8_t* out, uint32_t K, uint32_t rv)
+{
+  srslte_rm_turbo_gentables();
+  return srslte_rm_turbo_rx_lut_8bit(in, out, in_len, srslte_cbsegm_cbindex(K), rv);
 }
 
 /* --------------------------------------------------------------- extra stages */

@@ -29,7 +29,19 @@ inline int lte_cb_index_eq(uint32_t K)
   return -1;
 }
 
-inline std::vector<uint16_t> rm_rx_table(uint32_t K, uint32_t rv)
+// srslte_tdec_autoimp_get_subblocks_8bit (turbodecoder.c:410-424, AVX2 build): the 8-bit decoder buffer layout
+inline uint32_t tdec_subblocks_8bit(uint32_t K)
+{
+  if (!(K % 32) && K > 2048) return 32;
+  return tdec_subblocks(K);
+}
+
+std::vector<uint16_t> rm_rx_table_nsb(uint32_t K, uint32_t rv, uint32_t nsb);
+
+inline std::vector<uint16_t> rm_rx_table(uint32_t K, uint32_t rv) { return rm_rx_table_nsb(K, rv, tdec_subblocks(K)); }
+
+// the table for an explicit sub-block count (0: linear layout)
+inline std::vector<uint16_t> rm_rx_table_nsb(uint32_t K, uint32_t rv, uint32_t nsb)
 {
   static const int NC = 32;
   auto             colperm = [](int c) { // 5-bit bit reversal = 36.212 Table 5.1.4-1 (an involution)
@@ -38,8 +50,7 @@ inline std::vector<uint16_t> rm_rx_table(uint32_t K, uint32_t rv)
   const int D = (int)K + 4, R = (D + NC - 1) / NC, KP = R * NC, ND = KP - D, Ncb = 3 * KP;
   const int k0 = R * (2 * (int)ceilf((float)Ncb / (float)(8 * R)) * (int)rv + 2);
   std::vector<uint16_t> t(3 * (size_t)D);
-  const uint32_t        nsb = tdec_subblocks(K);
-  const uint32_t        L   = nsb ? K / nsb : 0;
+  const uint32_t        L = nsb ? K / nsb : 0;
   int                   k = 0;
   for (int j = 0; k < 3 * D; j++) {
     const int p = (k0 + j) % Ncb;

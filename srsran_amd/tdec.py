@@ -96,3 +96,40 @@ class TdecBatch:
             self.close()
         except Exception:
             pass
+
+
+class Tdec8Batch:
+    """The 8-bit turbo decoder and 8-bit rate dematching on one device (include/srsran_amd/tdec.h mi355_tdec8_*)."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        if not getattr(L, "_tdec8_declared", False):
+            vp, u32, sz = C.c_void_p, C.c_uint32, C.c_size_t
+            L.mi355_tdec8_create.argtypes = [C.POINTER(vp), C.c_int]
+            L.mi355_tdec8_destroy.argtypes = [vp]
+            L.mi355_tdec_autoimp_get_subblocks_8bit.restype = u32
+            L.mi355_tdec_autoimp_get_subblocks_8bit.argtypes = [u32]
+            L.mi355_tdec8_run_dev.argtypes = [vp, vp, sz, u32, u32, u32, vp, sz, vp, vp]
+            L.mi355_rm_turbo_rx_8bit_dev.argtypes = [vp, vp, sz, u32, vp, sz, u32, u32, u32, vp]
+            L._tdec8_declared = True
+        h = C.c_void_p()
+        check(L.mi355_tdec8_create(C.byref(h), device), "mi355_tdec8_create")
+        self.L, self.h = L, h
+
+    def run_dev(self, d_in: int, in_stride: int, ncb: int, K: int, nhalf: int, d_out: int, out_stride: int,
+                d_trace: int | None = None) -> int:
+        return self.L.mi355_tdec8_run_dev(self.h, d_in, in_stride, ncb, K, nhalf, d_out, out_stride, d_trace, None)
+
+    def rm_rx_dev(self, d_e: int, e_stride: int, E: int, d_out: int, out_stride: int, ncb: int, K: int, rv: int) -> int:
+        return self.L.mi355_rm_turbo_rx_8bit_dev(self.h, d_e, e_stride, E, d_out, out_stride, ncb, K, rv, None)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.mi355_tdec8_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

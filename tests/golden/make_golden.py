@@ -9,6 +9,10 @@ Contents
   tdec_auto.npz      AUTO-mode decoder (generic / 8-window / 16-window by K): inputs in the softbuffer
                      layout, decision bytes after every half-iteration 1..8 (srslte_tdec_iteration),
                      including failing code blocks, saturating and full-range int16 inputs.
+  tdec8.npz          the 8-bit AUTO decoder (srslte_tdec_iteration_8bit: 32-window AVX8 for K % 32 == 0 && K > 2048,
+                     16-window SSE8 for K % 16 == 0 && K > 800) on int8 inputs in the 8-bit sub-block layout,
+                     decision bytes after every half-iteration 1..8, incl. saturating and full-range int8 inputs;
+                     plus srslte_rm_turbo_rx_lut_8bit (E below / at / above the circular buffer, every rv, HARQ).
   tdec_generic.npz   GENERIC manual decoder + force_not_sb on linear input (turbodecoder_test -d 1).
   tcod_known.npz     the reference test's own known-answer vector (turbodecoder_test.h:69-125).
   crc_cbsegm.npz     CRC24A/24B/16/8 checksums and CB segmentation for a TBS sweep.
@@ -70,6 +74,76 @@ def gen_tdec_auto(rng):
     data["nhalf"] = np.int32(NHALF)
     np.savez_compressed(os.path.join(OUT, "tdec_auto.npz"), **data)
     print("tdec_auto.npz:", len(cases), "cases")
+
+
+def pack8(lin: np.ndarray, K: int, nsb: int) -> np.ndarray:
+    """Encoder-order LLRs (x z z' per step, 12 tails) -> the 8-bit decoder buffer: stream s at s*(K+32), step
+    w*L + j of window w at j*nsb + w, tails at 3*(K+32) in encoder order (rm_turbo_rx_lut_8bit's layout)."""
+    L = K // nsb
+    buf = np.zeros(3 * (K + 32) + 12, np.int8)
+    m = np.arange(K)
+    pos = (m % L) * nsb + m // L
+    for s in range(3):
+        buf[s * (K + 32) + pos] = lin[s: 3 * K: 3]
+    buf[3 * (K + 32):] = lin[3 * K:]
+    return buf
+
+
+def gen_tdec8(rng):
+    R = oracle.ref()
+    h = R.ref_tdec8_new(6144)
+    cases = []
+    # (K, kind, ebno, scale): awgn int8 LLRs round(scale * y) clipped to +-127; rand: uniform full-range int8
+    for K in (6144, 3072, 2112, 2048, 1024, 848):
+        cases += [(K, "awgn", 0.5, 16.0), (K, "awgn", 2.0, 16.0)]
+    cases += [(6144, "awgn", 6.0, 60.0), (1024, "awgn", 2.0, 90.0), (6144, "awgn", 10.0, 30.0), (1024, "awgn", 10.0, 30.0),
+              (2112, "awgn", 10.0, 30.0), (6144, "rand", 0.0, 0.0), (848, "rand", 0.0, 0.0)]
+    data = {}
+    for ci, (K, kind, eb, sc) in enumerate(cases):
+        nsb = 32 if (K % 32 == 0 and K > 2048) else 16
+        if kind == "rand":
+            bits = np.zeros(K, np.uint8)
+            lin = rng.integers(-128, 128, 3 * K + 12, dtype=np.int8)
+        else:
+            bits = rng.integers(0, 2, K, dtype=np.uint8)
+            enc = oracle.tcod_encode(bits, K)
+            sigma = 10 ** (-(eb + 10 * np.log10(1 / 3)) / 20)
+            y = np.where(enc.astype(bool), 1.0, -1.0) + sigma * rng.standard_normal(enc.size)
+            lin = np.clip(np.round(sc * y), -127, 127).astype(np.int8)
+        buf = pack8(lin, K, nsb)
+        out = np.zeros(K // 8, np.uint8)
+        tr = np.zeros((NHALF, K // 8), np.uint8)
+        work = buf.copy()
+        assert R.ref_tdec8_run(h, work, K, NHALF, out, tr.ctypes.data) == 0
+        data[f"c{ci}_K"] = np.int32(K)
+        data[f"c{ci}_kind"] = np.array(kind)
+        data[f"c{ci}_ebno"] = np.float32(eb)
+        data[f"c{ci}_bits"] = bits
+        data[f"c{ci}_buf"] = buf
+        data[f"c{ci}_trace"] = tr
+    R.ref_tdec8_free(h)
+    data["ncases"] = np.int32(len(cases))
+    data["nhalf"] = np.int32(NHALF)
+    # srslte_rm_turbo_rx_lut_8bit: (K, rv, E, amplitude) into a zero buffer, then a second (HARQ) accumulation
+    rm = []
+    for K in (6144, 2112, 1024, 848):
+        N = 3 * K + 12
+        for rv in range(4):
+            for E in (N // 3, N, N + N // 2 + 7):
+                rm.append((K, rv, E))
+    for ri, (K, rv, E) in enumerate(rm):
+        e1 = rng.integers(-40, 41, E, dtype=np.int8)
+        e2 = rng.integers(-128, 128, E, dtype=np.int8)
+        out = np.zeros(3 * (K + 32) + 12 + 64, np.int8)
+        assert R.ref_rm_turbo_rx_8bit(e1, E, out, K, rv) == 0
+        first = out.copy()
+        assert R.ref_rm_turbo_rx_8bit(e2, E, out, K, (rv + 2) % 4) == 0
+        data[f"rm{ri}_K"], data[f"rm{ri}_rv"], data[f"rm{ri}_E"] = np.int32(K), np.int32(rv), np.int32(E)
+        data[f"rm{ri}_e1"], data[f"rm{ri}_e2"] = e1, e2
+        data[f"rm{ri}_out1"], data[f"rm{ri}_out2"] = first[: 3 * (K + 32) + 12], out[: 3 * (K + 32) + 12]
+    data["rm_n"] = np.int32(len(rm))
+    np.savez_compressed(os.path.join(OUT, "tdec8.npz"), **data)
+    print("tdec8.npz:", len(cases), "decoder cases,", len(rm), "rate-dematching cases")
 
 
 def gen_tdec_generic(rng):
@@ -346,6 +420,9 @@ def main():
     if sys.argv[1:] == ["pdcch"]:
         gen_pdcch(np.random.default_rng(4004))
         return
+    if sys.argv[1:] == ["tdec8"]:
+        gen_tdec8(np.random.default_rng(8008))
+        return
     rng = np.random.default_rng(20201010)
     gen_tdec_auto(rng)
     gen_tdec_generic(rng)
@@ -354,6 +431,7 @@ def main():
     gen_rm(np.random.default_rng(1212))
     gen_pdsch_stages(np.random.default_rng(3003))
     gen_pdcch(np.random.default_rng(4004))
+    gen_tdec8(np.random.default_rng(8008))
 
 
 if __name__ == "__main__":

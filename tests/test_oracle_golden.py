@@ -76,3 +76,18 @@ def test_oracle_rate_dematch_harq_accumulation():
     acc = oracle.rm_turbo_rx(h["e0"], h["K"], 0)
     oracle.rm_turbo_rx(h["e2"], h["K"], 2, acc)
     np.testing.assert_array_equal(acc[: h["out"].size], h["out"])
+
+
+def test_tdec8_goldens_sane():
+    """The 8-bit reference goldens: every high-SNR case decodes its transmitted bits after 2 half-iterations (the
+    reference's 8-bit decoder is weaker than the 16-bit one and oscillates later), inputs are in the 8-bit layout."""
+    z = load("tdec8.npz")
+    hi = 0
+    for i in range(int(z["ncases"])):
+        K = int(z[f"c{i}_K"])
+        assert z[f"c{i}_buf"].dtype == np.int8 and z[f"c{i}_buf"].size == 3 * (K + 32) + 12
+        assert z[f"c{i}_trace"].shape == (int(z["nhalf"]), K // 8)
+        if float(z[f"c{i}_ebno"]) >= 10.0:
+            hi += 1
+            assert (np.unpackbits(z[f"c{i}_trace"][1]) != z[f"c{i}_bits"]).mean() < 2e-3
+    assert hi == 3
