@@ -9,7 +9,11 @@
  *     input in the layout srslte_rm_turbo_rx_lut() produces; GENERIC (+force_not_sb) takes linear input;
  *   - new_cb() fails with -1 for K > max_long_cb or K outside the 36.212 table.
  * The handle is caller-allocated and filled by init, exactly like srslte_tdec_t.  The 8-bit variants
- * (srslte_tdec_iteration_8bit / run_all_8bit) are not provided.
+ * (srslte_tdec_iteration_8bit / run_all_8bit, turbodecoder.c:552-575) run the 8-bit window decoders for
+ * K % 16 == 0 && K > 800 (32 windows when K % 32 == 0 && K > 2048) and, for K <= 400, the 16-bit generic decoder
+ * on the converted linear input as the reference does; for the remaining K the reference decodes a partly
+ * unconverted buffer (turbodecoder.c:497-503 converts only 3K+12 of the windowed layout) and these return
+ * without output (run_all_8bit: -1).
  */
 #ifndef SRSRAN_AMD_SRSLTE_TDEC_H
 #define SRSRAN_AMD_SRSLTE_TDEC_H
@@ -42,6 +46,9 @@ uint32_t mi355_srslte_tdec_autoimp_get_subblocks_8bit(uint32_t long_cb);
 void     mi355_srslte_tdec_iteration(mi355_srslte_tdec_t* h, int16_t* input, uint8_t* output);
 int mi355_srslte_tdec_run_all(mi355_srslte_tdec_t* h, int16_t* input, uint8_t* output, uint32_t nof_iterations,
                               uint32_t long_cb);
+void mi355_srslte_tdec_iteration_8bit(mi355_srslte_tdec_t* h, int8_t* input, uint8_t* output);
+int  mi355_srslte_tdec_run_all_8bit(mi355_srslte_tdec_t* h, int8_t* input, uint8_t* output, uint32_t nof_iterations,
+                                    uint32_t long_cb);
 
 #ifdef __cplusplus
 }

@@ -119,6 +119,10 @@ void     mi355_tdec8_destroy(mi355_tdec8_t* q);
 uint32_t mi355_tdec_autoimp_get_subblocks_8bit(uint32_t long_cb);
 int      mi355_tdec8_run_dev(mi355_tdec8_t* q, int8_t* in, size_t in_stride, uint32_t ncb, uint32_t K, uint32_t nhalf,
                              uint8_t* out, size_t out_stride, uint8_t* trace, void* stream);
+/* one half-iteration n of the same batch (srslte_tdec_iteration_8bit: n = 0 starts a new code block batch, later n
+ * continue it from the decoder's workspace); decision bytes after it into out. */
+int      mi355_tdec8_halfit_dev(mi355_tdec8_t* q, int8_t* in, size_t in_stride, uint32_t ncb, uint32_t K, uint32_t n,
+                                uint8_t* out, size_t out_stride, void* stream);
 /* srslte_rm_turbo_rx_lut_8bit (rm_turbo.c:456-495) for ncb code blocks of one (K, rv): out[deinter[i % N]] += e[i],
  * wrapping int8 (HARQ combining), in the 8-bit decoder layout of K. */
 int mi355_rm_turbo_rx_8bit_dev(mi355_tdec8_t* q, const int8_t* e, size_t e_stride, uint32_t E, int8_t* out,

@@ -15,6 +15,8 @@ struct CompatState {
   int16_t*            din  = nullptr;
   uint8_t*            dout = nullptr;
   size_t              stride;
+  mi355_tdec8_t*      dec8 = nullptr; // 8-bit decoder, created on first use
+  int8_t*             din8 = nullptr;
 };
 
 int cb_index(uint32_t K)
@@ -70,8 +72,10 @@ void mi355_srslte_tdec_free(mi355_srslte_tdec_t* h)
   if (!h || !h->impl) return;
   auto* st = (CompatState*)h->impl;
   mi355_tdec_batch_destroy(st->dec);
+  if (st->dec8) mi355_tdec8_destroy(st->dec8);
   (void)hipFree(st->din);
   (void)hipFree(st->dout);
+  if (st->din8) (void)hipFree(st->din8);
   delete st;
   memset(h, 0, sizeof(*h));
 }
@@ -144,6 +148,45 @@ int mi355_srslte_tdec_run_all(mi355_srslte_tdec_t* h, int16_t* input, uint8_t* o
   (void)hipDeviceSynchronize();
   if (hipMemcpy(output, st->dout, long_cb / 8, hipMemcpyDeviceToHost) != hipSuccess) return MI355_ERROR;
   h->n_iter = (int)nit;
+  return MI355_SUCCESS;
+}
+
+// turbodecoder.c:458-483, 552-575: K with an 8-bit window decoder run it; K <= 400 run the 16-bit generic decoder
+// on the int8 input converted to int16 (the linear layout, fully converted)
+static bool has_win8(uint32_t K) { return mi355_tdec_autoimp_get_subblocks_8bit(K) >= 16; }
+
+void mi355_srslte_tdec_iteration_8bit(mi355_srslte_tdec_t* h, int8_t* input, uint8_t* output)
+{
+  if (!h || !h->impl || h->current_cbidx < 0 || !input || !output) return;
+  auto*          st = (CompatState*)h->impl;
+  const uint32_t K  = h->current_long_cb;
+  if (has_win8(K)) {
+    if (!st->dec8 && mi355_tdec8_create(&st->dec8, current_device()) != MI355_SUCCESS) return;
+    if (!st->din8 && hipMalloc(&st->din8, st->stride) != hipSuccess) return;
+    const size_t len = 3 * (size_t)(K + 32) + 12;
+    if (h->n_iter == 0 && hipMemcpy(st->din8, input, len, hipMemcpyHostToDevice) != hipSuccess) return;
+    if (mi355_tdec8_halfit_dev(st->dec8, st->din8, st->stride, 1, K, (uint32_t)h->n_iter, st->dout, K / 8, nullptr))
+      return;
+    if (h->n_iter == 0) (void)hipMemcpy(input, st->din8, len, hipMemcpyDeviceToHost); // tails in the pads, as the reference
+    if (hipMemcpy(output, st->dout, K / 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    h->n_iter++;
+  } else if (mi355_tdec_autoimp_get_subblocks(K) == 0) {
+    int16_t conv[3 * 400 + 12];
+    for (uint32_t i = 0; i < 3 * K + 12; i++) conv[i] = input[i];
+    mi355_srslte_tdec_iteration(h, conv, output);
+  }
+}
+
+int mi355_srslte_tdec_run_all_8bit(mi355_srslte_tdec_t* h, int8_t* input, uint8_t* output, uint32_t nof_iterations,
+                                   uint32_t long_cb)
+{
+  if (mi355_srslte_tdec_new_cb(h, long_cb)) return MI355_ERROR;
+  if (!has_win8(long_cb) && mi355_tdec_autoimp_get_subblocks(long_cb) != 0) return MI355_ERROR;
+  do {
+    const int before = h->n_iter;
+    mi355_srslte_tdec_iteration_8bit(h, input, output);
+    if (h->n_iter == before) return MI355_ERROR;
+  } while ((uint32_t)h->n_iter < nof_iterations);
   return MI355_SUCCESS;
 }
 

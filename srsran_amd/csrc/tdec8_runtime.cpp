@@ -95,23 +95,24 @@ void mi355_tdec8_destroy(mi355_tdec8_t* q)
   delete q;
 }
 
-int mi355_tdec8_run_dev(mi355_tdec8_t* q, int8_t* in, size_t in_stride, uint32_t ncb, uint32_t K, uint32_t nhalf,
-                        uint8_t* out, size_t out_stride, uint8_t* trace, void* stream)
+int mi355_tdec8_halfit_dev(mi355_tdec8_t* q, int8_t* in, size_t in_stride, uint32_t ncb, uint32_t K, uint32_t n,
+                           uint8_t* out, size_t out_stride, void* stream)
 {
-  if (!q || (ncb && (!in || !out)) || nhalf == 0) return MI355_ERROR_INVALID_INPUTS;
+  if (!q || (ncb && (!in || !out))) return MI355_ERROR_INVALID_INPUTS;
   const uint32_t NB = tdec_subblocks_8bit(K);
   if (NB != 16 && NB != 32) return MI355_ERROR_INVALID_INPUTS; // the 8-bit window decoders only (see tdec.h)
   if (in_stride < 3 * (size_t)(K + 32) + 12 || out_stride < K / 8) return MI355_ERROR_INVALID_INPUTS;
   if (!ncb) return MI355_SUCCESS;
   std::lock_guard<std::mutex> lk(q->mu);
   CHECK_HIP(hipSetDevice(q->device));
-  hipStream_t     s = stream ? (hipStream_t)stream : q->own;
+  hipStream_t     s   = stream ? (hipStream_t)stream : q->own;
   const uint16_t* tab = nullptr;
   int             r   = get_interl(q, K, NB, &tab);
   if (r) return r;
   const uint32_t L         = K / NB;
   const size_t   ws_stride = (4 * (size_t)(K + 32) + 8 * (size_t)(L + 1) * NB + 255) / 256 * 256;
   if (ws_stride * ncb > q->ws_cap) {
+    if (n) return MI355_ERROR_INVALID_INPUTS; // a later half-iteration of a batch that was never started
     if (q->ws) {
       CHECK_HIP(hipDeviceSynchronize());
       CHECK_HIP(hipFree(q->ws));
@@ -122,25 +123,38 @@ int mi355_tdec8_run_dev(mi355_tdec8_t* q, int8_t* in, size_t in_stride, uint32_t
   }
   Tdec8MapArgs a{};
   a.in = in, a.in_stride = in_stride, a.ws = q->ws, a.ws_stride = ws_stride, a.K = K, a.NB = NB, a.L = L, a.ncb = ncb;
+  int src;
+  if (n == 0) CHECK_HIP(tdec8_launch_tails(in, in_stride, q->ws, ws_stride, K, ncb, s));
+  if (n % 2 == 0) { // DEC1 with the a-priori app1 - ext1 from n = 2 on
+    if (n) CHECK_HIP(tdec8_launch_sub(q->ws, ws_stride, K, ncb, T8_APP1, T8_EXT1, s));
+    a.dec2 = 0, a.has_app = n > 0;
+    CHECK_HIP(tdec8_launch_map(a, s));
+    src = T8_EXT1;
+  } else { // DEC2 on the deinterleaved extrinsic of DEC1
+    if (n > 1) CHECK_HIP(tdec8_launch_sub(q->ws, ws_stride, K, ncb, T8_EXT1, T8_APP1, s));
+    CHECK_HIP(tdec8_launch_lut(q->ws, ws_stride, K, ncb, T8_EXT1, T8_APP2, tab + K, s));
+    a.dec2 = 1, a.has_app = 0;
+    CHECK_HIP(tdec8_launch_map(a, s));
+    CHECK_HIP(tdec8_launch_lut(q->ws, ws_stride, K, ncb, T8_EXT2, T8_APP1, tab, s));
+    src = T8_APP1;
+  }
+  CHECK_HIP(tdec8_launch_decide(q->ws, ws_stride, K, NB, ncb, src, out, out_stride, s));
+  if (!stream) CHECK_HIP(hipStreamSynchronize(s));
+  return MI355_SUCCESS;
+}
+
+int mi355_tdec8_run_dev(mi355_tdec8_t* q, int8_t* in, size_t in_stride, uint32_t ncb, uint32_t K, uint32_t nhalf,
+                        uint8_t* out, size_t out_stride, uint8_t* trace, void* stream)
+{
+  if (!q || nhalf == 0) return MI355_ERROR_INVALID_INPUTS;
+  hipStream_t  s  = stream ? (hipStream_t)stream : q->own;
   const size_t KB = K / 8;
   for (uint32_t n = 0; n < nhalf; n++) {
-    if (n == 0) CHECK_HIP(tdec8_launch_tails(in, in_stride, q->ws, ws_stride, K, ncb, s));
-    int src;
-    if (n % 2 == 0) { // DEC1 with the a-priori app1 - ext1 from n = 2 on
-      if (n) CHECK_HIP(tdec8_launch_sub(q->ws, ws_stride, K, ncb, T8_APP1, T8_EXT1, s));
-      a.dec2 = 0, a.has_app = n > 0;
-      CHECK_HIP(tdec8_launch_map(a, s));
-      src = T8_EXT1;
-    } else { // DEC2 on the deinterleaved extrinsic of DEC1
-      if (n > 1) CHECK_HIP(tdec8_launch_sub(q->ws, ws_stride, K, ncb, T8_EXT1, T8_APP1, s));
-      CHECK_HIP(tdec8_launch_lut(q->ws, ws_stride, K, ncb, T8_EXT1, T8_APP2, tab + K, s));
-      a.dec2 = 1, a.has_app = 0;
-      CHECK_HIP(tdec8_launch_map(a, s));
-      CHECK_HIP(tdec8_launch_lut(q->ws, ws_stride, K, ncb, T8_EXT2, T8_APP1, tab, s));
-      src = T8_APP1;
-    }
-    if (trace) CHECK_HIP(tdec8_launch_decide(q->ws, ws_stride, K, NB, ncb, src, trace + n * KB, nhalf * KB, s));
-    if (n + 1 == nhalf) CHECK_HIP(tdec8_launch_decide(q->ws, ws_stride, K, NB, ncb, src, out, out_stride, s));
+    uint8_t* o  = trace ? trace + n * KB : out;
+    size_t   os = trace ? nhalf * KB : out_stride;
+    int      r  = mi355_tdec8_halfit_dev(q, in, in_stride, ncb, K, n, o, os, s);
+    if (r) return r;
+    if (trace && n + 1 == nhalf) CHECK_HIP(hipMemcpy2DAsync(out, out_stride, o, os, KB, ncb, hipMemcpyDeviceToDevice, s));
   }
   if (!stream) CHECK_HIP(hipStreamSynchronize(s));
   return MI355_SUCCESS;

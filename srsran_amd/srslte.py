@@ -37,6 +37,8 @@ def _declare():
     L.mi355_srslte_tdec_autoimp_get_subblocks_8bit.argtypes = [C.c_uint32]
     L.mi355_srslte_tdec_iteration.argtypes = [P, C.c_void_p, C.c_void_p]
     L.mi355_srslte_tdec_run_all.argtypes = [P, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32]
+    L.mi355_srslte_tdec_iteration_8bit.argtypes = [P, C.c_void_p, C.c_void_p]
+    L.mi355_srslte_tdec_run_all_8bit.argtypes = [P, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32]
     L._srslte_declared = True
     return L
 
@@ -70,6 +72,21 @@ class SrslteTdec:
         rc = self.L.mi355_srslte_tdec_run_all(C.byref(self.h), buf.ctypes.data, out.ctypes.data, nof_iterations, K)
         if rc != 0:
             raise RuntimeError(f"srslte_tdec_run_all failed ({rc})")
+        return out
+
+    def iteration_8bit(self, buf: np.ndarray) -> np.ndarray:
+        """srslte_tdec_iteration_8bit; buf (int8, the 8-bit decoder layout) receives the tails as in the reference."""
+        assert buf.dtype == np.int8 and buf.flags.c_contiguous
+        out = np.zeros(self.h.current_long_cb // 8, np.uint8)
+        self.L.mi355_srslte_tdec_iteration_8bit(C.byref(self.h), buf.ctypes.data, out.ctypes.data)
+        return out
+
+    def run_all_8bit(self, buf: np.ndarray, nof_iterations: int, K: int) -> np.ndarray:
+        assert buf.dtype == np.int8 and buf.flags.c_contiguous
+        out = np.zeros(K // 8, np.uint8)
+        rc = self.L.mi355_srslte_tdec_run_all_8bit(C.byref(self.h), buf.ctypes.data, out.ctypes.data, nof_iterations, K)
+        if rc != 0:
+            raise RuntimeError(f"srslte_tdec_run_all_8bit failed ({rc})")
         return out
 
     @property
