@@ -76,6 +76,16 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
                            float*                   avg_iterations,
                            void*                    stream);
 
+/* srsUE's pdsch_8bit_decoder mode (cc_worker.cc:98-101 -> sch.c:403-423 with llr_is_8bit): the same decode from
+ * int8 LLRs (e_offset in int8 units): srslte_rm_turbo_rx_lut_8bit into the code blocks' softbuffers (the int8
+ * buffer occupies the slot) and srslte_tdec_iteration_8bit with the CRC early stop.  Code blocks need an 8-bit
+ * window decoder (K % 16 == 0 && K > 800) or K <= 400 (the reference's 16-bit fallback on converted input);
+ * TBs with 400 < K <= 800 get -2 (the reference decodes a partly unconverted buffer there).  A softbuffer must
+ * not mix 8-bit and 16-bit transmissions (as in the reference, where the mode is fixed per UE). */
+int mi355_dlsch_decode8_dev(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const int8_t* d_e_bits,
+                            const mi355_dlsch_tb_t* tbs, uint32_t ntb, uint8_t* d_data, int32_t* ret,
+                            float* avg_iterations, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

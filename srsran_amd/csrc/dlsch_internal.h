@@ -5,6 +5,7 @@
 
 #define SB_STRIDE 18600 // SOFTBUFFER_SIZE (softbuffer.h:50): int16 per code-block softbuffer
 #define SB_DATA 768     // bytes of decoded CB data kept per code block (softbuffer.c:146)
+#define SB_CONV8 10240  // int16 offset in a slot of the converted copy of an int8 K <= 400 buffer (8-bit mode)
 
 namespace mi355 {
 
@@ -47,6 +48,21 @@ struct DlschRmArgs {
   size_t          sb_stride;
   const uint8_t*  sb_crc;
   uint8_t*        fresh;  // per slot: buffer logically zero (lazy srslte_softbuffer_rx_reset)
+};
+
+// 8-bit rate dematching (srslte_rm_turbo_rx_lut_8bit into (int8_t*)softbuffer->buffer_f[cb], sch.c:403-407):
+// thread per (code block, decoder position); the int8 buffer occupies the first bytes of the CB's slot
+struct DlschRm8Args {
+  const CbDesc*   desc;
+  int             ncb;
+  uint32_t        N, buflen;
+  const uint16_t* inv[4];
+  const int8_t*   e;
+  int8_t*         sb;        // pool buffer as bytes
+  size_t          sb_stride; // bytes per slot
+  const uint8_t*  sb_crc;
+  const uint8_t*  fresh;
+  int16_t*        conv;      // K <= 400: the int16 copy the reference's 16-bit fallback decodes (nullable)
 };
 
 struct DlschCheckArgs {
@@ -97,5 +113,7 @@ hipError_t dlsch_launch_check(const DlschCheckArgs& a, hipStream_t s);
 hipError_t dlsch_launch_prologue(const DlschTbArgs& a, hipStream_t s);
 hipError_t dlsch_launch_epilogue(const DlschTbArgs& a, hipStream_t s);
 hipError_t dlsch_launch_reset(const DlschResetArgs& a, hipStream_t s);
+
+hipError_t dlsch_launch_rm8(const DlschRm8Args& a, hipStream_t s);
 
 } // namespace mi355

@@ -325,6 +325,37 @@ hipError_t dlsch_launch_reset_list(const uint2* list, uint32_t n, uint32_t max_c
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------- 8-bit rate dematching
+// out[j] (+)= sum of the CB's LLRs at circular indices r, r + N, ... < n_e (int8, wrapping); a fresh slot (lazy
+// reset) is written whole, a CB that passed in an earlier transmission is left alone (sch.c:385)
+__global__ __launch_bounds__(256) void dlsch_rm8_rx(DlschRm8Args a)
+{
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)a.ncb * a.buflen) return;
+  const uint32_t b = (uint32_t)(t / a.buflen), j = (uint32_t)(t % a.buflen);
+  const CbDesc&  d = a.desc[b];
+  if (a.sb_crc[d.slot]) return;
+  int8_t*        o = a.sb + (size_t)d.slot * a.sb_stride;
+  const uint16_t r = a.inv[d.rv][j];
+  int            v = a.fresh[d.slot] ? 0 : o[j];
+  if (r != RM_NONE) {
+    const int8_t* e = a.e + d.e_off + d.rp;
+    for (uint32_t i = r; i < d.n_e; i += a.N) v += e[i];
+  }
+  o[j] = (int8_t)v;
+  if (a.conv) a.conv[(size_t)d.slot * (a.sb_stride / 2) + j] = (int16_t)(int8_t)v; // convert_8_to_16
+}
+
+hipError_t dlsch_launch_rm8(const DlschRm8Args& a, hipStream_t s)
+{
+  if (a.ncb <= 0) return hipSuccess;
+  const size_t n = (size_t)a.ncb * a.buflen;
+  hipLaunchKernelGGL(dlsch_rm8_rx, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(dlsch_rm_consume, dim3((unsigned)((a.ncb + 255) / 256)), dim3(256), 0, s, a.desc, a.ncb,
+                     (uint8_t*)a.fresh, a.sb_crc);
+  return hipGetLastError();
+}
+
 hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s)
 {
   if (a.ncb <= 0) return hipSuccess;

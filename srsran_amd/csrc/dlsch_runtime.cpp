@@ -22,6 +22,7 @@
 #include "../../include/srsran_amd/tdec.h"
 #include "dlsch_internal.h"
 #include "host_staging.h"
+#include "tdec8_internal.h"
 #include "rm_tables.h"
 #include "runtime_internal.h"
 #include "tdec_internal.h"
@@ -82,6 +83,8 @@ struct mi355_dlsch {
   uint32_t                               max_its = 10; // SRSLTE_PDSCH_MAX_TDEC_ITERS, sch.c:35
   std::map<uint32_t, mi355_tdec_batch_t*> dec;         // one decoder workspace per K
   std::map<uint64_t, uint16_t*>          rm;           // (K << 2 | rv) -> device table
+  std::map<uint64_t, uint16_t*>          rm8;          // the same for the 8-bit decoder layout
+  std::map<uint32_t, mi355_tdec8_t*>     dec8;         // 8-bit decoder workspace per K
   std::map<uint32_t, uint32_t*>          scales;       // K -> per-lane CRC scale factors
   CrcTable*                              crc = nullptr; // [0] CRC24A, [1] CRC24B
   // per-call scratch
@@ -108,6 +111,25 @@ static int rm_table(mi355_dlsch_t* q, uint32_t K, uint32_t rv, const uint16_t** 
     CHECK_HIP(hipMalloc(&d, inv.size() * 2));
     CHECK_HIP(hipMemcpy(d, inv.data(), inv.size() * 2, hipMemcpyHostToDevice));
     it = q->rm.emplace(key, d).first;
+  }
+  *out = it->second;
+  return MI355_SUCCESS;
+}
+
+// the same for the 8-bit decoder buffer layout (srslte_rm_turbo_rx_lut_8bit: sub-blocks of the 8-bit decoder)
+static int rm8_table(mi355_dlsch_t* q, uint32_t K, uint32_t rv, const uint16_t** out)
+{
+  const uint64_t key = ((uint64_t)K << 2) | rv;
+  auto           it  = q->rm8.find(key);
+  if (it == q->rm8.end()) {
+    const uint32_t              nsb = tdec_subblocks_8bit(K);
+    const std::vector<uint16_t> t   = rm_rx_table_nsb(K, rv, nsb);
+    std::vector<uint16_t>       inv((nsb ? 3 * (K + 32) + 12 : 3 * K + 12) + 1, RM_NONE);
+    for (size_t r = 0; r < t.size(); r++) inv[t[r]] = (uint16_t)r;
+    uint16_t* d = nullptr;
+    CHECK_HIP(hipMalloc(&d, inv.size() * 2));
+    CHECK_HIP(hipMemcpy(d, inv.data(), inv.size() * 2, hipMemcpyHostToDevice));
+    it = q->rm8.emplace(key, d).first;
   }
   *out = it->second;
   return MI355_SUCCESS;
@@ -310,6 +332,8 @@ void mi355_dlsch_destroy(mi355_dlsch_t* q)
   (void)hipDeviceSynchronize();
   for (auto& kv : q->dec) mi355_tdec_batch_destroy(kv.second);
   for (auto& kv : q->rm) (void)hipFree(kv.second);
+  for (auto& kv : q->rm8) (void)hipFree(kv.second);
+  for (auto& kv : q->dec8) mi355_tdec8_destroy(kv.second);
   for (auto& kv : q->scales) (void)hipFree(kv.second);
   (void)hipFree(q->crc);
   (void)hipFree(q->scratch);
@@ -362,11 +386,19 @@ int mi355_dlsch_decode_dev(mi355_dlsch_t*           q,
   return mi355::dlsch_decode_dev_hook(q, pool, d_e_bits, tbs, ntb, d_data, ret, avg_iterations, stream, mi355::WaitHook{});
 }
 
+int mi355_dlsch_decode8_dev(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const int8_t* d_e_bits,
+                            const mi355_dlsch_tb_t* tbs, uint32_t ntb, uint8_t* d_data, int32_t* ret,
+                            float* avg_iterations, void* stream)
+{
+  return mi355::dlsch_decode_dev_hook(q, pool, d_e_bits, tbs, ntb, d_data, ret, avg_iterations, stream,
+                                      mi355::WaitHook{}, true);
+}
+
 } // extern "C"
 
-int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const int16_t* d_e_bits,
+int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const void* d_e_bits,
                                  const mi355_dlsch_tb_t* tbs, uint32_t ntb, uint8_t* d_data, int32_t* ret,
-                                 float* avg_iterations, void* stream, mi355::WaitHook hook)
+                                 float* avg_iterations, void* stream, mi355::WaitHook hook, bool llr8)
 {
   if (!q || !pool || !tbs || !ret || (ntb && !d_e_bits)) return MI355_ERROR_INVALID_INPUTS;
   if (ntb == 0) return MI355_SUCCESS;
@@ -410,6 +442,13 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     }
     if (in.tbs == 0 || seg.C == 0) continue;                // nothing to decode: success
     if (seg.F || seg.C > pool->max_cb) {                   // sch.c:517-527
+      d.invalid = 1;
+      continue;
+    }
+    // int8 LLRs: the 8-bit window decoders, or K <= 400 through the 16-bit generic one (turbodecoder.c:458-483);
+    // 400 < K <= 800 would decode a partly unconverted buffer in the reference
+    auto ok8 = [](uint32_t K) { return tdec_subblocks_8bit(K) >= 16 || K <= 400; };
+    if (llr8 && ((seg.C1 && !ok8(seg.K1)) || (seg.C > seg.C1 && !ok8(seg.K2)))) {
       d.invalid = 1;
       continue;
     }
@@ -490,11 +529,54 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     uint8_t*            dec;
     mi355_tdec_batch_t* td;
     const uint32_t*     scale;
+    mi355_tdec8_t*      t8 = nullptr; // int8 LLRs with an 8-bit window decoder
   };
   std::vector<Live> live;
   size_t            off = 0, doff = 0;
   for (size_t gi = 0; gi < kcount.size(); gi++) {
     const uint32_t K = kcount[gi].first, n = kcount[gi].second;
+    if (llr8) {
+      const uint32_t nsb8 = tdec_subblocks_8bit(K);
+      DlschRm8Args   ra{};
+      ra.desc   = d_cb + off;
+      ra.ncb    = (int)n;
+      ra.N      = 3 * K + 12;
+      ra.buflen = nsb8 ? 3 * (K + 32) + 12 : 3 * K + 12;
+      for (uint32_t rv = 0; rv < 4; rv++) {
+        ra.inv[rv] = nullptr;
+        if (((rvmask[gi] >> rv) & 1u) && (r = rm8_table(q, K, rv, &ra.inv[rv]))) return r;
+      }
+      ra.e         = (const int8_t*)d_e_bits;
+      ra.sb        = (int8_t*)pool->buf;
+      ra.sb_stride = SB_STRIDE * sizeof(int16_t);
+      ra.sb_crc    = pool->cb_crc;
+      ra.fresh     = pool->fresh;
+      ra.conv      = nsb8 ? nullptr : pool->buf + SB_CONV8;
+      CHECK_HIP(dlsch_launch_rm8(ra, s));
+      const uint32_t* sc = nullptr;
+      if ((r = crc_scales(q, K, &sc))) return r;
+      mi355_tdec_batch_t* td = nullptr;
+      mi355_tdec8_t*      t8 = nullptr;
+      if (nsb8) {
+        auto it8 = q->dec8.find(K);
+        if (it8 == q->dec8.end()) {
+          if ((r = mi355_tdec8_create(&t8, q->device))) return r;
+          it8 = q->dec8.emplace(K, t8).first;
+        }
+        t8 = it8->second;
+      } else {
+        auto it = q->dec.find(K);
+        if (it == q->dec.end()) {
+          if ((r = mi355_tdec_batch_create(&td, q->device))) return r;
+          it = q->dec.emplace(K, td).first;
+        }
+        td = it->second;
+      }
+      live.push_back(Live{K, (uint32_t)off, n, d_dec + doff, td, sc, t8});
+      off += n;
+      doff += (size_t)n * (K / 8);
+      continue;
+    }
     DlschRmArgs    ra{};
     ra.desc = d_cb + off;
     ra.ncb  = (int)n;
@@ -505,7 +587,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
       if (((rvmask[gi] >> rv) & 1u) && (r = rm_table(q, K, rv, &ra.inv[rv]))) return r;
     }
     ra.fresh     = pool->fresh;
-    ra.e         = d_e_bits;
+    ra.e         = (const int16_t*)d_e_bits;
     ra.sb        = pool->buf;
     ra.sb_stride = SB_STRIDE;
     ra.sb_crc    = pool->cb_crc;
@@ -519,15 +601,23 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     }
     const uint32_t* sc = nullptr;
     if ((r = crc_scales(q, K, &sc))) return r;
-    live.push_back(Live{K, (uint32_t)off, n, d_dec + doff, it->second, sc});
+    live.push_back(Live{K, (uint32_t)off, n, d_dec + doff, it->second, sc, nullptr});
     off += n;
     doff += (size_t)n * (K / 8);
   }
 
   for (uint32_t h = 0; h < q->max_its; h++) {
     for (auto& lv : live) {
-      TdecRun rq{pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, d_run + h, lv.n, lv.K, h, h + 1, lv.dec, lv.K / 8, s};
-      if ((r = mi355_tdec_run_internal(lv.td, rq))) return r;
+      if (lv.t8) {
+        T8Batch b{};
+        b.in = (int8_t*)pool->buf, b.in_stride = SB_STRIDE * sizeof(int16_t), b.slot = d_slot + lv.off;
+        b.done = d_done + lv.off, b.running = d_run + h, b.K = lv.K, b.ncb = lv.n;
+        if ((r = tdec8_halfit_batch(lv.t8, b, h, lv.dec, lv.K / 8, s))) return r;
+      } else {
+        TdecRun rq{llr8 ? pool->buf + SB_CONV8 : pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, d_run + h, lv.n,
+                   lv.K, h, h + 1, lv.dec, lv.K / 8, s};
+        if ((r = mi355_tdec_run_internal(lv.td, rq))) return r;
+      }
       DlschCheckArgs ca{d_cb + lv.off, (int)lv.n, lv.K, h, q->max_its, lv.dec, lv.K / 8, d_data,
                         d_done + lv.off, d_run + h, d_run + h + 1, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1],
                         lv.scale};

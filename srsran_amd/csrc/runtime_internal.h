@@ -12,9 +12,10 @@ struct WaitHook {
 };
 
 // mi355_dlsch_decode_dev with a wait hook
-int dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const int16_t* d_e_bits,
+// llr8: int8 LLRs (srsUE's pdsch_8bit_decoder: sch.c:403-423 with llr_is_8bit), e_offset in int8 units
+int dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const void* d_e_bits,
                           const mi355_dlsch_tb_t* tbs, uint32_t ntb, uint8_t* d_data, int32_t* ret, float* avg_iterations,
-                          void* stream, WaitHook hook);
+                          void* stream, WaitHook hook, bool llr8 = false);
 
 // mi355_pdsch_decode_batch with the MMSE noise estimate of job i read from device memory d_noise[i] (written
 // by the channel estimator of the same stream), so no host round trip is needed between estimation and

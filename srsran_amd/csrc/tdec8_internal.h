@@ -3,19 +3,31 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+struct mi355_tdec8; // include/srsran_amd/tdec.h
+
 namespace mi355 {
 
 constexpr uint32_t T8_OVERLAP = 40; // win_overlap_len (turbodecoder_win.h:202)
 // per-code-block workspace: four K+32 int8 vectors, then the betas [L+1][8][NB]
 enum { T8_APP1 = 0, T8_APP2 = 1, T8_EXT1 = 2, T8_EXT2 = 3, T8_BETA = 4 };
 
+// a batch of code blocks of one K: input buffer of code block i at in + (slot ? slot[i] : i) * in_stride, its
+// workspace at ws + i * ws_stride; code blocks with done[i] != 0 and whole launches with *running == 0 are skipped
+// (the DL-SCH's CRC early stop, as the 16-bit decoder)
+struct T8Batch {
+  int8_t*         in;
+  size_t          in_stride;
+  const uint32_t* slot;    // nullable
+  const uint8_t*  done;    // nullable
+  const uint32_t* running; // nullable
+  int8_t*         ws;
+  size_t          ws_stride;
+  uint32_t        K, NB, L, ncb;
+};
+
 struct Tdec8MapArgs {
-  const int8_t* in;   // decoder input buffers (8-bit sub-block layout), in_stride bytes apart
-  size_t        in_stride;
-  int8_t*       ws;   // workspaces, ws_stride bytes apart
-  size_t        ws_stride;
-  uint32_t      K, NB, L, ncb;
-  int           dec2, has_app;
+  T8Batch b;
+  int     dec2, has_app;
 };
 
 struct Rm8Args {
@@ -27,14 +39,14 @@ struct Rm8Args {
   uint32_t        N, E, buflen, ncb;
 };
 
+// one half-iteration of a T8Batch (the proto's ws / ws_stride / NB / L are filled in): tdec8_runtime.cpp
+int tdec8_halfit_batch(::mi355_tdec8* q, T8Batch b, uint32_t n, uint8_t* out, size_t out_stride, hipStream_t s);
+
 hipError_t tdec8_launch_map(const Tdec8MapArgs& a, hipStream_t s);
-hipError_t tdec8_launch_tails(int8_t* in, size_t in_stride, int8_t* ws, size_t ws_stride, uint32_t K, uint32_t ncb,
-                              hipStream_t s);
-hipError_t tdec8_launch_sub(int8_t* ws, size_t ws_stride, uint32_t K, uint32_t ncb, int zx, int zy, hipStream_t s);
-hipError_t tdec8_launch_lut(int8_t* ws, size_t ws_stride, uint32_t K, uint32_t ncb, int src, int dst,
-                            const uint16_t* lut, hipStream_t s);
-hipError_t tdec8_launch_decide(const int8_t* ws, size_t ws_stride, uint32_t K, uint32_t NB, uint32_t ncb, int src,
-                               uint8_t* out, size_t out_stride, hipStream_t s);
+hipError_t tdec8_launch_tails(const T8Batch& b, hipStream_t s);
+hipError_t tdec8_launch_sub(const T8Batch& b, int zx, int zy, hipStream_t s);
+hipError_t tdec8_launch_lut(const T8Batch& b, int src, int dst, const uint16_t* lut, hipStream_t s);
+hipError_t tdec8_launch_decide(const T8Batch& b, int src, uint8_t* out, size_t out_stride, hipStream_t s);
 hipError_t rm8_launch_rx(const Rm8Args& a, hipStream_t s);
 
 } // namespace mi355

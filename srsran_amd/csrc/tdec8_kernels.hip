@@ -76,11 +76,13 @@ __device__ __forceinline__ void alpha_cands8(const int o[8], int x, int y, int m
 // ---------------------------------------------------------------------------- MAP (one constituent decoder)
 __global__ __launch_bounds__(256) void tdec8_map(Tdec8MapArgs a)
 {
+  const T8Batch& B = a.b;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.ncb * a.NB) return;
-  const uint32_t cb = t / a.NB, w = t % a.NB, NB = a.NB, L = a.L, K = a.K;
-  const int8_t*  in = a.in + (size_t)cb * a.in_stride;
-  int8_t*        ws = a.ws + (size_t)cb * a.ws_stride;
+  if (t >= B.ncb * B.NB || (B.running && *B.running == 0)) return;
+  const uint32_t cb = t / B.NB, w = t % B.NB, NB = B.NB, L = B.L, K = B.K;
+  if (B.done && B.done[cb]) return;
+  const int8_t*  in = B.in + (size_t)(B.slot ? B.slot[cb] : cb) * B.in_stride;
+  int8_t*        ws = B.ws + (size_t)cb * B.ws_stride;
   const int8_t*  X  = a.dec2 ? ws + T8_APP2 * (K + 32) : in;                 // systematic / interleaved prior
   const int8_t*  A  = (!a.dec2 && a.has_app) ? ws + T8_APP1 * (K + 32) : nullptr;
   const int8_t*  Y  = in + (a.dec2 ? 2 : 1) * (K + 32);                     // parity 0 / 1
@@ -155,14 +157,14 @@ __global__ __launch_bounds__(256) void tdec8_map(Tdec8MapArgs a)
 
 // ---------------------------------------------------------------------------- iteration glue
 // n = 0: the tails into the pads of the input buffer and app2 (extract_input_tail_sb, turbodecoder_iter.h:59-69)
-__global__ __launch_bounds__(256) void tdec8_tails(int8_t* in, size_t in_stride, int8_t* ws, size_t ws_stride,
-                                                   uint32_t K, uint32_t ncb)
+__global__ __launch_bounds__(256) void tdec8_tails(T8Batch B)
 {
   const uint32_t cb = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cb >= ncb) return;
-  int8_t*       b    = in + (size_t)cb * in_stride;
-  int8_t*       app2 = ws + (size_t)cb * ws_stride + T8_APP2 * (K + 32);
-  const int8_t* t    = b + 3 * (K + 32);
+  if (cb >= B.ncb || (B.running && *B.running == 0) || (B.done && B.done[cb])) return;
+  const uint32_t K    = B.K;
+  int8_t*        b    = B.in + (size_t)(B.slot ? B.slot[cb] : cb) * B.in_stride;
+  int8_t*        app2 = B.ws + (size_t)cb * B.ws_stride + T8_APP2 * (K + 32);
+  const int8_t*  t    = b + 3 * (K + 32);
   for (uint32_t i = 0; i < 3; i++) {
     const int8_t s = t[2 * i], p0 = t[2 * i + 1], a2 = t[6 + 2 * i], p1 = t[6 + 2 * i + 1];
     b[K + i]                = s;
@@ -173,38 +175,38 @@ __global__ __launch_bounds__(256) void tdec8_tails(int8_t* in, size_t in_stride,
 }
 
 // z = x - y (srslte_vec_sub_bbb: saturating over the 32-element SIMD body, wrapping scalar tail)
-__global__ __launch_bounds__(256) void tdec8_sub(int8_t* ws, size_t ws_stride, uint32_t K, uint32_t ncb, int zx,
-                                                 int zy)
+__global__ __launch_bounds__(256) void tdec8_sub(T8Batch B, int zx, int zy)
 {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ncb * K) return;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, K = B.K;
+  if (t >= B.ncb * K || (B.running && *B.running == 0)) return;
   const uint32_t cb = t / K, i = t % K;
-  int8_t*        b  = ws + (size_t)cb * ws_stride;
-  const int      x = b[zx * (K + 32) + i], y = b[zy * (K + 32) + i];
+  if (B.done && B.done[cb]) return;
+  int8_t*   b = B.ws + (size_t)cb * B.ws_stride;
+  const int x = b[zx * (K + 32) + i], y = b[zy * (K + 32) + i];
   b[zx * (K + 32) + i] = (int8_t)(i < K / 32 * 32 ? ssub8(x, y) : (int)(int8_t)(x - y));
 }
 
 // y[lut[i]] = x[i] (srslte_vec_lut_bbb)
-__global__ __launch_bounds__(256) void tdec8_lut(int8_t* ws, size_t ws_stride, uint32_t K, uint32_t ncb, int src,
-                                                 int dst, const uint16_t* lut)
+__global__ __launch_bounds__(256) void tdec8_lut(T8Batch B, int src, int dst, const uint16_t* lut)
 {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ncb * K) return;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, K = B.K;
+  if (t >= B.ncb * K || (B.running && *B.running == 0)) return;
   const uint32_t cb = t / K, i = t % K;
-  int8_t*        b  = ws + (size_t)cb * ws_stride;
+  if (B.done && B.done[cb]) return;
+  int8_t* b = B.ws + (size_t)cb * B.ws_stride;
   b[dst * (K + 32) + lut[i]] = b[src * (K + 32) + i];
 }
 
 // decision bytes of the natural-order bits (decision_byte, :945-993): bit i at window-ordered position
 // (i % L) * NB + i / L, MSB first
-__global__ __launch_bounds__(256) void tdec8_decide(const int8_t* ws, size_t ws_stride, uint32_t K, uint32_t NB,
-                                                    uint32_t ncb, int src, uint8_t* out, size_t out_stride)
+__global__ __launch_bounds__(256) void tdec8_decide(T8Batch B, int src, uint8_t* out, size_t out_stride)
 {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, KB = K / 8;
-  if (t >= ncb * KB) return;
-  const uint32_t cb = t / KB, j = t % KB, L = K / NB;
-  const int8_t*  v  = ws + (size_t)cb * ws_stride + src * (K + 32);
-  uint32_t       byte = 0;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, K = B.K, KB = K / 8;
+  if (t >= B.ncb * KB || (B.running && *B.running == 0)) return;
+  const uint32_t cb = t / KB, j = t % KB, NB = B.NB, L = B.L;
+  if (B.done && B.done[cb]) return;
+  const int8_t* v    = B.ws + (size_t)cb * B.ws_stride + src * (K + 32);
+  uint32_t      byte = 0;
 #pragma unroll
   for (uint32_t b = 0; b < 8; b++) {
     const uint32_t i = 8 * j + b;
@@ -234,31 +236,27 @@ static inline dim3 grid_of(size_t n) { return dim3((uint32_t)((n + 255) / 256));
 
 hipError_t tdec8_launch_map(const Tdec8MapArgs& a, hipStream_t s)
 {
-  hipLaunchKernelGGL(tdec8_map, grid_of((size_t)a.ncb * a.NB), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(tdec8_map, grid_of((size_t)a.b.ncb * a.b.NB), dim3(256), 0, s, a);
   return hipGetLastError();
 }
-hipError_t tdec8_launch_tails(int8_t* in, size_t in_stride, int8_t* ws, size_t ws_stride, uint32_t K, uint32_t ncb,
-                              hipStream_t s)
+hipError_t tdec8_launch_tails(const T8Batch& b, hipStream_t s)
 {
-  hipLaunchKernelGGL(tdec8_tails, grid_of(ncb), dim3(256), 0, s, in, in_stride, ws, ws_stride, K, ncb);
+  hipLaunchKernelGGL(tdec8_tails, grid_of(b.ncb), dim3(256), 0, s, b);
   return hipGetLastError();
 }
-hipError_t tdec8_launch_sub(int8_t* ws, size_t ws_stride, uint32_t K, uint32_t ncb, int zx, int zy, hipStream_t s)
+hipError_t tdec8_launch_sub(const T8Batch& b, int zx, int zy, hipStream_t s)
 {
-  hipLaunchKernelGGL(tdec8_sub, grid_of((size_t)ncb * K), dim3(256), 0, s, ws, ws_stride, K, ncb, zx, zy);
+  hipLaunchKernelGGL(tdec8_sub, grid_of((size_t)b.ncb * b.K), dim3(256), 0, s, b, zx, zy);
   return hipGetLastError();
 }
-hipError_t tdec8_launch_lut(int8_t* ws, size_t ws_stride, uint32_t K, uint32_t ncb, int src, int dst,
-                            const uint16_t* lut, hipStream_t s)
+hipError_t tdec8_launch_lut(const T8Batch& b, int src, int dst, const uint16_t* lut, hipStream_t s)
 {
-  hipLaunchKernelGGL(tdec8_lut, grid_of((size_t)ncb * K), dim3(256), 0, s, ws, ws_stride, K, ncb, src, dst, lut);
+  hipLaunchKernelGGL(tdec8_lut, grid_of((size_t)b.ncb * b.K), dim3(256), 0, s, b, src, dst, lut);
   return hipGetLastError();
 }
-hipError_t tdec8_launch_decide(const int8_t* ws, size_t ws_stride, uint32_t K, uint32_t NB, uint32_t ncb, int src,
-                               uint8_t* out, size_t out_stride, hipStream_t s)
+hipError_t tdec8_launch_decide(const T8Batch& b, int src, uint8_t* out, size_t out_stride, hipStream_t s)
 {
-  hipLaunchKernelGGL(tdec8_decide, grid_of((size_t)ncb * (K / 8)), dim3(256), 0, s, ws, ws_stride, K, NB, ncb, src,
-                     out, out_stride);
+  hipLaunchKernelGGL(tdec8_decide, grid_of((size_t)b.ncb * (b.K / 8)), dim3(256), 0, s, b, src, out, out_stride);
   return hipGetLastError();
 }
 hipError_t rm8_launch_rx(const Rm8Args& a, hipStream_t s)

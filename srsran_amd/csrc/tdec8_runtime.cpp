@@ -65,6 +65,49 @@ static int get_interl(mi355_tdec8_t* q, uint32_t K, uint32_t NB, const uint16_t*
   return MI355_SUCCESS;
 }
 
+// one half-iteration n over the batch b (K, in, slot/done/running set by the caller); the caller holds q->mu or
+// owns q exclusively
+int mi355::tdec8_halfit_batch(mi355_tdec8_t* q, T8Batch b, uint32_t n, uint8_t* out, size_t out_stride, hipStream_t s)
+{
+  const uint32_t K = b.K, NB = tdec_subblocks_8bit(K);
+  if (NB != 16 && NB != 32) return MI355_ERROR_INVALID_INPUTS;
+  const uint16_t* tab = nullptr;
+  int             r   = get_interl(q, K, NB, &tab);
+  if (r) return r;
+  const uint32_t L         = K / NB;
+  const size_t   ws_stride = (4 * (size_t)(K + 32) + 8 * (size_t)(L + 1) * NB + 255) / 256 * 256;
+  if (ws_stride * b.ncb > q->ws_cap) {
+    if (n) return MI355_ERROR_INVALID_INPUTS; // a later half-iteration of a batch that was never started
+    if (q->ws) {
+      CHECK_HIP(hipDeviceSynchronize());
+      CHECK_HIP(hipFree(q->ws));
+      q->ws = nullptr;
+    }
+    q->ws_cap = ws_stride * b.ncb;
+    CHECK_HIP(hipMalloc(&q->ws, q->ws_cap));
+  }
+  b.ws = q->ws, b.ws_stride = ws_stride, b.NB = NB, b.L = L;
+  Tdec8MapArgs a{};
+  a.b = b;
+  int src;
+  if (n == 0) CHECK_HIP(tdec8_launch_tails(b, s));
+  if (n % 2 == 0) { // DEC1 with the a-priori app1 - ext1 from n = 2 on
+    if (n) CHECK_HIP(tdec8_launch_sub(b, T8_APP1, T8_EXT1, s));
+    a.dec2 = 0, a.has_app = n > 0;
+    CHECK_HIP(tdec8_launch_map(a, s));
+    src = T8_EXT1;
+  } else { // DEC2 on the deinterleaved extrinsic of DEC1
+    if (n > 1) CHECK_HIP(tdec8_launch_sub(b, T8_EXT1, T8_APP1, s));
+    CHECK_HIP(tdec8_launch_lut(b, T8_EXT1, T8_APP2, tab + K, s));
+    a.dec2 = 1, a.has_app = 0;
+    CHECK_HIP(tdec8_launch_map(a, s));
+    CHECK_HIP(tdec8_launch_lut(b, T8_EXT2, T8_APP1, tab, s));
+    src = T8_APP1;
+  }
+  CHECK_HIP(tdec8_launch_decide(b, src, out, out_stride, s));
+  return MI355_SUCCESS;
+}
+
 extern "C" {
 
 uint32_t mi355_tdec_autoimp_get_subblocks_8bit(uint32_t long_cb) { return tdec_subblocks_8bit(long_cb); }
@@ -105,40 +148,11 @@ int mi355_tdec8_halfit_dev(mi355_tdec8_t* q, int8_t* in, size_t in_stride, uint3
   if (!ncb) return MI355_SUCCESS;
   std::lock_guard<std::mutex> lk(q->mu);
   CHECK_HIP(hipSetDevice(q->device));
-  hipStream_t     s   = stream ? (hipStream_t)stream : q->own;
-  const uint16_t* tab = nullptr;
-  int             r   = get_interl(q, K, NB, &tab);
+  hipStream_t s = stream ? (hipStream_t)stream : q->own;
+  T8Batch     b{};
+  b.in = in, b.in_stride = in_stride, b.K = K, b.ncb = ncb;
+  int r = mi355::tdec8_halfit_batch(q, b, n, out, out_stride, s);
   if (r) return r;
-  const uint32_t L         = K / NB;
-  const size_t   ws_stride = (4 * (size_t)(K + 32) + 8 * (size_t)(L + 1) * NB + 255) / 256 * 256;
-  if (ws_stride * ncb > q->ws_cap) {
-    if (n) return MI355_ERROR_INVALID_INPUTS; // a later half-iteration of a batch that was never started
-    if (q->ws) {
-      CHECK_HIP(hipDeviceSynchronize());
-      CHECK_HIP(hipFree(q->ws));
-      q->ws = nullptr;
-    }
-    q->ws_cap = ws_stride * ncb;
-    CHECK_HIP(hipMalloc(&q->ws, q->ws_cap));
-  }
-  Tdec8MapArgs a{};
-  a.in = in, a.in_stride = in_stride, a.ws = q->ws, a.ws_stride = ws_stride, a.K = K, a.NB = NB, a.L = L, a.ncb = ncb;
-  int src;
-  if (n == 0) CHECK_HIP(tdec8_launch_tails(in, in_stride, q->ws, ws_stride, K, ncb, s));
-  if (n % 2 == 0) { // DEC1 with the a-priori app1 - ext1 from n = 2 on
-    if (n) CHECK_HIP(tdec8_launch_sub(q->ws, ws_stride, K, ncb, T8_APP1, T8_EXT1, s));
-    a.dec2 = 0, a.has_app = n > 0;
-    CHECK_HIP(tdec8_launch_map(a, s));
-    src = T8_EXT1;
-  } else { // DEC2 on the deinterleaved extrinsic of DEC1
-    if (n > 1) CHECK_HIP(tdec8_launch_sub(q->ws, ws_stride, K, ncb, T8_EXT1, T8_APP1, s));
-    CHECK_HIP(tdec8_launch_lut(q->ws, ws_stride, K, ncb, T8_EXT1, T8_APP2, tab + K, s));
-    a.dec2 = 1, a.has_app = 0;
-    CHECK_HIP(tdec8_launch_map(a, s));
-    CHECK_HIP(tdec8_launch_lut(q->ws, ws_stride, K, ncb, T8_EXT2, T8_APP1, tab, s));
-    src = T8_APP1;
-  }
-  CHECK_HIP(tdec8_launch_decide(q->ws, ws_stride, K, NB, ncb, src, out, out_stride, s));
   if (!stream) CHECK_HIP(hipStreamSynchronize(s));
   return MI355_SUCCESS;
 }

@@ -31,6 +31,8 @@ def _declare():
     L.mi355_dlsch_set_max_iterations.argtypes = [vp, u32]
     L.mi355_dlsch_decode_dev.argtypes = [vp, vp, vp, C.POINTER(TbDesc), u32, vp, C.POINTER(C.c_int32),
                                          C.POINTER(C.c_float), vp]
+    L.mi355_dlsch_decode8_dev.argtypes = [vp, vp, vp, C.POINTER(TbDesc), u32, vp, C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_float), vp]
     L._dlsch_declared = True
     return L
 
@@ -73,12 +75,14 @@ class Dlsch:
     def set_max_iterations(self, n: int):
         check(self.L.mi355_dlsch_set_max_iterations(self.h, n), "set_max_iterations")
 
-    def decode(self, pool: SoftbufferPool, tbs: list[dict], e_bits: list[np.ndarray]):
-        """tbs[i] = dict(tbs, Qm, rv, softbuffer); e_bits[i] = int16 LLRs of TB i.
-        Returns (ret[i], data[i] bytes (tbs/8 + 6), avg_iterations[i])."""
+    def decode(self, pool: SoftbufferPool, tbs: list[dict], e_bits: list[np.ndarray], llr8: bool = False):
+        """tbs[i] = dict(tbs, Qm, rv, softbuffer); e_bits[i] = int16 LLRs of TB i (int8 with llr8: the
+        pdsch_8bit_decoder mode, mi355_dlsch_decode8_dev).  Returns (ret[i], data[i] bytes (tbs/8 + 6),
+        avg_iterations[i])."""
         n = len(tbs)
+        dt = np.int8 if llr8 else np.int16
         offs = np.cumsum([0] + [e.size for e in e_bits])
-        allE = np.concatenate([np.ascontiguousarray(e, np.int16) for e in e_bits]) if n else np.zeros(1, np.int16)
+        allE = np.concatenate([np.ascontiguousarray(e, dt) for e in e_bits]) if n else np.zeros(1, dt)
         doff = np.cumsum([0] + [t["tbs"] // 8 + 8 for t in tbs])
         d_e = DeviceBuffer(max(allE.nbytes, 2), self.device).upload(allE)
         d_data = DeviceBuffer(max(int(doff[-1]), 1), self.device)
@@ -89,8 +93,8 @@ class Dlsch:
                              int(offs[i]), int(doff[i]))
         ret = (C.c_int32 * n)()
         its = (C.c_float * n)()
-        check(self.L.mi355_dlsch_decode_dev(self.h, pool.h, d_e.ptr, desc, n, d_data.ptr, ret, its, None),
-              "dlsch_decode_dev")
+        fn = self.L.mi355_dlsch_decode8_dev if llr8 else self.L.mi355_dlsch_decode_dev
+        check(fn(self.h, pool.h, d_e.ptr, desc, n, d_data.ptr, ret, its, None), "dlsch_decode_dev")
         host = np.zeros(int(doff[-1]), np.uint8)
         d_data.download(host)
         datas = [host[doff[i]: doff[i] + tbs[i]["tbs"] // 8 + 6].copy() for i in range(n)]
