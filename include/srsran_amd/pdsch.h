@@ -140,6 +140,11 @@ uint32_t mi355_pdsch_re_map(const mi355_cell_t* cell, const mi355_pdsch_grant_t*
 int mi355_pdsch_debug_stage(mi355_pdsch_t* q, uint32_t job, uint32_t cw, const float** d, const float** csi,
                             const int16_t** e);
 
+/* srsUE's pdsch_8bit_decoder option (cc_worker.cc:98-101: pdsch.llr_is_8bit = pdsch.dl_sch.llr_is_8bit = true):
+ * int8 LLRs (srslte_demod_soft_demodulate_b, srslte_scrambling_sb_offset, the float CSI loop of pdsch.c:661-668)
+ * and the 8-bit DL-SCH decode (see mi355_dlsch_decode8_dev).  mi355_pdsch_debug_stage's e then points to int8. */
+int mi355_pdsch_set_llr_8bit(mi355_pdsch_t* q, int enable);
+
 /* Run only the symbol-level front-end (extraction .. CSI weighting) of a job list, no DL-SCH decode. */
 int mi355_pdsch_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, uint32_t njobs, void* stream);
 

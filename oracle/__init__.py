@@ -88,6 +88,7 @@ def ref() -> C.CDLL:
     global _REF
     if _REF is None:
         L = C.CDLL(os.path.join(HERE, "_ref", "libsrslte_ref.so"))
+        i8p = np.ctypeslib.ndpointer(np.int8, flags="C_CONTIGUOUS")
         L.ref_tdec_new.restype = C.c_void_p
         L.ref_tdec_new.argtypes = [C.c_uint32, C.c_int]
         L.ref_tdec_free.argtypes = [C.c_void_p]
@@ -97,7 +98,6 @@ def ref() -> C.CDLL:
         L.ref_crc_byte.argtypes = [C.c_uint32, C.c_int, u8p, C.c_int]
         L.ref_cbsegm.argtypes = [C.c_uint32, u32p]
         L.ref_rm_turbo_rx.argtypes = [i16p, C.c_uint32, i16p, C.c_uint32, C.c_uint32]
-        i8p = np.ctypeslib.ndpointer(np.int8, flags="C_CONTIGUOUS")
         L.ref_tdec8_new.restype = C.c_void_p
         L.ref_tdec8_new.argtypes = [C.c_uint32]
         L.ref_tdec8_free.argtypes = [C.c_void_p]
@@ -106,6 +106,8 @@ def ref() -> C.CDLL:
         L.ref_tdec_run_batch.argtypes = [i16p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, u8p, C.c_int]
         L.ref_demod_soft_s.argtypes = [C.c_int, f32p, i16p, C.c_int]
         L.ref_scramble_s.argtypes = [C.c_uint32, i16p, C.c_int, C.c_int]
+        L.ref_demod_soft_b.argtypes = [C.c_int, f32p, i8p, C.c_int]
+        L.ref_scramble_sb.argtypes = [C.c_uint32, i8p, C.c_int, C.c_int]
         L.ref_predecoding.argtypes = [C.c_void_p] * 10 + [C.c_int] * 6 + [C.c_float, C.c_float, C.c_int]
         _REF = L
     return _REF

@@ -27,6 +27,30 @@ int ref_demod_soft_s(int bits_per_symbol, const float* iq, int16_t* llr, int nsy
 }
 
 /* srslte_scrambling_s_offset over a freshly generated LTE Gold sequence (scrambling.c:43-47) */
+int ref_demod_soft_b(int bits_per_symbol, const float* iq, int8_t* llr, int nsymbols)
+{
+  srslte_mod_t m;
+  switch (bits_per_symbol) {
+    case 1: m = SRSLTE_MOD_BPSK; break;
+    case 2: m = SRSLTE_MOD_QPSK; break;
+    case 4: m = SRSLTE_MOD_16QAM; break;
+    case 6: m = SRSLTE_MOD_64QAM; break;
+    case 8: m = SRSLTE_MOD_256QAM; break;
+    default: return -1;
+  }
+  return srslte_demod_soft_demodulate_b(m, (const cf_t*)iq, llr, nsymbols);
+}
+
+int ref_scramble_sb(uint32_t c_init, int8_t* llr, int offset, int len)
+{
+  srslte_sequence_t seq;
+  memset(&seq, 0, sizeof(seq));
+  if (srslte_sequence_LTE_pr(&seq, offset + len, c_init)) return -1;
+  srslte_scrambling_sb_offset(&seq, llr, offset, len);
+  srslte_sequence_free(&seq);
+  return 0;
+}
+
 int ref_scramble_s(uint32_t c_init, int16_t* llr, int offset, int len)
 {
   srslte_sequence_t seq;

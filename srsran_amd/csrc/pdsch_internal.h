@@ -51,6 +51,12 @@ struct PdschCwDev {
   uint32_t      nof_re, nof_bits, qm, c_init, csi_enable;
   uint32_t      pairs; // kernel B work items: symbol pairs
   uint32_t      fused; // produced by pdsch_eq_llr (pdsch_llr / pdsch_cmax_reduce skip it)
+  // pdsch_8bit_decoder (pdsch.c:661-668, 816-850): int8 LLRs into e8 (srslte_demod_soft_demodulate_b,
+  // srslte_scrambling_sb_offset, the float CSI loop); k8 = the reference's float constants: QPSK scale
+  // (float)(-20 * M_SQRT2), 60 / sqrtf(10), 8, 4, 2 / sqrtf(170)
+  uint32_t      llr8;
+  int8_t*       e8;
+  float         k8[5];
 };
 
 // 2-D grids: blockIdx.y = job / codeword, blockIdx.x over the largest one's work items.

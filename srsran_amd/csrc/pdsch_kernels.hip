@@ -632,12 +632,100 @@ template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, 
   llr_syms<QM>(C, pr, ns, x, csi, cmax_bits);
 }
 
+// ---------------------------------------------------------------------------- 8-bit LLRs
+// srslte_demod_soft_demodulate_b (demod_soft.c:100-941, AVX2/SSE build) per symbol m of nof_re: QPSK
+// srslte_vec_convert_fb (vector_simd.c:524-589: truncating conversion, saturating packs over the 16-float SIMD body,
+// wrapping scalar tail); 16/64QAM the SSE demappers over 8-symbol bodies (round-to-nearest, saturating packs, byte
+// abs / wrapping subtracts of the truncated thresholds) with their scalar tails (truncating, wrapping); 256QAM
+// scalar; then the sign flip of srslte_scrambling_sb_offset (_mm256_sign_epi8: -(-128) = -128) and the float CSI
+// weighting (int8)((float)e * csi / csi_max) (pdsch.c:661-668)
+__device__ __forceinline__ int wrap8(int v) { return (int)(int8_t)(uint8_t)(v & 0xff); }
+__device__ __forceinline__ int sat8i(int v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
+__device__ __forceinline__ int abs8(int v) { return v == -128 ? -128 : (v < 0 ? -v : v); } // _mm_abs_epi8
+
+__device__ __forceinline__ void demod8(const PdschCwDev& C, float re, float im, bool body, int* o)
+{
+  switch (C.qm) {
+    case 1: { // demod_bpsk_lte_b: float sum times the double M_SQRT1_2
+      const double v = (double)(-20.0f * (re + im)) * 0.70710678118654752440;
+      o[0]           = wrap8((int)v);
+      break;
+    }
+    case 2: {
+      const float a = re * C.k8[0], b = im * C.k8[0];
+      o[0]          = body ? sat8i((int)a) : wrap8((int)a);
+      o[1]          = body ? sat8i((int)b) : wrap8((int)b);
+      break;
+    }
+    case 4:
+      if (body) {
+        const int sr = sat8i((int)rintf(re * -30.0f)), si = sat8i((int)rintf(im * -30.0f));
+        o[0] = sr, o[1] = si, o[2] = wrap8(abs8(sr) - 18), o[3] = wrap8(abs8(si) - 18);
+      } else {
+        const int yr = wrap8((int)(30.0f * re)), yi = wrap8((int)(30.0f * im));
+        o[0] = wrap8(-yr), o[1] = wrap8(-yi);
+        o[2] = wrap8((int)((float)abs(yr) - C.k8[1]));
+        o[3] = wrap8((int)((float)abs(yi) - C.k8[1]));
+      }
+      break;
+    case 6:
+      if (body) {
+        const int sr = sat8i((int)rintf(re * -40.0f)), si = sat8i((int)rintf(im * -40.0f));
+        const int ar = wrap8(abs8(sr) - 24), ai = wrap8(abs8(si) - 24);
+        o[0] = sr, o[1] = si, o[2] = ar, o[3] = ai, o[4] = wrap8(abs8(ar) - 12), o[5] = wrap8(abs8(ai) - 12);
+      } else {
+        const int yr = wrap8((int)(40.0f * re)), yi = wrap8((int)(40.0f * im));
+        o[0] = wrap8(-yr), o[1] = wrap8(-yi);
+        o[2] = wrap8(wrap8(abs(yr)) - 24), o[3] = wrap8(wrap8(abs(yi)) - 24);
+        o[4] = wrap8(wrap8(abs(o[2])) - 12), o[5] = wrap8(wrap8(abs(o[3])) - 12);
+      }
+      break;
+    default: {
+      float r = -re, i = -im;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        o[2 * k]     = wrap8((int)(50.0f * r));
+        o[2 * k + 1] = wrap8((int)(50.0f * i));
+        if (k < 3) {
+          r = fabsf(r) - C.k8[2 + k];
+          i = fabsf(i) - C.k8[2 + k];
+        }
+      }
+      break;
+    }
+  }
+}
+
+__device__ __forceinline__ void llr8_pair(const PdschCwDev& C, uint32_t pr, uint32_t cmax_bits)
+{
+  const uint32_t qm = C.qm, nbody = C.nof_re / 8 * 8;
+  const float    cmax = __uint_as_float(cmax_bits);
+  for (uint32_t m = 2 * pr; m < min(2 * pr + 2, C.nof_re); m++) {
+    const cf x = ld(gptr(C.d), m);
+    int      o[8];
+    demod8(C, x.re, x.im, m < nbody, o);
+    for (uint32_t k = 0; k < qm; k++) {
+      const uint32_t j = m * qm + k;
+      if ((gptr(C.scr)[j >> 5] >> (j & 31u)) & 1u) o[k] = wrap8(-o[k]);
+    }
+    if (C.csi_enable) {
+      const float c = gptr(C.csi)[m] / cmax;
+      for (uint32_t k = 0; k < qm; k++) o[k] = wrap8((int)((float)o[k] * c));
+    }
+    for (uint32_t k = 0; k < qm; k++) C.e8[m * qm + k] = (int8_t)o[k];
+  }
+}
+
 __global__ __launch_bounds__(256) void pdsch_llr(const PdschCwDev* __restrict__ cws)
 {
   const PdschCwDev& C  = cws[blockIdx.y];
   const uint32_t    pr = blockIdx.x * 256 + threadIdx.x;
   if (C.fused || pr >= C.pairs) return;
   const uint32_t cm = C.csi_enable ? *gptr(C.cmax_final) : 0u;
+  if (C.llr8) {
+    llr8_pair(C, pr, cm);
+    return;
+  }
   switch (C.qm) {
     case 1: llr_pair<1>(C, pr, cm); break;
     case 2: llr_pair<2>(C, pr, cm); break;

@@ -165,6 +165,7 @@ struct mi355_pdsch {
   float2*                              d_arena   = nullptr;
   float*                               csi_arena = nullptr;
   int16_t*                             e_arena   = nullptr;
+  bool                                 llr8      = false; // pdsch.llr_is_8bit (srsUE pdsch_8bit_decoder)
   HostStaging                          stage;
   std::mutex                           mu;
 };
@@ -450,6 +451,15 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
       cws[ci].nparts    = (plans[i].dev.units + EQ_BLOCK_ITEMS - 1) / EQ_BLOCK_ITEMS;
       cws[ci].cmax_final = d_cfin + ci;
       cws[ci].e         = q->e_arena + plans[i].e_off[t];
+      if (q->llr8) {
+        cws[ci].llr8  = 1;
+        cws[ci].e8    = (int8_t*)q->e_arena + plans[i].e_off[t];
+        cws[ci].k8[0] = (float)(-20 * M_SQRT2);
+        cws[ci].k8[1] = 2 * 30 / sqrtf(10);
+        cws[ci].k8[2] = 8.0f / sqrtf(170.0f);
+        cws[ci].k8[3] = 4.0f / sqrtf(170.0f);
+        cws[ci].k8[4] = 2.0f / sqrtf(170.0f);
+      }
       ci++;
     }
   }
@@ -516,6 +526,14 @@ void mi355_pdsch_destroy(mi355_pdsch_t* q)
 
 mi355_dlsch_t* mi355_pdsch_dlsch(mi355_pdsch_t* q) { return q ? q->dlsch : nullptr; }
 
+int mi355_pdsch_set_llr_8bit(mi355_pdsch_t* q, int enable)
+{
+  if (!q) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lk(q->mu);
+  q->llr8 = enable != 0;
+  return MI355_SUCCESS;
+}
+
 int mi355_pdsch_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, uint32_t njobs, void* stream)
 {
   if (!q || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;
@@ -544,7 +562,8 @@ int mi355_pdsch_debug_stage(mi355_pdsch_t* q, uint32_t job, uint32_t cw, const f
   if (e) {
     *e = nullptr;
     for (uint32_t t = 0; t < 2; t++)
-      if (P.decode[t] && P.cw_of_tb[t] == cw) *e = q->e_arena + P.e_off[t];
+      if (P.decode[t] && P.cw_of_tb[t] == cw)
+        *e = q->llr8 ? (const int16_t*)((const int8_t*)q->e_arena + P.e_off[t]) : q->e_arena + P.e_off[t];
   }
   return MI355_SUCCESS;
 }
@@ -580,8 +599,8 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
     if (d_noise && jobs[i].cfg.decoder_type != MI355_MIMO_DECODER_ZF) plans[i].dev.noise_dev = d_noise + i;
     plans[i].dev.h_invariant = ce_invariant ? 1u : 0u;
     // csi depends on the subcarrier only for these schemes (CDD alternates its precoder per RE, SFBC pairs REs)
-    plans[i].dev.fused = ce_invariant && (plans[i].dev.scheme == MI355_TXSCHEME_PORT0 ||
-                                          plans[i].dev.scheme == MI355_TXSCHEME_SPATIALMUX) ? 1u : 0u;
+    plans[i].dev.fused = !q->llr8 && ce_invariant && (plans[i].dev.scheme == MI355_TXSCHEME_PORT0 ||
+                                                      plans[i].dev.scheme == MI355_TXSCHEME_SPATIALMUX) ? 1u : 0u;
   }
   const auto t1 = now();
   int r = run_frontend(q, jobs, plans, s);
@@ -621,7 +640,7 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
     std::vector<float>     avg(kv.second.size());
     if ((r = mi355_dlsch_set_max_iterations(q->dlsch, its))) return r;
     r = dlsch_decode_dev_hook(q->dlsch, pool, q->e_arena, kv.second.data(), (uint32_t)kv.second.size(), nullptr,
-                              ret.data(), avg.data(), s, hook);
+                              ret.data(), avg.data(), s, hook, q->llr8);
     hook = WaitHook{}; // once
     if (r) return r;
     const auto& who = by_its[its];

@@ -66,6 +66,7 @@ def _declare():
     L.mi355_pdsch_decode_batch.argtypes = [vp, vp, C.POINTER(PdschJob), u32, C.POINTER(PdschRes), vp]
     L.mi355_pdsch_frontend.argtypes = [vp, C.POINTER(PdschJob), u32, vp]
     L.mi355_pdsch_debug_stage.argtypes = [vp, u32, u32, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
+    L.mi355_pdsch_set_llr_8bit.argtypes = [vp, C.c_int]
     L.mi355_pdsch_re_map.restype = u32
     L.mi355_pdsch_re_map.argtypes = [C.POINTER(Cell), C.POINTER(PdschGrant), u32, u32, C.c_void_p]
     L._pdsch_declared = True
@@ -135,8 +136,14 @@ class Pdsch:
         arr = (PdschJob * n)(*jobs)
         check(self.L.mi355_pdsch_frontend(self.h, arr, n, None), "pdsch_frontend")
 
+    def set_llr_8bit(self, enable: bool = True):
+        """pdsch.llr_is_8bit (srsUE pdsch_8bit_decoder): int8 LLRs and the 8-bit DL-SCH."""
+        check(self.L.mi355_pdsch_set_llr_8bit(self.h, int(enable)), "set_llr_8bit")
+        self.llr8 = bool(enable)
+
     def stage(self, job: int, cw: int, nof_re: int, nof_bits: int | None):
-        """(d complex64[nof_re], csi float32[nof_re], e int16[nof_bits] or None) of the last call."""
+        """(d complex64[nof_re], csi float32[nof_re], e int16[nof_bits] (int8 in 8-bit mode) or None) of the last
+        call."""
         d, c, e = C.c_void_p(), C.c_void_p(), C.c_void_p()
         check(self.L.mi355_pdsch_debug_stage(self.h, job, cw, C.byref(d), C.byref(c), C.byref(e)), "debug_stage")
         L = lib()
@@ -146,7 +153,7 @@ class Pdsch:
         check(L.mi355_memcpy_d2h(cc.ctypes.data, c.value, cc.nbytes), "d2h")
         ee = None
         if nof_bits and e.value:
-            ee = np.zeros(nof_bits, np.int16)
+            ee = np.zeros(nof_bits, np.int8 if getattr(self, "llr8", False) else np.int16)
             check(L.mi355_memcpy_d2h(ee.ctypes.data, e.value, ee.nbytes), "d2h")
         return dd, cc, ee
 

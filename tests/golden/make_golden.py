@@ -142,6 +142,28 @@ def gen_tdec8(rng):
         data[f"rm{ri}_e1"], data[f"rm{ri}_e2"] = e1, e2
         data[f"rm{ri}_out1"], data[f"rm{ri}_out2"] = first[: 3 * (K + 32) + 12], out[: 3 * (K + 32) + 12]
     data["rm_n"] = np.int32(len(rm))
+    # srslte_demod_soft_demodulate_b (SSE bodies / scalar tails, saturation and int8 wrap) and srslte_scrambling_sb_offset
+    k = 0
+    for qm in (2, 4, 6, 8):
+        for n in (1, 3, 7, 8, 9, 16, 17, 100, 301):
+            for amp in (1.0, 3.0, 9.0):
+                sym = (amp * (rng.standard_normal(n) + 1j * rng.standard_normal(n)) / np.sqrt(2)).astype(np.complex64)
+                iq = np.ascontiguousarray(sym.view(np.float32))
+                out = np.zeros(qm * n + 64, np.int8)
+                assert R.ref_demod_soft_b(qm, iq, out, n) == 0
+                data[f"dm{k}_qm"], data[f"dm{k}_sym"], data[f"dm{k}_llr"] = np.int32(qm), sym, out[: qm * n].copy()
+                k += 1
+    data["dm_n"] = np.int32(k)
+    k = 0
+    for (rnti, cw, sf, cid, n) in [(0x1234, 0, 3, 1, 1000), (0xffff, 1, 9, 503, 4097), (61, 0, 0, 0, 33)]:
+        c_init = oracle.pdsch_c_init(rnti, cw, sf, cid)
+        llr = rng.integers(-128, 128, n, dtype=np.int8)
+        llr[:4] = [-128, 127, 0, -1]
+        out = llr.copy()
+        assert R.ref_scramble_sb(c_init, out, 0, n) == 0
+        data[f"sb{k}_cinit"], data[f"sb{k}_in"], data[f"sb{k}_out"] = np.uint32(c_init), llr, out
+        k += 1
+    data["sb_n"] = np.int32(k)
     np.savez_compressed(os.path.join(OUT, "tdec8.npz"), **data)
     print("tdec8.npz:", len(cases), "decoder cases,", len(rm), "rate-dematching cases")
 

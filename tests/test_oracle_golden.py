@@ -91,3 +91,18 @@ def test_tdec8_goldens_sane():
             hi += 1
             assert (np.unpackbits(z[f"c{i}_trace"][1]) != z[f"c{i}_bits"]).mean() < 2e-3
     assert hi == 3
+
+
+def test_llr8_restatement_matches_reference_goldens():
+    """tests/llr8_ref.py (the checker of the GPU int8 LLR kernel) against srslte_demod_soft_demodulate_b and
+    srslte_scrambling_sb_offset as the reference computes them (SIMD bodies, scalar tails, saturation, wrap)."""
+    import oracle
+    from tests import llr8_ref
+    z = load("tdec8.npz")
+    for k in range(int(z["dm_n"])):
+        got = llr8_ref.demod_b(z[f"dm{k}_sym"], int(z[f"dm{k}_qm"]))
+        np.testing.assert_array_equal(got, z[f"dm{k}_llr"], err_msg=f"demod case {k} qm={int(z[f'dm{k}_qm'])}")
+    for k in range(int(z["sb_n"])):
+        n = z[f"sb{k}_in"].size
+        c = oracle.sequence_lte(int(z[f"sb{k}_cinit"]), n)
+        np.testing.assert_array_equal(llr8_ref.scramble_sb(z[f"sb{k}_in"], c), z[f"sb{k}_out"])
