@@ -79,6 +79,18 @@ int mi355_enb_dl_gen_signal_batch(mi355_enb_dl_t* q, const float* const* grids, 
 int mi355_channel_grid_batch(mi355_enb_dl_t* q, const float* const* tx, float* const* rx, uint32_t n,
                              uint32_t nof_rx, const float* H, float sigma, uint64_t seed, void* stream);
 
+/* Multipath fading test channel in the resource grid (srslte_channel_fading_t, channel/fading.c): model is the
+ * reference's string ("none<Fd>", "epa<Fd>", "eva<Fd>", "etu<Fd>", Fd the Doppler in Hz; parse_model,
+ * fading.c:48-78), taps and powers of 36.104 B.2 (fading.c:33-46), per link (rx r, port p) the Jakes phases
+ * std::mt19937(seed + r * nof_ports + p) draws as srslte_channel_fading_init does (fading.c:236-245), tap gains as
+ * get_doppler_dispersion (fading.c:143-152) at the centre of each OFDM symbol of job i's subframe starting at
+ * t_sf[i] seconds (host array), tap delays as phase ramps over the subcarriers.  Block fading per OFDM symbol
+ * (no inter-carrier interference), no path delay (the receiver's timing absorbs it).  AWGN as
+ * mi355_channel_grid_batch, keyed by (seed, i, r, k). */
+int mi355_channel_fading_grid_batch(mi355_enb_dl_t* q, const float* const* tx, float* const* rx, uint32_t n,
+                                    uint32_t nof_rx, const char* model, const double* t_sf, float sigma,
+                                    uint32_t seed, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

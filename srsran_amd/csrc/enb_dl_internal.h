@@ -58,6 +58,21 @@ struct EnbCrsJob {
   uint32_t sf;
 };
 
+// multipath fading test channel (srslte_channel_fading_t, fading.c): 36.104 B.2 tap tables, Jakes terms per tap
+constexpr uint32_t FADING_MAXTAPS = 9, FADING_NTERMS = 16;
+
+struct EnbFadingArgs {
+  const EnbChanJob* jobs;
+  const double*     t_sf;  // start time of each job's subframe (s)
+  const float*      coef;  // [link][tap][term] (a, b) phases, link = rx * nports + port
+  const float2*     steer; // [tap][nre]: exp(-j 2 pi f_k tau_tap) of grid subcarrier k
+  float2*           G;     // [job][symbol][link][tap] tap gains at the symbol centres
+  float             amp[FADING_MAXTAPS], cos_alpha[FADING_MAXTAPS];
+  float             doppler, sigma, tsym;
+  uint64_t          seed;
+  uint32_t          ntaps, nlinks, nports, nrx, nsym, nre;
+};
+
 hipError_t enb_launch_tb_crc(const EnbTbDev* tb, uint32_t ntb, const CrcTable* crc24a, hipStream_t s);
 hipError_t enb_launch_cb_encode(const EnbCbDev* cb, uint32_t ncb, const CrcTable* crc24b, hipStream_t s);
 hipError_t enb_launch_map(const EnbMapDev* jobs, uint32_t njobs, uint32_t max_units, hipStream_t s);
@@ -65,5 +80,6 @@ hipError_t enb_launch_crs(const EnbCrsJob* jobs, uint32_t njobs, const float2* p
                           uint32_t nof_ports, uint32_t cell_id, uint32_t nsymb, hipStream_t s);
 hipError_t enb_launch_channel(const EnbChanJob* jobs, uint32_t njobs, uint32_t nof_re, uint32_t nports, uint32_t nrx,
                               const EnbChanMat& H, float sigma, uint64_t seed, hipStream_t s);
+hipError_t enb_launch_fading(const EnbFadingArgs& a, uint32_t njobs, hipStream_t s);
 
 } // namespace mi355

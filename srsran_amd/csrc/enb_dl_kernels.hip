@@ -347,7 +347,81 @@ __global__ __launch_bounds__(256) void enb_channel(const EnbChanJob* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------- fading test channel
+// Tap gains of srslte_channel_fading_t (get_doppler_dispersion, fading.c:110-154, its generic branch) at every
+// OFDM symbol centre: g = amp / sqrt(NTERMS) sum_j [cos(w + a_j) + i sin(w + b_j)], w = pi F_d cos(alpha) t.
+// The phase is formed in double and wrapped (t grows without bound over a long run).
+__global__ __launch_bounds__(256) void enb_fading_gains(EnbFadingArgs a, uint32_t total)
+{
+  const uint32_t u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= total) return;
+  const uint32_t tap = u % a.ntaps, link = (u / a.ntaps) % a.nlinks, sym = (u / (a.ntaps * a.nlinks)) % a.nsym;
+  const uint32_t job = u / (a.ntaps * a.nlinks * a.nsym);
+  const double   t   = a.t_sf[job] + ((double)sym + 0.5) * (double)a.tsym;
+  const double   w   = 3.141592653589793 * (double)a.doppler * (double)a.cos_alpha[tap] * t;
+  const float    arg = (float)(w - 6.283185307179586 * floor(w / 6.283185307179586));
+  const float*   c   = a.coef + ((size_t)link * FADING_MAXTAPS + tap) * FADING_NTERMS * 2;
+  float          re = 0.f, im = 0.f;
+#pragma unroll
+  for (uint32_t j = 0; j < FADING_NTERMS; j++) {
+    re += cosf(arg + c[2 * j]);
+    im += sinf(arg + c[2 * j + 1]);
+  }
+  const float s = a.amp[tap] * 0.25f; // 1 / sqrt(NTERMS)
+  a.G[u]        = make_float2(re * s, im * s);
+}
+
+// thread per RE: H_rp(l, k) = sum_tap G[l][rp][tap] steer[tap][k]; y_r = sum_p H_rp x_p + AWGN
+__global__ __launch_bounds__(256) void enb_fading_apply(EnbFadingArgs a, uint32_t job0)
+{
+  const uint32_t    job = job0 + blockIdx.y;
+  const EnbChanJob& J   = a.jobs[job];
+  const uint32_t    k   = blockIdx.x * 256 + threadIdx.x;
+  if (k >= a.nsym * a.nre) return;
+  const uint32_t l = k / a.nre, sc = k - l * a.nre;
+  const float2*  G = a.G + ((size_t)job * a.nsym + l) * a.nlinks * a.ntaps;
+  float2         x[4];
+  for (uint32_t p = 0; p < a.nports; p++) x[p] = J.tx[p][k];
+  for (uint32_t r = 0; r < a.nrx; r++) {
+    float2 y = make_float2(0.f, 0.f);
+    for (uint32_t p = 0; p < a.nports; p++) {
+      const float2* g = G + (r * a.nports + p) * a.ntaps;
+      float2        h = make_float2(0.f, 0.f);
+      for (uint32_t i = 0; i < a.ntaps; i++) {
+        const float2 st = a.steer[i * a.nre + sc];
+        h.x += g[i].x * st.x - g[i].y * st.y;
+        h.y += g[i].x * st.y + g[i].y * st.x;
+      }
+      y.x += h.x * x[p].x - h.y * x[p].y;
+      y.y += h.x * x[p].y + h.y * x[p].x;
+    }
+    if (a.sigma > 0.f) {
+      const uint64_t z  = splitmix64(a.seed ^ splitmix64(((uint64_t)job << 32) | ((uint64_t)r << 28) | k));
+      const float    u1 = ((float)(uint32_t)(z >> 40) + 1.0f) * (1.0f / 16777216.0f);
+      const float    u2 = (float)(uint32_t)((z >> 16) & 0xffffffu) * (1.0f / 16777216.0f);
+      const float    rad = sqrtf(-2.0f * logf(u1));
+      float          sn, cs;
+      sincosf(6.283185307179586f * u2, &sn, &cs);
+      y.x += a.sigma * rad * cs;
+      y.y += a.sigma * rad * sn;
+    }
+    J.rx[r][k] = y;
+  }
+}
+
 // ---------------------------------------------------------------------------- launchers
+hipError_t enb_launch_fading(const EnbFadingArgs& a, uint32_t njobs, hipStream_t s)
+{
+  if (!njobs) return hipSuccess;
+  const uint32_t total = njobs * a.nsym * a.nlinks * a.ntaps;
+  hipLaunchKernelGGL(enb_fading_gains, dim3((total + 255) / 256), dim3(256), 0, s, a, total);
+  for (uint32_t j0 = 0; j0 < njobs; j0 += 65535) {
+    const uint32_t n = njobs - j0 < 65535 ? njobs - j0 : 65535;
+    hipLaunchKernelGGL(enb_fading_apply, dim3((a.nsym * a.nre + 255) / 256, n), dim3(256), 0, s, a, j0);
+  }
+  return hipGetLastError();
+}
+
 hipError_t enb_launch_tb_crc(const EnbTbDev* tb, uint32_t ntb, const CrcTable* crc24a, hipStream_t s)
 {
   if (!ntb) return hipSuccess;

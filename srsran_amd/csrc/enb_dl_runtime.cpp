@@ -9,7 +9,9 @@
 #include <cmath>
 #include <map>
 #include <mutex>
+#include <random>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 #include <vector>
@@ -459,6 +461,125 @@ int mi355_enb_dl_gen_signal_batch(mi355_enb_dl_t* q, const float* const* grids, 
   OfdmArgs a = q->ofdm;
   a.jobs     = (const OfdmJob*)base;
   CHECK_HIP(ofdm_launch_tx(a, 0.05f / sqrtf((float)q->cell.nof_prb), n, s)); // enb_dl_get_norm_factor
+  if (!stream) CHECK_HIP(hipStreamSynchronize(s));
+  return MI355_SUCCESS;
+}
+
+namespace {
+// 36.104 R10 B.2 multi-path fading propagation conditions (the tables of fading.c:33-46): none, EPA, EVA, ETU
+const uint32_t fading_ntaps[4]                     = {1, 7, 9, 9};
+const float    fading_delay_ns[4][FADING_MAXTAPS] = {{0},
+                                                     {0, 30, 70, 90, 110, 190, 410},
+                                                     {0, 30, 150, 310, 370, 710, 1090, 1730, 2510},
+                                                     {0, 50, 120, 200, 230, 500, 1600, 2300, 5000}};
+const float    fading_power_db[4][FADING_MAXTAPS] = {{0.0f},
+                                                     {0.0f, -1.0f, -2.0f, -3.0f, -8.0f, -17.2f, -20.8f},
+                                                     {0.0f, -1.5f, -1.4f, -3.6f, -0.6f, -9.1f, -7.0f, -12.0f, -16.9f},
+                                                     {-1.0f, -1.0f, -1.0f, 0.0f, 0.0f, 0.0f, -3.0f, -5.0f, -7.0f}};
+
+// "none" / "epa" / "eva" / "etu" followed by the Doppler frequency (parse_model, fading.c:48-78)
+int parse_fading(const char* str, uint32_t* model, float* doppler)
+{
+  if (!str) return -1;
+  size_t off = 3;
+  if (strncmp("none", str, 4) == 0) {
+    *model = 0;
+    off    = 4;
+  } else if (strncmp("epa", str, 3) == 0) {
+    *model = 1;
+  } else if (strncmp("eva", str, 3) == 0) {
+    *model = 2;
+  } else if (strncmp("etu", str, 3) == 0) {
+    *model = 3;
+  } else {
+    return -1;
+  }
+  if (strlen(str) <= off) return -1;
+  const float d = (float)strtod(str + off, nullptr);
+  *doppler      = (std::isnan(d) || std::isinf(d)) ? 0.0f : d;
+  return 0;
+}
+} // namespace
+
+int mi355_channel_fading_grid_batch(mi355_enb_dl_t* q, const float* const* tx, float* const* rx, uint32_t n,
+                                    uint32_t nof_rx, const char* model, const double* t_sf, float sigma, uint32_t seed,
+                                    void* stream)
+{
+  uint32_t m  = 0;
+  float    fd = 0.f;
+  if (!q || nof_rx == 0 || nof_rx > 2 || (n && (!tx || !rx || !t_sf)) || !(sigma >= 0.f) || parse_fading(model, &m, &fd))
+    return MI355_ERROR_INVALID_INPUTS;
+  if (!n) return MI355_SUCCESS;
+  std::lock_guard<std::mutex> lk(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t    s  = stream ? (hipStream_t)stream : q->own;
+  const uint32_t np = q->cell.nof_ports, nl = nof_rx * np, ntaps = fading_ntaps[m];
+  const uint32_t nre = q->ofdm.nre, nsym = 2 * q->ofdm.nsymb;
+  std::vector<EnbChanJob> jobs(n);
+  for (uint32_t i = 0; i < n; i++) {
+    jobs[i] = EnbChanJob{};
+    for (uint32_t p = 0; p < np; p++) {
+      if (!tx[(size_t)i * np + p]) return MI355_ERROR_INVALID_INPUTS;
+      jobs[i].tx[p] = (const float2*)tx[(size_t)i * np + p];
+    }
+    for (uint32_t r = 0; r < nof_rx; r++) {
+      if (!rx[(size_t)i * nof_rx + r]) return MI355_ERROR_INVALID_INPUTS;
+      jobs[i].rx[r] = (float2*)rx[(size_t)i * nof_rx + r];
+    }
+  }
+  // Jakes phases per link: one generator per link, tap-major, a before b (fading.c:236-245)
+  std::vector<float> coef((size_t)nl * FADING_MAXTAPS * FADING_NTERMS * 2, 0.0f);
+  for (uint32_t l = 0; l < nl; l++) {
+    std::mt19937 rng(seed + l);
+    for (uint32_t i = 0; i < ntaps; i++) {
+      for (uint32_t j = 0; j < FADING_NTERMS; j++) {
+        float* c = &coef[(((size_t)l * FADING_MAXTAPS + i) * FADING_NTERMS + j) * 2];
+        c[0]     = std::uniform_real_distribution<float>(0.0f, 2.0f * (float)M_PI)(rng);
+        c[1]     = std::uniform_real_distribution<float>(0.0f, 2.0f * (float)M_PI)(rng);
+      }
+    }
+  }
+  EnbFadingArgs A{};
+  for (uint32_t i = 0; i < ntaps; i++) {
+    A.amp[i]       = powf(10.0f, fading_power_db[m][i] / 10.0f); // srslte_convert_dB_to_power (vector.h:70-73)
+    A.cos_alpha[i] = cosf(((float)M_PI * ((float)i - 0.5f)) / (2.0f * (float)ntaps));
+  }
+  // subcarrier k of the grid sits at (k - nre/2) * 15 kHz below DC and (k - nre/2 + 1) * 15 kHz above it
+  std::vector<float2> steer((size_t)ntaps * nre);
+  for (uint32_t i = 0; i < ntaps; i++) {
+    for (uint32_t k = 0; k < nre; k++) {
+      const double f  = ((double)k - (double)(nre / 2) + (k >= nre / 2 ? 1.0 : 0.0)) * 15e3;
+      const double ph = -2.0 * M_PI * f * (double)fading_delay_ns[m][i] * 1e-9;
+      steer[(size_t)i * nre + k] = make_float2((float)cos(ph), (float)sin(ph));
+    }
+  }
+  const size_t sj = staged_size(n * sizeof(EnbChanJob)), stt = staged_size((size_t)n * 8),
+               sc = staged_size(coef.size() * 4), ss = staged_size(steer.size() * 8);
+  const size_t gbytes = (size_t)n * nsym * nl * ntaps * sizeof(float2);
+  char*        base   = nullptr;
+  if (get_scratch(q, sj + stt + sc + ss + gbytes, &base)) return MI355_ERROR;
+  if (q->st.reserve(sj + stt + sc + ss) != hipSuccess) return MI355_ERROR;
+  const size_t o_j = q->st.put(jobs.data(), n * sizeof(EnbChanJob));
+  const size_t o_t = q->st.put(t_sf, (size_t)n * 8);
+  const size_t o_c = q->st.put(coef.data(), coef.size() * 4);
+  const size_t o_s = q->st.put(steer.data(), steer.size() * 8);
+  if (upload_on(q->st, base, s)) return MI355_ERROR;
+  A.jobs    = (const EnbChanJob*)(base + o_j);
+  A.t_sf    = (const double*)(base + o_t);
+  A.coef    = (const float*)(base + o_c);
+  A.steer   = (const float2*)(base + o_s);
+  A.G       = (float2*)(base + sj + stt + sc + ss);
+  A.doppler = fd;
+  A.sigma   = sigma;
+  A.tsym    = 1e-3f / (float)nsym;
+  A.seed    = seed;
+  A.ntaps   = ntaps;
+  A.nlinks  = nl;
+  A.nports  = np;
+  A.nrx     = nof_rx;
+  A.nsym    = nsym;
+  A.nre     = nre;
+  CHECK_HIP(enb_launch_fading(A, n, s));
   if (!stream) CHECK_HIP(hipStreamSynchronize(s));
   return MI355_SUCCESS;
 }

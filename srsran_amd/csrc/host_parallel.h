@@ -34,11 +34,14 @@ public:
     }
     {
       std::lock_guard<std::mutex> lk(m_);
+      // a worker of the previous call may still be about to claim (and miss) a part: let it leave first, or it
+      // would claim a part of this call twice.  Workers enter under m_, so none can start while it is held.
+      while (inside_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
       fn_    = &fn;
       n_     = n;
       parts_ = T;
-      next_.store(1, std::memory_order_relaxed); // part 0 is the caller's
       left_.store(T, std::memory_order_relaxed);
+      next_.store(1, std::memory_order_relaxed); // part 0 is the caller's
       gen_++;
     }
     cv_.notify_all();
@@ -89,12 +92,14 @@ private:
         cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
         if (stop_) return;
         seen = gen_;
+        inside_.fetch_add(1, std::memory_order_relaxed);
       }
       while (true) {
         const uint32_t k = next_.fetch_add(1, std::memory_order_acq_rel);
         if (k >= parts_) break;
         run_part(k);
       }
+      inside_.fetch_sub(1, std::memory_order_release);
     }
   }
 
@@ -105,7 +110,7 @@ private:
   uint32_t                                         n_ = 0, parts_ = 0;
   uint64_t                                         gen_ = 0;
   bool                                             stop_ = false;
-  std::atomic<uint32_t>                            next_{0}, left_{0};
+  std::atomic<uint32_t>                            next_{0}, left_{0}, inside_{0};
 };
 
 inline void host_parallel_for(uint32_t n, uint32_t min_chunk, const std::function<void(uint32_t, uint32_t)>& fn)

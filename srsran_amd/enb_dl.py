@@ -63,6 +63,8 @@ def _declare_gpu():
     L.mi355_enb_dl_gen_signal_batch.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), u32, vp]
     L.mi355_channel_grid_batch.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), u32, u32, C.POINTER(C.c_float),
                                            C.c_float, C.c_uint64, vp]
+    L.mi355_channel_fading_grid_batch.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), u32, u32, C.c_char_p,
+                                                  C.POINTER(C.c_double), C.c_float, u32, vp]
     L._enb_gpu_declared = True
     return L
 
@@ -101,6 +103,15 @@ class EnbDl:
         hf = (C.c_float * len(h))(*h.tolist())
         check(self.L.mi355_channel_grid_batch(self.h, _arr(C.c_void_p, tx), _arr(C.c_void_p, rx), n, nof_rx, hf,
                                               float(sigma), int(seed) & (2**64 - 1), stream), "channel_grid")
+
+    def fading(self, tx, rx, nof_rx: int, model: str, t_sf, sigma: float, seed: int, stream=None):
+        """Multipath fading (srslte_channel_fading_t: model "epa5", "eva70", "etu300", "none0" ...) + AWGN in the
+        grid; job i's subframe starts at t_sf[i] seconds."""
+        n = len(rx) // nof_rx
+        ts = (C.c_double * max(n, 1))(*[float(t) for t in t_sf][:n])
+        check(self.L.mi355_channel_fading_grid_batch(self.h, _arr(C.c_void_p, tx), _arr(C.c_void_p, rx), n, nof_rx,
+                                                     model.encode(), ts, float(sigma), int(seed) & 0xFFFFFFFF,
+                                                     stream), "channel_fading")
 
     def close(self):
         if getattr(self, "h", None):
