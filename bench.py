@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """bench.py -- PDSCH receive on MI355X: decoded Mbps + code blocks/s on 20 MHz TM4 2x2 QAM256 subframes
-(BASELINE.json metric; configs[3] at N = 1, configs[4] as the weak-scaling multi-GPU run).
+(BASELINE.json metric; configs[3] at N = 1, configs[4] as the sharded multi-GPU run).
 
 Workload (one "step", per GPU): B subframes (default 2048 = 65,536 code blocks) of 100 PRB, 2 ports x 2 rx
 antennas, CFI 1, TM4 closed-loop spatial multiplexing with 2 codewords (codebook 0), MCS 27 QAM256 with
@@ -10,18 +10,22 @@ time-domain I/Q already resident in HBM:
     softbuffer reset (new TBs) -> OFDM demodulation (2 x 14 x 1536-pt DFT) -> CRS channel estimation
     (AVERAGE, Gauss, REFS noise) -> RE extraction + MMSE + demap + descramble + CSI -> rate dematching ->
     turbo decoding with per-CB CRC early stop -> TB CRC.
-Synthetic data (generated before the timed region): random payloads -> the product's GPU eNodeB generator
-(include/srsran_amd/enb_dl.h: DL-SCH encode, QAM256, TM4 precoding, CRS) -> phy_dl_test's crossed 2x2 channel
-[[1,1],[1,-1]] + AWGN (40 dB) -> IFFT + CP; every subframe of the batch distinct (sf_idx cycling 0..9), seeded
-per rank.  --gen host: D distinct subframes from the host encoder tiled over the batch (the earlier data).
+Synthetic data (generated before the timed region, keyed by the subframe's GLOBAL index i, so any shard of a run
+regenerates its own subframes): payloads = mi355_enb_synth_payloads(i) -> the product's GPU eNodeB generator
+(DL-SCH encode, QAM256, TM4 precoding, CRS) -> phy_dl_test's crossed 2x2 channel [[1,1],[1,-1]] + AWGN keyed by i
+(40 dB) -> IFFT + CP; sf_idx = i % 10.
 
-    python bench.py [--gpus N --steps K --warmup W]            # N > 1: launched by torch.distributed.run
-    python bench.py --workload tdec                            # configs[1]: batched turbo decode only
-    python bench.py --workload ue_dl                           # + PCFICH / PDCCH blind search -> DCI -> grant
-                                                               #   (phy_dl_test.c:194-247 work_ue per subframe)
+    python bench.py [--gpus N --steps K --warmup W]     # N > 1: re-launches itself under torch.distributed.run
+    python bench.py --gpus 8 --total-subframes 1048576  # configs[4]: 1M subframes sharded contiguously by rank
+    python bench.py --workload tdec                     # configs[1]: batched turbo decode only
+    python bench.py --workload ue_dl                    # + PCFICH / PDCCH blind search -> DCI -> grant
+    python bench.py --workload plumbing --gpus 2        # CPU dry run of the launcher / sharding / bitmap gather
 
-Multi-GPU: weak scaling -- every rank decodes its own B subframes (independent subframes shard with no
-data-path collective); ranks only meet at the timing barriers and the max-over-ranks reduction.
+Multi-GPU: one process per GPU.  Default: weak scaling, rank r decodes subframes [r B, (r+1) B) every step.
+--total-subframes T: rank r owns the contiguous shard [r T / N, (r+1) T / N), generated on its own GPU by index
+and decoded once in batches of B (the shard is held in HBM in resident sets of at most --resident-gb of I/Q).
+No data-path collective: ranks meet at the timing barriers, the max-over-ranks job time and one all-gather of
+the per-subframe CRC bitmaps (2 bits per subframe, RCCL over xGMI) to rank 0.
 
 Prints ONE JSON line on rank 0 (schema: DESIGN.md "Measurement").
 """
@@ -29,9 +33,12 @@ from __future__ import annotations
 
 import argparse
 import ctypes as C
+import hashlib
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,37 +48,68 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # lane-ops/s: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz
-# the MAP kernel's instructions are packed int16 (v_pk_add_i16 clamp / v_pk_max_i16), which issue at half that
-# rate on gfx950: tools/microbench/valu_rate.hip measured 0.555 wave-instr/ns/SIMD (profiles/r01c_valu_rate.txt)
-VALU_PK_I16_TOPS = 0.555 * 64 * 1024 / 1e3
+# "~78.6 T packed-int16 ops/s (256 CU x 128 ops/clk x 2.4 GHz)"; ~4.3 M int16 ops per CB
+# per 8-half-iteration decode and 37,848 compulsory HBM bytes per CB per decode
+VALU_PEAK_I16_TOPS = 256 * 128 * 2.4e9 / 1e12
+SURVEY_OPS_PER_CB_HALFIT = 4.3e6 / 8
+SURVEY_BYTES_PER_CB_DECODE = 37848
 METRIC = "PDSCH decoded Mbps + code-blocks/sec, 20 MHz TM4 QAM256, 1/2/4/8 GPU"
+TBS = 97896
+NB = TBS // 8
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_tdec_pmc.json")
+MAP_SOURCES = ("srsran_amd/csrc/tdec_kernels.hip", "srsran_amd/csrc/tdec_internal.h", "srsran_amd/csrc/lte_qpp_table.h")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["pdsch", "ue_dl", "tdec", "enb"], default="pdsch",
+    ap.add_argument("--workload", choices=["pdsch", "ue_dl", "tdec", "enb", "plumbing"], default="pdsch",
                     help="pdsch: known grants (decode_batch); ue_dl: phy_dl_test's work_ue with the PCFICH / PDCCH "
                          "blind search deriving every grant (find_and_decode); tdec: configs[1]; enb: the GPU "
-                         "eNodeB generator (encode side, SURVEY 8f row 2)")
-    ap.add_argument("--subframes", type=int, default=2048, help="TM4 subframes per GPU per step")
-    ap.add_argument("--gen", choices=["device", "host"], default="device",
-                    help="device: every subframe of the batch distinct, synthesised by the product's GPU eNodeB "
-                         "generator (mi355_enb_dl_*); host: --distinct subframes from the host encoder, tiled")
-    ap.add_argument("--distinct", type=int, default=20, help="--gen host: distinct synthetic subframes tiled")
+                         "eNodeB generator (encode side, SURVEY 8f row 2); plumbing: CPU dry run of the multi-rank "
+                         "launcher, sharding and CRC-bitmap gather (no GPU, no decoding)")
+    ap.add_argument("--subframes", type=int, default=2048, help="TM4 subframes per GPU per step (batch)")
+    ap.add_argument("--total-subframes", type=int, default=0,
+                    help="configs[4]: T subframes sharded contiguously over the ranks, each decoded once")
+    ap.add_argument("--resident-gb", type=float, default=96.0, help="HBM budget for one rank's resident I/Q")
+    ap.add_argument("--seed", type=int, default=4242)
     ap.add_argument("--snr", type=float, default=40.0)
+    ap.add_argument("--waterfall-snr", type=float, default=21.0,
+                    help="SNR of the decoder-bound e2e field (EPA 5 Hz fading)")
+    ap.add_argument("--no-waterfall", action="store_true")
     ap.add_argument("--ncb", type=int, default=65536, help="tdec workload: code blocks per GPU per step")
     ap.add_argument("--K", type=int, default=6144)
     ap.add_argument("--nhalf", type=int, default=8)
     ap.add_argument("--ebno", type=float, default=2.0)
     ap.add_argument("--pool", type=int, default=256, help="tdec workload: distinct code blocks tiled")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="skip the per-stage and MAP-kernel probes (profiling runs)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+# ====================================================================================== launcher / distributed
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def self_launch(args) -> None:
+    """`--gpus N` (N > 1) without a torch.distributed environment: start N rank processes under
+    torch.distributed.run and exit with its return code.  Nothing here touches the GPU (the ranks do)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd, env=env))
 
 
 def dist_backend() -> str:
@@ -79,12 +117,14 @@ def dist_backend() -> str:
     return os.environ.get("BENCH_DIST_BACKEND", "nccl")
 
 
-def dist_setup():
-    """One process per GPU (torch.distributed.run): the ranks share nothing but the timing barrier and the
-    max-over-ranks reduction -- subframes are independent, so there is no data-path collective."""
+def dist_setup(expect_world: int | None = None):
+    """One process per GPU (torch.distributed.run): the ranks share nothing but the timing barriers, the
+    max-over-ranks reduction and the CRC-bitmap gather -- subframes are independent."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if expect_world is not None and world != expect_world:
+        raise SystemExit(f"bench.py: --gpus {expect_world} but the launcher started WORLD_SIZE={world} ranks")
     pg = None
     if world > 1:
         import torch
@@ -107,12 +147,15 @@ def barrier(pg, local):
             pg.barrier()
 
 
+def _dev(local):
+    return f"cuda:{local}" if dist_backend() == "nccl" else "cpu"
+
+
 def max_over_ranks(pg, local, v: float) -> float:
     if pg is None:
         return v
     import torch
-    dev = f"cuda:{local}" if dist_backend() == "nccl" else "cpu"
-    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    t = torch.tensor([v], dtype=torch.float64, device=_dev(local))
     pg.all_reduce(t, op=pg.ReduceOp.MAX)
     return float(t.item())
 
@@ -121,14 +164,43 @@ def sum_over_ranks(pg, local, v: float) -> float:
     if pg is None:
         return v
     import torch
-    dev = f"cuda:{local}" if dist_backend() == "nccl" else "cpu"
-    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    t = torch.tensor([v], dtype=torch.float64, device=_dev(local))
     pg.all_reduce(t, op=pg.ReduceOp.SUM)
     return float(t.item())
 
 
+def gather_bitmap(pg, local, bits: np.ndarray):
+    """Per-subframe CRC bits of every rank (rank order) on rank 0: each rank packs its 0/1 bits (2 per subframe),
+    one all-gather of the packed bytes over RCCL (padded to the longest shard) and rank 0 trims each rank's part.
+    Returns the concatenated bits on rank 0, None elsewhere (the local bits without a process group)."""
+    bits = np.ascontiguousarray(bits, np.uint8)
+    if pg is None:
+        return bits
+    import torch
+    world, rank = pg.get_world_size(), pg.get_rank()
+    n = torch.tensor([bits.size], dtype=torch.int64, device=_dev(local))
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    pg.all_gather(ns, n)
+    ns = [int(x.item()) for x in ns]
+    nbytes = (max(ns) + 7) // 8
+    packed = np.zeros(nbytes, np.uint8)
+    p = np.packbits(bits)
+    packed[: p.size] = p
+    t = torch.from_numpy(packed).to(_dev(local))
+    outs = [torch.zeros_like(t) for _ in range(world)]
+    pg.all_gather(outs, t)
+    if rank != 0:
+        return None
+    return np.concatenate([np.unpackbits(o.cpu().numpy())[: ns[r]] for r, o in enumerate(outs)])
+
+
+def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous shard of rank r: [r T / N, (r + 1) T / N)."""
+    return total * rank // world, total * (rank + 1) // world
+
+
 def shard_seed(rank: int) -> int:
-    """Each rank synthesises its own subframes (weak scaling: per-GPU work fixed as N grows)."""
+    """Per-rank seed of the turbo-only workload's code-block pool (weak scaling: distinct work per rank)."""
     return 4242 + rank
 
 
@@ -137,51 +209,114 @@ def whole_job_rate(world: int, units_per_rank: int, steps: int, dt_max: float) -
     return world * units_per_rank * steps / dt_max
 
 
-def load_pmc():
-    p = os.path.join(ROOT, "profiles", "tdec_pmc_traffic.json")
-    if os.path.exists(p):
+def bitmap_summary(bits: np.ndarray, nsf: int) -> dict:
+    return {"subframes": nsf, "bits_per_subframe": 2, "length_bits": int(bits.size), "ok_tbs": int(bits.sum()),
+            "sha1": hashlib.sha1(np.packbits(bits).tobytes()).hexdigest()}
+
+
+# ====================================================================================== host facts
+
+def host_cores() -> tuple[int, dict]:
+    """CPU threads this process may use: the affinity mask, capped by the cgroup CPU quota (cpu.max / cfs)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except Exception:
         try:
-            return json.load(open(p))
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
         except Exception:
-            return None
-    return None
+            pass
+    n = aff if quota is None else max(1, min(aff, int(math.floor(quota))))
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return n, {"affinity_cpus": aff, "cgroup_quota_cpus": quota, "os_cpu_count": os.cpu_count(), "model": model}
+
+
+# ====================================================================================== roofline
+
+def map_kernel_hash() -> str:
+    h = hashlib.sha1()
+    for p in MAP_SOURCES:
+        h.update(open(os.path.join(ROOT, p), "rb").read())
+    return h.hexdigest()
+
+
+def load_pmc(ncb: int):
+    """PMC summary of the MAP kernel (tools/pmc_summary.py), accepted only if it was recorded on the current kernel
+    sources and the same launch size; otherwise (None, reason)."""
+    if not os.path.exists(PMC_FILE):
+        return None, "no PMC summary"
+    try:
+        pmc = json.load(open(PMC_FILE))
+    except Exception as e:  # noqa: BLE001
+        return None, f"unreadable PMC summary: {e}"
+    if pmc.get("kernel_src_sha1") != map_kernel_hash():
+        return None, "PMC summary recorded on different MAP kernel sources (stale): traffic not reported"
+    if pmc.get("launch_ncb") != ncb:
+        return None, f"PMC summary recorded at {pmc.get('launch_ncb')} CBs per launch, not {ncb}"
+    return pmc, None
 
 
 def tdec_roofline(ms, launches, ncb, K):
-    """Roofline of the MAP half-iteration kernel: algorithmic bytes per CB-half-iteration = DEC1 reads S, a1,
-    P0 and writes e; DEC2 reads e, P1 and writes a1 (int16 x K each) -> (4 + 3) / 2 * 2K on average."""
-    bytes_cb = 3.5 * 2 * K
+    """Roofline of the MAP half-iteration kernel (tdec_win_halfit) from HIP-event timing on its stream.
+    Primary (schema) entry: HBM against SURVEY 8(d)'s compulsory bytes, 37,848 B per CB per 8-half-iteration
+    decode (= 4,731 B per CB half-iteration).  The kernel is VALU-bound, so roofline_valu gives the
+    binding fraction: SURVEY's ~537.5 k int16 ops per CB half-iteration against 78.6 T ops/s."""
     avg = ms / max(launches, 1)
-    achieved = bytes_cb * ncb / (avg / 1e3) / 1e9
-    pmc = load_pmc() or {}
-    traffic = pmc.get("bytes_per_launch") if pmc.get("launch_ncb") == ncb else None
+    bytes_launch = SURVEY_BYTES_PER_CB_DECODE / 8 * ncb * K / 6144
+    achieved = bytes_launch / (avg / 1e3) / 1e9
+    pmc, why = load_pmc(ncb)
+    traffic = None
+    if pmc:
+        traffic = pmc["hbm_bytes_per_launch"]
+    design_bytes = 3.5 * 2 * K * ncb  # the design's own per-launch reads + writes (DESIGN.md 4)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "tdec_win_halfit<16,8>",
-            "avg_launch_ms": round(avg, 4), "algorithmic_bytes_per_launch": int(bytes_cb * ncb),
-            "cbs_per_launch": ncb}
-    valu = None
-    if pmc.get("valu_insts_per_launch") and pmc.get("launch_ncb") == ncb:
-        rate = pmc["valu_insts_per_launch"] * 64 / (avg / 1e3) / 1e12
-        valu = {"achieved": round(rate, 2), "peak": round(VALU_PEAK_TOPS, 1), "unit": "T lane-instr/s",
-                "frac": round(rate / VALU_PEAK_TOPS, 4), "peak_packed_i16": round(VALU_PK_I16_TOPS, 1),
-                "frac_packed_i16": round(rate / VALU_PK_I16_TOPS, 4),
-                "source": "SQ_INSTS_VALU, profiles/tdec_pmc_traffic.json; packed-int16 issue rate measured"}
+            "avg_launch_ms": round(avg, 4), "algorithmic_bytes_per_launch": int(bytes_launch),
+            "algorithmic_bytes_source": "SURVEY 8(d): 37,848 B per CB per decode / 8 half-iterations",
+            "design_bytes_per_launch": int(design_bytes),
+            "design_frac": round(design_bytes / (avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "cbs_per_launch": ncb, "binding_roof": "valu (roofline_valu)"}
+    if why:
+        roof["traffic_note"] = why
+    else:
+        roof["traffic_source"] = f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc.get('tag')}): 2 x FETCH_SIZE + WRITE_SIZE"
+    ops = SURVEY_OPS_PER_CB_HALFIT * ncb * K / 6144
+    rate = ops / (avg / 1e3) / 1e12
+    valu = {"bound": "valu", "achieved": round(rate, 2), "peak": round(VALU_PEAK_I16_TOPS, 1),
+            "unit": "T int16 ops/s", "frac": round(rate / VALU_PEAK_I16_TOPS, 4),
+            "ops_per_launch": int(ops), "ops_source": "SURVEY 8(d): ~4.3 M int16 ops per CB per 8 half-iterations"}
+    if pmc and pmc.get("valu_insts_per_launch"):
+        lane = pmc["valu_insts_per_launch"] * 64
+        valu["measured_valu_lane_instr_per_cb_halfit"] = round(lane / ncb)
+        valu["measured_lane_instr_rate_T"] = round(lane / (avg / 1e3) / 1e12, 2)
     return roof, valu
 
 
-# ====================================================================================== PDSCH (configs[3])
+# ====================================================================================== TM4 data + decoder
 
 def tm4_setup(nof_prb=100, cell_id=1):
     from srsran_amd import pdsch as P
-    cell = P.make_cell(nof_prb, 2, cell_id)
-    return cell
+    return P.make_cell(nof_prb, 2, cell_id)
 
 
 def tm4_cfg(P, cell, sf_idx, rnti=0x1234, softbuffers=(0, 1)):
     prb = np.ones((2, cell.nof_prb), np.uint8)
     g = P.make_grant(cell, prb, 1, sf_idx, P.TXSCHEME_SPATIALMUX, 2,
-                     [dict(mod=P.MOD_256QAM, tbs=97896, rv=0, cw_idx=0),
-                      dict(mod=P.MOD_256QAM, tbs=97896, rv=0, cw_idx=1)], pmi=0)
+                     [dict(mod=P.MOD_256QAM, tbs=TBS, rv=0, cw_idx=0),
+                      dict(mod=P.MOD_256QAM, tbs=TBS, rv=0, cw_idx=1)], pmi=0)
     cfg = P.PdschCfg()
     cfg.grant = g
     cfg.rnti = rnti
@@ -208,166 +343,124 @@ def tm4_dci_msg(cell, sf_idx, rnti=0x1234):
     return m
 
 
-def synth_tm4(cell, D, snr_db, seed, ctrl=False):
-    """D distinct subframes as time-domain I/Q (D, 2 rx, 15*N) + payloads, via the product encoder (with ctrl: the
-    PCFICH (CFI 1) and the subframe's DCI on the PDCCH too)."""
-    from srsran_amd import enb_dl
-    from srsran_amd import pdsch as P
-    from srsran_amd.ue_dl import symbol_sz
-    rng = np.random.default_rng(seed)
-    nre = 12 * cell.nof_prb
-    N = symbol_sz(cell.nof_prb)
-    cp0, cp1 = int(math.ceil(160 * N / 2048)), int(math.ceil(144 * N / 2048))
-    iq = np.zeros((D, 2, 15 * N), np.complex64)
-    payloads = []
-    sigma = math.sqrt(10 ** (-snr_db / 10) / 2)
-    for d in range(D):
-        sf = d % 10
-        cfg = tm4_cfg(P, cell, sf)
-        pl = [rng.integers(0, 256, 97896 // 8, dtype=np.uint8) for _ in range(2)]
-        payloads.append(pl)
-        grids = np.zeros((2, 14 * nre), np.complex64)
-        enb_dl.pdsch_encode(cell, P.DlSfCfg(sf, 1), cfg, pl, grids)
-        enb_dl.put_refs(cell, sf, grids)
-        if ctrl:
+class Tm4Source:
+    """Up to n_max TM4 subframes resident in HBM (I/Q per rx antenna + the transmitted payloads), synthesised on the
+    GPU by global subframe index with the product's eNodeB generator."""
+
+    def __init__(self, cell, n_max, device, ctrl=False, chunk=256):
+        from srsran_amd import enb_dl
+        from srsran_amd import pdsch as P
+        from srsran_amd.tdec import DeviceBuffer
+        from srsran_amd.ue_dl import symbol_sz
+        self.cell, self.n_max, self.device, self.ctrl = cell, n_max, device, ctrl
+        self.sf_len = 15 * symbol_sz(cell.nof_prb)
+        self.G, self.nre = 14 * 12 * cell.nof_prb, 12 * cell.nof_prb
+        self.d_iq = DeviceBuffer(n_max * 2 * self.sf_len * 8, device)
+        self.d_pl = DeviceBuffer(n_max * 2 * NB, device)
+        self.enb = enb_dl.EnbDl(cell, device)
+        self.chunk = min(chunk, n_max)
+        self.d_tx = DeviceBuffer(self.chunk * 2 * self.G * 8, device)
+        self.d_rx = DeviceBuffer(self.chunk * 2 * self.G * 8, device)
+        self.cfg_sf = {sf: tm4_cfg(P, cell, sf) for sf in range(10)}
+        self.rows = None
+        if ctrl:  # symbol 0 (CFI 1) of each port: CRS + PCFICH + the subframe's DCI on the PDCCH (host-encoded)
             from srsran_amd import pdcch as Dc
-            Dc.encode_ctrl_host(cell, sf, 1, [tm4_dci_msg(cell, sf)], grids)
-        # phy_dl_test crossed channel: rx0 = p0 + p1, rx1 = p0 - p1, plus AWGN per RE
-        y = np.stack([grids[0] + grids[1], grids[0] - grids[1]]).reshape(2, 14, nre)
-        y = y + sigma * (rng.standard_normal(y.shape) + 1j * rng.standard_normal(y.shape))
-        for r in range(2):
-            for s in range(14):
-                sl, l = divmod(s, 7)
-                X = np.zeros(N, np.complex128)
-                X[N - nre // 2:] = y[r, s, : nre // 2]
-                X[1: nre // 2 + 1] = y[r, s, nre // 2:]
-                t = np.fft.ifft(X)
-                cp = cp0 if l == 0 else cp1
-                start = sl * (15 * N // 2) + (0 if l == 0 else cp0 + N + (l - 1) * (N + cp1))
-                iq[d, r, start: start + cp] = t[N - cp:]
-                iq[d, r, start + cp: start + cp + N] = t
-    return iq, payloads
+            self.rows = {}
+            for sf in range(10):
+                g = np.zeros((2, self.G), np.complex64)
+                enb_dl.put_refs(cell, sf, g)
+                Dc.encode_ctrl_host(cell, sf, 1, [tm4_dci_msg(cell, sf)], g)
+                self.rows[sf] = np.ascontiguousarray(g[:, : self.nre])
+        self.first, self.n = 0, 0
 
+    def iq_ptr(self, k, r):
+        return self.d_iq.ptr + (k * 2 + r) * self.sf_len * 8
 
-def synth_tm4_device(cell, B, snr_db, seed, device, ctrl, d_iq, sf_len, chunk=256):
-    """B distinct subframes straight into d_iq (B x 2 rx x sf_len complex) with the product's GPU eNodeB generator:
-    random payloads -> mi355_enb_dl_put_pdsch_batch (TB/CB CRC, turbo coding, rate matching, scrambling, QAM256,
-    TM4 precoding, RE map) + put_refs (CRS) [+ the host-encoded PCFICH/PDCCH row of the subframe index, CFI 1] ->
-    phy_dl_test's crossed 2x2 channel + AWGN (mi355_channel_grid_batch) -> gen_signal (IFFT + CP).  Returns the
-    payloads (B, 2, tbs/8)."""
-    from srsran_amd import enb_dl, lib
-    from srsran_amd import pdsch as P
-    from srsran_amd.tdec import DeviceBuffer
-    rng = np.random.default_rng(seed)
-    G, nre, nb = 14 * 12 * cell.nof_prb, 12 * cell.nof_prb, 97896 // 8
-    payloads = rng.integers(0, 256, (B, 2, nb), dtype=np.uint8)
-    d_pl = DeviceBuffer(payloads.nbytes, device).upload(payloads)
-    enb = enb_dl.EnbDl(cell, device)
-    chunk = min(chunk, B)
-    d_tx = DeviceBuffer(chunk * 2 * G * 8, device)
-    d_rx = DeviceBuffer(chunk * 2 * G * 8, device)
-    cfg_sf = {sf: tm4_cfg(P, cell, sf) for sf in range(10)}
-    rows = None
-    if ctrl:  # symbol 0 (CFI 1) of each port: CRS + PCFICH + the subframe's DCI on the PDCCH
-        from srsran_amd import pdcch as Dc
-        rows = {}
-        for sf in range(10):
-            g = np.zeros((2, G), np.complex64)
-            enb_dl.put_refs(cell, sf, g)
-            Dc.encode_ctrl_host(cell, sf, 1, [tm4_dci_msg(cell, sf)], g)
-            rows[sf] = np.ascontiguousarray(g[:, :nre])
-    H = np.array([[1, 1], [1, -1]], np.complex64)
-    sigma = math.sqrt(10 ** (-snr_db / 10) / 2)
-    for c0 in range(0, B, chunk):
-        n = min(chunk, B - c0)
-        lib().mi355_memset_dev(d_tx.ptr, 0, n * 2 * G * 8)
-        jobs = []
-        tx = [d_tx.ptr + (k * 2 + p) * G * 8 for k in range(n) for p in range(2)]
-        rx = [d_rx.ptr + (k * 2 + r) * G * 8 for k in range(n) for r in range(2)]
-        for k in range(n):
-            i, sf = c0 + k, (c0 + k) % 10
-            j = enb_dl.EnbPdschJob()
-            j.sf.tti, j.sf.cfi = sf, 1
-            j.cfg = cfg_sf[sf]
-            for t in range(2):
-                j.data[t] = d_pl.ptr + (i * 2 + t) * nb
-            for p in range(2):
-                j.sf_symbols[p] = tx[2 * k + p]
-            jobs.append(j)
-        enb.put_pdsch(jobs)
-        enb.put_refs([(c0 + k) % 10 for k in range(n)], tx)
-        if ctrl:
-            for k in range(n):
+    def generate(self, first, n, snr_db, seed, fading=None):
+        """Subframes [first, first + n): payloads keyed by index -> put_pdsch -> put_refs [-> control row] ->
+        crossed 2x2 channel + AWGN keyed by index (or `fading`, a srslte_channel_fading_t model string) -> IFFT."""
+        from srsran_amd import enb_dl, lib
+        assert n <= self.n_max
+        self.first, self.n = first, n
+        enb, G = self.enb, self.G
+        enb.synth_payloads(self.d_pl.ptr, first, n, 2, NB, seed)
+        H = np.array([[1, 1], [1, -1]], np.complex64)
+        sigma = math.sqrt(10 ** (-snr_db / 10) / 2)
+        for c0 in range(0, n, self.chunk):
+            m = min(self.chunk, n - c0)
+            lib().mi355_memset_dev(self.d_tx.ptr, 0, m * 2 * G * 8)
+            tx = [self.d_tx.ptr + (k * 2 + p) * G * 8 for k in range(m) for p in range(2)]
+            rx = [self.d_rx.ptr + (k * 2 + r) * G * 8 for k in range(m) for r in range(2)]
+            jobs = []
+            for k in range(m):
+                i = first + c0 + k
+                j = enb_dl.EnbPdschJob()
+                j.sf.tti, j.sf.cfi = i % 10, 1
+                j.cfg = self.cfg_sf[i % 10]
+                for t in range(2):
+                    j.data[t] = self.d_pl.ptr + ((c0 + k) * 2 + t) * NB
                 for p in range(2):
-                    lib().mi355_memcpy_h2d(tx[2 * k + p], rows[(c0 + k) % 10][p].ctypes.data, nre * 8)
-        enb.channel(tx, rx, 2, H, sigma, seed * 1000003 + c0)
-        enb.gen_signal(rx, [d_iq.ptr + ((c0 + k) * 2 + r) * sf_len * 8 for k in range(n) for r in range(2)])
-    enb.close()
-    return payloads
+                    j.sf_symbols[p] = tx[2 * k + p]
+                jobs.append(j)
+            enb.put_pdsch(jobs)
+            enb.put_refs([(first + c0 + k) % 10 for k in range(m)], tx)
+            if self.rows is not None:
+                for k in range(m):
+                    for p in range(2):
+                        lib().mi355_memcpy_h2d(tx[2 * k + p], self.rows[(first + c0 + k) % 10][p].ctypes.data,
+                                               self.nre * 8)
+            if fading is None:
+                enb.channel(tx, rx, 2, H, sigma, seed, first_index=first + c0)
+            else:
+                enb.fading(tx, rx, 2, fading, [1e-3 * (first + c0 + k) for k in range(m)], sigma,
+                           (seed * 7919 + first + c0) & 0x7FFFFFFF)
+            enb.gen_signal(rx, [self.iq_ptr(c0 + k, r) for k in range(m) for r in range(2)])
+        lib().mi355_device_sync()
+
+    def payloads(self, k0, n):
+        """Transmitted payloads of resident subframes [k0, k0 + n) -> (n, 2, NB) host array."""
+        out = np.zeros((n, 2, NB), np.uint8)
+        from srsran_amd import lib
+        lib().mi355_memcpy_d2h(out.ctypes.data, self.d_pl.ptr + k0 * 2 * NB, out.nbytes)
+        return out
+
+    def iq_host(self, k0, n):
+        out = np.zeros((n, 2, self.sf_len), np.complex64)
+        from srsran_amd import lib
+        lib().mi355_memcpy_d2h(out.ctypes.data, self.iq_ptr(k0, 0), out.nbytes)
+        return out
+
+    def close(self):
+        self.enb.close()
 
 
-class Tm4Batch:
-    """B subframes resident in HBM with their grids, channel estimates, softbuffers and payload buffers."""
+class Tm4Rx:
+    """The UE side of one batch of B subframes: srslte_ue_dl_t + softbuffers + grids / estimates / payload buffers,
+    with job tables prebuilt per batch position of the resident set (no host work in the timed loop beyond the
+    library calls)."""
 
-    def __init__(self, cell, B, D, snr, seed, device, ctrl=False, gen="host"):
+    def __init__(self, cell, B, device, ctrl=False):
         from srsran_amd import lib
         from srsran_amd import pdsch as P
         from srsran_amd.dlsch import SoftbufferPool
         from srsran_amd.tdec import DeviceBuffer
-        from srsran_amd.ue_dl import DlSfJob, UeDl, default_chest_cfg
-        self.P, self.B, self.D = P, B, D
-        self.ctrl = ctrl
-        from srsran_amd.ue_dl import symbol_sz
-        sf_len = 15 * symbol_sz(cell.nof_prb)
-        G = 14 * 12 * cell.nof_prb
-        self.G = G
-        self.plen = 97896 // 8 + 16
-        # every subframe gets its own I/Q buffers, so the OFDM stage streams B inputs from HBM
-        self.d_iq = DeviceBuffer(B * 2 * sf_len * 8, device)
-        if gen == "device":  # all B subframes distinct, synthesised on the GPU
-            self.D = D = B
-            self.payloads = synth_tm4_device(cell, B, snr, seed, device, ctrl, self.d_iq, sf_len)
-            S = min(B, 10)  # the CPU baseline's sample
-            self.iq_host = np.zeros((S, 2, sf_len), np.complex64)
-            self.d_iq.download(self.iq_host)
-        else:  # D distinct host-encoded subframes tiled over the batch
-            self.iq_host, self.payloads = synth_tm4(cell, D, snr, seed, ctrl)
-            iq = np.ascontiguousarray(self.iq_host, np.complex64)
-            for i in range(B):
-                lib().mi355_memcpy_h2d(C.c_void_p(self.d_iq.ptr + i * 2 * sf_len * 8), iq[i % D].ctypes.data,
-                                       C.c_size_t(2 * sf_len * 8))
-        self.d_grid = DeviceBuffer(B * 2 * G * 8, device)
-        self.d_ce = DeviceBuffer(B * 4 * G * 8, device)
+        from srsran_amd.ue_dl import ChestRes, UeDl, _declare, default_chest_cfg
+        self.P, self.B, self.ctrl, self.cell = P, B, ctrl, cell
+        self.G = 14 * 12 * cell.nof_prb
+        self.plen = NB + 16
+        self.d_grid = DeviceBuffer(B * 2 * self.G * 8, device)
+        self.d_ce = DeviceBuffer(B * 4 * self.G * 8, device)
         self.d_pay = DeviceBuffer(B * 2 * self.plen, device)
         lib().mi355_memset_dev(self.d_pay.ptr, 0, B * 2 * self.plen)
         self.pool = SoftbufferPool(2 * B, max_cb=16, device=device)
         self.ue = UeDl(cell, 2, device)
         self.chest_cfg = default_chest_cfg()
-        self.jobs = (DlSfJob * B)()
-        self.sfs = (P.DlSfCfg * B)()
-        self.cfgs = (P.PdschCfg * B)()
-        self.pays = (C.c_void_p * (2 * B))()
-        self.res_chest = None
-        cfg_sf = {sf: tm4_cfg(P, cell, sf) for sf in range(10)}
-        for i in range(B):
-            d = i % D
-            j = self.jobs[i]
-            j.tti = d % 10
-            for r in range(2):
-                j.in_buffer[r] = self.d_iq.ptr + (i * 2 + r) * sf_len * 8
-                j.sf_symbols[r] = self.d_grid.ptr + (i * 2 + r) * G * 8
-                for p in range(2):
-                    j.ce[p][r] = self.d_ce.ptr + (i * 4 + p * 2 + r) * G * 8
-            self.sfs[i] = P.DlSfCfg(d % 10, 1)
-            self.cfgs[i] = cfg_sf[d % 10]
-            self.cfgs[i].softbuffer[0], self.cfgs[i].softbuffer[1] = 2 * i, 2 * i + 1
-            self.pays[2 * i] = self.d_pay.ptr + (2 * i) * self.plen
-            self.pays[2 * i + 1] = self.d_pay.ptr + (2 * i + 1) * self.plen
-        from srsran_amd.ue_dl import ChestRes, _declare
+        self.cfg_sf = {sf: tm4_cfg(P, cell, sf) for sf in range(10)}
         self.L = _declare()
         self.L.mi355_softbuffer_reset_range.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
         self.chest = (ChestRes * B)()
         self.res = (P.PdschRes * (2 * B))()
+        self.pays = (C.c_void_p * (2 * B))(*[self.d_pay.ptr + k * self.plen for k in range(2 * B)])
         if ctrl:
             from srsran_amd import pdcch as Dc
             self.Lc = Dc._declare()
@@ -377,193 +470,358 @@ class Tm4Batch:
             self.ctrl_res = (Dc.CtrlRes * B)()
             self.dci = (Dc.DciDl * (B * Dc.MAX_DCI_MSG))()
 
-    def step(self, stages=None):
-        """One batch: new-TB softbuffer reset + mi355_ue_dl_decode_batch (OFDM, estimation, PDSCH, DL-SCH).
-        With `stages`, the two-call form (decode_fft_estimate, then decode_pdsch) is timed per stage instead."""
+    def bind(self, src: Tm4Source, k0: int, n: int):
+        """Job tables for resident subframes [k0, k0 + n) of src (n <= B)."""
+        from srsran_amd.ue_dl import DlSfJob
+        P = self.P
+        jobs, sfs, cfgs = (DlSfJob * n)(), (P.DlSfCfg * n)(), (P.PdschCfg * n)()
+        for k in range(n):
+            i = src.first + k0 + k
+            j = jobs[k]
+            j.tti = i % 10
+            for r in range(2):
+                j.in_buffer[r] = src.iq_ptr(k0 + k, r)
+                j.sf_symbols[r] = self.d_grid.ptr + (k * 2 + r) * self.G * 8
+                for p in range(2):
+                    j.ce[p][r] = self.d_ce.ptr + (k * 4 + p * 2 + r) * self.G * 8
+            sfs[k] = P.DlSfCfg(i % 10, 1)
+            cfgs[k] = self.cfg_sf[i % 10]
+            cfgs[k].softbuffer[0], cfgs[k].softbuffer[1] = 2 * k, 2 * k + 1
+        return (jobs, sfs, cfgs, n, k0)
+
+    def step(self, bound, stages=None):
+        """One batch: new-TB softbuffer reset + mi355_ue_dl_decode_batch (OFDM, estimation, PDSCH, DL-SCH), or the
+        find_and_decode form with the control channels.  With `stages`, the two-call form (decode_fft_estimate,
+        then decode_pdsch) is timed per stage instead."""
         from srsran_amd import check, lib
-        t0 = time.perf_counter()
+        jobs, sfs, cfgs, n, _ = bound
+        C.memset(self.res, 0, C.sizeof(self.res))
         if self.ctrl:
             # find_and_decode resets each TB's softbuffer itself (ue_dl.c:1522-1529)
-            C.memset(self.res, 0, C.sizeof(self.res))
-            check(self.Lc.mi355_ue_dl_find_and_decode_batch(self.ue.h, self.pool.h, self.jobs, self.sfs, self.ue_cfgs,
-                                                            self.cfgs, C.byref(self.chest_cfg), self.chest, self.pays,
-                                                            self.B, self.ctrl_res, self.dci, self.res, None),
+            check(self.Lc.mi355_ue_dl_find_and_decode_batch(self.ue.h, self.pool.h, jobs, sfs, self.ue_cfgs, cfgs,
+                                                            C.byref(self.chest_cfg), self.chest, self.pays, n,
+                                                            self.ctrl_res, self.dci, self.res, None),
                   "ue_dl_find_and_decode_batch")
             return
-        check(self.L.mi355_softbuffer_reset_range(self.pool.h, 0, 2 * self.B, None), "softbuffer_reset_range")
-        C.memset(self.res, 0, C.sizeof(self.res))
+        check(self.L.mi355_softbuffer_reset_range(self.pool.h, 0, 2 * n, None), "softbuffer_reset_range")
         if stages is None:
-            check(self.L.mi355_ue_dl_decode_batch(self.ue.h, self.pool.h, self.jobs, self.sfs, self.cfgs,
-                                                  C.byref(self.chest_cfg), self.chest, self.pays, self.B, self.res,
-                                                  None), "ue_dl_decode_batch")
+            check(self.L.mi355_ue_dl_decode_batch(self.ue.h, self.pool.h, jobs, sfs, cfgs, C.byref(self.chest_cfg),
+                                                  self.chest, self.pays, n, self.res, None), "ue_dl_decode_batch")
             return
-        check(self.L.mi355_ue_dl_decode_fft_estimate_batch(self.ue.h, self.jobs, self.B, C.byref(self.chest_cfg),
-                                                           self.chest, None), "decode_fft_estimate")
+        t0 = time.perf_counter()
+        check(self.L.mi355_ue_dl_decode_fft_estimate_batch(self.ue.h, jobs, n, C.byref(self.chest_cfg), self.chest,
+                                                           None), "decode_fft_estimate")
         t1 = time.perf_counter()
-        check(self.L.mi355_ue_dl_decode_pdsch_batch(self.ue.h, self.pool.h, self.jobs, self.sfs, self.cfgs,
-                                                    self.chest, self.pays, self.B, self.res, None), "decode_pdsch")
+        check(self.L.mi355_ue_dl_decode_pdsch_batch(self.ue.h, self.pool.h, jobs, sfs, cfgs, self.chest, self.pays, n,
+                                                    self.res, None), "decode_pdsch")
         lib().mi355_device_sync()
         t2 = time.perf_counter()
-        stages["reset_fft_chest_ms"] = stages.get("reset_fft_chest_ms", 0) + (t1 - t0) * 1e3
+        stages["fft_chest_ms"] = stages.get("fft_chest_ms", 0) + (t1 - t0) * 1e3
         stages["pdsch_decode_ms"] = stages.get("pdsch_decode_ms", 0) + (t2 - t1) * 1e3
 
-    def check_payloads(self):
-        """All TBs CRC-ok and every payload equal to what the encoder was given (and, with the control channels,
-        exactly one DCI found per subframe)."""
-        host = np.zeros(self.B * 2 * self.plen, np.uint8)
-        self.d_pay.download(host)
-        host = host.reshape(self.B, 2, self.plen)
-        ok = 0
-        for i in range(self.B):
-            for t in range(2):
-                r = self.res[2 * i + t]
-                dci_ok = not self.ctrl or self.ctrl_res[i].nof_dci == 1
-                if dci_ok and r.crc and np.array_equal(host[i, t, : 97896 // 8], self.payloads[i % self.D][t]):
-                    ok += 1
-        its = float(np.mean([self.res[k].avg_iterations_block for k in range(2 * self.B)]))
-        return ok, its
+    def crc_bits(self, n):
+        """2 bits per subframe (TB0, TB1 CRC ok; with the control channels also exactly one DCI found)."""
+        r = np.ctypeslib.as_array(self.res)[: 2 * n]
+        bits = (r["crc"] != 0) & (r["ret"] == 0)
+        if self.ctrl:
+            nd = np.ctypeslib.as_array(self.ctrl_res)[:n]["nof_dci"]
+            bits &= np.repeat(nd == 1, 2)
+        return bits.astype(np.uint8)
+
+    def payload_ok(self, src: Tm4Source, bound):
+        """TBs whose CRC passed AND whose decoded bytes equal the transmitted payload."""
+        _, _, _, n, k0 = bound
+        host = np.zeros(n * 2 * self.plen, np.uint8)
+        from srsran_amd import lib
+        lib().mi355_memcpy_d2h(host.ctypes.data, self.d_pay.ptr, host.nbytes)
+        host = host.reshape(n, 2, self.plen)[:, :, :NB]
+        want = src.payloads(k0, n)
+        eq = np.all(host == want, axis=2).reshape(-1)
+        return int((eq & (self.crc_bits(n) == 1)).sum())
+
+    def avg_its(self, n):
+        return float(np.mean(np.ctypeslib.as_array(self.res)[: 2 * n]["avg_iterations_block"]))
 
 
-def cpu_baseline_pdsch(batch, nthreads, budget_s, avg_its):
-    """CPU reference-path timing on the host cores (rank 0, N = 1), bounded sample:
-    front-end (OFDM as a float64 numpy DFT, channel estimation and PDSCH symbol processing by the oracle's C
-    restatement of the reference) on S distinct subframes with a thread pool, plus the reference's own AVX2
-    turbo decoder (oracle/_ref, compiled from the srsLTE sources) on their 32 x S code blocks -- taken from
-    the GPU's softbuffers after rate dematching -- for ceil(avg half-iterations) half-iterations."""
+def cpu_baseline_pdsch(src: Tm4Source, gpu_bufs, avg_its, budget_s):
+    """CPU reference-path timing on the host cores (rank 0, N = 1), bounded sample of the same workload:
+    S subframes' I/Q (downloaded from HBM) through oracle/orc_front.c's C chain (OFDM by a float Stockham FFT,
+    estimation, RE extraction, MMSE + CSI, demapping, descrambling, rate dematching -- the oracle's scalar C
+    restatement, one subframe per thread task) and their 32 S code blocks through the reference's own AVX2 turbo
+    decoder (oracle/_ref, compiled from the srsLTE sources) for ceil(avg half-iterations) half-iterations;
+    1 thread and every usable core.  gpu_bufs: (ncb, stride) softbuffer contents the GPU produced for the same S
+    subframes -- the CPU front end must reproduce them (parity_vs_gpu)."""
     import oracle
-    from concurrent.futures import ThreadPoolExecutor
     from oracle import pdsch_chain as pc
-    from oracle import ue_dl_chain as uc
-    S = min(batch.D, 10)
-    cfgs = [pc.Cfg(nof_prb=100, nof_ports=2, nof_rx=2, cell_id=1, cfi=1, sf_idx=d % 10, scheme=2, nof_layers=2,
-                   qm=[8, 8], tbs=[97896, 97896], csi_enable=True) for d in range(S)]
+    nthreads, host = host_cores()
+    S = min(src.n, 16)
+    iq = np.ascontiguousarray(src.iq_host(0, S))
+    cfgs = (oracle.FrontCfg * S)()
+    for d in range(S):
+        cfgs[d] = oracle.front_cfg(pc.Cfg(nof_prb=100, nof_ports=2, nof_rx=2, cell_id=1, cfi=1,
+                                          sf_idx=(src.first + d) % 10, scheme=2, nof_layers=2, qm=[8, 8],
+                                          tbs=[TBS, TBS], csi_enable=True))
+    stride = 18600
+    sb = np.zeros(S * 2 * 16 * stride, np.int16)
+    L = oracle.lib()
 
-    def front(d):
-        grids = np.stack([uc.ofdm_rx_sf(batch.iq_host[d, r], 100) for r in range(2)])
-        ce, res = uc.chest_estimate(grids, 100, 2, 1, d % 10)
-        return pc.rx_front(cfgs[d], grids, ce, res["noise_estimate"])[2]
-
-    t0 = time.perf_counter()
-    reps_f = 0
-    with ThreadPoolExecutor(nthreads) as ex:
+    def front(nt):
+        reps, t0 = 0, time.perf_counter()
         while True:
-            list(ex.map(front, range(S)))
-            reps_f += 1
-            if time.perf_counter() - t0 >= budget_s / 2:
-                break
-    t_front = (time.perf_counter() - t0) / (reps_f * S)  # per subframe, nthreads cores
-    # turbo part: the first S subframes' code blocks (softbuffers 0 .. 2S-1) from the device pool
-    from srsran_amd import lib
-    buf, stride, mcb = C.POINTER(C.c_int16)(), C.c_uint32(), C.c_uint32()
-    lib().mi355_softbuffer_pool_buffer.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_int16)),
-                                                   C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
-    lib().mi355_softbuffer_pool_buffer(batch.pool.h, C.byref(buf), C.byref(stride), C.byref(mcb))
-    ncb = 2 * S * 16
-    host = np.zeros((ncb, stride.value), np.int16)
-    lib().mi355_memcpy_d2h(host.ctypes.data, C.cast(buf, C.c_void_p).value, host.nbytes)
-    nh = max(1, int(math.ceil(avg_its)))
+            assert L.orc_ue_dl_rx_batch(cfgs, S, iq.view(np.float32).reshape(-1), 2 * 2 * src.sf_len, sb, stride,
+                                        16, nt) == 0
+            reps += 1
+            if time.perf_counter() - t0 >= budget_s / 4:
+                return (time.perf_counter() - t0) / (reps * S), reps
+
     kind_t = "reference" if oracle.ref_available() else "port"
-    fn = oracle.ref().ref_tdec_run_batch if kind_t == "reference" else oracle.lib().orc_tdec_run_batch
-    out = np.zeros((ncb, 6144 // 8), np.uint8)
-    t1 = time.perf_counter()
-    reps = 0
-    while True:
-        fn(host, stride.value, ncb, 6144, nh, out, nthreads)
-        reps += 1
-        if time.perf_counter() - t1 >= budget_s / 2:
-            break
-    t_tdec = (time.perf_counter() - t1) / (reps * S)  # per subframe
-    per_sf = t_front + t_tdec
-    bits = 2 * 97896
+    fn = oracle.ref().ref_tdec_run_batch if kind_t == "reference" else L.orc_tdec_run_batch
+    nh = max(1, int(math.ceil(avg_its)))
+    ncb = 2 * S * 16
+    out = np.zeros((ncb, 768), np.uint8)
+    bufs = sb.reshape(ncb, stride)
+
+    def turbo(nt, n_cb):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            fn(bufs[:n_cb], stride, n_cb, 6144, nh, out[:n_cb], nt)
+            reps += 1
+            if time.perf_counter() - t0 >= budget_s / 4:
+                return (time.perf_counter() - t0) / reps / n_cb, reps
+
+    f1, r_f1 = front(1)
+    fN, r_fN = front(nthreads)
+    # the CPU chain's decoder buffers vs the GPU's for the same subframes (systematic, parity 1, parity 2, tails):
+    # equal up to the LSB-level LLR differences of the float32 FFT / estimator (tests: within +-2)
+    cols = np.r_[0:6144, 6176:6176 + 6144, 12352:12352 + 6144, 18528:18540]
+    diff = np.abs(bufs[:, cols].astype(np.int32) - gpu_bufs[:ncb, cols].astype(np.int32))
+    parity = {"max_abs_diff": int(diff.max()), "frac_entries_differing": round(float(np.mean(diff > 0)), 6)}
+    t1, r_t1 = turbo(1, min(ncb, 64))
+    tN, r_tN = turbo(nthreads, ncb)
+    per_sf_1 = f1 + 32 * t1
+    per_sf_N = fN + 32 * tN
+    bits = 2 * TBS
     return {
-        "value": round(bits / per_sf / 1e6, 2), "unit": "Mbps", "cb_per_s": round(32 / per_sf, 1),
-        "cores": nthreads, "kind": "port",
-        "sample": (f"{S} distinct TM4 subframes: front-end (numpy float64 DFT + oracle C chest/MMSE/demap) "
-                   f"{t_front * 1e3:.2f} ms/subframe x {reps_f} passes, reference AVX2 turbo decoder "
-                   f"({kind_t}, oracle/_ref) on their {ncb} CBs x {nh} half-iterations {t_tdec * 1e3:.2f} "
-                   f"ms/subframe x {reps} passes; {nthreads} threads"),
+        "value": round(bits / per_sf_N / 1e6, 2), "unit": "Mbps", "cb_per_s": round(32 / per_sf_N, 1),
+        "cores": nthreads, "kind": "reference" if kind_t == "reference" else "port",
+        "host": host,
+        "one_thread": {"value": round(bits / per_sf_1 / 1e6, 2), "cb_per_s": round(32 / per_sf_1, 1),
+                       "front_ms_per_subframe": round(f1 * 1e3, 3),
+                       "turbo_us_per_cb_halfit": round(t1 / nh * 1e6, 2)},
+        "all_cores": {"front_ms_per_subframe": round(fN * 1e3, 3),
+                      "turbo_us_per_cb_halfit_per_thread": round(tN / nh * nthreads * 1e6, 2)},
+        "parity_front_vs_gpu_softbuffers": parity,
+        "sample": (f"{S} distinct TM4 subframes of this batch: C front end (oracle/orc_front.c: float Stockham FFT, "
+                   f"oracle chest / MMSE+CSI / demap / descramble / rate dematching) {r_f1}+{r_fN} passes at 1 and "
+                   f"{nthreads} threads; their {ncb} CBs through the reference AVX2 turbo decoder ({kind_t}, "
+                   f"oracle/_ref) x {nh} half-iterations (= ceil of the GPU run's mean), {r_t1}+{r_tN} passes"),
         "turbo_kind": kind_t,
     }
 
 
-def run_pdsch(args, world, rank, local, pg):
+def softbuffer_contents(rx: Tm4Rx, ncb):
+    from srsran_amd import lib
+    buf, stride, mcb = C.POINTER(C.c_int16)(), C.c_uint32(), C.c_uint32()
+    lib().mi355_softbuffer_pool_buffer.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_int16)),
+                                                   C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    lib().mi355_softbuffer_pool_buffer(rx.pool.h, C.byref(buf), C.byref(stride), C.byref(mcb))
+    return C.cast(buf, C.c_void_p).value, stride.value
+
+
+def map_probe(rx: Tm4Rx, B, local, sample_check=True):
+    """Dominant kernel: the MAP half-iteration over this batch's 32 B code blocks (the softbuffers hold the
+    rate-dematched LLRs of the last step), a fixed 8 half-iterations without early stop (configs[1]'s regime on
+    the e2e code blocks), HIP events on the decoder's stream.  Returns (roofline, roofline_valu, fixed8 dict)."""
     from srsran_amd import lib
     from srsran_amd.tdec import DeviceBuffer, TdecBatch
+    ptr, stride = softbuffer_contents(rx, 2 * B * 16)
+    ncb = 2 * B * 16
+    d_out = DeviceBuffer(ncb * 768, local)
+    dec = TdecBatch(local)
+    dec.run_dev(ptr, stride, ncb, 6144, 8, d_out.ptr)
+    lib().mi355_device_sync()
+    t0 = time.perf_counter()
+    dec.run_dev(ptr, stride, ncb, 6144, 8, d_out.ptr)
+    lib().mi355_device_sync()
+    wall = time.perf_counter() - t0
+    dec.set_profiling(True)
+    for _ in range(2):
+        dec.run_dev(ptr, stride, ncb, 6144, 8, d_out.ptr)
+    kms, kl = dec.kernel_stats()
+    dec.set_profiling(False)
+    roof, valu = tdec_roofline(kms, kl, ncb, 6144)
+    fixed8 = {"code_blocks": ncb, "half_iterations": 8, "ms": round(wall * 1e3, 3),
+              "code_blocks_per_s": round(ncb / wall, 1), "mbps": round(ncb * 6120 / wall / 1e6, 1),
+              "note": "the batch's 65,536 rate-dematched CBs decoded with a fixed 8 half-iterations (no early stop), "
+                      "K-24 = 6,120 information bits per CB"}
+    dec.close()
+    return roof, valu, fixed8, (ptr, stride, d_out)
+
+
+def run_pdsch(args, world, rank, local, pg):
+    from srsran_amd import lib
     cell = tm4_setup()
     B = args.subframes
     ctrl = args.workload == "ue_dl"
-    b = Tm4Batch(cell, B, min(args.distinct, B), args.snr, seed=shard_seed(rank), device=local, ctrl=ctrl,
-                 gen=args.gen)
-    for _ in range(args.warmup):
-        b.step()
-    lib().mi355_device_sync()
-    ok, its = b.check_payloads()
+    sf_bytes = 2 * 15 * 1536 * 8
+    if args.total_subframes:
+        lo, hi = shard_range(args.total_subframes, world, rank)
+        max_shard = -(-args.total_subframes // world)
+        R = max(B, int(args.resident_gb * 1e9 / sf_bytes) // B * B)  # resident set, whole batches
+        R = min(R, -(-max_shard // B) * B)
+        nsets = -(-max_shard // R)
+    else:
+        lo, hi = rank * B, (rank + 1) * B
+        R, nsets = B, 1
+    src = Tm4Source(cell, R, local, ctrl)
+    rx = Tm4Rx(cell, B, local, ctrl)
+    dt_total, ok_sample, sample_tbs, bits_all, its_all, batches = 0.0, 0, 0, [], [], 0
+    for s in range(nsets):
+        a = lo + s * R
+        n = max(0, min(R, hi - a))
+        if n:
+            src.generate(a, n, args.snr, args.seed)
+        bound = [rx.bind(src, k0, min(B, n - k0)) for k0 in range(0, n, B)]
+        if s == 0 and bound:
+            for _ in range(args.warmup):
+                rx.step(bound[0])
+            lib().mi355_device_sync()
+        reps = 1 if args.total_subframes else args.steps
+        barrier(pg, local)
+        lib().mi355_device_sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for b in bound:
+                rx.step(b)
+                if args.total_subframes:
+                    bits_all.append(rx.crc_bits(b[3]))
+        lib().mi355_device_sync()
+        barrier(pg, local)
+        dt_total += time.perf_counter() - t0
+        batches += reps * len(bound)
+        if bound:  # payload check of the last batch decoded (all of it in the default mode)
+            ok_sample += rx.payload_ok(src, bound[-1])
+            sample_tbs += 2 * bound[-1][3]
+            its_all.append(rx.avg_its(bound[-1][3]))
+            if not args.total_subframes:
+                bits_all.append(rx.crc_bits(bound[-1][3]))
+    dt = max_over_ranks(pg, local, dt_total)
+    bits = np.concatenate(bits_all) if bits_all else np.zeros(0, np.uint8)
+    gathered = gather_bitmap(pg, local, bits)
+    ok_sample_all = int(sum_over_ranks(pg, local, ok_sample))
+    sample_all = int(sum_over_ranks(pg, local, sample_tbs))
+    its = float(np.mean(its_all)) if its_all else 0.0
 
-    barrier(pg, local)
-    lib().mi355_device_sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        b.step()
-    lib().mi355_device_sync()
-    barrier(pg, local)
-    dt = time.perf_counter() - t0
-    dt = max_over_ranks(pg, local, dt)
-    ok_last, _ = b.check_payloads()
-
-    stages = {}
-    roof, valu = None, None
-    if args.no_roofline:
-        kms = None
-    elif not ctrl:
-        b.step(stages)
-    # dominant kernel: the MAP half-iteration over this batch's 32*B code blocks (the softbuffers hold the
-    # rate-dematched LLRs of the last step), 8 half-iterations without early stop, HIP events on its stream
-    from srsran_amd.dlsch import _declare as _dd
-    L = _dd()
-    buf, stride, mcb = C.POINTER(C.c_int16)(), C.c_uint32(), C.c_uint32()
-    L.mi355_softbuffer_pool_buffer.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_int16)),
-                                               C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
-    L.mi355_softbuffer_pool_buffer(b.pool.h, C.byref(buf), C.byref(stride), C.byref(mcb))
-    ncb = 2 * B * 16
-    if not args.no_roofline:
-        d_out = DeviceBuffer(ncb * 768, local)
-        dec = TdecBatch(local)
-        ptr = C.cast(buf, C.c_void_p).value
-        dec.run_dev(ptr, stride.value, ncb, 6144, 8, d_out.ptr)
-        dec.set_profiling(True)
-        for _ in range(2):
-            dec.run_dev(ptr, stride.value, ncb, 6144, 8, d_out.ptr)
-        kms, kl = dec.kernel_stats()
-        dec.set_profiling(False)
-        roof, valu = tdec_roofline(kms, kl, ncb, 6144)
-
-    subframes = world * B * args.steps
-    ok_all = int(sum_over_ranks(pg, local, ok_last))  # CRC-ok TBs of the last step, all ranks
-    mbps = whole_job_rate(world, B * 2 * 97896, args.steps, dt) / 1e6 * (ok_all / (2 * B * world))
-    res = {
-        "metric": METRIC, "value": round(mbps, 1), "unit": "Mbps", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32+int16", "data": "synthetic",
-        "config": {"workload": f"srslte_ue_dl chain from time-domain I/Q: {B} subframes/GPU/step, 20 MHz (100 PRB), "
-                               "TM4 2x2 spatial multiplexing, 2 codewords QAM256 TBS 97896 (C=16, K=6144), "
-                               "MMSE+CSI, max 10 half-its with CRC early stop, 40 dB crossed 2x2 channel, " +
-                               ("every subframe distinct (GPU eNodeB generator)" if args.gen == "device" else
-                                f"{b.D} distinct host-encoded subframes tiled") +
-                               ("; grants from the PCFICH/PDCCH blind search (DCI format 2 per subframe, "
-                                "find_and_decode = phy_dl_test work_ue)" if ctrl else ""),
-                   "subframes_per_gpu": B, "code_blocks_per_gpu": 32 * B, "distinct_subframes": b.D,
-                   "parallelism": f"dp{world}"},
-        "code_blocks_per_s": round(world * 32 * B * args.steps / dt, 1),
-        "subframes_per_s": round(subframes / dt, 1),
-        "crc_ok_tbs": f"{ok_all}/{2 * B * world}", "avg_half_iterations": round(its, 3),
-        "stage_ms": {k: round(v, 3) for k, v in stages.items()},
-        "roofline": roof,
-    }
-    if valu:
+    res = {"metric": METRIC, "n_gpus": world}
+    if args.total_subframes:
+        T = args.total_subframes
+        ok_tbs = int(gathered.sum()) if rank == 0 else 0
+        mbps = ok_tbs * TBS / dt / 1e6
+        res.update({"value": round(mbps, 1), "unit": "Mbps", "steps": batches, "warmup": args.warmup,
+                    "ms_per_step": round(dt / max(batches, 1) * 1e3, 3),
+                    "code_blocks_per_s": round(T * 32 / dt, 1), "subframes_per_s": round(T / dt, 1),
+                    "job_seconds": round(dt, 3), "resident_sets": nsets})
+        nsf = T
+    else:
+        ok_tbs = int(gathered.sum()) if rank == 0 else 0
+        mbps = whole_job_rate(world, B * 2 * TBS, args.steps, dt) / 1e6 * (ok_tbs / (2 * B * world))
+        res.update({"value": round(mbps, 1), "unit": "Mbps", "steps": args.steps, "warmup": args.warmup,
+                    "ms_per_step": round(dt / args.steps * 1e3, 3),
+                    "code_blocks_per_s": round(world * 32 * B * args.steps / dt, 1),
+                    "subframes_per_s": round(world * B * args.steps / dt, 1)})
+        nsf = world * B
+    workload = (f"srslte_ue_dl chain from time-domain I/Q: {B} subframes/GPU/batch, 20 MHz (100 PRB), TM4 2x2 "
+                "spatial multiplexing, 2 codewords QAM256 TBS 97896 (C=16, K=6144), MMSE+CSI, max 10 half-its with "
+                f"CRC early stop, {args.snr:g} dB crossed 2x2 channel, every subframe distinct (GPU eNodeB generator, "
+                "keyed by global subframe index)")
+    if ctrl:
+        workload += ("; grants from the PCFICH/PDCCH blind search (DCI format 2 per subframe, find_and_decode = "
+                     "phy_dl_test work_ue)")
+    if args.total_subframes:
+        workload = (f"configs[4]: {args.total_subframes} subframes sharded contiguously over {world} GPU(s), each "
+                    "decoded once; " + workload)
+    res.update({
+        "higher_is_better": True, "scaling": "weak" if not args.total_subframes else "strong",
+        "vs_baseline": None, "dtype": "fp32+int16", "data": "synthetic",
+        "config": {"workload": workload, "subframes_per_gpu_batch": B, "code_blocks_per_gpu_batch": 32 * B,
+                   "total_subframes": args.total_subframes or None, "parallelism": f"dp{world}"},
+        "crc_ok_tbs": f"{ok_tbs}/{2 * nsf}",
+        "crc_bitmap": bitmap_summary(gathered, nsf) if rank == 0 else None,
+        "payload_checked_tbs": f"{ok_sample_all}/{sample_all}",
+        "avg_half_iterations": round(its, 3),
+    })
+    if args.no_roofline or args.total_subframes:
+        res["roofline"] = None
+    else:
+        stages = {}
+        if not ctrl:
+            last = rx.bind(src, 0, min(B, src.n))
+            rx.step(last, stages)
+            res["stage_ms"] = {k: round(v, 3) for k, v in stages.items()}
+        roof, valu, fixed8, (ptr, stride, _d_out) = map_probe(rx, B, local)
+        res["roofline"] = roof
         res["roofline_valu"] = valu
-    if rank == 0 and world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline_pdsch(b, min(os.cpu_count() or 1, 16), args.cpu_seconds, its)
+        res["decoder_bound_fixed8"] = fixed8
+        if rank == 0 and world == 1 and not args.no_cpu:
+            ncb = 2 * min(src.n, 16) * 16
+            gb = np.zeros((ncb, stride), np.int16)
+            lib().mi355_memcpy_d2h(gb.ctypes.data, ptr, gb.nbytes)
+            res["cpu_baseline"] = cpu_baseline_pdsch(src, gb, its, args.cpu_seconds)
+            # the fixed-8 decisions of a CB sample against the reference decoder (cpu_baseline leg)
+            res["decoder_bound_fixed8"]["parity_vs_reference"] = fixed8_parity(gb[:64], _d_out)
+    if not ctrl and not args.total_subframes and not args.no_waterfall:
+        res["e2e_waterfall"] = waterfall(args, cell, B, src, rx, pg, local, world)
+    rx.pool.close()
+    src.close()
     return res
+
+
+def fixed8_parity(bufs, d_out):
+    """GPU decisions after a fixed 8 half-iterations on the first CBs vs the reference's AVX2 decoder
+    (oracle/_ref where built, else the oracle restatement)."""
+    import oracle
+    n = bufs.shape[0]
+    got = np.zeros((n, 768), np.uint8)
+    from srsran_amd import lib
+    lib().mi355_memcpy_d2h(got.ctypes.data, d_out.ptr, got.nbytes)
+    want = np.zeros((n, 768), np.uint8)
+    b = np.ascontiguousarray(bufs)
+    if oracle.ref_available():
+        oracle.ref().ref_tdec_run_batch(b, b.shape[1], n, 6144, 8, want, 1)
+        kind = "reference"
+    else:
+        oracle.lib().orc_tdec_run_batch(b, b.shape[1], n, 6144, 8, want, 1)
+        kind = "port"
+    return {"cbs": n, "bit_exact": bool(np.array_equal(got, want)), "checker": kind}
+
+
+def waterfall(args, cell, B, src, rx, pg, local, world):
+    """Decoder-bound regime: the same batch shape through srslte_channel_fading_t EPA 5 Hz (generator, per-OFDM
+    symbol block fading) at a waterfall SNR where the turbo decoder needs most of its 10 half-iterations."""
+    from srsran_amd import lib
+    src.generate(10_000_000 + pg_rank(pg) * B, src.n_max, args.waterfall_snr, args.seed + 1, fading="epa5")
+    bound = [rx.bind(src, 0, min(B, src.n))]
+    rx.step(bound[0])
+    lib().mi355_device_sync()
+    barrier(pg, local)
+    t0 = time.perf_counter()
+    steps = max(1, min(args.steps, 3))
+    for _ in range(steps):
+        rx.step(bound[0])
+    lib().mi355_device_sync()
+    barrier(pg, local)
+    dt = max_over_ranks(pg, local, time.perf_counter() - t0)
+    ok = int(sum_over_ranks(pg, local, int(rx.crc_bits(bound[0][3]).sum())))
+    its = rx.avg_its(bound[0][3])
+    return {"snr_db": args.waterfall_snr, "channel": "EPA 5 Hz 2x2 (srslte_channel_fading_t taps, per-symbol)",
+            "avg_half_iterations": round(its, 3), "crc_ok_tbs": f"{ok}/{2 * B * world}",
+            "ms_per_step": round(dt / steps * 1e3, 3),
+            "mbps": round(ok * TBS * steps / dt / 1e6, 1),
+            "code_blocks_per_s": round(world * 32 * B * steps / dt, 1)}
+
+
+def pg_rank(pg) -> int:
+    return pg.get_rank() if pg is not None else 0
 
 
 # ====================================================================================== turbo only (configs[1])
@@ -600,7 +858,7 @@ def run_tdec(args, world, rank, local, pg):
     from srsran_amd.tdec import DeviceBuffer, TdecBatch
     K, nh, ncb = args.K, args.nhalf, args.ncb
     stride = 3 * (K + 32) + 12
-    pool = make_cb_pool(K, args.pool, args.ebno, seed=1234 + rank)
+    pool = make_cb_pool(K, args.pool, args.ebno, seed=shard_seed(rank))
     host = np.ascontiguousarray(np.tile(pool, (ncb // args.pool + 1, 1))[:ncb])
     d_in = DeviceBuffer(host.nbytes, local).upload(host)
     del host
@@ -637,28 +895,32 @@ def run_tdec(args, world, rank, local, pg):
         "config": {"workload": f"batched turbo decode (configs[1]): {ncb} x K={K} code blocks per GPU, {nh} "
                                f"half-iterations, AUTO 16-window bit-exact, Eb/N0 {args.ebno}",
                    "code_blocks_per_gpu": ncb, "K": K, "half_iterations": nh, "parallelism": f"dp{world}"},
-        "code_blocks_per_s": round(cb_s, 1), "roofline": roof,
+        "code_blocks_per_s": round(cb_s, 1), "roofline": roof, "roofline_valu": valu,
     }
-    if valu:
-        res["roofline_valu"] = valu
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle
-        nthreads = min(os.cpu_count() or 1, 16)
+        nthreads, hostinfo = host_cores()
         kind = "reference" if oracle.ref_available() else "port"
         fn = oracle.ref().ref_tdec_run_batch if kind == "reference" else oracle.lib().orc_tdec_run_batch
         sub = pool[: min(args.pool, 256)]
         out = np.zeros((sub.shape[0], K // 8), np.uint8)
-        reps, t1 = 0, time.perf_counter()
-        while True:
-            fn(sub, stride, sub.shape[0], K, nh, out, nthreads)
-            reps += 1
-            if time.perf_counter() - t1 >= min(args.cpu_seconds, 3.0):
-                break
-        dtc = time.perf_counter() - t1
-        n = reps * sub.shape[0]
+        legs = {}
+        for nt, n_cb in ((1, 16), (nthreads, sub.shape[0])):
+            reps, t1 = 0, time.perf_counter()
+            while True:
+                fn(sub[:n_cb], stride, n_cb, K, nh, out[:n_cb], nt)
+                reps += 1
+                if time.perf_counter() - t1 >= min(args.cpu_seconds, 4.0):
+                    break
+            legs[nt] = (reps * n_cb, time.perf_counter() - t1)
+        n, dtc = legs[nthreads]
+        n1, dt1 = legs[1]
         res["cpu_baseline"] = {"value": round(n * K / dtc / 1e6, 2), "unit": "Mbps", "cb_per_s": round(n / dtc, 1),
-                               "cores": nthreads, "kind": kind,
-                               "sample": f"{n} x K={K} CBs, {nh} half-its, {nthreads} threads, {dtc:.2f} s"}
+                               "cores": nthreads, "kind": kind, "host": hostinfo,
+                               "one_thread": {"cb_per_s": round(n1 / dt1, 1),
+                                              "us_per_cb_halfit": round(dt1 / n1 / nh * 1e6, 2)},
+                               "sample": f"{n} x K={K} CBs, {nh} half-its, {nthreads} threads, {dtc:.2f} s; "
+                                         f"{n1} CBs on 1 thread, {dt1:.2f} s"}
         res["parity_vs_cpu"] = bool(np.array_equal(got[: out.shape[0]], out))
     return res
 
@@ -675,10 +937,10 @@ def run_enb(args, world, rank, local, pg):
     from srsran_amd.ue_dl import symbol_sz
     cell = tm4_setup()
     B = args.subframes
-    G, N, nb = 14 * 12 * cell.nof_prb, symbol_sz(cell.nof_prb), 97896 // 8
+    G, N = 14 * 12 * cell.nof_prb, symbol_sz(cell.nof_prb)
     sf_len = 15 * N
     rng = np.random.default_rng(shard_seed(rank))
-    payloads = rng.integers(0, 256, (B, 2, nb), dtype=np.uint8)
+    payloads = rng.integers(0, 256, (B, 2, NB), dtype=np.uint8)
     d_pl = DeviceBuffer(payloads.nbytes, local).upload(payloads)
     d_tx = DeviceBuffer(B * 2 * G * 8, local)
     d_rx = DeviceBuffer(B * 2 * G * 8, local)
@@ -695,7 +957,7 @@ def run_enb(args, world, rank, local, pg):
         j.sf.tti, j.sf.cfi = i % 10, 1
         j.cfg = cfg_sf[i % 10]
         for t in range(2):
-            j.data[t] = d_pl.ptr + (i * 2 + t) * nb
+            j.data[t] = d_pl.ptr + (i * 2 + t) * NB
         for p in range(2):
             j.sf_symbols[p] = tx[2 * i + p]
         jobs.append(j)
@@ -721,16 +983,15 @@ def run_enb(args, world, rank, local, pg):
     lib().mi355_device_sync()
     barrier(pg, local)
     dt = max_over_ranks(pg, local, time.perf_counter() - t0)
-    # parity: decode the last step's I/Q with the product's UE chain
     ok = decode_check(cell, B, d_iq, payloads, local)
     ok_all = int(sum_over_ranks(pg, local, ok))
-    mbps = whole_job_rate(world, B * 2 * 97896, args.steps, dt) / 1e6
+    mbps = whole_job_rate(world, B * 2 * TBS, args.steps, dt) / 1e6
     # algorithmic HBM bytes per subframe of the chain: payload in, codeword bits out + in, PDSCH and
     # CRS REs out, channel grids in + out, IFFT grids in + I/Q out
     nre_pdsch = 2 * 14400
-    per_sf = 2 * nb + 2 * 2 * 115200 + 2 * nre_pdsch * 8 + 2 * 800 * 8 + 2 * 2 * G * 8 + 2 * G * 8 + 2 * sf_len * 8
+    per_sf = 2 * NB + 2 * 2 * 115200 + 2 * nre_pdsch * 8 + 2 * 800 * 8 + 2 * 2 * G * 8 + 2 * G * 8 + 2 * sf_len * 8
     ach = B * per_sf * args.steps / dt / 1e9
-    res = {
+    return {
         "metric": "PDSCH encoded Mbps (GPU eNodeB generator), 20 MHz TM4 QAM256", "value": round(mbps, 1),
         "unit": "Mbps", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
@@ -744,7 +1005,6 @@ def run_enb(args, world, rank, local, pg):
                      "frac": round(ach / 8000.0, 4), "traffic": None, "kernel": "whole generator chain",
                      "algorithmic_bytes_per_subframe": per_sf},
     }
-    return res
 
 
 def decode_check(cell, B, d_iq, payloads, device):
@@ -753,7 +1013,7 @@ def decode_check(cell, B, d_iq, payloads, device):
     from srsran_amd.dlsch import SoftbufferPool
     from srsran_amd.tdec import DeviceBuffer
     from srsran_amd.ue_dl import DlSfJob, UeDl, default_chest_cfg, symbol_sz
-    G, sf_len, plen = 14 * 12 * cell.nof_prb, 15 * symbol_sz(cell.nof_prb), 97896 // 8 + 16
+    G, sf_len, plen = 14 * 12 * cell.nof_prb, 15 * symbol_sz(cell.nof_prb), NB + 16
     ue = UeDl(cell, 2, device)
     d_grid = DeviceBuffer(B * 2 * G * 8, device)
     d_ce = DeviceBuffer(B * 4 * G * 8, device)
@@ -772,23 +1032,51 @@ def decode_check(cell, B, d_iq, payloads, device):
         sfs[i] = P.DlSfCfg(i % 10, 1)
         cfgs[i] = tm4_cfg(P, cell, i % 10, softbuffers=(2 * i, 2 * i + 1))
         pays[2 * i], pays[2 * i + 1] = d_pay.ptr + 2 * i * plen, d_pay.ptr + (2 * i + 1) * plen
-    chest, res = ue.decode(pool, list(jobs), list(sfs), list(cfgs), default_chest_cfg(), list(pays))
+    _chest, res = ue.decode(pool, list(jobs), list(sfs), list(cfgs), default_chest_cfg(), list(pays))
     host = d_pay.download(np.zeros(B * 2 * plen, np.uint8)).reshape(B, 2, plen)
     ok = 0
     for i in range(B):
         for t in range(2):
-            if res[2 * i + t].crc and np.array_equal(host[i, t, : 97896 // 8], payloads[i, t]):
+            if res[2 * i + t].crc and np.array_equal(host[i, t, :NB], payloads[i, t]):
                 ok += 1
     return ok
 
 
+# ====================================================================================== plumbing dry run (CPU)
+
+def run_plumbing(args, world, rank, local, pg):
+    """CPU dry run of the multi-GPU plumbing (launcher, contiguous sharding, barriers, max-over-ranks, CRC-bitmap
+    gather) with gloo: NO decoding happens -- each rank fabricates the CRC bits of its shard from the subframe index
+    (TB t of subframe i "fails" iff (i * 7 + t) % 13 == 0) so the gathered bitmap's order can be checked."""
+    T = args.total_subframes or world * args.subframes
+    lo, hi = shard_range(T, world, rank) if args.total_subframes else (rank * args.subframes, (rank + 1) * args.subframes)
+    barrier(pg, local)
+    t0 = time.perf_counter()
+    i = np.arange(lo, hi, dtype=np.int64)
+    bits = np.stack([(i * 7 + t) % 13 != 0 for t in range(2)], axis=1).reshape(-1).astype(np.uint8)
+    time.sleep(0.02 * (rank + 1))
+    barrier(pg, local)
+    dt = max_over_ranks(pg, local, time.perf_counter() - t0)
+    g = gather_bitmap(pg, local, bits)
+    return {"metric": "plumbing dry run (no decoding)", "value": None, "unit": None, "n_gpus": world,
+            "steps": 1, "warmup": 0, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak" if not args.total_subframes else "strong", "vs_baseline": None, "dtype": None,
+            "data": "synthetic", "config": {"workload": "plumbing", "total_subframes": T,
+                                            "parallelism": f"dp{world}"},
+            "shard": [lo, hi], "crc_bitmap": bitmap_summary(g, T) if rank == 0 else None,
+            "bitmap_bits": g.tolist() if (rank == 0 and T <= 4096) else None}
+
+
 def main():
     args = parse()
-    world, rank, local, pg = dist_setup()
+    self_launch(args)
+    world, rank, local, pg = dist_setup(args.gpus)
     if args.workload == "tdec":
         res = run_tdec(args, world, rank, local, pg)
     elif args.workload == "enb":
         res = run_enb(args, world, rank, local, pg)
+    elif args.workload == "plumbing":
+        res = run_plumbing(args, world, rank, local, pg)
     else:
         res = run_pdsch(args, world, rank, local, pg)
     if rank == 0:

@@ -79,6 +79,19 @@ int mi355_enb_dl_gen_signal_batch(mi355_enb_dl_t* q, const float* const* grids, 
 int mi355_channel_grid_batch(mi355_enb_dl_t* q, const float* const* tx, float* const* rx, uint32_t n,
                              uint32_t nof_rx, const float* H, float sigma, uint64_t seed, void* stream);
 
+/* mi355_channel_grid_batch with the noise keyed by (seed, first_index + i, r, k): job i is the subframe with global
+ * index first_index + i, so a shard of a large synthetic run reproduces its subframes independently of the others
+ * (mi355_channel_grid_batch == first_index 0). */
+int mi355_channel_grid_batch_at(mi355_enb_dl_t* q, const float* const* tx, float* const* rx, uint32_t n,
+                                uint32_t nof_rx, const float* H, float sigma, uint64_t seed, uint64_t first_index,
+                                void* stream);
+
+/* Synthetic payloads for n subframes of ntb transport blocks of nbytes each (device buffer out, TB-major per
+ * subframe): byte b of TB t of subframe first_index + i is byte b % 8 of
+ * splitmix64(seed ^ (splitmix64((first_index + i) << 8 | t) + b / 8)).  Test-data synthesis for the benchmark. */
+int mi355_enb_synth_payloads(mi355_enb_dl_t* q, uint8_t* out, uint64_t first_index, uint32_t n, uint32_t ntb,
+                             uint32_t nbytes, uint64_t seed, void* stream);
+
 /* Multipath fading test channel in the resource grid (srslte_channel_fading_t, channel/fading.c): model is the
  * reference's string ("none<Fd>", "epa<Fd>", "eva<Fd>", "etu<Fd>", Fd the Doppler in Hz; parse_model,
  * fading.c:48-78), taps and powers of 36.104 B.2 (fading.c:33-46), per link (rx r, port p) the Jakes phases

@@ -76,8 +76,48 @@ def lib() -> C.CDLL:
                                               C.c_float, C.c_float, C.c_int, f32p, f32p]
         L.orc_predecode.argtypes = [f32p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
                                     C.c_float, f32p, f32p, f32p]
+        L.orc_ofdm_rx_sf.argtypes = [f32p, C.c_uint32, f32p]
+        L.orc_ue_dl_front.argtypes = [C.POINTER(FrontCfg), C.c_void_p * 2, C.c_void_p * 2, C.POINTER(C.c_float)]
+        L.orc_dlsch_rm_tb.argtypes = [i16p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, i16p, C.c_uint32]
+        L.orc_ue_dl_rx_batch.argtypes = [C.POINTER(FrontCfg), C.c_uint32, f32p, C.c_size_t, i16p, C.c_uint32,
+                                         C.c_uint32, C.c_int]
         _LIB = L
     return _LIB
+
+
+class FrontCfg(C.Structure):
+    """orc_front_cfg_t (oracle.h)."""
+    _fields_ = [(n, C.c_uint32) for n in ("nof_prb", "nof_ports", "nof_rx", "cell_id", "cfi", "sf_idx", "rnti",
+                                          "scheme", "nof_layers", "cb", "nof_tb")] + \
+               [("qm", C.c_uint32 * 2), ("tbs", C.c_uint32 * 2), ("rv", C.c_uint32 * 2), ("csi_enable", C.c_int32),
+                ("power_scale", C.c_int32), ("mmse", C.c_int32), ("p_a", C.c_float), ("p_b", C.c_uint32)]
+
+
+def front_cfg(cfg) -> FrontCfg:
+    """pdsch_chain.Cfg -> orc_front_cfg_t."""
+    f = FrontCfg()
+    for n in ("nof_prb", "nof_ports", "nof_rx", "cell_id", "cfi", "sf_idx", "rnti", "scheme", "nof_layers"):
+        setattr(f, n, int(getattr(cfg, n)))
+    f.cb, f.nof_tb = cfg.codebook(), cfg.nof_tb
+    for t in range(cfg.nof_tb):
+        f.qm[t], f.tbs[t], f.rv[t] = cfg.qm[t], cfg.tbs[t], cfg.rv[t]
+    f.csi_enable, f.power_scale, f.mmse = int(cfg.csi_enable), int(cfg.power_scale), int(cfg.mmse)
+    f.p_a, f.p_b = float(cfg.p_a), int(cfg.p_b)
+    return f
+
+
+def ue_dl_front(cfg, iq: np.ndarray):
+    """orc_ue_dl_front: iq (nof_rx, 15 N) complex64 -> (e per TB int16, noise)."""
+    iq = np.ascontiguousarray(iq, np.complex64)
+    e = [np.zeros(8 * 14 * 1200, np.int16) for _ in range(2)]
+    ip = (C.c_void_p * 2)(iq[0].ctypes.data, iq[min(1, iq.shape[0] - 1)].ctypes.data)
+    ep = (C.c_void_p * 2)(e[0].ctypes.data, e[1].ctypes.data)
+    noise = C.c_float()
+    f = front_cfg(cfg)
+    nre = lib().orc_ue_dl_front(C.byref(f), ip, ep, C.byref(noise))
+    if nre < 0:
+        raise ValueError("orc_ue_dl_front: invalid configuration")
+    return [e[t][: nre * cfg.qm[t]].copy() for t in range(cfg.nof_tb)], float(noise.value)
 
 
 def ref_available() -> bool:

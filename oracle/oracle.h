@@ -48,6 +48,22 @@ int  orc_chest_estimate_port(const float* grid, uint32_t nof_prb, uint32_t cell_
 int orc_predecode(const float* y, const float* h, int nof_rx, int nof_ports, int nof_layers, int cb, int n,
                   int type, float scaling, float noise, float* x, float* csi0, float* csi1);
 
+/* C front end of the UE receive chain for the CPU baseline (orc_front.c) */
+typedef struct {
+  uint32_t nof_prb, nof_ports, nof_rx, cell_id, cfi, sf_idx, rnti;
+  uint32_t scheme, nof_layers, cb, nof_tb; /* scheme as orc_predecode's type: 0 port 0, 1 diversity, 2 spatial mux */
+  uint32_t qm[2], tbs[2], rv[2];
+  int32_t  csi_enable, power_scale, mmse;
+  float    p_a;
+  uint32_t p_b;
+} orc_front_cfg_t;
+int orc_ofdm_rx_sf(const float* iq, uint32_t nof_prb, float* grid);
+int orc_ue_dl_front(const orc_front_cfg_t* cfg, const float* const* iq, int16_t* const* e, float* noise_out);
+int orc_dlsch_rm_tb(const int16_t* e_bits, uint32_t nof_e_bits, uint32_t tbs, uint32_t Qm, uint32_t rv,
+                    int16_t* softbuf, uint32_t sb_stride);
+int orc_ue_dl_rx_batch(const orc_front_cfg_t* cfgs, uint32_t S, const float* iq, size_t iq_stride, int16_t* softbufs,
+                       uint32_t sb_stride, uint32_t max_cb, int nthreads);
+
 /* multi-threaded batch driver used as the CPU baseline (orc_batch.c) */
 int orc_tdec_run_batch(const int16_t* bufs, uint32_t stride, uint32_t ncb, uint32_t K, uint32_t nhalf, uint8_t* out,
                        int nthreads);

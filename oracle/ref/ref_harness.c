@@ -309,12 +309,18 @@ struct job {
   const int16_t* bufs;
   uint32_t       stride, first, count, K, nhalf;
   uint8_t*       out;
+  int            slot;
 };
+
+/* One srslte_tdec_t per worker slot, created on first use and kept across calls -- srsUE builds its decoder once
+ * per worker (srslte_sch_init), so the timed baseline must not pay srslte_tdec_init's table generation per call. */
+#define MAX_WORKERS 512
+static void* worker_tdec[MAX_WORKERS];
 
 static void* worker(void* arg)
 {
   struct job* j   = arg;
-  void*       h   = ref_tdec_new(6144, 0);
+  void*       h   = worker_tdec[j->slot];
   uint32_t    len = 3 * (j->K + 32) + 12;
   int16_t*    tmp = srslte_vec_i16_malloc(len + 32);
   for (uint32_t i = 0; i < j->count; i++) {
@@ -323,7 +329,6 @@ static void* worker(void* arg)
     ref_tdec_run(h, tmp, j->K, j->nhalf, &j->out[(size_t)cb * (j->K / 8)], NULL);
   }
   free(tmp);
-  ref_tdec_free(h);
   return NULL;
 }
 
@@ -332,13 +337,15 @@ int ref_tdec_run_batch(const int16_t* bufs, uint32_t stride, uint32_t ncb, uint3
                        int nthreads)
 {
   if (nthreads < 1) nthreads = 1;
+  if (nthreads > MAX_WORKERS) nthreads = MAX_WORKERS;
   pthread_t*  th   = calloc(nthreads, sizeof(pthread_t));
   struct job* jobs = calloc(nthreads, sizeof(struct job));
   uint32_t    base = ncb / nthreads, rem = ncb % nthreads, first = 0;
   for (int t = 0; t < nthreads; t++) {
     uint32_t c = base + ((uint32_t)t < rem);
-    jobs[t]    = (struct job){bufs, stride, first, c, K, nhalf, out};
+    jobs[t]    = (struct job){bufs, stride, first, c, K, nhalf, out, t};
     first += c;
+    if (!worker_tdec[t]) worker_tdec[t] = ref_tdec_new(6144, 0);
     pthread_create(&th[t], NULL, worker, &jobs[t]);
   }
   for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);

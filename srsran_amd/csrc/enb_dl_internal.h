@@ -79,7 +79,9 @@ hipError_t enb_launch_map(const EnbMapDev* jobs, uint32_t njobs, uint32_t max_un
 hipError_t enb_launch_crs(const EnbCrsJob* jobs, uint32_t njobs, const float2* pilots, uint32_t nof_prb,
                           uint32_t nof_ports, uint32_t cell_id, uint32_t nsymb, hipStream_t s);
 hipError_t enb_launch_channel(const EnbChanJob* jobs, uint32_t njobs, uint32_t nof_re, uint32_t nports, uint32_t nrx,
-                              const EnbChanMat& H, float sigma, uint64_t seed, hipStream_t s);
+                              const EnbChanMat& H, float sigma, uint64_t seed, uint64_t first, hipStream_t s);
+hipError_t enb_launch_synth_payloads(uint8_t* out, uint64_t first, uint32_t n, uint32_t ntb, uint32_t nbytes,
+                                     uint64_t seed, hipStream_t s);
 hipError_t enb_launch_fading(const EnbFadingArgs& a, uint32_t njobs, hipStream_t s);
 
 } // namespace mi355

@@ -319,7 +319,8 @@ __global__ __launch_bounds__(256) void enb_crs(const EnbCrsJob* __restrict__ job
 
 // ---------------------------------------------------------------------------- test channel
 __global__ __launch_bounds__(256) void enb_channel(const EnbChanJob* __restrict__ jobs, uint32_t nof_re, uint32_t nports,
-                                                   uint32_t nrx, EnbChanMat H, float sigma, uint64_t seed)
+                                                   uint32_t nrx, EnbChanMat H, float sigma, uint64_t seed,
+                                                   uint64_t first)
 {
   const EnbChanJob& J = jobs[blockIdx.y];
   const uint32_t    k = blockIdx.x * 256 + threadIdx.x;
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(256) void enb_channel(const EnbChanJob* __restrict_
       y.y += h.x * x[p].y + h.y * x[p].x;
     }
     if (sigma > 0.f) {
-      const uint64_t z  = splitmix64(seed ^ splitmix64(((uint64_t)blockIdx.y << 32) | ((uint64_t)r << 28) | k));
+      const uint64_t z  = splitmix64(seed ^ splitmix64(((first + blockIdx.y) << 32) | ((uint64_t)r << 28) | k));
       const float    u1 = ((float)(uint32_t)(z >> 40) + 1.0f) * (1.0f / 16777216.0f); // (0, 1]
       const float    u2 = (float)(uint32_t)((z >> 16) & 0xffffffu) * (1.0f / 16777216.0f);
       const float    rad = sqrtf(-2.0f * logf(u1));
@@ -459,15 +460,42 @@ hipError_t enb_launch_crs(const EnbCrsJob* jobs, uint32_t njobs, const float2* p
 }
 
 hipError_t enb_launch_channel(const EnbChanJob* jobs, uint32_t njobs, uint32_t nof_re, uint32_t nports, uint32_t nrx,
-                              const EnbChanMat& H, float sigma, uint64_t seed, hipStream_t s)
+                              const EnbChanMat& H, float sigma, uint64_t seed, uint64_t first, hipStream_t s)
 {
   if (!njobs) return hipSuccess;
   for (uint32_t j0 = 0; j0 < njobs; j0 += 65535) {
     const uint32_t n = njobs - j0 < 65535 ? njobs - j0 : 65535;
-    // the job index in the noise key is global (j0 + blockIdx.y): fold j0 into the seed's key space
+    // the noise key holds the job's global index (first + j0 + blockIdx.y)
     hipLaunchKernelGGL(enb_channel, dim3((nof_re + 255) / 256, n), dim3(256), 0, s, jobs + j0, nof_re, nports, nrx, H,
-                       sigma, seed + (uint64_t)j0 * 0x100000001ull);
+                       sigma, seed, first + j0);
   }
+  return hipGetLastError();
+}
+
+// Synthetic transport-block payloads keyed by the subframe's global index: byte b of TB t of subframe (first + i)
+// is byte b % 8 of splitmix64(seed ^ splitmix64(((first + i) << 8 | t) + b / 8)) -- any shard of a large run
+// regenerates its subframes without the others (bench.py --total-subframes).  Thread per 8 bytes.
+__global__ __launch_bounds__(256) void enb_synth_payloads(uint8_t* __restrict__ out, uint64_t first, uint32_t n,
+                                                          uint32_t ntb, uint32_t nbytes, uint64_t seed)
+{
+  const uint32_t words = (nbytes + 7) / 8;
+  const uint64_t g     = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (uint64_t)n * ntb * words) return;
+  const uint32_t w  = (uint32_t)(g % words);
+  const uint64_t it = g / words; // i * ntb + t
+  const uint64_t i = it / ntb, t = it % ntb;
+  const uint64_t z = splitmix64(seed ^ (splitmix64(((first + i) << 8) | t) + w));
+  uint8_t*       o = out + it * nbytes + (size_t)w * 8;
+  for (uint32_t b = 0; b < 8 && w * 8 + b < nbytes; b++) o[b] = (uint8_t)(z >> (8 * b));
+}
+
+hipError_t enb_launch_synth_payloads(uint8_t* out, uint64_t first, uint32_t n, uint32_t ntb, uint32_t nbytes,
+                                     uint64_t seed, hipStream_t s)
+{
+  const uint64_t total = (uint64_t)n * ntb * ((nbytes + 7) / 8);
+  if (!total) return hipSuccess;
+  hipLaunchKernelGGL(enb_synth_payloads, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, out, first, n, ntb,
+                     nbytes, seed);
   return hipGetLastError();
 }
 

@@ -587,6 +587,13 @@ int mi355_channel_fading_grid_batch(mi355_enb_dl_t* q, const float* const* tx, f
 int mi355_channel_grid_batch(mi355_enb_dl_t* q, const float* const* tx, float* const* rx, uint32_t n, uint32_t nof_rx,
                              const float* H, float sigma, uint64_t seed, void* stream)
 {
+  return mi355_channel_grid_batch_at(q, tx, rx, n, nof_rx, H, sigma, seed, 0, stream);
+}
+
+int mi355_channel_grid_batch_at(mi355_enb_dl_t* q, const float* const* tx, float* const* rx, uint32_t n,
+                                uint32_t nof_rx, const float* H, float sigma, uint64_t seed, uint64_t first_index,
+                                void* stream)
+{
   if (!q || !H || nof_rx == 0 || nof_rx > 2 || (n && (!tx || !rx)) || !(sigma >= 0.f)) return MI355_ERROR_INVALID_INPUTS;
   if (!n) return MI355_SUCCESS;
   std::lock_guard<std::mutex> lk(q->mu);
@@ -614,7 +621,21 @@ int mi355_channel_grid_batch(mi355_enb_dl_t* q, const float* const* tx, float* c
   q->st.put(jobs.data(), n * sizeof(EnbChanJob));
   if (upload_on(q->st, base, s)) return MI355_ERROR;
   const uint32_t nsym = 2 * q->ofdm.nsymb;
-  CHECK_HIP(enb_launch_channel((const EnbChanJob*)base, n, nsym * q->ofdm.nre, np, nof_rx, M, sigma, seed, s));
+  CHECK_HIP(enb_launch_channel((const EnbChanJob*)base, n, nsym * q->ofdm.nre, np, nof_rx, M, sigma, seed, first_index,
+                               s));
+  if (!stream) CHECK_HIP(hipStreamSynchronize(s));
+  return MI355_SUCCESS;
+}
+
+int mi355_enb_synth_payloads(mi355_enb_dl_t* q, uint8_t* out, uint64_t first_index, uint32_t n, uint32_t ntb,
+                             uint32_t nbytes, uint64_t seed, void* stream)
+{
+  if (!q || (n && !out) || ntb == 0 || ntb > 255 || nbytes == 0) return MI355_ERROR_INVALID_INPUTS;
+  if (!n) return MI355_SUCCESS;
+  std::lock_guard<std::mutex> lk(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t s = stream ? (hipStream_t)stream : q->own;
+  CHECK_HIP(enb_launch_synth_payloads(out, first_index, n, ntb, nbytes, seed, s));
   if (!stream) CHECK_HIP(hipStreamSynchronize(s));
   return MI355_SUCCESS;
 }

@@ -63,10 +63,30 @@ def _declare_gpu():
     L.mi355_enb_dl_gen_signal_batch.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), u32, vp]
     L.mi355_channel_grid_batch.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), u32, u32, C.POINTER(C.c_float),
                                            C.c_float, C.c_uint64, vp]
+    L.mi355_channel_grid_batch_at.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), u32, u32, C.POINTER(C.c_float),
+                                              C.c_float, C.c_uint64, C.c_uint64, vp]
+    L.mi355_enb_synth_payloads.argtypes = [vp, vp, C.c_uint64, u32, u32, u32, C.c_uint64, vp]
     L.mi355_channel_fading_grid_batch.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), u32, u32, C.c_char_p,
                                                   C.POINTER(C.c_double), C.c_float, u32, vp]
     L._enb_gpu_declared = True
     return L
+
+
+def _splitmix64(z: np.ndarray) -> np.ndarray:
+    z = (z + np.uint64(0x9E3779B97F4A7C15)).astype(np.uint64)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def synth_payloads_host(first_index: int, n: int, ntb: int, nbytes: int, seed: int) -> np.ndarray:
+    """Host restatement of mi355_enb_synth_payloads (checks a sample of a large run): (n, ntb, nbytes) uint8."""
+    words = (nbytes + 7) // 8
+    with np.errstate(over="ignore"):
+        it = (np.uint64(first_index) + np.arange(n, dtype=np.uint64))[:, None] << np.uint64(8)
+        key = _splitmix64(it | np.arange(ntb, dtype=np.uint64)[None, :])  # (n, ntb)
+        z = _splitmix64(np.uint64(seed) ^ (key[:, :, None] + np.arange(words, dtype=np.uint64)[None, None, :]))
+    return z.astype("<u8").view(np.uint8).reshape(n, ntb, words * 8)[:, :, :nbytes].copy()
 
 
 def _arr(t, v):
@@ -96,13 +116,24 @@ class EnbDl:
         check(self.L.mi355_enb_dl_gen_signal_batch(self.h, _arr(C.c_void_p, grids), _arr(C.c_void_p, out), len(grids),
                                                    stream), "enb_dl_gen_signal")
 
-    def channel(self, tx, rx, nof_rx: int, H: np.ndarray, sigma: float, seed: int, stream=None):
-        """rx grids (nof_rx per job) = H (nof_rx x nof_ports complex) . tx grids (nof_ports per job) + AWGN."""
+    def channel(self, tx, rx, nof_rx: int, H: np.ndarray, sigma: float, seed: int, stream=None, first_index=None):
+        """rx grids (nof_rx per job) = H (nof_rx x nof_ports complex) . tx grids (nof_ports per job) + AWGN; with
+        first_index the noise of job i is keyed by the global subframe index first_index + i."""
         n = len(rx) // nof_rx
         h = np.ascontiguousarray(np.asarray(H, np.complex64)).view(np.float32).ravel()
         hf = (C.c_float * len(h))(*h.tolist())
-        check(self.L.mi355_channel_grid_batch(self.h, _arr(C.c_void_p, tx), _arr(C.c_void_p, rx), n, nof_rx, hf,
-                                              float(sigma), int(seed) & (2**64 - 1), stream), "channel_grid")
+        if first_index is None:
+            check(self.L.mi355_channel_grid_batch(self.h, _arr(C.c_void_p, tx), _arr(C.c_void_p, rx), n, nof_rx, hf,
+                                                  float(sigma), int(seed) & (2**64 - 1), stream), "channel_grid")
+        else:
+            check(self.L.mi355_channel_grid_batch_at(self.h, _arr(C.c_void_p, tx), _arr(C.c_void_p, rx), n, nof_rx,
+                                                     hf, float(sigma), int(seed) & (2**64 - 1), int(first_index),
+                                                     stream), "channel_grid_at")
+
+    def synth_payloads(self, out: int, first_index: int, n: int, ntb: int, nbytes: int, seed: int, stream=None):
+        """Device payloads of n subframes keyed by their global index (mi355_enb_synth_payloads)."""
+        check(self.L.mi355_enb_synth_payloads(self.h, out, int(first_index), n, ntb, nbytes, int(seed) & (2**64 - 1),
+                                              stream), "enb_synth_payloads")
 
     def fading(self, tx, rx, nof_rx: int, model: str, t_sf, sigma: float, seed: int, stream=None):
         """Multipath fading (srslte_channel_fading_t: model "epa5", "eva70", "etu300", "none0" ...) + AWGN in the

@@ -241,3 +241,32 @@ def test_generator_round_trip_tm4():
             assert res[2 * i + t].ret == 0 and res[2 * i + t].crc, (i, t)
             got = outs[i][t].download(np.zeros(cfg0.tbs[t] // 8 + 16, np.uint8))[: cfg0.tbs[t] // 8]
             np.testing.assert_array_equal(got, pls[i][t])
+
+
+def test_indexed_synthesis_is_shard_invariant():
+    """bench.py --total-subframes: payloads (mi355_enb_synth_payloads) equal their host restatement, and the AWGN of
+    mi355_channel_grid_batch_at depends on the global subframe index only -- one call over [10, 14) equals two calls
+    over [10, 12) and [12, 14); first_index 0 equals the plain call."""
+    cell = P.make_cell(6, 2, 1)
+    G = 14 * 12 * 6
+    enb = enb_dl.EnbDl(cell)
+    d = dev_zeros(5 * 2 * 1001)
+    enb.synth_payloads(d.ptr, (1 << 40) + 3, 5, 2, 1001, 99)
+    got = d.download(np.zeros(5 * 2 * 1001, np.uint8)).reshape(5, 2, 1001)
+    assert np.array_equal(got, enb_dl.synth_payloads_host((1 << 40) + 3, 5, 2, 1001, 99))
+    assert not np.array_equal(got[0, 0], got[0, 1]) and not np.array_equal(got[0, 0], got[1, 0])
+    H = np.array([[1, 1], [1, -1]], np.complex64)
+    zero = [dev_zeros(G * 8) for _ in range(2 * 4)]
+    one = [dev_zeros(G * 8) for _ in range(2 * 4)]
+    two = [dev_zeros(G * 8) for _ in range(2 * 4)]
+    enb.channel([t.ptr for t in zero], [r.ptr for r in one], 2, H, 0.5, 77, first_index=10)
+    enb.channel([t.ptr for t in zero[:4]], [r.ptr for r in two[:4]], 2, H, 0.5, 77, first_index=10)
+    enb.channel([t.ptr for t in zero[4:]], [r.ptr for r in two[4:]], 2, H, 0.5, 77, first_index=12)
+    a = np.stack([r.download(np.zeros(G, np.complex64)) for r in one])
+    b = np.stack([r.download(np.zeros(G, np.complex64)) for r in two])
+    assert np.array_equal(a, b) and np.abs(a).max() > 0
+    enb.channel([t.ptr for t in zero], [r.ptr for r in one], 2, H, 0.5, 77, first_index=0)
+    enb.channel([t.ptr for t in zero], [r.ptr for r in two], 2, H, 0.5, 77)
+    a = np.stack([r.download(np.zeros(G, np.complex64)) for r in one])
+    b = np.stack([r.download(np.zeros(G, np.complex64)) for r in two])
+    assert np.array_equal(a, b)

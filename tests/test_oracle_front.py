@@ -1,0 +1,68 @@
+"""CPU tests of oracle/orc_front.c, the C front end bench.py's cpu_baseline times: its FFT against numpy's float64
+DFT (srslte_ofdm_rx_sf semantics, ofdm.c:392-471), and the whole OFDM -> estimation -> PDSCH chain against the
+Python oracle chain (ue_dl_chain + pdsch_chain) on the same I/Q."""
+import numpy as np
+import pytest
+
+import oracle
+from oracle import pdsch_chain as pc
+from oracle import ue_dl_chain as uc
+
+
+@pytest.mark.parametrize("nof_prb", [6, 15, 25, 50, 75, 100])
+def test_ofdm_rx_sf_matches_dft(nof_prb):
+    N = uc.symbol_sz(nof_prb)
+    rng = np.random.default_rng(nof_prb)
+    iq = (rng.standard_normal(15 * N) + 1j * rng.standard_normal(15 * N)).astype(np.complex64)
+    want = uc.ofdm_rx_sf(iq, nof_prb)
+    got = np.zeros(14 * 12 * nof_prb, np.complex64)
+    assert oracle.lib().orc_ofdm_rx_sf(iq.view(np.float32), nof_prb, got.view(np.float32)) == 0
+    rms = np.sqrt(np.mean(np.abs(want) ** 2))
+    assert np.abs(got - want).max() <= 2e-6 * rms  # float32 Stockham vs float64: measured <= 5e-7
+
+
+@pytest.mark.parametrize("case", ["tm4_256", "siso_qpsk", "tm4_16_power"])
+def test_front_matches_python_chain(case):
+    if case == "tm4_256":
+        cfg = pc.Cfg(nof_prb=25, nof_ports=2, nof_rx=2, cell_id=1, cfi=1, sf_idx=3, scheme=2, nof_layers=2,
+                     qm=[8, 8], tbs=[pc.valid_tbs(16000)] * 2, csi_enable=True)
+    elif case == "siso_qpsk":
+        cfg = pc.Cfg(nof_prb=15, nof_ports=1, nof_rx=1, cell_id=7, cfi=2, sf_idx=4, qm=[2], tbs=[pc.valid_tbs(2000)])
+    else:
+        cfg = pc.Cfg(nof_prb=25, nof_ports=2, nof_rx=2, cell_id=2, cfi=2, sf_idx=6, scheme=2, nof_layers=2,
+                     qm=[4, 4], tbs=[pc.valid_tbs(9000)] * 2, csi_enable=True, power_scale=True, p_a=-3.0, p_b=1)
+    iq, _payload, _h, _s2 = uc.synth_iq(cfg, np.random.default_rng(5), snr_db=30,
+                                        channel="cross" if cfg.nof_ports == 2 else "taps")
+    e_c, noise_c = oracle.ue_dl_front(cfg, iq)
+    grids = np.stack([uc.ofdm_rx_sf(iq[r], cfg.nof_prb) for r in range(cfg.nof_rx)])
+    ce, res = uc.chest_estimate(grids, cfg.nof_prb, cfg.nof_ports, cfg.cell_id, cfg.sf_idx)
+    _, _, e_p = pc.rx_front(cfg, grids, ce, res["noise_estimate"])
+    assert abs(noise_c - res["noise_estimate"]) <= 1e-3 * res["noise_estimate"]
+    for t in range(cfg.nof_tb):
+        assert e_c[t].shape == e_p[t].shape
+        d = np.abs(e_c[t].astype(np.int32) - e_p[t].astype(np.int32))
+        assert d.max() <= 2 and np.mean(d > 0) < 0.02  # float32 vs float64 FFT: LSB-level differences only
+
+
+def test_rm_tb_matches_decode_path():
+    """orc_dlsch_rm_tb writes the same decoder buffers as orc_dlsch_decode_tb's rate dematching (incl. gamma != 0)."""
+    rng = np.random.default_rng(3)
+    for tbs, qm, G in ((pc.valid_tbs(20000), 6, 6 * 5000 + 6 * 7), (97896, 8, 115200)):
+        e = rng.integers(-300, 300, G, dtype=np.int16)
+        seg = np.zeros(6, np.uint32)
+        oracle.lib().orc_cbsegm(tbs, seg)
+        Cn = int(seg[0])
+        sb = np.zeros(Cn * 18600, np.int16)
+        assert oracle.lib().orc_dlsch_rm_tb(e, G, tbs, qm, 0, sb, 18600) == Cn
+        Gp, gamma = G // qm, (G // qm) % Cn
+        rp = 0
+        for cb in range(Cn):
+            n_e = qm * (Gp // Cn) + (qm if cb > Cn - gamma else 0)
+            if cb > Cn - gamma:
+                rp = (Cn - gamma) * qm * (Gp // Cn) + (cb - (Cn - gamma)) * n_e
+            else:
+                rp = cb * qm * (Gp // Cn)
+            K = int(seg[1])
+            want = np.zeros(18600, np.int16)
+            oracle.lib().orc_rm_turbo_rx(np.ascontiguousarray(e[rp: rp + n_e]), n_e, want, K, 0)
+            assert np.array_equal(sb[cb * 18600:(cb + 1) * 18600], want)

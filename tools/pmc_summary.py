@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Summarise a tools/profile_tdec.sh run into profiles/<tag>_*.
+"""Summarise a tools/profile_tdec.sh run into profiles/<tag>_* and profiles/r02_tdec_pmc.json (read by bench.py).
 
-HBM bytes per MAP launch = FETCH_SIZE + WRITE_SIZE (KB units), with FETCH_SIZE corrected by a factor
-calibrated on this kernel's own access pattern: the loads-only diagnostic build (MI355_TDEC_DIAG=4)
-reads an exactly known byte count (MI355_MICROARCH.md "HBM": FETCH_SIZE under-reports wide streaming
-reads by 2x on gfx950 -- calibrate on a known byte count before trusting an absolute)."""
+HBM bytes per MAP launch, as MI355X_MICROARCH.md's HBM section prescribes for gfx950: 2 x FETCH_SIZE (it counts
+half the bytes of wide coalesced reads) + WRITE_SIZE (exact), both KB, each from its own --pmc pass.  The file is
+keyed by the SHA-1 of the MAP kernel's sources (bench.map_kernel_hash): bench.py refuses a summary recorded on
+other sources."""
 import collections
 import csv
 import glob
@@ -13,8 +13,9 @@ import os
 import shutil
 import sys
 
-TAG = sys.argv[1] if len(sys.argv) > 1 else "r01"
+TAG = sys.argv[1] if len(sys.argv) > 1 else "r02"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 P = os.path.join(ROOT, "gpurun_out", f"prof_{TAG}")
 OUTD = os.path.join(ROOT, "profiles")
 MAP = "tdec_win_halfit"
@@ -23,6 +24,8 @@ NCB, K = 65536, 6144
 
 def counters(sub):
     f = glob.glob(os.path.join(P, sub, "**", "*counter_collection.csv"), recursive=True)
+    if not f:
+        return {}
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f[0])):
         agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
@@ -31,35 +34,31 @@ def counters(sub):
 
 def per_kernel(agg, counter, pat=MAP):
     vals = [v for (k, c), vs in agg.items() if pat in k and c == counter for v in vs]
-    return sum(vals) / max(len(vals), 1), len(vals)
+    return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
 
 def main():
+    import bench
     os.makedirs(OUTD, exist_ok=True)
-    stats = glob.glob(os.path.join(P, "trace", "**", "*kernel_stats.csv"), recursive=True)[0]
-    shutil.copy(stats, os.path.join(OUTD, f"{TAG}_kernel_stats.csv"))
-    e2e = glob.glob(os.path.join(P, "e2e", "**", "*kernel_stats.csv"), recursive=True)
-    if e2e:
-        shutil.copy(e2e[0], os.path.join(OUTD, f"{TAG}_e2e_kernel_stats.csv"))
-    fetch, _ = per_kernel(counters("fetch"), "FETCH_SIZE")
-    write, _ = per_kernel(counters("write"), "WRITE_SIZE")
-    calib_fetch, _ = per_kernel(counters("calib"), "FETCH_SIZE")
-    # loads-only variant: the 8 launches of a step read S,P0 (n=0), E,P1 (DEC2) or S,A1,P0 (DEC1)
-    # twice?  No: the loads-only variant runs the backward pass only -> one read of each array.
-    known = NCB * 2 * K * (2 + 3 * 3 + 2 * 4) / 8  # avg over n=0..7 of arrays read once
-    factor = known / (calib_fetch * 1024) if calib_fetch else None
+    for sub, name in (("trace", "kernel_stats"), ("e2e", "e2e_kernel_stats")):
+        f = glob.glob(os.path.join(P, sub, "**", "*kernel_stats.csv"), recursive=True)
+        if f:
+            shutil.copy(f[0], os.path.join(OUTD, f"{TAG}_{name}.csv"))
+    fetch, nf = per_kernel(counters("fetch"), "FETCH_SIZE")
+    write, nw = per_kernel(counters("write"), "WRITE_SIZE")
     sq = counters("sq")
     valu, _ = per_kernel(sq, "SQ_INSTS_VALU")
     waves, _ = per_kernel(sq, "SQ_WAVES")
+    hbm = 2 * fetch * 1024 + write * 1024 if (fetch is not None and write is not None) else None
     res = {
-        "tag": TAG, "kernel": MAP, "launch_ncb": NCB, "K": K,
-        "fetch_size_kb_per_launch": fetch, "write_size_kb_per_launch": write,
-        "fetch_calibration": {"known_bytes": known, "fetch_size_kb": calib_fetch, "factor": factor},
-        "bytes_per_launch": (fetch * 1024 * (factor or 1.0) + write * 1024),
+        "tag": TAG, "kernel": MAP, "kernel_src_sha1": bench.map_kernel_hash(), "launch_ncb": NCB, "K": K,
+        "fetch_size_kb_per_launch": fetch, "write_size_kb_per_launch": write, "launches_counted": [nf, nw],
+        "hbm_bytes_per_launch": hbm,
+        "hbm_rule": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md, HBM [CDNA4])",
         "valu_insts_per_launch": valu, "waves_per_launch": waves,
-        "valu_lane_ops_per_cb_halfit": valu * 64 / NCB if valu else None,
+        "valu_lane_instr_per_cb_halfit": valu * 64 / NCB if valu else None,
     }
-    json.dump(res, open(os.path.join(OUTD, "tdec_pmc_traffic.json"), "w"), indent=1)
+    json.dump(res, open(os.path.join(OUTD, "r02_tdec_pmc.json"), "w"), indent=1)
     json.dump(res, open(os.path.join(OUTD, f"{TAG}_pmc_summary.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
