@@ -43,6 +43,11 @@ int mi355_softbuffer_reset_tbs_batch(mi355_softbuffer_pool_t* p, const uint32_t*
 /* device address of the pool's int16 code-block buffers (slot = sb * max_cb + cb, `stride` int16 apart) */
 int mi355_softbuffer_pool_buffer(mi355_softbuffer_pool_t* p, int16_t** buf, uint32_t* stride, uint32_t* max_cb);
 
+/* device address of the pool's per-code-block decoded bytes (slot = sb * max_cb + cb, `stride` bytes apart) and the
+ * pool's softbuffer count */
+int mi355_softbuffer_pool_data(mi355_softbuffer_pool_t* p, uint8_t** data, uint32_t* stride, uint32_t* nof_sb);
+/* host copy of softbuffer sb's per-code-block CRC flags (max_cb bytes, 1 = the CB passed in an earlier decode) */
+int mi355_softbuffer_get_cb_crc(mi355_softbuffer_pool_t* p, uint32_t sb, uint8_t* cb_crc, void* stream);
 typedef struct {
   uint32_t tbs;         /* transport block size in bits (grant.tb[i].tbs) */
   uint32_t nof_e_bits;  /* coded LLRs of the codeword (grant.tb[i].nof_bits) */

@@ -305,6 +305,25 @@ int mi355_softbuffer_pool_buffer(mi355_softbuffer_pool_t* p, int16_t** buf, uint
   return MI355_SUCCESS;
 }
 
+int mi355_softbuffer_pool_data(mi355_softbuffer_pool_t* p, uint8_t** data, uint32_t* stride, uint32_t* nof_sb)
+{
+  if (!p) return MI355_ERROR_INVALID_INPUTS;
+  if (data) *data = p->data;
+  if (stride) *stride = SB_DATA;
+  if (nof_sb) *nof_sb = p->nof_sb;
+  return MI355_SUCCESS;
+}
+
+int mi355_softbuffer_get_cb_crc(mi355_softbuffer_pool_t* p, uint32_t sb, uint8_t* cb_crc, void* stream)
+{
+  if (!p || !cb_crc || sb >= p->nof_sb) return MI355_ERROR_INVALID_INPUTS;
+  CHECK_HIP(hipSetDevice(p->device));
+  hipStream_t s = (hipStream_t)stream;
+  CHECK_HIP(hipMemcpyAsync(cb_crc, p->cb_crc + (size_t)sb * p->max_cb, p->max_cb, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(hipStreamSynchronize(s));
+  return MI355_SUCCESS;
+}
+
 int mi355_dlsch_create(mi355_dlsch_t** q, int device)
 {
   if (!q) return MI355_ERROR_INVALID_INPUTS;
