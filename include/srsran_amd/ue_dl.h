@@ -8,7 +8,9 @@
  *                                ue_dl.c:93 configures it), FFT-shift dropping DC: out[0:nre/2] =
  *                                X[N-nre/2:N], out[nre/2:nre] = X[1:nre/2+1].
  *   mi355_chest_dl_estimate_batch srslte_chest_dl_estimate_cfg (ch_estimation/chest_dl.c:985-1014) for normal
- *                                FDD subframes: CRS LS estimates, RSRP/RSSI, REFS noise estimation, Gauss /
+ *                                FDD subframes: sync-error estimation and correction (:731-786), CRS LS
+ *                                estimates, RSRP/RSSI, REFS / PSS / EMPTY noise estimation, CFO estimation
+ *                                (:596-618, in the subframes cfo_estimate_sf_mask selects), Gauss /
  *                                triangle / no smoothing, AVERAGE estimator (merged pilots, linear interpolation,
  *                                the same estimate on every OFDM symbol) or INTERPOLATE (each pilot symbol
  *                                smoothed and interpolated in frequency, then linearly in time, :430-531),
@@ -45,6 +47,7 @@ typedef struct {
   uint32_t rsrp_neighbour;
   uint32_t cfo_estimate_enable;
   uint32_t sync_error_enable;
+  uint32_t cfo_estimate_sf_mask; /* subframes (bit tti % 10) in which the CFO is estimated (chest_dl.c:635) */
 } mi355_chest_dl_cfg_t;
 
 /* srslte_chest_dl_res_t scalars (chest_dl.h:50-68); ce pointers live in the job */
@@ -75,7 +78,16 @@ typedef struct {
   const float* in_buffer[MI355_MAX_RX_ANT];
   float*       sf_symbols[MI355_MAX_RX_ANT];
   float*       ce[MI355_MAX_PORTS][MI355_MAX_RX_ANT];
+  uint32_t     link; /* the estimator state (one srslte_chest_dl_t) this subframe belongs to, < MI355_MAX_LINKS */
 } mi355_dl_sf_job_t;
+
+/* Estimator state.  srslte_chest_dl_t carries values from one subframe to the next: the CFO estimate (updated only
+ * in the subframes cfo_estimate_sf_mask selects), the PSS / EMPTY noise estimates (updated only in subframes 0 and 5;
+ * the Gauss filter's automatic sigma reads them) and the sync error.  Each job names its link; the jobs of one link
+ * are taken in batch order, and the state carries over to the link's jobs in later calls -- so one link is one UE
+ * receiver's srslte_chest_dl_t, and a batch may hold many links.  Links start zeroed (and are zeroed by
+ * mi355_ue_dl_reset_link). */
+#define MI355_MAX_LINKS 65536
 
 typedef struct mi355_ue_dl mi355_ue_dl_t;
 
@@ -86,6 +98,9 @@ int  mi355_ue_dl_create(mi355_ue_dl_t** q, const mi355_cell_t* cell, uint32_t no
 void mi355_ue_dl_destroy(mi355_ue_dl_t* q);
 /* srslte_use_standard_symbol_size: switch the DFT size to the 3GPP rates (2048 for 100 PRB) */
 int mi355_ue_dl_set_standard_rates(mi355_ue_dl_t* q, int enable);
+
+/* Zero one link's estimator state (srslte_chest_dl_init / set_cell). */
+int mi355_ue_dl_reset_link(mi355_ue_dl_t* q, uint32_t link);
 
 /* OFDM demodulation of every job's rx antennas (in_buffer -> sf_symbols). */
 int mi355_ofdm_rx_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, void* stream);

@@ -74,6 +74,19 @@ def lib() -> C.CDLL:
         L.orc_crs_pilots.argtypes = [C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, f32p]
         L.orc_chest_estimate_port.argtypes = [f32p, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, C.c_int,
                                               C.c_float, C.c_float, C.c_int, f32p, f32p]
+        L.orc_chest_estimate_port_st.argtypes = [f32p, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32,
+                                                 C.c_int, C.c_float, C.c_float, C.c_int, C.c_int, C.c_float, f32p,
+                                                 f32p]
+        L.orc_chest_sync_correct.argtypes = [f32p, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32,
+                                             C.c_uint32, f32p]
+        L.orc_chest_cfo.restype = C.c_float
+        L.orc_chest_cfo.argtypes = [f32p, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32,
+                                    C.c_uint32]
+        L.orc_noise_empty.restype = C.c_float
+        L.orc_noise_empty.argtypes = [f32p, C.c_uint32, C.c_int]
+        L.orc_pss_generate.argtypes = [C.c_uint32, f32p]
+        L.orc_noise_pss.restype = C.c_float
+        L.orc_noise_pss.argtypes = [f32p, f32p, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32]
         L.orc_predecode.argtypes = [f32p, f32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
                                     C.c_float, f32p, f32p, f32p]
         L.orc_ofdm_rx_sf.argtypes = [f32p, C.c_uint32, f32p]

@@ -45,6 +45,17 @@ void orc_crs_pilots(uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t p, 
 int  orc_chest_estimate_port(const float* grid, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf,
                              uint32_t port, int filter_type, float coef0, float coef1, int estimator_alg, float* ce,
                              float* out3);
+int  orc_chest_estimate_port_st(const float* grid, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf,
+                                uint32_t port, int filter_type, float coef0, float coef1, int estimator_alg,
+                                int noise_alg, float noise_state, float* ce, float* out3);
+void  orc_chest_sync_correct(float* grid, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf,
+                             uint32_t nof_ports, uint32_t symbol_sz, float* sync_err);
+float orc_chest_cfo(const float* grid, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf, uint32_t port_a,
+                    uint32_t port_b, uint32_t symbol_sz);
+float orc_noise_empty(const float* grid, uint32_t nof_prb, int cp_ext);
+void  orc_pss_generate(uint32_t n_id_2, float* out);
+float orc_noise_pss(const float* grid, const float* ce, uint32_t nof_prb, int cp_ext, uint32_t cell_id,
+                    uint32_t nof_ports);
 int orc_predecode(const float* y, const float* h, int nof_rx, int nof_ports, int nof_layers, int cb, int n,
                   int type, float scaling, float noise, float* x, float* csi0, float* csi1);
 

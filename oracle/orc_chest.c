@@ -187,9 +187,25 @@ static float noise_refs(const cf* pe, uint32_t nsymbols, uint32_t nref, uint32_t
  * output (INTERPOLATE with 2 pilot symbols -- ports 2, 3 -- copies the buffer's row 0, which it never writes,
  * over every other row: chest_dl.c:490-494 as the reference runs it).  out3: {noise_estimate, rsrp, rssi}.
  * Returns -1 for unsupported configurations. */
+int orc_chest_estimate_port_st(const float* grid_f, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf,
+                               uint32_t port, int filter_type, float coef0, float coef1, int estimator_alg,
+                               int noise_alg, float noise_state, float* ce_f, float* out3);
+
 int orc_chest_estimate_port(const float* grid_f, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf,
                             uint32_t port, int filter_type, float coef0, float coef1, int estimator_alg,
                             float* ce_f, float* out3)
+{
+  return orc_chest_estimate_port_st(grid_f, nof_prb, cell_id, cp_ext, sf, port, filter_type, coef0, coef1,
+                                    estimator_alg, 0, 0.0f, ce_f, out3);
+}
+
+/* estimate_port with the estimator's noise state: noise_alg 0 (REFS) estimates the noise from the pilots and the
+ * automatic Gauss sigma reads it; otherwise (PSS / EMPTY, whose estimates come after the interpolation,
+ * chest_dl.c:714-725) the sigma reads noise_state -- the state before this subframe -- and out3[0] = noise_state
+ * (the caller replaces it in subframes 0 and 5). */
+int orc_chest_estimate_port_st(const float* grid_f, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf,
+                               uint32_t port, int filter_type, float coef0, float coef1, int estimator_alg,
+                               int noise_alg, float noise_state, float* ce_f, float* out3)
 {
   if (estimator_alg != 0 && estimator_alg != 1) return -1;
   const cf*      grid  = (const cf*)grid_f;
@@ -216,7 +232,7 @@ int orc_chest_estimate_port(const float* grid_f, uint32_t nof_prb, uint32_t cell
   for (uint32_t k = 0; k < np; k++) rsrp += cpw(rx[k]);
   rsrp /= (float)np;
   rssi /= (float)nsym;
-  const float noise = noise_refs(pe, nsym, nref, crs_fidx(cell_id, 0, port));
+  const float noise = noise_alg == 0 ? noise_refs(pe, nsym, nref, crs_fidx(cell_id, 0, port)) : noise_state;
 
   float    filt[16];
   uint32_t flen = 0;
@@ -310,4 +326,162 @@ int orc_chest_estimate_port(const float* grid_f, uint32_t nof_prb, uint32_t cell
   free(smo);
   (void)nr;
   return 0;
+}
+
+/* ---- estimator state stages (chest_dl.c) ---------------------------------------------------------------------- */
+
+/* srslte_vec_estimate_frequency (utils/vector_simd.c:1720-1763), sequential sum */
+static float estimate_frequency(const cf* x, int len)
+{
+  double sre = 0, sim = 0; /* the reference's SIMD partial sums differ in order: tolerance */
+  for (int i = 1; i < len; i++) {
+    const cf z = cprod_conj(x[i], x[i - 1]);
+    sre += z.re;
+    sim += z.im;
+  }
+  return (float)(-atan2f((float)sim, (float)sre) * M_1_PI * 0.5f);
+}
+
+/* srslte_vec_apply_cfo (vector_simd.c:1670-1718) as the AVX2 build runs it: 8 lanes with phases cexpf(j 2 pi cfo k),
+ * advanced by cexpf(j 2 pi cfo 8) per 8 samples, then a scalar tail */
+static void apply_cfo(cf* x, float cfo, int len)
+{
+  const float TWOPI = 2.0f * (float)M_PI;
+  int         i     = 0;
+  cf          ph[8], osc8 = cmk(cosf(TWOPI * cfo * 8), sinf(TWOPI * cfo * 8));
+  for (int k = 0; k < 8; k++) ph[k] = cmk(cosf(TWOPI * cfo * k), sinf(TWOPI * cfo * k));
+  for (; i < len - 8 + 1; i += 8) {
+    for (int k = 0; k < 8; k++) {
+      const cf a = x[i + k], p = ph[k];
+      x[i + k]   = cmk(a.re * p.re - a.im * p.im, a.re * p.im + a.im * p.re);
+      ph[k]      = cmk(p.re * osc8.re - p.im * osc8.im, p.re * osc8.im + p.im * osc8.re);
+    }
+  }
+  cf osc = cmk(cosf(TWOPI * cfo), sinf(TWOPI * cfo)), phase = cmk(cosf(TWOPI * cfo * i), sinf(TWOPI * cfo * i));
+  for (; i < len; i++) {
+    const cf a = x[i];
+    x[i]       = cmk(a.re * phase.re - a.im * phase.im, a.re * phase.im + a.im * phase.re);
+    phase      = cmk(phase.re * osc.re - phase.im * osc.im, phase.re * osc.im + phase.im * osc.re);
+  }
+}
+
+/* LS estimates of one port's pilots (srslte_refsignal_cs_get_sf + srslte_vec_prod_conj_ccc) */
+static void ls_pilots(const cf* grid, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf, uint32_t port, cf* pe)
+{
+  const uint32_t nsymb = cp_ext ? 6 : 7, nre = 12 * nof_prb, nref = 2 * nof_prb, nsym = crs_nof_symbols(port);
+  cf*            crs   = malloc(sizeof(cf) * 4 * nref);
+  orc_crs_pilots(nof_prb, cell_id, cp_ext, port / 2, sf, (float*)crs);
+  for (uint32_t l = 0; l < nsym; l++) {
+    const uint32_t s = crs_nsymbol(l, nsymb, port), f = crs_fidx(cell_id, l, port);
+    for (uint32_t i = 0; i < nref; i++) pe[l * nref + i] = cprod_conj(grid[s * nre + f + 6 * i], crs[l * nref + i]);
+  }
+  free(crs);
+}
+
+/* chest_dl_estimate_correct_sync_error (chest_dl.c:731-786) for one rx antenna's grid, corrected in place;
+ * sync_err[port] receives q->sync_err[rx][port].  symbol_sz: srslte_symbol_sz(nof_prb). */
+void orc_chest_sync_correct(float* grid_f, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf,
+                            uint32_t nof_ports, uint32_t symbol_sz, float* sync_err)
+{
+  cf*            grid = (cf*)grid_f;
+  const uint32_t nref = 2 * nof_prb, nre = 12 * nof_prb, nsymb = cp_ext ? 6 : 7;
+  cf*            pe   = malloc(sizeof(cf) * 4 * nref);
+  float          pwr_sum = 0.0f, se = 0.0f;
+  for (uint32_t p = 0; p < nof_ports; p++) {
+    const uint32_t nsym = crs_nof_symbols(p), npilots = nsym * nref;
+    ls_pilots(grid, nof_prb, cell_id, cp_ext, sf, p, pe);
+    const float k   = (float)symbol_sz / 6.0f;
+    float       sum = 0.0f;
+    for (uint32_t i = 0; i < nsym; i++) sum += estimate_frequency(pe + i * npilots / nsym, npilots / nsym) * k;
+    float pwr = 0;
+    for (uint32_t i = 0; i < npilots; i++) pwr += cpw(pe[i]);
+    pwr /= (float)npilots; /* srslte_vec_avg_power_cf */
+    sync_err[p] = sum / nsym;
+    if (!isinf(sum) && !isnan(sum) && !isinf(pwr) && !isnan(pwr)) {
+      se += sync_err[p] * pwr;
+      pwr_sum += pwr;
+    }
+  }
+  if (isnormal(pwr_sum)) se /= pwr_sum;
+  if (isnormal(se) && fabsf(se) > 0.05f) {
+    const float cfo = se / (float)symbol_sz;
+    for (uint32_t i = 0; i < 2 * nsymb; i++) apply_cfo(&grid[i * nre], cfo, (int)nre);
+  }
+  free(pe);
+}
+
+/* chest_estimate_cfo (chest_dl.c:596-618): the LS buffer holds port_a's pilot symbols 0, 1 and port_b's 2, 3 (the
+ * last port estimated, and for ports 2 / 3 port 1's leftovers) */
+float orc_chest_cfo(const float* grid_f, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf, uint32_t port_a,
+                    uint32_t port_b, uint32_t symbol_sz)
+{
+  const cf*      grid = (const cf*)grid_f;
+  const uint32_t nref = 2 * nof_prb;
+  cf*            pa   = malloc(sizeof(cf) * 4 * nref);
+  cf*            pb   = malloc(sizeof(cf) * 4 * nref);
+  ls_pilots(grid, nof_prb, cell_id, cp_ext, sf, port_a, pa);
+  ls_pilots(grid, nof_prb, cell_id, cp_ext, sf, port_b, pb);
+  double sre = 0, sim = 0;
+  for (int i = 0; i < 2; i++) {
+    for (uint32_t k = 0; k < nref; k++) {
+      const cf z = cprod_conj(pa[i * nref + k], pb[(i + 2) * nref + k]);
+      sre += z.re;
+      sim += z.im;
+    }
+  }
+  free(pa);
+  free(pb);
+  const float n = (float)symbol_sz, ns = (float)(cp_ext ? 6 : 7);
+  const float ng = (float)(int)ceilf(144.0f * (float)symbol_sz / 2048.0f); /* SRSLTE_CP_LEN_NORM(1, n) */
+  return (float)(-atan2f((float)sim, (float)sre) * n / (ns * (n + ng)) / 2 / M_PI);
+}
+
+/* estimate_noise_empty_sc (chest_dl.c:419-430) */
+float orc_noise_empty(const float* grid_f, uint32_t nof_prb, int cp_ext)
+{
+  const cf* in    = (const cf*)grid_f;
+  const int nre   = 12 * (int)nof_prb, nsymb = cp_ext ? 6 : 7;
+  const int k_sss = (nsymb - 2) * nre + nre / 2 - 31, k_pss = (nsymb - 1) * nre + nre / 2 - 31;
+  const int ks[4] = {k_sss - 5, k_sss + 62, k_pss - 5, k_pss + 62};
+  float     np    = 0;
+  for (int g = 0; g < 4; g++) {
+    float s = 0;
+    for (int j = 0; j < 5; j++) s += cpw(in[ks[g] + j]);
+    np += s / 5.0f;
+  }
+  return np;
+}
+
+/* srslte_pss_generate (sync/pss.c:346-375) */
+void orc_pss_generate(uint32_t n_id_2, float* out)
+{
+  const float root_value[] = {25.0, 29.0, 34.0};
+  const int   sign         = -1;
+  cf*         sig          = (cf*)out;
+  for (int i = 0; i < 31; i++) {
+    const float arg = (float)sign * M_PI * root_value[n_id_2] * ((float)i * ((float)i + 1.0)) / 63.0;
+    sig[i]          = cmk(cosf(arg), sinf(arg));
+  }
+  for (int i = 31; i < 62; i++) {
+    const float arg = (float)sign * M_PI * root_value[n_id_2] * (((float)i + 2.0) * ((float)i + 1.0)) / 63.0;
+    sig[i]          = cmk(cosf(arg), sinf(arg));
+  }
+}
+
+/* estimate_noise_pss (chest_dl.c:399-416): grid / ce of one (rx, port) */
+float orc_noise_pss(const float* grid_f, const float* ce_f, uint32_t nof_prb, int cp_ext, uint32_t cell_id,
+                    uint32_t nof_ports)
+{
+  const cf* in = (const cf*)grid_f;
+  const cf* ce = (const cf*)ce_f;
+  cf        pss[62];
+  orc_pss_generate(cell_id % 3, (float*)pss);
+  const int nre = 12 * (int)nof_prb, k = ((cp_ext ? 6 : 7) - 1) * nre + nre / 2 - 31;
+  float     s   = 0;
+  for (int n = 0; n < 62; n++) {
+    const cf c = ce[k + n], p = pss[n], y = in[k + n];
+    const cf t = cmk(c.re * p.re - c.im * p.im - y.re, c.re * p.im + c.im * p.re - y.im);
+    s += cpw(t);
+  }
+  return (float)(nof_ports * (s / 62.0f) * M_SQRT1_2);
 }

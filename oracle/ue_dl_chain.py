@@ -133,6 +133,63 @@ def chest_estimate(grids: np.ndarray, nof_prb: int, nof_ports: int, cell_id: int
     return ce, fill_res(vals, nof_prb)
 
 
+class ChestState:
+    """The values srslte_chest_dl_t carries from one subframe to the next (chest_dl.c: q->cfo, q->noise_estimate,
+    q->sync_err), zero after srslte_chest_dl_init."""
+
+    def __init__(self, nof_rx: int, nof_ports: int):
+        self.cfo = np.float32(0)
+        self.noise = np.zeros((nof_rx, nof_ports), np.float32)
+        self.sync = np.zeros((nof_rx, nof_ports), np.float32)
+
+
+def chest_estimate_st(grids: np.ndarray, nof_prb: int, nof_ports: int, cell_id: int, tti: int, state: ChestState,
+                      filter_type: int = 0, coef=(4.0, 1.0), alg: int = 0, noise_alg: int = 0, cfo_enable=False,
+                      cfo_mask: int = 0, sync_enable=False, cp_ext: bool = False, std: bool = False):
+    """srslte_chest_dl_estimate_cfg (chest_dl.c:985-1014) with the estimator's state, advanced by one subframe:
+    per rx antenna the sync-error correction of the grid (:731-786, when enabled), then per port estimate_port
+    (:788-816) -> chest_interpolate_noise_est (:621-728): the CFO (:596-618) where the mask selects the subframe,
+    REFS noise before / PSS or EMPTY noise (subframes 0 and 5 only) after the interpolation.
+    Returns (corrected grids, ce, res) -- res as chest_estimate's plus "cfo" and "sync_error"."""
+    L = lib()
+    R = grids.shape[0]
+    G = grids.shape[1]
+    sf = tti % 10
+    N = symbol_sz(nof_prb, std)
+    f32 = np.float32
+    grids = np.array(grids, np.complex64)
+    ce = np.zeros((nof_ports, R, G), np.complex64)
+    vals = np.zeros((R, nof_ports, 3), np.float32)
+    for a in range(R):
+        g = grids[a]
+        if sync_enable:
+            se = np.zeros(nof_ports, np.float32)
+            L.orc_chest_sync_correct(g.view(f32), nof_prb, cell_id, int(cp_ext), sf, nof_ports, N, se)
+            state.sync[a, :] = se
+        for p in range(nof_ports):
+            out = np.zeros(G, np.complex64)
+            o3 = np.zeros(3, np.float32)
+            r = L.orc_chest_estimate_port_st(g.view(f32), nof_prb, cell_id, int(cp_ext), sf, p, filter_type,
+                                             float(coef[0]), float(coef[1]), alg, noise_alg, float(state.noise[a, p]),
+                                             out.view(f32), o3)
+            assert r == 0
+            if cfo_enable and (cfo_mask >> sf) & 1:
+                state.cfo = f32(L.orc_chest_cfo(g.view(f32), nof_prb, cell_id, int(cp_ext), sf, p, p if p < 2 else 1,
+                                                N))
+            if noise_alg == 0:
+                state.noise[a, p] = o3[0]
+            elif sf in (0, 5):
+                state.noise[a, p] = (L.orc_noise_pss(g.view(f32), out.view(f32), nof_prb, int(cp_ext), cell_id,
+                                                     nof_ports) if noise_alg == 1
+                                     else L.orc_noise_empty(g.view(f32), nof_prb, int(cp_ext)))
+            ce[p, a] = out
+            vals[a, p] = (state.noise[a, p], o3[1], o3[2])
+    res = fill_res(vals, nof_prb)
+    res["cfo"] = float(state.cfo)
+    res["sync_error"] = float(state.sync[0, 0])
+    return grids, ce, res
+
+
 def fill_res(vals: np.ndarray, nof_prb: int) -> dict:
     """fill_res (chest_dl.c:944-972) incl. get_rsrp's rx-count-indexed port loop (:897-905)."""
     R, P = vals.shape[:2]

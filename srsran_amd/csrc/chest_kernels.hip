@@ -8,6 +8,12 @@
 // reference's extrapolated edges), linearly interpolated onto the 12*nof_prb subcarriers and the row is
 // streamed to every OFDM symbol of ce (the AVERAGE estimator's time-invariant estimate).  HBM traffic per
 // (rx, port): the 4 pilot rows read (RSSI), 14 ce rows written.
+//
+// Around it: chest_pre (block per (subframe, rx)) estimates the synchronisation error from the pilots' phase slope
+// over every port and rotates the grid in place (chest_dl_estimate_correct_sync_error, :731-786) and takes the
+// EMPTY noise estimate (:419-430); chest_estimate also takes the PSS noise estimate (:399-416) and the CFO
+// (chest_estimate_cfo, :596-618); chest_resolve turns the per-subframe estimates into the noise estimate the
+// reference's state holds after each subframe (PSS / EMPTY only update it in subframes 0 and 5) and its get_noise.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -120,6 +126,57 @@ __device__ __forceinline__ void interp_rows(float2 in0, float2 in1, float2 start
 
 } // namespace
 
+// outputs of one (subframe, rx, port) block, the PSS noise estimate (estimate_noise_pss, chest_dl.c:399-416: ce and
+// the grid on the PSS subcarriers of the slot's last symbol, nof_ports * avg |ce * pss - y|^2 / sqrt(2)) and the
+// CFO (chest_estimate_cfo :596-618: the LS pilots of symbols 0, 1 against those of symbols 2, 3 -- the buffer the
+// reference reads holds the current port's first pilot symbols and, for ports 2 and 3, port 1's last two, which
+// the earlier port left there)
+__device__ void chest_tail(const ChestArgs& a, const ChestJob& J, const float2* pe, const float (&acc)[4], float noise,
+                           uint32_t np, uint32_t nsym, float* red)
+{
+  const uint32_t nprb = a.nof_prb, nre = 12 * nprb, nref = 2 * nprb;
+  const bool     sf05 = (J.flags & CHEST_F_NOISE_SF05) != 0;
+  if (a.noise_alg == 1 && sf05) {
+    __syncthreads(); // the ce rows this block wrote
+    float v[1] = {0.f};
+    if (threadIdx.x < 62) {
+      const uint32_t k = (a.nsymb - 1) * nre + nre / 2 - 31 + threadIdx.x;
+      const float2   c = J.ce[k], p = a.pss[threadIdx.x], y = J.grid[k];
+      const float2   t = make_float2(c.x * p.x - c.y * p.y - y.x, c.x * p.y + c.y * p.x - y.y);
+      v[0]             = cpw(t);
+    }
+    block_sum<1>(v, red);
+    if (threadIdx.x == 0) J.out[CHEST_O_NOISE] = (float)((double)((float)a.nof_ports * (v[0] / 62.0f)) * M_SQRT1_2);
+  }
+  if (J.flags & CHEST_F_CFO) {
+    float v[2] = {0.f, 0.f};
+    for (uint32_t t = threadIdx.x; t < 2 * nref; t += blockDim.x) {
+      const uint32_t l = t / nref, k = t % nref;
+      float2         late;
+      if (J.port < 2) {
+        late = pe[(l + 2) * nref + k];
+      } else { // port 1's LS estimate of pilot symbol l + 2
+        const uint32_t l2 = l + 2;
+        const float2   x  = J.grid[crs_nsymbol(l2, a.nsymb, 1) * nre + crs_fidx(a.cell_id, l2, 1) + 6 * k];
+        late              = cprod_conj(x, a.pilots[(size_t)J.sf * (4 * nref) + l2 * nref + k]);
+      }
+      const float2 z = cprod_conj(pe[l * nref + k], late);
+      v[0] += z.x;
+      v[1] += z.y;
+    }
+    block_sum<2>(v, red);
+    if (threadIdx.x == 0)
+      J.out[CHEST_O_CFO] = (float)((double)(-atan2f(v[1], v[0]) * a.cfo_n / (a.cfo_ns * (a.cfo_n + a.cfo_ng)) / 2) / M_PI);
+  }
+  if (threadIdx.x == 0) {
+    if (a.noise_alg == 0) J.out[CHEST_O_NOISE] = noise;
+    J.out[CHEST_O_RSRP]  = acc[0] / (float)np;
+    J.out[CHEST_O_RSSI]  = acc[1] / (float)nsym;
+    J.out[CHEST_O_PE_RE] = acc[2];
+    J.out[CHEST_O_PE_IM] = acc[3];
+  }
+}
+
 __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
 {
   __shared__ float2 pe[4 * 2 * MAXPRB];
@@ -157,7 +214,7 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
   // 2. REFS noise (estimate_noise_pilots :320-397): only the last pilot symbol's residual power survives
   //    the reference's loop, divided by the symbol count and scaled by sqrt(5)
   float nz[1] = {0.f};
-  {
+  if (a.noise_alg == 0) {
     const uint32_t fidx0 = crs_fidx(a.cell_id, 0, port);
     const uint32_t off   = ((fidx0 < 3) ^ (nsym & 1)) ? 0 : 1;
     const float2*  cen   = &pe[(nsym - 1) * nref];
@@ -188,13 +245,16 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
     block_sum<1>(nz, red);
   }
   const float noise = nz[0] / (float)nref / (float)nsym * sqrtf(5.0f);
+  // the Gauss filter's automatic sigma reads the state's noise estimate: REFS has just updated it (:640-645), PSS
+  // and EMPTY update it only after the interpolation (:714-725), so it is the previous subframe-0/5 estimate
+  const float fnoise = a.noise_alg == 0 ? noise : (J.src >= 0 ? a.out_all[J.src + CHEST_O_NOISE] : J.noise_prev);
 
   // 3. smoothing filter (chest_common.c:42-88)
   if (threadIdx.x == 0) {
     uint32_t flen = 0;
     if (a.filter_type == 0) {
       const uint32_t order = a.coef0 <= 0 ? 4u : (uint32_t)a.coef0;
-      const float    sd    = a.coef0 <= 0 ? noise * 200.0f : a.coef1;
+      const float    sd    = a.coef0 <= 0 ? fnoise * 200.0f : a.coef1;
       flen                 = min(order + 1, 15u);
       const int c          = (int)(flen - 1) / 2;
       float     nrm        = 0.f;
@@ -254,13 +314,7 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
         interp_rows(P[2], P[3], P[3], 3, 2, o, 10, nre);
       }
     }
-    if (threadIdx.x == 0) {
-      J.out[0] = noise;
-      J.out[1] = acc[0] / (float)np;
-      J.out[2] = acc[1] / (float)nsym;
-      J.out[3] = acc[2];
-      J.out[4] = acc[3];
-    }
+    chest_tail(a, J, pe, acc, noise, np, nsym, red);
     return;
   }
 
@@ -330,33 +384,156 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
   __syncthreads();
   const uint32_t nrows = 2 * a.nsymb;
   for (uint32_t k = threadIdx.x; k < nrows * nre; k += blockDim.x) J.ce[k] = row[k % nre];
-  if (threadIdx.x == 0) {
-    J.out[0] = noise;
-    J.out[1] = acc[0] / (float)np;
-    J.out[2] = acc[1] / (float)nsym;
-    J.out[3] = acc[2];
-    J.out[4] = acc[3];
+  chest_tail(a, J, pe, acc, noise, np, nsym, red);
+}
+
+// chest_dl_estimate_correct_sync_error (chest_dl.c:731-786) and estimate_noise_empty_sc (:419-430) for one
+// (subframe, rx): per port the LS pilots' phase slope over each pilot symbol (srslte_vec_estimate_frequency, in
+// samples: * symbol_sz / 6) averaged over the symbols, the ports combined weighted by their pilot power, and when
+// |error| > 0.05 samples every OFDM symbol of the grid rotated by exp(j 2 pi k error / symbol_sz) in place; then the
+// EMPTY estimate (the 5 empty subcarriers either side of the SSS and the PSS) from the corrected grid.
+__global__ __launch_bounds__(256) void chest_pre(ChestArgs a, uint32_t do_sync, uint32_t do_empty)
+{
+  constexpr int NA = 36; // per port: 4 symbols' slope sums (re, im) + pilot power -> 4 * 9
+  __shared__ float red[4 * NA];
+  __shared__ float cfo_s;
+  const uint32_t   P = a.nof_ports, R = a.nof_rx;
+  const uint32_t   job = blockIdx.x / R, rx = blockIdx.x % R;
+  const ChestJob&  J0  = a.jobs[((size_t)job * R + rx) * P];
+  float2*          g   = J0.grid;
+  const uint32_t   nprb = a.nof_prb, nre = 12 * nprb, nref = 2 * nprb;
+  if (do_sync) {
+    float acc[NA];
+#pragma unroll
+    for (int k = 0; k < NA; k++) acc[k] = 0.f;
+    // item = (port, pilot symbol, pilot index)
+    const uint32_t per_port[4] = {4 * nref, 4 * nref, 2 * nref, 2 * nref};
+#pragma unroll
+    for (uint32_t p = 0; p < 4; p++) { // unrolled: acc[] indices are compile-time constants
+      if (p >= P) break;
+      const float2*  crs  = a.pilots + (size_t)((p / 2) * 10 + J0.sf) * (4 * nref);
+      for (uint32_t t = threadIdx.x; t < per_port[p]; t += blockDim.x) {
+        const uint32_t l = t / nref, i = t % nref;
+        const uint32_t base = crs_nsymbol(l, a.nsymb, p) * nre + crs_fidx(a.cell_id, l, p);
+        const float2   e    = cprod_conj(g[base + 6 * i], crs[l * nref + i]);
+        float2         sre  = make_float2(0.f, 0.f);
+        if (i > 0) { // x[i] * conj(x[i-1])
+          const float2 e1 = cprod_conj(g[base + 6 * (i - 1)], crs[l * nref + i - 1]);
+          sre             = cprod_conj(e, e1);
+        }
+        // register-indexed accumulation: unrolled selects keep acc[] in VGPRs
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+          if (q == l) {
+            acc[p * 9 + 2 * q] += sre.x;
+            acc[p * 9 + 2 * q + 1] += sre.y;
+          }
+        }
+        acc[p * 9 + 8] += cpw(e);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NA; k++) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) acc[k] += __shfl_xor(acc[k], o, 64);
+    }
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < NA; k++) red[w * NA + k] = acc[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float tot[NA];
+      for (int k = 0; k < NA; k++) tot[k] = red[k] + red[NA + k] + red[2 * NA + k] + red[3 * NA + k];
+      float pwr_sum = 0.f, sync_err = 0.f;
+      for (uint32_t p = 0; p < P; p++) {
+        const uint32_t nsym = p < 2 ? 4 : 2;
+        float          sum  = 0.f;
+        for (uint32_t l = 0; l < nsym; l++) {
+          const float f = (float)((double)-atan2f(tot[p * 9 + 2 * l + 1], tot[p * 9 + 2 * l]) * M_1_PI * 0.5f);
+          sum += f * a.sync_k;
+        }
+        const float pwr = tot[p * 9 + 8] / (float)(nsym * nref);
+        const float se  = sum / (float)nsym;
+        a.jobs[((size_t)job * R + rx) * P + p].out[CHEST_O_SYNC] = se;
+        if (!isinf(sum) && !isnan(sum) && !isinf(pwr) && !isnan(pwr)) {
+          sync_err += se * pwr;
+          pwr_sum += pwr;
+        }
+      }
+      if (isnormal(pwr_sum)) sync_err /= pwr_sum;
+      cfo_s = (isnormal(sync_err) && fabsf(sync_err) > 0.05f) ? sync_err / (float)a.symbol_sz : 0.f;
+    }
+    __syncthreads();
+    const float cfo = cfo_s;
+    if (cfo != 0.f) { // srslte_vec_apply_cfo on every OFDM symbol (phase restarts at each symbol)
+      const uint32_t nrows = 2 * a.nsymb;
+      for (uint32_t t = threadIdx.x; t < nrows * nre; t += blockDim.x) {
+        const uint32_t k = t % nre;
+        float          sn, cs;
+        sincosf(2.0f * (float)M_PI * cfo * (float)k, &sn, &cs);
+        const float2 x = g[t];
+        g[t]           = make_float2(x.x * cs - x.y * sn, x.x * sn + x.y * cs);
+      }
+      __syncthreads();
+    }
+  }
+  if (do_empty && (J0.flags & CHEST_F_NOISE_SF05)) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (threadIdx.x < 20) {
+      const int k_sss = (int)((a.nsymb - 2) * nre + nre / 2) - 31, k_pss = (int)((a.nsymb - 1) * nre + nre / 2) - 31;
+      const int grp = threadIdx.x / 5, j = threadIdx.x % 5;
+      const int k   = grp == 0 ? k_sss - 5 : grp == 1 ? k_sss + 62 : grp == 2 ? k_pss - 5 : k_pss + 62;
+      v[grp]        = cpw(g[k + j]);
+    }
+    block_sum<4>(v, red);
+    if (threadIdx.x == 0) {
+      float np = 0.f;
+      np += v[0] / 5.0f;
+      np += v[1] / 5.0f;
+      np += v[2] / 5.0f;
+      np += v[3] / 5.0f;
+      for (uint32_t p = 0; p < P; p++) a.jobs[((size_t)job * R + rx) * P + p].out[CHEST_O_NOISE] = np;
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void chest_noise(const float* out, uint32_t R, uint32_t P, uint32_t njobs,
-                                                   float* noise)
+// thread per job: the noise estimate the reference's state holds after the subframe, and get_noise (:847-857)
+__global__ __launch_bounds__(256) void chest_resolve(ChestArgs a, uint32_t njobs, float* noise)
 {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= njobs) return;
-  float n = 0.f;
-  for (uint32_t a = 0; a < R; a++) {
+  const uint32_t R = a.nof_rx, P = a.nof_ports;
+  float          n = 0.f;
+  for (uint32_t r = 0; r < R; r++) {
     float acc = 0.f;
-    for (uint32_t p = 0; p < P; p++) acc += out[(((size_t)i * R + a) * P + p) * 5];
+    for (uint32_t p = 0; p < P; p++) {
+      const ChestJob& J = a.jobs[((size_t)i * R + r) * P + p];
+      float           nf;
+      if (a.noise_alg == 0 || (J.flags & CHEST_F_NOISE_SF05))
+        nf = J.out[CHEST_O_NOISE];
+      else
+        nf = J.src >= 0 ? a.out_all[J.src + CHEST_O_NOISE] : J.noise_prev;
+      J.out[CHEST_O_NF] = nf;
+      acc += nf;
+    }
     n += acc / (float)P;
   }
-  noise[i] = n / (float)R;
+  if (noise) noise[i] = n / (float)R;
 }
 
-hipError_t chest_launch_noise(const float* out, uint32_t R, uint32_t P, uint32_t njobs, float* noise, hipStream_t s)
+hipError_t chest_launch_pre(const ChestArgs& a, uint32_t njobs, bool sync, bool empty, hipStream_t s)
+{
+  if (!njobs || (!sync && !empty)) return hipSuccess;
+  hipLaunchKernelGGL(chest_pre, dim3(njobs * a.nof_rx), dim3(256), 0, s, a, (uint32_t)sync, (uint32_t)empty);
+  return hipGetLastError();
+}
+
+hipError_t chest_launch_resolve(const ChestArgs& a, uint32_t njobs, float* noise, hipStream_t s)
 {
   if (!njobs) return hipSuccess;
-  hipLaunchKernelGGL(chest_noise, dim3((njobs + 255) / 256), dim3(256), 0, s, out, R, P, njobs, noise);
+  hipLaunchKernelGGL(chest_resolve, dim3((njobs + 255) / 256), dim3(256), 0, s, a, njobs, noise);
   return hipGetLastError();
 }
 

@@ -1,11 +1,14 @@
 // srsran_amd/csrc/host_parallel.h -- a small persistent host thread pool for the per-subframe host work of a batch
 // call (blind-search replay, DCI unpacking, grants): independent per subframe, so a batch of 2,048 splits into
 // contiguous chunks.  MI355_HOST_THREADS sets the pool size (default min(8, hardware threads / 2); 1 = serial).
-// A caller that finds the pool busy (another object's call in another thread) runs its loop serially.
+// A caller that finds the pool busy (another object's call in another thread) runs its loop serially.  An exception
+// thrown by fn in any part is caught there, every part still completes (so fn stays alive until no worker can call
+// it), and the first one is rethrown to the caller.
 #pragma once
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <stdint.h>
@@ -52,6 +55,12 @@ public:
       run_part(k);
     }
     while (left_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    std::exception_ptr err;
+    {
+      std::lock_guard<std::mutex> lk(err_m_);
+      err.swap(err_);
+    }
+    if (err) std::rethrow_exception(err);
   }
 
   ~HostPool()
@@ -68,10 +77,12 @@ private:
   HostPool()
   {
     uint32_t T = 0;
+    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
     if (const char* e = getenv("MI355_HOST_THREADS")) {
-      T = (uint32_t)atoi(e);
+      const long v = strtol(e, nullptr, 10); // clamped to [1, hardware threads]
+      T            = (uint32_t)std::min<long>(std::max<long>(v, 1), (long)hw);
     } else {
-      T = std::min(8u, std::max(1u, std::thread::hardware_concurrency() / 2));
+      T = std::min(8u, std::max(1u, hw / 2));
     }
     for (uint32_t i = 1; i < T; i++) workers_.emplace_back([this] { loop(); });
   }
@@ -79,7 +90,14 @@ private:
   void run_part(uint32_t k)
   {
     const uint32_t b = (uint32_t)((uint64_t)n_ * k / parts_), e = (uint32_t)((uint64_t)n_ * (k + 1) / parts_);
-    if (b < e) (*fn_)(b, e);
+    if (b < e) {
+      try {
+        (*fn_)(b, e);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(err_m_);
+        if (!err_) err_ = std::current_exception();
+      }
+    }
     left_.fetch_sub(1, std::memory_order_acq_rel);
   }
 
@@ -104,7 +122,8 @@ private:
   }
 
   std::vector<std::thread>                         workers_;
-  std::mutex                                       m_, use_;
+  std::mutex                                       m_, use_, err_m_;
+  std::exception_ptr                               err_;
   std::condition_variable                          cv_;
   const std::function<void(uint32_t, uint32_t)>*  fn_ = nullptr;
   uint32_t                                         n_ = 0, parts_ = 0;

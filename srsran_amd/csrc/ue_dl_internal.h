@@ -53,26 +53,53 @@ struct OfdmArgs {
   uint32_t       radix[OFDM_MAX_STAGES];
 };
 
-struct ChestJob {
-  const float2* grid; // sf_symbols of one rx antenna
-  float2*       ce;   // ce[port][rx]
-  float*        out;  // [5]: noise, rsrp, rssi, sum(pe).re, sum(pe).im
-  uint32_t      sf, port;
+// per (job, rx, port) estimator outputs, CHEST_OUT floats each
+enum : uint32_t {
+  CHEST_O_NOISE = 0, // this subframe's own noise estimate (REFS always; EMPTY / PSS in subframes 0 and 5)
+  CHEST_O_RSRP,
+  CHEST_O_RSSI,
+  CHEST_O_PE_RE, // sum of the LS pilot estimates (rsrp_neighbour)
+  CHEST_O_PE_IM,
+  CHEST_O_SYNC, // sync_err[rx][port] (chest_dl_estimate_correct_sync_error)
+  CHEST_O_CFO,  // chest_estimate_cfo (written by the job's last (rx, port) block when the job asks for it)
+  CHEST_O_NF,   // the noise estimate the reference's state holds after this subframe (chest_resolve)
+  CHEST_OUT
 };
+
+struct ChestJob {
+  float2*  grid;       // sf_symbols of one rx antenna (corrected in place by the sync-error stage)
+  float2*  ce;         // ce[port][rx]
+  float*   out;        // [CHEST_OUT]
+  uint32_t sf, port;
+  uint32_t flags;      // CHEST_F_*
+  int32_t  src;        // EMPTY / PSS: batch-relative job whose subframe-0/5 estimate is the state before this one (-1: prev)
+  float    noise_prev; // the link's noise_estimate[rx][port] before this batch
+};
+enum : uint32_t { CHEST_F_CFO = 1, CHEST_F_NOISE_SF05 = 2 };
 
 struct ChestArgs {
   const ChestJob* jobs;
   const float2*   pilots; // [pair][sf][4 * 2 * nof_prb]
-  uint32_t        nof_prb, cell_id, nsymb, filter_type;
+  const float2*   pss;    // srslte_pss_generate(cell.id % 3), 62 values
+  const float*    out_all; // out of job 0 (stride R * P * CHEST_OUT per job)
+  uint32_t        nof_prb, cell_id, nsymb, filter_type, nof_ports, nof_rx;
   float           coef0, coef1;
-  uint32_t        alg; // srslte_chest_dl_estimator_alg_t: 0 AVERAGE, 1 INTERPOLATE
+  uint32_t        alg;       // srslte_chest_dl_estimator_alg_t: 0 AVERAGE, 1 INTERPOLATE
+  uint32_t        noise_alg; // srslte_chest_dl_noise_alg_t: 0 REFS, 1 PSS, 2 EMPTY
+  float           cfo_n, cfo_ns, cfo_ng; // chest_estimate_cfo's n, ns, ng
+  float           sync_k;               // srslte_symbol_sz / 6 (chest_dl_estimate_correct_sync_error)
+  uint32_t        symbol_sz;
 };
 
 hipError_t ofdm_launch_rx(const OfdmArgs& a, uint32_t njobs, hipStream_t s);
 // srslte_ofdm_tx_sf + the srslte_enb_dl_gen_signal scale; jobs: in = grid, out = time-domain subframe
 hipError_t ofdm_launch_tx(const OfdmArgs& a, float scale, uint32_t njobs, hipStream_t s);
 hipError_t chest_launch(const ChestArgs& a, uint32_t njobs, hipStream_t s);
-// get_noise (chest_dl.c:847-857) per job from the [job][rx][port][5] estimator outputs
-hipError_t chest_launch_noise(const float* out, uint32_t R, uint32_t P, uint32_t njobs, float* noise, hipStream_t s);
+// chest_dl_estimate_correct_sync_error (chest_dl.c:731-786) and the EMPTY noise estimate (:419-430), one block per
+// (job, rx); a.jobs holds the (job, rx, port) entries as chest_launch does
+hipError_t chest_launch_pre(const ChestArgs& a, uint32_t njobs, bool sync, bool empty, hipStream_t s);
+// the noise estimate each job leaves in the estimator's state (CHEST_O_NF) and get_noise (chest_dl.c:847-857) per
+// job for the equaliser (noise may be null)
+hipError_t chest_launch_resolve(const ChestArgs& a, uint32_t njobs, float* noise, hipStream_t s);
 
 } // namespace mi355

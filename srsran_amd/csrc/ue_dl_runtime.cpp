@@ -39,6 +39,13 @@ float to_dbm(float v) { return to_db(v) + 30.0f; }
 
 } // namespace
 
+// the values srslte_chest_dl_t carries from one subframe to the next (chest_dl.c: q->cfo, q->noise_estimate,
+// q->sync_err)
+struct ChestLink {
+  float cfo = 0.f, sync = 0.f;
+  float noise[MI355_MAX_RX_ANT][MI355_MAX_PORTS] = {};
+};
+
 struct mi355_ue_dl {
   int            device = 0;
   mi355_cell_t   cell{};
@@ -48,7 +55,9 @@ struct mi355_ue_dl {
   OfdmArgs       ofdm{};
   float2*        tw     = nullptr;
   float2*        pilots = nullptr;
+  float2*        pss    = nullptr; // srslte_pss_generate(cell.id % 3)
   mi355_pdsch_t* pdsch  = nullptr;
+  std::vector<ChestLink> links;
   char*          scratch = nullptr;
   size_t         scratch_cap = 0;
   HostStaging    st_ofdm, st_chest, back; // pinned descriptor uploads / estimator read-back
@@ -131,24 +140,33 @@ static int ofdm_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t nj
   return MI355_SUCCESS;
 }
 
-// fill_res (chest_dl.c:944-972) from per (rx, port) noise / rsrp / rssi / sum(pe)
-static void fill_res(const mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const float* v, mi355_chest_dl_res_t* res)
+// fill_res (chest_dl.c:944-972) for one job from its per (rx, port) outputs v[(rx * P + port) * CHEST_OUT], then the
+// link's state moves on to this subframe (jobs are filled in batch order)
+static void fill_res(mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const float* v, const mi355_dl_sf_job_t& job,
+                     mi355_chest_dl_res_t* res)
 {
   const uint32_t P = q->cell.nof_ports, R = q->nof_rx, nprb = q->cell.nof_prb;
+  ChestLink&     L = q->links[job.link];
   float          noise[4][4] = {}, rsrp[4][4] = {}, rssi[4][4] = {}, rsrp_corr[4][4] = {};
   const uint32_t npil[4] = {8 * nprb, 8 * nprb, 4 * nprb, 4 * nprb};
   for (uint32_t a = 0; a < R; a++) {
     for (uint32_t p = 0; p < P; p++) {
-      const float* o = &v[(a * P + p) * 5];
-      noise[a][p]    = o[0];
-      rsrp[a][p]     = o[1];
-      rssi[a][p]     = o[2];
+      const float* o = &v[(a * P + p) * CHEST_OUT];
+      noise[a][p]    = o[CHEST_O_NF];
+      rsrp[a][p]     = o[CHEST_O_RSRP];
+      rssi[a][p]     = o[CHEST_O_RSSI];
+      L.noise[a][p]  = noise[a][p];
       if (cfg->rsrp_neighbour) { // estimate_port :797-800
-        const double e  = std::sqrt((double)(o[3] / npil[p]) * (o[3] / npil[p]) + (double)(o[4] / npil[p]) * (o[4] / npil[p]));
+        const float re = o[CHEST_O_PE_RE], im = o[CHEST_O_PE_IM];
+        const double e  = std::sqrt((double)(re / npil[p]) * (re / npil[p]) + (double)(im / npil[p]) * (im / npil[p]));
         rsrp_corr[a][p] = (float)(e * e);
       }
     }
   }
+  const uint32_t sf = job.tti % 10;
+  if (cfg->cfo_estimate_enable && ((1u << sf) & cfg->cfo_estimate_sf_mask)) // :635-637
+    L.cfo = v[((R - 1) * P + (P - 1)) * CHEST_OUT + CHEST_O_CFO];
+  if (cfg->sync_error_enable) L.sync = v[CHEST_O_SYNC]; // sync_err[0][0]
   memset(res, 0, sizeof(*res));
   res->nof_re = 2 * (q->cell.cp == MI355_CP_EXT ? 6 : 7) * 12 * nprb;
   // get_noise
@@ -182,7 +200,7 @@ static void fill_res(const mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, co
   ri /= R;
   res->noise_estimate     = n;
   res->noise_estimate_dbm = to_dbm(n);
-  res->cfo                = 0.f;
+  res->cfo                = L.cfo;
   res->rsrp               = rs;
   res->rsrp_dbm           = to_dbm(rs);
   res->rsrp_neigh         = neigh;
@@ -190,7 +208,7 @@ static void fill_res(const mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, co
   res->rsrq_db            = to_db(rq);
   res->snr_db             = to_db(rs / n);
   res->rssi_dbm           = to_dbm(ri);
-  res->sync_error         = 0.f;
+  res->sync_error         = L.sync;
   for (uint32_t p = 0; p < P; p++) {
     res->rsrp_port_dbm[p] = to_dbm(rsrp_port(p));
     for (uint32_t a = 0; a < R; a++) {
@@ -204,16 +222,16 @@ static void fill_res(const mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, co
 static int chest_check_cfg(const mi355_chest_dl_cfg_t* cfg)
 {
   if (!cfg) return MI355_ERROR_INVALID_INPUTS;
-  // supported: AVERAGE estimator, REFS noise, no CFO / sync-error correction (the srsUE and phy_dl_test setup)
+  // the Wiener estimator (wiener_dl.c) is not supported
   if ((cfg->estimator_alg != MI355_ESTIMATOR_ALG_AVERAGE && cfg->estimator_alg != MI355_ESTIMATOR_ALG_INTERPOLATE) ||
-      cfg->noise_alg != MI355_NOISE_ALG_REFS ||
-      cfg->cfo_estimate_enable || cfg->sync_error_enable || cfg->filter_type > MI355_CHEST_FILTER_NONE)
+      cfg->noise_alg > MI355_NOISE_ALG_EMPTY || cfg->filter_type > MI355_CHEST_FILTER_NONE)
     return MI355_ERROR;
   return MI355_SUCCESS;
 }
 
-// launches the estimator (and, when d_noise is wanted, the per-job noise average of get_noise) without
-// synchronising; the scratch region starts after `offset` bytes (the OFDM job table may live before it)
+// launches the estimator (sync-error stage, estimation, noise resolution and, when d_noise is wanted, the per-job
+// get_noise) without synchronising; the scratch region starts after `offset` bytes (the OFDM job table may live
+// before it)
 static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs,
                              const mi355_chest_dl_cfg_t* cfg, hipStream_t s, size_t offset, float** d_out_p,
                              float** d_noise_p)
@@ -222,54 +240,101 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
   if (r) return r;
   const uint32_t P = q->cell.nof_ports, R = q->nof_rx;
   const size_t   ncj = (size_t)njobs * P * R;
+  uint32_t       maxl = 0;
+  for (uint32_t i = 0; i < njobs; i++) {
+    if (jobs[i].link >= MI355_MAX_LINKS) return MI355_ERROR_INVALID_INPUTS;
+    maxl = std::max(maxl, jobs[i].link);
+  }
+  if (njobs && q->links.size() <= maxl) q->links.resize((size_t)maxl + 1);
   CHECK_HIP(q->st_chest.reserve(ncj * sizeof(ChestJob)));
-  auto*  cj = (ChestJob*)q->st_chest.slot(ncj * sizeof(ChestJob));
-  size_t k  = 0;
-  const size_t nout = (size_t)njobs * P * R * 5;
+  auto*        cj   = (ChestJob*)q->st_chest.slot(ncj * sizeof(ChestJob));
+  const size_t nout = ncj * CHEST_OUT;
   char*        base = nullptr;
-  const size_t jb   = ((size_t)njobs * P * R * sizeof(ChestJob) + 255) / 256 * 256;
+  const size_t jb   = (ncj * sizeof(ChestJob) + 255) / 256 * 256;
   const size_t ob   = (nout * 4 + 255) / 256 * 256;
   if ((r = get_scratch(q, offset + jb + ob + (size_t)njobs * 4 + 256, &base))) return r;
   base += offset;
-  float* d_out   = (float*)(base + jb);
-  float* d_noise = (float*)(base + jb + ob);
+  float*     d_out   = (float*)(base + jb);
+  float*     d_noise = (float*)(base + jb + ob);
+  const bool sf05_alg = cfg->noise_alg != MI355_NOISE_ALG_REFS; // PSS / EMPTY: state updated in subframes 0 and 5
+  std::vector<int32_t> last05(sf05_alg ? (size_t)maxl + 1 : 0, -1);
+  size_t               k = 0;
   for (uint32_t i = 0; i < njobs; i++) {
+    const uint32_t sf   = jobs[i].tti % 10;
+    const bool     is05 = sf05_alg && (sf == 0 || sf == 5);
+    const bool     cfo  = cfg->cfo_estimate_enable && ((1u << sf) & cfg->cfo_estimate_sf_mask);
+    const ChestLink& L  = q->links[jobs[i].link];
+    const int32_t  src  = sf05_alg ? last05[jobs[i].link] : -1;
     for (uint32_t a = 0; a < R; a++) {
       for (uint32_t p = 0; p < P; p++) {
         if (!jobs[i].sf_symbols[a] || !jobs[i].ce[p][a]) return MI355_ERROR_INVALID_INPUTS;
-        cj[k++] = ChestJob{(const float2*)jobs[i].sf_symbols[a], (float2*)jobs[i].ce[p][a],
-                           d_out + ((size_t)i * R * P + a * P + p) * 5, jobs[i].tti % 10, p};
+        ChestJob& J  = cj[k++];
+        J.grid       = (float2*)jobs[i].sf_symbols[a];
+        J.ce         = (float2*)jobs[i].ce[p][a];
+        J.out        = d_out + (((size_t)i * R + a) * P + p) * CHEST_OUT;
+        J.sf         = sf;
+        J.port       = p;
+        J.flags      = (is05 ? CHEST_F_NOISE_SF05 : 0u) | (cfo && a == R - 1 && p == P - 1 ? CHEST_F_CFO : 0u);
+        J.src        = src >= 0 ? (int32_t)((((size_t)src * R + a) * P + p) * CHEST_OUT) : -1;
+        J.noise_prev = L.noise[a][p];
       }
     }
+    if (is05) last05[jobs[i].link] = (int32_t)i;
   }
   CHECK_HIP(q->st_chest.upload(base, s));
   ChestArgs ca{};
   ca.jobs        = (const ChestJob*)base;
   ca.pilots      = q->pilots;
+  ca.pss         = q->pss;
+  ca.out_all     = d_out;
   ca.nof_prb     = q->cell.nof_prb;
   ca.cell_id     = q->cell.id;
   ca.nsymb       = q->cell.cp == MI355_CP_EXT ? 6 : 7;
+  ca.nof_ports   = P;
+  ca.nof_rx      = R;
   ca.filter_type = cfg->filter_type;
   ca.alg         = cfg->estimator_alg;
+  ca.noise_alg   = cfg->noise_alg;
   ca.coef0       = cfg->filter_coef[0];
   ca.coef1       = cfg->filter_coef[1];
-  CHECK_HIP(chest_launch(ca, (uint32_t)ncj, s));
-  if (d_noise_p) CHECK_HIP(chest_launch_noise(d_out, R, P, njobs, d_noise, s));
+  ca.symbol_sz   = q->ofdm.N;
+  ca.cfo_n       = (float)q->ofdm.N;
+  ca.cfo_ns      = (float)ca.nsymb;
+  ca.cfo_ng      = (float)cp_len(q->ofdm.N, 144); // SRSLTE_CP_LEN_NORM(1, n)
+  ca.sync_k      = (float)q->ofdm.N / 6.0f;
+  CHECK_HIP(chest_launch_pre(ca, njobs, cfg->sync_error_enable != 0, cfg->noise_alg == MI355_NOISE_ALG_EMPTY, s));
+  if (cfg->noise_alg == MI355_NOISE_ALG_PSS && cfg->filter_type == MI355_CHEST_FILTER_GAUSS && cfg->filter_coef[0] <= 0) {
+    // the automatic Gauss sigma of a subframe reads the PSS estimate of the link's previous subframe 0/5, which
+    // itself comes after that subframe's interpolation: launch up to and including each subframe 0/5 in turn
+    uint32_t b = 0;
+    for (uint32_t i = 0; i < njobs; i++) {
+      const uint32_t sf = jobs[i].tti % 10;
+      if (sf == 0 || sf == 5 || i + 1 == njobs) {
+        ChestArgs cs = ca;
+        cs.jobs      = ca.jobs + (size_t)b * R * P;
+        CHECK_HIP(chest_launch(cs, (i + 1 - b) * R * P, s));
+        b = i + 1;
+      }
+    }
+  } else {
+    CHECK_HIP(chest_launch(ca, (uint32_t)ncj, s));
+  }
+  CHECK_HIP(chest_launch_resolve(ca, njobs, d_noise_p ? d_noise : nullptr, s));
   *d_out_p = d_out;
   if (d_noise_p) *d_noise_p = d_noise;
   return MI355_SUCCESS;
 }
 
-static int chest_finish(mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const float* d_out, uint32_t njobs,
-                        mi355_chest_dl_res_t* res, hipStream_t s)
+static int chest_finish(mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const float* d_out,
+                        const mi355_dl_sf_job_t* jobs, uint32_t njobs, mi355_chest_dl_res_t* res, hipStream_t s)
 {
   const uint32_t     P = q->cell.nof_ports, R = q->nof_rx;
-  const size_t       nout = (size_t)njobs * P * R * 5;
+  const size_t       nout = (size_t)njobs * P * R * CHEST_OUT;
   CHECK_HIP(q->back.reserve(nout * 4));
   const float* out = (const float*)q->back.host;
   CHECK_HIP(hipMemcpyAsync(q->back.host, d_out, nout * 4, hipMemcpyDeviceToHost, s));
   CHECK_HIP(hipStreamSynchronize(s));
-  for (uint32_t i = 0; i < njobs; i++) fill_res(q, cfg, &out[(size_t)i * R * P * 5], &res[i]);
+  for (uint32_t i = 0; i < njobs; i++) fill_res(q, cfg, &out[(size_t)i * R * P * CHEST_OUT], jobs[i], &res[i]);
   return MI355_SUCCESS;
 }
 
@@ -277,9 +342,10 @@ static int chest_finish(mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const
 // finished, and fill_res runs on the calling thread as the DL-SCH's wait hook (after every decode kernel is
 // enqueued, before the final wait).
 struct ChestFill {
-  const mi355_ue_dl_t*        q;
+  mi355_ue_dl_t*              q;
   const mi355_chest_dl_cfg_t* cfg;
   const float*                out;
+  const mi355_dl_sf_job_t*    jobs;
   uint32_t                    njobs;
   mi355_chest_dl_res_t*       res;
   bool                        done;
@@ -287,18 +353,18 @@ struct ChestFill {
 
 static void chest_fill_cb(void* p)
 {
-  const ChestFill* f = (const ChestFill*)p;
-  if (hipStreamSynchronize(f->q->side) != hipSuccess) return; // the read-back has landed
-  const uint32_t   k = f->q->cell.nof_ports * f->q->nof_rx * 5;
-  for (uint32_t i = 0; i < f->njobs; i++) fill_res(f->q, f->cfg, &f->out[(size_t)i * k], &f->res[i]);
-  ((ChestFill*)p)->done = true;
+  ChestFill* f = (ChestFill*)p;
+  if (f->done || hipStreamSynchronize(f->q->side) != hipSuccess) return; // the read-back has landed
+  const uint32_t k = f->q->cell.nof_ports * f->q->nof_rx * CHEST_OUT;
+  for (uint32_t i = 0; i < f->njobs; i++) fill_res(f->q, f->cfg, &f->out[(size_t)i * k], f->jobs[i], &f->res[i]);
+  f->done = true;
 }
 
 static int chest_finish_async(mi355_ue_dl_t* q, ChestFill* f, const float* d_out, hipStream_t s)
 {
   if (!q->side) CHECK_HIP(hipStreamCreateWithFlags(&q->side, hipStreamNonBlocking));
   if (!q->ev_chest) CHECK_HIP(hipEventCreateWithFlags(&q->ev_chest, hipEventDisableTiming));
-  const size_t nout = (size_t)f->njobs * q->cell.nof_ports * q->nof_rx * 5;
+  const size_t nout = (size_t)f->njobs * q->cell.nof_ports * q->nof_rx * CHEST_OUT;
   CHECK_HIP(q->back.reserve(nout * 4));
   f->out = (const float*)q->back.host;
   CHECK_HIP(hipEventRecord(q->ev_chest, s));
@@ -314,7 +380,7 @@ static int chest_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t n
   float* d_out = nullptr;
   int    r     = chest_launch_only(q, jobs, njobs, cfg, s, offset, &d_out, nullptr);
   if (r) return r;
-  return chest_finish(q, cfg, d_out, njobs, res, s);
+  return chest_finish(q, cfg, d_out, jobs, njobs, res, s);
 }
 
 extern "C" {
@@ -333,9 +399,23 @@ int mi355_ue_dl_create(mi355_ue_dl_t** q, const mi355_cell_t* cell, uint32_t nof
   d->cell   = *cell;
   d->nof_rx = nof_rx_antennas;
   const std::vector<float2> pil = crs_table(*cell);
+  // srslte_pss_generate (sync/pss.c:346-375) for N_id_2 = cell.id % 3, the same float / double expression
+  std::vector<float2> pss(62);
+  {
+    const float root_value[] = {25.0, 29.0, 34.0};
+    const int   sign         = -1;
+    const float root         = root_value[cell->id % 3];
+    for (int i = 0; i < 62; i++) {
+      const float arg = i < 31 ? (float)sign * M_PI * root * ((float)i * ((float)i + 1.0)) / 63.0
+                               : (float)sign * M_PI * root * (((float)i + 2.0) * ((float)i + 1.0)) / 63.0;
+      pss[i] = make_float2(cosf(arg), sinf(arg));
+    }
+  }
   if (hipStreamCreateWithFlags(&d->own, hipStreamNonBlocking) != hipSuccess || set_dft(d) != MI355_SUCCESS ||
       hipMalloc(&d->pilots, pil.size() * sizeof(float2)) != hipSuccess ||
       hipMemcpy(d->pilots, pil.data(), pil.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMalloc(&d->pss, pss.size() * sizeof(float2)) != hipSuccess ||
+      hipMemcpy(d->pss, pss.data(), pss.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
       mi355_pdsch_create(&d->pdsch, cell, nof_rx_antennas, device) != MI355_SUCCESS) {
     mi355_ue_dl_destroy(d);
     return MI355_ERROR;
@@ -351,6 +431,7 @@ void mi355_ue_dl_destroy(mi355_ue_dl_t* q)
   (void)hipDeviceSynchronize();
   (void)hipFree(q->tw);
   (void)hipFree(q->pilots);
+  (void)hipFree(q->pss);
   (void)hipFree(q->scratch);
   mi355_pdsch_destroy(q->pdsch);
   if (q->own) (void)hipStreamDestroy(q->own);
@@ -366,6 +447,14 @@ int mi355_ue_dl_set_standard_rates(mi355_ue_dl_t* q, int enable)
   std::lock_guard<std::mutex> lock(q->mu);
   q->std_rates = enable != 0;
   return set_dft(q);
+}
+
+int mi355_ue_dl_reset_link(mi355_ue_dl_t* q, uint32_t link)
+{
+  if (!q || link >= MI355_MAX_LINKS) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  if (link < q->links.size()) q->links[link] = ChestLink{};
+  return MI355_SUCCESS;
 }
 
 int mi355_ofdm_rx_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, void* stream)
@@ -436,7 +525,7 @@ int mi355_ue_dl_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, co
     j.payload[0] = payloads[2 * i];
     j.payload[1] = payloads[2 * i + 1];
   }
-  ChestFill fill{q, chest_cfg, nullptr, njobs, chest, false};
+  ChestFill fill{q, chest_cfg, nullptr, sfjobs, njobs, chest, false};
   if ((r = chest_finish_async(q, &fill, d_out, s))) return r;
   const auto t1 = now();
   // the AVERAGE estimator writes the same estimate into every OFDM symbol: the equaliser may read row 0 only
@@ -552,7 +641,7 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   if ((r = ofdm_run(q, sfjobs, njobs, s, &used))) return r;
   float *d_out = nullptr, *d_noise = nullptr;
   if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise))) return r;
-  ChestFill fill{q, chest_cfg, nullptr, njobs, chest, false};
+  ChestFill fill{q, chest_cfg, nullptr, sfjobs, njobs, chest, false};
   if ((r = chest_finish_async(q, &fill, d_out, s))) return r;
   std::vector<uint16_t>        rntis(njobs);
   std::vector<mi355_dci_msg_t> msgs((size_t)njobs * MI355_MAX_DCI_MSG);

@@ -235,9 +235,11 @@ mi355_chest_dl_cfg_t chest_cfg_to_mi355(const srslte_chest_dl_cfg_t& c, uint32_t
   m.filter_coef[0] = c.filter_coef[0];
   m.filter_coef[1] = c.filter_coef[1];
   m.rsrp_neighbour = c.rsrp_neighbour;
-  // chest_dl.c:635: the CFO is estimated in the subframes cfo_estimate_sf_mask selects
-  m.cfo_estimate_enable = c.cfo_estimate_enable && ((1u << (tti % 10)) & c.cfo_estimate_sf_mask);
-  m.sync_error_enable   = c.sync_error_enable;
+  // chest_dl.c:635: the CFO is estimated in the subframes cfo_estimate_sf_mask selects (the library applies the mask)
+  m.cfo_estimate_enable  = c.cfo_estimate_enable;
+  m.cfo_estimate_sf_mask = c.cfo_estimate_sf_mask;
+  m.sync_error_enable    = c.sync_error_enable;
+  (void)tti;
   return m;
 }
 

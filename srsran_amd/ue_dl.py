@@ -11,12 +11,14 @@ from .pdsch import Cell, Pdsch, _declare as _declare_pdsch
 
 MAX_PORTS = 4
 CHEST_FILTER_GAUSS, CHEST_FILTER_TRIANGLE, CHEST_FILTER_NONE = range(3)
+NOISE_ALG_REFS, NOISE_ALG_PSS, NOISE_ALG_EMPTY = range(3)
+MAX_LINKS = 65536
 
 
 class ChestCfg(C.Structure):
     _fields_ = [("estimator_alg", C.c_uint32), ("noise_alg", C.c_uint32), ("filter_type", C.c_uint32),
                 ("filter_coef", C.c_float * 2), ("rsrp_neighbour", C.c_uint32), ("cfo_estimate_enable", C.c_uint32),
-                ("sync_error_enable", C.c_uint32)]
+                ("sync_error_enable", C.c_uint32), ("cfo_estimate_sf_mask", C.c_uint32)]
 
 
 def default_chest_cfg(filter_type: int = CHEST_FILTER_GAUSS, coef=(4.0, 1.0)) -> ChestCfg:
@@ -40,7 +42,7 @@ class ChestRes(C.Structure):
 
 class DlSfJob(C.Structure):
     _fields_ = [("tti", C.c_uint32), ("in_buffer", C.c_void_p * 2), ("sf_symbols", C.c_void_p * 2),
-                ("ce", (C.c_void_p * 2) * 4)]
+                ("ce", (C.c_void_p * 2) * 4), ("link", C.c_uint32)]
 
 
 def _declare():
@@ -53,6 +55,7 @@ def _declare():
     L.mi355_ue_dl_create.argtypes = [C.POINTER(vp), C.POINTER(Cell), u32, i32]
     L.mi355_ue_dl_destroy.argtypes = [vp]
     L.mi355_ue_dl_set_standard_rates.argtypes = [vp, i32]
+    L.mi355_ue_dl_reset_link.argtypes = [vp, u32]
     L.mi355_ofdm_rx_batch.argtypes = [vp, C.POINTER(DlSfJob), u32, vp]
     L.mi355_chest_dl_estimate_batch.argtypes = [vp, C.POINTER(DlSfJob), u32, C.POINTER(ChestCfg),
                                                 C.POINTER(ChestRes), vp]
@@ -88,6 +91,9 @@ class UeDl:
             self.L.mi355_ue_dl_pdsch(self.h)), cell, nof_rx_antennas
         self.pdsch.device = device
         self.pdsch.close = lambda: None
+
+    def reset_link(self, link: int):
+        check(self.L.mi355_ue_dl_reset_link(self.h, link), "reset_link")
 
     def ofdm(self, jobs: list[DlSfJob]):
         arr = (DlSfJob * len(jobs))(*jobs)

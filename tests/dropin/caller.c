@@ -65,7 +65,7 @@ typedef struct {
 
 typedef struct {
   uint32_t nof_prb, nof_ports, nof_rx, cell_id, rnti, tm, use_tbs_index_alt, decoder_type, csi_enable;
-  uint32_t max_nof_iterations, cfo_estimate_enable, estimator_alg, noise_alg;
+  uint32_t max_nof_iterations, cfo_estimate_enable, estimator_alg, noise_alg, sync_error_enable;
 } caller_cfg_t;
 
 /* iq: nsf x nof_rx x SRSLTE_SF_LEN_PRB(nof_prb) complex samples; payload: nsf x 3 decoders x 2 TBs x max_bytes */
@@ -110,6 +110,7 @@ int caller_ue_dl(const caller_cfg_t* c, const cf_t* iq, const uint32_t* ttis, ui
   ue_dl_cfg.chest_cfg.estimator_alg          = (srslte_chest_dl_estimator_alg_t)c->estimator_alg;
   ue_dl_cfg.chest_cfg.cfo_estimate_enable    = c->cfo_estimate_enable;
   ue_dl_cfg.chest_cfg.cfo_estimate_sf_mask   = 1023;
+  ue_dl_cfg.chest_cfg.sync_error_enable      = c->sync_error_enable;
 
   for (uint32_t i = 0; i < nsf; i++) {
     caller_sf_res_t* o = &out[i];
@@ -131,6 +132,7 @@ int caller_ue_dl(const caller_cfg_t* c, const cf_t* iq, const uint32_t* ttis, ui
     o->noise_estimate = ue_dl.chest_res.noise_estimate;
     o->snr_db         = ue_dl.chest_res.snr_db;
     o->rsrp           = ue_dl.chest_res.rsrp;
+    o->cfo            = ue_dl.chest_res.cfo;
     o->cfo            = ue_dl.chest_res.cfo;
     if (o->ret_fft < 0) continue;
     srslte_dci_dl_t dci_dl[SRSLTE_MAX_DCI_MSG];

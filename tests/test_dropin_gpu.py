@@ -31,7 +31,8 @@ CALLER = os.path.join(ROOT, "tests", "dropin", "libdropin_caller.so")
 class CallerCfg(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ("nof_prb", "nof_ports", "nof_rx", "cell_id", "rnti", "tm",
                                           "use_tbs_index_alt", "decoder_type", "csi_enable", "max_nof_iterations",
-                                          "cfo_estimate_enable", "estimator_alg", "noise_alg")]
+                                          "cfo_estimate_enable", "estimator_alg", "noise_alg",
+                                          "sync_error_enable")]
 
 
 class SfRes(C.Structure):
@@ -143,9 +144,12 @@ def test_ue_dl_drop_in_phy_dl_test_flow(case):
     rnti = 0x46
     ttis = [10 * 7 + 0, 10 * 7 + 3, 10 * 8 + 6, 10 * 9 + 9]
     iq, expect = _synth(case, ttis, rnti)
+    # srsUE's set_ue_dl_cfg defaults (phy_common.cc:78-108, main.cc:317-318): CFO estimation on in every subframe
+    # (cfo_ref_mask 1023), REFS noise, AVERAGE; sync-error correction (an option, off by default) on every other case
+    sync = CASES.index(case) % 2
     c = CallerCfg(nof_prb=nprb, nof_ports=ports, nof_rx=nrx, cell_id=cid, rnti=rnti, tm=tm, use_tbs_index_alt=int(alt),
-                  decoder_type=1, csi_enable=1, max_nof_iterations=10, cfo_estimate_enable=0, estimator_alg=0,
-                  noise_alg=0)
+                  decoder_type=1, csi_enable=1, max_nof_iterations=10, cfo_estimate_enable=1, estimator_alg=0,
+                  noise_alg=0, sync_error_enable=sync)
     nsf = len(ttis)
     maxb = max(t for e in expect for t in e[0].tbs) // 8 + 16
     pay = np.zeros((nsf, 3, 2, maxb), np.uint8)
@@ -161,6 +165,7 @@ def test_ue_dl_drop_in_phy_dl_test_flow(case):
         assert o.ret_pdsch == 0 and o.ret_host == 0 and o.ret_fad == 1, (o.ret_pdsch, o.ret_host, o.ret_fad)
         # the chest result scalars are filled (noise tracks the 32 / 40 dB AWGN)
         assert o.noise_estimate > 0 and np.isfinite(o.snr_db) and o.rsrp > 0
+        assert np.isfinite(o.cfo) and abs(o.cfo) < 0.05  # no carrier offset in the synthetic channel
         for t in range(cfg.nof_tb):
             nb = cfg.tbs[t] // 8
             assert o.crc[t] and o.crc_host[t] and o.ack_fad[t], (name, i, t)
