@@ -43,6 +43,17 @@ __device__ __forceinline__ v2s vmax(v2s a, v2s b) { return __builtin_elementwise
 __device__ __forceinline__ v2s splat(short s) { return (v2s){s, s}; }
 // (a.hi, b.lo): the pair "second window of this lane, first window of the next lane"
 __device__ __forceinline__ uint32_t hi_lo(uint32_t a, uint32_t b) { return __builtin_amdgcn_alignbit(b, a, 16); }
+// the word lane q-1 / q+1 holds (DPP row_shr:1 / row_shl:1 inside 16-lane rows; a code block's NL <= 8 lanes never
+// straddle a row, and the lanes at a code-block edge, whose value comes from another code block or is 0, discard
+// what they compute from it)
+__device__ __forceinline__ uint32_t from_prev(uint32_t v)
+{
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t from_next(uint32_t v)
+{
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xf, 0xf, true);
+}
 
 // ---------------------------------------------------------------------------- trellis steps
 // State numbering reg0<<2|reg1<<1|reg2, branch metric u*x + p*y (turbocoder.c:403-421).
@@ -131,8 +142,14 @@ __device__ __forceinline__ void set_minf(v2s s[8])
 // DIAG (diagnostic builds only, selected by MI355_TDEC_DIAG): 1 = backward pass only, 2 = forward only
 // FULL: L % SEG == 0 (every K whose window length is a multiple of 8, e.g. K = 6144): no ragged last segment,
 // so every segment-bound test folds at compile time and the unrolled steps stay one basic block.
-template <int NSB, int SEG, int MODE, int DIAG = 0, bool FULL = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void tdec_win_halfit(TdecWinArgs a)
+#ifndef TDEC_WAVES_PER_EU
+#define TDEC_WAVES_PER_EU 3
+#endif
+// OUTK: what the half-iteration emits besides the extrinsic (compile time, so the forward loop has no per-step
+// branches): 0 nothing, 1 decision bytes (a.dec: DEC1 from registers, DEC2 through an LDS bitmap), 2 the decision
+// LLRs D (the decide kernel packs them)
+template <int NSB, int SEG, int MODE, int DIAG = 0, bool FULL = false, int OUTK = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_PER_EU))) void tdec_win_halfit(TdecWinArgs a)
 {
   constexpr int NL = NSB / 2;
   constexpr int G  = 64 / NL;
@@ -165,7 +182,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   const uint32_t* AP   = a.A1 + wg0;
   uint32_t*       ck   = a.ckpt + (size_t)grp * nseg * 8 * 64 + q;
 
-  v2s st[8], nw[8];
+  v2s st[8], nw[8], aw[8];
+
+  // ------------------------------------------------ forward-pass boundary, computed first
+  // alpha warm-up over the LAST 40 steps of the PREVIOUS window (lane q-1), turbodecoder_win.h:705-757.  Done
+  // before the backward pass, whose first rows are these: they are read from HBM once (the backward pass finds them
+  // in cache) and the forward pass starts from aw without reading them again.
+  set_minf(aw);
+#pragma unroll 1
+  for (int b = 0; b < TDEC_WARMUP / 8; b++) {
+    uint32_t xo[8], yo[8], ao[8] = {};
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = (L - TDEC_WARMUP) + 8 * b + i;
+      xo[i]       = X[j * xs];
+      yo[i]       = Y[j * NL];
+      if constexpr (has_ap) ao[i] = AP[j * 64];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int k = 8 * b + i;
+      v2s       x = U(hi_lo(from_prev(xo[i]), xo[i]));
+      if constexpr (has_ap) x = sadd(x, U(hi_lo(from_prev(ao[i]), ao[i])));
+      v2s c0[8], c1[8];
+      alpha_cands<true>(aw, x, U(hi_lo(from_prev(yo[i]), yo[i])), c0, c1);
+#pragma unroll
+      for (int s = 0; s < 8; s++) aw[s] = vmax(c0[s], c1[s]);
+      if ((k & 1) == 0 && k != 0) normalize<true>(aw);
+    }
+  }
 
   if constexpr (DIAG != 2) {
   // ------------------------------------------------ backward pass: boundary (row L)
@@ -175,23 +220,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   set_minf(st);
 #pragma unroll 1
   for (int b = TDEC_WARMUP / 8 - 1; b >= 0; b--) {
-    uint32_t xo[8], xn[8], yo[8], yn[8], ao[8] = {}, an[8] = {};
+    uint32_t xo[8], yo[8], ao[8] = {};
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = 8 * b + i;
       xo[i]       = X[j * xs];
-      xn[i]       = X[j * xs + 1];
       yo[i]       = Y[j * NL];
-      yn[i]       = Y[j * NL + 1];
       if constexpr (has_ap) ao[i] = AP[j * 64];
-      if constexpr (has_ap) an[i] = AP[j * 64 + 1];
     }
 #pragma unroll
     for (int i = 7; i >= 0; i--) {
       const int k = 8 * b + i;
-      v2s       x = U(hi_lo(xo[i], xn[i]));
-      if constexpr (has_ap) x = sadd(x, U(hi_lo(ao[i], an[i])));
-      beta_step<true>(st, x, U(hi_lo(yo[i], yn[i])), nw);
+      v2s       x = U(hi_lo(xo[i], from_next(xo[i])));
+      if constexpr (has_ap) x = sadd(x, U(hi_lo(ao[i], from_next(ao[i]))));
+      beta_step<true>(st, x, U(hi_lo(yo[i], from_next(yo[i]))), nw);
 #pragma unroll
       for (int s = 0; s < 8; s++) st[s] = nw[s];
       if ((k & 1) == 0 && k != 0) normalize<true>(st);
@@ -273,34 +315,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
     if (st[0].x == 12345 && st[1].y == 777) a.D[q] = W(st[0]); // keep the diagnostic loads alive
     return;
   }
-  // ------------------------------------------------ forward pass: boundary at the window start
-  // warm-up over the LAST 40 steps of the PREVIOUS window (lane q-1), turbodecoder_win.h:705-757
-  set_minf(st);
-#pragma unroll 1
-  for (int b = 0; b < TDEC_WARMUP / 8; b++) {
-    uint32_t xo[8], xp[8], yo[8], yp[8], ao[8] = {}, ap_[8] = {};
+  // ------------------------------------------------ forward pass: boundary at the window start (aw, above)
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int j = (L - TDEC_WARMUP) + 8 * b + i;
-      xo[i]       = X[j * xs];
-      xp[i]       = X[j * xs - 1];
-      yo[i]       = Y[j * NL];
-      yp[i]       = Y[j * NL - 1];
-      if constexpr (has_ap) ao[i] = AP[j * 64];
-      if constexpr (has_ap) ap_[i] = AP[j * 64 - 1];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int k = 8 * b + i;
-      v2s       x = U(hi_lo(xp[i], xo[i]));
-      if constexpr (has_ap) x = sadd(x, U(hi_lo(ap_[i], ao[i])));
-      v2s c0[8], c1[8];
-      alpha_cands<true>(st, x, U(hi_lo(yp[i], yo[i])), c0, c1);
-#pragma unroll
-      for (int s = 0; s < 8; s++) st[s] = vmax(c0[s], c1[s]);
-      if ((k & 1) == 0 && k != 0) normalize<true>(st);
-    }
-  }
+  for (int s = 0; s < 8; s++) st[s] = aw[s];
   if (l == 0) {
     // first window starts in the known state 0
     st[0].x = 0;
@@ -314,9 +331,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   int16_t*        D16  = (int16_t*)a.D + (size_t)grp * Lp * 128;
   const uint32_t* tab  = (dec2 ? a.dstA : a.dstE) + l;
   const int       lane0 = cbg * NL; // first lane of this code block inside the 64-lane row
-  const bool      wr_bits = !dec2 && a.dec != nullptr; // fused decision bytes (DEC1: ext1 in natural order)
-  const bool      wr_bm   = dec2 && a.dec != nullptr;  // fused decision bytes (DEC2: app1 de-interleaved)
-  const bool      wr_d    = a.write_d && !wr_bits && !wr_bm;
+  constexpr bool  wr_bits = !dec2 && OUTK == 1; // fused decision bytes (DEC1: ext1 in natural order)
+  constexpr bool  wr_bm   = dec2 && OUTK == 1;  // fused decision bytes (DEC2: app1 de-interleaved)
+  constexpr bool  wr_d    = OUTK == 2;
   // DEC2 decisions land at scattered natural positions (row j' of windows wlo/whi), so they are collected
   // as a bitmap of the code block in LDS (K/8 bytes, byte order of the output) and stored at the end
   constexpr int BMW = NSB == 16 ? 192 : 25; // u32 words per code block (K <= 6144 / K <= 800)
@@ -324,7 +341,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
   if constexpr (dec2) {
     __shared__ uint32_t bm_lds[4 * G * BMW];
     bm = bm_lds + ((threadIdx.x >> 6) * G + cbg) * BMW;
-    if (wr_bm) {
+    if constexpr (wr_bm) {
       for (int w = l; w < K / 32; w += NL) bm[w] = 0;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -354,6 +371,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
     uint32_t  nx[SEG], ny[SEG], na[SEG] = {}, nd[SEG], nc[8];
     uint32_t  bits = 0; // decision bits of the segment: window 2l in bits 8..15, 2l+1 in 0..7 (MSB first)
     if (wr_bits && (t & 1)) bits = dbits;
+    (void)dbits;
     if (t + 1 < nseg) load(t + 1, nx, ny, na, nd, nc);
 
     v2s xin[SEG];
@@ -429,21 +447,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
           const v2s ev = has_ap ? out - U(ca[i]) : out;
           E16[olo]     = ev.x;
           E16[ohi]     = ev.y;
-          if (wr_d) WG_AT(a.D, j) = W(out);
+          if constexpr (wr_d) WG_AT(a.D, j) = W(out);
           bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
         } else {
           // a1 = app1 - ext1 (wrapping) of the next DEC1, turbodecoder_iter.h:108-110
           const v2s av = out - xin[i];
           A16[olo]     = av.x;
           A16[ohi]     = av.y;
-          if (wr_bm) { // natural bit w*L + j': byte w*L/8 + j'/8, bit 7 - j'%8 (turbodecoder_win.h:973-993)
+          if constexpr (wr_bm) { // natural bit w*L + j': byte w*L/8 + j'/8, bit 7 - j'%8 (turbodecoder_win.h:973-993)
             const uint32_t jd = (tb & 0xffffu) >> 7, wlo = tb & 15u, whi = (tb >> 16) & 15u;
             const uint32_t blo = wlo * (L / 8) + (jd >> 3), bhi = whi * (L / 8) + (jd >> 3);
             const uint32_t sh  = 7 - (jd & 7);
             atomicOr(&bm[blo >> 2], (uint32_t)(out.x > 0) << (((blo & 3) << 3) + sh));
             atomicOr(&bm[bhi >> 2], (uint32_t)(out.y > 0) << (((bhi & 3) << 3) + sh));
           }
-          if (wr_d) {
+          if constexpr (wr_d) {
             D16[olo] = out.x;
             D16[ohi] = out.y;
           }
@@ -451,7 +469,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
       }
     }
     }
-    if (wr_bits) { // turbodecoder_win.h:973-993: bit = LLR > 0, natural order, MSB first
+    if constexpr (wr_bits) { // turbodecoder_win.h:973-993: bit = LLR > 0, natural order, MSB first
       // two segments per store: bytes t-1, t of each window as one 16-bit word (the segment of an odd t
       // lands in the high byte); a trailing even segment is stored alone
       if ((t & 1) || t + 1 == nseg) {
@@ -478,7 +496,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void t
     for (int s = 0; s < 8; s++) cc[s] = nc[s];
   }
   if constexpr (dec2) {
-    if (wr_bm) { // the code block's K/8 decision bytes, 8-byte stores by its NL lanes
+    if constexpr (wr_bm) { // the code block's K/8 decision bytes, 8-byte stores by its NL lanes
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -555,15 +573,39 @@ static int diag_mode()
   return m;
 }
 
+// MI355_TDEC_LDS (diagnostic): reserve that many bytes of LDS per workgroup, capping the waves per CU
+static size_t diag_lds()
+{
+  static long m = -1;
+  if (m < 0) {
+    const char* e = getenv("MI355_TDEC_LDS");
+    m             = e ? atol(e) : 0;
+  }
+  return (size_t)m;
+}
+
+template <int NSB, int DIAG, bool FULL, int OUTK>
+static void launch_mode_o(int mode, int blocks, const TdecWinArgs& a, hipStream_t s)
+{
+  const size_t lds = diag_lds();
+  if (mode == 0) {
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 0, DIAG, FULL, OUTK>), dim3(blocks), dim3(256), lds, s, a);
+  } else if (mode == 1) {
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 1, DIAG, FULL, OUTK>), dim3(blocks), dim3(256), lds, s, a);
+  } else {
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 2, DIAG, FULL, OUTK>), dim3(blocks), dim3(256), lds, s, a);
+  }
+}
+
 template <int NSB, int DIAG, bool FULL = false>
 static void launch_mode(int mode, int blocks, const TdecWinArgs& a, hipStream_t s)
 {
-  if (mode == 0) {
-    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 0, DIAG, FULL>), dim3(blocks), dim3(256), 0, s, a);
-  } else if (mode == 1) {
-    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 1, DIAG, FULL>), dim3(blocks), dim3(256), 0, s, a);
+  if (a.dec) {
+    launch_mode_o<NSB, DIAG, FULL, 1>(mode, blocks, a, s);
+  } else if (a.write_d) {
+    launch_mode_o<NSB, DIAG, FULL, 2>(mode, blocks, a, s);
   } else {
-    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 2, DIAG, FULL>), dim3(blocks), dim3(256), 0, s, a);
+    launch_mode_o<NSB, DIAG, FULL, 0>(mode, blocks, a, s);
   }
 }
 
