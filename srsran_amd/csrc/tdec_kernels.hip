@@ -143,7 +143,7 @@ __device__ __forceinline__ void set_minf(v2s s[8])
 // FULL: L % SEG == 0 (every K whose window length is a multiple of 8, e.g. K = 6144): no ragged last segment,
 // so every segment-bound test folds at compile time and the unrolled steps stay one basic block.
 #ifndef TDEC_WAVES_PER_EU
-#define TDEC_WAVES_PER_EU 3
+#define TDEC_WAVES_PER_EU 2
 #endif
 // OUTK: what the half-iteration emits besides the extrinsic (compile time, so the forward loop has no per-step
 // branches): 0 nothing, 1 decision bytes (a.dec: DEC1 from registers, DEC2 through an LDS bitmap), 2 the decision
@@ -271,25 +271,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
         if constexpr (has_ap) ap[i] = AP[j * 64];
       }
     };
-    // two segments in flight ahead of the one being consumed (registers are free in this pass)
-    uint32_t n1x[SEG], n1y[SEG], n1a[SEG] = {};
+    // two segments in flight ahead of the one being consumed (registers are free in this pass).  The three
+    // register sets rotate by position in a loop unrolled three times, so no copies move them between segments.
+    uint32_t bx[SEG], by[SEG], ba[SEG] = {}, dx[SEG], dy[SEG], da[SEG] = {};
     load(nseg - 1, cx, cy, ca);
-    if (nseg > 1) load(nseg - 2, n1x, n1y, n1a);
-#pragma unroll 1
-    for (int t = nseg - 1; t >= 0; t--) {
-      uint32_t n2x[SEG], n2y[SEG], n2a[SEG] = {};
-      if (t > 1) load(t - 2, n2x, n2y, n2a);
+    if (nseg > 1) load(nseg - 2, bx, by, ba);
+    auto seg = [&](int t, const uint32_t* sx, const uint32_t* sy, const uint32_t* sa, uint32_t* lx, uint32_t* ly,
+                   uint32_t* la) {
+      if (t > 1) load(t - 2, lx, ly, la);
 #pragma unroll
       for (int i = SEG - 1; i >= 0; i--) {
         const int k = t * SEG + i;
         if (FULL || k < L) {
-          v2s x = U(cx[i]);
-          if constexpr (has_ap) x = sadd(x, U(ca[i]));
+          v2s x = U(sx[i]);
+          if constexpr (has_ap) x = sadd(x, U(sa[i]));
           if constexpr (DIAG == 4) {
-            st[0] = st[0] ^ x ^ U(cy[i]);
+            st[0] = st[0] ^ x ^ U(sy[i]);
             continue;
           }
-          beta_step<true>(st, x, U(cy[i]), nw);
+          beta_step<true>(st, x, U(sy[i]), nw);
 #pragma unroll
           for (int s = 0; s < 8; s++) st[s] = nw[s];
           if (i == 0 && t > 0 && DIAG != 3) {
@@ -299,15 +299,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
           if ((i & 1) == 0 && k != 0) normalize<true>(st);
         }
       }
-#pragma unroll
-      for (int i = 0; i < SEG; i++) {
-        cx[i]  = n1x[i];
-        cy[i]  = n1y[i];
-        ca[i]  = n1a[i];
-        n1x[i] = n2x[i];
-        n1y[i] = n2y[i];
-        n1a[i] = n2a[i];
-      }
+    };
+#pragma unroll 1
+    for (int t = nseg - 1; t >= 0; t -= 3) {
+      seg(t, cx, cy, ca, dx, dy, da);
+      if (t >= 1) seg(t - 1, bx, by, ba, cx, cy, ca);
+      if (t >= 2) seg(t - 2, dx, dy, da, bx, by, ba);
     }
   }
   } // DIAG != 2
@@ -364,11 +361,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
   load(0, cx, cy, ca, cd, cc);
   uint32_t dbits = 0; // decision bits of the previous (even) segment, bits 16..31
 
-#pragma unroll 1
-  for (int t = 0; t < nseg; t++) {
+  // segment t is processed from one register set while segment t+1 loads into the other; the loop is unrolled
+  // twice so the two sets swap roles by position instead of being copied
+  uint32_t nx[SEG], ny[SEG], na[SEG] = {}, nd[SEG], nc[8];
+  auto fseg = [&](int t, const uint32_t* cx, const uint32_t* cy, const uint32_t* ca, const uint32_t* cd,
+                  const uint32_t* cc, uint32_t* nx, uint32_t* ny, uint32_t* na, uint32_t* nd, uint32_t* nc) {
     const int s0 = t * SEG;
     const int e  = FULL ? s0 + SEG : ((s0 + SEG < L) ? s0 + SEG : L);
-    uint32_t  nx[SEG], ny[SEG], na[SEG] = {}, nd[SEG], nc[8];
     uint32_t  bits = 0; // decision bits of the segment: window 2l in bits 8..15, 2l+1 in 0..7 (MSB first)
     if (wr_bits && (t & 1)) bits = dbits;
     (void)dbits;
@@ -427,13 +426,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
       if (FULL ? i < SEG : j < e) {
         v2s c0[8], c1[8];
         alpha_cands<true>(st, xin[i], U(cy[i]), c0, c1);
-        v2s m0 = sadd(R[ii][0], c0[0]);
-        v2s m1 = sadd(R[ii][0], c1[0]);
+        // max over the 8 states as a tree (max is exact, so the order is free): no serial dependency chain
+        v2s t0[8], t1[8];
 #pragma unroll
-        for (int s = 1; s < 8; s++) {
-          m0 = vmax(m0, sadd(R[ii][s], c0[s]));
-          m1 = vmax(m1, sadd(R[ii][s], c1[s]));
+        for (int s = 0; s < 8; s++) {
+          t0[s] = sadd(R[ii][s], c0[s]);
+          t1[s] = sadd(R[ii][s], c1[s]);
         }
+        const v2s m0 = vmax(vmax(vmax(t0[0], t0[1]), vmax(t0[2], t0[3])), vmax(vmax(t0[4], t0[5]), vmax(t0[6], t0[7])));
+        const v2s m1 = vmax(vmax(vmax(t1[0], t1[1]), vmax(t1[2], t1[3])), vmax(vmax(t1[4], t1[5]), vmax(t1[6], t1[7])));
         const v2s out = ssub(m1, m0);
 #pragma unroll
         for (int s = 0; s < 8; s++) st[s] = vmax(c0[s], c1[s]);
@@ -485,15 +486,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
         dbits = bits << 16; // keep segment t (even) in the upper half for the next segment's store
       }
     }
-#pragma unroll
-    for (int i = 0; i < SEG; i++) {
-      cx[i] = nx[i];
-      cy[i] = ny[i];
-      ca[i] = na[i];
-      cd[i] = nd[i];
-    }
-#pragma unroll
-    for (int s = 0; s < 8; s++) cc[s] = nc[s];
+  };
+#pragma unroll 1
+  for (int t = 0; t < nseg; t += 2) {
+    fseg(t, cx, cy, ca, cd, cc, nx, ny, na, nd, nc);
+    if (t + 1 < nseg) fseg(t + 1, nx, ny, na, nd, nc, cx, cy, ca, cd, cc);
   }
   if constexpr (dec2) {
     if constexpr (wr_bm) { // the code block's K/8 decision bytes, 8-byte stores by its NL lanes
