@@ -224,16 +224,18 @@ def fill_res(vals: np.ndarray, nof_prb: int) -> dict:
 
 
 def channel_freq(rng: np.random.Generator, nof_ports: int, nof_rx: int, nof_prb: int, ntaps: int = 3,
-                 max_delay: int = 6) -> np.ndarray:
+                 max_delay: int = 6, common_delays: bool = False) -> np.ndarray:
     """Time-invariant frequency-selective channel: per (port, rx) a few taps within the CP, as per-subcarrier
-    gains (nof_ports, nof_rx, 12*nof_prb) in grid order (negative frequencies first)."""
+    gains (nof_ports, nof_rx, 12*nof_prb) in grid order (negative frequencies first).  common_delays: one delay
+    profile for every (port, rx) pair (independent gains), as a physical array sees it."""
     nre = 12 * nof_prb
     N = symbol_sz(nof_prb)
     k = np.concatenate([np.arange(-nre // 2, 0), np.arange(1, nre // 2 + 1)])
     h = np.zeros((nof_ports, nof_rx, nre), np.complex128)
+    d0 = np.sort(rng.integers(0, max_delay, ntaps)) if common_delays else None
     for p in range(nof_ports):
         for r in range(nof_rx):
-            d = np.sort(rng.integers(0, max_delay, ntaps))
+            d = d0 if common_delays else np.sort(rng.integers(0, max_delay, ntaps))
             a = (rng.standard_normal(ntaps) + 1j * rng.standard_normal(ntaps)) / np.sqrt(2 * ntaps)
             for t in range(ntaps):
                 h[p, r] += a[t] * np.exp(-2j * np.pi * k * d[t] / N)
@@ -241,7 +243,7 @@ def channel_freq(rng: np.random.Generator, nof_ports: int, nof_rx: int, nof_prb:
 
 
 def synth_iq(cfg: pc.Cfg, rng: np.random.Generator, snr_db: float = 30.0, payload_bits=None, max_delay: int = 6,
-             channel: str = "taps", ctrl=None):
+             channel: str = "taps", ctrl=None, common_delays: bool = False):
     """channel: "taps" (random taps up to max_delay samples) or "cross" (phy_dl_test's flat 2x2 [[1,1],[1,-1]]).
     ctrl: optional callable(tx) writing the control region (PCFICH / PDCCH) into the (ports, grid) tx grids.
     Returns (iq (nof_rx, N*15) complex64, payload bytes per TB, true per-subcarrier channel, noise var)."""
@@ -267,7 +269,7 @@ def synth_iq(cfg: pc.Cfg, rng: np.random.Generator, snr_db: float = 30.0, payloa
         w = np.array([[1, 1], [1, -1]], np.complex64)[: cfg.nof_ports, : cfg.nof_rx]
         h = np.repeat(w[:, :, None], nre, axis=2).astype(np.complex64)
     else:
-        h = channel_freq(rng, cfg.nof_ports, cfg.nof_rx, cfg.nof_prb, max_delay=max_delay)
+        h = channel_freq(rng, cfg.nof_ports, cfg.nof_rx, cfg.nof_prb, max_delay=max_delay, common_delays=common_delays)
     sigma2 = 10 ** (-snr_db / 10)
     iq = []
     for r in range(cfg.nof_rx):

@@ -201,6 +201,7 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
     acc[0] += cpw(x);
     const float2 e = cprod_conj(x, crs[k]);
     pe[k]          = e;
+    if (a.pe_out) a.pe_out[(size_t)blockIdx.x * (4 * nref) + k] = e; // the Wiener estimator's pilots (wiener_kernels.hip)
     acc[2] += e.x;
     acc[3] += e.y;
   }

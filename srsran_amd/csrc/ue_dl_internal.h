@@ -89,6 +89,7 @@ struct ChestArgs {
   float           cfo_n, cfo_ns, cfo_ng; // chest_estimate_cfo's n, ns, ng
   float           sync_k;               // srslte_symbol_sz / 6 (chest_dl_estimate_correct_sync_error)
   uint32_t        symbol_sz;
+  float2*         pe_out; // WIENER: the LS pilot estimates of every (job, rx, port), [4][2 nof_prb] each (or null)
 };
 
 hipError_t ofdm_launch_rx(const OfdmArgs& a, uint32_t njobs, hipStream_t s);

@@ -20,6 +20,7 @@
 #include "host_staging.h"
 #include "pdcch_runtime.h"
 #include "ue_dl_internal.h"
+#include "wiener_bank.h"
 
 using namespace mi355;
 
@@ -47,6 +48,7 @@ struct ChestLink {
 };
 
 struct mi355_ue_dl {
+  WienerBank*    wiener = nullptr; // WIENER estimator states per link (srslte_wiener_dl_t), built on first use
   int            device = 0;
   mi355_cell_t   cell{};
   uint32_t       nof_rx = 1;
@@ -219,12 +221,17 @@ static void fill_res(mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const fl
   }
 }
 
-static int chest_check_cfg(const mi355_chest_dl_cfg_t* cfg)
+static int chest_check_cfg(const mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg)
 {
   if (!cfg) return MI355_ERROR_INVALID_INPUTS;
-  // the Wiener estimator (wiener_dl.c) is not supported
-  if ((cfg->estimator_alg != MI355_ESTIMATOR_ALG_AVERAGE && cfg->estimator_alg != MI355_ESTIMATOR_ALG_INTERPOLATE) ||
-      cfg->noise_alg > MI355_NOISE_ALG_EMPTY || cfg->filter_type > MI355_CHEST_FILTER_NONE)
+  if (cfg->estimator_alg > MI355_ESTIMATOR_ALG_WIENER || cfg->noise_alg > MI355_NOISE_ALG_EMPTY ||
+      cfg->filter_type > MI355_CHEST_FILTER_NONE)
+    return MI355_ERROR;
+  // WIENER (chest_dl.c:648-676): the reference allocates its states for 2 ports (chest_dl.c:147) and its ready path
+  // skips the PSS / EMPTY noise update; supported with REFS noise, 1-2 ports, 1-2 rx, >= 6 PRB, normal CP
+  if (cfg->estimator_alg == MI355_ESTIMATOR_ALG_WIENER &&
+      (cfg->noise_alg != MI355_NOISE_ALG_REFS || q->cell.nof_ports > WNR_MAX_TX || q->nof_rx > WNR_MAX_RX ||
+       q->cell.nof_prb < 6 || q->cell.cp != MI355_CP_NORM))
     return MI355_ERROR;
   return MI355_SUCCESS;
 }
@@ -236,9 +243,18 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
                              const mi355_chest_dl_cfg_t* cfg, hipStream_t s, size_t offset, float** d_out_p,
                              float** d_noise_p)
 {
-  int r = chest_check_cfg(cfg);
+  int r = chest_check_cfg(q, cfg);
   if (r) return r;
   const uint32_t P = q->cell.nof_ports, R = q->nof_rx;
+  const bool     wiener = cfg->estimator_alg == MI355_ESTIMATOR_ALG_WIENER;
+  if (wiener && !q->wiener) {
+    auto* b = new WienerBank();
+    if ((r = b->init(q->device, q->cell.nof_prb, P, R))) {
+      delete b;
+      return r;
+    }
+    q->wiener = b;
+  }
   const size_t   ncj = (size_t)njobs * P * R;
   uint32_t       maxl = 0;
   for (uint32_t i = 0; i < njobs; i++) {
@@ -252,10 +268,13 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
   char*        base = nullptr;
   const size_t jb   = (ncj * sizeof(ChestJob) + 255) / 256 * 256;
   const size_t ob   = (nout * 4 + 255) / 256 * 256;
-  if ((r = get_scratch(q, offset + jb + ob + (size_t)njobs * 4 + 256, &base))) return r;
+  const size_t nb   = ((size_t)njobs * 4 + 255) / 256 * 256;
+  const size_t pb   = wiener ? ncj * 4 * 2 * q->cell.nof_prb * sizeof(float2) : 0; // LS pilots for the Wiener stage
+  if ((r = get_scratch(q, offset + jb + ob + nb + pb + 256, &base))) return r;
   base += offset;
   float*     d_out   = (float*)(base + jb);
   float*     d_noise = (float*)(base + jb + ob);
+  float2*    d_pe    = wiener ? (float2*)(base + jb + ob + nb) : nullptr;
   const bool sf05_alg = cfg->noise_alg != MI355_NOISE_ALG_REFS; // PSS / EMPTY: state updated in subframes 0 and 5
   std::vector<int32_t> last05(sf05_alg ? (size_t)maxl + 1 : 0, -1);
   size_t               k = 0;
@@ -293,7 +312,8 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
   ca.nof_ports   = P;
   ca.nof_rx      = R;
   ca.filter_type = cfg->filter_type;
-  ca.alg         = cfg->estimator_alg;
+  ca.alg         = wiener ? MI355_ESTIMATOR_ALG_AVERAGE : cfg->estimator_alg; // WIENER falls back to AVERAGE until ready
+  ca.pe_out      = d_pe;
   ca.noise_alg   = cfg->noise_alg;
   ca.coef0       = cfg->filter_coef[0];
   ca.coef1       = cfg->filter_coef[1];
@@ -320,6 +340,25 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
     CHECK_HIP(chest_launch(ca, (uint32_t)ncj, s));
   }
   CHECK_HIP(chest_launch_resolve(ca, njobs, d_noise_p ? d_noise : nullptr, s));
+  if (wiener) {
+    // srslte_wiener_dl_run for m = 0..17 of every (rx, port) with this subframe's REFS noise and RSRP; the Wiener rows
+    // replace the AVERAGE estimate where the link was ready (chest_dl.c:648-676)
+    std::vector<WienerJob> wj(njobs);
+    std::vector<uint32_t>  wl(njobs);
+    const size_t           nref = 2 * q->cell.nof_prb;
+    for (uint32_t i = 0; i < njobs; i++) {
+      WienerJob& J = wj[i];
+      memset(&J, 0, sizeof(J));
+      J.pilots    = d_pe + (size_t)i * R * P * 4 * nref;
+      J.chest_out = d_out + (size_t)i * R * P * CHEST_OUT;
+      for (uint32_t a = 0; a < R; a++)
+        for (uint32_t p = 0; p < P; p++) J.ce[p][a] = (float2*)jobs[i].ce[p][a];
+      wl[i] = jobs[i].link;
+    }
+    const uint32_t shift[WNR_MAX_TX] = {q->cell.id % 6, (3 + q->cell.id % 6) % 6}; // srslte_refsignal_cs_fidx(cell, 0, p, 0)
+    if ((r = q->wiener->launch(wj.data(), wl.data(), njobs, shift, false, CHEST_OUT, CHEST_O_NOISE, CHEST_O_RSRP, s)))
+      return r;
+  }
   *d_out_p = d_out;
   if (d_noise_p) *d_noise_p = d_noise;
   return MI355_SUCCESS;
@@ -438,6 +477,7 @@ void mi355_ue_dl_destroy(mi355_ue_dl_t* q)
   if (q->side) (void)hipStreamDestroy(q->side);
   if (q->ev_chest) (void)hipEventDestroy(q->ev_chest);
   delete q->ctrl;
+  delete q->wiener;
   delete q;
 }
 
@@ -454,6 +494,7 @@ int mi355_ue_dl_reset_link(mi355_ue_dl_t* q, uint32_t link)
   if (!q || link >= MI355_MAX_LINKS) return MI355_ERROR_INVALID_INPUTS;
   std::lock_guard<std::mutex> lock(q->mu);
   if (link < q->links.size()) q->links[link] = ChestLink{};
+  if (q->wiener && link < q->wiener->slabs.size() && q->wiener->slabs[link]) return q->wiener->reset(link);
   return MI355_SUCCESS;
 }
 
