@@ -88,3 +88,17 @@ def test_reference_header_caller_links():
     assert "libsrslte_mi355.so" in out and "not found" not in out
     und = subprocess.run(["nm", "-D", "--undefined-only", caller], check=True, capture_output=True, text=True).stdout
     assert "srslte_ue_dl_find_dl_dci" in und and "srslte_pdsch_decode" in und
+
+
+def test_tdec_shim_fits_reference_storage(tmp_path):
+    """INTEGRATION 2.3's shim casts the caller's srslte_tdec_t* to mi355_srslte_tdec_t*: the reference object must
+    be at least as large (its size from the reference-layout fixture)."""
+    m = re.search(r"^srslte_tdec_t\s+size\s+(\d+)", open(FIXTURE).read(), flags=re.M)
+    assert m, "srslte_tdec_t size missing from the fixture"
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "srsran_amd/srslte_tdec.h"\n'
+                   'int main(void) { printf("%zu", sizeof(mi355_srslte_tdec_t)); return 0; }\n')
+    exe = str(tmp_path / "sz")
+    subprocess.run(["gcc", "-std=gnu11", "-I", os.path.join(ROOT, "include"), "-o", exe, str(src)], check=True)
+    ours = int(subprocess.run([exe], check=True, capture_output=True, text=True).stdout)
+    assert ours <= int(m.group(1)), (ours, m.group(1))
