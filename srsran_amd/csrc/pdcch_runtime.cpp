@@ -30,6 +30,7 @@ namespace mi355 {
 
 CtrlState::~CtrlState()
 {
+  for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   (void)hipFree(d_tab);
   (void)hipFree(d_buf);
   delete st;
@@ -69,6 +70,16 @@ int CtrlState::run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, con
                    mi355_ctrl_res_t* res, mi355_dci_msg_t* msgs)
 {
   if (!n) return MI355_SUCCESS;
+  int r = launch(sfjobs, host_noise, d_noise, rntis, cfgs, n, 1, s);
+  return r ? r : finish(0, rntis, cfgs, res, msgs);
+}
+
+int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, const float* d_noise,
+                      const uint16_t* rntis, const mi355_ue_dl_cfg_t* cfgs, uint32_t n, uint32_t nchunks,
+                      hipStream_t s)
+{
+  if (!n) return MI355_SUCCESS;
+  nchunks = std::max(1u, std::min(nchunks, n));
   const uint32_t stride = (8 * regs.nregs[2] + 63) / 64 * 64; // LLRs per subframe (CFI 3 worst case)
   const size_t   b_jobs = staged_size((size_t)n * sizeof(CtrlJob)), b_blind = staged_size((size_t)n * sizeof(BlindJob));
   const size_t   b_llr = staged_size((size_t)n * stride * 4), b_cfi = staged_size((size_t)n * 4);
@@ -122,42 +133,67 @@ int CtrlState::run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, con
   uint32_t* d_cfi  = (uint32_t*)(base + b_jobs + b_blind + b_llr);
   float*    d_corr = (float*)(base + b_jobs + b_blind + b_llr + b_cfi);
   DciCand*  d_cand = (DciCand*)(base + b_jobs + b_blind + b_llr + b_cfi + b_corr);
-  CtrlArgs  a{};
-  a.jobs       = (const CtrlJob*)base;
-  a.pcfich_re  = d_tab;
-  a.pdcch_re   = d_tab + 16;
-  a.pcfich_seq = d_tab + 16 + 3 * PDCCH_MAX_REGS * 4;
-  a.pdcch_seq  = a.pcfich_seq + 10;
-  a.seq_words  = seq_words;
-  for (int c = 0; c < 3; c++) a.nregs[c] = regs.nregs[c];
-  a.nof_rx     = nof_rx;
-  a.nof_ports  = cell.nof_ports;
-  a.llr        = d_llr;
-  a.llr_stride = stride;
-  a.cfi        = d_cfi;
-  a.corr       = d_corr;
-  CHECK_HIP(ctrl_launch_llr(a, n, s));
-  BlindArgs b{};
-  b.jobs       = (const BlindJob*)(base + b_jobs);
-  b.llr        = d_llr;
-  b.llr_stride = stride;
-  b.cfi        = d_cfi;
-  for (int c = 0; c < 3; c++) b.ncce[c] = regs.nregs[c] / 9;
-  b.out = d_cand;
-  CHECK_HIP(ctrl_launch_blind(b, n, s));
+  const size_t ncand = (size_t)PDCCH_SLOTS * PDCCH_FMTS;
+  // host read-back area: cfi | corr | candidates of all n subframes (the device arena's order)
+  CHECK_HIP(back->reserve(b_cfi + b_corr + (size_t)n * ncand * sizeof(DciCand)));
+  b_cfi_  = b_cfi;
+  b_corr_ = b_corr;
+  chunk_end.assign(nchunks, 0);
+  while (ev.size() < nchunks) {
+    hipEvent_t e;
+    CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ev.push_back(e);
+  }
+  for (uint32_t c = 0; c < nchunks; c++) {
+    const uint32_t o = (uint32_t)((uint64_t)n * c / nchunks), m = (uint32_t)((uint64_t)n * (c + 1) / nchunks) - o;
+    chunk_end[c]     = o + m;
+    CtrlArgs a{};
+    a.jobs       = (const CtrlJob*)base + o;
+    a.pcfich_re  = d_tab;
+    a.pdcch_re   = d_tab + 16;
+    a.pcfich_seq = d_tab + 16 + 3 * PDCCH_MAX_REGS * 4;
+    a.pdcch_seq  = a.pcfich_seq + 10;
+    a.seq_words  = seq_words;
+    for (int k = 0; k < 3; k++) a.nregs[k] = regs.nregs[k];
+    a.nof_rx     = nof_rx;
+    a.nof_ports  = cell.nof_ports;
+    a.llr        = d_llr + (size_t)o * stride;
+    a.llr_stride = stride;
+    a.cfi        = d_cfi + o;
+    a.corr       = d_corr + 3 * (size_t)o;
+    CHECK_HIP(ctrl_launch_llr(a, m, s));
+    BlindArgs b{};
+    b.jobs       = (const BlindJob*)(base + b_jobs) + o;
+    b.llr        = d_llr + (size_t)o * stride;
+    b.llr_stride = stride;
+    b.cfi        = d_cfi + o;
+    for (int k = 0; k < 3; k++) b.ncce[k] = regs.nregs[k] / 9;
+    b.out = d_cand + (size_t)o * ncand;
+    CHECK_HIP(ctrl_launch_blind(b, m, s));
+    CHECK_HIP(hipMemcpyAsync(back->host + 4 * (size_t)o, d_cfi + o, 4 * (size_t)m, hipMemcpyDeviceToHost, s));
+    CHECK_HIP(hipMemcpyAsync(back->host + b_cfi + 12 * (size_t)o, d_corr + 3 * (size_t)o, 12 * (size_t)m,
+                             hipMemcpyDeviceToHost, s));
+    CHECK_HIP(hipMemcpyAsync(back->host + b_cfi + b_corr + (size_t)o * ncand * sizeof(DciCand), d_cand + (size_t)o * ncand,
+                             (size_t)m * ncand * sizeof(DciCand), hipMemcpyDeviceToHost, s));
+    CHECK_HIP(hipEventRecord(ev[c], s));
+  }
   last_n = n, last_stride = stride, last_llr = d_llr, last_cand = d_cand;
-  // one read-back: cfi | corr | candidates (contiguous in the arena)
-  const size_t nback = b_cfi + b_corr + (size_t)n * PDCCH_SLOTS * PDCCH_FMTS * sizeof(DciCand);
-  CHECK_HIP(back->reserve(nback));
-  CHECK_HIP(hipMemcpyAsync(back->host, d_cfi, nback, hipMemcpyDeviceToHost, s));
-  CHECK_HIP(hipStreamSynchronize(s));
+  return MI355_SUCCESS;
+}
+
+int CtrlState::finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_cfg_t* cfgs, mi355_ctrl_res_t* res,
+                      mi355_dci_msg_t* msgs)
+{
+  if (chunk >= chunk_end.size()) return MI355_ERROR_INVALID_INPUTS;
+  CHECK_HIP(hipEventSynchronize(ev[chunk]));
   static const bool prof = getenv("MI355_HOST_PROF") != nullptr;
   const auto        tr0  = std::chrono::steady_clock::now();
+  const uint32_t    b    = chunk ? chunk_end[chunk - 1] : 0, e = chunk_end[chunk];
   const uint32_t* h_cfi  = (const uint32_t*)back->host;
-  const float*    h_corr = (const float*)(back->host + b_cfi);
-  const DciCand*  h_cand = (const DciCand*)(back->host + b_cfi + b_corr);
-  host_parallel_for(n, 128, [&](uint32_t b, uint32_t e) { // subframes are independent
-    for (uint32_t i = b; i < e; i++) {
+  const float*    h_corr = (const float*)(back->host + b_cfi_);
+  const DciCand*  h_cand = (const DciCand*)(back->host + b_cfi_ + b_corr_);
+  host_parallel_for(e - b, 128, [&](uint32_t lo, uint32_t hi) { // subframes are independent
+    for (uint32_t i = b + lo; i < b + hi; i++) {
       const uint32_t cfi = h_cfi[i];
       res[i].cfi         = cfi;
       res[i].cfi_corr    = std::max({0.f, h_corr[3 * i], h_corr[3 * i + 1], h_corr[3 * i + 2]});
@@ -169,7 +205,7 @@ int CtrlState::run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, con
   });
   if (prof)
     fprintf(stderr, "[mi355 host] control stage: blind-search replay %.1f us for %u subframes\n",
-            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tr0).count(), n);
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tr0).count(), e - b);
   return MI355_SUCCESS;
 }
 

@@ -27,12 +27,24 @@ struct CtrlState {
   std::unordered_map<uint64_t, BlindJob> plans; // search plan per (rnti, subframe, UE configuration)
   std::vector<BlindJob>                  plan_of; // this call's plan per subframe
 
+  // launch(): the arena layout and the per-chunk completion events of the pending call
+  size_t                b_cfi_ = 0, b_corr_ = 0;
+  std::vector<uint32_t> chunk_end;
+  std::vector<hipEvent_t> ev;
+
   ~CtrlState();
   int init(const mi355_cell_t& c, uint32_t nof_rx);
   // PCFICH + PDCCH LLRs + blind decoding of n subframes on s, then the blind-search replay (synchronous).
   // Noise per subframe from host_noise[i] or, when host_noise is null, from device memory d_noise[i].
   int run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, const float* d_noise, const uint16_t* rntis,
           const mi355_ue_dl_cfg_t* cfgs, uint32_t n, hipStream_t s, mi355_ctrl_res_t* res, mi355_dci_msg_t* msgs);
+  // run() in two halves: launch() enqueues the kernels and read-backs of n subframes in nchunks consecutive chunks
+  // (one completion event each); finish(c) waits for chunk c only and replays its blind searches, so the host
+  // works on chunk c while the GPU runs the later chunks (and whatever the caller enqueued after them)
+  int launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, const float* d_noise, const uint16_t* rntis,
+             const mi355_ue_dl_cfg_t* cfgs, uint32_t n, uint32_t nchunks, hipStream_t s);
+  int finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_cfg_t* cfgs, mi355_ctrl_res_t* res,
+             mi355_dci_msg_t* msgs);
 };
 
 } // namespace mi355

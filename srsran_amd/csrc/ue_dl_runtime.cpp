@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <functional>
 #include <cmath>
 #include <stdlib.h>
 #include <mutex>
@@ -624,10 +625,10 @@ static int ctrl_ready(mi355_ue_dl_t* q)
 
 // search results -> srslte_dci_dl_t (srslte_dci_msg_unpack_pdsch with the UE's DCI configuration, ue_dl.c:722-728)
 static int unpack_all(mi355_ue_dl_t* q, const mi355_dl_sf_cfg_t* sfs, const mi355_ue_dl_cfg_t* cfgs, uint32_t n,
-                      mi355_ctrl_res_t* ctrl, std::vector<mi355_dci_msg_t>& msgs, mi355_dci_dl_t* dci)
+                      mi355_ctrl_res_t* ctrl, std::vector<mi355_dci_msg_t>& msgs, mi355_dci_dl_t* dci, uint32_t first = 0)
 {
-  host_parallel_for(n, 128, [&](uint32_t b, uint32_t e) {
-    for (uint32_t i = b; i < e; i++) {
+  host_parallel_for(n - first, 128, [&](uint32_t b, uint32_t e) {
+    for (uint32_t i = first + b; i < first + e; i++) {
       for (int k = 0; k < ctrl[i].nof_dci; k++) {
         mi355_dci_msg_t& m = msgs[(size_t)i * MI355_MAX_DCI_MSG + k];
         if (mi355_dci_msg_unpack_pdsch(&q->cell, &sfs[i], &cfgs[i].dci, &m, &dci[(size_t)i * MI355_MAX_DCI_MSG + k]))
@@ -688,81 +689,129 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   std::vector<mi355_dci_msg_t> msgs((size_t)njobs * MI355_MAX_DCI_MSG);
   for (uint32_t i = 0; i < njobs; i++) rntis[i] = cfgs[i].rnti;
   const auto t1 = now();
-  r = q->ctrl->run(sfjobs, nullptr, d_noise, rntis.data(), ue_cfgs, njobs, s, ctrl, msgs.data());
-  const auto t2 = now();
-  if (r) {
+  // Two chunks: the host replays chunk 0's blind searches and builds its grants while the GPU decodes chunk 1's
+  // control channels, and does chunk 1's while the GPU decodes chunk 0's PDSCH (its DL-SCH wait hook), so the GPU
+  // never waits for the host's sequential find -> grant order.  Every subframe's outcome is the same as in one
+  // chunk: subframes are independent.
+  const uint32_t nchunks = njobs >= 256 ? 2u : 1u;
+  if ((r = q->ctrl->launch(sfjobs, nullptr, d_noise, rntis.data(), ue_cfgs, njobs, nchunks, s))) {
     chest_fill_cb(&fill);
     return r;
   }
-  for (uint32_t i = 0; i < njobs; i++) sfs[i].cfi = ctrl[i].cfi;
-  if ((r = unpack_all(q, sfs, ue_cfgs, njobs, ctrl, msgs, dci))) return r;
-  // DCI -> grant, RV from the SFN for format 1C, softbuffer reset (ue_dl.c:1494-1535)
-  std::vector<mi355_pdsch_job_t> jobs;
-  std::vector<uint32_t>          which, rs_sb, rs_tbs;
-  host_parallel_for(njobs, 128, [&](uint32_t b, uint32_t e) { // grants: independent per subframe
-    for (uint32_t i = b; i < e; i++) {
-      if (ctrl[i].nof_dci != 1) continue; // the reference decodes only when exactly one DCI was found
-      const mi355_dci_dl_t& d = dci[(size_t)i * MI355_MAX_DCI_MSG];
-      if (mi355_ra_dl_dci_to_grant(&q->cell, &sfs[i], ue_cfgs[i].tm, ue_cfgs[i].use_tbs_index_alt, &d, &cfgs[i].grant)) {
-        ctrl[i].nof_dci = -1; // "Error unpacking DCI"
-        continue;
-      }
-      for (int tb = 0; tb < MI355_MAX_CODEWORDS; tb++) {
-        mi355_ra_tb_t& t = cfgs[i].grant.tb[tb];
-        if (t.enabled && (int32_t)t.rv < 0) {
-          const uint32_t k = ((sfs[i].tti / 10) / 2) % 4;
-          t.rv             = ((uint32_t)ceilf(1.5f * k)) % 4;
+  struct Chunk {
+    uint32_t                       b = 0, e = 0;
+    std::vector<mi355_pdsch_job_t> jobs;
+    std::vector<uint32_t>          which, rs_sb, rs_tbs;
+    int                            r = MI355_SUCCESS;
+  };
+  std::vector<Chunk> ck(nchunks);
+  // srslte_ue_dl_find_dl_dci + DCI -> grant, RV from the SFN for format 1C, softbuffer reset list (ue_dl.c:1494-1535)
+  auto prepare = [&](uint32_t c) {
+    Chunk& C = ck[c];
+    C.b      = c ? q->ctrl->chunk_end[c - 1] : 0;
+    C.e      = q->ctrl->chunk_end[c];
+    if ((C.r = q->ctrl->finish(c, rntis.data(), ue_cfgs, ctrl, msgs.data()))) return;
+    for (uint32_t i = C.b; i < C.e; i++) sfs[i].cfi = ctrl[i].cfi;
+    if ((C.r = unpack_all(q, sfs, ue_cfgs, C.e, ctrl, msgs, dci, C.b))) return;
+    host_parallel_for(C.e - C.b, 128, [&](uint32_t lo, uint32_t hi) { // grants: independent per subframe
+      for (uint32_t i = C.b + lo; i < C.b + hi; i++) {
+        if (ctrl[i].nof_dci != 1) continue; // the reference decodes only when exactly one DCI was found
+        const mi355_dci_dl_t& d = dci[(size_t)i * MI355_MAX_DCI_MSG];
+        if (mi355_ra_dl_dci_to_grant(&q->cell, &sfs[i], ue_cfgs[i].tm, ue_cfgs[i].use_tbs_index_alt, &d, &cfgs[i].grant)) {
+          ctrl[i].nof_dci = -1; // "Error unpacking DCI"
+          continue;
+        }
+        for (int tb = 0; tb < MI355_MAX_CODEWORDS; tb++) {
+          mi355_ra_tb_t& t = cfgs[i].grant.tb[tb];
+          if (t.enabled && (int32_t)t.rv < 0) {
+            const uint32_t k = ((sfs[i].tti / 10) / 2) % 4;
+            t.rv             = ((uint32_t)ceilf(1.5f * k)) % 4;
+          }
         }
       }
+    });
+    for (uint32_t i = C.b; i < C.e; i++) {
+      if (ctrl[i].nof_dci != 1) continue;
+      for (int tb = 0; tb < MI355_MAX_CODEWORDS; tb++) {
+        const mi355_ra_tb_t& t = cfgs[i].grant.tb[tb];
+        if (!t.enabled) continue;
+        C.rs_sb.push_back(cfgs[i].softbuffer[tb]);
+        C.rs_tbs.push_back((uint32_t)t.tbs);
+      }
+      mi355_pdsch_job_t j;
+      memset(&j, 0, sizeof(j));
+      j.sf             = sfs[i];
+      j.cfg            = cfgs[i];
+      for (uint32_t a = 0; a < q->nof_rx; a++) {
+        j.sf_symbols[a] = sfjobs[i].sf_symbols[a];
+        for (uint32_t p = 0; p < q->cell.nof_ports; p++) j.ce[p][a] = sfjobs[i].ce[p][a];
+      }
+      j.payload[0] = payloads[2 * i];
+      j.payload[1] = payloads[2 * i + 1];
+      for (int tb = 0; tb < 2; tb++) res[2 * i + tb].crc = 0;
+      C.jobs.push_back(j);
+      C.which.push_back(i);
     }
-  });
-  for (uint32_t i = 0; i < njobs; i++) {
-    if (ctrl[i].nof_dci != 1) continue;
-    for (int tb = 0; tb < MI355_MAX_CODEWORDS; tb++) {
-      const mi355_ra_tb_t& t = cfgs[i].grant.tb[tb];
-      if (!t.enabled) continue;
-      rs_sb.push_back(cfgs[i].softbuffer[tb]);
-      rs_tbs.push_back((uint32_t)t.tbs);
-    }
-    mi355_pdsch_job_t j;
-    memset(&j, 0, sizeof(j));
-    j.sf             = sfs[i];
-    j.cfg            = cfgs[i];
-    for (uint32_t a = 0; a < q->nof_rx; a++) {
-      j.sf_symbols[a] = sfjobs[i].sf_symbols[a];
-      for (uint32_t p = 0; p < q->cell.nof_ports; p++) j.ce[p][a] = sfjobs[i].ce[p][a];
-    }
-    j.payload[0] = payloads[2 * i];
-    j.payload[1] = payloads[2 * i + 1];
-    for (int tb = 0; tb < 2; tb++) res[2 * i + tb].crc = 0;
-    jobs.push_back(j);
-    which.push_back(i);
-  }
-  const auto t3 = now();
-  // every subframe decodes (the usual case): the equaliser reads the device noise estimates and srslte_chest_dl_res_t
-  // is filled on the host while the DL-SCH runs; otherwise the host values are needed first
-  const bool all = jobs.size() == njobs;
-  if (!all) {
+  };
+  prepare(0);
+  const auto t2 = now();
+  if (ck[0].r) {
     chest_fill_cb(&fill);
-    for (size_t k = 0; k < jobs.size(); k++) jobs[k].noise_estimate = chest[which[k]].noise_estimate;
+    return ck[0].r;
   }
-  if (jobs.empty()) return MI355_SUCCESS;
-  if ((r = mi355_softbuffer_reset_tbs_batch(pool, rs_sb.data(), rs_tbs.data(), (uint32_t)rs_sb.size(), s))) return r;
-  std::vector<mi355_pdsch_res_t> sub(2 * jobs.size());
-  for (size_t k = 0; k < jobs.size(); k++) sub[2 * k] = res[2 * which[k]], sub[2 * k + 1] = res[2 * which[k] + 1];
-  r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), (uint32_t)jobs.size(), sub.data(), s,
-                                   all ? d_noise : nullptr, all ? WaitHook{chest_fill_cb, &fill} : WaitHook{},
-                                   chest_cfg->estimator_alg == MI355_ESTIMATOR_ALG_AVERAGE);
-  if (all) {
-    CHECK_HIP(hipStreamSynchronize(q->side));
-    if (!fill.done) chest_fill_cb(&fill);
+  const bool ce_inv = chest_cfg->estimator_alg == MI355_ESTIMATOR_ALG_AVERAGE;
+  struct Hook {
+    std::function<void()> fn;
+    bool                  ran = false;
+    static void call(void* p)
+    {
+      Hook* h = (Hook*)p;
+      if (!h->ran) h->fn();
+      h->ran = true;
+    }
+  };
+  for (uint32_t c = 0; c < nchunks && !r; c++) {
+    Chunk& C = ck[c];
+    if (C.r) {
+      r = C.r;
+      break;
+    }
+    // every subframe of the chunk decodes (the usual case): the equaliser reads the device noise estimates;
+    // otherwise the host values of srslte_chest_dl_res_t are needed first
+    const bool all = C.jobs.size() == C.e - C.b;
+    if (!all) {
+      chest_fill_cb(&fill);
+      for (size_t k = 0; k < C.jobs.size(); k++) C.jobs[k].noise_estimate = chest[C.which[k]].noise_estimate;
+    }
+    Hook h{[&] {
+      if (c + 1 < nchunks) {
+        prepare(c + 1);
+      } else {
+        chest_fill_cb(&fill);
+      }
+    }};
+    if (C.jobs.empty()) {
+      Hook::call(&h);
+      continue;
+    }
+    if ((r = mi355_softbuffer_reset_tbs_batch(pool, C.rs_sb.data(), C.rs_tbs.data(), (uint32_t)C.rs_sb.size(), s))) {
+      Hook::call(&h);
+      break;
+    }
+    std::vector<mi355_pdsch_res_t> sub(2 * C.jobs.size());
+    for (size_t k = 0; k < C.jobs.size(); k++) sub[2 * k] = res[2 * C.which[k]], sub[2 * k + 1] = res[2 * C.which[k] + 1];
+    r = pdsch_decode_batch_dev_noise(q->pdsch, pool, C.jobs.data(), (uint32_t)C.jobs.size(), sub.data(), s,
+                                     all ? d_noise + C.b : nullptr, WaitHook{Hook::call, &h}, ce_inv);
+    for (size_t k = 0; k < C.jobs.size(); k++) res[2 * C.which[k]] = sub[2 * k], res[2 * C.which[k] + 1] = sub[2 * k + 1];
+    Hook::call(&h); // no DL-SCH work in the chunk: the decode did not run the hook
   }
-  for (size_t k = 0; k < jobs.size(); k++) res[2 * which[k]] = sub[2 * k], res[2 * which[k] + 1] = sub[2 * k + 1];
+  CHECK_HIP(hipStreamSynchronize(q->side));
+  if (!fill.done) chest_fill_cb(&fill);
+  const auto t3 = now();
   if (prof) {
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-    fprintf(stderr, "[mi355 host] find_and_decode: launch ofdm/chest %.1f us, control stage (incl. sync + replay) "
-                    "%.1f us, fill/unpack/grants %.1f us, pdsch+dlsch %.1f us\n", us(t0, t1), us(t1, t2), us(t2, t3),
-            us(t3, now()));
+    fprintf(stderr, "[mi355 host] find_and_decode: launch ofdm/chest %.1f us, control launch + chunk 0 replay/grants "
+                    "%.1f us, pdsch+dlsch (chunk 1 host work hidden) %.1f us\n", us(t0, t1), us(t1, t2), us(t2, t3));
   }
   return r;
 }
