@@ -272,8 +272,10 @@ def load_pmc(ncb: int):
 def tdec_roofline(ms, launches, ncb, K):
     """Roofline of the MAP half-iteration kernel (tdec_win_halfit) from HIP-event timing on its stream.
     Primary (schema) entry: HBM against SURVEY 8(d)'s compulsory bytes, 37,848 B per CB per 8-half-iteration
-    decode (= 4,731 B per CB half-iteration).  The kernel is VALU-bound, so roofline_valu gives the
-    binding fraction: SURVEY's ~537.5 k int16 ops per CB half-iteration against 78.6 T ops/s."""
+    decode (= 4,731 B per CB half-iteration); roofline_valu: SURVEY's ~537.5 k int16 ops per CB half-iteration
+    against 78.6 T ops/s.  What actually binds is HBM on the kernel's REAL traffic (both passes read the inputs, beta
+    checkpoints are written and read back: DESIGN.md 4.1, profiles/r02f_mapexp): traffic_frac = PMC bytes per launch
+    / launch time / peak, reported when the PMC summary matches the kernel sources."""
     avg = ms / max(launches, 1)
     bytes_launch = SURVEY_BYTES_PER_CB_DECODE / 8 * ncb * K / 6144
     achieved = bytes_launch / (avg / 1e3) / 1e9
@@ -288,11 +290,13 @@ def tdec_roofline(ms, launches, ncb, K):
             "algorithmic_bytes_source": "SURVEY 8(d): 37,848 B per CB per decode / 8 half-iterations",
             "design_bytes_per_launch": int(design_bytes),
             "design_frac": round(design_bytes / (avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-            "cbs_per_launch": ncb, "binding_roof": "valu (roofline_valu)"}
+            "cbs_per_launch": ncb, "binding_roof": "hbm on the real traffic (traffic_frac)"}
     if why:
         roof["traffic_note"] = why
     else:
         roof["traffic_source"] = f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc.get('tag')}): 2 x FETCH_SIZE + WRITE_SIZE"
+        roof["traffic_gbs"] = round(traffic / (avg / 1e3) / 1e9, 1)
+        roof["traffic_frac"] = round(traffic / (avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
     ops = SURVEY_OPS_PER_CB_HALFIT * ncb * K / 6144
     rate = ops / (avg / 1e3) / 1e12
     valu = {"bound": "valu", "achieved": round(rate, 2), "peak": round(VALU_PEAK_I16_TOPS, 1),

@@ -27,6 +27,8 @@ struct TdecWinArgs {
   int             ncb, L, Lp, nseg, n, write_d;
   uint8_t*        dec;  // optional (L % 8 == 0): decision bytes written directly, D not written
   size_t          dec_stride;
+  const uint32_t* gS;   // microbenchmarks only (GI builds): wave-group interleaved systematic / parity
+  const uint32_t* gP;
 };
 
 struct TdecDecideArgs {

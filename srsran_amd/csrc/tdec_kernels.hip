@@ -145,22 +145,36 @@ __device__ __forceinline__ void set_minf(v2s s[8])
 #ifndef TDEC_WAVES_PER_EU
 #define TDEC_WAVES_PER_EU 2
 #endif
+#ifndef TDEC_NPH
+#define TDEC_NPH 1
+#endif
 // OUTK: what the half-iteration emits besides the extrinsic (compile time, so the forward loop has no per-step
 // branches): 0 nothing, 1 decision bytes (a.dec: DEC1 from registers, DEC2 through an LDS bitmap), 2 the decision
 // LLRs D (the decide kernel packs them)
-template <int NSB, int SEG, int MODE, int DIAG = 0, bool FULL = false, int OUTK = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_PER_EU))) void tdec_win_halfit(TdecWinArgs a)
+// The body works on global lane index gl (the kernel below passes its own; tools/microbench drives it from kernels
+// that give different workgroups different roles).
+//
+// TX (16-window code blocks, L % 8 == 0, 16-byte aligned buffers, all 8 code blocks of the wave unfinished): the
+// softbuffer-layout streams are not read as 4-byte words (one 32-byte piece of 8 code blocks' rows per load
+// instruction) but as 16-byte pieces: lane i loads piece k = 2*(i>>4) + (i&1) of the 128-byte block (4 steps x 8
+// lanes) of code block (i>>1)&7, so one wave instruction reads 8 whole 128-byte lines.  Stored to LDS in lane order,
+// that 1 KB is exactly [step][64 lanes] (lane q = cbg*8 + l finds step s at word 64*s + q, one bank per lane), so the
+// transposition costs one ds_write_b128 per 4 steps and one ds_read_b32 per step.
+template <int NSB, int SEG, int MODE, int DIAG, bool FULL, int OUTK, bool GI = false, bool TX = false>
+__device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl)
 {
   constexpr int NL = NSB / 2;
   constexpr int G  = 64 / NL;
-  const int     gl = blockIdx.x * blockDim.x + threadIdx.x;
+  static_assert(!TX || (NSB == 16 && FULL && SEG == 8), "TX loads need 8-lane rows and whole 8-step segments");
   // the wave's group index is wave-uniform: readfirstlane keeps it (and every per-group base pointer) in SGPRs,
   // so stores address as SGPR base + 32-bit lane offset instead of per-lane 64-bit arithmetic
   const int     grp = __builtin_amdgcn_readfirstlane(gl >> 6), q = gl & 63;
   const int     cbg = q / NL, l = q % NL;
-  if (grp * G + cbg >= a.ncb) return;
+  if constexpr (!TX) { // (TX waves are launched only when all their code blocks are unfinished)
+    if (grp * G + cbg >= a.ncb) return;
+    if (a.done && a.done[grp * G + cbg]) return; // CRC early stop: this code block is finished
+  }
   if (a.remaining && *a.remaining == 0) return;  // every code block of the batch has finished
-  if (a.done && a.done[grp * G + cbg]) return; // CRC early stop: this code block is finished
 
   const int  L = a.L, Lp = a.Lp, nseg = a.nseg;
   constexpr bool dec2   = MODE == 2;
@@ -176,11 +190,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
   const size_t    bidx = a.in_idx ? a.in_idx[cb] : (size_t)cb;
   const uint32_t* in32 = (const uint32_t*)(a.in + bidx * a.in_stride);
   const size_t    wg0  = (size_t)grp * Lp * 64 + q;
-  const uint32_t* X    = dec2 ? a.E + wg0 : in32 + l;
-  const int       xs   = dec2 ? 64 : NL;
-  const uint32_t* Y    = in32 + (dec2 ? (K + 32) : (K + 32) / 2) + l;
+  // GI (microbenchmarks only): systematic and parity read from wave-group interleaved copies (a.gS, a.gP)
+  const uint32_t* X    = dec2 ? a.E + wg0 : (GI ? a.gS + wg0 : in32 + l);
+  const int       xs   = (dec2 || GI) ? 64 : NL;
+  const uint32_t* Y    = GI ? a.gP + wg0 : in32 + (dec2 ? (K + 32) : (K + 32) / 2) + l;
+  const int       ys   = GI ? 64 : NL;
   const uint32_t* AP   = a.A1 + wg0;
   uint32_t*       ck   = a.ckpt + (size_t)grp * nseg * 8 * 64 + q;
+
+  // TX: this lane's 16-byte piece of the code block it loads for (not its own), and the wave's transposition buffers
+  const uint4*    txin  = nullptr;
+  if constexpr (TX) {
+    const int txc = grp * G + ((q >> 1) & 7);
+    txin = (const uint4*)(a.in + (a.in_idx ? (size_t)a.in_idx[txc] : (size_t)txc) * a.in_stride) + (2 * (q >> 4) + (q & 1));
+  }
+  const int       txoX  = 0;                                          // systematic stream, uint4 units
+  const int       txoY  = (dec2 ? (L * NSB + 32) : (L * NSB + 32) / 2) / 4; // parity stream (P1 for DEC2, else P0)
+  uint32_t*       txb   = nullptr;
+  if constexpr (TX) {
+    __shared__ uint32_t tx_lds[4][2][SEG * 64];
+    txb = &tx_lds[threadIdx.x >> 6][0][0];
+  }
+  // 8 steps j0..j0+7 of a softbuffer stream as two 16-byte pieces
+  auto tx_load = [&](int so, int j0, uint32_t* r) {
+    const uint4 v0 = txin[so + j0 * 2], v1 = txin[so + (j0 + 4) * 2];
+    r[0] = v0.x; r[1] = v0.y; r[2] = v0.z; r[3] = v0.w;
+    r[4] = v1.x; r[5] = v1.y; r[6] = v1.z; r[7] = v1.w;
+  };
+  // the lane's own words of those 8 steps (buffer b of the wave)
+  auto tx_unpack = [&](int b, const uint32_t* r, uint32_t* o) {
+    uint32_t* w = txb + b * SEG * 64;
+    ((uint4*)w)[q]      = make_uint4(r[0], r[1], r[2], r[3]);
+    ((uint4*)w)[64 + q] = make_uint4(r[4], r[5], r[6], r[7]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < SEG; i++) o[i] = w[64 * i + q];
+  };
 
   v2s st[8], nw[8], aw[8];
 
@@ -196,7 +243,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
     for (int i = 0; i < 8; i++) {
       const int j = (L - TDEC_WARMUP) + 8 * b + i;
       xo[i]       = X[j * xs];
-      yo[i]       = Y[j * NL];
+      yo[i]       = Y[j * ys];
       if constexpr (has_ap) ao[i] = AP[j * 64];
     }
 #pragma unroll
@@ -225,7 +272,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
     for (int i = 0; i < 8; i++) {
       const int j = 8 * b + i;
       xo[i]       = X[j * xs];
-      yo[i]       = Y[j * NL];
+      yo[i]       = Y[j * ys];
       if constexpr (has_ap) ao[i] = AP[j * 64];
     }
 #pragma unroll
@@ -257,17 +304,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
   }
   // ckpt[nseg-1] = row L (not normalised)
 #pragma unroll
-  for (int s = 0; s < 8; s++) ck[((size_t)(nseg - 1) * 8 + s) * 64] = W(st[s]);
+  for (int s = 0; s < 8; s++) {
+    if constexpr (DIAG == 9) {
+      __builtin_nontemporal_store(W(st[s]), &ck[((size_t)(nseg - 1) * 8 + s) * 64]);
+    } else if constexpr (DIAG != 5 && DIAG != 7) {
+      ck[((size_t)(nseg - 1) * 8 + s) * 64] = W(st[s]);
+    }
+  }
 
   // ------------------------------------------------ backward pass: main, one checkpoint per segment
   {
     uint32_t cx[SEG], cy[SEG], ca[SEG] = {};
     auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap) {
+      if constexpr (TX) { // raw 16-byte pieces, transposed when the segment is consumed
+        if constexpr (!dec2) tx_load(txoX, t * SEG, x);
+        tx_load(txoY, t * SEG, y);
+      }
 #pragma unroll
       for (int i = 0; i < SEG; i++) {
         const int j = FULL ? t * SEG + i : min(t * SEG + i, L - 1); // clamp the ragged last segment
-        x[i]        = X[j * xs];
-        y[i]        = Y[j * NL];
+        if constexpr (!TX || dec2) x[i] = X[j * xs];
+        if constexpr (!TX) y[i] = Y[j * ys];
         if constexpr (has_ap) ap[i] = AP[j * 64];
       }
     };
@@ -276,8 +333,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
     uint32_t bx[SEG], by[SEG], ba[SEG] = {}, dx[SEG], dy[SEG], da[SEG] = {};
     load(nseg - 1, cx, cy, ca);
     if (nseg > 1) load(nseg - 2, bx, by, ba);
-    auto seg = [&](int t, const uint32_t* sx, const uint32_t* sy, const uint32_t* sa, uint32_t* lx, uint32_t* ly,
+    auto seg = [&](int t, const uint32_t* rx, const uint32_t* ry, const uint32_t* sa, uint32_t* lx, uint32_t* ly,
                    uint32_t* la) {
+      uint32_t sx[SEG], sy[SEG];
+      if constexpr (TX) {
+        if constexpr (!dec2) tx_unpack(0, rx, sx);
+        tx_unpack(1, ry, sy);
+      }
+#pragma unroll
+      for (int i = 0; i < SEG; i++) {
+        if constexpr (!TX || dec2) sx[i] = rx[i];
+        if constexpr (!TX) sy[i] = ry[i];
+      }
       if (t > 1) load(t - 2, lx, ly, la);
 #pragma unroll
       for (int i = SEG - 1; i >= 0; i--) {
@@ -292,9 +359,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
           beta_step<true>(st, x, U(sy[i]), nw);
 #pragma unroll
           for (int s = 0; s < 8; s++) st[s] = nw[s];
-          if (i == 0 && t > 0 && DIAG != 3) {
+          if (i == 0 && t > 0 && DIAG != 3 && DIAG != 5 && DIAG != 7) {
 #pragma unroll
-            for (int s = 0; s < 8; s++) ck[((size_t)(t - 1) * 8 + s) * 64] = W(st[s]);
+            for (int s = 0; s < 8; s++) {
+              if constexpr (DIAG == 9) {
+                __builtin_nontemporal_store(W(st[s]), &ck[((size_t)(t - 1) * 8 + s) * 64]);
+              } else if constexpr (DIAG == 10) { // every other checkpoint only
+                if (t & 1) ck[((size_t)(t - 1) * 8 + s) * 64] = W(st[s]);
+              } else if constexpr (DIAG == 11 || (DIAG >= 100 && (DIAG & 4))) { // into group 0's region (cache resident)
+                a.ckpt[q + ((size_t)(t - 1) * 8 + s) * 64] = W(st[s]);
+              } else {
+                ck[((size_t)(t - 1) * 8 + s) * 64] = W(st[s]);
+              }
+            }
           }
           if ((i & 1) == 0 && k != 0) normalize<true>(st);
         }
@@ -345,18 +422,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
     }
   }
 
+  // DIAG 5: no checkpoint traffic (stores skipped, rows read from group 0's, cache resident); DIAG 6: the forward
+  // pass reads its inputs from code block / group 0 (cache resident) -- bounds on what removing either would gain
+  // (DIAG >= 100: bit 0 = 6, bit 1 = 8, bit 2 = 11, combined)
+  constexpr bool  FI  = DIAG == 6 || (DIAG >= 100 && (DIAG & 1));
+  const uint32_t* Xf  = FI ? (dec2 ? a.E + q : (const uint32_t*)a.in + l) : X;
+  const uint32_t* Yf  = FI ? (const uint32_t*)a.in + (dec2 ? (K + 32) : (K + 32) / 2) + l : Y;
+  const uint32_t* APf = FI ? a.A1 + q : AP;
+  // (7: stores skipped, rows read from the own region; 8: stores kept, rows read from group 0's; 9: non-temporal
+  // checkpoint stores)
+  const uint32_t* ckf = (DIAG == 5 || DIAG == 8 || (DIAG >= 100 && (DIAG & 2))) ? a.ckpt + q : ck;
   uint32_t cx[SEG], cy[SEG], ca[SEG] = {}, cd[SEG], cc[8];
   auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap, uint32_t* d, uint32_t* c) {
+    if constexpr (TX) {
+      if constexpr (!dec2) tx_load(txoX, t * SEG, x);
+      tx_load(txoY, t * SEG, y);
+    }
 #pragma unroll
     for (int i = 0; i < SEG; i++) {
       const int j = FULL ? t * SEG + i : min(t * SEG + i, L - 1); // clamp the ragged last segment
-      x[i]        = X[j * xs];
-      y[i]        = Y[j * NL];
-      if constexpr (has_ap) ap[i] = AP[j * 64];
+      if constexpr (!TX || dec2) x[i] = Xf[j * xs];
+      if constexpr (!TX) y[i] = Yf[j * ys];
+      if constexpr (has_ap) ap[i] = APf[j * 64];
       d[i]        = tab[(size_t)j * NL];
     }
 #pragma unroll
-    for (int s = 0; s < 8; s++) c[s] = ck[((size_t)t * 8 + s) * 64];
+    for (int s = 0; s < 8; s++) c[s] = ckf[((size_t)t * 8 + s) * 64];
   };
   load(0, cx, cy, ca, cd, cc);
   uint32_t dbits = 0; // decision bits of the previous (even) segment, bits 16..31
@@ -364,8 +455,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
   // segment t is processed from one register set while segment t+1 loads into the other; the loop is unrolled
   // twice so the two sets swap roles by position instead of being copied
   uint32_t nx[SEG], ny[SEG], na[SEG] = {}, nd[SEG], nc[8];
-  auto fseg = [&](int t, const uint32_t* cx, const uint32_t* cy, const uint32_t* ca, const uint32_t* cd,
+  auto fseg = [&](int t, const uint32_t* rx, const uint32_t* ry, const uint32_t* ca, const uint32_t* cd,
                   const uint32_t* cc, uint32_t* nx, uint32_t* ny, uint32_t* na, uint32_t* nd, uint32_t* nc) {
+    uint32_t cx[SEG], cy[SEG];
+    if constexpr (TX) {
+      if constexpr (!dec2) tx_unpack(0, rx, cx);
+      tx_unpack(1, ry, cy);
+    }
+#pragma unroll
+    for (int i = 0; i < SEG; i++) {
+      if constexpr (!TX || dec2) cx[i] = rx[i];
+      if constexpr (!TX) cy[i] = ry[i];
+    }
     const int s0 = t * SEG;
     const int e  = FULL ? s0 + SEG : ((s0 + SEG < L) ? s0 + SEG : L);
     uint32_t  bits = 0; // decision bits of the segment: window 2l in bits 8..15, 2l+1 in 0..7 (MSB first)
@@ -386,15 +487,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
     // Beta rows s0+1 .. e are rebuilt from the checkpoint (row e) in two halves so that only 4 rows
     // are live at a time (the upper half is recomputed twice): phase A keeps rows 1..4 for alpha
     // steps 0..3, phase B rows 5..8 for alpha steps 4..7.
+    // (TDEC_NPH = 1: all 8 rows live, one pass -- 32 more VGPRs, 2 fewer beta steps per segment)
     static_assert(SEG == 8, "two-phase recompute assumes 8-row segments");
-    v2s ck8[8], cur[8], R[4][8];
+    constexpr int NPH = TDEC_NPH, RP = 8 / NPH;
+    v2s ck8[8], cur[8], R[RP][8];
 #pragma unroll
     for (int s = 0; s < 8; s++) ck8[s] = U(cc[s]);
     const bool ck_norm = (e & 1) == 0 && e != L;
 
 #pragma unroll
-    for (int ph = 0; ph < 2; ph++) {
-      const int lo = ph ? 5 : 1; // rows kept in this phase: lo .. lo+3
+    for (int ph = 0; ph < NPH; ph++) {
+      const int lo = 1 + ph * RP; // rows kept in this phase: lo .. lo+RP-1
 #pragma unroll
       for (int s = 0; s < 8; s++) cur[s] = ck8[s];
       if (ck_norm) normalize<true>(cur);
@@ -402,7 +505,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
       for (int i = SEG; i >= lo; i--) {
         const int j = s0 + i;
         if (FULL ? i == SEG : j == e) {
-          if (i <= lo + 3) {
+          if (i <= lo + RP - 1) {
 #pragma unroll
             for (int s = 0; s < 8; s++) R[i - lo][s] = ck8[s];
           }
@@ -411,7 +514,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
           beta_step<true>(cur, xin[i], U(cy[i]), row);
 #pragma unroll
           for (int s = 0; s < 8; s++) cur[s] = row[s];
-          if (i <= lo + 3) {
+          if (i <= lo + RP - 1) {
 #pragma unroll
             for (int s = 0; s < 8; s++) R[i - lo][s] = row[s];
           }
@@ -420,7 +523,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
       }
       // alpha steps lo-1 .. lo+2 with outputs
 #pragma unroll
-      for (int ii = 0; ii < 4; ii++) {
+      for (int ii = 0; ii < RP; ii++) {
         const int i = lo - 1 + ii;
         const int j = s0 + i;
       if (FULL ? i < SEG : j < e) {
@@ -446,8 +549,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
         if constexpr (!dec2) {
           // e = ext1 - app1 (wrapping), turbodecoder_iter.h:118-120 of the next DEC2
           const v2s ev = has_ap ? out - U(ca[i]) : out;
-          E16[olo]     = ev.x;
-          E16[ohi]     = ev.y;
+          if constexpr (DIAG != 12) {
+            E16[olo] = ev.x;
+            E16[ohi] = ev.y;
+          }
           if constexpr (wr_d) WG_AT(a.D, j) = W(out);
           bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
         } else {
@@ -501,6 +606,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
       for (int w = l; w < K / 64; w += NL) o[w] = make_uint2(bm[2 * w], bm[2 * w + 1]);
     }
   }
+}
+
+// TX: waves whose 8 code blocks are all unfinished take the 16-byte-load path (the others, at the ragged end of
+// the batch or after some CRC early stops, the 4-byte one)
+template <int NSB, int SEG, int MODE, int DIAG = 0, bool FULL = false, int OUTK = 0, bool TX = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_PER_EU))) void tdec_win_halfit(TdecWinArgs a)
+{
+  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (TX) {
+    const int  cb  = (gl >> 6) * (128 / NSB) + (gl & 63) / (NSB / 2);
+    const bool act = cb < a.ncb && !(a.done && a.done[cb]);
+    if (__builtin_amdgcn_ballot_w64(act) == ~0ull) {
+      tdec_win_body<NSB, SEG, MODE, DIAG, FULL, OUTK, false, true>(a, gl);
+      return;
+    }
+  }
+  tdec_win_body<NSB, SEG, MODE, DIAG, FULL, OUTK>(a, gl);
 }
 
 // ---------------------------------------------------------------------------- layout kernels
@@ -581,17 +703,42 @@ static size_t diag_lds()
   return (size_t)m;
 }
 
-template <int NSB, int DIAG, bool FULL, int OUTK>
-static void launch_mode_o(int mode, int blocks, const TdecWinArgs& a, hipStream_t s)
+template <int NSB, int DIAG, bool FULL, int OUTK, bool TX = false>
+static void launch_mode_t(int mode, int blocks, const TdecWinArgs& a, hipStream_t s)
 {
   const size_t lds = diag_lds();
   if (mode == 0) {
-    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 0, DIAG, FULL, OUTK>), dim3(blocks), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 0, DIAG, FULL, OUTK, TX>), dim3(blocks), dim3(256), lds, s, a);
   } else if (mode == 1) {
-    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 1, DIAG, FULL, OUTK>), dim3(blocks), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 1, DIAG, FULL, OUTK, TX>), dim3(blocks), dim3(256), lds, s, a);
   } else {
-    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 2, DIAG, FULL, OUTK>), dim3(blocks), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((tdec_win_halfit<NSB, TDEC_SEG, 2, DIAG, FULL, OUTK, TX>), dim3(blocks), dim3(256), lds, s, a);
   }
+}
+
+// MI355_TDEC_TX=0 (A/B timing): never take the 16-byte-load path
+static bool tx_enabled()
+{
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("MI355_TDEC_TX");
+    m             = e ? atoi(e) != 0 : 1;
+  }
+  return m != 0;
+}
+
+template <int NSB, int DIAG, bool FULL, int OUTK>
+static void launch_mode_o(int mode, int blocks, const TdecWinArgs& a, hipStream_t s)
+{
+  // 16-byte pieces need every code block's buffer (and so the stream offsets, multiples of 16 bytes for these K)
+  // 16-byte aligned
+  if constexpr (NSB == 16 && FULL && DIAG == 0) {
+    if (tx_enabled() && (uintptr_t)a.in % 16 == 0 && (a.in_stride * sizeof(int16_t)) % 16 == 0 && (a.L * 16 + 32) % 16 == 0) {
+      launch_mode_t<NSB, DIAG, FULL, OUTK, true>(mode, blocks, a, s);
+      return;
+    }
+  }
+  launch_mode_t<NSB, DIAG, FULL, OUTK>(mode, blocks, a, s);
 }
 
 template <int NSB, int DIAG, bool FULL = false>
