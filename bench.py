@@ -844,7 +844,7 @@ def make_cb_pool(K, n, ebno, seed):
     nsb = 16 if (K > 800 and K % 16 == 0) else (8 if (K > 400 and K % 8 == 0) else 0)
     assert nsb, "tdec workload uses the windowed layout"
     Lw = K // nsb
-    stride = 3 * (K + 32) + 12
+    stride = tdec_stride(K)
     pool = np.zeros((n, stride), np.int16)
     sigma = 10 ** (-(ebno + 10 * np.log10(1 / 3)) / 20)
     m = np.arange(K)
@@ -861,11 +861,17 @@ def make_cb_pool(K, n, ebno, seed):
     return pool
 
 
+def tdec_stride(K):
+    """int16 per code-block buffer of the tdec workload: the windowed layout (3 (K+32) + 12) rounded up to 8, so
+    every buffer is 16-byte aligned as the softbuffer pool's are (the MAP kernel's 16-byte loads need it)."""
+    return (3 * (K + 32) + 12 + 7) // 8 * 8
+
+
 def run_tdec(args, world, rank, local, pg):
     from srsran_amd import lib
     from srsran_amd.tdec import DeviceBuffer, TdecBatch
     K, nh, ncb = args.K, args.nhalf, args.ncb
-    stride = 3 * (K + 32) + 12
+    stride = tdec_stride(K)
     pool = make_cb_pool(K, args.pool, args.ebno, seed=shard_seed(rank))
     host = np.ascontiguousarray(np.tile(pool, (ncb // args.pool + 1, 1))[:ncb])
     d_in = DeviceBuffer(host.nbytes, local).upload(host)

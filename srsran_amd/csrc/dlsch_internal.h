@@ -48,6 +48,7 @@ struct DlschRmArgs {
   size_t          sb_stride;
   const uint8_t*  sb_crc;
   uint8_t*        fresh;  // per slot: buffer logically zero (lazy srslte_softbuffer_rx_reset)
+  uint32_t        fold2;  // LDS pairs: >= max over the launch's code blocks of min(n_e, N) / 2 (0: N / 2)
 };
 
 // 8-bit rate dematching (srslte_rm_turbo_rx_lut_8bit into (int8_t*)softbuffer->buffer_f[cb], sch.c:403-407):

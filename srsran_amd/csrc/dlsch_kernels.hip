@@ -17,9 +17,11 @@ namespace mi355 {
 // independent) -- no atomics, no scattered stores.  A slot marked fresh by the lazy reset is written whole
 // (sums or zeros) instead of read, which is srslte_softbuffer_rx_reset + the first accumulation in one pass.
 // One workgroup per code block: the CB's LLRs are folded modulo N into LDS (coalesced reads, wrap-around
-// sums for E > N), then the decoder buffer is written in order from LDS gathers.
+// sums for E > N), then the decoder buffer is written in order from LDS gathers.  The LDS image is sized to the
+// launch's largest min(E, N) (a.fold2 pairs), not N: at the usual code rates E is a third of N, so four code blocks
+// (512-thread workgroups) are in flight per CU instead of two.
 constexpr uint32_t RM_LDS     = 3 * 6144 + 12; // N of the largest code block
-constexpr uint32_t RM_THREADS = 1024;
+constexpr uint32_t RM_THREADS = 512;
 constexpr int      RM_Q       = (3 * (6144 + 32) + 12 + 8 * RM_THREADS - 1) / (8 * RM_THREADS); // buffer quads per thread
 constexpr int      RM_EQ      = (RM_LDS + 8 * RM_THREADS - 1) / (8 * RM_THREADS);             // LLR quads per thread
 constexpr int      RM_CPB     = 1;                                                              // code blocks per workgroup
@@ -50,9 +52,9 @@ __device__ __forceinline__ uint32_t ld_llr_pair(const int16_t* e, uint32_t r2, b
 // even and the LLRs are handled as int16 pairs.
 __global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
 {
-  __shared__ __attribute__((aligned(16))) uint32_t acc32[RM_LDS / 2 + 4];
+  extern __shared__ __attribute__((aligned(16))) uint32_t acc32[]; // a.fold2 pairs
   const uint16_t* acc   = (const uint16_t*)acc32;
-  const uint32_t  N     = a.N, tid = threadIdx.x, N2 = N / 2;
+  const uint32_t  N     = a.N, tid = threadIdx.x, N2 = min(N / 2, a.fold2);
   const uint32_t  pairs = a.buflen / 2;
   uint4           iv[RM_Q];
   uint32_t        iv_rv = 0xffffffffu;
@@ -360,7 +362,10 @@ hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s)
 {
   if (a.ncb <= 0) return hipSuccess;
   if (a.N > RM_LDS) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(dlsch_rm_rx, dim3((unsigned)((a.ncb + RM_CPB - 1) / RM_CPB)), dim3(RM_THREADS), 0, s, a);
+  DlschRmArgs b = a;
+  b.fold2       = (a.fold2 && a.fold2 < a.N / 2) ? a.fold2 : a.N / 2;
+  const size_t lds = (size_t)((b.fold2 + 3) & ~3u) * 4;
+  hipLaunchKernelGGL(dlsch_rm_rx, dim3((unsigned)((a.ncb + RM_CPB - 1) / RM_CPB)), dim3(RM_THREADS), lds, s, b);
   hipLaunchKernelGGL(dlsch_rm_consume, dim3((unsigned)((a.ncb + 255) / 256)), dim3(256), 0, s, a.desc, a.ncb, a.fresh,
                      a.sb_crc);
   return hipGetLastError();

@@ -434,6 +434,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
   std::vector<TbDesc>                        tbd(ntb);
   std::vector<std::pair<uint32_t, uint32_t>> kcount; // (K, code blocks) in first-seen order; few distinct K
   std::vector<uint32_t>                      rvmask; // per group: redundancy versions present
+  std::vector<uint32_t>                      fold2;  // per group: LDS pairs of the rate dematcher
   auto group_of = [&](uint32_t K) {
     for (uint32_t i = 0; i < kcount.size(); i++)
       if (kcount[i].first == K) return i;
@@ -480,12 +481,20 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     d.nof_e_bits = in.nof_e_bits;
     d.rv         = in.rv;
     d.e_off      = in.e_offset;
+    // the largest E of the TB's code blocks (sch.c:391-401: Qm * (G' / C), +Qm for the last gamma), for the rate
+    // dematcher's LDS image (min(E, N) per code block)
+    const uint32_t emax = in.Qm * (in.nof_e_bits / in.Qm / seg.C + 1);
+    auto           fold = [&](uint32_t g, uint32_t K) {
+      if (fold2.size() <= g) fold2.resize(g + 1, 0);
+      fold2[g] = std::max(fold2[g], std::min(emax, 3 * K + 12) / 2);
+    };
     if (seg.C1) {
       const uint32_t g = group_of(seg.K1);
       grp[2 * t]       = (uint8_t)g;
       d.cb_base[0]     = kcount[g].second;
       kcount[g].second += seg.C1;
       rvmask[g] |= 1u << in.rv;
+      fold(g, seg.K1);
     }
     if (seg.C > seg.C1) {
       const uint32_t g = group_of(seg.K2);
@@ -493,6 +502,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
       d.cb_base[1]     = kcount[g].second;
       kcount[g].second += seg.C - seg.C1;
       rvmask[g] |= 1u << in.rv;
+      fold(g, seg.K2);
     }
   }
   std::vector<uint32_t> goff(kcount.size());
@@ -610,6 +620,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     ra.sb        = pool->buf;
     ra.sb_stride = SB_STRIDE;
     ra.sb_crc    = pool->cb_crc;
+    ra.fold2     = gi < fold2.size() ? fold2[gi] : 0;
     CHECK_HIP(dlsch_launch_rm(ra, s));
     auto it = q->dec.find(K);
     if (it == q->dec.end()) {

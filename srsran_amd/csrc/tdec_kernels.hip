@@ -408,11 +408,13 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   constexpr bool  wr_bits = !dec2 && OUTK == 1; // fused decision bytes (DEC1: ext1 in natural order)
   constexpr bool  wr_bm   = dec2 && OUTK == 1;  // fused decision bytes (DEC2: app1 de-interleaved)
   constexpr bool  wr_d    = OUTK == 2;
-  // DEC2 decisions land at scattered natural positions (row j' of windows wlo/whi), so they are collected
-  // as a bitmap of the code block in LDS (K/8 bytes, byte order of the output) and stored at the end
-  constexpr int BMW = NSB == 16 ? 192 : 25; // u32 words per code block (K <= 6144 / K <= 800)
+  // The decision bytes are collected in LDS as the code block's K/8 output bytes and stored at the end with 8-byte
+  // stores: DEC2's land at scattered natural positions (row j' of windows wlo/whi) as a bitmap, DEC1's are one byte
+  // per window and segment (narrow scattered global stores of either cost 15-25 % of the launch).  193 words per
+  // code block (not 192): the 8 code blocks of a wave start in different banks.
+  constexpr int BMW = NSB == 16 ? 193 : 25; // u32 words per code block (K <= 6144 / K <= 800)
   uint32_t*     bm  = nullptr;
-  if constexpr (dec2) {
+  if constexpr (dec2 || wr_bits) {
     __shared__ uint32_t bm_lds[4 * G * BMW];
     bm = bm_lds + ((threadIdx.x >> 6) * G + cbg) * BMW;
     if constexpr (wr_bm) {
@@ -450,7 +452,6 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     for (int s = 0; s < 8; s++) c[s] = ckf[((size_t)t * 8 + s) * 64];
   };
   load(0, cx, cy, ca, cd, cc);
-  uint32_t dbits = 0; // decision bits of the previous (even) segment, bits 16..31
 
   // segment t is processed from one register set while segment t+1 loads into the other; the loop is unrolled
   // twice so the two sets swap roles by position instead of being copied
@@ -470,8 +471,6 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     const int s0 = t * SEG;
     const int e  = FULL ? s0 + SEG : ((s0 + SEG < L) ? s0 + SEG : L);
     uint32_t  bits = 0; // decision bits of the segment: window 2l in bits 8..15, 2l+1 in 0..7 (MSB first)
-    if (wr_bits && (t & 1)) bits = dbits;
-    (void)dbits;
     if (t + 1 < nseg) load(t + 1, nx, ny, na, nd, nc);
 
     v2s xin[SEG];
@@ -576,20 +575,9 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     }
     }
     if constexpr (wr_bits) { // turbodecoder_win.h:973-993: bit = LLR > 0, natural order, MSB first
-      // two segments per store: bytes t-1, t of each window as one 16-bit word (the segment of an odd t
-      // lands in the high byte); a trailing even segment is stored alone
-      if ((t & 1) || t + 1 == nseg) {
-        uint8_t* o = a.dec + (size_t)cb * a.dec_stride + (size_t)(2 * l) * (L / 8) + (t & ~1);
-        if (t & 1) {
-          *(uint16_t*)o           = (uint16_t)(((bits >> 8) & 0xffu) << 8 | ((bits >> 24) & 0xffu));
-          *(uint16_t*)(o + L / 8) = (uint16_t)((bits & 0xffu) << 8 | ((bits >> 16) & 0xffu));
-        } else {
-          o[0]     = (uint8_t)(bits >> 8);
-          o[L / 8] = (uint8_t)bits;
-        }
-      } else {
-        dbits = bits << 16; // keep segment t (even) in the upper half for the next segment's store
-      }
+      uint8_t* bb = (uint8_t*)bm + (size_t)(2 * l) * (L / 8) + t;
+      bb[0]       = (uint8_t)(bits >> 8);
+      bb[L / 8]   = (uint8_t)bits;
     }
   };
 #pragma unroll 1
@@ -597,14 +585,12 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     fseg(t, cx, cy, ca, cd, cc, nx, ny, na, nd, nc);
     if (t + 1 < nseg) fseg(t + 1, nx, ny, na, nd, nc, cx, cy, ca, cd, cc);
   }
-  if constexpr (dec2) {
-    if constexpr (wr_bm) { // the code block's K/8 decision bytes, 8-byte stores by its NL lanes
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      uint2* o = (uint2*)(a.dec + (size_t)cb * a.dec_stride);
-      for (int w = l; w < K / 64; w += NL) o[w] = make_uint2(bm[2 * w], bm[2 * w + 1]);
-    }
+  if constexpr (wr_bm || wr_bits) { // the code block's K/8 decision bytes, 8-byte stores by its NL lanes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint2* o = (uint2*)(a.dec + (size_t)cb * a.dec_stride);
+    for (int w = l; w < K / 64; w += NL) o[w] = make_uint2(bm[2 * w], bm[2 * w + 1]);
   }
 }
 
