@@ -171,6 +171,19 @@ int main(int argc, char** argv)
       float c7 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 107, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
       float c6 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 106, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
       printf("DEC1 cached: fwd inputs + ckpt loads %.4f, + ckpt stores %.4f, ckpt loads + stores %.4f ms\n", c3, c7, c6);
+      {
+        uint8_t* dec;
+        CK(hipMalloc(&dec, (size_t)ncb * (K / 8)));
+        TdecWinArgs o = args(0, ncb);
+        o.dec        = dec;
+        o.dec_stride = K / 8;
+        float d20 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 2, 0, true, 0, true>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
+        float d21 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 2, 0, true, 1, true>), dim3(blocks(ncb)), dim3(256), 0, s1, o); }, 10);
+        float d00 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 0, 0, true, 0, true>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
+        float d01 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 0, 0, true, 1, true>), dim3(blocks(ncb)), dim3(256), 0, s1, o); }, 10);
+        printf("decision output: DEC2 none %.4f, bitmap %.4f ms; DEC1 (n=0) none %.4f, bytes %.4f ms\n", d20, d21, d00, d01);
+        CK(hipFree(dec));
+      }
       printf("16-byte transposed loads: DEC1 %.4f ms (4-byte %.4f), DEC2 %.4f ms (4-byte %.4f)\n", tx1, to1, tx2, to2);
     }
     // sequential pair on one stream for comparison
