@@ -57,10 +57,14 @@ static int fft_plan_init(struct fft_plan* P, uint32_t N)
   return 0;
 }
 
-static void fft_plan_free(struct fft_plan* P)
+/* a * b as libgcc's __mulsc3 computes it for finite operands (ac - bd, ad + bc), inline */
+static inline cfl cmul(cfl a, cfl b)
 {
-  for (uint32_t s = 0; s < P->nstage; s++) free(P->tw[s]);
+  const float ar = crealf(a), ai = cimagf(a), br = crealf(b), bi = cimagf(b);
+  return (ar * br - ai * bi) + I * (ar * bi + ai * br);
 }
+/* a * -i */
+static inline cfl mul_mi(cfl a) { return cimagf(a) - I * crealf(a); }
 
 /* x -> X (natural order, no scaling); y: work buffer of N.  Returns the buffer holding the result. */
 static cfl* fft_run(const struct fft_plan* P, cfl* x, cfl* y)
@@ -76,20 +80,20 @@ static cfl* fft_run(const struct fft_plan* P, cfl* x, cfl* y)
         if (r == 4) {
           const cfl a0 = x[q + s * p], a1 = x[q + s * (p + m)], a2 = x[q + s * (p + 2 * m)],
                     a3 = x[q + s * (p + 3 * m)];
-          const cfl b0 = a0 + a2, b1 = a0 - a2, b2 = a1 + a3, b3 = (a1 - a3) * -I;
+          const cfl b0 = a0 + a2, b1 = a0 - a2, b2 = a1 + a3, b3 = mul_mi(a1 - a3);
           y[q + s * (4 * p + 0)] = b0 + b2;
-          y[q + s * (4 * p + 1)] = (b1 + b3) * w[1];
-          y[q + s * (4 * p + 2)] = (b0 - b2) * w[2];
-          y[q + s * (4 * p + 3)] = (b1 - b3) * w[3];
+          y[q + s * (4 * p + 1)] = cmul(b1 + b3, w[1]);
+          y[q + s * (4 * p + 2)] = cmul(b0 - b2, w[2]);
+          y[q + s * (4 * p + 3)] = cmul(b1 - b3, w[3]);
         } else if (r == 2) {
           const cfl a0 = x[q + s * p], a1 = x[q + s * (p + m)];
           y[q + s * (2 * p + 0)] = a0 + a1;
-          y[q + s * (2 * p + 1)] = (a0 - a1) * w[1];
+          y[q + s * (2 * p + 1)] = cmul(a0 - a1, w[1]);
         } else {
           const cfl a0 = x[q + s * p], a1 = x[q + s * (p + m)], a2 = x[q + s * (p + 2 * m)];
           y[q + s * (3 * p + 0)] = a0 + a1 + a2;
-          y[q + s * (3 * p + 1)] = (a0 + a1 * w3 + a2 * conjf(w3)) * w[1];
-          y[q + s * (3 * p + 2)] = (a0 + a1 * conjf(w3) + a2 * w3) * w[2];
+          y[q + s * (3 * p + 1)] = cmul(a0 + cmul(a1, w3) + cmul(a2, conjf(w3)), w[1]);
+          y[q + s * (3 * p + 2)] = cmul(a0 + cmul(a1, conjf(w3)) + cmul(a2, w3), w[2]);
         }
       }
     }
@@ -112,12 +116,31 @@ static uint32_t symbol_sz(uint32_t nof_prb)
 
 /* srslte_ofdm_rx_sf (ofdm.c:392-471), normal CP: per slot 7 symbols at cp0 + l (N + cp1), FFT-shifted without
  * DC, no normalisation.  iq: 15 N complex; grid: 14 x 12 nof_prb complex. */
+/* one plan per transform size, built once (FFTW plans are likewise made once per srslte_ofdm_t) */
+static struct fft_plan plans[6];
+static int             plan_ok[6];
+static pthread_mutex_t plan_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static const struct fft_plan* plan_for(uint32_t N)
+{
+  static const uint32_t sizes[6] = {128, 256, 384, 768, 1024, 1536};
+  int k = -1;
+  for (int i = 0; i < 6; i++)
+    if (sizes[i] == N) k = i;
+  if (k < 0) return NULL;
+  if (__atomic_load_n(&plan_ok[k], __ATOMIC_ACQUIRE)) return &plans[k];
+  pthread_mutex_lock(&plan_mu);
+  if (!plan_ok[k] && !fft_plan_init(&plans[k], N)) __atomic_store_n(&plan_ok[k], 1, __ATOMIC_RELEASE);
+  pthread_mutex_unlock(&plan_mu);
+  return plan_ok[k] ? &plans[k] : NULL;
+}
+
 int orc_ofdm_rx_sf(const float* iq, uint32_t nof_prb, float* grid)
 {
   const uint32_t N = symbol_sz(nof_prb);
   if (!N) return -1;
-  struct fft_plan P;
-  if (fft_plan_init(&P, N)) return -1;
+  const struct fft_plan* P = plan_for(N);
+  if (!P) return -1;
   const uint32_t cp0 = (uint32_t)ceilf(160.0f * (float)N / 2048.0f), cp1 = (uint32_t)ceilf(144.0f * (float)N / 2048.0f);
   const uint32_t nre = 12 * nof_prb, slot = 15 * N / 2;
   cfl*           a   = malloc(sizeof(cfl) * N);
@@ -127,13 +150,12 @@ int orc_ofdm_rx_sf(const float* iq, uint32_t nof_prb, float* grid)
   for (uint32_t sym = 0; sym < 14; sym++) {
     const uint32_t sl = sym / 7, l = sym % 7;
     memcpy(a, &in[sl * slot + cp0 + l * (N + cp1)], sizeof(cfl) * N);
-    const cfl* X = fft_run(&P, a, b);
+    const cfl* X = fft_run(P, a, b);
     memcpy(&out[sym * nre], &X[N - nre / 2], sizeof(cfl) * (nre / 2));
     memcpy(&out[sym * nre + nre / 2], &X[1], sizeof(cfl) * (nre / 2));
   }
   free(a);
   free(b);
-  fft_plan_free(&P);
   return 0;
 }
 

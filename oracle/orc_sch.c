@@ -15,6 +15,7 @@
  * decoder and CRC it calls are pinned against the compiled reference through tests/golden/.
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -77,16 +78,34 @@ void orc_rm_turbo_table(uint32_t K, uint32_t rv, uint16_t* table)
   }
 }
 
+/* The tables are built once per (K, rv) and kept, as the reference's srslte_rm_turbo_gentables() does
+ * (rm_turbo.c:717-822): immutable once published, so readers need no lock. */
+static uint16_t* volatile rm_tabs[188][4]; /* 188 LTE code-block sizes (36.212 Table 5.1.3-3) */
+static pthread_mutex_t    rm_tabs_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static const uint16_t* rm_table_cached(uint32_t K, uint32_t rv)
+{
+  const int ci = orc_cb_index(K);
+  uint16_t* t  = rm_tabs[ci][rv];
+  if (t) return t;
+  pthread_mutex_lock(&rm_tabs_mu);
+  if (!(t = rm_tabs[ci][rv])) {
+    t = malloc(sizeof(uint16_t) * (3 * K + 12));
+    orc_rm_turbo_table(K, rv, t);
+    __atomic_store_n(&rm_tabs[ci][rv], t, __ATOMIC_RELEASE);
+  }
+  pthread_mutex_unlock(&rm_tabs_mu);
+  return t;
+}
+
 int orc_rm_turbo_rx(const int16_t* in, uint32_t in_len, int16_t* out, uint32_t K, uint32_t rv)
 {
   if (orc_cb_index(K) < 0 || rv > 3) return -2;
-  const uint32_t N = 3 * K + 12;
-  uint16_t*      t = malloc(sizeof(uint16_t) * N);
-  orc_rm_turbo_table(K, rv, t);
+  const uint32_t  N = 3 * K + 12;
+  const uint16_t* t = rm_table_cached(K, rv);
   for (uint32_t i = 0; i < in_len; i++) {
     out[t[i % N]] = (int16_t)(uint16_t)((unsigned)(uint16_t)out[t[i % N]] + (unsigned)(uint16_t)in[i]);
   }
-  free(t);
   return 0;
 }
 
