@@ -17,3 +17,14 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture(autouse=True)
+def _fault_tracebacks(request):
+    """The HIP runtime installs its own SIGSEGV handler when it initialises, replacing faulthandler's: re-arm
+    faulthandler before every GPU test, so a host crash prints the Python stack of every thread."""
+    if request.node.get_closest_marker("gpu") is not None:
+        import faulthandler
+
+        faulthandler.enable(all_threads=True)
+    yield

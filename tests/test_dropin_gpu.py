@@ -63,8 +63,11 @@ def _caller():
     L.caller_tdec_run_all.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_int)]
     L.caller_ue_dl.argtypes = [C.POINTER(CallerCfg), C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                C.POINTER(SfRes)]
+    # (c, tti, cfi, grant, grid, ce, noise, ncalls, rvs, payload, crc_out, its_out): every pointer declared -- an
+    # undeclared trailing argument is passed as a 32-bit C int and truncates the address
     L.caller_pdsch_decode.argtypes = [C.POINTER(CallerCfg), C.c_uint32, C.c_uint32, C.POINTER(Grant), C.c_void_p,
-                                      C.c_void_p, C.c_float, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+                                      C.c_void_p, C.c_float, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p]
     return L
 
 

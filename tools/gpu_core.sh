@@ -2,7 +2,7 @@
 # the GPU suite up to 3 times; on a host crash, a backtrace from the core file (tools/core_rip.py)
 mkdir -p gpurun_out/fl
 ulimit -c unlimited
-for i in 1 2 3; do
+for i in 1 2 3 4 5 6 7 8; do
   rm -f core core.*
   timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/fl/suite$i.log 2>&1
   rc=$?
