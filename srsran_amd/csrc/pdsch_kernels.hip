@@ -831,7 +831,10 @@ __global__ __launch_bounds__(256) void pdsch_csimax_cols(const PdschJobDev* __re
   }
 }
 
-constexpr int FU_P = 1; // RE pairs per thread
+#ifndef PDSCH_FU_P
+#define PDSCH_FU_P 1
+#endif
+constexpr int FU_P = PDSCH_FU_P; // RE pairs per thread
 
 // grid (pair blocks of the largest job, jobs): work item = RE pair (2pr, 2pr+1), the granule of the LLR kernel.
 // One instantiation per (layer-0, layer-1) modulation order pair present in the batch (0: layer not decoded);

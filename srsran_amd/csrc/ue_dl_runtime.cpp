@@ -693,7 +693,10 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   // control channels, and does chunk 1's while the GPU decodes chunk 0's PDSCH (its DL-SCH wait hook), so the GPU
   // never waits for the host's sequential find -> grant order.  Every subframe's outcome is the same as in one
   // chunk: subframes are independent.
-  const uint32_t nchunks = njobs >= 256 ? 2u : 1u;
+  // (MI355_UEDL_CHUNKS = 1..8 overrides the choice: A/B timing)
+  static const int chunk_env = getenv("MI355_UEDL_CHUNKS") ? atoi(getenv("MI355_UEDL_CHUNKS")) : 0;
+  const uint32_t   nchunks   = chunk_env >= 1 && chunk_env <= 8 ? std::max(1u, std::min((uint32_t)chunk_env, njobs))
+                                                                 : (njobs >= 256 ? 2u : 1u);
   if ((r = q->ctrl->launch(sfjobs, nullptr, d_noise, rntis.data(), ue_cfgs, njobs, nchunks, s))) {
     chest_fill_cb(&fill);
     return r;
