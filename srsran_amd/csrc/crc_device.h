@@ -40,6 +40,55 @@ __device__ __forceinline__ uint32_t crc24_bytes(const uint8_t* p, uint32_t n, co
   return crc;
 }
 
+// slice-by-4: t4[k][x] = the CRC register after byte x followed by k zero bytes (t4[0] = the byte table), so four
+// bytes fold with four independent lookups, s' = t4[3][s2 ^ b0] ^ t4[2][s1 ^ b1] ^ t4[1][s0 ^ b2] ^ t4[0][b3]
+// (s2 s1 s0: the register's bytes, MSB first; 24 < 32, so nothing of s survives the shift).  The byte chain of a
+// lane's chunk becomes a word chain a quarter as long.  t4[1..3] are derived from t4[0] by the caller.
+__device__ __forceinline__ uint32_t crc24_step_table(uint32_t v, const uint32_t* t0)
+{
+  return ((v << 8) ^ t0[(v >> 16) & 0xff]) & 0xffffffu;
+}
+
+__device__ __forceinline__ uint32_t crc24_words(const uint8_t* p, uint32_t n, const uint32_t (*t4)[256])
+{
+  uint32_t crc = 0, i = 0;
+  if (((uintptr_t)p & 3) == 0) {
+    const uint32_t nw = n / 4;
+    uint32_t       w[4];
+    for (; i + 16 <= 4 * nw; i += 16) { // 4 words loaded together, independently of the fold
+#pragma unroll
+      for (int k = 0; k < 4; k++) w[k] = ((const uint32_t*)(p + i))[k];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t v = w[k];
+        crc = t4[3][((crc >> 16) ^ v) & 0xff] ^ t4[2][((crc >> 8) ^ (v >> 8)) & 0xff] ^
+              t4[1][(crc ^ (v >> 16)) & 0xff] ^ t4[0][v >> 24];
+      }
+    }
+    for (; i + 4 <= 4 * nw; i += 4) {
+      const uint32_t v = *(const uint32_t*)(p + i);
+      crc = t4[3][((crc >> 16) ^ v) & 0xff] ^ t4[2][((crc >> 8) ^ (v >> 8)) & 0xff] ^ t4[1][(crc ^ (v >> 16)) & 0xff] ^
+            t4[0][v >> 24];
+    }
+  }
+  for (; i < n; i++) crc = ((crc << 8) ^ t4[0][((crc >> 16) & 0xff) ^ p[i]]) & 0xffffffu;
+  return crc;
+}
+
+// wave CRC as wave_crc24_scaled, with slice-by-4 tables
+__device__ __forceinline__ uint32_t wave_crc24_scaled4(const uint8_t* bytes, uint32_t nbytes, const uint32_t (*t4)[256],
+                                                       uint32_t poly, const uint32_t* scale)
+{
+  const int      lane  = threadIdx.x & 63;
+  const uint32_t chunk = (nbytes + 63) / 64;
+  const uint32_t b0    = min(nbytes, lane * chunk), b1 = min(nbytes, b0 + chunk);
+  uint32_t       crc   = crc24_words(bytes + b0, b1 - b0, t4);
+  crc                  = gf2_mulmod24(crc, scale[lane], poly);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
+  return crc;
+}
+
 // wave CRC with the per-lane scale factors x^(8*after) precomputed for this byte count (scale[lane])
 __device__ __forceinline__ uint32_t wave_crc24_scaled(const uint8_t* bytes, uint32_t nbytes, const uint32_t* tl,
                                                       uint32_t poly, const uint32_t* scale)

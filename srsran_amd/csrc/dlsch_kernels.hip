@@ -165,18 +165,24 @@ __device__ __forceinline__ void flag_set(uint32_t* f)
 __global__ __launch_bounds__(1024) void dlsch_cb_check(DlschCheckArgs a)
 {
   __shared__ uint32_t unfinished;
-  __shared__ uint32_t tl[2][256]; // CRC24A | CRC24B tables
+  __shared__ uint32_t tl[2][4][256]; // CRC24A | CRC24B slice-by-4 tables
   if (threadIdx.x == 0) unfinished = 0;
   if (a.ncb && *a.remaining == 0) return; // uniform: every code block has finished
-  if (threadIdx.x < 512) tl[threadIdx.x >> 8][threadIdx.x & 255] = (threadIdx.x < 256 ? a.crc24a : a.crc24b)->t[threadIdx.x & 255];
+  const uint32_t ti = threadIdx.x & 255, tt = (threadIdx.x >> 8) & 1;
+  if (threadIdx.x < 512) tl[tt][0][ti] = (tt ? a.crc24b : a.crc24a)->t[ti];
   __syncthreads();
+#pragma unroll
+  for (int k = 1; k < 4; k++) { // one more zero byte per table
+    if (threadIdx.x < 512) tl[tt][k][ti] = crc24_step_table(tl[tt][k - 1][ti], tl[tt][0]);
+    __syncthreads();
+  }
   const int b    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (b < a.ncb && *a.remaining != 0 && !a.done[b]) {
     const CbDesc&  d   = a.desc[b];
     const uint8_t* dec = a.dec + (size_t)b * a.dec_stride;
-    const uint32_t crc = wave_crc24_scaled(dec, a.K / 8, tl[d.C > 1 ? 1 : 0], d.C > 1 ? a.crc24b->poly : a.crc24a->poly,
-                                           a.scale + (d.C > 1 ? 64 : 0));
+    const uint32_t crc = wave_crc24_scaled4(dec, a.K / 8, tl[d.C > 1 ? 1 : 0], d.C > 1 ? a.crc24b->poly : a.crc24a->poly,
+                                            a.scale + (d.C > 1 ? 64 : 0));
     const bool     ok  = crc == 0;
     const bool     fin = ok || a.h + 1 == a.max_its;
     if (!fin) {
