@@ -284,11 +284,15 @@ __global__ __launch_bounds__(256) void pdcch_blind(BlindArgs a)
   // rate dematching (rm_conv.c:98-148)
   const uint32_t F = nbits + 16, N = 3 * F;
   const uint32_t nrows = (F - 1) / 32 + 1, Kp = 32 * nrows, ndummy = Kp - F;
+  const float    rcp_rows = 1.0f / (float)nrows;
   for (uint32_t j = lane; j < 3 * Kp; j += 64) S.tmp[j] = RX_NULL;
   uint32_t run = 0;
   for (uint32_t base = 0; base < 3 * Kp; base += 64) {
-    const uint32_t j = base + lane, jj = j % Kp;
-    const bool     v = j < 3 * Kp && (jj % nrows) * 32 + c_perm[jj / nrows] >= ndummy;
+    // jj = j mod Kp and jj = qn * nrows + rn without integer division (j < 3 Kp + 64, jj < 160, nrows <= 5:
+    // (jj + 0.5) / nrows sits at least 0.1 away from an integer, far beyond float rounding)
+    const uint32_t j  = base + lane, jj = j >= 2 * Kp ? j - 2 * Kp : j >= Kp ? j - Kp : j;
+    const uint32_t qn = (uint32_t)(((float)jj + 0.5f) * rcp_rows), rn = jj - qn * nrows;
+    const bool     v  = j < 3 * Kp && rn * 32 + c_perm[qn & 31] >= ndummy;
     const uint64_t m = __ballot(v);
     if (v) S.rank_pos[run + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)j;
     run += __popcll(m);
@@ -334,8 +338,8 @@ __global__ __launch_bounds__(256) void pdcch_blind(BlindArgs a)
                  b2 = par((2 * j) & 0x57u) ? 0xFFFFu : 0u;
   const bool odd = lane & 1u;
   uint32_t   met = 0;
-  for (uint32_t t = 0; t < 3 * F; t++) {
-    const uint32_t o  = 3 * (t % F);
+  // symbol triple of step t, 3 (t mod F), kept incrementally (a scalar division per step is ~40 SALU instructions)
+  for (uint32_t t = 0, o = 0; t < 3 * F; t++, o = (o + 3 == 3 * F) ? 0 : o + 3) {
     const uint32_t s0 = S.q[o], s1 = S.q[o + 1], s2 = S.q[o + 2];
     const uint32_t av = ((b0 ^ s0) + (b1 ^ s1) + 1) >> 1;
     const uint32_t mt = (((b2 ^ s2) + av + 1) >> 1) >> 3, mm = 8191u - mt;
