@@ -307,7 +307,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   for (int s = 0; s < 8; s++) {
     if constexpr (DIAG == 9) {
       __builtin_nontemporal_store(W(st[s]), &ck[((size_t)(nseg - 1) * 8 + s) * 64]);
-    } else if constexpr (DIAG != 5 && DIAG != 7) {
+    } else {
       ck[((size_t)(nseg - 1) * 8 + s) * 64] = W(st[s]);
     }
   }
@@ -359,7 +359,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
           beta_step<true>(st, x, U(sy[i]), nw);
 #pragma unroll
           for (int s = 0; s < 8; s++) st[s] = nw[s];
-          if (i == 0 && t > 0 && DIAG != 3 && DIAG != 5 && DIAG != 7) {
+          if (i == 0 && t > 0 && DIAG != 3) {
 #pragma unroll
             for (int s = 0; s < 8; s++) {
               if constexpr (DIAG == 9) {
@@ -424,16 +424,15 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     }
   }
 
-  // DIAG 5: no checkpoint traffic (stores skipped, rows read from group 0's, cache resident); DIAG 6: the forward
-  // pass reads its inputs from code block / group 0 (cache resident) -- bounds on what removing either would gain
-  // (DIAG >= 100: bit 0 = 6, bit 1 = 8, bit 2 = 11, combined)
+  // Diagnostic builds that keep every computation alive but serve some traffic from cache (bounds on what removing it
+  // would gain): 6 = the forward pass reads its inputs from code block / group 0, 8 = checkpoint rows read from group
+  // 0's region, 11 = checkpoint stores into group 0's region; DIAG >= 100 combines them (bit 0 = 6, 1 = 8, 2 = 11).
+  // 9 = non-temporal checkpoint stores, 10 = every other checkpoint stored.
   constexpr bool  FI  = DIAG == 6 || (DIAG >= 100 && (DIAG & 1));
   const uint32_t* Xf  = FI ? (dec2 ? a.E + q : (const uint32_t*)a.in + l) : X;
   const uint32_t* Yf  = FI ? (const uint32_t*)a.in + (dec2 ? (K + 32) : (K + 32) / 2) + l : Y;
   const uint32_t* APf = FI ? a.A1 + q : AP;
-  // (7: stores skipped, rows read from the own region; 8: stores kept, rows read from group 0's; 9: non-temporal
-  // checkpoint stores)
-  const uint32_t* ckf = (DIAG == 5 || DIAG == 8 || (DIAG >= 100 && (DIAG & 2))) ? a.ckpt + q : ck;
+  const uint32_t* ckf = (DIAG == 8 || (DIAG >= 100 && (DIAG & 2))) ? a.ckpt + q : ck;
   uint32_t cx[SEG], cy[SEG], ca[SEG] = {}, cd[SEG], cc[8];
   auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap, uint32_t* d, uint32_t* c) {
     if constexpr (TX) {
@@ -548,10 +547,8 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
         if constexpr (!dec2) {
           // e = ext1 - app1 (wrapping), turbodecoder_iter.h:118-120 of the next DEC2
           const v2s ev = has_ap ? out - U(ca[i]) : out;
-          if constexpr (DIAG != 12) {
-            E16[olo] = ev.x;
-            E16[ohi] = ev.y;
-          }
+          E16[olo]     = ev.x;
+          E16[ohi]     = ev.y;
           if constexpr (wr_d) WG_AT(a.D, j) = W(out);
           bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
         } else {

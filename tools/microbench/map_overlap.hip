@@ -153,20 +153,16 @@ int main(int argc, char** argv)
       float tx2 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 2, 0, true, 0, true>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
       float to2 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 2, 0, true, 0, false>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
       float to1 = time1([&] { full(s1, 0, ncb); }, 10);
-      float td5 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 5, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
       float td6 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 6, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
-      float te5 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 2, 5, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
       float te6 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 2, 6, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
-      printf("bounds: DEC1 no-checkpoint-traffic %.4f ms, forward inputs cache-resident %.4f ms; DEC2 %.4f / %.4f ms\n", td5, td6, te5, te6);
-      float t7 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 7, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
+      printf("bounds: forward inputs cache-resident: DEC1 %.4f ms, DEC2 %.4f ms\n", td6, te6);
       float t8 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 8, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
       float t9 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 9, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
       float t3 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 3, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
-      printf("DEC1: checkpoint stores skipped %.4f, loads from group 0 %.4f, non-temporal stores %.4f ms; backward without stores %.4f ms\n", t7, t8, t9, t3);
+      printf("DEC1: checkpoint loads from group 0 %.4f, non-temporal stores %.4f ms; backward without stores %.4f ms\n", t8, t9, t3);
       float t10 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 10, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
       float t11 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 11, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
-      float t12 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 12, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
-      printf("DEC1: half the checkpoint stores %.4f, checkpoint stores to group 0 %.4f, extrinsic stores skipped %.4f ms\n", t10, t11, t12);
+      printf("DEC1: half the checkpoint stores %.4f, checkpoint stores to group 0 %.4f ms\n", t10, t11);
       float c3 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 103, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
       float c7 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 107, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
       float c6 = time1([&] { hipLaunchKernelGGL((tdec_win_halfit<16, 8, 1, 106, true, 0>), dim3(blocks(ncb)), dim3(256), 0, s1, args(0, ncb)); }, 10);
