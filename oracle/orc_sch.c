@@ -80,13 +80,13 @@ void orc_rm_turbo_table(uint32_t K, uint32_t rv, uint16_t* table)
 
 /* The tables are built once per (K, rv) and kept, as the reference's srslte_rm_turbo_gentables() does
  * (rm_turbo.c:717-822): immutable once published, so readers need no lock. */
-static uint16_t* volatile rm_tabs[188][4]; /* 188 LTE code-block sizes (36.212 Table 5.1.3-3) */
+static uint16_t*        rm_tabs[188][4]; /* 188 LTE code-block sizes (36.212 Table 5.1.3-3) */
 static pthread_mutex_t    rm_tabs_mu = PTHREAD_MUTEX_INITIALIZER;
 
 static const uint16_t* rm_table_cached(uint32_t K, uint32_t rv)
 {
   const int ci = orc_cb_index(K);
-  uint16_t* t  = rm_tabs[ci][rv];
+  uint16_t* t  = __atomic_load_n(&rm_tabs[ci][rv], __ATOMIC_ACQUIRE);
   if (t) return t;
   pthread_mutex_lock(&rm_tabs_mu);
   if (!(t = rm_tabs[ci][rv])) {
