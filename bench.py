@@ -82,7 +82,7 @@ def parse(argv=None):
     ap.add_argument("--ncb", type=int, default=65536, help="tdec workload: code blocks per GPU per step")
     ap.add_argument("--K", type=int, default=6144)
     ap.add_argument("--nhalf", type=int, default=8)
-    ap.add_argument("--ebno", type=float, default=2.0)
+    ap.add_argument("--ebno", type=float, default=6.0, help="tdec workload Eb/N0 (SURVEY 8(d) config 2: 6.0 and 4.0)")
     ap.add_argument("--pool", type=int, default=256, help="tdec workload: distinct code blocks tiled")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
