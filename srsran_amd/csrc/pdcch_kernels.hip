@@ -201,8 +201,13 @@ __constant__ uint8_t c_perm_inv[32] = {16, 0, 24, 8, 20, 4, 28, 12, 18, 2, 26, 1
                                        17, 1, 25, 9, 21, 5, 29, 13, 19, 3, 27, 11, 23, 7, 31, 15};
 
 struct WaveLds {
-  float    tmp[3 * 32 * 5];   // rate-dematching circular buffer (3 K_pi, K_pi <= 160)
-  uint16_t rank_pos[MAXSYM];  // position of the r-th non-dummy bit in the circular buffer
+  union {
+    struct {
+      float    tmp[3 * 32 * 5];  // rate-dematching circular buffer (3 K_pi, K_pi <= 160)
+      uint16_t rank_pos[MAXSYM]; // position of the r-th non-dummy bit in the circular buffer
+    };
+    uint16_t bm[PDCCH_MAX_F * 8]; // branch metric per (t mod F, encoder output pattern), once the above are dead
+  };
   uint16_t q[MAXSYM];         // quantised soft symbols
   uint64_t dec[MAXSYM + 8];   // decision words per trellis step (bit s: survivor choice of state s)
   uint8_t  bits[PDCCH_MAX_F]; // decoded bits (middle repetition)
@@ -223,6 +228,20 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v)
   for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
   return v;
 }
+
+// lane k of (lo, hi) := the two halves of w (w and k wave-uniform; the lane select goes through M0, one SGPR
+// operand per VALU instruction).  M0 is reserved, so the compiler keeps no value in it across code that does not
+// set it up right before use (nothing else in this file does); clang warns that it does not track the clobber.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void writelane2(uint32_t& lo, uint32_t& hi, uint64_t w, uint32_t k)
+{
+  asm volatile("s_mov_b32 m0, %4\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
+               : "+v"(lo), "+v"(hi)
+               : "s"((uint32_t)w), "s"((uint32_t)(w >> 32)), "s"(k)
+               : "m0");
+}
+#pragma clang diagnostic pop
 
 __device__ __forceinline__ uint32_t par(uint32_t x) { return __builtin_popcount(x) & 1u; }
 
@@ -332,24 +351,37 @@ __global__ __launch_bounds__(256) void pdcch_blind(BlindArgs a)
   }
   for (uint32_t i = lane; i < 8; i += 64) S.dec[3 * F + i] = 0;
   __builtin_amdgcn_wave_barrier();
-  // 64-state Viterbi, lane = state; state s takes predecessors j = s >> 1 and j + 32
-  const uint32_t j  = lane >> 1;
-  const uint32_t b0 = par((2 * j) & 0x6Du) ? 0xFFFFu : 0u, b1 = par((2 * j) & 0x4Fu) ? 0xFFFFu : 0u,
-                 b2 = par((2 * j) & 0x57u) ? 0xFFFFu : 0u;
-  const bool odd = lane & 1u;
-  uint32_t   met = 0;
-  // symbol triple of step t, 3 (t mod F), kept incrementally (a scalar division per step is ~40 SALU instructions)
-  for (uint32_t t = 0, o = 0; t < 3 * F; t++, o = (o + 3 == 3 * F) ? 0 : o + 3) {
-    const uint32_t s0 = S.q[o], s1 = S.q[o + 1], s2 = S.q[o + 2];
-    const uint32_t av = ((b0 ^ s0) + (b1 ^ s1) + 1) >> 1;
-    const uint32_t mt = (((b2 ^ s2) + av + 1) >> 1) >> 3, mm = 8191u - mt;
-    const uint32_t oj = (uint32_t)__shfl((int)met, (int)j, 64), oj32 = (uint32_t)__shfl((int)met, (int)(j + 32), 64);
-    const uint32_t x = (oj + (odd ? mm : mt)) & 0xFFFFu, y = (oj32 + (odd ? mt : mm)) & 0xFFFFu;
-    const bool     d = (int16_t)(uint16_t)(x - y) > 0;
-    met              = d ? y : x;
-    const uint64_t w = __ballot(d);
-    if (lane == 0) S.dec[t] = w;
+  // the branch metric of step t depends only on the symbol triple (t mod F) and the state's encoder output pattern
+  // (8 of them): tabulate it once instead of recomputing it 3 times per trellis step in all 64 lanes
+  for (uint32_t e = lane; e < 8 * F; e += 64) {
+    const uint32_t o = 3 * (e >> 3), pt = e & 7u;
+    const uint32_t c0 = (pt & 1u) ? 0xFFFFu : 0u, c1 = (pt & 2u) ? 0xFFFFu : 0u, c2 = (pt & 4u) ? 0xFFFFu : 0u;
+    const uint32_t av = ((c0 ^ S.q[o]) + (c1 ^ S.q[o + 1]) + 1) >> 1;
+    S.bm[e]           = (uint16_t)((((c2 ^ S.q[o + 2]) + av + 1) >> 1) >> 3);
   }
+  __builtin_amdgcn_wave_barrier();
+  // 64-state Viterbi, lane = state; state s takes predecessors j = s >> 1 and j + 32
+  const uint32_t j   = lane >> 1;
+  const uint32_t pat = par((2 * j) & 0x6Du) | par((2 * j) & 0x4Fu) << 1 | par((2 * j) & 0x57u) << 2;
+  const bool     odd = lane & 1u;
+  const uint32_t Fs  = __builtin_amdgcn_readfirstlane(F); // uniform: the step counters live in scalar registers
+  uint32_t       met = 0;
+  // decision words: step tb + k's ballot goes to lane k of (dlo, dhi), one 64-lane store per 64 steps
+  for (uint32_t tb = 0, o = 0; tb < 3 * Fs; tb += 64) {
+    const uint32_t te  = min(3 * Fs - tb, 64u);
+    uint32_t       dlo = 0, dhi = 0;
+    for (uint32_t k = 0; k < te; k++, o = (o + 1 == Fs) ? 0 : o + 1) {
+      const uint32_t mt = S.bm[8 * o + pat], xa = odd ? 8191u - mt : mt, ya = 8191u - xa;
+      const uint32_t oj = (uint32_t)__shfl((int)met, (int)j, 64), oj32 = (uint32_t)__shfl((int)met, (int)(j + 32), 64);
+      const uint32_t x = oj + xa, y = oj32 + ya; // only the low 16 bits matter (wrapping u16 metrics)
+      const bool     d = (int16_t)(uint16_t)(x - y) > 0;
+      met              = d ? y : x;
+      const uint64_t w = __ballot(d);
+      writelane2(dlo, dhi, w, k);
+    }
+    if (lane < te) S.dec[tb + lane] = (uint64_t)dhi << 32 | dlo;
+  }
+  met &= 0xFFFFu;
   // best end state: the last index of the smallest (unsigned) metric
   const uint32_t key  = wave_min((met << 6) | (63u - lane));
   const uint32_t best = 63u - (key & 63u);
