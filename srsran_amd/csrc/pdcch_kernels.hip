@@ -241,6 +241,10 @@ __device__ __forceinline__ void writelane2(uint32_t& lo, uint32_t& hi, uint64_t 
                : "s"((uint32_t)w), "s"((uint32_t)(w >> 32)), "s"(k)
                : "m0");
 }
+__device__ __forceinline__ void writelane1(uint32_t& v, uint32_t x, uint32_t k)
+{
+  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(x), "s"(k) : "m0");
+}
 #pragma clang diagnostic pop
 
 __device__ __forceinline__ uint32_t par(uint32_t x) { return __builtin_popcount(x) & 1u; }
@@ -368,10 +372,10 @@ __global__ __launch_bounds__(256) void pdcch_blind(BlindArgs a)
   uint32_t       met = 0;
   // decision words: step tb + k's ballot goes to lane k of (dlo, dhi), one 64-lane store per 64 steps
   for (uint32_t tb = 0, o = 0; tb < 3 * Fs; tb += 64) {
-    const uint32_t te  = min(3 * Fs - tb, 64u);
+    const uint32_t te  = __builtin_amdgcn_readfirstlane(min(3 * Fs - tb, 64u));
     uint32_t       dlo = 0, dhi = 0;
     for (uint32_t k = 0; k < te; k++, o = (o + 1 == Fs) ? 0 : o + 1) {
-      const uint32_t mt = S.bm[8 * o + pat], xa = odd ? 8191u - mt : mt, ya = 8191u - xa;
+      const uint32_t mt = (uint16_t)S.bm[8 * o + pat], xa = odd ? 8191u - mt : mt, ya = 8191u - xa;
       const uint32_t oj = (uint32_t)__shfl((int)met, (int)j, 64), oj32 = (uint32_t)__shfl((int)met, (int)(j + 32), 64);
       const uint32_t x = oj + xa, y = oj32 + ya; // only the low 16 bits matter (wrapping u16 metrics)
       const bool     d = (int16_t)(uint16_t)(x - y) > 0;
@@ -384,15 +388,31 @@ __global__ __launch_bounds__(256) void pdcch_blind(BlindArgs a)
   met &= 0xFFFFu;
   // best end state: the last index of the smallest (unsigned) metric
   const uint32_t key  = wave_min((met << 6) | (63u - lane));
-  const uint32_t best = 63u - (key & 63u);
+  const uint32_t best = 63u - ((uint32_t)__builtin_amdgcn_readfirstlane((int)key) & 63u);
+  __builtin_amdgcn_wave_barrier();
+  // chainback over steps 3F-1 .. F (decision word of step n read at n + 6, as the AVX2 traceback) in blocks of 64:
+  // lane k holds the word of step nb-1-k, the survivor state walks through scalar registers by readlane, and the
+  // decoded bits of the middle repetition are stored once per block
+  uint32_t es = best << 2;
+  for (uint32_t nb = 3 * Fs; nb > Fs;) {
+    const uint32_t cnt = min(64u, nb - Fs);
+    const uint64_t v   = lane < cnt ? S.dec[nb - 1 - lane + 6] : 0;
+    const int      vlo = (int)(uint32_t)v, vhi = (int)(uint32_t)(v >> 32);
+    uint32_t       bitv = 0;
+    for (uint32_t k = 0; k < cnt; k++) {
+      const uint32_t sh = es >> 2;
+      const uint64_t w  = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, (int)k) << 32 |
+                         (uint32_t)__builtin_amdgcn_readlane(vlo, (int)k);
+      const uint32_t kb = (uint32_t)(w >> sh) & 1u;
+      es                = (es >> 1) | (kb << 7);
+      writelane1(bitv, kb, k);
+    }
+    const uint32_t n = nb - 1 - lane;
+    if (lane < cnt && n < 2 * Fs) S.bits[n - Fs] = (uint8_t)bitv;
+    nb -= cnt;
+  }
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) {
-    uint32_t es = best << 2;
-    for (uint32_t n = 3 * F; n-- > F;) {
-      const uint32_t kb = (uint32_t)(S.dec[n + 6] >> (es >> 2)) & 1u;
-      es                = (es >> 1) | (kb << 7);
-      if (n < 2 * F) S.bits[n - F] = (uint8_t)kb;
-    }
     uint32_t crc = 0, p = 0;
     for (uint32_t i = 0; i < nbits; i++) {
       const uint32_t fb = ((crc >> 15) ^ S.bits[i]) & 1u;
