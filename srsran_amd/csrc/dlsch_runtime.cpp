@@ -94,6 +94,8 @@ struct mi355_dlsch {
   bool       prof = false;
   HostStaging stage;
   HostStaging back; // pinned read-back of ret | avg
+  hipEvent_t  done_ev    = nullptr; // after the previous batch's epilogue
+  bool        done_armed = false;
 };
 
 static uint32_t rm_buflen(uint32_t K) { return tdec_subblocks(K) ? 3 * (K + 32) + 12 : 3 * K + 12; }
@@ -271,7 +273,8 @@ int mi355_softbuffer_reset_tbs_batch(mi355_softbuffer_pool_t* p, const uint32_t*
     if (sbs[i] >= p->nof_sb) return MI355_ERROR_INVALID_INPUTS;
     l[i] = make_uint2(sbs[i], std::min((tbs[i] + 24) / (6144 - 24) + 1, p->max_cb)); // softbuffer.c:128-132
   }
-  CHECK_HIP(p->st_list.upload(p->d_list, s));
+  // the list buffer is reused by every call: the copy waits for an earlier call's reset kernel on s
+  CHECK_HIP(p->st_list.upload(p->d_list, s, true));
   CHECK_HIP(dlsch_launch_reset_list(p->d_list, n, p->max_cb, p->fresh, p->cb_crc, s));
   return MI355_SUCCESS;
 }
@@ -356,6 +359,7 @@ void mi355_dlsch_destroy(mi355_dlsch_t* q)
   for (auto& kv : q->scales) (void)hipFree(kv.second);
   (void)hipFree(q->crc);
   (void)hipFree(q->scratch);
+  if (q->done_ev) (void)hipEventDestroy(q->done_ev);
   if (q->own) (void)hipStreamDestroy(q->own);
   delete q;
 }
@@ -415,9 +419,30 @@ int mi355_dlsch_decode8_dev(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, con
 
 } // extern "C"
 
+mi355::DlschPending::~DlschPending()
+{
+  if (armed && ev) (void)hipEventSynchronize(ev);
+  if (ev) (void)hipEventDestroy(ev);
+  if (host) (void)hipHostFree(host);
+}
+
+int mi355::DlschPending::collect()
+{
+  if (!armed) return MI355_SUCCESS;
+  armed = false;
+  CHECK_HIP(hipEventSynchronize(ev));
+  memcpy(ret, host, ntb * 4);
+  for (uint32_t t = 0; t < ntb; t++) {
+    if (invalid[t]) ret[t] = MI355_ERROR_INVALID_INPUTS;
+  }
+  if (avg) memcpy(avg, host + avg_off, ntb * 4);
+  return MI355_SUCCESS;
+}
+
 int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const void* d_e_bits,
                                  const mi355_dlsch_tb_t* tbs, uint32_t ntb, uint8_t* d_data, int32_t* ret,
-                                 float* avg_iterations, void* stream, mi355::WaitHook hook, bool llr8)
+                                 float* avg_iterations, void* stream, mi355::WaitHook hook, bool llr8,
+                                 mi355::DlschPending* pend, bool after_s)
 {
   if (!q || !pool || !tbs || !ret || (ntb && !d_e_bits)) return MI355_ERROR_INVALID_INPUTS;
   if (ntb == 0) return MI355_SUCCESS;
@@ -546,7 +571,9 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
   CHECK_HIP(q->stage.reserve(staged));
   q->stage.put(tbd.data(), ntb * sizeof(TbDesc));
   q->stage.zeros(4 * (q->max_its + 1));
-  CHECK_HIP(q->stage.upload(base, s));
+  // after_s: the previous batch may still be in flight; its epilogue (the last reader of the staged part) is done
+  // at done_ev
+  CHECK_HIP(q->stage.upload(base, s, after_s, after_s && q->done_armed ? q->done_ev : nullptr));
 
   DlschTbArgs ta{d_tb,  (int)ntb, d_data, pool->cb_crc, pool->data, d_ret, &q->crc[0],
                  d_cb,  d_slot,   d_its,  d_done,       d_run,      d_avg};
@@ -655,8 +682,34 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     }
   }
   CHECK_HIP(dlsch_launch_epilogue(ta, s));
+  if (!q->done_ev) CHECK_HIP(hipEventCreateWithFlags(&q->done_ev, hipEventDisableTiming));
+  CHECK_HIP(hipEventRecord(q->done_ev, s));
+  q->done_armed = true;
 
   const auto t1 = now();
+  if (pend) {
+    // results left in flight: read back into the pending object's own pinned buffer
+    if (pend->armed) return MI355_ERROR; // not collected
+    const size_t bytes = rnd(ntb * 4) + ntb * 4;
+    if (bytes > pend->cap) {
+      if (pend->host) (void)hipHostFree(pend->host);
+      pend->host = nullptr;
+      pend->cap  = 0;
+      CHECK_HIP(hipHostMalloc((void**)&pend->host, bytes + bytes / 2 + 4096, hipHostMallocDefault));
+      pend->cap = bytes + bytes / 2 + 4096;
+    }
+    if (!pend->ev) CHECK_HIP(hipEventCreateWithFlags(&pend->ev, hipEventDisableTiming));
+    CHECK_HIP(hipMemcpyAsync(pend->host, d_ret, bytes, hipMemcpyDeviceToHost, s));
+    CHECK_HIP(hipEventRecord(pend->ev, s));
+    pend->invalid.resize(ntb);
+    for (uint32_t t = 0; t < ntb; t++) pend->invalid[t] = tbd[t].invalid ? 1 : 0;
+    pend->ntb     = ntb;
+    pend->avg_off = rnd(ntb * 4);
+    pend->ret     = ret;
+    pend->avg     = avg_iterations;
+    pend->armed   = true;
+    return MI355_SUCCESS;
+  }
   if (hook.fn) hook.fn(hook.ctx);
   CHECK_HIP(q->back.reserve(rnd(ntb * 4) + ntb * 4));
   CHECK_HIP(hipMemcpyAsync(q->back.host, d_ret, rnd(ntb * 4) + ntb * 4, hipMemcpyDeviceToHost, s));

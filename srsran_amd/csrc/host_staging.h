@@ -14,6 +14,7 @@ struct HostStaging {
   char*      host = nullptr;
   size_t     cap = 0, used = 0;
   hipEvent_t  ev      = nullptr; // recorded after the last upload from this buffer
+  hipEvent_t  sev     = nullptr; // upload(after_s): s's work up to the upload
   hipStream_t cs      = nullptr; // copy stream: uploads overlap the compute stream's earlier work
   bool        pending = false;
 
@@ -21,6 +22,7 @@ struct HostStaging {
   {
     if (pending) (void)hipEventSynchronize(ev);
     if (ev) (void)hipEventDestroy(ev);
+    if (sev) (void)hipEventDestroy(sev);
     if (cs) (void)hipStreamDestroy(cs);
     if (host) (void)hipHostFree(host);
   }
@@ -66,13 +68,21 @@ struct HostStaging {
   }
   // one asynchronous copy of everything put so far to dst, ordered before the work enqueued on s after this
   // call.  The copy runs on the staging's own stream, so it does not wait behind s's earlier kernels (the
-  // destination must not be in use by them: callers upload into per-call descriptor space).
-  hipError_t upload(void* dst, hipStream_t s)
+  // destination must not be in use by them: callers upload into per-call descriptor space) -- unless after_s:
+  // then it waits for them (the destination may still be read by work of an earlier call left in flight), or only
+  // for the event after (recorded by the caller after the last reader of the destination).
+  hipError_t upload(void* dst, hipStream_t s, bool after_s = false, hipEvent_t after = nullptr)
   {
     if (!used) return hipSuccess;
     hipError_t e = hipSuccess;
     if (!cs && (e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking)) != hipSuccess) return e;
     if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (after) {
+      if ((e = hipStreamWaitEvent(cs, after, 0)) != hipSuccess) return e;
+    } else if (after_s) {
+      if (!sev && (e = hipEventCreateWithFlags(&sev, hipEventDisableTiming)) != hipSuccess) return e;
+      if ((e = hipEventRecord(sev, s)) != hipSuccess || (e = hipStreamWaitEvent(cs, sev, 0)) != hipSuccess) return e;
+    }
     if ((e = hipMemcpyAsync(dst, host, used, hipMemcpyHostToDevice, cs)) != hipSuccess) return e;
     if ((e = hipEventRecord(ev, cs)) != hipSuccess) return e;
     pending = true;

@@ -167,6 +167,8 @@ struct mi355_pdsch {
   int16_t*                             e_arena   = nullptr;
   bool                                 llr8      = false; // pdsch.llr_is_8bit (srsUE pdsch_8bit_decoder)
   HostStaging                          stage;
+  hipEvent_t                           fe_done  = nullptr; // after the last front-end kernel of the previous batch
+  bool                                 fe_armed = false;
   std::mutex                           mu;
 };
 
@@ -331,7 +333,8 @@ static int plan_job(mi355_pdsch_t* q, const mi355_pdsch_job_t& j, const mi355_pd
 }
 
 // front-end over planned jobs; fills P.d_off/csi_off/e_off and runs kernels A and B on s
-static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::vector<JobPlan>& plans, hipStream_t s)
+static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::vector<JobPlan>& plans, hipStream_t s,
+                        bool after_s = false)
 {
   const uint32_t njobs = (uint32_t)plans.size();
   size_t         nd = 0, ne = 0;
@@ -467,13 +470,18 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   q->stage.put(cws.data(), ncw * sizeof(PdschCwDev));
   q->stage.put(new_ci.data(), new_ci.size() * 4);
   q->stage.put(new_dst.data(), new_dst.size() * 8);
-  CHECK_HIP(q->stage.upload(base, s));
+  // after_s: the previous batch may still be in flight; its front end (the only reader of the descriptors) is done
+  // at fe_done
+  CHECK_HIP(q->stage.upload(base, s, after_s, after_s && q->fe_armed ? q->fe_done : nullptr));
   CHECK_HIP(pdsch_launch_equalize((const PdschJobDev*)(base + o_jobs), njobs, max_units, s));
   CHECK_HIP(pdsch_launch_scr_pack((const uint32_t*)(base + o_nci), (uint32_t* const*)(base + o_ndst),
                                   (uint32_t)new_ci.size(), q->gold, PDSCH_GOLD_MAX / 32, s));
   CHECK_HIP(pdsch_launch_fused((const PdschJobDev*)(base + o_jobs), njobs, max_fpairs, fkeys.data(),
                                (uint32_t)fkeys.size(), s));
   CHECK_HIP(pdsch_launch_llr((const PdschCwDev*)(base + o_cws), (uint32_t)ncw, max_pairs, s));
+  if (!q->fe_done) CHECK_HIP(hipEventCreateWithFlags(&q->fe_done, hipEventDisableTiming));
+  CHECK_HIP(hipEventRecord(q->fe_done, s));
+  q->fe_armed = true;
   return MI355_SUCCESS;
 }
 
@@ -519,6 +527,7 @@ void mi355_pdsch_destroy(mi355_pdsch_t* q)
   for (auto& kv : q->scr) (void)hipFree(kv.second);
   (void)hipFree(q->gold);
   (void)hipFree(q->scratch);
+  if (q->fe_done) (void)hipEventDestroy(q->fe_done);
   mi355_dlsch_destroy(q->dlsch);
   if (q->own) (void)hipStreamDestroy(q->own);
   delete q;
@@ -580,9 +589,21 @@ int mi355_pdsch_decode_batch(mi355_pdsch_t*           q,
 
 } // extern "C"
 
+// srslte_pdsch_codeword_decode's result fields (pdsch.c:862-871) from one DL-SCH batch's per-TB returns
+static void fill_results(mi355_pdsch_res_t* res, const std::vector<std::pair<uint32_t, uint32_t>>& who,
+                         const std::vector<int32_t>& ret, const std::vector<float>& avg)
+{
+  for (size_t k = 0; k < who.size(); k++) {
+    mi355_pdsch_res_t& o   = res[2 * who[k].first + who[k].second];
+    o.crc                  = ret[k] == 0;
+    o.ret                  = ret[k] == MI355_ERROR_INVALID_INPUTS ? MI355_ERROR : MI355_SUCCESS;
+    o.avg_iterations_block = avg[k];
+  }
+}
+
 int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi355_pdsch_job_t* jobs,
                                         uint32_t njobs, mi355_pdsch_res_t* res, void* stream, const float* d_noise,
-                                        WaitHook hook, bool ce_invariant)
+                                        WaitHook hook, bool ce_invariant, PdschPending* pend, bool after_s)
 {
   if (!q || !pool || !res || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;
   std::lock_guard<std::mutex> lock(q->mu);
@@ -603,7 +624,7 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
                                                       plans[i].dev.scheme == MI355_TXSCHEME_SPATIALMUX) ? 1u : 0u;
   }
   const auto t1 = now();
-  int r = run_frontend(q, jobs, plans, s);
+  int r = run_frontend(q, jobs, plans, s, after_s);
   if (r) return r;
   if (prof) {
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
@@ -634,25 +655,54 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
       tbs[q->max_its].push_back(d);
     }
   }
+  if (pend) {
+    pend->used = 0;
+    pend->res  = res;
+  }
   for (auto& kv : tbs) {
-    const uint32_t         its = kv.first;
-    std::vector<int32_t>   ret(kv.second.size());
-    std::vector<float>     avg(kv.second.size());
+    const uint32_t       its = kv.first;
+    std::vector<int32_t> ret_local, *ret = &ret_local;
+    std::vector<float>   avg_local, *avg = &avg_local;
+    DlschPending*        dp = nullptr;
+    if (pend) { // results stay in flight: the arrays live in the pending object until collect()
+      const uint32_t g = pend->used; // counted once its decode is enqueued
+      if (pend->groups.size() <= g) {
+        pend->groups.emplace_back(new DlschPending);
+        pend->ret.emplace_back();
+        pend->avg.emplace_back();
+        pend->who.emplace_back();
+      }
+      dp = pend->groups[g].get(), ret = &pend->ret[g], avg = &pend->avg[g];
+      pend->who[g] = by_its[its];
+    }
+    ret->assign(kv.second.size(), 0);
+    avg->assign(kv.second.size(), 0.f);
     if ((r = mi355_dlsch_set_max_iterations(q->dlsch, its))) return r;
     r = dlsch_decode_dev_hook(q->dlsch, pool, q->e_arena, kv.second.data(), (uint32_t)kv.second.size(), nullptr,
-                              ret.data(), avg.data(), s, hook, q->llr8);
+                              ret->data(), avg->data(), s, hook, q->llr8, dp, after_s);
     hook = WaitHook{}; // once
     if (r) return r;
-    const auto& who = by_its[its];
-    for (size_t k = 0; k < who.size(); k++) {
-      mi355_pdsch_res_t& o = res[2 * who[k].first + who[k].second];
-      // srslte_pdsch_codeword_decode (pdsch.c:862-871)
-      o.crc                  = ret[k] == 0;
-      o.ret                  = ret[k] == MI355_ERROR_INVALID_INPUTS ? MI355_ERROR : MI355_SUCCESS;
-      o.avg_iterations_block = avg[k];
-    }
+    if (pend)
+      pend->used++;
+    else
+      fill_results(res, by_its[its], *ret, *avg);
   }
   return MI355_SUCCESS;
+}
+
+int mi355::PdschPending::collect()
+{
+  int r = MI355_SUCCESS;
+  for (uint32_t g = 0; g < used; g++) {
+    const int e = groups[g]->collect();
+    if (e) {
+      r = e;
+      continue;
+    }
+    fill_results(res, who[g], ret[g], avg[g]);
+  }
+  used = 0;
+  return r;
 }
 
 

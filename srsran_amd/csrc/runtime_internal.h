@@ -3,6 +3,12 @@
 #include "../../include/srsran_amd/dlsch.h"
 #include "../../include/srsran_amd/pdsch.h"
 
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <utility>
+#include <vector>
+
 namespace mi355 {
 
 // Host work a caller wants done while the GPU decodes: run once, right before the final wait of the call.
@@ -11,19 +17,56 @@ struct WaitHook {
   void* ctx         = nullptr;
 };
 
+// A DL-SCH decode whose per-TB results are still in flight: the read-back is enqueued into this object's pinned
+// buffer and the call returns without waiting; collect() waits and writes ret / avg_iterations.  Reused across
+// calls (the pinned buffer grows once); the caller keeps it and the ret / avg arrays alive until collect().
+struct DlschPending {
+  char*                host = nullptr;
+  size_t               cap  = 0;
+  hipEvent_t           ev   = nullptr;
+  bool                 armed = false;
+  uint32_t             ntb   = 0;
+  size_t               avg_off = 0;
+  std::vector<uint8_t> invalid;
+  int32_t*             ret = nullptr;
+  float*               avg = nullptr;
+  DlschPending()                    = default;
+  DlschPending(const DlschPending&) = delete;
+  ~DlschPending();
+  int collect();
+};
+
 // mi355_dlsch_decode_dev with a wait hook
 // llr8: int8 LLRs (srsUE's pdsch_8bit_decoder: sch.c:403-423 with llr_is_8bit), e_offset in int8 units
+// pend: leave the results in flight (see DlschPending; the hook is not run); after_s: the call's descriptor upload
+// waits for the stream's earlier work (an earlier call's decode may still be in flight on it)
 int dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const void* d_e_bits,
                           const mi355_dlsch_tb_t* tbs, uint32_t ntb, uint8_t* d_data, int32_t* ret, float* avg_iterations,
-                          void* stream, WaitHook hook, bool llr8 = false);
+                          void* stream, WaitHook hook, bool llr8 = false, DlschPending* pend = nullptr,
+                          bool after_s = false);
+
+// A PDSCH batch decode left in flight (pdsch_decode_batch_dev_noise with pend): one DlschPending per
+// max-iterations group; collect() waits for all of them and fills the mi355_pdsch_res_t array of the call.
+struct PdschPending {
+  std::vector<std::unique_ptr<DlschPending>>                   groups;
+  std::vector<std::vector<int32_t>>                            ret;
+  std::vector<std::vector<float>>                              avg;
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>>      who; // (job, tb) per group
+  uint32_t                                                     used = 0;
+  mi355_pdsch_res_t*                                           res  = nullptr;
+  int collect();
+};
 
 // mi355_pdsch_decode_batch with the MMSE noise estimate of job i read from device memory d_noise[i] (written
 // by the channel estimator of the same stream), so no host round trip is needed between estimation and
 // equalisation.  d_noise == nullptr: the jobs' noise_estimate fields.  ce_invariant: the channel estimates
 // were just written by this library's estimator, whose every OFDM symbol row is the same (AVERAGE estimator,
 // chest_dl.c average_pilots + interpolation), so the equaliser may read them from the first row.
+// pend: launch only, the results stay in flight until pend->collect() (res must stay valid until then);
+// after_s: the descriptor uploads wait for the stream's earlier work (a previous pending batch)
 int pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi355_pdsch_job_t* jobs,
                                  uint32_t njobs, mi355_pdsch_res_t* res, void* stream, const float* d_noise,
-                                 WaitHook hook = WaitHook{}, bool ce_invariant = false);
+                                 WaitHook hook = WaitHook{}, bool ce_invariant = false, PdschPending* pend = nullptr,
+                                 bool after_s = false);
 
 } // namespace mi355

@@ -6,6 +6,7 @@
 #include <functional>
 #include <cmath>
 #include <stdlib.h>
+#include <memory>
 #include <mutex>
 #include <stdio.h>
 #include <string.h>
@@ -67,6 +68,7 @@ struct mi355_ue_dl {
   hipStream_t    side     = nullptr;       // estimator read-back + fill_res overlapping the PDSCH decode
   hipEvent_t     ev_chest = nullptr;
   CtrlState*     ctrl     = nullptr;       // PCFICH / PDCCH stage, built on first use
+  std::vector<std::unique_ptr<mi355::PdschPending>> pend; // find_and_decode: per chunk, decodes left in flight
   std::mutex     mu;
 };
 
@@ -690,8 +692,8 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   for (uint32_t i = 0; i < njobs; i++) rntis[i] = cfgs[i].rnti;
   const auto t1 = now();
   // Two chunks: the host replays chunk 0's blind searches and builds its grants while the GPU decodes chunk 1's
-  // control channels, and does chunk 1's while the GPU decodes chunk 0's PDSCH (its DL-SCH wait hook), so the GPU
-  // never waits for the host's sequential find -> grant order.  Every subframe's outcome is the same as in one
+  // control channels, and does chunk 1's while the GPU decodes chunk 0's PDSCH, so the GPU never waits for the
+  // host's sequential find -> grant order.  Every subframe's outcome is the same as in one
   // chunk: subframes are independent.
   // (MI355_UEDL_CHUNKS = 1..8 overrides the choice: A/B timing)
   static const int chunk_env = getenv("MI355_UEDL_CHUNKS") ? atoi(getenv("MI355_UEDL_CHUNKS")) : 0;
@@ -705,6 +707,7 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
     uint32_t                       b = 0, e = 0;
     std::vector<mi355_pdsch_job_t> jobs;
     std::vector<uint32_t>          which, rs_sb, rs_tbs;
+    std::vector<mi355_pdsch_res_t> sub; // the chunk's results while its decode is in flight
     int                            r = MI355_SUCCESS;
   };
   std::vector<Chunk> ck(nchunks);
@@ -763,18 +766,14 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
     return ck[0].r;
   }
   const bool ce_inv = chest_cfg->estimator_alg == MI355_ESTIMATOR_ALG_AVERAGE;
-  struct Hook {
-    std::function<void()> fn;
-    bool                  ran = false;
-    static void call(void* p)
-    {
-      Hook* h = (Hook*)p;
-      if (!h->ran) h->fn();
-      h->ran = true;
-    }
-  };
+  // Chunk c's PDSCH + DL-SCH are enqueued with their results left in flight; chunk c+1's replay and grants then run
+  // on the host while the GPU decodes chunk c, and chunk c+1's decode is enqueued right behind it (its descriptor
+  // uploads ordered after chunk c's kernels), so the GPU goes from chunk to chunk without waiting for a read-back.
+  while (q->pend.size() < nchunks) q->pend.emplace_back(new PdschPending);
+  std::vector<uint8_t> launched(nchunks, 0);
   for (uint32_t c = 0; c < nchunks && !r; c++) {
     Chunk& C = ck[c];
+    if (c) prepare(c);
     if (C.r) {
       r = C.r;
       break;
@@ -786,27 +785,21 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
       chest_fill_cb(&fill);
       for (size_t k = 0; k < C.jobs.size(); k++) C.jobs[k].noise_estimate = chest[C.which[k]].noise_estimate;
     }
-    Hook h{[&] {
-      if (c + 1 < nchunks) {
-        prepare(c + 1);
-      } else {
-        chest_fill_cb(&fill);
-      }
-    }};
-    if (C.jobs.empty()) {
-      Hook::call(&h);
-      continue;
-    }
-    if ((r = mi355_softbuffer_reset_tbs_batch(pool, C.rs_sb.data(), C.rs_tbs.data(), (uint32_t)C.rs_sb.size(), s))) {
-      Hook::call(&h);
-      break;
-    }
-    std::vector<mi355_pdsch_res_t> sub(2 * C.jobs.size());
-    for (size_t k = 0; k < C.jobs.size(); k++) sub[2 * k] = res[2 * C.which[k]], sub[2 * k + 1] = res[2 * C.which[k] + 1];
-    r = pdsch_decode_batch_dev_noise(q->pdsch, pool, C.jobs.data(), (uint32_t)C.jobs.size(), sub.data(), s,
-                                     all ? d_noise + C.b : nullptr, WaitHook{Hook::call, &h}, ce_inv);
-    for (size_t k = 0; k < C.jobs.size(); k++) res[2 * C.which[k]] = sub[2 * k], res[2 * C.which[k] + 1] = sub[2 * k + 1];
-    Hook::call(&h); // no DL-SCH work in the chunk: the decode did not run the hook
+    if (C.jobs.empty()) continue;
+    if ((r = mi355_softbuffer_reset_tbs_batch(pool, C.rs_sb.data(), C.rs_tbs.data(), (uint32_t)C.rs_sb.size(), s))) break;
+    C.sub.resize(2 * C.jobs.size());
+    for (size_t k = 0; k < C.jobs.size(); k++) C.sub[2 * k] = res[2 * C.which[k]], C.sub[2 * k + 1] = res[2 * C.which[k] + 1];
+    r = pdsch_decode_batch_dev_noise(q->pdsch, pool, C.jobs.data(), (uint32_t)C.jobs.size(), C.sub.data(), s,
+                                     all ? d_noise + C.b : nullptr, WaitHook{}, ce_inv, q->pend[c].get(), c > 0);
+    launched[c] = 1; // collected below even after an error (its enqueued groups)
+  }
+  if (!fill.done) chest_fill_cb(&fill); // srslte_chest_dl_res_t on the host while the GPU decodes
+  for (uint32_t c = 0; c < nchunks; c++) {
+    if (!launched[c]) continue;
+    const int e = q->pend[c]->collect();
+    if (e && !r) r = e;
+    Chunk& C = ck[c];
+    for (size_t k = 0; k < C.jobs.size(); k++) res[2 * C.which[k]] = C.sub[2 * k], res[2 * C.which[k] + 1] = C.sub[2 * k + 1];
   }
   CHECK_HIP(hipStreamSynchronize(q->side));
   if (!fill.done) chest_fill_cb(&fill);
