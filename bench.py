@@ -326,6 +326,9 @@ def tm4_cfg(P, cell, sf_idx, rnti=0x1234, softbuffers=(0, 1)):
     cfg.rnti = rnti
     cfg.decoder_type = P.MIMO_DECODER_MMSE
     cfg.csi_enable = 1
+    # p_a = 0 dB: the transmitter scales the PDSCH by rho_a = sqrt(2) (2 ports) whatever power_scale says
+    # (pdsch.c:1174-1188), the UE undoes it with power_scale; p_b = 1: rho_b = 1 (phy_dl_test.c:173-175, 213-215)
+    cfg.power_scale, cfg.p_a, cfg.p_b = 1, 0.0, 1
     cfg.softbuffer[0], cfg.softbuffer[1] = softbuffers
     return cfg
 
@@ -347,207 +350,37 @@ def tm4_dci_msg(cell, sf_idx, rnti=0x1234):
     return m
 
 
-class Tm4Source:
+def tm4_plans(cell, ctrl):
+    """One SfPlan per subframe index 0..9: the TM4 grant of tm4_cfg (+ its DCI format 2 on the PDCCH)."""
+    from srsran_amd import pdsch as P
+    from srsran_amd.synth import SfPlan
+    return {sf: SfPlan(sf, 1, tm4_cfg(P, cell, sf), tm4_dci_msg(cell, sf) if ctrl else None, tm=3, tbs_alt=True)
+            for sf in range(10)}
+
+
+def Tm4Source(cell, n_max, device, ctrl=False, chunk=256):
     """Up to n_max TM4 subframes resident in HBM (I/Q per rx antenna + the transmitted payloads), synthesised on the
-    GPU by global subframe index with the product's eNodeB generator."""
+    GPU by global subframe index with the product's eNodeB generator (srsran_amd.synth.DlSource): payloads keyed by
+    index -> put_pdsch -> put_refs [-> control region] -> crossed 2x2 channel + AWGN keyed by index -> IFFT."""
+    from srsran_amd.synth import DlSource
 
-    def __init__(self, cell, n_max, device, ctrl=False, chunk=256):
-        from srsran_amd import enb_dl
-        from srsran_amd import pdsch as P
-        from srsran_amd.tdec import DeviceBuffer
-        from srsran_amd.ue_dl import symbol_sz
-        self.cell, self.n_max, self.device, self.ctrl = cell, n_max, device, ctrl
-        self.sf_len = 15 * symbol_sz(cell.nof_prb)
-        self.G, self.nre = 14 * 12 * cell.nof_prb, 12 * cell.nof_prb
-        self.d_iq = DeviceBuffer(n_max * 2 * self.sf_len * 8, device)
-        self.d_pl = DeviceBuffer(n_max * 2 * NB, device)
-        self.enb = enb_dl.EnbDl(cell, device)
-        self.chunk = min(chunk, n_max)
-        self.d_tx = DeviceBuffer(self.chunk * 2 * self.G * 8, device)
-        self.d_rx = DeviceBuffer(self.chunk * 2 * self.G * 8, device)
-        self.cfg_sf = {sf: tm4_cfg(P, cell, sf) for sf in range(10)}
-        self.rows = None
-        if ctrl:  # symbol 0 (CFI 1) of each port: CRS + PCFICH + the subframe's DCI on the PDCCH (host-encoded)
-            from srsran_amd import pdcch as Dc
-            self.rows = {}
-            for sf in range(10):
-                g = np.zeros((2, self.G), np.complex64)
-                enb_dl.put_refs(cell, sf, g)
-                Dc.encode_ctrl_host(cell, sf, 1, [tm4_dci_msg(cell, sf)], g)
-                self.rows[sf] = np.ascontiguousarray(g[:, : self.nre])
-        self.first, self.n = 0, 0
+    class _Tm4(DlSource):
+        def generate(self, first, n, snr_db, seed, fading=None):
+            super().generate(first, [self.plan_sf[(first + k) % 10] for k in range(n)], snr_db, seed, fading,
+                             ctrl=self.ctrl)
 
-    def iq_ptr(self, k, r):
-        return self.d_iq.ptr + (k * 2 + r) * self.sf_len * 8
-
-    def generate(self, first, n, snr_db, seed, fading=None):
-        """Subframes [first, first + n): payloads keyed by index -> put_pdsch -> put_refs [-> control row] ->
-        crossed 2x2 channel + AWGN keyed by index (or `fading`, a srslte_channel_fading_t model string) -> IFFT."""
-        from srsran_amd import enb_dl, lib
-        assert n <= self.n_max
-        self.first, self.n = first, n
-        enb, G = self.enb, self.G
-        enb.synth_payloads(self.d_pl.ptr, first, n, 2, NB, seed)
-        H = np.array([[1, 1], [1, -1]], np.complex64)
-        sigma = math.sqrt(10 ** (-snr_db / 10) / 2)
-        for c0 in range(0, n, self.chunk):
-            m = min(self.chunk, n - c0)
-            lib().mi355_memset_dev(self.d_tx.ptr, 0, m * 2 * G * 8)
-            tx = [self.d_tx.ptr + (k * 2 + p) * G * 8 for k in range(m) for p in range(2)]
-            rx = [self.d_rx.ptr + (k * 2 + r) * G * 8 for k in range(m) for r in range(2)]
-            jobs = []
-            for k in range(m):
-                i = first + c0 + k
-                j = enb_dl.EnbPdschJob()
-                j.sf.tti, j.sf.cfi = i % 10, 1
-                j.cfg = self.cfg_sf[i % 10]
-                for t in range(2):
-                    j.data[t] = self.d_pl.ptr + ((c0 + k) * 2 + t) * NB
-                for p in range(2):
-                    j.sf_symbols[p] = tx[2 * k + p]
-                jobs.append(j)
-            enb.put_pdsch(jobs)
-            enb.put_refs([(first + c0 + k) % 10 for k in range(m)], tx)
-            if self.rows is not None:
-                for k in range(m):
-                    for p in range(2):
-                        lib().mi355_memcpy_h2d(tx[2 * k + p], self.rows[(first + c0 + k) % 10][p].ctypes.data,
-                                               self.nre * 8)
-            if fading is None:
-                enb.channel(tx, rx, 2, H, sigma, seed, first_index=first + c0)
-            else:
-                enb.fading(tx, rx, 2, fading, [1e-3 * (first + c0 + k) for k in range(m)], sigma,
-                           (seed * 7919 + first + c0) & 0x7FFFFFFF)
-            enb.gen_signal(rx, [self.iq_ptr(c0 + k, r) for k in range(m) for r in range(2)])
-        lib().mi355_device_sync()
-
-    def payloads(self, k0, n):
-        """Transmitted payloads of resident subframes [k0, k0 + n) -> (n, 2, NB) host array."""
-        out = np.zeros((n, 2, NB), np.uint8)
-        from srsran_amd import lib
-        lib().mi355_memcpy_d2h(out.ctypes.data, self.d_pl.ptr + k0 * 2 * NB, out.nbytes)
-        return out
-
-    def iq_host(self, k0, n):
-        out = np.zeros((n, 2, self.sf_len), np.complex64)
-        from srsran_amd import lib
-        lib().mi355_memcpy_d2h(out.ctypes.data, self.iq_ptr(k0, 0), out.nbytes)
-        return out
-
-    def close(self):
-        self.enb.close()
+    src = _Tm4(cell, 2, n_max, NB, device, H=[[1, 1], [1, -1]], chunk=chunk)
+    src.ctrl, src.plan_sf = ctrl, tm4_plans(cell, ctrl)
+    return src
 
 
-class Tm4Rx:
-    """The UE side of one batch of B subframes: srslte_ue_dl_t + softbuffers + grids / estimates / payload buffers,
-    with job tables prebuilt per batch position of the resident set (no host work in the timed loop beyond the
-    library calls)."""
-
-    def __init__(self, cell, B, device, ctrl=False):
-        from srsran_amd import lib
-        from srsran_amd import pdsch as P
-        from srsran_amd.dlsch import SoftbufferPool
-        from srsran_amd.tdec import DeviceBuffer
-        from srsran_amd.ue_dl import ChestRes, UeDl, _declare, default_chest_cfg
-        self.P, self.B, self.ctrl, self.cell = P, B, ctrl, cell
-        self.G = 14 * 12 * cell.nof_prb
-        self.plen = NB + 16
-        self.d_grid = DeviceBuffer(B * 2 * self.G * 8, device)
-        self.d_ce = DeviceBuffer(B * 4 * self.G * 8, device)
-        self.d_pay = DeviceBuffer(B * 2 * self.plen, device)
-        lib().mi355_memset_dev(self.d_pay.ptr, 0, B * 2 * self.plen)
-        self.pool = SoftbufferPool(2 * B, max_cb=16, device=device)
-        self.ue = UeDl(cell, 2, device)
-        self.chest_cfg = default_chest_cfg()
-        self.cfg_sf = {sf: tm4_cfg(P, cell, sf) for sf in range(10)}
-        self.L = _declare()
-        self.L.mi355_softbuffer_reset_range.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
-        self.chest = (ChestRes * B)()
-        self.res = (P.PdschRes * (2 * B))()
-        self.pays = (C.c_void_p * (2 * B))(*[self.d_pay.ptr + k * self.plen for k in range(2 * B)])
-        if ctrl:
-            from srsran_amd import pdcch as Dc
-            self.Lc = Dc._declare()
-            u = Dc.UeDlCfg()
-            u.tm, u.use_tbs_index_alt = Dc.TM4, 1
-            self.ue_cfgs = (Dc.UeDlCfg * B)(*([u] * B))
-            self.ctrl_res = (Dc.CtrlRes * B)()
-            self.dci = (Dc.DciDl * (B * Dc.MAX_DCI_MSG))()
-
-    def bind(self, src: Tm4Source, k0: int, n: int):
-        """Job tables for resident subframes [k0, k0 + n) of src (n <= B)."""
-        from srsran_amd.ue_dl import DlSfJob
-        P = self.P
-        jobs, sfs, cfgs = (DlSfJob * n)(), (P.DlSfCfg * n)(), (P.PdschCfg * n)()
-        for k in range(n):
-            i = src.first + k0 + k
-            j = jobs[k]
-            j.tti = i % 10
-            for r in range(2):
-                j.in_buffer[r] = src.iq_ptr(k0 + k, r)
-                j.sf_symbols[r] = self.d_grid.ptr + (k * 2 + r) * self.G * 8
-                for p in range(2):
-                    j.ce[p][r] = self.d_ce.ptr + (k * 4 + p * 2 + r) * self.G * 8
-            sfs[k] = P.DlSfCfg(i % 10, 1)
-            cfgs[k] = self.cfg_sf[i % 10]
-            cfgs[k].softbuffer[0], cfgs[k].softbuffer[1] = 2 * k, 2 * k + 1
-        return (jobs, sfs, cfgs, n, k0)
-
-    def step(self, bound, stages=None):
-        """One batch: new-TB softbuffer reset + mi355_ue_dl_decode_batch (OFDM, estimation, PDSCH, DL-SCH), or the
-        find_and_decode form with the control channels.  With `stages`, the two-call form (decode_fft_estimate,
-        then decode_pdsch) is timed per stage instead."""
-        from srsran_amd import check, lib
-        jobs, sfs, cfgs, n, _ = bound
-        C.memset(self.res, 0, C.sizeof(self.res))
-        if self.ctrl:
-            # find_and_decode resets each TB's softbuffer itself (ue_dl.c:1522-1529)
-            check(self.Lc.mi355_ue_dl_find_and_decode_batch(self.ue.h, self.pool.h, jobs, sfs, self.ue_cfgs, cfgs,
-                                                            C.byref(self.chest_cfg), self.chest, self.pays, n,
-                                                            self.ctrl_res, self.dci, self.res, None),
-                  "ue_dl_find_and_decode_batch")
-            return
-        check(self.L.mi355_softbuffer_reset_range(self.pool.h, 0, 2 * n, None), "softbuffer_reset_range")
-        if stages is None:
-            check(self.L.mi355_ue_dl_decode_batch(self.ue.h, self.pool.h, jobs, sfs, cfgs, C.byref(self.chest_cfg),
-                                                  self.chest, self.pays, n, self.res, None), "ue_dl_decode_batch")
-            return
-        t0 = time.perf_counter()
-        check(self.L.mi355_ue_dl_decode_fft_estimate_batch(self.ue.h, jobs, n, C.byref(self.chest_cfg), self.chest,
-                                                           None), "decode_fft_estimate")
-        t1 = time.perf_counter()
-        check(self.L.mi355_ue_dl_decode_pdsch_batch(self.ue.h, self.pool.h, jobs, sfs, cfgs, self.chest, self.pays, n,
-                                                    self.res, None), "decode_pdsch")
-        lib().mi355_device_sync()
-        t2 = time.perf_counter()
-        stages["fft_chest_ms"] = stages.get("fft_chest_ms", 0) + (t1 - t0) * 1e3
-        stages["pdsch_decode_ms"] = stages.get("pdsch_decode_ms", 0) + (t2 - t1) * 1e3
-
-    def crc_bits(self, n):
-        """2 bits per subframe (TB0, TB1 CRC ok; with the control channels also exactly one DCI found)."""
-        r = np.ctypeslib.as_array(self.res)[: 2 * n]
-        bits = (r["crc"] != 0) & (r["ret"] == 0)
-        if self.ctrl:
-            nd = np.ctypeslib.as_array(self.ctrl_res)[:n]["nof_dci"]
-            bits &= np.repeat(nd == 1, 2)
-        return bits.astype(np.uint8)
-
-    def payload_ok(self, src: Tm4Source, bound):
-        """TBs whose CRC passed AND whose decoded bytes equal the transmitted payload."""
-        _, _, _, n, k0 = bound
-        host = np.zeros(n * 2 * self.plen, np.uint8)
-        from srsran_amd import lib
-        lib().mi355_memcpy_d2h(host.ctypes.data, self.d_pay.ptr, host.nbytes)
-        host = host.reshape(n, 2, self.plen)[:, :, :NB]
-        want = src.payloads(k0, n)
-        eq = np.all(host == want, axis=2).reshape(-1)
-        return int((eq & (self.crc_bits(n) == 1)).sum())
-
-    def avg_its(self, n):
-        return float(np.mean(np.ctypeslib.as_array(self.res)[: 2 * n]["avg_iterations_block"]))
+def Tm4Rx(cell, B, device, ctrl=False):
+    """The UE side of one TM4 batch of B subframes (srsran_amd.synth.DlReceiver)."""
+    from srsran_amd.synth import DlReceiver
+    return DlReceiver(cell, 2, B, NB, device, ctrl=ctrl, max_cb=16)
 
 
-def cpu_baseline_pdsch(src: Tm4Source, gpu_bufs, avg_its, budget_s):
+def cpu_baseline_pdsch(src, gpu_bufs, avg_its, budget_s):
     """CPU reference-path timing on the host cores (rank 0, N = 1), bounded sample of the same workload:
     S subframes' I/Q (downloaded from HBM) through oracle/orc_front.c's C chain (OFDM by a float Stockham FFT,
     estimation, RE extraction, MMSE + CSI, demapping, descrambling, rate dematching -- the oracle's scalar C
@@ -564,7 +397,8 @@ def cpu_baseline_pdsch(src: Tm4Source, gpu_bufs, avg_its, budget_s):
     for d in range(S):
         cfgs[d] = oracle.front_cfg(pc.Cfg(nof_prb=100, nof_ports=2, nof_rx=2, cell_id=1, cfi=1,
                                           sf_idx=(src.first + d) % 10, scheme=2, nof_layers=2, qm=[8, 8],
-                                          tbs=[TBS, TBS], csi_enable=True))
+                                          tbs=[TBS, TBS], csi_enable=True, power_scale=True, p_a=0.0,
+                                          p_b=1))
     stride = 18600
     sb = np.zeros(S * 2 * 16 * stride, np.int16)
     L = oracle.lib()
@@ -627,7 +461,7 @@ def cpu_baseline_pdsch(src: Tm4Source, gpu_bufs, avg_its, budget_s):
     }
 
 
-def softbuffer_contents(rx: Tm4Rx, ncb):
+def softbuffer_contents(rx, ncb):
     from srsran_amd import lib
     buf, stride, mcb = C.POINTER(C.c_int16)(), C.c_uint32(), C.c_uint32()
     lib().mi355_softbuffer_pool_buffer.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_int16)),
@@ -636,7 +470,7 @@ def softbuffer_contents(rx: Tm4Rx, ncb):
     return C.cast(buf, C.c_void_p).value, stride.value
 
 
-def map_probe(rx: Tm4Rx, B, local, sample_check=True):
+def map_probe(rx, B, local, sample_check=True):
     """Dominant kernel: the MAP half-iteration over this batch's 32 B code blocks (the softbuffers hold the
     rate-dematched LLRs of the last step), a fixed 8 half-iterations without early stop (configs[1]'s regime on
     the e2e code blocks), HIP events on the decoder's stream.  Returns (roofline, roofline_valu, fixed8 dict)."""

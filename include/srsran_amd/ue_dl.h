@@ -99,6 +99,10 @@ void mi355_ue_dl_destroy(mi355_ue_dl_t* q);
 /* srslte_use_standard_symbol_size: switch the DFT size to the 3GPP rates (2048 for 100 PRB) */
 int mi355_ue_dl_set_standard_rates(mi355_ue_dl_t* q, int enable);
 
+/* find_and_decode's pipelining: number of chunks a batch is split into (1..8; 0 = automatic, 2 from 256 subframes).
+ * Results do not depend on it (subframes are independent); tests and A/B timing set it. */
+int mi355_ue_dl_set_chunks(mi355_ue_dl_t* q, uint32_t nof_chunks);
+
 /* Zero one link's estimator state (srslte_chest_dl_init / set_cell). */
 int mi355_ue_dl_reset_link(mi355_ue_dl_t* q, uint32_t link);
 

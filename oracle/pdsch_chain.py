@@ -99,9 +99,46 @@ def modulate(bits: np.ndarray, qm: int) -> np.ndarray:
 
 
 # ------------------------------------------------------------------ 36.211 6.3.3 / 6.3.4
-def precode(d: list[np.ndarray], cfg: Cfg) -> np.ndarray:
-    """codeword symbols -> per-port transmit symbols (nof_ports, nof_re)."""
+def tx_scales(cfg: Cfg) -> tuple[np.float32, np.float32, np.float32]:
+    """srslte_pdsch_encode's rho_a, applied whatever cfg.power_scale says (pdsch.c:1174-1188, :582), and the
+    precoders' folded factors rho_a / sqrt(2) (diversity, codebook 0, one layer) and rho_a / 2 (codebooks 1-2,
+    CDD) as precoding.c:1945-2200 rounds them (float32)."""
+    amp = np.float64(np.float32(10.0) ** np.float32(cfg.p_a / 20.0))
+    rho_a = np.float32(amp * (1.0 if cfg.nof_ports == 1 else np.sqrt(2.0)))
+    s = rho_a if rho_a != 0 else np.float32(1.0)
+    return s, np.float32(np.float64(s) * np.sqrt(0.5)), np.float32(s / np.float32(2.0))
+
+
+def precode(d: list[np.ndarray], cfg: Cfg, ref_scaling: bool = False) -> np.ndarray:
+    """codeword symbols -> per-port transmit symbols (nof_ports, nof_re).  ref_scaling: the reference
+    transmitter's amplitudes (rho_a folded in, tx_scales); otherwise unit-power precoders (test channels)."""
     n = d[0].size
+    if ref_scaling:
+        s0, s1, s2 = tx_scales(cfg)
+        m1 = lambda v: (v.real * s1 + 1j * (v.imag * s1)).astype(np.complex64)  # noqa: E731
+        m2 = lambda v: (v.real * s2 + 1j * (v.imag * s2)).astype(np.complex64)  # noqa: E731
+        if cfg.scheme == PORT0:
+            x = d[0]
+            return (x if s0 == 1 else (x.real * s0 + 1j * (x.imag * s0)).astype(np.complex64))[None, :].copy()
+        if cfg.scheme == DIVERSITY:
+            x0, x1 = d[0][0::2], d[0][1::2]
+            y = np.zeros((2, n), np.complex64)
+            y[0, 0::2], y[1, 0::2] = m1(x0), m1(-np.conj(x1))
+            y[0, 1::2], y[1, 1::2] = m1(x1), m1(np.conj(x0))
+            return y
+        cb = cfg.codebook()
+        if cfg.scheme == SPATIALMUX and cfg.nof_layers == 1:
+            w1 = {0: 1, 1: -1, 2: 1j, 3: -1j}[cb]
+            return np.stack([m1(d[0]), m1(w1 * d[0])]).astype(np.complex64)
+        x0, x1 = d[0], d[1]
+        if cfg.scheme == SPATIALMUX:
+            if cb == 0:
+                return np.stack([m1(x0), m1(x1)])
+            if cb == 1:
+                return np.stack([m2(x0 + x1), m2(x0 - x1)])
+            return np.stack([m2(x0 + x1), m2(1j * (x0 - x1))])
+        ev = (np.arange(n) % 2) == 0
+        return np.stack([m2(x0 + x1), np.where(ev, m2(x0 - x1), m2(x1 - x0))])
     r2 = np.float32(np.sqrt(2.0))
     if cfg.scheme == PORT0:
         return d[0][None, :].copy()

@@ -201,20 +201,21 @@ int mi355_pdsch_encode_host(const mi355_cell_t* cell, const mi355_dl_sf_cfg_t* s
   const uint32_t np = cell->nof_ports;
   std::vector<cf> y[4];
   for (uint32_t p = 0; p < np; p++) y[p].assign(nre, cf{0.f, 0.f});
-  const float r2 = (float)M_SQRT1_2;
+  float s0, s1, s2; // rho_a folded into the precoders
+  mi355::pdsch_tx_scales(cfg->p_a, np, &s0, &s1, &s2);
   switch (g.tx_scheme) {
-    case MI355_TXSCHEME_PORT0:
+    case MI355_TXSCHEME_PORT0: // srslte_pdsch_encode: memcpy when rho_a is 1, else x * rho_a (pdsch.c:1236-1240)
       if (np != 1 || d[0].size() < nre) return MI355_ERROR_INVALID_INPUTS;
-      y[0].assign(d[0].begin(), d[0].begin() + nre);
+      for (uint32_t i = 0; i < nre; i++) y[0][i] = s0 == 1.0f ? d[0][i] : cf{d[0][i].re * s0, d[0][i].im * s0};
       break;
     case MI355_TXSCHEME_DIVERSITY: // srslte_layermap_diversity + srslte_precoding_diversity (2 ports)
       if (np != 2 || d[0].size() < nre) return MI355_ERROR_INVALID_INPUTS;
       for (uint32_t i = 0; i < nre / 2; i++) {
         const cf x0 = d[0][2 * i], x1 = d[0][2 * i + 1];
-        y[0][2 * i]     = cf{x0.re * r2, x0.im * r2};
-        y[1][2 * i]     = cf{-x1.re * r2, x1.im * r2};
-        y[0][2 * i + 1] = cf{x1.re * r2, x1.im * r2};
-        y[1][2 * i + 1] = cf{x0.re * r2, -x0.im * r2};
+        y[0][2 * i]     = cf{x0.re * s1, x0.im * s1};
+        y[1][2 * i]     = cf{-x1.re * s1, x1.im * s1};
+        y[0][2 * i + 1] = cf{x1.re * s1, x1.im * s1};
+        y[1][2 * i + 1] = cf{x0.re * s1, -x0.im * s1};
       }
       break;
     case MI355_TXSCHEME_SPATIALMUX:
@@ -225,31 +226,31 @@ int mi355_pdsch_encode_host(const mi355_cell_t* cell, const mi355_dl_sf_cfg_t* s
         if (g.tx_scheme != MI355_TXSCHEME_SPATIALMUX || cb > 3) return MI355_ERROR_INVALID_INPUTS;
         for (uint32_t i = 0; i < nre; i++) {
           const cf x = d[0][i];
-          y[0][i]    = cf{x.re * r2, x.im * r2};
+          y[0][i]    = cf{x.re * s1, x.im * s1};
           switch (cb) {
-            case 0: y[1][i] = cf{x.re * r2, x.im * r2}; break;
-            case 1: y[1][i] = cf{-x.re * r2, -x.im * r2}; break;
-            case 2: y[1][i] = cf{-x.im * r2, x.re * r2}; break;
-            default: y[1][i] = cf{x.im * r2, -x.re * r2}; break;
+            case 0: y[1][i] = cf{x.re * s1, x.im * s1}; break;
+            case 1: y[1][i] = cf{-x.re * s1, -x.im * s1}; break;
+            case 2: y[1][i] = cf{-x.im * s1, x.re * s1}; break;
+            default: y[1][i] = cf{x.im * s1, -x.re * s1}; break;
           }
         }
       } else {
         if (d[0].size() < nre || d[1].size() < nre) return MI355_ERROR_INVALID_INPUTS;
         for (uint32_t i = 0; i < nre; i++) {
           const cf x0 = d[0][i], x1 = d[1][i];
-          const cf s{(x0.re + x1.re) * 0.5f, (x0.im + x1.im) * 0.5f}, m{(x0.re - x1.re) * 0.5f, (x0.im - x1.im) * 0.5f};
+          const cf s{(x0.re + x1.re) * s2, (x0.im + x1.im) * s2}, m{(x0.re - x1.re) * s2, (x0.im - x1.im) * s2};
           if (g.tx_scheme == MI355_TXSCHEME_CDD) { // large-delay CDD, 2 layers: alternating W D(i) U
             y[0][i] = s;
             y[1][i] = (i & 1) ? cf{-m.re, -m.im} : m;
           } else if (cb == 0) {
-            y[0][i] = cf{x0.re * r2, x0.im * r2};
-            y[1][i] = cf{x1.re * r2, x1.im * r2};
+            y[0][i] = cf{x0.re * s1, x0.im * s1};
+            y[1][i] = cf{x1.re * s1, x1.im * s1};
           } else if (cb == 1) {
             y[0][i] = s;
             y[1][i] = m;
           } else {
             y[0][i] = s;
-            y[1][i] = cf{-m.im, m.re}; // j * (x0 - x1) / 2
+            y[1][i] = cf{-m.im, m.re}; // j * (x0 - x1) * rho_a / 2
           }
         }
       }

@@ -2,6 +2,7 @@
 // (enb_dl_kernels.hip) and the host helpers the GPU runtime shares with the host encoder (enb_dl_host.cpp).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 #include <vector>
@@ -42,6 +43,7 @@ struct EnbMapDev {        // one PDSCH job: codeword bits -> symbols -> layers -
   uint32_t        qm[2];
   uint32_t        scheme, nports, nlayers, cb;
   float           r2, n16, n64, n256; // 1/sqrt(2), 1/sqrt(10), 1/sqrt(42), 1/sqrt(170) as the host encoder rounds them
+  float           s0, s1, s2;         // rho_a folded into the precoders: rho_a, rho_a/sqrt(2), rho_a/2 (pdsch_tx_scales)
 };
 
 struct EnbChanJob {
@@ -83,5 +85,18 @@ hipError_t enb_launch_channel(const EnbChanJob* jobs, uint32_t njobs, uint32_t n
 hipError_t enb_launch_synth_payloads(uint8_t* out, uint64_t first, uint32_t n, uint32_t ntb, uint32_t nbytes,
                                      uint64_t seed, hipStream_t s);
 hipError_t enb_launch_fading(const EnbFadingArgs& a, uint32_t njobs, hipStream_t s);
+
+// srslte_pdsch_encode scales the PDSCH by rho_a = 10^(p_a/20) (x sqrt(2) with 2+ ports) whatever cfg->power_scale
+// says (pdsch.c:1174-1188, apply_power_allocation :582; the eNodeB object has no rx antennas, so rho_b is never
+// applied), and the precoders fold it into their normalisation: x rho_a (port 0), x (float)(rho_a/sqrt(2))
+// (diversity, multiplexing codebook 0 / one layer), x rho_a/2 (codebooks 1-2, CDD) (precoding.c:1945-2200).
+inline void pdsch_tx_scales(float p_a, uint32_t nof_ports, float* s0, float* s1, float* s2)
+{
+  const float rho_a = (float)((double)powf(10.0f, p_a / 20.0f) * (nof_ports == 1 ? 1.0 : M_SQRT2));
+  const float s     = rho_a != 0.0f ? rho_a : 1.0f;
+  *s0               = s;
+  *s1               = (float)(s * M_SQRT1_2);
+  *s2               = s / 2.0f;
+}
 
 } // namespace mi355

@@ -250,20 +250,21 @@ __global__ __launch_bounds__(256) void enb_map(const EnbMapDev* __restrict__ job
   const uint32_t   u = blockIdx.x * 256 + threadIdx.x;
   if (u >= J.units) return;
   const uint16_t* map = J.map;
-  const float     r2  = J.r2;
+  const float     s1  = J.s1, s2 = J.s2; // rho_a / sqrt(2), rho_a / 2 (srslte_precoding_*, precoding.c:1945-2200)
   switch (J.scheme) {
-    case 0: { // port 0
-      const float2 x            = cw_symbol(J, 0, u);
-      J.grid[0][map[u]]         = x;
+    case 0: { // port 0: x * rho_a (srslte_pdsch_encode copies when rho_a is 1)
+      float2 x = cw_symbol(J, 0, u);
+      if (J.s0 != 1.0f) x = make_float2(x.x * J.s0, x.y * J.s0);
+      J.grid[0][map[u]] = x;
       break;
     }
     case 1: { // srslte_layermap_diversity + srslte_precoding_diversity, 2 ports (Alamouti over RE pairs)
       const float2 x0 = cw_symbol(J, 0, 2 * u), x1 = cw_symbol(J, 0, 2 * u + 1);
       const uint32_t g0 = map[2 * u], g1 = map[2 * u + 1];
-      J.grid[0][g0] = make_float2(x0.x * r2, x0.y * r2);
-      J.grid[1][g0] = make_float2(-x1.x * r2, x1.y * r2);
-      J.grid[0][g1] = make_float2(x1.x * r2, x1.y * r2);
-      J.grid[1][g1] = make_float2(x0.x * r2, -x0.y * r2);
+      J.grid[0][g0] = make_float2(x0.x * s1, x0.y * s1);
+      J.grid[1][g0] = make_float2(-x1.x * s1, x1.y * s1);
+      J.grid[0][g1] = make_float2(x1.x * s1, x1.y * s1);
+      J.grid[1][g1] = make_float2(x0.x * s1, -x0.y * s1);
       break;
     }
     default: { // spatial multiplexing (codebooks) / large-delay CDD, 2 ports
@@ -271,23 +272,23 @@ __global__ __launch_bounds__(256) void enb_map(const EnbMapDev* __restrict__ job
       float2         y0, y1;
       if (J.nlayers == 1) {
         const float2 x = cw_symbol(J, 0, u);
-        y0             = make_float2(x.x * r2, x.y * r2);
+        y0             = make_float2(x.x * s1, x.y * s1);
         switch (J.cb) {
-          case 0: y1 = make_float2(x.x * r2, x.y * r2); break;
-          case 1: y1 = make_float2(-x.x * r2, -x.y * r2); break;
-          case 2: y1 = make_float2(-x.y * r2, x.x * r2); break;
-          default: y1 = make_float2(x.y * r2, -x.x * r2); break;
+          case 0: y1 = make_float2(x.x * s1, x.y * s1); break;
+          case 1: y1 = make_float2(-x.x * s1, -x.y * s1); break;
+          case 2: y1 = make_float2(-x.y * s1, x.x * s1); break;
+          default: y1 = make_float2(x.y * s1, -x.x * s1); break;
         }
       } else {
         const float2 x0 = cw_symbol(J, 0, u), x1 = cw_symbol(J, 1, u);
-        const float2 sm = make_float2((x0.x + x1.x) * 0.5f, (x0.y + x1.y) * 0.5f);
-        const float2 df = make_float2((x0.x - x1.x) * 0.5f, (x0.y - x1.y) * 0.5f);
+        const float2 sm = make_float2((x0.x + x1.x) * s2, (x0.y + x1.y) * s2);
+        const float2 df = make_float2((x0.x - x1.x) * s2, (x0.y - x1.y) * s2);
         if (J.scheme == 3) { // CDD
           y0 = sm;
           y1 = (u & 1u) ? make_float2(-df.x, -df.y) : df;
         } else if (J.cb == 0) {
-          y0 = make_float2(x0.x * r2, x0.y * r2);
-          y1 = make_float2(x1.x * r2, x1.y * r2);
+          y0 = make_float2(x0.x * s1, x0.y * s1);
+          y1 = make_float2(x1.x * s1, x1.y * s1);
         } else if (J.cb == 1) {
           y0 = sm;
           y1 = df;

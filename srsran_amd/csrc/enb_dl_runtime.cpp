@@ -283,6 +283,7 @@ int mi355_enb_dl_put_pdsch_batch(mi355_enb_dl_t* q, const mi355_enb_dl_pdsch_job
     M.nports     = cell.nof_ports;
     M.nlayers    = g.nof_layers;
     M.r2 = r2, M.n16 = n16, M.n64 = n64, M.n256 = n256;
+    pdsch_tx_scales(J.cfg.p_a, cell.nof_ports, &M.s0, &M.s1, &M.s2);
     for (uint32_t p = 0; p < cell.nof_ports; p++) {
       if (!J.sf_symbols[p]) return MI355_ERROR_INVALID_INPUTS;
       M.grid[p] = (float2*)J.sf_symbols[p];

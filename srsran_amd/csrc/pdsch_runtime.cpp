@@ -678,8 +678,11 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
     ret->assign(kv.second.size(), 0);
     avg->assign(kv.second.size(), 0.f);
     if ((r = mi355_dlsch_set_max_iterations(q->dlsch, its))) return r;
+    // with results left in flight, a later iteration-count batch shares the DL-SCH descriptor scratch with the
+    // earlier ones still queued on s: its upload waits for their epilogue (done_ev)
+    const bool after = after_s || (pend && pend->used > 0);
     r = dlsch_decode_dev_hook(q->dlsch, pool, q->e_arena, kv.second.data(), (uint32_t)kv.second.size(), nullptr,
-                              ret->data(), avg->data(), s, hook, q->llr8, dp, after_s);
+                              ret->data(), avg->data(), s, hook, q->llr8, dp, after);
     hook = WaitHook{}; // once
     if (r) return r;
     if (pend)

@@ -69,6 +69,7 @@ struct mi355_ue_dl {
   hipEvent_t     ev_chest = nullptr;
   CtrlState*     ctrl     = nullptr;       // PCFICH / PDCCH stage, built on first use
   std::vector<std::unique_ptr<mi355::PdschPending>> pend; // find_and_decode: per chunk, decodes left in flight
+  uint32_t       chunks = 0;                              // find_and_decode chunk count (0: automatic)
   std::mutex     mu;
 };
 
@@ -492,6 +493,14 @@ int mi355_ue_dl_set_standard_rates(mi355_ue_dl_t* q, int enable)
   return set_dft(q);
 }
 
+int mi355_ue_dl_set_chunks(mi355_ue_dl_t* q, uint32_t nof_chunks)
+{
+  if (!q || nof_chunks > 8) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  q->chunks = nof_chunks;
+  return MI355_SUCCESS;
+}
+
 int mi355_ue_dl_reset_link(mi355_ue_dl_t* q, uint32_t link)
 {
   if (!q || link >= MI355_MAX_LINKS) return MI355_ERROR_INVALID_INPUTS;
@@ -695,10 +704,10 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   // control channels, and does chunk 1's while the GPU decodes chunk 0's PDSCH, so the GPU never waits for the
   // host's sequential find -> grant order.  Every subframe's outcome is the same as in one
   // chunk: subframes are independent.
-  // (MI355_UEDL_CHUNKS = 1..8 overrides the choice: A/B timing)
+  // (mi355_ue_dl_set_chunks, or MI355_UEDL_CHUNKS = 1..8 when it is not set, overrides the choice: tests, A/B timing)
   static const int chunk_env = getenv("MI355_UEDL_CHUNKS") ? atoi(getenv("MI355_UEDL_CHUNKS")) : 0;
-  const uint32_t   nchunks   = chunk_env >= 1 && chunk_env <= 8 ? std::max(1u, std::min((uint32_t)chunk_env, njobs))
-                                                                 : (njobs >= 256 ? 2u : 1u);
+  const uint32_t   forced    = q->chunks ? q->chunks : (chunk_env >= 1 && chunk_env <= 8 ? (uint32_t)chunk_env : 0u);
+  const uint32_t   nchunks   = forced ? std::max(1u, std::min(forced, njobs)) : (njobs >= 256 ? 2u : 1u);
   if ((r = q->ctrl->launch(sfjobs, nullptr, d_noise, rntis.data(), ue_cfgs, njobs, nchunks, s))) {
     chest_fill_cb(&fill);
     return r;

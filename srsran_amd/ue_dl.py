@@ -56,6 +56,7 @@ def _declare():
     L.mi355_ue_dl_destroy.argtypes = [vp]
     L.mi355_ue_dl_set_standard_rates.argtypes = [vp, i32]
     L.mi355_ue_dl_reset_link.argtypes = [vp, u32]
+    L.mi355_ue_dl_set_chunks.argtypes = [vp, u32]
     L.mi355_ofdm_rx_batch.argtypes = [vp, C.POINTER(DlSfJob), u32, vp]
     L.mi355_chest_dl_estimate_batch.argtypes = [vp, C.POINTER(DlSfJob), u32, C.POINTER(ChestCfg),
                                                 C.POINTER(ChestRes), vp]
@@ -91,6 +92,10 @@ class UeDl:
             self.L.mi355_ue_dl_pdsch(self.h)), cell, nof_rx_antennas
         self.pdsch.device = device
         self.pdsch.close = lambda: None
+
+    def set_chunks(self, n: int):
+        """find_and_decode's chunk count (0 = automatic)."""
+        check(self.L.mi355_ue_dl_set_chunks(self.h, n), "set_chunks")
 
     def reset_link(self, link: int):
         check(self.L.mi355_ue_dl_reset_link(self.h, link), "reset_link")

@@ -103,3 +103,45 @@ class DevIqSubframe:
     def payload_bytes(self, t: int) -> np.ndarray:
         out = np.zeros(self.cfg.tbs[t] // 8 + 16, np.uint8)
         return self.payload[t].download(out)
+
+
+def oracle_cfg(cell: P.Cell, nof_rx: int, tti: int, cfi: int, pcfg: P.PdschCfg) -> pc.Cfg:
+    """The oracle chain's Cfg for a product PdschCfg (grant from the DCI, the UE's power / CSI / decoder fields)."""
+    g = pcfg.grant
+    tbs = [t for t in range(2) if g.tb[t].enabled]
+    prb = np.array([[g.prb_idx[s][n] for n in range(cell.nof_prb)] for s in range(2)], np.uint8)
+    return pc.Cfg(nof_prb=cell.nof_prb, nof_ports=cell.nof_ports, cell_id=cell.id, nof_rx=nof_rx, cfi=cfi,
+                  sf_idx=tti % 10, rnti=pcfg.rnti, scheme=g.tx_scheme, nof_layers=g.nof_layers, pmi=g.pmi,
+                  qm=[P.MOD_BITS[g.tb[t].mod] for t in tbs], tbs=[g.tb[t].tbs for t in tbs],
+                  rv=[g.tb[t].rv for t in tbs] + [0] * (2 - len(tbs)), prb=prb, csi_enable=bool(pcfg.csi_enable),
+                  power_scale=bool(pcfg.power_scale), p_a=pcfg.p_a, p_b=pcfg.p_b,
+                  mmse=pcfg.decoder_type == P.MIMO_DECODER_MMSE)
+
+
+def llr_spot_check(rx, k: int, ocfg: pc.Cfg, payload_bytes: list, decoded_job: int | None = None):
+    """Subframe k of a DlReceiver's last (single-chunk) call: the GPU's soft bits of every TB equal the oracle
+    chain's (oracle/pdsch_chain.rx_front on the GPU's own grid, estimates and noise estimate) bit for bit, and their
+    signs equal the codeword the transmitter sent (phy_dl_test.c check_softbits)."""
+    import oracle
+    from srsran_amd import lib
+    G = 14 * 12 * ocfg.nof_prb
+
+    def d2h(ptr):
+        out = np.zeros(G, np.complex64)
+        lib().mi355_memcpy_d2h(out.ctypes.data, ptr, out.nbytes)
+        return out
+
+    grids = np.stack([d2h(rx.grid_ptr(k, r)) for r in range(ocfg.nof_rx)])
+    ces = np.stack([np.stack([d2h(rx.ce_ptr(k, p, r)) for r in range(ocfg.nof_rx)]) for p in range(ocfg.nof_ports)])
+    noise = rx.chest[k].noise_estimate
+    _d, _csi, e_o = pc.rx_front(ocfg, grids, ces, noise)
+    j = k if decoded_job is None else decoded_job
+    Nl = 2 if ocfg.nof_layers != ocfg.nof_tb else 1
+    for t in range(ocfg.nof_tb):
+        nbits = e_o[t].size
+        nre = nbits // ocfg.qm[t]
+        e_g = rx.ue.pdsch.stage(j, t, nre, nbits)[2]
+        assert np.array_equal(e_g, e_o[t]), (k, t, int(np.abs(e_g.astype(np.int32) - e_o[t]).max()))
+        bits = np.unpackbits(np.asarray(payload_bytes[t], np.uint8))[: ocfg.tbs[t]]
+        coded = oracle.dlsch_encode_tb(bits, ocfg.tbs[t], ocfg.qm[t] * Nl, nbits, ocfg.rv[t])
+        assert np.array_equal(e_g > 0, coded == 1), (k, t, int(np.sum((e_g > 0) != (coded == 1))))

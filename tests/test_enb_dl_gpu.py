@@ -35,6 +35,7 @@ def enb_job(cfg: pc.Cfg, payloads: list[DeviceBuffer], grids: list[DeviceBuffer]
     j.sf.cfi = cfg.cfi
     j.cfg.grant = grant_of(cfg)
     j.cfg.rnti = cfg.rnti
+    j.cfg.p_a = cfg.p_a  # the transmitter scales by rho_a whatever power_scale says (pdsch.c:1174-1188)
     for t, b in enumerate(payloads):
         j.data[t] = b.ptr
     for p, g in enumerate(grids):
@@ -232,6 +233,7 @@ def test_generator_round_trip_tm4():
         pc_.rnti = cfg.rnti
         pc_.decoder_type = P.MIMO_DECODER_MMSE
         pc_.csi_enable = 1
+        pc_.power_scale, pc_.p_a, pc_.p_b = 1, 0.0, 1  # undo the transmitter's rho_a, rho_b = 1 (as phy_dl_test)
         pc_.softbuffer[0], pc_.softbuffer[1] = 2 * i, 2 * i + 1
         pcfgs.append(pc_)
         pays += [outs[i][0].ptr, outs[i][1].ptr]
