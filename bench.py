@@ -19,6 +19,7 @@ regenerates its own subframes): payloads = mi355_enb_synth_payloads(i) -> the pr
     python bench.py --gpus 8 --total-subframes 1048576  # configs[4]: 1M subframes sharded contiguously by rank
     python bench.py --workload tdec                     # configs[1]: batched turbo decode only
     python bench.py --workload ue_dl                    # + PCFICH / PDCCH blind search -> DCI -> grant
+    python bench.py --workload siso_qpsk                # configs[2]: phy_dl_test -p 100 -t 1 -m 9 (SISO QPSK)
     python bench.py --workload plumbing --gpus 2        # CPU dry run of the launcher / sharding / bitmap gather
 
 Multi-GPU: one process per GPU.  Default: weak scaling, rank r decodes subframes [r B, (r+1) B) every step.
@@ -65,9 +66,10 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["pdsch", "ue_dl", "tdec", "enb", "plumbing"], default="pdsch",
+    ap.add_argument("--workload", choices=["pdsch", "ue_dl", "siso_qpsk", "tdec", "enb", "plumbing"], default="pdsch",
                     help="pdsch: known grants (decode_batch); ue_dl: phy_dl_test's work_ue with the PCFICH / PDCCH "
-                         "blind search deriving every grant (find_and_decode); tdec: configs[1]; enb: the GPU "
+                         "blind search deriving every grant (find_and_decode); siso_qpsk: configs[2], phy_dl_test -p "
+                         "100 -t 1 -m 9 through find_and_decode; tdec: configs[1]; enb: the GPU "
                          "eNodeB generator (encode side, SURVEY 8f row 2); plumbing: CPU dry run of the multi-rank "
                          "launcher, sharding and CRC-bitmap gather (no GPU, no decoding)")
     ap.add_argument("--subframes", type=int, default=2048, help="TM4 subframes per GPU per step (batch)")
@@ -76,6 +78,7 @@ def parse(argv=None):
     ap.add_argument("--resident-gb", type=float, default=96.0, help="HBM budget for one rank's resident I/Q")
     ap.add_argument("--seed", type=int, default=4242)
     ap.add_argument("--snr", type=float, default=40.0)
+    ap.add_argument("--siso-snr", type=float, default=None, help="siso_qpsk AWGN SNR (default none, as phy_dl_test)")
     ap.add_argument("--waterfall-snr", type=float, default=28.0,
                     help="SNR of the decoder-bound e2e field (EPA 5 Hz fading)")
     ap.add_argument("--no-waterfall", action="store_true")
@@ -380,34 +383,37 @@ def Tm4Rx(cell, B, device, ctrl=False):
     return DlReceiver(cell, 2, B, NB, device, ctrl=ctrl, max_cb=16)
 
 
-def cpu_baseline_pdsch(src, gpu_bufs, avg_its, budget_s):
+def cpu_baseline_pdsch(src, gpu_bufs, avg_its, budget_s, ocfg_of=None, K=6144, C=16, ntb=2, tbs=TBS, max_cb=16,
+                       S_max=16, label="TM4"):
     """CPU reference-path timing on the host cores (rank 0, N = 1), bounded sample of the same workload:
     S subframes' I/Q (downloaded from HBM) through oracle/orc_front.c's C chain (OFDM by a float Stockham FFT,
     estimation, RE extraction, MMSE + CSI, demapping, descrambling, rate dematching -- the oracle's scalar C
-    restatement, one subframe per thread task) and their 32 S code blocks through the reference's own AVX2 turbo
+    restatement, one subframe per thread task) and their ntb C S code blocks through the reference's own AVX2 turbo
     decoder (oracle/_ref, compiled from the srsLTE sources) for ceil(avg half-iterations) half-iterations;
     1 thread and every usable core.  gpu_bufs: (ncb, stride) softbuffer contents the GPU produced for the same S
-    subframes -- the CPU front end must reproduce them (parity_vs_gpu)."""
+    subframes -- the CPU front end must reproduce them (parity_vs_gpu).  ocfg_of(d): the oracle Cfg of resident
+    subframe d (default: the TM4 bench grant)."""
     import oracle
     from oracle import pdsch_chain as pc
     nthreads, host = host_cores()
-    S = min(src.n, 16)
+    S = min(src.n, S_max)
     iq = np.ascontiguousarray(src.iq_host(0, S))
+    if ocfg_of is None:
+        def ocfg_of(d):
+            return pc.Cfg(nof_prb=100, nof_ports=2, nof_rx=2, cell_id=1, cfi=1, sf_idx=(src.first + d) % 10, scheme=2,
+                          nof_layers=2, qm=[8, 8], tbs=[TBS, TBS], csi_enable=True, power_scale=True, p_a=0.0, p_b=1)
     cfgs = (oracle.FrontCfg * S)()
     for d in range(S):
-        cfgs[d] = oracle.front_cfg(pc.Cfg(nof_prb=100, nof_ports=2, nof_rx=2, cell_id=1, cfi=1,
-                                          sf_idx=(src.first + d) % 10, scheme=2, nof_layers=2, qm=[8, 8],
-                                          tbs=[TBS, TBS], csi_enable=True, power_scale=True, p_a=0.0,
-                                          p_b=1))
+        cfgs[d] = oracle.front_cfg(ocfg_of(d))
     stride = 18600
-    sb = np.zeros(S * 2 * 16 * stride, np.int16)
+    sb = np.zeros(S * 2 * max_cb * stride, np.int16)
     L = oracle.lib()
 
     def front(nt):
         reps, t0 = 0, time.perf_counter()
         while True:
-            assert L.orc_ue_dl_rx_batch(cfgs, S, iq.view(np.float32).reshape(-1), 2 * 2 * src.sf_len, sb, stride,
-                                        16, nt) == 0
+            assert L.orc_ue_dl_rx_batch(cfgs, S, iq.view(np.float32).reshape(-1), 2 * src.nof_rx * src.sf_len, sb,
+                                        stride, max_cb, nt) == 0
             reps += 1
             if time.perf_counter() - t0 >= budget_s / 4:
                 return (time.perf_counter() - t0) / (reps * S), reps
@@ -415,23 +421,24 @@ def cpu_baseline_pdsch(src, gpu_bufs, avg_its, budget_s):
     kind_t = "reference" if oracle.ref_available() else "port"
     fn = oracle.ref().ref_tdec_run_batch if kind_t == "reference" else L.orc_tdec_run_batch
     nh = max(1, int(math.ceil(avg_its)))
-    ncb = 2 * S * 16
-    out = np.zeros((ncb, 768), np.uint8)
-    bufs = sb.reshape(ncb, stride)
+    ncb = ntb * S * C
+    out = np.zeros((ncb, K // 8), np.uint8)
+    cpb = ntb * C  # code blocks per subframe
 
     def turbo(nt, n_cb, nhalf=nh):
         reps, t0 = 0, time.perf_counter()
         while True:
-            fn(bufs[:n_cb], stride, n_cb, 6144, nhalf, out[:n_cb], nt)
+            fn(bufs[:n_cb], stride, n_cb, K, nhalf, out[:n_cb], nt)
             reps += 1
             if time.perf_counter() - t0 >= budget_s / 4:
                 return (time.perf_counter() - t0) / reps / n_cb, reps
 
     f1, r_f1 = front(1)
     fN, r_fN = front(nthreads)
+    bufs = np.ascontiguousarray(sb.reshape(S, 2, max_cb, stride)[:, :ntb, :C].reshape(ncb, stride))
     # the CPU chain's decoder buffers vs the GPU's for the same subframes (systematic, parity 1, parity 2, tails):
     # equal up to the LSB-level LLR differences of the float32 FFT / estimator (tests: within +-2)
-    cols = np.r_[0:6144, 6176:6176 + 6144, 12352:12352 + 6144, 18528:18540]
+    cols = np.r_[0:K, K + 32:2 * K + 32, 2 * K + 64:3 * K + 64, 3 * K + 96:3 * K + 108]
     diff = np.abs(bufs[:, cols].astype(np.int32) - gpu_bufs[:ncb, cols].astype(np.int32))
     parity = {"max_abs_diff": int(diff.max()), "frac_entries_differing": round(float(np.mean(diff > 0)), 6)}
     t1, r_t1 = turbo(1, min(ncb, 64))
@@ -439,24 +446,25 @@ def cpu_baseline_pdsch(src, gpu_bufs, avg_its, budget_s):
     # the decoder-bound regime (fixed 8 half-iterations), one thread: per-CB fixed costs
     # (input copy, extract_input, decision) amortised as in SURVEY 6's turbodecoder_test figure
     t1_8, _ = turbo(1, min(ncb, 64), 8)
-    per_sf_1 = f1 + 32 * t1
-    per_sf_N = fN + 32 * tN
-    bits = 2 * TBS
+    per_sf_1 = f1 + cpb * t1
+    per_sf_N = fN + cpb * tN
+    bits = ntb * tbs
     return {
-        "value": round(bits / per_sf_N / 1e6, 2), "unit": "Mbps", "cb_per_s": round(32 / per_sf_N, 1),
+        "value": round(bits / per_sf_N / 1e6, 2), "unit": "Mbps", "cb_per_s": round(cpb / per_sf_N, 1),
         "cores": nthreads, "kind": "reference" if kind_t == "reference" else "port",
         "host": host,
-        "one_thread": {"value": round(bits / per_sf_1 / 1e6, 2), "cb_per_s": round(32 / per_sf_1, 1),
+        "one_thread": {"value": round(bits / per_sf_1 / 1e6, 2), "cb_per_s": round(cpb / per_sf_1, 1),
                        "front_ms_per_subframe": round(f1 * 1e3, 3),
                        "turbo_us_per_cb_halfit": round(t1 / nh * 1e6, 2),
                        "turbo_us_per_cb_halfit_at_8": round(t1_8 / 8 * 1e6, 2)},
         "all_cores": {"front_ms_per_subframe": round(fN * 1e3, 3),
                       "turbo_us_per_cb_halfit_per_thread": round(tN / nh * nthreads * 1e6, 2)},
         "parity_front_vs_gpu_softbuffers": parity,
-        "sample": (f"{S} distinct TM4 subframes of this batch: C front end (oracle/orc_front.c: float Stockham FFT, "
-                   f"oracle chest / MMSE+CSI / demap / descramble / rate dematching) {r_f1}+{r_fN} passes at 1 and "
-                   f"{nthreads} threads; their {ncb} CBs through the reference AVX2 turbo decoder ({kind_t}, "
-                   f"oracle/_ref) x {nh} half-iterations (= ceil of the GPU run's mean), {r_t1}+{r_tN} passes"),
+        "sample": (f"{S} distinct {label} subframes of this batch: C front end (oracle/orc_front.c: float Stockham "
+                   f"FFT, oracle chest / MMSE+CSI / demap / descramble / rate dematching) {r_f1}+{r_fN} passes at 1 "
+                   f"and {nthreads} threads; their {ncb} CBs (K={K}) through the reference AVX2 turbo decoder "
+                   f"({kind_t}, oracle/_ref) x {nh} half-iterations (= ceil of the GPU run's mean), "
+                   f"{r_t1}+{r_tN} passes"),
         "turbo_kind": kind_t,
     }
 
@@ -470,34 +478,96 @@ def softbuffer_contents(rx, ncb):
     return C.cast(buf, C.c_void_p).value, stride.value
 
 
-def map_probe(rx, B, local, sample_check=True):
-    """Dominant kernel: the MAP half-iteration over this batch's 32 B code blocks (the softbuffers hold the
-    rate-dematched LLRs of the last step), a fixed 8 half-iterations without early stop (configs[1]'s regime on
-    the e2e code blocks), HIP events on the decoder's stream.  Returns (roofline, roofline_valu, fixed8 dict)."""
+def map_probe(rx, ncb, local, K=6144):
+    """Dominant kernel: the MAP half-iteration over this batch's ncb code blocks (the first ncb softbuffer slots hold
+    the rate-dematched LLRs of the last step), a fixed 8 half-iterations without early stop (configs[1]'s regime
+    on the e2e code blocks), HIP events on the decoder's stream.  Returns (roofline, roofline_valu, fixed8 dict)."""
     from srsran_amd import lib
     from srsran_amd.tdec import DeviceBuffer, TdecBatch
-    ptr, stride = softbuffer_contents(rx, 2 * B * 16)
-    ncb = 2 * B * 16
-    d_out = DeviceBuffer(ncb * 768, local)
+    ptr, stride = softbuffer_contents(rx, ncb)
+    d_out = DeviceBuffer(ncb * (K // 8), local)
     dec = TdecBatch(local)
-    dec.run_dev(ptr, stride, ncb, 6144, 8, d_out.ptr)
+    dec.run_dev(ptr, stride, ncb, K, 8, d_out.ptr)
     lib().mi355_device_sync()
     t0 = time.perf_counter()
-    dec.run_dev(ptr, stride, ncb, 6144, 8, d_out.ptr)
+    dec.run_dev(ptr, stride, ncb, K, 8, d_out.ptr)
     lib().mi355_device_sync()
     wall = time.perf_counter() - t0
     dec.set_profiling(True)
     for _ in range(2):
-        dec.run_dev(ptr, stride, ncb, 6144, 8, d_out.ptr)
+        dec.run_dev(ptr, stride, ncb, K, 8, d_out.ptr)
     kms, kl = dec.kernel_stats()
     dec.set_profiling(False)
-    roof, valu = tdec_roofline(kms, kl, ncb, 6144)
+    roof, valu = tdec_roofline(kms, kl, ncb, K)
     fixed8 = {"code_blocks": ncb, "half_iterations": 8, "ms": round(wall * 1e3, 3),
-              "code_blocks_per_s": round(ncb / wall, 1), "mbps": round(ncb * 6120 / wall / 1e6, 1),
-              "note": "the batch's 65,536 rate-dematched CBs decoded with a fixed 8 half-iterations (no early stop), "
-                      "K-24 = 6,120 information bits per CB"}
+              "code_blocks_per_s": round(ncb / wall, 1), "mbps": round(ncb * (K - 24) / wall / 1e6, 1),
+              "note": f"the batch's {ncb:,} rate-dematched CBs decoded with a fixed 8 half-iterations (no early stop), "
+                      f"K-24 = {K - 24:,} information bits per CB"}
     dec.close()
     return roof, valu, fixed8, (ptr, stride, d_out)
+
+
+def config1_generic(local, budget_s=2.0, with_cpu=True):
+    """configs[0] (turbodecoder_test -l 6144 -i 8 -d 1, turbodecoder_test.c:106-310): the GENERIC max-log-MAP on
+    ONE K=6144 code block in the linear [s p0 p1] + tails layout, 8 half-iterations, on the reference's own
+    input (tests/golden/tdec_generic.npz, recorded from the reference harness).  GPU: the srslte_tdec_* drop-in
+    (init_manual GENERIC + force_not_sb + run_all from a host buffer, as the test calls it) -- one code block is a
+    latency figure; the batched generic kernel on 16,384 copies gives its throughput.  CPU: the reference's
+    generic decoder (oracle/_ref) on one host core.  Parity: every output equals the golden trace."""
+    from srsran_amd import lib
+    from srsran_amd.srslte import SRSLTE_TDEC_GENERIC, SrslteTdec
+    from srsran_amd.tdec import DeviceBuffer, TdecBatch
+    z = np.load(os.path.join(ROOT, "tests", "golden", "tdec_generic.npz"), allow_pickle=False)
+    c = next(i for i in range(int(z["ncases"])) if int(z[f"c{i}_K"]) == 6144)
+    K, lin, want = 6144, z[f"c{c}_lin"], z[f"c{c}_trace"][-1]
+    buf = np.zeros(3 * (K + 32) + 12, np.int16)
+    buf[: lin.size] = lin
+    dec = SrslteTdec(6144, SRSLTE_TDEC_GENERIC)
+    dec.force_not_sb()
+    ok = np.array_equal(dec.run_all(buf.copy(), 8, K), want)
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s / 4:
+        dec.run_all(buf.copy(), 8, K)
+        reps += 1
+    gpu_one = (time.perf_counter() - t0) / reps
+    dec.free()
+    n = 16384
+    stride = (3 * K + 12 + 7) // 8 * 8
+    host = np.zeros((n, stride), np.int16)
+    host[:, : lin.size] = lin
+    d_in = DeviceBuffer(host.nbytes, local).upload(host)
+    d_out = DeviceBuffer(n * (K // 8), local)
+    tb = TdecBatch(local)
+    lib().mi355_tdec_batch_set_impl(tb.h, 1)  # MI355_TDEC_GENERIC
+    tb.run_dev(d_in.ptr, stride, n, K, 8, d_out.ptr)
+    lib().mi355_device_sync()
+    t0 = time.perf_counter()
+    tb.run_dev(d_in.ptr, stride, n, K, 8, d_out.ptr)
+    lib().mi355_device_sync()
+    gpu_batch = time.perf_counter() - t0
+    outs = d_out.download(np.zeros((n, K // 8), np.uint8))
+    ok_batch = bool((outs == want[None, :]).all())
+    tb.close()
+    res = {"workload": "configs[0]: turbodecoder_test -l 6144 -i 8 -d 1 (generic MAP, linear layout, 8 half-its)",
+           "gpu_one_cb_us": round(gpu_one * 1e6, 1), "gpu_one_cb_path": "srslte_tdec_run_all drop-in, host buffers",
+           "gpu_batch_cbs": n, "gpu_batch_cb_per_s": round(n / gpu_batch, 1),
+           "gpu_batch_mbps": round(n * K / gpu_batch / 1e6, 1), "bit_exact_vs_golden": bool(ok and ok_batch)}
+    if with_cpu:
+        import oracle
+        if oracle.ref_available():
+            ref = oracle.RefTdec(generic=True)
+            okc = np.array_equal(ref.run(buf, K, 8), want)
+            reps, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < budget_s / 2:
+                ref.run(buf, K, 8)
+                reps += 1
+            cpu_one = (time.perf_counter() - t0) / reps
+            res["cpu_baseline"] = {"value_us_per_cb": round(cpu_one * 1e6, 1), "cb_per_s": round(1 / cpu_one, 1),
+                                   "mbps": round(K / cpu_one / 1e6, 2), "cores": 1, "kind": "reference",
+                                   "bit_exact_vs_golden": bool(okc),
+                                   "sample": f"{reps} decodes of the golden K=6144 block, reference generic "
+                                             "decoder (turbodecoder_gen.c) on one host thread"}
+    return res
 
 
 def run_pdsch(args, world, rank, local, pg):
@@ -600,7 +670,7 @@ def run_pdsch(args, world, rank, local, pg):
             last = rx.bind(src, 0, min(B, src.n))
             rx.step(last, stages)
             res["stage_ms"] = {k: round(v, 3) for k, v in stages.items()}
-        roof, valu, fixed8, (ptr, stride, _d_out) = map_probe(rx, B, local)
+        roof, valu, fixed8, (ptr, stride, _d_out) = map_probe(rx, 32 * B, local)
         res["roofline"] = roof
         res["roofline_valu"] = valu
         res["decoder_bound_fixed8"] = fixed8
@@ -611,9 +681,82 @@ def run_pdsch(args, world, rank, local, pg):
             res["cpu_baseline"] = cpu_baseline_pdsch(src, gb, its, args.cpu_seconds)
             # the fixed-8 decisions of a CB sample against the reference decoder (cpu_baseline leg)
             res["decoder_bound_fixed8"]["parity_vs_reference"] = fixed8_parity(gb[:64], _d_out)
+        if rank == 0 and world == 1:
+            res["config1_generic"] = config1_generic(local, with_cpu=not args.no_cpu)
     if not ctrl and not args.total_subframes and not args.no_waterfall:
         res["e2e_waterfall"] = waterfall(args, cell, B, src, rx, pg, local, world)
     rx.pool.close()
+    src.close()
+    return res
+
+
+SISO_TBS, SISO_K, SISO_C = 15840, 5312, 3
+
+
+def run_siso(args, world, rank, local, pg):
+    """configs[2]: phy_dl_test -p 100 -t 1 -m 9 (lib/test/phy/phy_dl_test.c:308-660) at batch scale: B subframes per
+    GPU per step of a 20 MHz SISO cell (1 port, 1 rx, CFI 1, DCI format 1 over every RBG, MCS 9 QPSK, TBS 15,840 =
+    3 CBs of K = 5312), no noise and the DCI at the test's UE-specific locations, synthesised by the GPU generator;
+    the UE side is phy_dl_test's work_ue as one mi355_ue_dl_find_and_decode_batch (OFDM, estimation, PCFICH /
+    PDCCH blind search, grant, PDSCH, DL-SCH) from I/Q resident in HBM."""
+    from srsran_amd import lib, synth
+    cell, nrx = synth.phy_dl_test_cell(100, 0)
+    B = args.subframes
+    lo = rank * B
+    nb = SISO_TBS // 8
+    plans = synth.phy_dl_test_plans(cell, 0, 9, False, nof_subframes=B, first=lo)
+    src = synth.DlSource(cell, nrx, B, nb, local)
+    src.generate(lo, plans, args.siso_snr, args.seed, ctrl=True)
+    rx = synth.DlReceiver(cell, nrx, B, nb, local, ctrl=True, max_cb=SISO_C)
+    bound = rx.bind(src, 0, B, tb_major=True)  # TB0 code blocks contiguous in the pool (MAP probe)
+    for _ in range(args.warmup):
+        rx.step(bound)
+    lib().mi355_device_sync()
+    barrier(pg, local)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rx.step(bound)
+    lib().mi355_device_sync()
+    barrier(pg, local)
+    dt = max_over_ranks(pg, local, time.perf_counter() - t0)
+    bits = rx.crc_bits(B).reshape(B, 2)[:, 0].copy()  # one TB per subframe
+    gathered = gather_bitmap(pg, local, bits)
+    ok_pay = int(sum_over_ranks(pg, local, rx.payload_ok(src, bound)))
+    its = rx.avg_its(B) * 2  # the disabled second TB reads 0
+    ok_tbs = int(gathered.sum()) if rank == 0 else 0
+    mbps = whole_job_rate(world, B * SISO_TBS, args.steps, dt) / 1e6 * (ok_tbs / (B * world))
+    res = {"metric": "PDSCH decoded Mbps + code-blocks/sec, 20 MHz SISO QPSK MCS 9 (configs[2], phy_dl_test -p 100 "
+                     "-t 1 -m 9)",
+           "value": round(mbps, 1), "unit": "Mbps", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "fp32+int16", "data": "synthetic",
+           "config": {"workload": f"phy_dl_test -p 100 -t 1 -m 9 work_ue as mi355_ue_dl_find_and_decode_batch: {B} "
+                                  "subframes/GPU/batch from time-domain I/Q, 1 port / 1 rx, CFI 1, DCI format 1 at the "
+                                  "test's UE locations, TBS 15840 (3 x K=5312), "
+                                  + ("no noise (as phy_dl_test)" if args.siso_snr is None else f"{args.siso_snr:g} dB"),
+                      "subframes_per_gpu_batch": B, "code_blocks_per_gpu_batch": SISO_C * B,
+                      "parallelism": f"dp{world}"},
+           "code_blocks_per_s": round(world * SISO_C * B * args.steps / dt, 1),
+           "subframes_per_s": round(world * B * args.steps / dt, 1),
+           "crc_ok_tbs": f"{ok_tbs}/{B * world}", "crc_bitmap": bitmap_summary(gathered, B * world) if rank == 0 else None,
+           "payload_checked_tbs": f"{ok_pay}/{B * world}", "avg_half_iterations": round(its, 3)}
+    if not args.no_roofline:
+        roof, valu, fixed8, (ptr, stride, _d_out) = map_probe(rx, SISO_C * B, local, K=SISO_K)
+        res["roofline"], res["roofline_valu"], res["decoder_bound_fixed8"] = roof, valu, fixed8
+        if rank == 0 and world == 1 and not args.no_cpu:
+            from oracle import pdsch_chain as pc
+            S = min(B, 48)
+            gb = np.zeros((S * SISO_C, stride), np.int16)
+            lib().mi355_memcpy_d2h(gb.ctypes.data, ptr, gb.nbytes)
+
+            def ocfg(d):
+                return pc.Cfg(nof_prb=100, nof_ports=1, nof_rx=1, cell_id=1, cfi=1, sf_idx=(lo + d) % 10, scheme=0,
+                              nof_layers=1, qm=[2], tbs=[SISO_TBS], csi_enable=False, power_scale=True, p_a=0.0,
+                              p_b=0)
+            res["cpu_baseline"] = cpu_baseline_pdsch(src, gb, its, args.cpu_seconds, ocfg_of=ocfg, K=SISO_K,
+                                                     C=SISO_C, ntb=1, tbs=SISO_TBS, max_cb=SISO_C, S_max=S,
+                                                     label="SISO QPSK")
+    rx.close()
     src.close()
     return res
 
@@ -925,6 +1068,8 @@ def main():
         res = run_enb(args, world, rank, local, pg)
     elif args.workload == "plumbing":
         res = run_plumbing(args, world, rank, local, pg)
+    elif args.workload == "siso_qpsk":
+        res = run_siso(args, world, rank, local, pg)
     else:
         res = run_pdsch(args, world, rank, local, pg)
     if rank == 0:

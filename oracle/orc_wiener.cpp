@@ -417,3 +417,15 @@ void orc_uniform_int_draws(uint32_t seed, int lo, int hi, uint32_t n, int32_t* o
 }
 
 } // extern "C"
+
+// the standard library the restatement's draws come from: libstdc++'s release date (__GLIBCXX__), 0 for another
+// library.  The GPU kernel restates libstdc++'s uniform_int_distribution as of GCC 11 (Lemire's nearly
+// divisionless method); a reference built against an older libstdc++ or libc++ draws other sub-bands.
+extern "C" long orc_stdlib_glibcxx(void)
+{
+#ifdef __GLIBCXX__
+  return (long)__GLIBCXX__;
+#else
+  return 0;
+#endif
+}

@@ -157,6 +157,8 @@ struct mi355_wiener_dl {
   WienerBank  bank;
   uint32_t    nlinks = 0;
   hipStream_t own    = nullptr;
+  char*       d_io   = nullptr; // per-call snr | ready block, grow-only (no hipFree, which synchronises the device)
+  size_t      io_cap = 0;
 };
 
 extern "C" {
@@ -186,6 +188,7 @@ void mi355_wiener_dl_free(mi355_wiener_dl_t* q)
     (void)hipStreamSynchronize(q->own);
     (void)hipStreamDestroy(q->own);
   }
+  if (q->d_io) (void)hipFree(q->d_io);
   delete q;
 }
 
@@ -207,11 +210,20 @@ int mi355_wiener_dl_run_batch(mi355_wiener_dl_t* q, const uint32_t* link, uint32
   CHECK_HIP(hipSetDevice(q->bank.device));
   hipStream_t    s  = stream ? (hipStream_t)stream : q->own;
   const uint32_t np = d.ntx * d.nrx;
-  // snr and ready live in a device block next to nothing else: upload / read back around the launch
-  float*   d_snr   = nullptr;
-  int32_t* d_ready = nullptr;
-  CHECK_HIP(hipMalloc(&d_snr, (size_t)njobs * np * 4 + 4));
-  CHECK_HIP(hipMalloc(&d_ready, (size_t)njobs * np * 4 + 4));
+  // snr and ready live in the object's grow-only device block: upload / read back around the launch
+  const size_t part = ((size_t)njobs * np * 4 + 255) / 256 * 256;
+  if (2 * part > q->io_cap) {
+    if (q->d_io) {
+      CHECK_HIP(hipStreamSynchronize(s));
+      CHECK_HIP(hipFree(q->d_io));
+      q->d_io   = nullptr;
+      q->io_cap = 0;
+    }
+    CHECK_HIP(hipMalloc(&q->d_io, 2 * part + 256));
+    q->io_cap = 2 * part + 256;
+  }
+  float*   d_snr   = (float*)q->d_io;
+  int32_t* d_ready = (int32_t*)(q->d_io + part);
   int r = MI355_SUCCESS;
   if (hipMemcpy(d_snr, snr, (size_t)njobs * np * 4, hipMemcpyHostToDevice) != hipSuccess) r = MI355_ERROR;
   std::vector<WienerJob> jobs(njobs);
@@ -232,8 +244,6 @@ int mi355_wiener_dl_run_batch(mi355_wiener_dl_t* q, const uint32_t* link, uint32
   if (!r && njobs &&
       hipMemcpy(&draws, q->bank.slabs[link[0]] + offsetof(WienerLinkState, draws), 4, hipMemcpyDeviceToHost) != hipSuccess)
     r = MI355_ERROR;
-  (void)hipFree(d_snr);
-  (void)hipFree(d_ready);
   return r ? r : (int)draws;
 }
 

@@ -177,8 +177,9 @@ class DlReceiver:
     def ce_ptr(self, k: int, p: int, r: int) -> int:
         return self.d_ce.ptr + ((k * self.np + p) * self.nof_rx + r) * self.G * 8
 
-    def bind(self, src: DlSource, k0: int, n: int):
-        """Job tables for resident subframes [k0, k0 + n) of src (n <= B); softbuffers 2k, 2k + 1."""
+    def bind(self, src: DlSource, k0: int, n: int, tb_major: bool = False):
+        """Job tables for resident subframes [k0, k0 + n) of src (n <= B); softbuffers 2k, 2k + 1 (tb_major: k and
+        B + k, so the first TBs' code blocks are contiguous in the pool)."""
         from .ue_dl import DlSfJob
         assert n <= self.B
         jobs, sfs, cfgs = (DlSfJob * n)(), (P.DlSfCfg * n)(), (P.PdschCfg * n)()
@@ -193,7 +194,7 @@ class DlReceiver:
                     j.ce[p][r] = self.ce_ptr(k, p, r)
             sfs[k] = P.DlSfCfg(pl.tti % 10, pl.cfi)
             cfgs[k] = pl.cfg
-            cfgs[k].softbuffer[0], cfgs[k].softbuffer[1] = 2 * k, 2 * k + 1
+            cfgs[k].softbuffer[0], cfgs[k].softbuffer[1] = (k, self.B + k) if tb_major else (2 * k, 2 * k + 1)
             if self.ctrl:
                 u = self.ue_cfgs[k]
                 u.tm, u.use_tbs_index_alt = pl.tm, int(pl.tbs_alt)
@@ -279,20 +280,20 @@ def phy_dl_test_cell(nof_prb: int, tm: int, cell_id: int = 1) -> tuple[P.Cell, i
 
 
 def phy_dl_test_plans(cell: P.Cell, tm: int, mcs: int, enable_256qam: bool, nof_subframes: int | None = None,
-                      cfi: int = 1, rnti: int = 0x1234) -> list[SfPlan]:
+                      cfi: int = 1, rnti: int = 0x1234, first: int = 0) -> list[SfPlan]:
     """The subframes phy_dl_test transmits (phy_dl_test.c:412-540): DCI format 1 (TM1/TM2), 2A (TM3) or 2 (TM4,
     pinfo 0), resource allocation type 0 over every RBG, rv 0, the DCI at UE-specific location
     (sf / 10) % nof_locations of subframe sf % 10, MCS 0 (6 PRB) / min(MCS, 27) (15 PRB) in subframes 0 and 5;
     eNodeB PDSCH p_a 0 dB, p_b 1 for TM2-4 (:173-175); the UE side as work_ue sets it (:213-219, :571-575:
     MMSE, power_scale on, CSI off, 10 iterations).  nof_subframes defaults to the number of UE locations over
-    one frame, as the test does (:427-429)."""
+    one frame, as the test does (:427-429); first: global index of the first subframe (a shard of a longer run)."""
     from . import pdcch as D
     nloc = [D.ue_locations(D.nof_cce(cell, cfi), sf, rnti) for sf in range(10)]
     if nof_subframes is None:
         nof_subframes = sum(len(v) for v in nloc)
     fmt = D.FORMAT1 if tm < 2 else (D.FORMAT2A if tm == 2 else D.FORMAT2)
     plans = []
-    for sf_idx in range(nof_subframes):
+    for sf_idx in range(first, first + nof_subframes):
         tti = sf_idx % 10
         d = D.DciDl()
         d.rnti, d.format, d.alloc_type = rnti, fmt, D.ALLOC_TYPE0

@@ -74,6 +74,8 @@ def test_library_loads_without_a_gpu():
     import ctypes
     L = ctypes.CDLL(LIB)
     L.srslte_tdec_autoimp_get_subblocks.restype = ctypes.c_uint32
+    L.srslte_tdec_autoimp_get_subblocks.argtypes = [ctypes.c_uint32]
+    L.srslte_symbol_sz.argtypes = [ctypes.c_uint32]
     assert L.srslte_tdec_autoimp_get_subblocks(6144) == 16
     assert L.srslte_tdec_autoimp_get_subblocks(512) == 8
     assert L.srslte_tdec_autoimp_get_subblocks(40) == 0

@@ -9,6 +9,21 @@ import pytest
 from oracle import wiener_chain as wc
 
 
+def test_stdlib_draws_are_libstdcxx_lemire():
+    """The restatement's sub-band draws come from the host's standard library: libstdc++ with Lemire's
+    uniform_int_distribution (GCC 11 and later, __GLIBCXX__ >= 20210427), which the GPU kernel restates.  The
+    reference's srslte_random_uniform_int_dist draws the same only when built against such a library."""
+    import ctypes
+    import oracle
+    f = oracle.lib().orc_stdlib_glibcxx
+    f.restype, f.argtypes = ctypes.c_long, []
+    v = f()
+    if v < 20210427:
+        pytest.skip(f"oracle built against {'libstdc++ ' + str(v) if v else 'a non-libstdc++ library'}: its "
+                    "uniform_int_distribution is not Lemire's, so the Wiener sub-band draws are not the GPU's")
+    assert v >= 20210427
+
+
 @pytest.mark.parametrize("hi", [3, 12, 50, 1, 0])
 def test_uniform_int_is_lemire(hi):
     std = wc.std_uniform_int(0xDEAD, 0, hi, 300)
