@@ -378,9 +378,10 @@ def Tm4Source(cell, n_max, device, ctrl=False, chunk=256):
 
 
 def Tm4Rx(cell, B, device, ctrl=False):
-    """The UE side of one TM4 batch of B subframes (srsran_amd.synth.DlReceiver)."""
+    """The UE side of one TM4 batch of B subframes (srsran_amd.synth.DlReceiver); the AVERAGE estimate is written to
+    row 0 only (mi355_chest_dl_cfg_t.ce_rows = 1: the fused chain reads nothing else)."""
     from srsran_amd.synth import DlReceiver
-    return DlReceiver(cell, 2, B, NB, device, ctrl=ctrl, max_cb=16)
+    return DlReceiver(cell, 2, B, NB, device, ctrl=ctrl, max_cb=16, ce_rows=1)
 
 
 def cpu_baseline_pdsch(src, gpu_bufs, avg_its, budget_s, ocfg_of=None, K=6144, C=16, ntb=2, tbs=TBS, max_cb=16,
@@ -707,7 +708,7 @@ def run_siso(args, world, rank, local, pg):
     plans = synth.phy_dl_test_plans(cell, 0, 9, False, nof_subframes=B, first=lo)
     src = synth.DlSource(cell, nrx, B, nb, local)
     src.generate(lo, plans, args.siso_snr, args.seed, ctrl=True)
-    rx = synth.DlReceiver(cell, nrx, B, nb, local, ctrl=True, max_cb=SISO_C)
+    rx = synth.DlReceiver(cell, nrx, B, nb, local, ctrl=True, max_cb=SISO_C, ce_rows=1)
     bound = rx.bind(src, 0, B, tb_major=True)  # TB0 code blocks contiguous in the pool (MAP probe)
     for _ in range(args.warmup):
         rx.step(bound)

@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include "ue_dl_internal.h"
+#include "xcd.h"
 
 namespace mi355 {
 
@@ -141,7 +142,7 @@ __device__ void chest_tail(const ChestArgs& a, const ChestJob& J, const float2* 
     float v[1] = {0.f};
     if (threadIdx.x < 62) {
       const uint32_t k = (a.nsymb - 1) * nre + nre / 2 - 31 + threadIdx.x;
-      const float2   c = J.ce[k], p = a.pss[threadIdx.x], y = J.grid[k];
+      const float2   c = J.ce[a.ce_rows == 1 ? k % nre : k], p = a.pss[threadIdx.x], y = J.grid[k];
       const float2   t = make_float2(c.x * p.x - c.y * p.y - y.x, c.x * p.y + c.y * p.x - y.y);
       v[0]             = cpw(t);
     }
@@ -187,7 +188,9 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
   __shared__ float  filt[16];
   __shared__ uint32_t flen_s;
 
-  const ChestJob J    = a.jobs[blockIdx.x];
+  // the blocks of one subframe's (rx, port) estimates read the same pilot rows: keep them on one L2
+  const uint32_t blk  = xcd_chunk(blockIdx.x, gridDim.x);
+  const ChestJob J    = a.jobs[blk];
   const uint32_t nprb = a.nof_prb, nre = 12 * nprb, nref = 2 * nprb, port = J.port;
   const uint32_t nsym = port < 2 ? 4 : 2, np = nsym * nref;
   const float2*  crs  = a.pilots + (size_t)((port / 2) * 10 + J.sf) * (4 * nref);
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
     acc[0] += cpw(x);
     const float2 e = cprod_conj(x, crs[k]);
     pe[k]          = e;
-    if (a.pe_out) a.pe_out[(size_t)blockIdx.x * (4 * nref) + k] = e; // the Wiener estimator's pilots (wiener_kernels.hip)
+    if (a.pe_out) a.pe_out[(size_t)blk * (4 * nref) + k] = e; // the Wiener estimator's pilots (wiener_kernels.hip)
     acc[2] += e.x;
     acc[3] += e.y;
   }
@@ -383,7 +386,7 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
     (void)off_end;
   }
   __syncthreads();
-  const uint32_t nrows = 2 * a.nsymb;
+  const uint32_t nrows = a.ce_rows == 1 ? 1u : 2 * a.nsymb;
   for (uint32_t k = threadIdx.x; k < nrows * nre; k += blockDim.x) J.ce[k] = row[k % nre];
   chest_tail(a, J, pe, acc, noise, np, nsym, red);
 }

@@ -46,6 +46,7 @@ struct CtrlArgs {
   uint32_t        llr_stride;
   uint32_t*       cfi;         // [job]
   float*          corr;        // [job][3]
+  uint32_t        ce_row;      // non-zero: the estimates are time-invariant, read at (re mod ce_row) (row 0)
 };
 
 // Blind decoding: one wave per (job, candidate slot, DCI size)

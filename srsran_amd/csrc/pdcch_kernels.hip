@@ -20,13 +20,15 @@ namespace mi355 {
 namespace {
 
 __device__ __forceinline__ float2 ld(const float2* p, uint32_t i) { return p[i]; }
+// an estimate at grid index re: row 0 when the estimates are time-invariant (CtrlArgs::ce_row)
+__device__ __forceinline__ float2 ldh(const CtrlArgs& a, const float2* p, uint32_t re) { return p[a.ce_row ? re % a.ce_row : re]; }
 
 // 1 port: x = sum_r y_r conj(h_r) / (sum_r |h_r|^2 + noise)
 __device__ __forceinline__ float2 eq_single(const CtrlArgs& a, const CtrlJob& J, uint32_t re, float noise)
 {
   float rr = 0.f, ri = 0.f, hh = 0.f;
   for (uint32_t r = 0; r < a.nof_rx; r++) {
-    const float2 y = ld(J.grid[r], re), h = ld(J.ce[0][r], re);
+    const float2 y = ld(J.grid[r], re), h = ldh(a, J.ce[0][r], re);
     rr += y.x * h.x + y.y * h.y;
     ri += y.y * h.x - y.x * h.y;
     hh += h.x * h.x + h.y * h.y;
@@ -41,8 +43,8 @@ __device__ __forceinline__ void eq_pair(const CtrlArgs& a, const CtrlJob& J, uin
 {
   float x0r = 0.f, x0i = 0.f, x1r = 0.f, x1i = 0.f, hh = 0.f;
   for (uint32_t p = 0; p < a.nof_rx; p++) {
-    const float2 h00 = ld(J.ce[0][p], re0), h01 = ld(J.ce[0][p], re1), h10 = ld(J.ce[1][p], re0),
-                 h11 = ld(J.ce[1][p], re1);
+    const float2 h00 = ldh(a, J.ce[0][p], re0), h01 = ldh(a, J.ce[0][p], re1), h10 = ldh(a, J.ce[1][p], re0),
+                 h11 = ldh(a, J.ce[1][p], re1);
     const float2 r0 = ld(J.grid[p], re0), r1 = ld(J.grid[p], re1);
     const float a0r = h00.x * r0.x + h00.y * r0.y, a0i = h00.x * r0.y - h00.y * r0.x;
     const float b0r = h11.x * r1.x + h11.y * r1.y, b0i = h11.y * r1.x - h11.x * r1.y;
@@ -77,8 +79,8 @@ __device__ __forceinline__ void eq_quad(const CtrlArgs& a, const CtrlJob& J, con
 {
   float hh02 = 0.f, hh13 = 0.f, x[4][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
   for (uint32_t p = 0; p < a.nof_rx; p++) {
-    const float2 h0 = ld(J.ce[0][p], re[0]), h1 = ld(J.ce[1][p], re[2]), h2 = ld(J.ce[2][p], re[0]),
-                 h3 = ld(J.ce[3][p], re[2]);
+    const float2 h0 = ldh(a, J.ce[0][p], re[0]), h1 = ldh(a, J.ce[1][p], re[2]), h2 = ldh(a, J.ce[2][p], re[0]),
+                 h3 = ldh(a, J.ce[3][p], re[2]);
     hh02 += (h0.x * h0.x + h0.y * h0.y) + (h2.x * h2.x + h2.y * h2.y);
     hh13 += (h1.x * h1.x + h1.y * h1.y) + (h3.x * h3.x + h3.y * h3.y);
     const float2 r0 = ld(J.grid[p], re[0]), r1 = ld(J.grid[p], re[1]), r2 = ld(J.grid[p], re[2]),

@@ -161,6 +161,7 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
     a.llr_stride = stride;
     a.cfi        = d_cfi + o;
     a.corr       = d_corr + 3 * (size_t)o;
+    a.ce_row     = ce_row;
     CHECK_HIP(ctrl_launch_llr(a, m, s));
     BlindArgs b{};
     b.jobs       = (const BlindJob*)(base + b_jobs) + o;

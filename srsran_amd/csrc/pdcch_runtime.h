@@ -26,6 +26,7 @@ struct CtrlState {
   DciCand*     last_cand = nullptr;
   std::unordered_map<uint64_t, BlindJob> plans; // search plan per (rnti, subframe, UE configuration)
   std::vector<BlindJob>                  plan_of; // this call's plan per subframe
+  uint32_t                               ce_row = 0; // set by the caller: estimates time-invariant, read row 0
 
   // launch(): the arena layout and the per-chunk completion events of the pending call
   size_t                b_cfi_ = 0, b_corr_ = 0;

@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "pdsch_internal.h"
+#include "xcd.h"
 
 namespace mi355 {
 
@@ -839,13 +840,17 @@ constexpr int FU_P = PDSCH_FU_P; // RE pairs per thread
 // grid (pair blocks of the largest job, jobs): work item = RE pair (2pr, 2pr+1), the granule of the LLR kernel.
 // One instantiation per (layer-0, layer-1) modulation order pair present in the batch (0: layer not decoded);
 // blocks of jobs with another pair return at once.
+// 1-D grid of nblk blocks per job: the blocks of one job run on one XCD (xcd_chunk), so the row-0 estimates all
+// 14 symbols of the subframe read, and the RE map, stay in that XCD's L2 instead of being fetched per block
 template <int QM0, int QM1>
-__global__ __launch_bounds__(256) void pdsch_eq_llr(const PdschJobDev* __restrict__ jobs)
+__global__ __launch_bounds__(256) void pdsch_eq_llr(const PdschJobDev* __restrict__ jobs, uint32_t nblk)
 {
-  const PdschJobDev& J     = jobs[blockIdx.y];
+  const uint32_t     L     = xcd_chunk(blockIdx.x, gridDim.x);
+  const uint32_t     bx    = L % nblk;
+  const PdschJobDev& J     = jobs[L / nblk];
   const uint32_t     pairs = (J.nof_re + 1) / 2;
-  const uint32_t     base  = blockIdx.x * 256 * FU_P + threadIdx.x;
-  if (!J.fused || J.fused_key != (uint32_t)(QM0 * 16 + QM1) || blockIdx.x * 256 * FU_P >= pairs) return;
+  const uint32_t     base  = bx * 256 * FU_P + threadIdx.x;
+  if (!J.fused || J.fused_key != (uint32_t)(QM0 * 16 + QM1) || bx * 256 * FU_P >= pairs) return;
   // the codeword descriptors and csi maxima, once per block
   __shared__ PdschCwDev cwd[2];
   __shared__ uint32_t   cmb[2];
@@ -946,14 +951,14 @@ __global__ __launch_bounds__(256) void pdsch_eq_llr(const PdschJobDev* __restric
 }
 
 template <int QM0>
-static void launch_eq_llr_1(uint32_t qm1, const dim3& g, const PdschJobDev* jobs, hipStream_t s)
+static void launch_eq_llr_1(uint32_t qm1, const dim3& g, const PdschJobDev* jobs, uint32_t nblk, hipStream_t s)
 {
   switch (qm1) {
-    case 0: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 0>), g, dim3(256), 0, s, jobs); break;
-    case 2: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 2>), g, dim3(256), 0, s, jobs); break;
-    case 4: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 4>), g, dim3(256), 0, s, jobs); break;
-    case 6: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 6>), g, dim3(256), 0, s, jobs); break;
-    default: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 8>), g, dim3(256), 0, s, jobs); break;
+    case 0: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 0>), g, dim3(256), 0, s, jobs, nblk); break;
+    case 2: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 2>), g, dim3(256), 0, s, jobs, nblk); break;
+    case 4: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 4>), g, dim3(256), 0, s, jobs, nblk); break;
+    case 6: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 6>), g, dim3(256), 0, s, jobs, nblk); break;
+    default: hipLaunchKernelGGL((pdsch_eq_llr<QM0, 8>), g, dim3(256), 0, s, jobs, nblk); break;
   }
 }
 
@@ -966,13 +971,13 @@ hipError_t pdsch_launch_fused(const PdschJobDev* jobs, uint32_t njobs, uint32_t 
   for (uint32_t k = 0; k < nkeys; k++) {
     const uint32_t q0 = keys[k] >> 4, q1 = keys[k] & 15;
     for (uint32_t j0 = 0; j0 < njobs; j0 += 65535) {
-      const dim3 g(nblk, std::min(65535u, njobs - j0));
+      const dim3 g(nblk * std::min(65535u, njobs - j0));
       switch (q0) {
-        case 0: launch_eq_llr_1<0>(q1, g, jobs + j0, s); break;
-        case 2: launch_eq_llr_1<2>(q1, g, jobs + j0, s); break;
-        case 4: launch_eq_llr_1<4>(q1, g, jobs + j0, s); break;
-        case 6: launch_eq_llr_1<6>(q1, g, jobs + j0, s); break;
-        default: launch_eq_llr_1<8>(q1, g, jobs + j0, s); break;
+        case 0: launch_eq_llr_1<0>(q1, g, jobs + j0, nblk, s); break;
+        case 2: launch_eq_llr_1<2>(q1, g, jobs + j0, nblk, s); break;
+        case 4: launch_eq_llr_1<4>(q1, g, jobs + j0, nblk, s); break;
+        case 6: launch_eq_llr_1<6>(q1, g, jobs + j0, nblk, s); break;
+        default: launch_eq_llr_1<8>(q1, g, jobs + j0, nblk, s); break;
       }
     }
   }

@@ -90,6 +90,7 @@ struct ChestArgs {
   float           sync_k;               // srslte_symbol_sz / 6 (chest_dl_estimate_correct_sync_error)
   uint32_t        symbol_sz;
   float2*         pe_out; // WIENER: the LS pilot estimates of every (job, rx, port), [4][2 nof_prb] each (or null)
+  uint32_t        ce_rows; // AVERAGE: estimate rows written (every row, 2 nsymb, or 1: row 0 only)
 };
 
 hipError_t ofdm_launch_rx(const OfdmArgs& a, uint32_t njobs, hipStream_t s);

@@ -245,7 +245,7 @@ static int chest_check_cfg(const mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* c
 // before it)
 static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs,
                              const mi355_chest_dl_cfg_t* cfg, hipStream_t s, size_t offset, float** d_out_p,
-                             float** d_noise_p)
+                             float** d_noise_p, bool row0 = false)
 {
   int r = chest_check_cfg(q, cfg);
   if (r) return r;
@@ -326,6 +326,8 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
   ca.cfo_ns      = (float)ca.nsymb;
   ca.cfo_ng      = (float)cp_len(q->ofdm.N, 144); // SRSLTE_CP_LEN_NORM(1, n)
   ca.sync_k      = (float)q->ofdm.N / 6.0f;
+  // row 0 only: AVERAGE estimates are the same in every OFDM symbol and the calling chain reads row 0
+  ca.ce_rows     = row0 && cfg->estimator_alg == MI355_ESTIMATOR_ALG_AVERAGE ? 1u : 2 * ca.nsymb;
   CHECK_HIP(chest_launch_pre(ca, njobs, cfg->sync_error_enable != 0, cfg->noise_alg == MI355_NOISE_ALG_EMPTY, s));
   if (cfg->noise_alg == MI355_NOISE_ALG_PSS && cfg->filter_type == MI355_CHEST_FILTER_GAUSS && cfg->filter_coef[0] <= 0) {
     // the automatic Gauss sigma of a subframe reads the PSS estimate of the link's previous subframe 0/5, which
@@ -563,7 +565,7 @@ int mi355_ue_dl_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, co
   int         r    = ofdm_run(q, sfjobs, njobs, s, &used);
   if (r) return r;
   float *d_out = nullptr, *d_noise = nullptr;
-  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise))) return r;
+  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise, chest_cfg->ce_rows == 1))) return r;
   // the PDSCH jobs are planned on the host while the GPU demodulates and estimates
   std::vector<mi355_pdsch_job_t> jobs(njobs);
   for (uint32_t i = 0; i < njobs; i++) {
@@ -664,6 +666,7 @@ int mi355_ue_dl_find_dl_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* sfj
   std::vector<float>           noise(njobs);
   std::vector<mi355_dci_msg_t> msgs((size_t)njobs * MI355_MAX_DCI_MSG);
   for (uint32_t i = 0; i < njobs; i++) noise[i] = chest[i].noise_estimate;
+  q->ctrl->ce_row = 0; // the caller's estimates, read where they lie
   if ((r = q->ctrl->run(sfjobs, noise.data(), nullptr, rntis, cfgs, njobs, stream ? (hipStream_t)stream : q->own, ctrl,
                         msgs.data())))
     return r;
@@ -693,7 +696,7 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   size_t used = 0;
   if ((r = ofdm_run(q, sfjobs, njobs, s, &used))) return r;
   float *d_out = nullptr, *d_noise = nullptr;
-  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise))) return r;
+  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise, chest_cfg->ce_rows == 1))) return r;
   ChestFill fill{q, chest_cfg, nullptr, sfjobs, njobs, chest, false};
   if ((r = chest_finish_async(q, &fill, d_out, s))) return r;
   std::vector<uint16_t>        rntis(njobs);
@@ -708,6 +711,8 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   static const int chunk_env = getenv("MI355_UEDL_CHUNKS") ? atoi(getenv("MI355_UEDL_CHUNKS")) : 0;
   const uint32_t   forced    = q->chunks ? q->chunks : (chunk_env >= 1 && chunk_env <= 8 ? (uint32_t)chunk_env : 0u);
   const uint32_t   nchunks   = forced ? std::max(1u, std::min(forced, njobs)) : (njobs >= 256 ? 2u : 1u);
+  // AVERAGE estimates are time-invariant: the control channels read row 0 (the only one written with ce_rows = 1)
+  q->ctrl->ce_row = chest_cfg->estimator_alg == MI355_ESTIMATOR_ALG_AVERAGE ? 12 * q->cell.nof_prb : 0u;
   if ((r = q->ctrl->launch(sfjobs, nullptr, d_noise, rntis.data(), ue_cfgs, njobs, nchunks, s))) {
     chest_fill_cb(&fill);
     return r;

@@ -144,7 +144,7 @@ class DlReceiver:
     library calls)."""
 
     def __init__(self, cell: P.Cell, nof_rx: int, B: int, nbytes: int, device: int = 0, ctrl: bool = False,
-                 max_cb: int = 16):
+                 max_cb: int = 16, ce_rows: int = 0):
         from .dlsch import SoftbufferPool
         from .tdec import DeviceBuffer
         from .ue_dl import ChestRes, UeDl, _declare, default_chest_cfg
@@ -159,6 +159,7 @@ class DlReceiver:
         self.pool = SoftbufferPool(2 * B, max_cb=max_cb, device=device)
         self.ue = UeDl(cell, nof_rx, device)
         self.chest_cfg = default_chest_cfg()
+        self.chest_cfg.ce_rows = ce_rows  # 1: the AVERAGE estimate's row 0 only (the chain reads nothing else)
         self.L = _declare()
         self.L.mi355_softbuffer_reset_range.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
         self.chest = (ChestRes * B)()

@@ -18,7 +18,8 @@ MAX_LINKS = 65536
 class ChestCfg(C.Structure):
     _fields_ = [("estimator_alg", C.c_uint32), ("noise_alg", C.c_uint32), ("filter_type", C.c_uint32),
                 ("filter_coef", C.c_float * 2), ("rsrp_neighbour", C.c_uint32), ("cfo_estimate_enable", C.c_uint32),
-                ("sync_error_enable", C.c_uint32), ("cfo_estimate_sf_mask", C.c_uint32)]
+                ("sync_error_enable", C.c_uint32), ("cfo_estimate_sf_mask", C.c_uint32), ("ce_rows", C.c_uint32)]
+CE_ROWS_ALL, CE_ROWS_FIRST = 0, 1
 
 
 def default_chest_cfg(filter_type: int = CHEST_FILTER_GAUSS, coef=(4.0, 1.0)) -> ChestCfg:

@@ -249,3 +249,43 @@ def test_ue_dl_decode_interpolate():
         for t in range(cfg.nof_tb):
             assert res[t].ret == 0 and res[t].crc, (k, t)
             np.testing.assert_array_equal(ds.payload_bytes(t)[: cfg.tbs[t] // 8], payload[t])
+
+
+@pytest.mark.parametrize("ctrl", [False, True], ids=["decode_batch", "find_and_decode"])
+def test_ce_rows_first_only(ctrl):
+    """mi355_chest_dl_cfg_t.ce_rows = 1 (AVERAGE): the batched calls write row 0 of every estimate only -- the other
+    13 rows keep whatever the buffer held -- and every result is the one of the all-rows run: estimator outputs,
+    CFI / DCIs, CRCs, iteration counts, payloads and the soft bits of a sample."""
+    import bench
+    from srsran_amd import lib
+    cell = bench.tm4_setup()
+    B = 24
+    src = bench.Tm4Source(cell, B, 0, ctrl=ctrl)
+    src.generate(3000, B, 30.0, 5)
+    outs = []
+    for rows in (0, 1):
+        from srsran_amd.synth import DlReceiver
+        rx = DlReceiver(cell, 2, B, bench.NB, 0, ctrl=ctrl, ce_rows=rows)
+        rx.ue.set_chunks(1)
+        lib().mi355_memset_dev(rx.d_ce.ptr, 0xFF, rx.d_ce.nbytes)  # NaN sentinel
+        bound = rx.bind(src, 0, B)
+        rx.step(bound)
+        ce = rx.d_ce.download(np.zeros(rx.d_ce.nbytes // 8, np.complex64)).reshape(B, 4, 14, 1200)
+        chest = np.ctypeslib.as_array(rx.chest)[:B].copy()
+        res = np.ctypeslib.as_array(rx.res)[: 2 * B].copy()
+        e = [rx.ue.pdsch.stage(k, t, 14400, 14400 * 8)[2] for k in (0, 7, 23) for t in range(2)]
+        ctl = np.ctypeslib.as_array(rx.ctrl_res)[:B].copy() if ctrl else None
+        outs.append((ce, chest, res, rx.received(B), e, ctl))
+        rx.close()
+    (ce0, ch0, r0, p0, e0, c0), (ce1, ch1, r1, p1, e1, c1) = outs
+    assert np.array_equal(ce1[:, :, 0], ce0[:, :, 0])
+    assert np.isnan(ce1[:, :, 1:].view(np.float32)).all()  # untouched
+    assert np.array_equal(ce0[:, :, 1:], np.repeat(ce0[:, :, :1], 13, axis=2))
+    assert ch0.tobytes() == ch1.tobytes()
+    assert r0.tobytes() == r1.tobytes() and r0["crc"].all()
+    assert np.array_equal(p0, p1)
+    for a, b in zip(e0, e1):
+        assert np.array_equal(a, b)
+    if ctrl:
+        assert c0.tobytes() == c1.tobytes() and (c0["nof_dci"] == 1).all()
+    src.close()
