@@ -193,7 +193,10 @@ __global__ __launch_bounds__(256) void ctrl_llr(CtrlArgs a)
 // ------------------------------------------------------------------------------------------------ blind decoding
 
 constexpr float    RX_NULL = 10000.0f;
-constexpr uint32_t WAVES   = 4;
+// one wave per workgroup: most candidates fail the mean-|LLR| gate at once while a decoding wave runs a long serial
+// trellis, and a workgroup's LDS is released only when all its waves are done -- with 4 waves per workgroup a CU held
+// 5 workgroups (LDS-bound) whatever few of their waves were decoding
+constexpr uint32_t WAVES   = 1;
 constexpr uint32_t MAXSYM  = 3 * PDCCH_MAX_F; // 432
 static_assert((PDCCH_SLOTS * PDCCH_FMTS) % WAVES == 0, "a workgroup never straddles two subframes' tail");
 
@@ -251,7 +254,7 @@ __device__ __forceinline__ void writelane1(uint32_t& v, uint32_t x, uint32_t k)
 
 __device__ __forceinline__ uint32_t par(uint32_t x) { return __builtin_popcount(x) & 1u; }
 
-__global__ __launch_bounds__(256) void pdcch_blind(BlindArgs a)
+__global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
 {
   __shared__ WaveLds lds[WAVES];
   const uint32_t     lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
