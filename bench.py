@@ -384,6 +384,57 @@ def Tm4Rx(cell, B, device, ctrl=False):
     return DlReceiver(cell, 2, B, NB, device, ctrl=ctrl, max_cb=16, ce_rows=1)
 
 
+CALLER_SO = os.path.join(ROOT, "tests", "dropin", "libdropin_caller.so")
+
+
+class CallerCfg(C.Structure):  # caller_cfg_t of tests/dropin/caller.c
+    _fields_ = [(n, C.c_uint32) for n in ("nof_prb", "nof_ports", "nof_rx", "cell_id", "rnti", "tm",
+                                          "use_tbs_index_alt", "decoder_type", "csi_enable", "max_nof_iterations",
+                                          "cfo_estimate_enable", "estimator_alg", "noise_alg", "sync_error_enable",
+                                          "power_scale")]
+
+
+def dropin_tti_latency(args, cell, local, ntti=1000, nwarm=20):
+    """Per-TTI latency of the srslte_* drop-in as srsUE's DL worker drives it (cc_worker.cc:214-300, :423-470):
+    decode_fft_estimate -> find_dl_dci -> dci_to_pdsch_grant -> softbuffer reset -> decode_pdsch on ONE TM4 100-PRB
+    subframe at a time, from host I/Q buffers (staged over PCIe by the drop-in), in the calling thread
+    (tests/dropin/caller.c caller_tti_latency, compiled against the reference headers).  10 subframes (sf_idx 0..9,
+    DCI format 2 on the PDCCH, the bench's TM4 grant) from the GPU generator, cycled over `ntti` timed TTIs."""
+    if not os.path.exists(CALLER_SO):
+        return {"error": f"{os.path.relpath(CALLER_SO, ROOT)} not built (make -C tests/dropin where the reference "
+                         "headers exist)"}
+    L = C.CDLL(CALLER_SO)
+    L.caller_tti_latency.argtypes = [C.POINTER(CallerCfg), C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                     C.c_void_p, C.c_void_p]
+    L.caller_tti_latency.restype = C.c_int
+    from srsran_amd import pdsch as P
+    cell = P.make_cell(cell.nof_prb, 2, cell.id, phich_resources=2)  # the caller's cell: SRSLTE_PHICH_R_1
+    src = Tm4Source(cell, 10, local, ctrl=True)
+    try:
+        src.generate(0, 10, args.snr, args.seed)
+        iq = np.ascontiguousarray(src.iq_host(0, 10))
+    finally:
+        src.close()
+    c = CallerCfg(nof_prb=cell.nof_prb, nof_ports=2, nof_rx=2, cell_id=cell.id, rnti=0x1234, tm=3,
+                  use_tbs_index_alt=1, decoder_type=1, csi_enable=1, max_nof_iterations=10, cfo_estimate_enable=1,
+                  estimator_alg=0, noise_alg=0, sync_error_enable=0, power_scale=1)
+    us = np.zeros((ntti, 3), np.float32)
+    ok = np.zeros(ntti, np.int32)
+    r = L.caller_tti_latency(C.byref(c), iq.ctypes.data, 10, nwarm, ntti, us.ctypes.data, ok.ctypes.data)
+    if r != 0:
+        return {"error": f"caller_tti_latency returned {r}"}
+    tot = us.sum(axis=1) / 1e3
+    pct = lambda v, q: round(float(np.percentile(v, q)), 3)  # noqa: E731
+    return {"flow": "srslte_ue_dl_decode_fft_estimate + find_dl_dci + dci_to_pdsch_grant + decode_pdsch, one TM4 "
+                    "100-PRB 2x2 QAM256 subframe per call from host I/Q (PCIe-inclusive), caller's thread",
+            "ttis": ntti, "p50_ms": pct(tot, 50), "p99_ms": pct(tot, 99), "max_ms": round(float(tot.max()), 3),
+            "stage_p50_ms": {"fft_estimate": pct(us[:, 0] / 1e3, 50), "pdcch_grant": pct(us[:, 1] / 1e3, 50),
+                             "pdsch": pct(us[:, 2] / 1e3, 50)},
+            "tbs_ok": f"{int(ok.sum())}/{2 * ntti}",
+            "budget_note": "srsUE: a TTI's DL decode + UL encode must finish before its n+4 uplink (36.213 10.1); "
+                           "with srsUE's default 3 PHY workers each worker has ~3 ms per TTI"}
+
+
 def cpu_baseline_pdsch(src, gpu_bufs, avg_its, budget_s, ocfg_of=None, K=6144, C=16, ntb=2, tbs=TBS, max_cb=16,
                        S_max=16, label="TM4"):
     """CPU reference-path timing on the host cores (rank 0, N = 1), bounded sample of the same workload:
@@ -684,6 +735,8 @@ def run_pdsch(args, world, rank, local, pg):
             res["decoder_bound_fixed8"]["parity_vs_reference"] = fixed8_parity(gb[:64], _d_out)
         if rank == 0 and world == 1:
             res["config1_generic"] = config1_generic(local, with_cpu=not args.no_cpu)
+            if not ctrl:
+                res["dropin_tti_latency"] = dropin_tti_latency(args, cell, local)
     if not ctrl and not args.total_subframes and not args.no_waterfall:
         res["e2e_waterfall"] = waterfall(args, cell, B, src, rx, pg, local, world)
     rx.pool.close()

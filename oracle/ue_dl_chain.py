@@ -219,7 +219,10 @@ def fill_res(vals: np.ndarray, nof_prb: int) -> dict:
         ri = f(ri + f(f(f(f(4) * rssi[a, 0]) / f(nof_prb)) / f(12)))
     rq, ri = f(rq / f(R)), f(ri / f(R))
     db = lambda v: float(10 * np.log10(v))  # noqa: E731
-    return dict(noise_estimate=float(n), rsrp=float(rs), rsrq=float(rq), rssi_dbm=db(ri) + 30, snr_db=db(rs / n),
+    # a zero noise estimate (noiseless input) gives +inf dB (nan for 0/0), as the reference's float division does
+    with np.errstate(divide="ignore", invalid="ignore"):
+        snr = db(rs / n)
+    return dict(noise_estimate=float(n), rsrp=float(rs), rsrq=float(rq), rssi_dbm=db(ri) + 30, snr_db=snr,
                 noise=noise.copy(), rsrp_ant_port=rsrp.copy(), rssi_ant_port=rssi.copy())
 
 

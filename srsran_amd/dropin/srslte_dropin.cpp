@@ -1194,6 +1194,12 @@ int srslte_ue_dl_find_and_decode(srslte_ue_dl_t*     q,
   TRACE();
   // ue_dl.c:1453-1560 for FDD normal subframes (mi = 1)
   if (!q || !sf || !cfg || !pdsch_cfg || !data || !acks) return SRSLTE_ERROR_INVALID_INPUTS;
+  // TDD (the PHICH mi blind search, ue_dl.c:1470-1490) and MBSFN (the forced MRNTI grant, ue_dl.c:1500-1508) are
+  // outside this drop-in: refuse them instead of decoding them as FDD normal subframes
+  if (q->cell.frame_type != SRSLTE_FDD || sf->sf_type != SRSLTE_SF_NORM) {
+    DROPIN_ERR("find_and_decode: only FDD normal subframes are supported\n");
+    return SRSLTE_ERROR;
+  }
   srslte_dci_dl_t dci_dl[SRSLTE_MAX_DCI_MSG];
   memset(dci_dl, 0, sizeof(dci_dl));
   srslte_ue_dl_set_mi_auto(q);

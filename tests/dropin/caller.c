@@ -5,8 +5,11 @@
  *   caller_tdec_run_all  turbodecoder_test.c:188-260 (srslte_tdec_init_manual / run_all / free)
  *   caller_ue_dl         phy_dl_test.c:194-247 work_ue (+ srslte_pdsch_decode on the ue_dl's host grids, and
  *                        srslte_ue_dl_find_and_decode, ue_dl.c:1453)
+ *   caller_tti_latency   srsUE's per-TTI DL worker flow (cc_worker.cc:214-300, :423-470), timed per stage (bench.py's
+ *                        dropin_tti_latency field and tests/test_dropin_gpu.py)
  * Built by tests/dropin/Makefile (only where the reference headers exist); the .so travels to the GPU box. */
 #include <execinfo.h>
+#include <time.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -66,6 +69,7 @@ typedef struct {
 typedef struct {
   uint32_t nof_prb, nof_ports, nof_rx, cell_id, rnti, tm, use_tbs_index_alt, decoder_type, csi_enable;
   uint32_t max_nof_iterations, cfo_estimate_enable, estimator_alg, noise_alg, sync_error_enable;
+  uint32_t power_scale; /* caller_tti_latency: p_a 0 dB / p_b 1 power allocation on, as phy_dl_test.c:216-218 */
 } caller_cfg_t;
 
 /* iq: nsf x nof_rx x SRSLTE_SF_LEN_PRB(nof_prb) complex samples; payload: nsf x 3 decoders x 2 TBs x max_bytes */
@@ -247,5 +251,114 @@ int caller_pdsch_decode(const caller_cfg_t* c, uint32_t tti, uint32_t cfi, srslt
   }
   for (int t = 0; t < 2; t++) srslte_softbuffer_rx_free(&sb[t]);
   srslte_pdsch_free(&pdsch);
+  return ret;
+}
+
+/* Per-TTI latency of srsUE's DL worker flow on the drop-in (cc_worker.cc:214-300 work_dl_regular, :423-470
+ * decode_pdsch): srslte_ue_dl_decode_fft_estimate -> find_dl_dci -> dci_to_pdsch_grant -> softbuffer reset (the MAC's
+ * new-data action) -> decode_pdsch, one subframe at a time in the caller's thread, from the HOST buffers captured at
+ * srslte_ue_dl_init (the radio writes them; that copy is outside the timed region).  iq: nsf subframes cycled over
+ * nwarm untimed + ntti timed TTIs (tti = i mod 10240, subframe i mod nsf, so nsf must be a multiple of 10 for the
+ * grants to match the subframe index).  us[3 * k + s]: stage s of timed TTI k (0 fft+estimate, 1 PDCCH search +
+ * grant, 2 PDSCH); ok[k]: TBs whose CRC passed. */
+static double caller_now_us(void)
+{
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+int caller_tti_latency(const caller_cfg_t* c, const cf_t* iq, uint32_t nsf, uint32_t nwarm, uint32_t ntti, float* us,
+                       int32_t* ok)
+{
+  const uint32_t sflen = SRSLTE_SF_LEN_PRB(c->nof_prb);
+  srslte_cell_t  cell  = {c->nof_prb, c->nof_ports, c->cell_id, SRSLTE_CP_NORM, SRSLTE_PHICH_NORM, SRSLTE_PHICH_R_1,
+                        SRSLTE_FDD};
+  cf_t*          buffers[SRSLTE_MAX_PORTS] = {};
+  for (uint32_t r = 0; r < c->nof_rx; r++) buffers[r] = (cf_t*)calloc(sflen, sizeof(cf_t));
+  srslte_ue_dl_t ue_dl;
+  if (srslte_ue_dl_init(&ue_dl, buffers, c->nof_prb, c->nof_rx) || srslte_ue_dl_set_cell(&ue_dl, cell)) return -1;
+  srslte_ue_dl_set_rnti(&ue_dl, c->rnti);
+  srslte_softbuffer_rx_t sb[SRSLTE_MAX_CODEWORDS];
+  for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++)
+    if (srslte_softbuffer_rx_init(&sb[t], c->nof_prb)) return -2;
+  uint8_t* pay[SRSLTE_MAX_CODEWORDS];
+  for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++) pay[t] = (uint8_t*)calloc(1 << 17, 1) /* > the largest TB (391,656 bits) + 6 */;
+
+  srslte_ue_dl_cfg_t ue_dl_cfg;
+  memset(&ue_dl_cfg, 0, sizeof(ue_dl_cfg));
+  ue_dl_cfg.cfg.tm                        = (srslte_tm_t)c->tm;
+  ue_dl_cfg.cfg.pdsch.use_tbs_index_alt   = c->use_tbs_index_alt;
+  ue_dl_cfg.cfg.pdsch.rnti                = c->rnti;
+  ue_dl_cfg.cfg.pdsch.decoder_type        = (srslte_mimo_decoder_t)c->decoder_type;
+  ue_dl_cfg.cfg.pdsch.csi_enable          = c->csi_enable;
+  ue_dl_cfg.cfg.pdsch.max_nof_iterations  = c->max_nof_iterations;
+  ue_dl_cfg.chest_cfg.filter_type         = SRSLTE_CHEST_FILTER_GAUSS;
+  ue_dl_cfg.chest_cfg.filter_coef[0]      = 4;
+  ue_dl_cfg.chest_cfg.filter_coef[1]      = 1.0f;
+  ue_dl_cfg.chest_cfg.noise_alg           = (srslte_chest_dl_noise_alg_t)c->noise_alg;
+  ue_dl_cfg.chest_cfg.estimator_alg       = (srslte_chest_dl_estimator_alg_t)c->estimator_alg;
+  ue_dl_cfg.chest_cfg.cfo_estimate_enable = c->cfo_estimate_enable;
+  ue_dl_cfg.chest_cfg.cfo_estimate_sf_mask = 1023;
+  ue_dl_cfg.chest_cfg.sync_error_enable   = c->sync_error_enable;
+  if (c->power_scale) { /* phy_dl_test.c:216-218: the transmitter applied rho_a (srslte_pdsch_encode) */
+    ue_dl_cfg.cfg.pdsch.power_scale = true;
+    ue_dl_cfg.cfg.pdsch.p_a         = 0.0f;
+    ue_dl_cfg.cfg.pdsch.p_b         = (c->tm > SRSLTE_TM1) ? 1 : 0;
+  }
+
+  int ret = 0;
+  for (uint32_t i = 0; i < nwarm + ntti && !ret; i++) {
+    const uint32_t sfi = i % nsf;
+    for (uint32_t r = 0; r < c->nof_rx; r++)
+      memcpy(buffers[r], iq + ((size_t)sfi * c->nof_rx + r) * sflen, sflen * sizeof(cf_t));
+    srslte_dl_sf_cfg_t sf_cfg_dl;
+    memset(&sf_cfg_dl, 0, sizeof(sf_cfg_dl));
+    sf_cfg_dl.tti     = i % 10240;
+    sf_cfg_dl.sf_type = SRSLTE_SF_NORM;
+    const double t0 = caller_now_us();
+    srslte_ue_dl_set_mi_auto(&ue_dl);
+    if (srslte_ue_dl_decode_fft_estimate(&ue_dl, &sf_cfg_dl, &ue_dl_cfg) < 0) {
+      ret = -3;
+      break;
+    }
+    const double    t1 = caller_now_us();
+    srslte_dci_dl_t dci_dl[SRSLTE_MAX_DCI_MSG];
+    memset(dci_dl, 0, sizeof(dci_dl));
+    int n_ok = 0;
+    if (srslte_ue_dl_find_dl_dci(&ue_dl, &sf_cfg_dl, &ue_dl_cfg, c->rnti, dci_dl) != 1 ||
+        srslte_ue_dl_dci_to_pdsch_grant(&ue_dl, &sf_cfg_dl, &ue_dl_cfg, &dci_dl[0], &ue_dl_cfg.cfg.pdsch.grant)) {
+      ret = -4;
+      break;
+    }
+    const double       t2 = caller_now_us();
+    srslte_pdsch_res_t res[SRSLTE_MAX_CODEWORDS];
+    memset(res, 0, sizeof(res));
+    for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++) {
+      ue_dl_cfg.cfg.pdsch.softbuffers.rx[t] = &sb[t];
+      res[t].payload                        = pay[t];
+      if (ue_dl_cfg.cfg.pdsch.grant.tb[t].enabled)
+        srslte_softbuffer_rx_reset_tbs(&sb[t], (uint32_t)ue_dl_cfg.cfg.pdsch.grant.tb[t].tbs);
+    }
+    if (srslte_ue_dl_decode_pdsch(&ue_dl, &sf_cfg_dl, &ue_dl_cfg.cfg.pdsch, res)) {
+      ret = -5;
+      break;
+    }
+    const double t3 = caller_now_us();
+    for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++) n_ok += ue_dl_cfg.cfg.pdsch.grant.tb[t].enabled && res[t].crc;
+    if (i >= nwarm) {
+      const uint32_t k = i - nwarm;
+      us[3 * k + 0]    = (float)(t1 - t0);
+      us[3 * k + 1]    = (float)(t2 - t1);
+      us[3 * k + 2]    = (float)(t3 - t2);
+      ok[k]            = n_ok;
+    }
+  }
+  for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++) {
+    srslte_softbuffer_rx_free(&sb[t]);
+    free(pay[t]);
+  }
+  srslte_ue_dl_free(&ue_dl);
+  for (uint32_t r = 0; r < c->nof_rx; r++) free(buffers[r]);
   return ret;
 }

@@ -32,7 +32,7 @@ class CallerCfg(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ("nof_prb", "nof_ports", "nof_rx", "cell_id", "rnti", "tm",
                                           "use_tbs_index_alt", "decoder_type", "csi_enable", "max_nof_iterations",
                                           "cfo_estimate_enable", "estimator_alg", "noise_alg",
-                                          "sync_error_enable")]
+                                          "sync_error_enable", "power_scale")]
 
 
 class SfRes(C.Structure):
@@ -65,6 +65,8 @@ def _caller():
                                C.POINTER(SfRes)]
     # (c, tti, cfi, grant, grid, ce, noise, ncalls, rvs, payload, crc_out, its_out): every pointer declared -- an
     # undeclared trailing argument is passed as a 32-bit C int and truncates the address
+    L.caller_tti_latency.argtypes = [C.POINTER(CallerCfg), C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                                     C.c_void_p]
     L.caller_pdsch_decode.argtypes = [C.POINTER(CallerCfg), C.c_uint32, C.c_uint32, C.POINTER(Grant), C.c_void_p,
                                       C.c_void_p, C.c_float, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p]
@@ -220,3 +222,22 @@ def test_pdsch_drop_in_host_buffers_and_softbuffer_reuse():
     # second call on the same softbuffers: every code block is skipped (cb_crc) and its bytes "restored" from the
     # softbuffer, but sch.c:476-483 saves them only when the TB failed, so the reference's TB CRC fails here
     assert crc[2] == 0 and crc[3] == 0 and its[2] == 0 and its[3] == 0
+
+
+def test_tti_latency_flow_decodes_every_tti():
+    """caller_tti_latency (srsUE's per-TTI worker flow, bench.py's dropin_tti_latency field): 10 distinct TM4
+    subframes cycled over 30 TTIs, every TB decodes, every stage timed."""
+    L = _caller()
+    case = CASES[0]
+    name, nprb, ports, nrx, tm, fmt, mcs, alt, cid = case
+    rnti = 0x46
+    iq, _expect = _synth(case, list(range(10)), rnti)
+    c = CallerCfg(nof_prb=nprb, nof_ports=ports, nof_rx=nrx, cell_id=cid, rnti=rnti, tm=tm, use_tbs_index_alt=int(alt),
+                  decoder_type=1, csi_enable=1, max_nof_iterations=10, cfo_estimate_enable=1, estimator_alg=0,
+                  noise_alg=0, sync_error_enable=0)
+    n = 30
+    us = np.zeros((n, 3), np.float32)
+    ok = np.zeros(n, np.int32)
+    assert L.caller_tti_latency(C.byref(c), iq.ctypes.data, 10, 2, n, us.ctypes.data, ok.ctypes.data) == 0
+    assert np.all(ok == 2), ok
+    assert np.all(us > 0) and np.all(np.isfinite(us))
