@@ -392,6 +392,7 @@ static bool common_search_only(uint16_t rnti) { return rnti == MI355_SIRNTI || r
 BlindJob blind_plan(const mi355_cell_t& cell, uint32_t sf_idx, uint16_t rnti, const mi355_ue_dl_cfg_t& cfg)
 {
   BlindJob         j{};
+  j.rnti              = rnti;
   mi355_dci_cfg_t  cc = cfg.dci;
   cc.is_not_ue_ss     = 1; // srslte_dci_cfg_set_common_ss (dci.c:1413-1416)
   if (common_search_only(rnti)) {

@@ -54,6 +54,7 @@ struct BlindJob {
   uint32_t Yk;           // UE-specific search-space hash for (rnti, sf_idx) (pdcch.c:247-251)
   uint32_t spaces;       // bit 0: UE-specific space, bit 1: common space
   uint16_t nbits[2][2];  // [space][format slot] payload sizes, 0 = not searched
+  uint32_t rnti;         // the RNTI searched for (the replay keeps only candidates whose CRC remainder equals it)
 };
 
 struct DciCand {
@@ -61,6 +62,25 @@ struct DciCand {
   uint32_t crc_rem; // received parity ^ CRC16(payload)
   uint32_t L, ncce;
   uint32_t bits[4]; // payload bits, MSB-first within each 32-bit word
+};
+
+// What the host replay of one subframe needs from its candidates (pdcch_compact): dci_blind_search (ue_dl.c:450-550)
+// acts only on candidates that decoded (status 2) with the searched RNTI as CRC remainder, so the read-back carries
+// those alone, in slot order: 96 bytes per subframe instead of 1,408.  n > PDCCH_HMAX: the host reads that subframe's
+// full candidate array instead.
+constexpr uint32_t PDCCH_HMAX = 4;
+struct DciHits {
+  uint32_t n;                 // matching candidates of the subframe
+  uint32_t slot[PDCCH_HMAX];  // slot * PDCCH_FMTS + format slot
+  uint32_t bits[PDCCH_HMAX][4];
+  uint32_t pad[3];
+};
+static_assert(sizeof(DciHits) == 96, "DciHits layout");
+
+struct CompactArgs {
+  const BlindJob* jobs;
+  const DciCand*  cand; // [job][PDCCH_SLOTS][PDCCH_FMTS]
+  DciHits*        hits; // [job]
 };
 
 struct BlindArgs {
@@ -74,6 +94,7 @@ struct BlindArgs {
 
 hipError_t ctrl_launch_llr(const CtrlArgs& a, uint32_t njobs, hipStream_t s);
 hipError_t ctrl_launch_blind(const BlindArgs& a, uint32_t njobs, hipStream_t s);
+hipError_t ctrl_launch_compact(const CompactArgs& a, uint32_t njobs, hipStream_t s);
 
 // host search-space generation (pdcch.c:222-330), shared by the runtime's blind-search replay
 uint32_t ue_locations(uint32_t nof_cce, uint32_t Yk, mi355_dci_location_t* c);

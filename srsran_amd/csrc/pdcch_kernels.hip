@@ -8,6 +8,8 @@
 //                 tail-biting Viterbi decoder with one lane per trellis state (cross-lane reads by ds_bpermute,
 //                 decision words by ballot into LDS; viterbi37_avx2_16bit.c semantics: wrapping u16 metrics,
 //                 modular compare), chainback and CRC16 -> the CRC remainder the host compares with the RNTI.
+//   pdcch_compact one wave per subframe: the candidates whose remainder is the searched RNTI, in slot order (the
+//                 only ones the host replay acts on) -> the small per-subframe record the host reads back.
 //
 // Integer / byte-level work throughout; nothing here is GEMM-shaped.  The equaliser evaluates the reference's
 // formulas without FMA contraction (built with -ffp-contract=off) so it equals oracle/orc_pdcch.c bit for bit.
@@ -452,6 +454,40 @@ hipError_t ctrl_launch_blind(const BlindArgs& a, uint32_t njobs, hipStream_t s)
   if (!njobs) return hipSuccess;
   const uint32_t waves = njobs * PDCCH_SLOTS * PDCCH_FMTS;
   hipLaunchKernelGGL(pdcch_blind, dim3((waves + WAVES - 1) / WAVES), dim3(64 * WAVES), 0, s, a);
+  return hipGetLastError();
+}
+
+// one wave per subframe: lane k checks candidate k (slot k / PDCCH_FMTS, format slot k % PDCCH_FMTS); the matching
+// ones (decoded, CRC remainder = the searched RNTI: the only candidates dci_blind_search acts on, ue_dl.c:480-484)
+// are written in slot order by their rank in the wave's ballot
+__global__ __launch_bounds__(256) void pdcch_compact(CompactArgs a, uint32_t njobs)
+{
+  constexpr uint32_t NC = PDCCH_SLOTS * PDCCH_FMTS;
+  static_assert(NC <= 64, "one candidate per lane");
+  const uint32_t job  = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (job >= njobs) return;
+  const DciCand* c   = a.cand + (size_t)job * NC;
+  const uint32_t rnti = a.jobs[job].rnti;
+  bool           hit  = false;
+  if (lane < NC) hit = c[lane].status == 2 && c[lane].crc_rem == rnti;
+  const uint64_t mask = __builtin_amdgcn_ballot_w64(hit);
+  DciHits*       h    = a.hits + job;
+  if (lane == 0) h->n = (uint32_t)__builtin_popcountll(mask);
+  if (hit) {
+    const uint32_t rank = (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1));
+    if (rank < PDCCH_HMAX) {
+      h->slot[rank] = lane;
+#pragma unroll
+      for (int w = 0; w < 4; w++) h->bits[rank][w] = c[lane].bits[w];
+    }
+  }
+}
+
+hipError_t ctrl_launch_compact(const CompactArgs& a, uint32_t njobs, hipStream_t s)
+{
+  if (!njobs) return hipSuccess;
+  hipLaunchKernelGGL(pdcch_compact, dim3((njobs + 3) / 4), dim3(256), 0, s, a, njobs);
   return hipGetLastError();
 }
 

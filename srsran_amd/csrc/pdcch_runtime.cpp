@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <stdlib.h>
 #include <stdio.h>
@@ -76,7 +77,7 @@ int CtrlState::run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, con
 
 int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, const float* d_noise,
                       const uint16_t* rntis, const mi355_ue_dl_cfg_t* cfgs, uint32_t n, uint32_t nchunks,
-                      hipStream_t s)
+                      hipStream_t s, const std::function<int(uint32_t, uint32_t)>& front)
 {
   if (!n) return MI355_SUCCESS;
   nchunks = std::max(1u, std::min(nchunks, n));
@@ -85,7 +86,8 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
   const size_t   b_llr = staged_size((size_t)n * stride * 4), b_cfi = staged_size((size_t)n * 4);
   const size_t   b_corr = staged_size((size_t)n * 12);
   const size_t   b_cand = staged_size((size_t)n * PDCCH_SLOTS * PDCCH_FMTS * sizeof(DciCand));
-  const size_t   need   = b_jobs + b_blind + b_llr + b_cfi + b_corr + b_cand;
+  const size_t   b_hits = staged_size((size_t)n * sizeof(DciHits));
+  const size_t   need   = b_jobs + b_blind + b_llr + b_cfi + b_corr + b_cand + b_hits;
   if (need > cap) {
     if (d_buf) {
       CHECK_HIP(hipStreamSynchronize(s));
@@ -133,9 +135,10 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
   uint32_t* d_cfi  = (uint32_t*)(base + b_jobs + b_blind + b_llr);
   float*    d_corr = (float*)(base + b_jobs + b_blind + b_llr + b_cfi);
   DciCand*  d_cand = (DciCand*)(base + b_jobs + b_blind + b_llr + b_cfi + b_corr);
+  DciHits*  d_hits = (DciHits*)(base + b_jobs + b_blind + b_llr + b_cfi + b_corr + b_cand);
   const size_t ncand = (size_t)PDCCH_SLOTS * PDCCH_FMTS;
-  // host read-back area: cfi | corr | candidates of all n subframes (the device arena's order)
-  CHECK_HIP(back->reserve(b_cfi + b_corr + (size_t)n * ncand * sizeof(DciCand)));
+  // host read-back area: cfi | corr | hit records of all n subframes (the device arena's order)
+  CHECK_HIP(back->reserve(b_cfi + b_corr + (size_t)n * sizeof(DciHits)));
   b_cfi_  = b_cfi;
   b_corr_ = b_corr;
   chunk_end.assign(nchunks, 0);
@@ -147,6 +150,10 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
   for (uint32_t c = 0; c < nchunks; c++) {
     const uint32_t o = (uint32_t)((uint64_t)n * c / nchunks), m = (uint32_t)((uint64_t)n * (c + 1) / nchunks) - o;
     chunk_end[c]     = o + m;
+    if (front) {
+      const int e = front(o, m);
+      if (e) return e;
+    }
     CtrlArgs a{};
     a.jobs       = (const CtrlJob*)base + o;
     a.pcfich_re  = d_tab;
@@ -171,11 +178,13 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
     for (int k = 0; k < 3; k++) b.ncce[k] = regs.nregs[k] / 9;
     b.out = d_cand + (size_t)o * ncand;
     CHECK_HIP(ctrl_launch_blind(b, m, s));
+    CompactArgs h{(const BlindJob*)(base + b_jobs) + o, d_cand + (size_t)o * ncand, d_hits + o};
+    CHECK_HIP(ctrl_launch_compact(h, m, s));
     CHECK_HIP(hipMemcpyAsync(back->host + 4 * (size_t)o, d_cfi + o, 4 * (size_t)m, hipMemcpyDeviceToHost, s));
     CHECK_HIP(hipMemcpyAsync(back->host + b_cfi + 12 * (size_t)o, d_corr + 3 * (size_t)o, 12 * (size_t)m,
                              hipMemcpyDeviceToHost, s));
-    CHECK_HIP(hipMemcpyAsync(back->host + b_cfi + b_corr + (size_t)o * ncand * sizeof(DciCand), d_cand + (size_t)o * ncand,
-                             (size_t)m * ncand * sizeof(DciCand), hipMemcpyDeviceToHost, s));
+    CHECK_HIP(hipMemcpyAsync(back->host + b_cfi + b_corr + (size_t)o * sizeof(DciHits), d_hits + o,
+                             (size_t)m * sizeof(DciHits), hipMemcpyDeviceToHost, s));
     CHECK_HIP(hipEventRecord(ev[c], s));
   }
   last_n = n, last_stride = stride, last_llr = d_llr, last_cand = d_cand;
@@ -192,18 +201,40 @@ int CtrlState::finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_c
   const uint32_t    b    = chunk ? chunk_end[chunk - 1] : 0, e = chunk_end[chunk];
   const uint32_t* h_cfi  = (const uint32_t*)back->host;
   const float*    h_corr = (const float*)(back->host + b_cfi_);
-  const DciCand*  h_cand = (const DciCand*)(back->host + b_cfi_ + b_corr_);
+  const DciHits*  h_hits = (const DciHits*)(back->host + b_cfi_ + b_corr_);
+  constexpr uint32_t NC  = PDCCH_SLOTS * PDCCH_FMTS;
+  std::atomic<int>   err{0};
+  // MI355_PDCCH_HMAX (tests): treat records with more matches than this as overflowing (0: always the full path)
+  const char*        he   = getenv("MI355_PDCCH_HMAX");
+  const uint32_t     hmax = he ? std::min<uint32_t>((uint32_t)atoi(he), PDCCH_HMAX) : PDCCH_HMAX;
   host_parallel_for(e - b, 128, [&](uint32_t lo, uint32_t hi) { // subframes are independent
+    DciCand cand[NC];
     for (uint32_t i = b + lo; i < b + hi; i++) {
       const uint32_t cfi = h_cfi[i];
       res[i].cfi         = cfi;
       res[i].cfi_corr    = std::max({0.f, h_corr[3 * i], h_corr[3 * i + 1], h_corr[3 * i + 2]});
       res[i].nof_cce     = regs.nregs[cfi - 1] / 9;
-      res[i].nof_dci     = blind_search_replay(cell, res[i].nof_cce, rntis[i], cfgs[i], plan_of[i],
-                                           h_cand + (size_t)i * PDCCH_SLOTS * PDCCH_FMTS,
+      // the replay's view of the candidates: the matching ones, everything else "not decoded"
+      const DciHits& H = h_hits[i];
+      if (H.n > hmax) { // more matches than the record holds: the subframe's whole candidate array
+        if (hipMemcpy(cand, last_cand + (size_t)i * NC, sizeof(cand), hipMemcpyDeviceToHost) != hipSuccess) {
+          err = 1;
+          continue;
+        }
+      } else {
+        memset(cand, 0, sizeof(cand));
+        for (uint32_t k = 0; k < H.n; k++) {
+          DciCand& c = cand[H.slot[k]];
+          c.status   = 2;
+          c.crc_rem  = plan_of[i].rnti;
+          memcpy(c.bits, H.bits[k], sizeof(c.bits));
+        }
+      }
+      res[i].nof_dci = blind_search_replay(cell, res[i].nof_cce, rntis[i], cfgs[i], plan_of[i], cand,
                                            msgs + (size_t)i * MI355_MAX_DCI_MSG);
     }
   });
+  if (err) return MI355_ERROR;
   if (prof)
     fprintf(stderr, "[mi355 host] control stage: blind-search replay %.1f us for %u subframes\n",
             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tr0).count(), e - b);

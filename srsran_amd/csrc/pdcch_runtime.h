@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <unordered_map>
 #include <vector>
 
@@ -42,8 +43,10 @@ struct CtrlState {
   // run() in two halves: launch() enqueues the kernels and read-backs of n subframes in nchunks consecutive chunks
   // (one completion event each); finish(c) waits for chunk c only and replays its blind searches, so the host
   // works on chunk c while the GPU runs the later chunks (and whatever the caller enqueued after them)
+  // front(o, m), when given, enqueues what chunk [o, o + m) needs first (its OFDM and estimation) ahead of its kernels
   int launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, const float* d_noise, const uint16_t* rntis,
-             const mi355_ue_dl_cfg_t* cfgs, uint32_t n, uint32_t nchunks, hipStream_t s);
+             const mi355_ue_dl_cfg_t* cfgs, uint32_t n, uint32_t nchunks, hipStream_t s,
+             const std::function<int(uint32_t, uint32_t)>& front = nullptr);
   int finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_cfg_t* cfgs, mi355_ctrl_res_t* res,
              mi355_dci_msg_t* msgs);
 };

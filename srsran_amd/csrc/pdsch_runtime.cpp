@@ -336,6 +336,7 @@ static int plan_job(mi355_pdsch_t* q, const mi355_pdsch_job_t& j, const mi355_pd
 static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::vector<JobPlan>& plans, hipStream_t s,
                         bool after_s = false)
 {
+  const auto     t_in  = std::chrono::steady_clock::now();
   const uint32_t njobs = (uint32_t)plans.size();
   size_t         nd = 0, ne = 0;
   std::vector<PdschCwDev> cws;
@@ -466,13 +467,18 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
       ci++;
     }
   }
+  static const bool prof = getenv("MI355_HOST_PROF") != nullptr;
+  auto              now  = [] { return std::chrono::steady_clock::now(); };
+  const auto        ta   = now();
   q->stage.put(hj.data(), njobs * sizeof(PdschJobDev));
   q->stage.put(cws.data(), ncw * sizeof(PdschCwDev));
   q->stage.put(new_ci.data(), new_ci.size() * 4);
   q->stage.put(new_dst.data(), new_dst.size() * 8);
   // after_s: the previous batch may still be in flight; its front end (the only reader of the descriptors) is done
   // at fe_done
+  const auto tb = now();
   CHECK_HIP(q->stage.upload(base, s, after_s, after_s && q->fe_armed ? q->fe_done : nullptr));
+  const auto tc = now();
   CHECK_HIP(pdsch_launch_equalize((const PdschJobDev*)(base + o_jobs), njobs, max_units, s));
   CHECK_HIP(pdsch_launch_scr_pack((const uint32_t*)(base + o_nci), (uint32_t* const*)(base + o_ndst),
                                   (uint32_t)new_ci.size(), q->gold, PDSCH_GOLD_MAX / 32, s));
@@ -482,6 +488,11 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   if (!q->fe_done) CHECK_HIP(hipEventCreateWithFlags(&q->fe_done, hipEventDisableTiming));
   CHECK_HIP(hipEventRecord(q->fe_done, s));
   q->fe_armed = true;
+  if (prof) {
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    fprintf(stderr, "[mi355 host] pdsch frontend: tables %.1f us, put %.1f us, upload %.1f us, launches %.1f us\n",
+            us(t_in, ta), us(ta, tb), us(tb, tc), us(tc, now()));
+  }
   return MI355_SUCCESS;
 }
 

@@ -70,6 +70,12 @@ struct mi355_ue_dl {
   CtrlState*     ctrl     = nullptr;       // PCFICH / PDCCH stage, built on first use
   std::vector<std::unique_ptr<mi355::PdschPending>> pend; // find_and_decode: per chunk, decodes left in flight
   uint32_t       chunks = 0;                              // find_and_decode chunk count (0: automatic)
+  // find_and_decode: OFDM / estimator job tables uploaded for the whole batch, kernels launched per chunk in front
+  // of the chunk's control kernels (ofdm_launch_range / chest_launch_range)
+  OfdmArgs       ofdm_def{};
+  ChestArgs      chest_def{};
+  bool           chest_def_sync = false, chest_def_empty = false;
+  float*         chest_def_noise = nullptr;
   std::mutex     mu;
 };
 
@@ -120,7 +126,7 @@ static int get_scratch(mi355_ue_dl_t* q, size_t bytes, char** p)
 }
 
 static int ofdm_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, hipStream_t s,
-                    size_t* used = nullptr)
+                    size_t* used = nullptr, bool defer = false)
 {
   const size_t nj = (size_t)njobs * q->nof_rx;
   CHECK_HIP(q->st_ofdm.reserve(nj * sizeof(OfdmJob)));
@@ -137,12 +143,28 @@ static int ofdm_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t nj
   CHECK_HIP(q->st_ofdm.upload(base, s));
   OfdmArgs a = q->ofdm;
   a.jobs     = (const OfdmJob*)base;
+  if (used) *used = (nj * sizeof(OfdmJob) + 255) / 256 * 256;
+  if (defer) { // the caller launches subframe ranges (ofdm_launch_range)
+    q->ofdm_def = a;
+    return MI355_SUCCESS;
+  }
   // grid.y is limited to 65535: launch in chunks
   for (size_t off = 0; off < nj; off += 65535) {
     a.jobs = (const OfdmJob*)base + off;
     CHECK_HIP(ofdm_launch_rx(a, (uint32_t)std::min<size_t>(65535, nj - off), s));
   }
-  if (used) *used = (nj * sizeof(OfdmJob) + 255) / 256 * 256;
+  return MI355_SUCCESS;
+}
+
+// subframes [o, o + m) of a deferred ofdm_run
+static int ofdm_launch_range(mi355_ue_dl_t* q, uint32_t o, uint32_t m, hipStream_t s)
+{
+  OfdmArgs     a  = q->ofdm_def;
+  const size_t b  = (size_t)o * q->nof_rx, e = (size_t)(o + m) * q->nof_rx;
+  for (size_t off = b; off < e; off += 65535) {
+    a.jobs = q->ofdm_def.jobs + off;
+    CHECK_HIP(ofdm_launch_rx(a, (uint32_t)std::min<size_t>(65535, e - off), s));
+  }
   return MI355_SUCCESS;
 }
 
@@ -243,9 +265,20 @@ static int chest_check_cfg(const mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* c
 // launches the estimator (sync-error stage, estimation, noise resolution and, when d_noise is wanted, the per-job
 // get_noise) without synchronising; the scratch region starts after `offset` bytes (the OFDM job table may live
 // before it)
+// the estimator can run in consecutive subframe ranges (chest_launch_range) unless a subframe's kernels depend on
+// the estimate of an earlier subframe of the batch (the automatic Gauss sigma of the PSS noise, and WIENER, whose
+// stage walks each link's subframes after the whole batch's estimates)
+static bool chest_deferrable(const mi355_chest_dl_cfg_t* cfg)
+{
+  return cfg && cfg->estimator_alg != MI355_ESTIMATOR_ALG_WIENER &&
+         !(cfg->noise_alg == MI355_NOISE_ALG_PSS && cfg->filter_type == MI355_CHEST_FILTER_GAUSS && cfg->filter_coef[0] <= 0);
+}
+
+// defer (chest_deferrable configurations only): build and upload the batch's tables, launch nothing; the caller
+// launches subframe ranges in order with chest_launch_range
 static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs,
                              const mi355_chest_dl_cfg_t* cfg, hipStream_t s, size_t offset, float** d_out_p,
-                             float** d_noise_p, bool row0 = false)
+                             float** d_noise_p, bool row0 = false, bool defer = false)
 {
   int r = chest_check_cfg(q, cfg);
   if (r) return r;
@@ -328,6 +361,16 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
   ca.sync_k      = (float)q->ofdm.N / 6.0f;
   // row 0 only: AVERAGE estimates are the same in every OFDM symbol and the calling chain reads row 0
   ca.ce_rows     = row0 && cfg->estimator_alg == MI355_ESTIMATOR_ALG_AVERAGE ? 1u : 2 * ca.nsymb;
+  if (defer) {
+    if (!chest_deferrable(cfg)) return MI355_ERROR;
+    q->chest_def       = ca;
+    q->chest_def_sync  = cfg->sync_error_enable != 0;
+    q->chest_def_empty = cfg->noise_alg == MI355_NOISE_ALG_EMPTY;
+    q->chest_def_noise = d_noise_p ? d_noise : nullptr;
+    *d_out_p           = d_out;
+    if (d_noise_p) *d_noise_p = d_noise;
+    return MI355_SUCCESS;
+  }
   CHECK_HIP(chest_launch_pre(ca, njobs, cfg->sync_error_enable != 0, cfg->noise_alg == MI355_NOISE_ALG_EMPTY, s));
   if (cfg->noise_alg == MI355_NOISE_ALG_PSS && cfg->filter_type == MI355_CHEST_FILTER_GAUSS && cfg->filter_coef[0] <= 0) {
     // the automatic Gauss sigma of a subframe reads the PSS estimate of the link's previous subframe 0/5, which
@@ -367,6 +410,19 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
   }
   *d_out_p = d_out;
   if (d_noise_p) *d_noise_p = d_noise;
+  return MI355_SUCCESS;
+}
+
+// subframes [o, o + m) of a deferred chest_launch_only (ranges launched in order: a subframe 0/5 noise hold reads
+// out_all of an earlier range only in chest_resolve)
+static int chest_launch_range(mi355_ue_dl_t* q, uint32_t o, uint32_t m, hipStream_t s)
+{
+  const uint32_t RP = q->nof_rx * q->cell.nof_ports;
+  ChestArgs      a  = q->chest_def;
+  a.jobs            = q->chest_def.jobs + (size_t)o * RP;
+  CHECK_HIP(chest_launch_pre(a, m, q->chest_def_sync, q->chest_def_empty, s));
+  CHECK_HIP(chest_launch(a, m * RP, s));
+  CHECK_HIP(chest_launch_resolve(a, m, q->chest_def_noise ? q->chest_def_noise + o : nullptr, s));
   return MI355_SUCCESS;
 }
 
@@ -638,7 +694,7 @@ static int ctrl_ready(mi355_ue_dl_t* q)
 
 // search results -> srslte_dci_dl_t (srslte_dci_msg_unpack_pdsch with the UE's DCI configuration, ue_dl.c:722-728)
 static int unpack_all(mi355_ue_dl_t* q, const mi355_dl_sf_cfg_t* sfs, const mi355_ue_dl_cfg_t* cfgs, uint32_t n,
-                      mi355_ctrl_res_t* ctrl, std::vector<mi355_dci_msg_t>& msgs, mi355_dci_dl_t* dci, uint32_t first = 0)
+                      mi355_ctrl_res_t* ctrl, mi355_dci_msg_t* msgs, mi355_dci_dl_t* dci, uint32_t first = 0)
 {
   host_parallel_for(n - first, 128, [&](uint32_t b, uint32_t e) {
     for (uint32_t i = first + b; i < first + e; i++) {
@@ -664,14 +720,15 @@ int mi355_ue_dl_find_dl_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* sfj
   int r = ctrl_ready(q);
   if (r) return r;
   std::vector<float>           noise(njobs);
-  std::vector<mi355_dci_msg_t> msgs((size_t)njobs * MI355_MAX_DCI_MSG);
+  // uninitialised: the replay writes every message it reports (1.5 MB of zeroing per 2,048 subframes otherwise)
+  std::unique_ptr<mi355_dci_msg_t[]> msgs(new mi355_dci_msg_t[(size_t)njobs * MI355_MAX_DCI_MSG]);
   for (uint32_t i = 0; i < njobs; i++) noise[i] = chest[i].noise_estimate;
   q->ctrl->ce_row = 0; // the caller's estimates, read where they lie
   if ((r = q->ctrl->run(sfjobs, noise.data(), nullptr, rntis, cfgs, njobs, stream ? (hipStream_t)stream : q->own, ctrl,
-                        msgs.data())))
+                        msgs.get())))
     return r;
   for (uint32_t i = 0; i < njobs; i++) sfs[i].cfi = ctrl[i].cfi;
-  return unpack_all(q, sfs, cfgs, njobs, ctrl, msgs, dci);
+  return unpack_all(q, sfs, cfgs, njobs, ctrl, msgs.get(), dci);
 }
 
 int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, const mi355_dl_sf_job_t* sfjobs,
@@ -693,30 +750,52 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   if (r) return r;
   // srslte_ue_dl_decode_fft_estimate: OFDM + estimation; the noise estimate stays on the device for the control
   // channels, the host fills srslte_chest_dl_res_t while the control kernels run
-  size_t used = 0;
-  if ((r = ofdm_run(q, sfjobs, njobs, s, &used))) return r;
+  // OFDM and estimation of chunk c are launched right in front of chunk c's control kernels (deferred launches),
+  // so the host replays chunk 0's blind searches while the GPU demodulates, estimates and searches chunk 1
+  // (chunk 0's are launched as soon as their tables are up, so the GPU works while the host builds the rest)
+  static const int chunk_env = getenv("MI355_UEDL_CHUNKS") ? atoi(getenv("MI355_UEDL_CHUNKS")) : 0;
+  const uint32_t   forced    = q->chunks ? q->chunks : (chunk_env >= 1 && chunk_env <= 8 ? (uint32_t)chunk_env : 0u);
+  const uint32_t   nchunks   = forced ? std::max(1u, std::min(forced, njobs)) : (njobs >= 256 ? 2u : 1u);
+  const uint32_t   end0      = (uint32_t)((uint64_t)njobs / nchunks); // CtrlState::launch's first chunk boundary
+  const bool       defer     = chest_deferrable(chest_cfg) && njobs > 0;
+  size_t           used      = 0;
+  if ((r = ofdm_run(q, sfjobs, njobs, s, &used, defer))) return r;
+  if (defer && (r = ofdm_launch_range(q, 0, end0, s))) return r;
   float *d_out = nullptr, *d_noise = nullptr;
-  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise, chest_cfg->ce_rows == 1))) return r;
+  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise, chest_cfg->ce_rows == 1, defer)))
+    return r;
+  if (defer && (r = chest_launch_range(q, 0, end0, s))) return r;
   ChestFill fill{q, chest_cfg, nullptr, sfjobs, njobs, chest, false};
-  if ((r = chest_finish_async(q, &fill, d_out, s))) return r;
+  if (!defer && (r = chest_finish_async(q, &fill, d_out, s))) return r;
   std::vector<uint16_t>        rntis(njobs);
-  std::vector<mi355_dci_msg_t> msgs((size_t)njobs * MI355_MAX_DCI_MSG);
+  // uninitialised: the replay writes every message it reports (1.5 MB of zeroing per 2,048 subframes otherwise)
+  std::unique_ptr<mi355_dci_msg_t[]> msgs(new mi355_dci_msg_t[(size_t)njobs * MI355_MAX_DCI_MSG]);
   for (uint32_t i = 0; i < njobs; i++) rntis[i] = cfgs[i].rnti;
   const auto t1 = now();
   // Two chunks: the host replays chunk 0's blind searches and builds its grants while the GPU decodes chunk 1's
   // control channels, and does chunk 1's while the GPU decodes chunk 0's PDSCH, so the GPU never waits for the
   // host's sequential find -> grant order.  Every subframe's outcome is the same as in one
   // chunk: subframes are independent.
-  // (mi355_ue_dl_set_chunks, or MI355_UEDL_CHUNKS = 1..8 when it is not set, overrides the choice: tests, A/B timing)
-  static const int chunk_env = getenv("MI355_UEDL_CHUNKS") ? atoi(getenv("MI355_UEDL_CHUNKS")) : 0;
-  const uint32_t   forced    = q->chunks ? q->chunks : (chunk_env >= 1 && chunk_env <= 8 ? (uint32_t)chunk_env : 0u);
-  const uint32_t   nchunks   = forced ? std::max(1u, std::min(forced, njobs)) : (njobs >= 256 ? 2u : 1u);
+  // (mi355_ue_dl_set_chunks, or MI355_UEDL_CHUNKS = 1..8 when it is not set, overrides the choice: tests, A/B timing;
+  // nchunks above)
   // AVERAGE estimates are time-invariant: the control channels read row 0 (the only one written with ce_rows = 1)
   q->ctrl->ce_row = chest_cfg->estimator_alg == MI355_ESTIMATOR_ALG_AVERAGE ? 12 * q->cell.nof_prb : 0u;
-  if ((r = q->ctrl->launch(sfjobs, nullptr, d_noise, rntis.data(), ue_cfgs, njobs, nchunks, s))) {
+  auto front = [&](uint32_t o, uint32_t m) -> int {
+    if (o == 0) return MI355_SUCCESS; // chunk 0: launched above
+    int e = ofdm_launch_range(q, o, m, s);
+    return e ? e : chest_launch_range(q, o, m, s);
+  };
+  if ((r = q->ctrl->launch(sfjobs, nullptr, d_noise, rntis.data(), ue_cfgs, njobs, nchunks, s,
+                           defer ? std::function<int(uint32_t, uint32_t)>(front) : nullptr))) {
+    if (defer) {
+      (void)hipStreamSynchronize(s);
+      return r; // srslte_chest_dl_res_t left unfilled: the call failed
+    }
     chest_fill_cb(&fill);
     return r;
   }
+  if (defer && (r = chest_finish_async(q, &fill, d_out, s))) return r;
+  const auto t1c = now();
   struct Chunk {
     uint32_t                       b = 0, e = 0;
     std::vector<mi355_pdsch_job_t> jobs;
@@ -730,9 +809,9 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
     Chunk& C = ck[c];
     C.b      = c ? q->ctrl->chunk_end[c - 1] : 0;
     C.e      = q->ctrl->chunk_end[c];
-    if ((C.r = q->ctrl->finish(c, rntis.data(), ue_cfgs, ctrl, msgs.data()))) return;
+    if ((C.r = q->ctrl->finish(c, rntis.data(), ue_cfgs, ctrl, msgs.get()))) return;
     for (uint32_t i = C.b; i < C.e; i++) sfs[i].cfi = ctrl[i].cfi;
-    if ((C.r = unpack_all(q, sfs, ue_cfgs, C.e, ctrl, msgs, dci, C.b))) return;
+    if ((C.r = unpack_all(q, sfs, ue_cfgs, C.e, ctrl, msgs.get(), dci, C.b))) return;
     host_parallel_for(C.e - C.b, 128, [&](uint32_t lo, uint32_t hi) { // grants: independent per subframe
       for (uint32_t i = C.b + lo; i < C.b + hi; i++) {
         if (ctrl[i].nof_dci != 1) continue; // the reference decodes only when exactly one DCI was found
@@ -773,6 +852,7 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
       C.which.push_back(i);
     }
   };
+  const auto t2a = now();
   prepare(0);
   const auto t2 = now();
   if (ck[0].r) {
@@ -820,8 +900,9 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   const auto t3 = now();
   if (prof) {
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-    fprintf(stderr, "[mi355 host] find_and_decode: launch ofdm/chest %.1f us, control launch + chunk 0 replay/grants "
-                    "%.1f us, pdsch+dlsch (chunk 1 host work hidden) %.1f us\n", us(t0, t1), us(t1, t2), us(t2, t3));
+    fprintf(stderr, "[mi355 host] find_and_decode: launch ofdm/chest %.1f us, control launch %.1f us, chunk 0 "
+                    "replay/grants %.1f us (wait included), pdsch+dlsch (chunk 1 host work hidden) %.1f us\n",
+            us(t0, t1), us(t1, t1c), us(t2a, t2), us(t2, t3));
   }
   return r;
 }

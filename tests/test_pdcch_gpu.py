@@ -115,12 +115,17 @@ def _make_dci(D, cell, fmt, mcs, rnti):
     return d
 
 
+@pytest.mark.parametrize("full", [False, True], ids=["hits", "full_readback"])
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_find_and_decode_end_to_end(case):
+def test_find_and_decode_end_to_end(case, full, monkeypatch):
     """Subframes synthesised with the product's eNodeB-side encoders (DCI pack, PCFICH / PDCCH, PDSCH) through a
     frequency-selective channel; mi355_ue_dl_find_and_decode_batch must find exactly the transmitted DCI at its
     UE-specific candidate, derive the transmitted grant and decode every TB with CRC ok.  The control-channel
-    LLRs and blind-search result are checked bit-exactly against the oracle on the GPU's own grids."""
+    LLRs and blind-search result are checked bit-exactly against the oracle on the GPU's own grids.
+    full: the replay reads every subframe's whole candidate array (the overflow path of the compact per-subframe
+    hit records, pdcch_runtime.cpp) instead of the records."""
+    if full:
+        monkeypatch.setenv("MI355_PDCCH_HMAX", "0")
     from srsran_amd import pdcch as D
     from srsran_amd import pdsch as S
     from srsran_amd.dlsch import SoftbufferPool

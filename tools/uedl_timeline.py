@@ -1,14 +1,18 @@
 #!/usr/bin/env python3
-"""Kernel timeline (with GPU idle gaps) of the last find_and_decode step of a tools/trace_uedl.sh run."""
+"""Kernel timeline (with GPU idle gaps) of the last find_and_decode step of a tools/trace_uedl.sh run: from the first
+kernel after the previous step's last DL-SCH epilogue to the step's own last epilogue (each step ends with one
+epilogue per chunk: --chunks, default 2).  -v prints every kernel, otherwise only gaps > 20 us and kernels > 100 us."""
 import csv
 import glob
 import sys
 
-tag = sys.argv[1] if len(sys.argv) > 1 else "cur"
+tag = next((a for a in sys.argv[1:] if not a.startswith("-")), "cur")
+nch = next((int(a.split("=")[1]) for a in sys.argv[1:] if a.startswith("--chunks=")), 2)
 f = glob.glob(f"gpurun_out/tu_{tag}/**/*kernel_trace.csv", recursive=True)[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
-last = max(i for i, r in enumerate(rows) if "dlsch_tb_epilogue" in r["Kernel_Name"])
-first = max(i for i, r in enumerate(rows[:last]) if "ofdm_rx" in r["Kernel_Name"])
+eps = [i for i, r in enumerate(rows) if "dlsch_tb_epilogue" in r["Kernel_Name"]]
+last = eps[-1]
+first = eps[-1 - nch] + 1 if len(eps) > nch else 0
 t0 = int(rows[first]["Start_Timestamp"])
 prev_end, busy = t0, 0
 agg = {}
