@@ -123,4 +123,13 @@ __device__ inline uint32_t block_crc24(const uint8_t* bytes, uint32_t nbytes, co
   return part[0] ^ part[1] ^ part[2] ^ part[3];
 }
 
+// running flags (dlsch_runtime.cpp): flag[h] != 0 means some code block is still being decoded at half-iteration h.
+// Writers store only when the flag still reads 0 (L2-coherent load), so the flag line is not hammered by thousands
+// of stores.
+__device__ __forceinline__ void flag_set(uint32_t* f)
+{
+  if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 } // namespace mi355

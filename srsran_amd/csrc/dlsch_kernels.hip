@@ -154,13 +154,9 @@ __global__ __launch_bounds__(256) void dlsch_rm_consume(const CbDesc* desc, int 
 // TB payload; only the last CB keeps its trailing CRC bytes (the earlier ones are overwritten by the
 // next CB in the reference's sequential loop, sch.c:422-424).
 // "work remains" flags instead of a counter: running[h] != 0 iff some code block is unfinished before
-// half-iteration h.  Writers aggregate per workgroup and only store when the flag still reads 0 (L2-coherent
-// load), so the flag line is not hammered by thousands of stores.
-__device__ __forceinline__ void flag_set(uint32_t* f)
-{
-  if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-    __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// half-iteration h (flag_set, crc_device.h; writers aggregate per workgroup).
+// When the window decoder writes decision bytes itself, it runs this check in its own epilogue (tdec_kernels.hip
+// tdec_fused_check, same semantics) and this kernel is not launched.
 
 __global__ __launch_bounds__(1024) void dlsch_cb_check(DlschCheckArgs a)
 {

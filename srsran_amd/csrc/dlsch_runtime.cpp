@@ -153,19 +153,26 @@ static int crc_scales(mi355_dlsch_t* q, uint32_t K, const uint32_t** out)
 {
   auto it = q->scales.find(K);
   if (it == q->scales.end()) {
-    std::vector<uint32_t> t(128);
+    // [0, 128): 64 lanes of a wave (dlsch_cb_check); [128, 144): the NL = nsb / 2 lanes of a code block in the
+    // window decoder's fused check (tdec_kernels.hip), 8 per polynomial
+    std::vector<uint32_t> t(144, 0u);
     const uint32_t        nbytes = K / 8, chunk = (nbytes + 63) / 64;
     const uint32_t        polys[2] = {0x1864CFB, 0x1800063};
+    auto                  xpow = [](uint32_t after, uint32_t poly) { // x^(8 * after) mod P
+      uint32_t sc = 1, x8 = 1u << 8; // x^(8 * 2^i)
+      for (; after; after >>= 1) {
+        if (after & 1) sc = gf2_mulmod24_host(sc, x8, poly);
+        x8 = gf2_mulmod24_host(x8, x8, poly);
+      }
+      return sc;
+    };
+    const uint32_t nl = std::max(1u, mi355_tdec_autoimp_get_subblocks(K) / 2), cl = nbytes / nl;
     for (int pi = 0; pi < 2; pi++) {
       for (uint32_t lane = 0; lane < 64; lane++) {
         const uint32_t b0 = std::min(nbytes, lane * chunk), b1 = std::min(nbytes, b0 + chunk);
-        uint32_t       sc = 1, x8 = 1u << 8; // x^(8 * 2^i)
-        for (uint32_t after = nbytes - b1; after; after >>= 1) {
-          if (after & 1) sc = gf2_mulmod24_host(sc, x8, polys[pi]);
-          x8 = gf2_mulmod24_host(x8, x8, polys[pi]);
-        }
-        t[pi * 64 + lane] = sc;
+        t[pi * 64 + lane] = xpow(nbytes - b1, polys[pi]);
       }
+      for (uint32_t l = 0; l < nl && l < 8; l++) t[128 + 8 * pi + l] = xpow(nbytes - (l + 1) * cl, polys[pi]);
     }
     uint32_t* d = nullptr;
     CHECK_HIP(hipMalloc(&d, t.size() * 4));
@@ -670,15 +677,17 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
         b.in = (int8_t*)pool->buf, b.in_stride = SB_STRIDE * sizeof(int16_t), b.slot = d_slot + lv.off;
         b.done = d_done + lv.off, b.running = d_run + h, b.K = lv.K, b.ncb = lv.n;
         if ((r = tdec8_halfit_batch(lv.t8, b, h, lv.dec, lv.K / 8, s))) return r;
-      } else {
-        TdecRun rq{llr8 ? pool->buf + SB_CONV8 : pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, d_run + h, lv.n,
-                   lv.K, h, h + 1, lv.dec, lv.K / 8, s};
-        if ((r = mi355_tdec_run_internal(lv.td, rq))) return r;
       }
       DlschCheckArgs ca{d_cb + lv.off, (int)lv.n, lv.K, h, q->max_its, lv.dec, lv.K / 8, d_data,
                         d_done + lv.off, d_run + h, d_run + h + 1, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1],
                         lv.scale};
-      CHECK_HIP(dlsch_launch_check(ca, s));
+      bool fused = false; // the window decoder's decision-byte launches run the check in their epilogue
+      if (!lv.t8) {
+        TdecRun rq{llr8 ? pool->buf + SB_CONV8 : pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, d_run + h, lv.n,
+                   lv.K, h, h + 1, lv.dec, lv.K / 8, s, &ca, &fused};
+        if ((r = mi355_tdec_run_internal(lv.td, rq))) return r;
+      }
+      if (!fused) CHECK_HIP(dlsch_launch_check(ca, s));
     }
   }
   CHECK_HIP(dlsch_launch_epilogue(ta, s));

@@ -32,6 +32,8 @@ namespace mi355 {
 CtrlState::~CtrlState()
 {
   for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : kev) (void)hipEventDestroy(e);
+  if (rb) (void)hipStreamDestroy(rb);
   (void)hipFree(d_tab);
   (void)hipFree(d_buf);
   delete st;
@@ -143,10 +145,13 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
   b_corr_ = b_corr;
   chunk_end.assign(nchunks, 0);
   while (ev.size() < nchunks) {
-    hipEvent_t e;
+    hipEvent_t e, k;
     CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    CHECK_HIP(hipEventCreateWithFlags(&k, hipEventDisableTiming));
     ev.push_back(e);
+    kev.push_back(k);
   }
+  if (!rb) CHECK_HIP(hipStreamCreateWithFlags(&rb, hipStreamNonBlocking));
   for (uint32_t c = 0; c < nchunks; c++) {
     const uint32_t o = (uint32_t)((uint64_t)n * c / nchunks), m = (uint32_t)((uint64_t)n * (c + 1) / nchunks) - o;
     chunk_end[c]     = o + m;
@@ -180,12 +185,16 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
     CHECK_HIP(ctrl_launch_blind(b, m, s));
     CompactArgs h{(const BlindJob*)(base + b_jobs) + o, d_cand + (size_t)o * ncand, d_hits + o};
     CHECK_HIP(ctrl_launch_compact(h, m, s));
-    CHECK_HIP(hipMemcpyAsync(back->host + 4 * (size_t)o, d_cfi + o, 4 * (size_t)m, hipMemcpyDeviceToHost, s));
+    // the read-backs run on a stream of their own behind the chunk's kernels: the compute stream goes on to the next
+    // chunk (and to the PDSCH the caller enqueues) without device-to-host copies in its queue
+    CHECK_HIP(hipEventRecord(kev[c], s));
+    CHECK_HIP(hipStreamWaitEvent(rb, kev[c], 0));
+    CHECK_HIP(hipMemcpyAsync(back->host + 4 * (size_t)o, d_cfi + o, 4 * (size_t)m, hipMemcpyDeviceToHost, rb));
     CHECK_HIP(hipMemcpyAsync(back->host + b_cfi + 12 * (size_t)o, d_corr + 3 * (size_t)o, 12 * (size_t)m,
-                             hipMemcpyDeviceToHost, s));
+                             hipMemcpyDeviceToHost, rb));
     CHECK_HIP(hipMemcpyAsync(back->host + b_cfi + b_corr + (size_t)o * sizeof(DciHits), d_hits + o,
-                             (size_t)m * sizeof(DciHits), hipMemcpyDeviceToHost, s));
-    CHECK_HIP(hipEventRecord(ev[c], s));
+                             (size_t)m * sizeof(DciHits), hipMemcpyDeviceToHost, rb));
+    CHECK_HIP(hipEventRecord(ev[c], rb));
   }
   last_n = n, last_stride = stride, last_llr = d_llr, last_cand = d_cand;
   return MI355_SUCCESS;

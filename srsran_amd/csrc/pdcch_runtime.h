@@ -32,7 +32,9 @@ struct CtrlState {
   // launch(): the arena layout and the per-chunk completion events of the pending call
   size_t                b_cfi_ = 0, b_corr_ = 0;
   std::vector<uint32_t> chunk_end;
-  std::vector<hipEvent_t> ev;
+  std::vector<hipEvent_t> ev;  // chunk c's read-back landed (on rb)
+  std::vector<hipEvent_t> kev; // chunk c's kernels done (on the compute stream)
+  hipStream_t             rb = nullptr; // read-back stream
 
   ~CtrlState();
   int init(const mi355_cell_t& c, uint32_t nof_rx);

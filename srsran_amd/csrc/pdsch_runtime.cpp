@@ -480,18 +480,24 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   CHECK_HIP(q->stage.upload(base, s, after_s, after_s && q->fe_armed ? q->fe_done : nullptr));
   const auto tc = now();
   CHECK_HIP(pdsch_launch_equalize((const PdschJobDev*)(base + o_jobs), njobs, max_units, s));
+  const auto tl0 = now();
   CHECK_HIP(pdsch_launch_scr_pack((const uint32_t*)(base + o_nci), (uint32_t* const*)(base + o_ndst),
                                   (uint32_t)new_ci.size(), q->gold, PDSCH_GOLD_MAX / 32, s));
+  const auto tl1 = now();
   CHECK_HIP(pdsch_launch_fused((const PdschJobDev*)(base + o_jobs), njobs, max_fpairs, fkeys.data(),
                                (uint32_t)fkeys.size(), s));
+  const auto tl2 = now();
   CHECK_HIP(pdsch_launch_llr((const PdschCwDev*)(base + o_cws), (uint32_t)ncw, max_pairs, s));
+  const auto tl3 = now();
   if (!q->fe_done) CHECK_HIP(hipEventCreateWithFlags(&q->fe_done, hipEventDisableTiming));
   CHECK_HIP(hipEventRecord(q->fe_done, s));
   q->fe_armed = true;
   if (prof) {
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-    fprintf(stderr, "[mi355 host] pdsch frontend: tables %.1f us, put %.1f us, upload %.1f us, launches %.1f us\n",
-            us(t_in, ta), us(ta, tb), us(tb, tc), us(tc, now()));
+    fprintf(stderr, "[mi355 host] pdsch frontend: tables %.1f us, put %.1f us, upload %.1f us, launches %.1f us "
+                    "(equalize %.1f, scr %.1f, fused %.1f, llr %.1f, event %.1f)\n",
+            us(t_in, ta), us(ta, tb), us(tb, tc), us(tc, now()), us(tc, tl0), us(tl0, tl1), us(tl1, tl2), us(tl2, tl3),
+            us(tl3, now()));
   }
   return MI355_SUCCESS;
 }

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "dlsch_internal.h"
+
 #define TDEC_INF 10000   // turbodecoder_win.h:151 / turbodecoder_gen.c:37
 #define TDEC_WARMUP 40   // win_overlap_len, turbodecoder_win.h:149
 #define TDEC_SEG 8       // beta checkpoint spacing (rows) of the window kernel
@@ -29,6 +31,12 @@ struct TdecWinArgs {
   size_t          dec_stride;
   const uint32_t* gS;   // microbenchmarks only (GI builds): wave-group interleaved systematic / parity
   const uint32_t* gP;
+  // DL-SCH code-block check fused into the epilogue of a decision-byte half-iteration (chk_on != 0, dec != nullptr):
+  // dlsch_cb_check's semantics (CRC of the K/8 decision bytes, payload copy, done / iteration / softbuffer CRC flags,
+  // next running flag) on the code block's own lanes, the decision bytes taken from LDS; chk.desc etc. indexed like
+  // the batch's code blocks.  chk.scale[128 + 8 * (C > 1) + l]: x^(8 * bytes after lane l's K/(8 NL)-byte chunk).
+  DlschCheckArgs  chk;
+  int             chk_on;
 };
 
 struct TdecDecideArgs {
@@ -79,6 +87,8 @@ struct TdecRun {
   uint8_t*        out;
   size_t          out_stride;
   hipStream_t     stream;
+  const DlschCheckArgs* chk = nullptr;       // DL-SCH: the check of each half-iteration, fused where the kernel can
+  bool*                 chk_fused = nullptr; // set when it was (the caller then launches no dlsch_cb_check)
 };
 
 hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s);

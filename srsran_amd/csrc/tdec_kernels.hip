@@ -29,6 +29,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "crc_device.h"
 #include "tdec_internal.h"
 
 namespace mi355 {
@@ -124,6 +125,46 @@ __device__ __forceinline__ void set_minf(v2s s[8])
   for (int i = 0; i < 8; i++) s[i] = splat(-TDEC_INF);
 }
 
+// ---------------------------------------------------------------------------- fused code-block check
+// dlsch_cb_check (dlsch_kernels.hip; sch.c:420-450) on the NL lanes of one code block, right after the
+// half-iteration that produced its K/8 decision bytes in LDS (bm): lane l folds bytes [l c, (l + 1) c), c = K/(8 NL),
+// with the slice-by-4 tables t4 (LDS), scales by x^(8 * bytes after its chunk) and the NL partial CRCs are xor-
+// reduced inside the code block's lane group.  CRC 0 (CRC24B for C > 1, CRC24A for C = 1), or the last allowed
+// half-iteration: the bytes go to the TB payload at cb * rlen / 8 (the last CB keeps its CRC bytes), the
+// iteration count and the done / softbuffer-CRC flags are set; otherwise the next half-iteration's running flag.
+template <int NL>
+__device__ __forceinline__ void tdec_fused_check(const TdecWinArgs& a, int cb, int l, int K, const uint32_t* bm,
+                                                 const uint32_t (*t4)[4][256])
+{
+  const DlschCheckArgs& c      = a.chk;
+  const CbDesc&         d      = c.desc[cb];
+  const uint32_t        nbytes = (uint32_t)K / 8, chunk = nbytes / NL;
+  const int             pi     = d.C > 1 ? 1 : 0;
+  const uint8_t*        bytes  = (const uint8_t*)bm;
+  uint32_t              crc    = crc24_words(bytes + l * chunk, chunk, t4[pi]);
+  crc = gf2_mulmod24(crc, c.scale[128 + 8 * pi + l], pi ? c.crc24b->poly : c.crc24a->poly);
+#pragma unroll
+  for (int o = NL / 2; o >= 1; o >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o, 64);
+  const bool ok  = crc == 0;
+  const bool fin = ok || c.h + 1 == c.max_its;
+  if (fin) {
+    uint8_t*       dst = c.data + d.data_off + (size_t)d.cb * d.rlen / 8;
+    const uint32_t nb  = (d.cb + 1 == d.C) ? nbytes : d.rlen / 8;
+    for (uint32_t i = l; i < nb; i += NL) dst[i] = bytes[i];
+    if (l == 0) {
+      c.its[cb] = c.h + 1;
+      if (ok) {
+        c.done[cb]       = 1;
+        c.sb_crc[d.slot] = 1;
+      } else {
+        c.done[cb] = 2; // gave up: CRC error after max_iterations
+      }
+    }
+  }
+  const uint64_t un = __builtin_amdgcn_ballot_w64(l == 0 && !fin); // one store per wave at most
+  if (un && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(un)) flag_set(c.next);
+}
+
 // ---------------------------------------------------------------------------- window MAP kernel
 //
 // HBM layout ("wave-group interleaved"): code blocks are grouped G = 64/NL at a time so
@@ -161,7 +202,8 @@ __device__ __forceinline__ void set_minf(v2s s[8])
 // that 1 KB is exactly [step][64 lanes] (lane q = cbg*8 + l finds step s at word 64*s + q, one bank per lane), so the
 // transposition costs one ds_write_b128 per 4 steps and one ds_read_b32 per step.
 template <int NSB, int SEG, int MODE, int DIAG, bool FULL, int OUTK, bool GI = false, bool TX = false>
-__device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl)
+__device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl,
+                                              const uint32_t (*crc_t4)[4][256] = nullptr)
 {
   constexpr int NL = NSB / 2;
   constexpr int G  = 64 / NL;
@@ -586,8 +628,12 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint2* o = (uint2*)(a.dec + (size_t)cb * a.dec_stride);
-    for (int w = l; w < K / 64; w += NL) o[w] = make_uint2(bm[2 * w], bm[2 * w + 1]);
+    if (crc_t4) { // DL-SCH: the code-block check straight from LDS (nothing else reads the decision bytes)
+      tdec_fused_check<NL>(a, cb, l, K, bm, crc_t4);
+    } else {
+      uint2* o = (uint2*)(a.dec + (size_t)cb * a.dec_stride);
+      for (int w = l; w < K / 64; w += NL) o[w] = make_uint2(bm[2 * w], bm[2 * w + 1]);
+    }
   }
 }
 
@@ -597,15 +643,33 @@ template <int NSB, int SEG, int MODE, int DIAG = 0, bool FULL = false, int OUTK 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_PER_EU))) void tdec_win_halfit(TdecWinArgs a)
 {
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t (*t4)[4][256] = nullptr;
+  if constexpr (OUTK == 1) {
+    __shared__ uint32_t crc_t4[2][4][256]; // CRC24A | CRC24B slice-by-4 tables (fused code-block check)
+    if (a.chk_on) { // uniform: the whole block builds the tables before any wave decodes
+      if (a.remaining && *a.remaining == 0) return; // every code block of the batch has finished
+      const uint32_t ti = threadIdx.x;
+      crc_t4[0][0][ti] = a.chk.crc24a->t[ti]; // blockDim == 256
+      crc_t4[1][0][ti] = a.chk.crc24b->t[ti];
+      __syncthreads();
+#pragma unroll
+      for (int k = 1; k < 4; k++) { // one more zero byte per table
+        crc_t4[0][k][ti] = crc24_step_table(crc_t4[0][k - 1][ti], crc_t4[0][0]);
+        crc_t4[1][k][ti] = crc24_step_table(crc_t4[1][k - 1][ti], crc_t4[1][0]);
+        __syncthreads();
+      }
+      t4 = crc_t4;
+    }
+  }
   if constexpr (TX) {
     const int  cb  = (gl >> 6) * (128 / NSB) + (gl & 63) / (NSB / 2);
     const bool act = cb < a.ncb && !(a.done && a.done[cb]);
     if (__builtin_amdgcn_ballot_w64(act) == ~0ull) {
-      tdec_win_body<NSB, SEG, MODE, DIAG, FULL, OUTK, false, true>(a, gl);
+      tdec_win_body<NSB, SEG, MODE, DIAG, FULL, OUTK, false, true>(a, gl, t4);
       return;
     }
   }
-  tdec_win_body<NSB, SEG, MODE, DIAG, FULL, OUTK>(a, gl);
+  tdec_win_body<NSB, SEG, MODE, DIAG, FULL, OUTK>(a, gl, t4);
 }
 
 // ---------------------------------------------------------------------------- layout kernels

@@ -285,6 +285,12 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
       TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, rq.remaining, A1, E, D, CK, t->dstE, t->dstA,
                      (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == h1,
                      (fuse && h + 1 == h1) ? d_out : nullptr, out_stride};
+      if (rq.chk && fuse && h + 1 == h1) { // the DL-SCH check of this half-iteration in the kernel's epilogue
+        wa.chk    = *rq.chk;
+        wa.chk.h  = h;
+        wa.chk_on = 1;
+        if (rq.chk_fused) *rq.chk_fused = true;
+      }
       hipEvent_t e0 = nullptr, e1 = nullptr;
       if (q->prof) {
         e0 = next_event(q);
