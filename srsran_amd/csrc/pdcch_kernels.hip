@@ -202,6 +202,22 @@ constexpr uint32_t WAVES   = 1;
 constexpr uint32_t MAXSYM  = 3 * PDCCH_MAX_F; // 432
 static_assert((PDCCH_SLOTS * PDCCH_FMTS) % WAVES == 0, "a workgroup never straddles two subframes' tail");
 
+// x^(d + 16) mod (x^16 + x^12 + x^5 + 1) for d < 128: the CRC16 contribution of a payload bit d places from the end
+struct Crc16Pow {
+  uint16_t v[128];
+  constexpr Crc16Pow() : v()
+  {
+    uint32_t r = 0x1021u; // x^16 mod P
+    for (int d = 0; d < 128; d++) {
+      v[d] = (uint16_t)r;
+      r    = (r << 1) ^ ((r & 0x8000u) ? 0x1021u : 0u);
+      r &= 0xFFFFu;
+    }
+  }
+};
+__constant__ Crc16Pow c_crc16_pow_t = Crc16Pow();
+#define c_crc16_pow (c_crc16_pow_t.v)
+
 __constant__ uint8_t c_perm[32]     = {1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31,
                                    0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30};
 __constant__ uint8_t c_perm_inv[32] = {16, 0, 24, 8, 20, 4, 28, 12, 18, 2, 26, 10, 22, 6, 30, 14,
@@ -374,7 +390,9 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
   // 64-state Viterbi, lane = state; state s takes predecessors j = s >> 1 and j + 32
   const uint32_t j   = lane >> 1;
   const uint32_t pat = par((2 * j) & 0x6Du) | par((2 * j) & 0x4Fu) << 1 | par((2 * j) & 0x57u) << 2;
-  const bool     odd = lane & 1u;
+  // branch metrics are 13-bit (a 16-bit sum >> 3), so 8191 - m = m ^ 8191: the odd states' complement is one xor
+  const uint32_t flip = (lane & 1u) ? 8191u : 0u;
+  const uint16_t* bml = S.bm + pat;
   const uint32_t Fs  = __builtin_amdgcn_readfirstlane(F); // uniform: the step counters live in scalar registers
   uint32_t       met = 0;
   // decision words: step tb + k's ballot goes to lane k of (dlo, dhi), one 64-lane store per 64 steps
@@ -382,9 +400,9 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
     const uint32_t te  = __builtin_amdgcn_readfirstlane(min(3 * Fs - tb, 64u));
     uint32_t       dlo = 0, dhi = 0;
     for (uint32_t k = 0; k < te; k++, o = (o + 1 == Fs) ? 0 : o + 1) {
-      const uint32_t mt = (uint16_t)S.bm[8 * o + pat], xa = odd ? 8191u - mt : mt, ya = 8191u - xa;
+      const uint32_t xa = (uint32_t)bml[8 * o] ^ flip; // ya = 8191 - xa = xa ^ 8191
       const uint32_t oj = (uint32_t)__shfl((int)met, (int)j, 64), oj32 = (uint32_t)__shfl((int)met, (int)(j + 32), 64);
-      const uint32_t x = oj + xa, y = oj32 + ya; // only the low 16 bits matter (wrapping u16 metrics)
+      const uint32_t x = oj + xa, y = (xa ^ 8191u) + oj32; // only the low 16 bits matter (wrapping u16 metrics)
       const bool     d = (int16_t)(uint16_t)(x - y) > 0;
       met              = d ? y : x;
       const uint64_t w = __ballot(d);
@@ -419,23 +437,49 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
     nb -= cnt;
   }
   __builtin_amdgcn_wave_barrier();
-  if (lane == 0) {
-    uint32_t crc = 0, p = 0;
-    for (uint32_t i = 0; i < nbits; i++) {
-      const uint32_t fb = ((crc >> 15) ^ S.bits[i]) & 1u;
-      crc               = (crc << 1) & 0xFFFFu;
-      if (fb) crc ^= 0x1021u;
+  // CRC16 (crc.c, poly 0x1021, zero init: payload(x) * x^16 mod P) is linear in the payload bits: bit i contributes
+  // x^(nbits - 1 - i + 16) mod P, so every lane takes its bits' terms and the wave xor-reduces; the payload words
+  // (MSB first) and the received parity come from ballots of the decoded bits -- no serial per-bit loop on one lane
+  if (F > 128) { // (no LTE DCI is this long: MI355_DCI_MAX_BITS bounds the buffer) the serial form
+    if (lane == 0) {
+      uint32_t crc = 0, p = 0;
+      for (uint32_t i = 0; i < nbits; i++) {
+        const uint32_t fb = ((crc >> 15) ^ S.bits[i]) & 1u;
+        crc               = (crc << 1) & 0xFFFFu;
+        if (fb) crc ^= 0x1021u;
+      }
+      for (uint32_t i = 0; i < 16; i++) p = (p << 1) | S.bits[nbits + i];
+      out->status = 2, out->crc_rem = p ^ crc, out->L = L, out->ncce = ncce;
+      for (uint32_t q = 0; q < 4; q++) {
+        uint32_t w = 0;
+        for (uint32_t b = 0; b < 32; b++)
+          if (32 * q + b < nbits) w |= (uint32_t)S.bits[32 * q + b] << (31 - b);
+        out->bits[q] = w;
+      }
     }
-    for (uint32_t i = 0; i < 16; i++) p = (p << 1) | S.bits[nbits + i];
+    return;
+  }
+  uint32_t       crc = 0;
+  const uint32_t b0 = lane < F ? S.bits[lane] : 0u, b1 = lane + 64 < F ? S.bits[lane + 64] : 0u;
+  if (lane < nbits && b0) crc ^= c_crc16_pow[nbits - 1 - lane];
+  if (lane + 64 < nbits && b1) crc ^= c_crc16_pow[nbits - 1 - (lane + 64)];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o, 64);
+  const uint64_t m0 = __ballot(b0 != 0), m1 = __ballot(b1 != 0); // bit i of the decoded block: lane i of (m0, m1)
+  if (lane == 0) {
+    // the 16 parity bits follow the payload, MSB first: bits nbits .. nbits + 15 of the 128-bit (m1:m0)
+    const uint32_t sh = nbits, p = (uint32_t)__builtin_bitreverse32(
+                                       (uint32_t)(sh < 64 ? (m0 >> sh) | (sh ? m1 << (64 - sh) : 0ull) : m1 >> (sh - 64))) >>
+                                   16;
     out->status  = 2;
     out->crc_rem = p ^ crc;
     out->L       = L;
     out->ncce    = ncce;
+    const uint32_t w[4] = {(uint32_t)m0, (uint32_t)(m0 >> 32), (uint32_t)m1, (uint32_t)(m1 >> 32)};
+#pragma unroll
     for (uint32_t q = 0; q < 4; q++) {
-      uint32_t w = 0;
-      for (uint32_t b = 0; b < 32; b++)
-        if (32 * q + b < nbits) w |= (uint32_t)S.bits[32 * q + b] << (31 - b);
-      out->bits[q] = w;
+      const uint32_t n = nbits > 32 * q ? min(32u, nbits - 32 * q) : 0u; // payload bits in word q
+      out->bits[q]     = n ? __builtin_bitreverse32(w[q]) & (0xFFFFFFFFu << (32 - n)) : 0u;
     }
   }
 }
