@@ -223,17 +223,26 @@ __constant__ uint8_t c_perm[32]     = {1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 2
 __constant__ uint8_t c_perm_inv[32] = {16, 0, 24, 8, 20, 4, 28, 12, 18, 2, 26, 10, 22, 6, 30, 14,
                                        17, 1, 25, 9, 21, 5, 29, 13, 19, 3, 27, 11, 23, 7, 31, 15};
 
+// 5,152 B per wave (31 waves per CU by LDS): every array shares storage with one that is dead by the time it is
+// written -- bm and the decoded bits with the rate-dematching buffers, the decision words with the quantised symbols
+// (the Viterbi reads the branch-metric table only) -- and only the decisions the traceback reads (steps F .. 3F-1)
+// are kept
 struct WaveLds {
   union {
     struct {
       float    tmp[3 * 32 * 5];  // rate-dematching circular buffer (3 K_pi, K_pi <= 160)
       uint16_t rank_pos[MAXSYM]; // position of the r-th non-dummy bit in the circular buffer
     };
-    uint16_t bm[PDCCH_MAX_F * 8]; // branch metric per (t mod F, encoder output pattern), once the above are dead
+    struct {
+      uint16_t bm[PDCCH_MAX_F * 8]; // branch metric per (t mod F, encoder output pattern), once the above are dead
+      uint8_t  bits[PDCCH_MAX_F];   // decoded bits (middle repetition), written by the traceback
+    };
   };
-  uint16_t q[MAXSYM];         // quantised soft symbols
-  uint64_t dec[MAXSYM + 8];   // decision words per trellis step (bit s: survivor choice of state s)
-  uint8_t  bits[PDCCH_MAX_F]; // decoded bits (middle repetition)
+  union {
+    uint16_t q[MAXSYM];                // quantised soft symbols, dead once bm is built
+    uint64_t dec[2 * PDCCH_MAX_F + 8]; // decision word of step F + i (bit s: survivor choice of state s); the
+                                       // traceback reads 6 steps ahead, past 3F - 1: zero words
+  };
 };
 
 __device__ __forceinline__ double wave_sum(double v)
@@ -376,7 +385,6 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
       S.q[i]    = (uint16_t)q;
     }
   }
-  for (uint32_t i = lane; i < 8; i += 64) S.dec[3 * F + i] = 0;
   __builtin_amdgcn_wave_barrier();
   // the branch metric of step t depends only on the symbol triple (t mod F) and the state's encoder output pattern
   // (8 of them): tabulate it once instead of recomputing it 3 times per trellis step in all 64 lanes
@@ -387,6 +395,7 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
     S.bm[e]           = (uint16_t)((((c2 ^ S.q[o + 2]) + av + 1) >> 1) >> 3);
   }
   __builtin_amdgcn_wave_barrier();
+  for (uint32_t i = lane; i < 8; i += 64) S.dec[2 * F + i] = 0; // (q is dead now: dec shares its storage)
   // 64-state Viterbi, lane = state; state s takes predecessors j = s >> 1 and j + 32
   const uint32_t j   = lane >> 1;
   const uint32_t pat = par((2 * j) & 0x6Du) | par((2 * j) & 0x4Fu) << 1 | par((2 * j) & 0x57u) << 2;
@@ -408,20 +417,21 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
       const uint64_t w = __ballot(d);
       writelane2(dlo, dhi, w, k);
     }
-    if (lane < te) S.dec[tb + lane] = (uint64_t)dhi << 32 | dlo;
+    if (lane < te && tb + lane >= Fs) S.dec[tb + lane - Fs] = (uint64_t)dhi << 32 | dlo;
   }
   met &= 0xFFFFu;
   // best end state: the last index of the smallest (unsigned) metric
   const uint32_t key  = wave_min((met << 6) | (63u - lane));
   const uint32_t best = 63u - ((uint32_t)__builtin_amdgcn_readfirstlane((int)key) & 63u);
   __builtin_amdgcn_wave_barrier();
-  // chainback over steps 3F-1 .. F (decision word of step n read at n + 6, as the AVX2 traceback) in blocks of 64:
+  // chainback over steps 3F-1 .. F (decision word of step n read at n + 6, as the AVX2 traceback; kept at dec[n - F])
+  // in blocks of 64:
   // lane k holds the word of step nb-1-k, the survivor state walks through scalar registers by readlane, and the
   // decoded bits of the middle repetition are stored once per block
   uint32_t es = best << 2;
   for (uint32_t nb = 3 * Fs; nb > Fs;) {
     const uint32_t cnt = min(64u, nb - Fs);
-    const uint64_t v   = lane < cnt ? S.dec[nb - 1 - lane + 6] : 0;
+    const uint64_t v   = lane < cnt ? S.dec[nb - 1 - lane + 6 - Fs] : 0;
     const int      vlo = (int)(uint32_t)v, vhi = (int)(uint32_t)(v >> 32);
     uint32_t       bitv = 0;
     for (uint32_t k = 0; k < cnt; k++) {

@@ -148,9 +148,20 @@ __device__ __forceinline__ void tdec_fused_check(const TdecWinArgs& a, int cb, i
   const bool ok  = crc == 0;
   const bool fin = ok || c.h + 1 == c.max_its;
   if (fin) {
-    uint8_t*       dst = c.data + d.data_off + (size_t)d.cb * d.rlen / 8;
-    const uint32_t nb  = (d.cb + 1 == d.C) ? nbytes : d.rlen / 8;
-    for (uint32_t i = l; i < nb; i += NL) dst[i] = bytes[i];
+    // payload bytes [0, nb) to dst (any alignment: cb * rlen / 8): the unaligned head and tail byte by byte (the
+    // neighbouring code blocks' bytes share those words), the rest as dwords cut from two LDS words by alignbyte
+    uint8_t*       dst  = c.data + d.data_off + (size_t)d.cb * d.rlen / 8;
+    const uint32_t nb   = (d.cb + 1 == d.C) ? nbytes : d.rlen / 8;
+    const uint32_t head = min(nb, (4u - (uint32_t)((uintptr_t)dst & 3u)) & 3u);
+    const uint32_t nw   = (nb - head) / 4, tail0 = head + 4 * nw;
+    for (uint32_t i = l; i < head; i += NL) dst[i] = bytes[i];
+    for (uint32_t i = tail0 + l; i < nb; i += NL) dst[i] = bytes[i];
+    uint32_t* dw = (uint32_t*)(dst + head); // 4-byte aligned
+    const uint32_t sh = head;               // word w takes bytes head + 4w .. head + 4w + 3
+    for (uint32_t w = l; w < nw; w += NL) {
+      const uint32_t lo = bm[w + sh / 4], hi = bm[w + sh / 4 + 1]; // bytes 4(w + sh/4) .. +7 (sh < 4: sh/4 = 0)
+      dw[w]             = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+    }
     if (l == 0) {
       c.its[cb] = c.h + 1;
       if (ok) {
