@@ -75,6 +75,23 @@ __device__ __forceinline__ uint32_t crc24_words(const uint8_t* p, uint32_t n, co
   return crc;
 }
 
+// crc24_words for any alignment of p: the bytes up to the first 4-byte boundary, then words
+__device__ __forceinline__ uint32_t crc24_words_any(const uint8_t* p, uint32_t n, const uint32_t (*t4)[256])
+{
+  const uint32_t head = min(n, (4u - (uint32_t)((uintptr_t)p & 3u)) & 3u);
+  uint32_t       crc  = 0;
+  for (uint32_t i = 0; i < head; i++) crc = ((crc << 8) ^ t4[0][((crc >> 16) & 0xff) ^ p[i]]) & 0xffffffu;
+  const uint8_t* q  = p + head;
+  const uint32_t m  = n - head, nw = m / 4;
+  for (uint32_t i = 0; i < nw; i++) {
+    const uint32_t v = ((const uint32_t*)q)[i];
+    crc = t4[3][((crc >> 16) ^ v) & 0xff] ^ t4[2][((crc >> 8) ^ (v >> 8)) & 0xff] ^ t4[1][(crc ^ (v >> 16)) & 0xff] ^
+          t4[0][v >> 24];
+  }
+  for (uint32_t i = 4 * nw; i < m; i++) crc = ((crc << 8) ^ t4[0][((crc >> 16) & 0xff) ^ q[i]]) & 0xffffffu;
+  return crc;
+}
+
 // wave CRC as wave_crc24_scaled, with slice-by-4 tables
 __device__ __forceinline__ uint32_t wave_crc24_scaled4(const uint8_t* bytes, uint32_t nbytes, const uint32_t (*t4)[256],
                                                        uint32_t poly, const uint32_t* scale)
@@ -101,6 +118,23 @@ __device__ __forceinline__ uint32_t wave_crc24_scaled(const uint8_t* bytes, uint
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
   return crc;
+}
+
+// a 256-thread workgroup's CRC (TB CRC over up to 49 KB) with slice-by-4 tables and the precomputed per-thread
+// scale factors of this byte count (chunk = ceil(nbytes / 256) rounded up to a word)
+__device__ inline uint32_t block_crc24_scaled4(const uint8_t* bytes, uint32_t nbytes, const uint32_t (*t4)[256],
+                                               uint32_t poly, const uint32_t* scale)
+{
+  __shared__ uint32_t part4[4];
+  const uint32_t tid   = threadIdx.x;
+  const uint32_t chunk = ((nbytes + 255) / 256 + 3) / 4 * 4;
+  const uint32_t b0 = min(nbytes, tid * chunk), b1 = min(nbytes, b0 + chunk);
+  uint32_t       crc = gf2_mulmod24(crc24_words_any(bytes + b0, b1 - b0, t4), scale[tid], poly);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) crc ^= __shfl_xor(crc, o, 64);
+  if ((tid & 63) == 0) part4[tid >> 6] = crc;
+  __syncthreads();
+  return part4[0] ^ part4[1] ^ part4[2] ^ part4[3];
 }
 
 // the same with a whole 256-thread workgroup (TB CRC over up to 49 KB), scale factors by square-and-multiply

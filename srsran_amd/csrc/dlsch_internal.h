@@ -25,6 +25,7 @@ struct TbDesc {
   uint32_t cb_base[2]; // index of the TB's first K1 / K2 code block in the call's (K-grouped) CB arrays
   uint64_t e_off;      // element offset of the TB's LLRs in the e_bits buffer
   uint64_t data_off;
+  const uint32_t* crc_scale; // TB CRC24A over tbs/8 bytes by 256 threads: x^(8 * bytes after thread t's chunk) mod P
 };
 
 struct CrcTable {

@@ -259,10 +259,17 @@ __global__ __launch_bounds__(256) void dlsch_tb_epilogue(DlschTbArgs a)
   const int t   = blockIdx.x;
   const int tid = threadIdx.x;
   if (t >= a.ntb) return;
-  __shared__ uint32_t tl[256];
-  tl[tid] = a.crc24a->t[tid]; // blockDim == 256
+  __shared__ uint32_t t4[4][256]; // CRC24A slice-by-4 tables
+  t4[0][tid] = a.crc24a->t[tid];  // blockDim == 256
   __syncthreads();
   const TbDesc& tb = a.tb[t];
+  if (tb.crc_scale) {
+#pragma unroll
+    for (int k = 1; k < 4; k++) { // one more zero byte per table
+      t4[k][tid] = crc24_step_table(t4[k - 1][tid], t4[0]);
+      __syncthreads();
+    }
+  }
   if (tid == 0) { // srslte_pdsch_res_t.avg_iterations_block (sch.c:451-453): mean over the TB's code blocks
     double sum = 0.0;
     for (uint32_t c = 0; c < tb.C; c++) sum += a.its[c < tb.C1 ? tb.cb_base[0] + c : tb.cb_base[1] + (c - tb.C1)];
@@ -286,7 +293,8 @@ __global__ __launch_bounds__(256) void dlsch_tb_epilogue(DlschTbArgs a)
     if (tid == 0) a.ret[t] = -1;
     return;
   }
-  const uint32_t par_rx = block_crc24(data, tb.tbs / 8, tl, *a.crc24a);
+  const uint32_t par_rx = tb.crc_scale ? block_crc24_scaled4(data, tb.tbs / 8, t4, a.crc24a->poly, tb.crc_scale)
+                                        : block_crc24(data, tb.tbs / 8, t4[0], *a.crc24a);
   if (tid == 0) {
     const uint32_t par_tx = ((uint32_t)data[tb.tbs / 8] << 16) | ((uint32_t)data[tb.tbs / 8 + 1] << 8) |
                             (uint32_t)data[tb.tbs / 8 + 2];

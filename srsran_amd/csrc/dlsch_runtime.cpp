@@ -86,6 +86,7 @@ struct mi355_dlsch {
   std::map<uint64_t, uint16_t*>          rm8;          // the same for the 8-bit decoder layout
   std::map<uint32_t, mi355_tdec8_t*>     dec8;         // 8-bit decoder workspace per K
   std::map<uint32_t, uint32_t*>          scales;       // K -> per-lane CRC scale factors
+  std::map<uint32_t, uint32_t*>          tb_scales;    // TB bytes -> per-thread CRC24A scale factors (epilogue)
   CrcTable*                              crc = nullptr; // [0] CRC24A, [1] CRC24B
   // per-call scratch
   char*  scratch     = nullptr;
@@ -178,6 +179,37 @@ static int crc_scales(mi355_dlsch_t* q, uint32_t K, const uint32_t** out)
     CHECK_HIP(hipMalloc(&d, t.size() * 4));
     CHECK_HIP(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
     it = q->scales.emplace(K, d).first;
+  }
+  *out = it->second;
+  return MI355_SUCCESS;
+}
+
+// the TB epilogue's CRC24A of nbytes bytes by 256 threads (block_crc24_scaled4): thread t's factor
+// x^(8 * bytes after its chunk) mod P, chunk = ceil(nbytes / 256) rounded up to a word
+static int tb_crc_scales(mi355_dlsch_t* q, uint32_t nbytes, const uint32_t** out)
+{
+  auto it = q->tb_scales.find(nbytes);
+  if (it == q->tb_scales.end()) {
+    if (q->tb_scales.size() >= 512) { // bounded: distinct TB sizes
+      CHECK_HIP(hipDeviceSynchronize());
+      for (auto& kv : q->tb_scales) (void)hipFree(kv.second);
+      q->tb_scales.clear();
+    }
+    std::vector<uint32_t> t(256);
+    const uint32_t        chunk = ((nbytes + 255) / 256 + 3) / 4 * 4, poly = 0x1864CFB;
+    for (uint32_t tid = 0; tid < 256; tid++) {
+      const uint32_t b0 = std::min(nbytes, tid * chunk), b1 = std::min(nbytes, b0 + chunk);
+      uint32_t       sc = 1, x8 = 1u << 8; // x^(8 * 2^i)
+      for (uint32_t after = nbytes - b1; after; after >>= 1) {
+        if (after & 1) sc = gf2_mulmod24_host(sc, x8, poly);
+        x8 = gf2_mulmod24_host(x8, x8, poly);
+      }
+      t[tid] = sc;
+    }
+    uint32_t* d = nullptr;
+    CHECK_HIP(hipMalloc(&d, t.size() * 4));
+    CHECK_HIP(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    it = q->tb_scales.emplace(nbytes, d).first;
   }
   *out = it->second;
   return MI355_SUCCESS;
@@ -364,6 +396,7 @@ void mi355_dlsch_destroy(mi355_dlsch_t* q)
   for (auto& kv : q->rm8) (void)hipFree(kv.second);
   for (auto& kv : q->dec8) mi355_tdec8_destroy(kv.second);
   for (auto& kv : q->scales) (void)hipFree(kv.second);
+  for (auto& kv : q->tb_scales) (void)hipFree(kv.second);
   (void)hipFree(q->crc);
   (void)hipFree(q->scratch);
   if (q->done_ev) (void)hipEventDestroy(q->done_ev);
@@ -504,6 +537,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
       d.invalid = 1;
       continue;
     }
+    if (int e = tb_crc_scales(q, in.tbs / 8, &d.crc_scale)) return e;
     d.C          = seg.C;
     d.C1         = seg.C1;
     d.K1         = seg.K1;
