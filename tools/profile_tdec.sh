@@ -8,7 +8,7 @@ TAG=${1:-r02}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-E="python3 bench.py --steps 3 --warmup 1 --no-cpu --no-waterfall"
+E="python3 bench.py --steps 3 --warmup 1 --no-cpu --no-waterfall --no-roofline"
 B="python3 bench.py --workload tdec --steps 3 --warmup 1 --no-cpu"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/e2e -o e2e -- $E > $OUT/e2e.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- $B > $OUT/trace.log 2>&1
