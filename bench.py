@@ -439,8 +439,9 @@ def cpu_baseline_pdsch(src, gpu_bufs, avg_its, budget_s, ocfg_of=None, K=6144, C
                        S_max=16, label="TM4"):
     """CPU reference-path timing on the host cores (rank 0, N = 1), bounded sample of the same workload:
     S subframes' I/Q (downloaded from HBM) through oracle/orc_front.c's C chain (OFDM by a float Stockham FFT,
-    estimation, RE extraction, MMSE + CSI, demapping, descrambling, rate dematching -- the oracle's scalar C
-    restatement, one subframe per thread task) and their ntb C S code blocks through the reference's own AVX2 turbo
+    estimation, RE extraction and CSI weighting restated in C; MMSE equalisation, demapping, descrambling and rate
+    dematching through the reference's own AVX2 code when oracle/_ref is built, else the scalar restatement; one
+    subframe per thread task) and their ntb C S code blocks through the reference's own AVX2 turbo
     decoder (oracle/_ref, compiled from the srsLTE sources) for ceil(avg half-iterations) half-iterations;
     1 thread and every usable core.  gpu_bufs: (ncb, stride) softbuffer contents the GPU produced for the same S
     subframes -- the CPU front end must reproduce them (parity_vs_gpu).  ocfg_of(d): the oracle Cfg of resident
@@ -485,8 +486,19 @@ def cpu_baseline_pdsch(src, gpu_bufs, avg_its, budget_s, ocfg_of=None, K=6144, C
             if time.perf_counter() - t0 >= budget_s / 4:
                 return (time.perf_counter() - t0) / reps / n_cb, reps
 
-    f1, r_f1 = front(1)
-    fN, r_fN = front(nthreads)
+    # the equaliser, demapper, descrambler and rate dematcher run as the reference's own AVX2 code when oracle/_ref
+    # is built (oracle/ref/ref_front.c); OFDM, estimation, RE extraction and CSI weighting stay the C restatement's
+    front_ref = oracle.front_use_reference(True)
+    try:
+        if front_ref:  # the rate-matching tables once, single-threaded (srslte_rm_turbo_gentables is not thread-safe)
+            oracle.ref().ref_rm_turbo_rx(np.zeros(64, np.int16), 64, np.zeros(stride, np.int16), 40, 0)
+        f1, r_f1 = front(1)
+        fN, r_fN = front(nthreads)
+    finally:
+        oracle.front_use_reference(False)
+    front_desc = ("float Stockham FFT, oracle chest / RE extraction / CSI weighting; the reference's AVX2 MMSE "
+                  "equaliser, demapper, descrambler and rate dematcher (oracle/_ref)" if front_ref else
+                  "float Stockham FFT, oracle chest / MMSE+CSI / demap / descramble / rate dematching")
     bufs = np.ascontiguousarray(sb.reshape(S, 2, max_cb, stride)[:, :ntb, :C].reshape(ncb, stride))
     # the CPU chain's decoder buffers vs the GPU's for the same subframes (systematic, parity 1, parity 2, tails):
     # equal up to the LSB-level LLR differences of the float32 FFT / estimator (tests: within +-2)
@@ -512,8 +524,9 @@ def cpu_baseline_pdsch(src, gpu_bufs, avg_its, budget_s, ocfg_of=None, K=6144, C
         "all_cores": {"front_ms_per_subframe": round(fN * 1e3, 3),
                       "turbo_us_per_cb_halfit_per_thread": round(tN / nh * nthreads * 1e6, 2)},
         "parity_front_vs_gpu_softbuffers": parity,
-        "sample": (f"{S} distinct {label} subframes of this batch: C front end (oracle/orc_front.c: float Stockham "
-                   f"FFT, oracle chest / MMSE+CSI / demap / descramble / rate dematching) {r_f1}+{r_fN} passes at 1 "
+        "front_kind": "reference stages" if front_ref else "port",
+        "sample": (f"{S} distinct {label} subframes of this batch: C front end (oracle/orc_front.c: {front_desc}) "
+                   f"{r_f1}+{r_fN} passes at 1 "
                    f"and {nthreads} threads; their {ncb} CBs (K={K}) through the reference AVX2 turbo decoder "
                    f"({kind_t}, oracle/_ref) x {nh} half-iterations (= ceil of the GPU run's mean), "
                    f"{r_t1}+{r_tN} passes"),

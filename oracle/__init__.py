@@ -94,6 +94,7 @@ def lib() -> C.CDLL:
         L.orc_dlsch_rm_tb.argtypes = [i16p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, i16p, C.c_uint32]
         L.orc_ue_dl_rx_batch.argtypes = [C.POINTER(FrontCfg), C.c_uint32, f32p, C.c_size_t, i16p, C.c_uint32,
                                          C.c_uint32, C.c_int]
+        L.orc_front_set_stages.argtypes = [C.c_void_p]
         _LIB = L
     return _LIB
 
@@ -119,10 +120,37 @@ def front_cfg(cfg) -> FrontCfg:
     return f
 
 
+class FrontStages(C.Structure):
+    """orc_front_stages_t (oracle.h): the front end's replaceable stage functions, as raw addresses."""
+    _fields_ = [(n, C.c_void_p) for n in ("predecode", "demod_soft_s", "scramble_s", "rm_turbo_rx")]
+
+
+def front_use_reference(on: bool = True) -> bool:
+    """Run orc_ue_dl_front's equaliser, demapper, descrambler and rate dematcher through the reference's own AVX2
+    code (oracle/ref/ref_front.c, ref_pdsch.c, ref_harness.c in oracle/_ref) instead of the restatement's (on=False:
+    back to the restatement).  Returns whether the reference stages are installed."""
+    L = lib()
+    if not on or not ref_available():
+        L.orc_front_set_stages(None)
+        return False
+    R = ref()
+    addr = lambda f: C.cast(f, C.c_void_p).value  # noqa: E731
+    st = FrontStages(addr(R.ref_front_predecode), addr(R.ref_demod_soft_s), addr(R.ref_front_scramble_s),
+                     addr(R.ref_rm_turbo_rx))
+    L.orc_front_set_stages(C.byref(st))
+    return True
+
+
+def _aligned_i16(n: int, align: int = 64) -> np.ndarray:
+    buf = np.zeros(n + align, np.int16)
+    off = (-buf.ctypes.data % align) // 2
+    return buf[off: off + n]
+
+
 def ue_dl_front(cfg, iq: np.ndarray):
     """orc_ue_dl_front: iq (nof_rx, 15 N) complex64 -> (e per TB int16, noise)."""
     iq = np.ascontiguousarray(iq, np.complex64)
-    e = [np.zeros(8 * 14 * 1200, np.int16) for _ in range(2)]
+    e = [_aligned_i16(8 * 14 * 1200) for _ in range(2)]  # 64-byte aligned: the reference stages' SIMD stores
     ip = (C.c_void_p * 2)(iq[0].ctypes.data, iq[min(1, iq.shape[0] - 1)].ctypes.data)
     ep = (C.c_void_p * 2)(e[0].ctypes.data, e[1].ctypes.data)
     noise = C.c_float()
@@ -162,6 +190,8 @@ def ref() -> C.CDLL:
         L.ref_demod_soft_b.argtypes = [C.c_int, f32p, i8p, C.c_int]
         L.ref_scramble_sb.argtypes = [C.c_uint32, i8p, C.c_int, C.c_int]
         L.ref_predecoding.argtypes = [C.c_void_p] * 10 + [C.c_int] * 6 + [C.c_float, C.c_float, C.c_int]
+        L.ref_front_predecode.argtypes = [f32p, f32p] + [C.c_int] * 6 + [C.c_float, C.c_float, f32p, f32p, f32p]
+        L.ref_front_scramble_s.argtypes = [C.c_uint32, i16p, C.c_int]
         _REF = L
     return _REF
 

@@ -69,6 +69,18 @@ typedef struct {
   uint32_t p_b;
 } orc_front_cfg_t;
 int orc_ofdm_rx_sf(const float* iq, uint32_t nof_prb, float* grid);
+/* the front end's replaceable stages (default: this restatement's).  The CPU baseline installs the reference's own
+ * AVX2 equaliser, demapper, descrambler and rate dematcher (oracle/ref/ref_front.c, compiled from the reference
+ * sources); OFDM (FFTW), estimation (chest_dl.c needs the generated version.h), RE extraction and the CSI weighting
+ * (pdsch.c, same) stay restated. */
+typedef struct {
+  int (*predecode)(const float* y, const float* h, int nof_rx, int nof_ports, int nof_layers, int cb, int n, int type,
+                   float scaling, float noise, float* x, float* csi0, float* csi1);
+  int (*demod_soft_s)(int qm, const float* iq, int16_t* llr, int nsym);
+  int (*scramble_s)(uint32_t c_init, int16_t* llr, int len);
+  int (*rm_turbo_rx)(const int16_t* in, uint32_t in_len, int16_t* out, uint32_t K, uint32_t rv);
+} orc_front_stages_t;
+void orc_front_set_stages(const orc_front_stages_t* st); /* NULL: the restatement's */
 int orc_ue_dl_front(const orc_front_cfg_t* cfg, const float* const* iq, int16_t* const* e, float* noise_out);
 int orc_dlsch_rm_tb(const int16_t* e_bits, uint32_t nof_e_bits, uint32_t tbs, uint32_t Qm, uint32_t rv,
                     int16_t* softbuf, uint32_t sb_stride);

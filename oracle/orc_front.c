@@ -196,6 +196,29 @@ static const uint8_t* pdsch_sequence(uint32_t c_init)
   return r;
 }
 
+/* the replaceable stages (oracle.h orc_front_stages_t) */
+static int orc_scramble_cached(uint32_t c_init, int16_t* llr, int len)
+{
+  const uint8_t* seq = pdsch_sequence(c_init); /* e = c ? -e : e (wrapping, as _mm256_sign_epi16) */
+  for (int i = 0; i < len; i++)
+    if (seq[i]) llr[i] = (int16_t)(uint16_t)(-(int)llr[i]);
+  return 0;
+}
+static int orc_rm_turbo_rx_c(const int16_t* in, uint32_t in_len, int16_t* out, uint32_t K, uint32_t rv)
+{
+  return orc_rm_turbo_rx(in, in_len, out, K, rv);
+}
+static orc_front_stages_t stages = {orc_predecode, orc_demod_soft_s, orc_scramble_cached, orc_rm_turbo_rx_c};
+
+void orc_front_set_stages(const orc_front_stages_t* st)
+{
+  const orc_front_stages_t dflt = {orc_predecode, orc_demod_soft_s, orc_scramble_cached, orc_rm_turbo_rx_c};
+  stages                        = st ? *st : dflt;
+}
+
+/* 64-byte aligned buffers: the reference's SIMD stages (oracle/ref/ref_front.c) use aligned loads and stores */
+static void* amalloc(size_t n) { return aligned_alloc(64, (n + 63) & ~(size_t)63); }
+
 static const float cell_specific_ratio[2][4] = {{1.0f, 4.0f / 5, 3.0f / 5, 2.0f / 5}, {5.0f / 4, 1.0f, 3.0f / 4, 1.0f / 2}};
 
 /* OFDM -> estimation -> PDSCH symbol processing: e[t] receives nre * qm[t] LLRs.  Returns nre or < 0. */
@@ -237,8 +260,8 @@ int orc_ue_dl_front(const orc_front_cfg_t* c, const float* const* iq, int16_t* c
       for (int s = 0; s < 2; s++) sc[s * 7 + 0] = sc[s * 7 + 4] = 1.0f / rho_b;
     scaling = (rho_a != 0.0f && isfinite(rho_a)) ? rho_a : 1.0f;
   }
-  cfl* ys = malloc(sizeof(cfl) * nre * R);
-  cfl* hs = malloc(sizeof(cfl) * nre * 2 * 2);
+  cfl* ys = amalloc(sizeof(cfl) * nre * R);
+  cfl* hs = amalloc(sizeof(cfl) * nre * 2 * 2);
   const cfl* gr = (const cfl*)grids;
   const cfl* cc = (const cfl*)ce;
   for (uint32_t r = 0; r < R; r++)
@@ -247,19 +270,17 @@ int orc_ue_dl_front(const orc_front_cfg_t* c, const float* const* iq, int16_t* c
     for (uint32_t r = 0; r < 2; r++)
       for (uint32_t i = 0; i < nre; i++)
         hs[((size_t)p * 2 + r) * nre + i] = r < R ? cc[((size_t)p * 2 + r) * G + idx[i]] : 0;
-  cfl*   x   = malloc(sizeof(cfl) * nre * 2);
-  float* csi = malloc(sizeof(float) * nre * 2);
-  if (orc_predecode((const float*)ys, (const float*)hs, R, P, c->nof_layers, c->cb, nre, c->scheme, scaling,
-                    c->mmse ? noise : 0.0f, (float*)x, csi, csi + nre) < 0)
+  cfl*   x   = amalloc(sizeof(cfl) * nre * 2);
+  const uint32_t cst = (nre + 15) & ~15u; /* each codeword's CSI row 64-byte aligned, as the reference's own buffers */
+  float*         csi = amalloc(sizeof(float) * cst * 2);
+  if (stages.predecode((const float*)ys, (const float*)hs, R, P, c->nof_layers, c->cb, nre, c->scheme, scaling,
+                       c->mmse ? noise : 0.0f, (float*)x, csi, csi + cst) < 0)
     return -1;
   for (uint32_t t = 0; t < c->nof_tb; t++) {
     const uint32_t qm = c->qm[t];
-    orc_demod_soft_s(qm, (const float*)&x[(size_t)t * nre], e[t], nre);
-    /* orc_scramble_s with the cached sequence: e = c ? -e : e (wrapping, as _mm256_sign_epi16) */
-    const uint8_t* seq = pdsch_sequence((c->rnti << 14) + (t << 13) + (c->sf_idx << 9) + c->cell_id);
-    for (uint32_t i = 0; i < nre * qm; i++)
-      if (seq[i]) e[t][i] = (int16_t)(uint16_t)(-(int)e[t][i]);
-    if (c->csi_enable) orc_csi_correction_s(qm, e[t], &csi[(size_t)t * nre], nre * qm);
+    stages.demod_soft_s(qm, (const float*)&x[(size_t)t * nre], e[t], nre);
+    stages.scramble_s((c->rnti << 14) + (t << 13) + (c->sf_idx << 9) + c->cell_id, e[t], (int)(nre * qm));
+    if (c->csi_enable) orc_csi_correction_s(qm, e[t], &csi[(size_t)t * cst], nre * qm);
   }
   free(grids);
   free(ce);
@@ -289,7 +310,7 @@ int orc_dlsch_rm_tb(const int16_t* e_bits, uint32_t nof_e_bits, uint32_t tbs, ui
     }
     int16_t* buf = &softbuf[(size_t)cb * sb_stride];
     memset(buf, 0, sizeof(int16_t) * sb_stride);
-    orc_rm_turbo_rx(&e_bits[rp], n_e2, buf, K, rv);
+    stages.rm_turbo_rx(&e_bits[rp], n_e2, buf, K, rv);
   }
   return (int)C;
 }
@@ -310,7 +331,7 @@ struct front_task {
 static void* front_worker(void* arg)
 {
   struct front_task* T   = arg;
-  int16_t*           e[2] = {malloc(sizeof(int16_t) * 8 * 14 * 1200), malloc(sizeof(int16_t) * 8 * 14 * 1200)};
+  int16_t*           e[2] = {amalloc(sizeof(int16_t) * 8 * 14 * 1200), amalloc(sizeof(int16_t) * 8 * 14 * 1200)};
   for (;;) {
     pthread_mutex_lock(&T->mu);
     const uint32_t i = T->next++;
