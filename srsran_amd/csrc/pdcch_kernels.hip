@@ -199,7 +199,21 @@ constexpr float    RX_NULL = 10000.0f;
 // trellis, and a workgroup's LDS is released only when all its waves are done -- with 4 waves per workgroup a CU held
 // 5 workgroups (LDS-bound) whatever few of their waves were decoding
 constexpr uint32_t WAVES   = 1;
+#ifndef BLIND_DIAG
+#define BLIND_DIAG 0 // (timing diagnostics: 1 stop after the gate, 2 after the branch-metric table, 3 after the Viterbi)
+#endif
 constexpr uint32_t MAXSYM  = 3 * PDCCH_MAX_F; // 432
+// 30-step decision blocks the traceback reads: steps F + 6 .. 3F + 5
+constexpr uint32_t tb_blocks()
+{
+  uint32_t m = 0;
+  for (uint32_t F = 17; F <= PDCCH_MAX_F; F++) m = (3 * F + 5) / 30 - (F + 6) / 30 + 1 > m ? (3 * F + 5) / 30 - (F + 6) / 30 + 1 : m;
+  return m;
+}
+constexpr uint32_t TB_BLOCKS = tb_blocks(); // 11
+#ifndef VIT_ROTATE
+#define VIT_ROTATE 1 // 1: rotating state layout with DPP / permlane partner exchange; 0: ds_bpermute gathers
+#endif
 static_assert((PDCCH_SLOTS * PDCCH_FMTS) % WAVES == 0, "a workgroup never straddles two subframes' tail");
 
 // x^(d + 16) mod (x^16 + x^12 + x^5 + 1) for d < 128: the CRC16 contribution of a payload bit d places from the end
@@ -223,10 +237,10 @@ __constant__ uint8_t c_perm[32]     = {1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 2
 __constant__ uint8_t c_perm_inv[32] = {16, 0, 24, 8, 20, 4, 28, 12, 18, 2, 26, 10, 22, 6, 30, 14,
                                        17, 1, 25, 9, 21, 5, 29, 13, 19, 3, 27, 11, 23, 7, 31, 15};
 
-// 5,152 B per wave (31 waves per CU by LDS): every array shares storage with one that is dead by the time it is
-// written -- bm and the decoded bits with the rate-dematching buffers, the decision words with the quantised symbols
-// (the Viterbi reads the branch-metric table only) -- and only the decisions the traceback reads (steps F .. 3F-1)
-// are kept
+// 5,600 B per wave (29 waves per CU by LDS): every array shares storage with one that is dead by the time it is
+// written -- bm and the decoded bits with the rate-dematching buffers, the decision strings with the quantised
+// symbols (the Viterbi reads the branch-metric table only) -- and only the decision blocks the traceback reads are
+// kept
 struct WaveLds {
   union {
     struct {
@@ -239,9 +253,8 @@ struct WaveLds {
     };
   };
   union {
-    uint16_t q[MAXSYM];                // quantised soft symbols, dead once bm is built
-    uint64_t dec[2 * PDCCH_MAX_F + 8]; // decision word of step F + i (bit s: survivor choice of state s); the
-                                       // traceback reads 6 steps ahead, past 3F - 1: zero words
+    uint16_t q[MAXSYM];          // quantised soft symbols, dead once bm is built
+    uint32_t tdec[TB_BLOCKS][64]; // Viterbi decisions, lane-major bit strings of 30 steps (blocks tb0 .. tb1)
   };
 };
 
@@ -280,6 +293,46 @@ __device__ __forceinline__ void writelane1(uint32_t& v, uint32_t x, uint32_t k)
 #pragma clang diagnostic pop
 
 __device__ __forceinline__ uint32_t par(uint32_t x) { return __builtin_popcount(x) & 1u; }
+__device__ __forceinline__ uint32_t rotl6(uint32_t x, uint32_t r) { return ((x << r) | (x >> (6 - r))) & 63u; }
+__device__ __forceinline__ uint32_t rotr6(uint32_t x, uint32_t r) { return ((x >> r) | (x << (6 - r))) & 63u; }
+
+// One trellis step of the 64-state Viterbi in the rotating layout.  At phase K lane l holds state rotl6(l, K), so the
+// predecessors j and j + 32 of a successor pair (2j, 2j + 1) sit in the lanes l and l ^ (32 >> K), and the pair's
+// successors land in the same two lanes at phase K + 1 (rotr6(2j, K + 1) = rotr6(j, K)): every step exchanges with
+// one fixed partner -- a permlane32 / permlane16 swap, DPP row shifts under a bank mask, DPP quad permutes -- in place
+// of two ds_bpermute gathers through LDS.  X / Y: the metric of the pair's low / high predecessor, in both lanes.
+// Returns the decision (survivor from j + 32); xa: this lane's branch metric, complemented for the odd successor.
+template <int K> __device__ __forceinline__ bool vit_step(uint32_t& met, uint32_t xa)
+{
+  uint32_t X, Y;
+  if constexpr (!VIT_ROTATE) { // identity layout: state s takes predecessors s >> 1 and (s >> 1) + 32
+    const int j = (int)(__lane_id() >> 1);
+    X           = (uint32_t)__shfl((int)met, j, 64);
+    Y           = (uint32_t)__shfl((int)met, j + 32, 64);
+  } else if constexpr (K == 0) {
+    const auto r = __builtin_amdgcn_permlane32_swap(met, met, false, false);
+    X = r[0], Y = r[1];
+  } else if constexpr (K == 1) {
+    const auto r = __builtin_amdgcn_permlane16_swap(met, met, false, false);
+    X = r[0], Y = r[1];
+  } else if constexpr (K == 2) { // partner 8 apart: row_shr:8 into banks 2-3, row_shl:8 into banks 0-1
+    X = (uint32_t)__builtin_amdgcn_update_dpp((int)met, (int)met, 0x118, 0xF, 0xC, false);
+    Y = (uint32_t)__builtin_amdgcn_update_dpp((int)met, (int)met, 0x108, 0xF, 0x3, false);
+  } else if constexpr (K == 3) { // 4 apart: row_shr:4 into banks 1 and 3, row_shl:4 into banks 0 and 2
+    X = (uint32_t)__builtin_amdgcn_update_dpp((int)met, (int)met, 0x114, 0xF, 0xA, false);
+    Y = (uint32_t)__builtin_amdgcn_update_dpp((int)met, (int)met, 0x104, 0xF, 0x5, false);
+  } else if constexpr (K == 4) { // 2 apart: quad_perm [0,1,0,1] / [2,3,2,3]
+    X = (uint32_t)__builtin_amdgcn_mov_dpp((int)met, 0x44, 0xF, 0xF, true);
+    Y = (uint32_t)__builtin_amdgcn_mov_dpp((int)met, 0xEE, 0xF, 0xF, true);
+  } else { // 1 apart: quad_perm [0,0,2,2] / [1,1,3,3]
+    X = (uint32_t)__builtin_amdgcn_mov_dpp((int)met, 0xA0, 0xF, 0xF, true);
+    Y = (uint32_t)__builtin_amdgcn_mov_dpp((int)met, 0xF5, 0xF, 0xF, true);
+  }
+  const uint32_t x = X + xa, y = (xa ^ 8191u) + Y; // only the low 16 bits matter (wrapping u16 metrics)
+  const bool     d = (int16_t)(uint16_t)(x - y) > 0;
+  met              = d ? y : x;
+  return d;
+}
 
 __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
 {
@@ -336,6 +389,7 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
     if (lane == 0) out->status = 1, out->L = L, out->ncce = ncce;
     return;
   }
+  if (BLIND_DIAG == 1) return;
   // rate dematching (rm_conv.c:98-148)
   const uint32_t F = nbits + 16, N = 3 * F;
   const uint32_t nrows = (F - 1) / 32 + 1, Kp = 32 * nrows, ndummy = Kp - F;
@@ -395,56 +449,124 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
     S.bm[e]           = (uint16_t)((((c2 ^ S.q[o + 2]) + av + 1) >> 1) >> 3);
   }
   __builtin_amdgcn_wave_barrier();
-  for (uint32_t i = lane; i < 8; i += 64) S.dec[2 * F + i] = 0; // (q is dead now: dec shares its storage)
-  // 64-state Viterbi, lane = state; state s takes predecessors j = s >> 1 and j + 32
-  const uint32_t j   = lane >> 1;
-  const uint32_t pat = par((2 * j) & 0x6Du) | par((2 * j) & 0x4Fu) << 1 | par((2 * j) & 0x57u) << 2;
-  // branch metrics are 13-bit (a 16-bit sum >> 3), so 8191 - m = m ^ 8191: the odd states' complement is one xor
-  const uint32_t flip = (lane & 1u) ? 8191u : 0u;
-  const uint16_t* bml = S.bm + pat;
-  const uint32_t Fs  = __builtin_amdgcn_readfirstlane(F); // uniform: the step counters live in scalar registers
-  uint32_t       met = 0;
-  // decision words: step tb + k's ballot goes to lane k of (dlo, dhi), one 64-lane store per 64 steps
-  for (uint32_t tb = 0, o = 0; tb < 3 * Fs; tb += 64) {
-    const uint32_t te  = __builtin_amdgcn_readfirstlane(min(3 * Fs - tb, 64u));
-    uint32_t       dlo = 0, dhi = 0;
-    for (uint32_t k = 0; k < te; k++, o = (o + 1 == Fs) ? 0 : o + 1) {
-      const uint32_t xa = (uint32_t)bml[8 * o] ^ flip; // ya = 8191 - xa = xa ^ 8191
-      const uint32_t oj = (uint32_t)__shfl((int)met, (int)j, 64), oj32 = (uint32_t)__shfl((int)met, (int)(j + 32), 64);
-      const uint32_t x = oj + xa, y = (xa ^ 8191u) + oj32; // only the low 16 bits matter (wrapping u16 metrics)
-      const bool     d = (int16_t)(uint16_t)(x - y) > 0;
-      met              = d ? y : x;
-      const uint64_t w = __ballot(d);
-      writelane2(dlo, dhi, w, k);
+  if (BLIND_DIAG == 2) return;
+  // 64-state Viterbi over 3F steps, one lane per state (vit_step), decisions kept as per-lane bit strings: step
+  // 30 b + r's decision of lane l is bit 29 - r of tdec[b - tb0][l] (one v_addc per step, one 64-lane store per 30
+  // steps; 30 is a multiple of the state layout's period).  Only the blocks the traceback reads are kept: steps
+  // F + 6 .. 3F + 5 (decision of step n read at n + 6, as the AVX2 traceback), the ones past 3F - 1 zero
+  const uint32_t Fs = __builtin_amdgcn_readfirstlane(F); // uniform: the step counters live in scalar registers
+  const uint32_t tb0 = (Fs + 6) / 30, tb1 = (3 * Fs + 5) / 30;
+  // per phase k: the branch-metric pattern of the lane's pair (encoder output of its low predecessor j doubled) and
+  // whether the lane takes the odd successor (the complemented metric; 13-bit metrics: 8191 - m = m ^ 8191)
+  uint32_t boff[6], flip[6];
+#pragma unroll
+  for (uint32_t k = 0; k < 6; k++) {
+    const uint32_t j = (VIT_ROTATE ? rotl6(lane, k) : lane >> 1) & 31u;
+    boff[k]          = par((2 * j) & 0x6Du) | par((2 * j) & 0x4Fu) << 1 | par((2 * j) & 0x57u) << 2;
+    flip[k]          = (VIT_ROTATE ? (lane >> (5 - k)) & 1u : lane & 1u) ? 8191u : 0u;
+  }
+  uint32_t met = 0, o = 0;
+  // branch metrics of the next six steps, read one group ahead so that no LDS latency sits on the metric chain
+  uint32_t cur[6], nxt[6];
+  const auto load6 = [&](uint32_t* xa) {
+#pragma unroll
+    for (int K = 0; K < 6; K++) {
+      xa[K] = (uint32_t)S.bm[8 * o + boff[K]] ^ flip[K];
+      o     = (o + 1 == Fs) ? 0 : o + 1;
     }
-    if (lane < te && tb + lane >= Fs) S.dec[tb + lane - Fs] = (uint64_t)dhi << 32 | dlo;
+  };
+  load6(cur);
+  for (uint32_t tb = 0, b = 0; tb < 3 * Fs; tb += 30, b++) {
+    const uint32_t te   = __builtin_amdgcn_readfirstlane(min(3 * Fs - tb, 30u));
+    uint32_t       dreg = 0, k = 0;
+#define VIT_STEP(K)                                                                                                   \
+  do {                                                                                                               \
+    const bool d = vit_step<K>(met, cur[K]);                                                                         \
+    dreg         = dreg + dreg + (uint32_t)d;                                                                        \
+    k++;                                                                                                             \
+  } while (0)
+    while (k + 6 <= te) {
+      load6(nxt); // (past the last step these read valid, unused entries)
+      VIT_STEP(0);
+      VIT_STEP(1);
+      VIT_STEP(2);
+      VIT_STEP(3);
+      VIT_STEP(4);
+      VIT_STEP(5);
+#pragma unroll
+      for (int K = 0; K < 6; K++) cur[K] = nxt[K];
+    }
+    if (k < te) { // (the last block only: 3F need not be a multiple of 6)
+      VIT_STEP(0);
+      if (k < te) {
+        VIT_STEP(1);
+        if (k < te) {
+          VIT_STEP(2);
+          if (k < te) {
+            VIT_STEP(3);
+            if (k < te) VIT_STEP(4);
+          }
+        }
+      }
+    }
+#undef VIT_STEP
+    if (b >= tb0) S.tdec[b - tb0][lane] = dreg << (30 - te);
+  }
+  if (tb1 > (3 * Fs - 1) / 30) S.tdec[tb1 - tb0][lane] = 0;
+  if (BLIND_DIAG == 3) {
+    if (met == 12345678u) out->L = 9; // (keeps the Viterbi live)
+    return;
   }
   met &= 0xFFFFu;
-  // best end state: the last index of the smallest (unsigned) metric
-  const uint32_t key  = wave_min((met << 6) | (63u - lane));
+  // best end state: the last index of the smallest (unsigned) metric; after 3F steps lane l holds state
+  // rotl6(l, 3F mod 6) in the rotating layout
+  const uint32_t pe   = VIT_ROTATE ? (3 * Fs) % 6 : 0u;
+  const uint32_t key  = wave_min((met << 6) | (63u - rotl6(lane, pe)));
   const uint32_t best = 63u - ((uint32_t)__builtin_amdgcn_readfirstlane((int)key) & 63u);
   __builtin_amdgcn_wave_barrier();
-  // chainback over steps 3F-1 .. F (decision word of step n read at n + 6, as the AVX2 traceback; kept at dec[n - F])
-  // in blocks of 64:
-  // lane k holds the word of step nb-1-k, the survivor state walks through scalar registers by readlane, and the
-  // decoded bits of the middle repetition are stored once per block
-  uint32_t es = best << 2;
-  for (uint32_t nb = 3 * Fs; nb > Fs;) {
-    const uint32_t cnt = min(64u, nb - Fs);
-    const uint64_t v   = lane < cnt ? S.dec[nb - 1 - lane + 6 - Fs] : 0;
-    const int      vlo = (int)(uint32_t)v, vhi = (int)(uint32_t)(v >> 32);
-    uint32_t       bitv = 0;
-    for (uint32_t k = 0; k < cnt; k++) {
-      const uint32_t sh = es >> 2;
-      const uint64_t w  = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, (int)k) << 32 |
-                         (uint32_t)__builtin_amdgcn_readlane(vlo, (int)k);
-      const uint32_t kb = (uint32_t)(w >> sh) & 1u;
-      es                = (es >> 1) | (kb << 7);
-      writelane1(bitv, kb, k);
+  // chainback from step 3F - 1 down to F, walking the survivor's LANE in a scalar register: the decision of step
+  // n + 6 for it is one readlane of that block's bit strings.  Identity layout: state s -> (s >> 1) | kb << 5.
+  // Rotating layout: the decision of step t sits in lane rotr6(s, (t + 1) mod 6) and one step back the predecessor's
+  // lane is the same lane with bit (5 - t mod 6) mod 6 ... i.e. bit (6 - (t + 1) mod 6) mod 6 replaced by kb.
+  // Decoded bits of the middle repetition (n < 2F) are gathered per block (acc: bit i = step t_lo + i) and stored
+  // once per block.
+  uint32_t ln = rotr6(best, pe);
+  for (int b = (int)tb1; b >= (int)tb0; b--) {
+    const uint32_t tr  = S.tdec[b - (int)tb0][lane];
+    const int      t0  = 30 * b;
+    const int      rhi = min(29, (int)(3 * Fs + 5) - t0), rlo = max(0, (int)(Fs + 6) - t0);
+    uint32_t       acc = 0;
+#define TB_STEP(R)                                                                                                    \
+  do {                                                                                                               \
+    const uint32_t kb = ((uint32_t)__builtin_amdgcn_readlane((int)tr, (int)ln) >> (29 - (R))) & 1u;                  \
+    if (VIT_ROTATE) {                                                                                                \
+      constexpr uint32_t q = (6u - ((R) + 1u) % 6u) % 6u;                                                            \
+      ln                   = (ln & ~(1u << q)) | (kb << q);                                                          \
+    } else {                                                                                                         \
+      ln = (ln >> 1) | (kb << 5);                                                                                    \
+    }                                                                                                                \
+    acc = acc + acc + kb;                                                                                            \
+  } while (0)
+#define TB_STEP_IF(R)                                                                                                 \
+  if ((R) <= rhi && (R) >= rlo) TB_STEP(R)
+    if (rhi == 29 && rlo == 0) {
+      TB_STEP(29); TB_STEP(28); TB_STEP(27); TB_STEP(26); TB_STEP(25); TB_STEP(24);
+      TB_STEP(23); TB_STEP(22); TB_STEP(21); TB_STEP(20); TB_STEP(19); TB_STEP(18);
+      TB_STEP(17); TB_STEP(16); TB_STEP(15); TB_STEP(14); TB_STEP(13); TB_STEP(12);
+      TB_STEP(11); TB_STEP(10); TB_STEP(9); TB_STEP(8); TB_STEP(7); TB_STEP(6);
+      TB_STEP(5); TB_STEP(4); TB_STEP(3); TB_STEP(2); TB_STEP(1); TB_STEP(0);
+    } else {
+      TB_STEP_IF(29); TB_STEP_IF(28); TB_STEP_IF(27); TB_STEP_IF(26); TB_STEP_IF(25); TB_STEP_IF(24);
+      TB_STEP_IF(23); TB_STEP_IF(22); TB_STEP_IF(21); TB_STEP_IF(20); TB_STEP_IF(19); TB_STEP_IF(18);
+      TB_STEP_IF(17); TB_STEP_IF(16); TB_STEP_IF(15); TB_STEP_IF(14); TB_STEP_IF(13); TB_STEP_IF(12);
+      TB_STEP_IF(11); TB_STEP_IF(10); TB_STEP_IF(9); TB_STEP_IF(8); TB_STEP_IF(7); TB_STEP_IF(6);
+      TB_STEP_IF(5); TB_STEP_IF(4); TB_STEP_IF(3); TB_STEP_IF(2); TB_STEP_IF(1); TB_STEP_IF(0);
     }
-    const uint32_t n = nb - 1 - lane;
-    if (lane < cnt && n < 2 * Fs) S.bits[n - Fs] = (uint8_t)bitv;
-    nb -= cnt;
+#undef TB_STEP_IF
+#undef TB_STEP
+    // step t = t0 + rlo + i decoded bit i of acc; it is bit n - F of the block for n = t - 6 in [F, 2F)
+    const int n = t0 + rlo + (int)lane - 6;
+    if ((int)lane <= rhi - rlo && n < 2 * (int)Fs) S.bits[n - (int)Fs] = (uint8_t)((acc >> lane) & 1u);
   }
   __builtin_amdgcn_wave_barrier();
   // CRC16 (crc.c, poly 0x1021, zero init: payload(x) * x^16 mod P) is linear in the payload bits: bit i contributes
