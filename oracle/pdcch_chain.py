@@ -639,9 +639,10 @@ def find_dl_dci(llr, nof_cce, sf_idx, rnti, nof_prb, nof_ports, tm=0, cfg=None, 
     allocated, found = [], []
 
     def overlaps(L, n):
+        # dci_location_is_allocated (ue_dl.c:436-448) as written: location.L is the level index (pdcch.c:270) and
+        # serves as the width
         for (aL, an) in allocated:
-            aw, w = 1 << aL, 1 << L
-            if (an <= n < an + aw) or (n <= an < n + w):
+            if (an <= n < an + aL) or (n <= an < n + L):
                 return True
         return False
 

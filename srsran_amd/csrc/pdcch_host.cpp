@@ -418,11 +418,11 @@ int blind_search_replay(const mi355_cell_t& cell, uint32_t nof_cce, uint16_t rnt
   int                               total = 0;
   mi355_dci_location_t              com[MI355_MAX_CANDIDATES_COM];
   const uint32_t                    ncom = common_locations(nof_cce, com);
+  // dci_location_is_allocated (ue_dl.c:436-448) as written: location.L is the level index (pdcch.c:270), used as the
+  // width, so a level-0 allocation covers no CCE and a level-3 one the first 3 of its 8
   auto overlaps = [&](const mi355_dci_location_t& x) {
-    for (auto& a : allocated) {
-      const uint32_t aw = 1u << a.L, w = 1u << x.L;
-      if ((a.ncce <= x.ncce && x.ncce < a.ncce + aw) || (x.ncce <= a.ncce && a.ncce < x.ncce + w)) return true;
-    }
+    for (auto& a : allocated)
+      if ((a.ncce <= x.ncce && x.ncce < a.ncce + a.L) || (x.ncce <= a.ncce && a.ncce < x.ncce + x.L)) return true;
     return false;
   };
   auto search = [&](uint32_t space, const mi355_dci_location_t* locs, uint32_t nloc, const uint32_t* fmts,

@@ -334,62 +334,13 @@ template <int K> __device__ __forceinline__ bool vit_step(uint32_t& met, uint32_
   return d;
 }
 
-__global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
+// Decode one candidate that passed the gate: rate dematching (rm_conv.c:98-148), the AVX2 decoder's quantisation, a
+// 64-state tail-biting Viterbi over three repetitions and its chainback, CRC16 remainder.  Lane 0 writes out (status
+// 2); returns the CRC remainder (wave-uniform) and w0 = payload bits 0..31, MSB first.
+__device__ __forceinline__ uint32_t decode_cand(WaveLds& S, const float* llr, uint32_t E, uint32_t nbits, uint32_t L,
+                                                uint32_t ncce, DciCand* out, uint32_t& w0)
 {
-  __shared__ WaveLds lds[WAVES];
-  const uint32_t     lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t     gw   = blockIdx.x * WAVES + wv;
-  const uint32_t     job  = gw / (PDCCH_SLOTS * PDCCH_FMTS);
-  const uint32_t     slot = (gw / PDCCH_FMTS) % PDCCH_SLOTS, fmt = gw % PDCCH_FMTS;
-  WaveLds&           S    = lds[wv];
-  DciCand*           out  = a.out + gw;
-  const BlindJob&    bj   = a.jobs[job]; // read in place (a private copy indexed by space / fmt would go to scratch)
-  const uint32_t     space = slot < MI355_MAX_CANDIDATES_UE ? 0u : 1u;
-  const uint32_t     cidx  = space ? slot - MI355_MAX_CANDIDATES_UE : slot;
-  const uint32_t     nbits = bj.nbits[space][fmt];
-  const uint32_t     cfi   = a.cfi[job];
-  const uint32_t     ntot  = (cfi >= 1 && cfi <= 3) ? a.ncce[cfi - 1] : 0u;
-  // candidate location of this slot (pdcch.c:230-330), computed uniformly by every lane
-  uint32_t L = 0, ncce = 0, k = 0;
-  bool     have = false;
-  if (((bj.spaces >> space) & 1u) && nbits) {
-    if (space == 0) {
-      // pdcch.c:230-290 without the candidate list: within a level, candidate i repeats an earlier one exactly when
-      // i >= N / L (the modulo wraps), and candidates of different levels never coincide, so level l contributes
-      // min(6/6/2/2, N / L) candidates in order
-      for (uint32_t l = 0; l < 4 && !have; l++) {
-        const uint32_t LL = 1u << l, m = ntot / LL, cnt = min(l < 2 ? 6u : 2u, m);
-        if (cidx < k + cnt) {
-          have = true, L = l, ncce = LL * ((bj.Yk + (cidx - k)) % m);
-        }
-        k += cnt;
-      }
-    } else {
-      for (uint32_t l = 2; l <= 3 && !have; l++) {
-        const uint32_t LL = 1u << l;
-        for (uint32_t i = 0; i < min(ntot, 16u) / LL && !have; i++)
-          if (k < MI355_MAX_CANDIDATES_COM && LL * i + LL <= ntot) {
-            if (k == cidx) have = true, L = l, ncce = LL * i;
-            k++;
-          }
-      }
-    }
-  }
-  if (!have) {
-    if (lane == 0) out->status = 0;
-    return;
-  }
-  const uint32_t E   = 72u << L;
-  const float*   llr = a.llr + (size_t)job * a.llr_stride + 72 * ncce;
-  // srslte_pdcch_decode_msg's gate: mean |llr| > 0.3
-  double s = 0;
-  for (uint32_t i = lane; i < E; i += 64) s += (double)fabsf(llr[i]);
-  s = wave_sum(s);
-  if (!(s / E > 0.3)) {
-    if (lane == 0) out->status = 1, out->L = L, out->ncce = ncce;
-    return;
-  }
-  if (BLIND_DIAG == 1) return;
+  const uint32_t lane = __lane_id();
   // rate dematching (rm_conv.c:98-148)
   const uint32_t F = nbits + 16, N = 3 * F;
   const uint32_t nrows = (F - 1) / 32 + 1, Kp = 32 * nrows, ndummy = Kp - F;
@@ -449,7 +400,7 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
     S.bm[e]           = (uint16_t)((((c2 ^ S.q[o + 2]) + av + 1) >> 1) >> 3);
   }
   __builtin_amdgcn_wave_barrier();
-  if (BLIND_DIAG == 2) return;
+  if (BLIND_DIAG == 2) return ~0u;
   // 64-state Viterbi over 3F steps, one lane per state (vit_step), decisions kept as per-lane bit strings: step
   // 30 b + r's decision of lane l is bit 29 - r of tdec[b - tb0][l] (one v_addc per step, one 64-lane store per 30
   // steps; 30 is a multiple of the state layout's period).  Only the blocks the traceback reads are kept: steps
@@ -515,7 +466,7 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
   if (tb1 > (3 * Fs - 1) / 30) S.tdec[tb1 - tb0][lane] = 0;
   if (BLIND_DIAG == 3) {
     if (met == 12345678u) out->L = 9; // (keeps the Viterbi live)
-    return;
+    return ~0u;
   }
   met &= 0xFFFFu;
   // best end state: the last index of the smallest (unsigned) metric; after 3F steps lane l holds state
@@ -572,6 +523,7 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
   // CRC16 (crc.c, poly 0x1021, zero init: payload(x) * x^16 mod P) is linear in the payload bits: bit i contributes
   // x^(nbits - 1 - i + 16) mod P, so every lane takes its bits' terms and the wave xor-reduces; the payload words
   // (MSB first) and the received parity come from ballots of the decoded bits -- no serial per-bit loop on one lane
+  uint32_t rem = 0;
   if (F > 128) { // (no LTE DCI is this long: MI355_DCI_MAX_BITS bounds the buffer) the serial form
     if (lane == 0) {
       uint32_t crc = 0, p = 0;
@@ -588,8 +540,11 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
           if (32 * q + b < nbits) w |= (uint32_t)S.bits[32 * q + b] << (31 - b);
         out->bits[q] = w;
       }
+      rem = p ^ crc, w0 = out->bits[0];
     }
-    return;
+    rem = (uint32_t)__builtin_amdgcn_readfirstlane((int)rem);
+    w0  = (uint32_t)__builtin_amdgcn_readfirstlane((int)w0);
+    return rem;
   }
   uint32_t       crc = 0;
   const uint32_t b0 = lane < F ? S.bits[lane] : 0u, b1 = lane + 64 < F ? S.bits[lane + 64] : 0u;
@@ -613,7 +568,88 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
       const uint32_t n = nbits > 32 * q ? min(32u, nbits - 32 * q) : 0u; // payload bits in word q
       out->bits[q]     = n ? __builtin_bitreverse32(w[q]) & (0xFFFFFFFFu << (32 - n)) : 0u;
     }
+    rem = p ^ crc;
   }
+  w0 = __builtin_bitreverse32((uint32_t)m0); // payload bits 0 .. 31, MSB first (bits past nbits are not looked at)
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)rem);
+}
+
+// candidate location of a slot (pdcch.c:230-330), computed uniformly by every lane; false: no candidate there
+__device__ __forceinline__ bool slot_location(const BlindJob& bj, uint32_t slot, uint32_t ntot, uint32_t& L,
+                                              uint32_t& ncce)
+{
+  const uint32_t space = slot < MI355_MAX_CANDIDATES_UE ? 0u : 1u;
+  const uint32_t cidx  = space ? slot - MI355_MAX_CANDIDATES_UE : slot;
+  uint32_t       k     = 0;
+  if (space == 0) {
+    // pdcch.c:230-290 without the candidate list: within a level, candidate i repeats an earlier one exactly when
+    // i >= N / L (the modulo wraps), and candidates of different levels never coincide, so level l contributes
+    // min(6/6/2/2, N / L) candidates in order
+    for (uint32_t l = 0; l < 4; l++) {
+      const uint32_t LL = 1u << l, m = ntot / LL, cnt = min(l < 2 ? 6u : 2u, m);
+      if (cidx < k + cnt) {
+        L = l, ncce = LL * ((bj.Yk + (cidx - k)) % m);
+        return true;
+      }
+      k += cnt;
+    }
+  } else {
+    for (uint32_t l = 2; l <= 3; l++) {
+      const uint32_t LL = 1u << l;
+      for (uint32_t i = 0; i < min(ntot, 16u) / LL; i++)
+        if (k < MI355_MAX_CANDIDATES_COM && LL * i + LL <= ntot) {
+          if (k == cidx) {
+            L = l, ncce = LL * i;
+            return true;
+          }
+          k++;
+        }
+    }
+  }
+  return false;
+}
+
+// srslte_pdcch_decode_msg's gate (pdcch.c:392-397): mean |llr| > 0.3, the sum in double
+__device__ __forceinline__ bool gate_pass(const float* llr, uint32_t E)
+{
+  double s = 0;
+  for (uint32_t i = __lane_id(); i < E; i += 64) s += (double)fabsf(llr[i]);
+  s = wave_sum(s);
+  return s / E > 0.3;
+}
+
+// One wave per (subframe, search-space candidate, DCI size): every candidate that passes the gate is decoded and the
+// host replays dci_blind_search over the results.  (A sequential walk -- one wave per subframe decoding only what
+// dci_blind_search reaches -- was measured and dropped: 255 vs 121 us per 1,024 subframes.  A hit at level 0 or 1
+// allocates a width of 0 or 1 CCE in the reference's overlap test, so little is skipped, and one serial decode chain
+// per SIMD leaves the VALU idle.)
+__global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
+{
+  __shared__ WaveLds lds[WAVES];
+  const uint32_t     lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t     gw   = blockIdx.x * WAVES + wv;
+  const uint32_t     job  = gw / (PDCCH_SLOTS * PDCCH_FMTS);
+  const uint32_t     slot = (gw / PDCCH_FMTS) % PDCCH_SLOTS, fmt = gw % PDCCH_FMTS;
+  DciCand*           out  = a.out + gw;
+  const BlindJob&    bj   = a.jobs[job]; // read in place (a private copy indexed by space / fmt would go to scratch)
+  const uint32_t     space = slot < MI355_MAX_CANDIDATES_UE ? 0u : 1u;
+  const uint32_t     nbits = bj.nbits[space][fmt];
+  const uint32_t     cfi   = a.cfi[job];
+  const uint32_t     ntot  = (cfi >= 1 && cfi <= 3) ? a.ncce[cfi - 1] : 0u;
+  uint32_t           L = 0, ncce = 0;
+  if (!((bj.spaces >> space) & 1u) || !nbits || !slot_location(bj, slot, ntot, L, ncce)) {
+    if (lane == 0) out->status = 0;
+    return;
+  }
+  const uint32_t E   = 72u << L;
+  const float*   llr = a.llr + (size_t)job * a.llr_stride + 72 * ncce;
+  if (!gate_pass(llr, E)) {
+    if (lane == 0) out->status = 1, out->L = L, out->ncce = ncce;
+    return;
+  }
+  if (BLIND_DIAG == 1) return;
+  uint32_t w0;
+  decode_cand(lds[wv], llr, E, nbits, L, ncce, out, w0);
 }
 
 } // namespace

@@ -205,3 +205,67 @@ def test_find_and_decode_end_to_end(case, full, monkeypatch):
 def _with_rnti(m, rnti):
     m.rnti = rnti
     return m
+
+
+@pytest.mark.parametrize("common_ss", [False, True], ids=["ue_ss", "ue_and_common_ss"])
+def test_blind_search_two_dcis(common_ss):
+    """Two DL DCIs for the same RNTI in every subframe, at non-overlapping UE-specific locations (the TM's format 2 at
+    level 2, a format 1A at level 3): the blind search finds both, in dci_blind_search's order, as the oracle's
+    find_dl_dci does on the same LLRs (ue_dl.c:450-550, the reference's overlap test for allocated locations)."""
+    from srsran_amd import pdcch as D
+    from srsran_amd import pdsch as S
+    from srsran_amd.dlsch import SoftbufferPool
+    from srsran_amd.ue_dl import UeDl, default_chest_cfg
+    from pdsch_jobs import DevIqSubframe
+    nprb, ports, nrx, tm, cid, rnti = 50, 2, 2, 3, 11, 0x4602
+    cell = S.make_cell(nprb, ports, cid)
+    rng = np.random.default_rng(77)
+    subs, placed = [], []
+    for sf_idx in (1, 4, 7, 8):
+        cfi = 3
+        ncce = D.nof_cce(cell, cfi)
+        locs = D.ue_locations(ncce, sf_idx, rnti)
+        la = next(lv for lv in locs if lv[0] == 2)
+        lb = next((lv for lv in locs if lv[0] == 3 and (lv[1] + 8 <= la[1] or la[1] + 4 <= lv[1])), None)
+        if lb is None:
+            continue
+        mA = D.pack(cell, _make_dci(D, cell, P.FORMAT2, 14, rnti), sf_idx)
+        mB = D.pack(cell, _make_dci(D, cell, P.FORMAT1A, 9, rnti), sf_idx)
+        mA.location, mB.location = D.DciLocation(*la), D.DciLocation(*lb)
+        mA.rnti = mB.rnti = rnti
+        g = D.dci_to_grant(cell, D.unpack(cell, _with_rnti(mA, rnti), sf_idx), sf_idx, cfi, tm, False)
+        prb = np.array([[g.prb_idx[s][k] for k in range(nprb)] for s in range(2)], np.uint8)
+        cfg = pc.Cfg(nof_prb=nprb, nof_ports=ports, cell_id=cid, nof_rx=nrx, cfi=cfi, sf_idx=sf_idx, rnti=rnti,
+                     scheme=g.tx_scheme, nof_layers=g.nof_layers, pmi=g.pmi,
+                     qm=[[1, 2, 4, 6, 8][g.tb[t].mod] for t in range(g.nof_tb)],
+                     tbs=[g.tb[t].tbs for t in range(g.nof_tb)], rv=[0, 0], prb=prb, csi_enable=True)
+
+        def ctrl(tx, ms=(mA, mB), sf_idx=sf_idx, cfi=cfi):
+            D.encode_ctrl_host(cell, sf_idx, cfi, list(ms), tx)
+
+        iq, _payload, _h, _s2 = uc.synth_iq(cfg, rng, snr_db=32, ctrl=ctrl, channel="taps")
+        subs.append(DevIqSubframe(cfg, iq, softbuffers=(2 * len(subs), 2 * len(subs) + 1)))
+        placed.append((sf_idx, cfi))
+    assert len(subs) >= 2
+    ucfg = D.UeDlCfg()
+    ucfg.tm, ucfg.dci_common_ss = tm, int(common_ss)
+    ue = UeDl(cell, nrx)
+    pool = SoftbufferPool(2 * len(subs), max_cb=32)
+    cfgs = []
+    for s in subs:
+        c = S.PdschCfg()
+        c.rnti, c.decoder_type, c.csi_enable = rnti, S.MIMO_DECODER_MMSE, 1
+        c.softbuffer[0], c.softbuffer[1] = s.job.cfg.softbuffer[0], s.job.cfg.softbuffer[1]
+        cfgs.append(c)
+    pays = [p for s in subs for p in (s.job.payload[0] or s.payload[0].ptr, s.job.payload[1] or s.payload[0].ptr)]
+    _sfs, chest, ctrl, dcis, _res, _g = D.find_and_decode(ue, pool, [s.sfjob for s in subs], [ucfg] * len(subs),
+                                                          cfgs, default_chest_cfg(), pays)
+    rg = P.regs(nprb, ports, cid, 0)
+    for i, (s, (sf_idx, cfi)) in enumerate(zip(subs, placed)):
+        assert ctrl[i].nof_dci == 2, (i, ctrl[i].nof_dci)
+        o_llr = P.pdcch_llr(s.grids(), s.ces(), rg, cfi, cid, sf_idx, chest[i].noise_estimate)
+        assert np.array_equal(D.last_llr(ue, i), o_llr)
+        found = P.find_dl_dci(o_llr, rg.nof_cce(cfi), sf_idx, rnti, nprb, ports, tm=tm, dci_common_ss=common_ss)
+        assert [(f["format"], f["L"], f["ncce"]) for f in found] == [(d.format, d.location.L, d.location.ncce)
+                                                                     for d in dcis[i]]
+    ue.close()
