@@ -45,8 +45,13 @@ struct mi355_softbuffer_pool {
   uint8_t* cb_crc = nullptr; // nof_sb * max_cb
   uint8_t* data   = nullptr; // nof_sb * max_cb * SB_DATA
   uint8_t* fresh  = nullptr; // nof_sb * max_cb: buffer logically zero (lazy reset)
-  uint2*   d_list = nullptr; // batched reset list {softbuffer, code blocks to reset}
-  uint32_t list_cap = 0;
+  // batched reset lists {softbuffer, code blocks to reset}, two in turn: a call's list upload waits only for the
+  // reset kernel that read the same buffer two calls ago (ev_list), not for everything queued before it
+  uint2*     d_list[2]   = {nullptr, nullptr};
+  uint32_t   list_cap[2] = {0, 0};
+  hipEvent_t ev_list[2]  = {nullptr, nullptr};
+  bool       ev_armed[2] = {false, false};
+  uint32_t   lpar        = 0;
   mi355::HostStaging st_list;
 };
 
@@ -88,15 +93,18 @@ struct mi355_dlsch {
   std::map<uint32_t, uint32_t*>          scales;       // K -> per-lane CRC scale factors
   std::map<uint32_t, uint32_t*>          tb_scales;    // TB bytes -> per-thread CRC24A scale factors (epilogue)
   CrcTable*                              crc = nullptr; // [0] CRC24A, [1] CRC24B
-  // per-call scratch
-  char*  scratch     = nullptr;
-  size_t scratch_cap = 0;
+  // per-call scratch, two in turn: a call's descriptor upload waits only for the epilogue of the call before last
+  // (done_ev of the same slot, the last reader of its staged part), so a batch enqueued behind one still in flight
+  // (find_and_decode's second chunk) uploads at once instead of at the first one's end
+  char*      scratch[2]     = {nullptr, nullptr};
+  size_t     scratch_cap[2] = {0, 0};
+  hipEvent_t done_ev[2]     = {nullptr, nullptr};
+  bool       done_armed[2]  = {false, false};
+  uint32_t   par            = 0;
   std::mutex mu;
   bool       prof = false;
   HostStaging stage;
   HostStaging back; // pinned read-back of ret | avg
-  hipEvent_t  done_ev    = nullptr; // after the previous batch's epilogue
-  bool        done_armed = false;
 };
 
 static uint32_t rm_buflen(uint32_t K) { return tdec_subblocks(K) ? 3 * (K + 32) + 12 : 3 * K + 12; }
@@ -215,19 +223,20 @@ static int tb_crc_scales(mi355_dlsch_t* q, uint32_t nbytes, const uint32_t** out
   return MI355_SUCCESS;
 }
 
-static int scratch(mi355_dlsch_t* q, size_t bytes, char** p)
+static int scratch(mi355_dlsch_t* q, uint32_t k, size_t bytes, char** p)
 {
-  if (bytes > q->scratch_cap) {
-    if (q->scratch) {
+  if (bytes > q->scratch_cap[k]) {
+    if (q->scratch[k]) {
       CHECK_HIP(hipDeviceSynchronize());
-      CHECK_HIP(hipFree(q->scratch));
-      q->scratch = nullptr;
+      CHECK_HIP(hipFree(q->scratch[k]));
+      q->scratch[k]    = nullptr;
+      q->done_armed[k] = false;
     }
     size_t cap = bytes + bytes / 4 + 4096;
-    CHECK_HIP(hipMalloc(&q->scratch, cap));
-    q->scratch_cap = cap;
+    CHECK_HIP(hipMalloc(&q->scratch[k], cap));
+    q->scratch_cap[k] = cap;
   }
-  *p = q->scratch;
+  *p = q->scratch[k];
   return MI355_SUCCESS;
 }
 
@@ -262,7 +271,11 @@ void mi355_softbuffer_pool_destroy(mi355_softbuffer_pool_t* p)
   (void)hipFree(p->cb_crc);
   (void)hipFree(p->data);
   (void)hipFree(p->fresh);
-  (void)hipFree(p->d_list);
+  for (int k = 0; k < 2; k++) {
+    if (p->ev_armed[k]) (void)hipEventSynchronize(p->ev_list[k]);
+    if (p->ev_list[k]) (void)hipEventDestroy(p->ev_list[k]);
+    (void)hipFree(p->d_list[k]);
+  }
   delete p;
 }
 
@@ -297,24 +310,30 @@ int mi355_softbuffer_reset_tbs_batch(mi355_softbuffer_pool_t* p, const uint32_t*
   if (!p || (n && (!sbs || !tbs))) return MI355_ERROR_INVALID_INPUTS;
   if (!n) return MI355_SUCCESS;
   CHECK_HIP(hipSetDevice(p->device));
-  hipStream_t s = (hipStream_t)stream;
-  if (n > p->list_cap) {
-    if (p->d_list) {
-      CHECK_HIP(hipStreamSynchronize(s));
-      CHECK_HIP(hipFree(p->d_list));
+  hipStream_t    s = (hipStream_t)stream;
+  const uint32_t k = p->lpar;
+  p->lpar ^= 1u;
+  if (n > p->list_cap[k]) {
+    if (p->d_list[k]) {
+      if (p->ev_armed[k]) CHECK_HIP(hipEventSynchronize(p->ev_list[k]));
+      CHECK_HIP(hipFree(p->d_list[k]));
+      p->ev_armed[k] = false;
     }
-    p->list_cap = n + n / 2 + 64;
-    CHECK_HIP(hipMalloc(&p->d_list, p->list_cap * sizeof(uint2)));
+    p->list_cap[k] = n + n / 2 + 64;
+    CHECK_HIP(hipMalloc(&p->d_list[k], p->list_cap[k] * sizeof(uint2)));
   }
+  if (!p->ev_list[k]) CHECK_HIP(hipEventCreateWithFlags(&p->ev_list[k], hipEventDisableTiming));
   CHECK_HIP(p->st_list.reserve(n * sizeof(uint2)));
   auto* l = (uint2*)p->st_list.slot(n * sizeof(uint2));
   for (uint32_t i = 0; i < n; i++) {
     if (sbs[i] >= p->nof_sb) return MI355_ERROR_INVALID_INPUTS;
     l[i] = make_uint2(sbs[i], std::min((tbs[i] + 24) / (6144 - 24) + 1, p->max_cb)); // softbuffer.c:128-132
   }
-  // the list buffer is reused by every call: the copy waits for an earlier call's reset kernel on s
-  CHECK_HIP(p->st_list.upload(p->d_list, s, true));
-  CHECK_HIP(dlsch_launch_reset_list(p->d_list, n, p->max_cb, p->fresh, p->cb_crc, s));
+  // list buffer k was last read by the reset kernel of the call before last: the copy waits for that one only
+  CHECK_HIP(p->st_list.upload(p->d_list[k], s, false, p->ev_armed[k] ? p->ev_list[k] : nullptr));
+  CHECK_HIP(dlsch_launch_reset_list(p->d_list[k], n, p->max_cb, p->fresh, p->cb_crc, s));
+  CHECK_HIP(hipEventRecord(p->ev_list[k], s));
+  p->ev_armed[k] = true;
   return MI355_SUCCESS;
 }
 
@@ -398,8 +417,10 @@ void mi355_dlsch_destroy(mi355_dlsch_t* q)
   for (auto& kv : q->scales) (void)hipFree(kv.second);
   for (auto& kv : q->tb_scales) (void)hipFree(kv.second);
   (void)hipFree(q->crc);
-  (void)hipFree(q->scratch);
-  if (q->done_ev) (void)hipEventDestroy(q->done_ev);
+  for (int k = 0; k < 2; k++) {
+    (void)hipFree(q->scratch[k]);
+    if (q->done_ev[k]) (void)hipEventDestroy(q->done_ev[k]);
+  }
   if (q->own) (void)hipStreamDestroy(q->own);
   delete q;
 }
@@ -588,8 +609,10 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
   auto rnd = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t need = rnd(ntb * sizeof(TbDesc)) + rnd(4 * (q->max_its + 1)) + rnd(total_cb * sizeof(CbDesc)) +
                       3 * rnd(total_cb * 4) + rnd(total_cb) + rnd(dec_bytes) + 2 * rnd(ntb * 4);
+  const uint32_t slot = q->par;
+  q->par ^= 1u;
   char* base = nullptr;
-  int   r    = scratch(q, need, &base);
+  int   r    = scratch(q, slot, need, &base);
   if (r) return r;
   char* p     = base;
   auto  carve = [&](size_t b) {
@@ -612,9 +635,9 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
   CHECK_HIP(q->stage.reserve(staged));
   q->stage.put(tbd.data(), ntb * sizeof(TbDesc));
   q->stage.zeros(4 * (q->max_its + 1));
-  // after_s: the previous batch may still be in flight; its epilogue (the last reader of the staged part) is done
-  // at done_ev
-  CHECK_HIP(q->stage.upload(base, s, after_s, after_s && q->done_armed ? q->done_ev : nullptr));
+  // the batch that last used this slot may still be in flight (after_s): its epilogue, the last reader of the staged
+  // part, is done at done_ev[slot]; a slot never used (or just reallocated) needs no wait
+  CHECK_HIP(q->stage.upload(base, s, false, after_s && q->done_armed[slot] ? q->done_ev[slot] : nullptr));
 
   DlschTbArgs ta{d_tb,  (int)ntb, d_data, pool->cb_crc, pool->data, d_ret, &q->crc[0],
                  d_cb,  d_slot,   d_its,  d_done,       d_run,      d_avg};
@@ -725,9 +748,9 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     }
   }
   CHECK_HIP(dlsch_launch_epilogue(ta, s));
-  if (!q->done_ev) CHECK_HIP(hipEventCreateWithFlags(&q->done_ev, hipEventDisableTiming));
-  CHECK_HIP(hipEventRecord(q->done_ev, s));
-  q->done_armed = true;
+  if (!q->done_ev[slot]) CHECK_HIP(hipEventCreateWithFlags(&q->done_ev[slot], hipEventDisableTiming));
+  CHECK_HIP(hipEventRecord(q->done_ev[slot], s));
+  q->done_armed[slot] = true;
 
   const auto t1 = now();
   if (pend) {

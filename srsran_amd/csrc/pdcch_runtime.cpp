@@ -153,7 +153,10 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
   }
   if (!rb) CHECK_HIP(hipStreamCreateWithFlags(&rb, hipStreamNonBlocking));
   for (uint32_t c = 0; c < nchunks; c++) {
-    const uint32_t o = (uint32_t)((uint64_t)n * c / nchunks), m = (uint32_t)((uint64_t)n * (c + 1) / nchunks) - o;
+    auto bound = [&](uint32_t k) { // first boundary at split0 when set (two chunks)
+      return k == 1 && nchunks == 2 && split0 && split0 < n ? split0 : (uint32_t)((uint64_t)n * k / nchunks);
+    };
+    const uint32_t o = bound(c), m = bound(c + 1) - o;
     chunk_end[c]     = o + m;
     if (front) {
       const int e = front(o, m);

@@ -42,6 +42,7 @@ struct CtrlState {
   // Noise per subframe from host_noise[i] or, when host_noise is null, from device memory d_noise[i].
   int run(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, const float* d_noise, const uint16_t* rntis,
           const mi355_ue_dl_cfg_t* cfgs, uint32_t n, hipStream_t s, mi355_ctrl_res_t* res, mi355_dci_msg_t* msgs);
+  uint32_t split0 = 0; // launch(): first chunk's size with two chunks (0: n / 2)
   // run() in two halves: launch() enqueues the kernels and read-backs of n subframes in nchunks consecutive chunks
   // (one completion event each); finish(c) waits for chunk c only and replays its blind searches, so the host
   // works on chunk c while the GPU runs the later chunks (and whatever the caller enqueued after them)

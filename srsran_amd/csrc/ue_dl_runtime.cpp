@@ -756,7 +756,10 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   static const int chunk_env = getenv("MI355_UEDL_CHUNKS") ? atoi(getenv("MI355_UEDL_CHUNKS")) : 0;
   const uint32_t   forced    = q->chunks ? q->chunks : (chunk_env >= 1 && chunk_env <= 8 ? (uint32_t)chunk_env : 0u);
   const uint32_t   nchunks   = forced ? std::max(1u, std::min(forced, njobs)) : (njobs >= 256 ? 2u : 1u);
-  const uint32_t   end0      = (uint32_t)((uint64_t)njobs / nchunks); // CtrlState::launch's first chunk boundary
+  // MI355_UEDL_SPLIT0 (A/B timing): the first of two chunks' share in percent
+  static const int split_env = getenv("MI355_UEDL_SPLIT0") ? atoi(getenv("MI355_UEDL_SPLIT0")) : 0;
+  q->ctrl->split0 = nchunks == 2 && split_env > 0 && split_env < 100 ? (uint32_t)((uint64_t)njobs * split_env / 100) : 0u;
+  const uint32_t end0 = q->ctrl->split0 ? q->ctrl->split0 : (uint32_t)((uint64_t)njobs / nchunks); // launch()'s
   const bool       defer     = chest_deferrable(chest_cfg) && njobs > 0;
   size_t           used      = 0;
   if ((r = ofdm_run(q, sfjobs, njobs, s, &used, defer))) return r;
