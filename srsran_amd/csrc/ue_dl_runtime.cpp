@@ -49,6 +49,15 @@ struct ChestLink {
   float noise[MI355_MAX_RX_ANT][MI355_MAX_PORTS] = {};
 };
 
+// find_and_decode: one chunk's PDSCH jobs and the bookkeeping of its decode in flight
+struct FdChunk {
+  uint32_t                       b = 0, e = 0;
+  std::vector<mi355_pdsch_job_t> jobs;
+  std::vector<uint32_t>          which, rs_sb, rs_tbs;
+  std::vector<mi355_pdsch_res_t> sub; // the chunk's results while its decode is in flight
+  int                            r = MI355_SUCCESS;
+};
+
 struct mi355_ue_dl {
   WienerBank*    wiener = nullptr; // WIENER estimator states per link (srslte_wiener_dl_t), built on first use
   int            device = 0;
@@ -70,6 +79,12 @@ struct mi355_ue_dl {
   CtrlState*     ctrl     = nullptr;       // PCFICH / PDCCH stage, built on first use
   std::vector<std::unique_ptr<mi355::PdschPending>> pend; // find_and_decode: per chunk, decodes left in flight
   uint32_t       chunks = 0;                              // find_and_decode chunk count (0: automatic)
+  // find_and_decode's host arrays, kept from call to call: a batch's replay and grant building then write into
+  // memory already mapped (1.5 MB of DCI messages and ~1 MB of job descriptors per 2,048 subframes otherwise newly
+  // allocated, their first-touch page faults on the host's critical path between the chunks)
+  std::vector<mi355_dci_msg_t> fd_msgs;
+  std::vector<uint16_t>        fd_rntis;
+  std::vector<FdChunk>         fd_ck;
   // find_and_decode: OFDM / estimator job tables uploaded for the whole batch, kernels launched per chunk in front
   // of the chunk's control kernels (ofdm_launch_range / chest_launch_range)
   OfdmArgs       ofdm_def{};
@@ -770,9 +785,11 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   if (defer && (r = chest_launch_range(q, 0, end0, s))) return r;
   ChestFill fill{q, chest_cfg, nullptr, sfjobs, njobs, chest, false};
   if (!defer && (r = chest_finish_async(q, &fill, d_out, s))) return r;
-  std::vector<uint16_t>        rntis(njobs);
-  // uninitialised: the replay writes every message it reports (1.5 MB of zeroing per 2,048 subframes otherwise)
-  std::unique_ptr<mi355_dci_msg_t[]> msgs(new mi355_dci_msg_t[(size_t)njobs * MI355_MAX_DCI_MSG]);
+  std::vector<uint16_t>& rntis = q->fd_rntis;
+  rntis.resize(njobs);
+  // the replay writes every message it reports: stale contents of earlier calls are never read
+  if (q->fd_msgs.size() < (size_t)njobs * MI355_MAX_DCI_MSG) q->fd_msgs.resize((size_t)njobs * MI355_MAX_DCI_MSG);
+  mi355_dci_msg_t* const msgs = q->fd_msgs.data();
   for (uint32_t i = 0; i < njobs; i++) rntis[i] = cfgs[i].rnti;
   const auto t1 = now();
   // Two chunks: the host replays chunk 0's blind searches and builds its grants while the GPU decodes chunk 1's
@@ -799,22 +816,21 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   }
   if (defer && (r = chest_finish_async(q, &fill, d_out, s))) return r;
   const auto t1c = now();
-  struct Chunk {
-    uint32_t                       b = 0, e = 0;
-    std::vector<mi355_pdsch_job_t> jobs;
-    std::vector<uint32_t>          which, rs_sb, rs_tbs;
-    std::vector<mi355_pdsch_res_t> sub; // the chunk's results while its decode is in flight
-    int                            r = MI355_SUCCESS;
-  };
-  std::vector<Chunk> ck(nchunks);
+  using Chunk = FdChunk;
+  std::vector<Chunk>& ck = q->fd_ck;
+  if (ck.size() < nchunks) ck.resize(nchunks);
+  for (uint32_t c = 0; c < nchunks; c++) { // (capacity kept)
+    ck[c].jobs.clear(), ck[c].which.clear(), ck[c].rs_sb.clear(), ck[c].rs_tbs.clear(), ck[c].sub.clear();
+    ck[c].r = MI355_SUCCESS;
+  }
   // srslte_ue_dl_find_dl_dci + DCI -> grant, RV from the SFN for format 1C, softbuffer reset list (ue_dl.c:1494-1535)
   auto prepare = [&](uint32_t c) {
     Chunk& C = ck[c];
     C.b      = c ? q->ctrl->chunk_end[c - 1] : 0;
     C.e      = q->ctrl->chunk_end[c];
-    if ((C.r = q->ctrl->finish(c, rntis.data(), ue_cfgs, ctrl, msgs.get()))) return;
+    if ((C.r = q->ctrl->finish(c, rntis.data(), ue_cfgs, ctrl, msgs))) return;
     for (uint32_t i = C.b; i < C.e; i++) sfs[i].cfi = ctrl[i].cfi;
-    if ((C.r = unpack_all(q, sfs, ue_cfgs, C.e, ctrl, msgs.get(), dci, C.b))) return;
+    if ((C.r = unpack_all(q, sfs, ue_cfgs, C.e, ctrl, msgs, dci, C.b))) return;
     host_parallel_for(C.e - C.b, 128, [&](uint32_t lo, uint32_t hi) { // grants: independent per subframe
       for (uint32_t i = C.b + lo; i < C.b + hi; i++) {
         if (ctrl[i].nof_dci != 1) continue; // the reference decodes only when exactly one DCI was found
