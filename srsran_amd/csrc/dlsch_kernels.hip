@@ -6,6 +6,7 @@
 
 #include "crc_device.h"
 #include "dlsch_internal.h"
+#include "rm_image.h"
 
 namespace mi355 {
 
@@ -24,7 +25,10 @@ constexpr uint32_t RM_LDS     = 3 * 6144 + 12; // N of the largest code block
 constexpr uint32_t RM_THREADS = 512;
 constexpr int      RM_Q       = (3 * (6144 + 32) + 12 + 8 * RM_THREADS - 1) / (8 * RM_THREADS); // buffer quads per thread
 constexpr int      RM_EQ      = (RM_LDS + 8 * RM_THREADS - 1) / (8 * RM_THREADS);             // LLR quads per thread
-constexpr int      RM_CPB     = 1;                                                              // code blocks per workgroup
+#ifndef RM_CPB_N
+#define RM_CPB_N 1
+#endif
+constexpr int      RM_CPB     = RM_CPB_N;                                                       // code blocks per workgroup
 
 __device__ __forceinline__ uint32_t add_pairs(uint32_t a, uint32_t b) // two wrapping int16 additions
 {
@@ -52,7 +56,7 @@ __device__ __forceinline__ uint32_t ld_llr_pair(const int16_t* e, uint32_t r2, b
 // even and the LLRs are handled as int16 pairs.
 __global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
 {
-  extern __shared__ __attribute__((aligned(16))) uint32_t acc32[]; // a.fold2 pairs
+  extern __shared__ __attribute__((aligned(16))) uint32_t acc32[]; // a.fold2 pairs, padded (img_u32)
   const uint16_t* acc   = (const uint16_t*)acc32;
   const uint32_t  N     = a.N, tid = threadIdx.x, N2 = min(N / 2, a.fold2);
   const uint32_t  pairs = a.buflen / 2;
@@ -98,11 +102,11 @@ __global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
     for (int k = 0; k < RM_EQ; k++) {
       const uint32_t i = 4 * (tid + k * RM_THREADS);
       if (i + 3 < N2) {
-        *(uint4*)&acc32[i] = ev[k];
+        *(uint4*)&acc32[img_u32(i)] = ev[k];
       } else {
-        if (i < N2) acc32[i] = ev[k].x;
-        if (i + 1 < N2) acc32[i + 1] = ev[k].y;
-        if (i + 2 < N2) acc32[i + 2] = ev[k].z;
+        if (i < N2) acc32[img_u32(i)] = ev[k].x;
+        if (i + 1 < N2) acc32[img_u32(i + 1)] = ev[k].y;
+        if (i + 2 < N2) acc32[img_u32(i + 2)] = ev[k].z;
       }
     }
     // later wraps (E > N) accumulate
@@ -110,7 +114,7 @@ __global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
       __syncthreads();
       const uint32_t lim2 = min(N, n_e - base) / 2;
       for (uint32_t r2 = tid; r2 < lim2; r2 += RM_THREADS)
-        acc32[r2] = add_pairs(acc32[r2], ld_llr_pair(e + base, r2, e4));
+        acc32[img_u32(r2)] = add_pairs(acc32[img_u32(r2)], ld_llr_pair(e + base, r2, e4));
     }
     __syncthreads();
 #pragma unroll
@@ -126,7 +130,7 @@ __global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
         const uint32_t r0 = w[cc] & 0xffffu, r1 = w[cc] >> 16;
         const bool     h0 = r0 != RM_NONE && r0 < n_e, h1 = r1 != RM_NONE && r1 < n_e;
         any |= h0 || h1;
-        v[cc] = add_pairs(o[cc], (h0 ? acc[r0] : 0u) | ((h1 ? acc[r1] : 0u) << 16));
+        v[cc] = add_pairs(o[cc], (h0 ? acc[img_i16(r0)] : 0u) | ((h1 ? acc[img_i16(r1)] : 0u) << 16));
       }
       if (!any) continue; // nothing to add to an old buffer
       if (sb16 && i + 3 < pairs) {
@@ -374,7 +378,7 @@ hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s)
   if (a.N > RM_LDS) return hipErrorInvalidValue;
   DlschRmArgs b = a;
   b.fold2       = (a.fold2 && a.fold2 < a.N / 2) ? a.fold2 : a.N / 2;
-  const size_t lds = (size_t)((b.fold2 + 3) & ~3u) * 4;
+  const size_t lds = (size_t)img_elems(2 * ((b.fold2 + 3) & ~3u)) * 2;
   hipLaunchKernelGGL(dlsch_rm_rx, dim3((unsigned)((a.ncb + RM_CPB - 1) / RM_CPB)), dim3(RM_THREADS), lds, s, b);
   hipLaunchKernelGGL(dlsch_rm_consume, dim3((unsigned)((a.ncb + 255) / 256)), dim3(256), 0, s, a.desc, a.ncb, a.fresh,
                      a.sb_crc);

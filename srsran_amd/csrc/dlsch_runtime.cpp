@@ -500,10 +500,25 @@ int mi355::DlschPending::collect()
   return MI355_SUCCESS;
 }
 
+int mi355::dlsch_rm_inv(mi355_dlsch_t* q, uint32_t K, uint32_t rv, const uint16_t** out)
+{
+  if (!q || rv > 3) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  return rm_table(q, K, rv, out);
+}
+
+uint32_t mi355::dlsch_rm_buflen(uint32_t K) { return rm_buflen(K); }
+
+mi355::SoftbufferView mi355::softbuffer_view(mi355_softbuffer_pool_t* p)
+{
+  return SoftbufferView{p->buf, SB_STRIDE, p->cb_crc, p->fresh, p->nof_sb, p->max_cb};
+}
+
 int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const void* d_e_bits,
                                  const mi355_dlsch_tb_t* tbs, uint32_t ntb, uint8_t* d_data, int32_t* ret,
                                  float* avg_iterations, void* stream, mi355::WaitHook hook, bool llr8,
-                                 mi355::DlschPending* pend, bool after_s)
+                                 mi355::DlschPending* pend, bool after_s, bool rm_done)
 {
   if (!q || !pool || !tbs || !ret || (ntb && !d_e_bits)) return MI355_ERROR_INVALID_INPUTS;
   if (ntb == 0) return MI355_SUCCESS;
@@ -712,7 +727,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     ra.sb_stride = SB_STRIDE;
     ra.sb_crc    = pool->cb_crc;
     ra.fold2     = gi < fold2.size() ? fold2[gi] : 0;
-    CHECK_HIP(dlsch_launch_rm(ra, s));
+    if (!rm_done) CHECK_HIP(dlsch_launch_rm(ra, s));
     auto it = q->dec.find(K);
     if (it == q->dec.end()) {
       mi355_tdec_batch_t* td = nullptr;

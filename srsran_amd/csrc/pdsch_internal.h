@@ -68,4 +68,29 @@ hipError_t pdsch_launch_llr(const PdschCwDev* cws, uint32_t ncw, uint32_t max_pa
 hipError_t pdsch_launch_fused(const PdschJobDev* jobs, uint32_t njobs, uint32_t max_pairs, const uint32_t* keys,
                               uint32_t nkeys, hipStream_t s);
 
+// Equaliser + LLRs + rate dematching in one pass (pdsch_eq_rm): one workgroup per (job, code block index c) takes the
+// RE span that code block c's LLRs come from -- the same in both codewords when they share modulation and transport
+// block size -- equalises it, keeps both codewords' LLRs of the span in LDS and rate-dematches them straight into the
+// two softbuffers: the LLRs (e) never go through HBM.  For batches whose jobs are all fused, whose code blocks have
+// E <= N, in the 16-bit LLR mode; the DL-SCH then skips its own rate dematching.
+struct EqRmLayer {           // the transport block fed by one layer (codeword)
+  const uint16_t* inv[2];    // rate-dematching tables (decoder position -> circular index) for K1 / K2 at its rv
+  uint32_t        N[2];      // 3K + 12
+  uint32_t        buflen[2]; // decoder buffer length of K1 / K2
+  uint32_t        C1;        // code blocks of size K1
+  uint32_t        slot0;     // softbuffer slot of its code block 0 (softbuffer * max_cb)
+};
+struct EqRmJob {
+  uint32_t  C, Qm, Gp; // code blocks (same in both codewords), bits per symbol, nof_e_bits / Qm
+  EqRmLayer layer[2];  // by layer; a layer without a transport block to decode has J.cw[l] == nullptr
+};
+struct EqRmPool {
+  int16_t*       sb;
+  size_t         sb_stride; // int16 per slot
+  const uint8_t* sb_crc;
+  uint8_t*       fresh;
+};
+hipError_t pdsch_launch_eq_rm(const PdschJobDev* jobs, const EqRmJob* rj, uint32_t njobs, uint32_t max_c, uint32_t img,
+                              const uint32_t* keys, uint32_t nkeys, const EqRmPool& pool, hipStream_t s);
+
 } // namespace mi355

@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "pdsch_internal.h"
+#include "rm_image.h"
 #include "xcd.h"
 
 namespace mi355 {
@@ -543,14 +544,13 @@ template <int QM> __device__ __forceinline__ void store_llrs(GLB int16_t* e, con
     if ((uint32_t)k < nb) e[k] = o[k];
 }
 
-// LLRs of symbol pair pr (symbols 2pr, 2pr+1; ns of them exist) of codeword C from the symbols and csi
+// LLRs o of symbol pair pr (symbols 2pr, 2pr+1; ns of them exist) of codeword C from the symbols and csi
 template <int QM>
-__device__ __forceinline__ void llr_syms(const PdschCwDev& C, uint32_t pr, uint32_t ns, const cf (&x)[2],
-                                         const float (&csi)[2], uint32_t cmax_bits)
+__device__ __forceinline__ void llr_compute(const PdschCwDev& C, uint32_t pr, uint32_t ns, const cf (&x)[2],
+                                            const float (&csi)[2], uint32_t cmax_bits, int16_t (&o)[2 * QM])
 {
   const uint32_t n  = C.nof_re;
   const uint32_t s0 = 2 * pr;
-  int16_t        o[2 * QM];
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     if ((uint32_t)k < ns) {
@@ -561,7 +561,7 @@ __device__ __forceinline__ void llr_syms(const PdschCwDev& C, uint32_t pr, uint3
     }
   }
   // descrambling e = c ? -e : e (srslte_scrambling_s_offset, scrambling.c:43-47) with the packed sequence
-  const uint32_t b0 = s0 * QM, nb = ns * QM;
+  const uint32_t b0 = s0 * QM;
   const uint32_t w0 = b0 >> 5, sh = b0 & 31;
   const GLB uint32_t* scr = gptr(C.scr);
   const uint64_t bits = (uint64_t)scr[w0] | ((sh + 2 * QM > 32 && (b0 + 2 * QM - 1) / 32 < (C.nof_bits + 31) / 32)
@@ -609,7 +609,16 @@ __device__ __forceinline__ void llr_syms(const PdschCwDev& C, uint32_t pr, uint3
       }
     }
   }
-  store_llrs<QM>(gptr(C.e) + b0, o, nb);
+}
+
+// ... stored into the codeword's e at bit 2 pr QM
+template <int QM>
+__device__ __forceinline__ void llr_syms(const PdschCwDev& C, uint32_t pr, uint32_t ns, const cf (&x)[2],
+                                         const float (&csi)[2], uint32_t cmax_bits)
+{
+  int16_t o[2 * QM];
+  llr_compute<QM>(C, pr, ns, x, csi, cmax_bits, o);
+  store_llrs<QM>(gptr(C.e) + 2 * pr * QM, o, ns * QM);
 }
 
 template <int QM> __device__ __forceinline__ void llr_pair(const PdschCwDev& C, uint32_t pr, uint32_t cmax_bits)
@@ -832,6 +841,53 @@ __global__ __launch_bounds__(256) void pdsch_csimax_cols(const PdschJobDev* __re
   }
 }
 
+// one RE of a fused job: equalised symbols and csi of both layers (precoding.c:345-355, 1519-1548, 1786-1820)
+__device__ __forceinline__ void eq_re(const PdschJobDev& J, const cf (&h)[4], const cf (&y)[2], float noise, cf& x0,
+                                      cf& x1, float& c0, float& c1)
+{
+  if (J.scheme == 0) { // precoding.c:345-355
+    cf    r  = mk(0.f, 0.f);
+    float hh = 0.f;
+#pragma unroll
+    for (int p = 0; p < 2; p++) {
+      if ((uint32_t)p < J.nof_rx) {
+        r = r + y[p] * cj(h[p]);
+        hh += h[p].re * h[p].re + h[p].im * h[p].im;
+      }
+    }
+    const float c = hh + noise, nrm = 1.0f / J.scaling;
+    x0 = mk(r.re * nrm / c, r.im * nrm / c);
+    c0 = c;
+    x1 = mk(0.f, 0.f);
+    c1 = 0.f;
+  } else if (J.nof_layers == 2) { // precoding.c:1519-1548
+    const float norm = J.cb == 0 ? 0x1.6a09e6p+0f / J.scaling : 2.0f / J.scaling;
+    cf          h00, h01, h10, h11;
+    if (J.cb == 0) {
+      h00 = h[0], h01 = h[2], h10 = h[1], h11 = h[3];
+    } else if (J.cb == 1) {
+      h00 = h[0] + h[2], h01 = h[0] - h[2], h10 = h[1] + h[3], h11 = h[1] - h[3];
+    } else {
+      h00 = h[0] + mulj(h[2]), h01 = h[0] - mulj(h[2]), h10 = h[1] + mulj(h[3]), h11 = h[1] - mulj(h[3]);
+    }
+    mmse_2x2_csi(y[0], y[1], h00, h01, h10, h11, x0, x1, c0, c1, noise, norm);
+  } else { // precoding.c:1786-1820
+    const float norm = 0x1.6a09e6p+0f / J.scaling;
+    cf          hv[2];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const cf a = h[r], b = h[2 + r];
+      hv[r] = J.cb == 0 ? a + b : J.cb == 1 ? a - b : J.cb == 2 ? a + mulj(b) : a - mulj(b);
+    }
+    const float c  = hv[0].re * hv[0].re + hv[0].im * hv[0].im + hv[1].re * hv[1].re + hv[1].im * hv[1].im;
+    const float hh = norm / c;
+    x0 = (cj(hv[0]) * y[0] + cj(hv[1]) * y[1]) * hh;
+    c0 = (float)((double)(c / norm) * 0.70710678118654752);
+    x1 = mk(0.f, 0.f);
+    c1 = 0.f;
+  }
+}
+
 #ifndef PDSCH_FU_P
 #define PDSCH_FU_P 1
 #endif
@@ -892,51 +948,7 @@ __global__ __launch_bounds__(256) void pdsch_eq_llr(const PdschJobDev* __restric
     cf             xs[2][2]; // [layer][RE]
     float          cs[2][2];
 #pragma unroll
-    for (int e = 0; e < 2; e++) {
-      const cf(&h)[4] = H[k][e];
-      const cf(&y)[2] = Y[k][e];
-      if (J.scheme == 0) { // precoding.c:345-355
-        cf    r  = mk(0.f, 0.f);
-        float hh = 0.f;
-#pragma unroll
-        for (int p = 0; p < 2; p++) {
-          if ((uint32_t)p < J.nof_rx) {
-            r = r + y[p] * cj(h[p]);
-            hh += h[p].re * h[p].re + h[p].im * h[p].im;
-          }
-        }
-        const float c = hh + noise, nrm = 1.0f / J.scaling;
-        xs[0][e]      = mk(r.re * nrm / c, r.im * nrm / c);
-        cs[0][e]      = c;
-        xs[1][e]      = mk(0.f, 0.f);
-        cs[1][e]      = 0.f;
-      } else if (J.nof_layers == 2) { // precoding.c:1519-1548
-        const float norm = J.cb == 0 ? 0x1.6a09e6p+0f / J.scaling : 2.0f / J.scaling;
-        cf          h00, h01, h10, h11;
-        if (J.cb == 0) {
-          h00 = h[0], h01 = h[2], h10 = h[1], h11 = h[3];
-        } else if (J.cb == 1) {
-          h00 = h[0] + h[2], h01 = h[0] - h[2], h10 = h[1] + h[3], h11 = h[1] - h[3];
-        } else {
-          h00 = h[0] + mulj(h[2]), h01 = h[0] - mulj(h[2]), h10 = h[1] + mulj(h[3]), h11 = h[1] - mulj(h[3]);
-        }
-        mmse_2x2_csi(y[0], y[1], h00, h01, h10, h11, xs[0][e], xs[1][e], cs[0][e], cs[1][e], noise, norm);
-      } else { // precoding.c:1786-1820
-        const float norm = 0x1.6a09e6p+0f / J.scaling;
-        cf          hv[2];
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-          const cf a = h[r], b = h[2 + r];
-          hv[r] = J.cb == 0 ? a + b : J.cb == 1 ? a - b : J.cb == 2 ? a + mulj(b) : a - mulj(b);
-        }
-        const float c  = hv[0].re * hv[0].re + hv[0].im * hv[0].im + hv[1].re * hv[1].re + hv[1].im * hv[1].im;
-        const float hh = norm / c;
-        xs[0][e]       = (cj(hv[0]) * y[0] + cj(hv[1]) * y[1]) * hh;
-        cs[0][e]       = (float)((double)(c / norm) * 0.70710678118654752);
-        xs[1][e]       = mk(0.f, 0.f);
-        cs[1][e]       = 0.f;
-      }
-    }
+    for (int e = 0; e < 2; e++) eq_re(J, H[k][e], Y[k][e], noise, xs[0][e], xs[1][e], cs[0][e], cs[1][e]);
     if constexpr (QM0 != 0) {
       const cf    x[2]   = {xs[0][0], xs[0][1]};
       const float csi[2] = {cs[0][0], cs[0][1]};
@@ -978,6 +990,294 @@ hipError_t pdsch_launch_fused(const PdschJobDev* jobs, uint32_t njobs, uint32_t 
         case 4: launch_eq_llr_1<4>(q1, g, jobs + j0, nblk, s); break;
         case 6: launch_eq_llr_1<6>(q1, g, jobs + j0, nblk, s); break;
         default: launch_eq_llr_1<8>(q1, g, jobs + j0, nblk, s); break;
+      }
+    }
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- equaliser + LLRs + rate dematching
+// pdsch_eq_rm (pdsch_internal.h): workgroup (job, c).  Code block c of either codeword takes the LLR bits
+// [rp, rp + n_e) of its codeword (sch.c:391-401 with the reference's '>' quirk, as dlsch_tb_prologue), i.e. the REs
+// [rp / Qm, (rp + n_e) / Qm): the RE pairs overlapping them are equalised and turned into LLRs exactly as
+// pdsch_eq_llr does (same descrambling and CSI weighting, whatever the pair's place), the span's LLRs of each layer
+// land in an LDS image, and each image is rate-dematched as dlsch_rm_rx does it (the decoder buffer walked in order,
+// circular index r = inv[j] gathered from the image, a fresh slot written whole, an old one read-modified) -- E <= N,
+// so the image needs no wrap-around fold.  A code block decoded in an earlier transmission (sb_crc) is left alone.
+#ifndef PDSCH_ER_THREADS
+#define PDSCH_ER_THREADS 256
+#endif
+constexpr uint32_t ER_THREADS = PDSCH_ER_THREADS;
+constexpr int      ER_Q       = 5;                                                                 // quads per round
+constexpr int      ER_R       = (3 * (6144 + 32) + 12 + 8 * ER_THREADS * ER_Q - 1) / (8 * ER_THREADS * ER_Q); // rounds
+constexpr int      ER_Q2      = 3; // quads per round when both layers share a pass
+constexpr int      ER_R2      = (3 * (6144 + 32) + 12 + 8 * ER_THREADS * ER_Q2 - 1) / (8 * ER_THREADS * ER_Q2);
+
+__device__ __forceinline__ uint32_t add_pairs16(uint32_t a, uint32_t b) // two wrapping int16 additions
+{
+  return ((a + b) & 0xffffu) | (((a >> 16) + (b >> 16)) << 16);
+}
+
+// a pair's 2 QM LLRs at span offset b (wrapping below 0) into the padded image (rm_image.h), LLRs outside
+// [0, n_e) dropped: whole pairs inside the span as 16- (QM 8) or 8-byte (QM 4) stores, 8 / 4 int16 aligned
+template <int QM> __device__ __forceinline__ void img_put(int16_t* im, uint32_t b, uint32_t n_e, const int16_t (&o)[2 * QM])
+{
+  auto pk = [&](int k) { return (uint32_t)(uint16_t)o[k] | ((uint32_t)(uint16_t)o[k + 1] << 16); };
+  if (b < n_e && b + 2 * QM <= n_e) {
+    if constexpr (QM == 8) {
+      *(uint4*)&im[img_i16(b)]     = make_uint4(pk(0), pk(2), pk(4), pk(6));
+      *(uint4*)&im[img_i16(b + 8)] = make_uint4(pk(8), pk(10), pk(12), pk(14));
+      return;
+    } else if constexpr (QM == 4) {
+      *(uint2*)&im[img_i16(b)]     = make_uint2(pk(0), pk(2));
+      *(uint2*)&im[img_i16(b + 4)] = make_uint2(pk(4), pk(6));
+      return;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2 * QM; k++)
+    if (b + k < n_e) im[img_i16(b + k)] = o[k];
+}
+
+template <int QM0, int QM1>
+__global__ __launch_bounds__(ER_THREADS) void pdsch_eq_rm(const PdschJobDev* __restrict__ jobs,
+                                                          const EqRmJob* __restrict__ rjobs, uint32_t max_c, uint32_t img,
+                                                          EqRmPool P)
+{
+  extern __shared__ __attribute__((aligned(16))) int16_t imgs[]; // [layer][img]
+  const uint32_t     Lb = xcd_chunk(blockIdx.x, gridDim.x);      // a job's code blocks on one XCD: its estimates
+  const uint32_t     jn = Lb / max_c, c = Lb % max_c;             // and RE map stay in that L2
+  const PdschJobDev& J  = jobs[jn];
+  const EqRmJob&     R  = rjobs[jn];
+  const uint32_t     tid = threadIdx.x;
+  if (!J.fused || J.fused_key != (uint32_t)(QM0 * 16 + QM1) || c >= R.C) return;
+  const uint32_t Qm = R.Qm, gamma = R.Gp % R.C, n_e0 = Qm * (R.Gp / R.C);
+  uint32_t       rp = c * n_e0, n_e = n_e0;
+  if (c > R.C - gamma) {
+    n_e = n_e0 + Qm;
+    rp  = (R.C - gamma) * n_e0 + (c - (R.C - gamma)) * n_e;
+  }
+  bool need[2], fresh[2];
+  uint32_t slot[2];
+#pragma unroll
+  for (int l = 0; l < 2; l++) {
+    slot[l]  = R.layer[l].slot0 + c;
+    need[l]  = J.cw[l] != nullptr && !P.sb_crc[slot[l]]; // sch.c:385
+    fresh[l] = need[l] && P.fresh[slot[l]] != 0;
+  }
+  if (!need[0] && !need[1]) return;
+  __shared__ PdschCwDev cwd[2];
+  __shared__ uint32_t   cmb[2];
+  if (tid < 2 && J.cw[tid]) {
+    cwd[tid] = *J.cw[tid];
+    cmb[tid] = cwd[tid].csi_enable ? *gptr(cwd[tid].cmax_final) : 0u;
+  }
+  __syncthreads();
+  // equalise the RE pairs overlapping the span; keep the span's LLRs
+  const float         noise = J.noise_dev ? *gptr(J.noise_dev) : J.noise;
+  const uint32_t      row = J.row, magic = J.row_magic, rmask = J.rhob_mask;
+  const float         rinv = J.rhob_inv;
+  const GLB uint32_t* map2 = (const GLB uint32_t*)gptr(J.map);
+  const GLB float2*   yp[2] = {gptr(J.y[0]), gptr(J.nof_rx > 1 ? J.y[1] : J.y[0])};
+  const GLB float2*   hp[4];
+  h_ptrs(J, hp);
+  const uint32_t re0 = rp / Qm, re1 = (rp + n_e) / Qm, pairs = (J.nof_re + 1) / 2;
+  const uint32_t p1  = min((re1 + 1) / 2, pairs);
+  for (uint32_t pr = re0 / 2 + tid; pr < p1; pr += ER_THREADS) {
+    const uint32_t m = map2[pr];
+    cf             Y[2][2], H[2][4];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const uint32_t g  = e ? (m >> 16) : (m & 0xffffu);
+      const uint32_t gc = g < 14 * row ? g : 0u; // the odd tail's second index is padding
+      const uint32_t l  = __umulhi(gc, magic);
+      const float    sc = ((rmask >> l) & 1u) ? rinv : 1.0f;
+#pragma unroll
+      for (int r = 0; r < 2; r++) Y[e][r] = ld(yp[r], gc) * sc;
+#pragma unroll
+      for (int q = 0; q < 4; q++) H[e][q] = ld(hp[q], gc - l * row);
+    }
+    const uint32_t ns = min(2u, J.nof_re - 2 * pr);
+    cf             xs[2][2];
+    float          cs[2][2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) eq_re(J, H[e], Y[e], noise, xs[0][e], xs[1][e], cs[0][e], cs[1][e]);
+    if constexpr (QM0 != 0) {
+      const cf    x[2]   = {xs[0][0], xs[0][1]};
+      const float csi[2] = {cs[0][0], cs[0][1]};
+      int16_t     o[2 * QM0];
+      llr_compute<QM0>(cwd[0], pr, ns, x, csi, cmb[0], o);
+      img_put<QM0>(imgs, 2 * pr * QM0 - rp, n_e, o);
+    }
+    if constexpr (QM1 != 0) {
+      const cf    x[2]   = {xs[1][0], xs[1][1]};
+      const float csi[2] = {cs[1][0], cs[1][1]};
+      int16_t     o[2 * QM1];
+      llr_compute<QM1>(cwd[1], pr, ns, x, csi, cmb[1], o);
+      img_put<QM1>(imgs + img, 2 * pr * QM1 - rp, n_e, o);
+    }
+  }
+  __syncthreads();
+  // rate dematching of each layer's image into its softbuffer (dlsch_rm_rx's gather, E <= N); both layers through
+  // one pass when they share the table (same K and rv: the usual case), so the table is read and decoded once
+  {
+    const uint32_t kx0 = c < R.layer[0].C1 ? 0u : 1u, kx1 = c < R.layer[1].C1 ? 0u : 1u;
+    if (need[0] && need[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
+        R.layer[0].buflen[kx0] == R.layer[1].buflen[kx1]) {
+      const uint32_t  npairs = R.layer[0].buflen[kx0] / 2;
+      const uint32_t* inv32  = (const uint32_t*)R.layer[0].inv[kx0];
+      uint32_t*       sb[2]  = {(uint32_t*)(P.sb + (size_t)slot[0] * P.sb_stride),
+                                (uint32_t*)(P.sb + (size_t)slot[1] * P.sb_stride)};
+      const bool      al     = (((uintptr_t)sb[0] | (uintptr_t)sb[1]) & 15) == 0;
+#pragma unroll 1
+      for (int rd = 0; rd < ER_R2; rd++) {
+        uint4 iv[ER_Q2], old[2][ER_Q2];
+#pragma unroll
+        for (int k = 0; k < ER_Q2; k++) {
+          const uint32_t i = 4 * (tid + (rd * ER_Q2 + k) * ER_THREADS);
+          iv[k]            = i + 3 < npairs ? *(const uint4*)(inv32 + i)
+                                            : make_uint4(i < npairs ? inv32[i] : 0xffffffffu,
+                                                         i + 1 < npairs ? inv32[i + 1] : 0xffffffffu,
+                                                         i + 2 < npairs ? inv32[i + 2] : 0xffffffffu, 0xffffffffu);
+#pragma unroll
+          for (int l = 0; l < 2; l++) {
+            if (fresh[l] || i >= npairs) {
+              old[l][k] = make_uint4(0u, 0u, 0u, 0u);
+            } else if (al && i + 3 < npairs) {
+              old[l][k] = *(const uint4*)(sb[l] + i);
+            } else {
+              old[l][k] = make_uint4(sb[l][i], i + 1 < npairs ? sb[l][i + 1] : 0u, i + 2 < npairs ? sb[l][i + 2] : 0u,
+                                     i + 3 < npairs ? sb[l][i + 3] : 0u);
+            }
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < ER_Q2; k++) {
+          const uint32_t i = 4 * (tid + (rd * ER_Q2 + k) * ER_THREADS);
+          if (i >= npairs) continue;
+          const uint32_t w[4] = {iv[k].x, iv[k].y, iv[k].z, iv[k].w};
+          uint32_t       v[2][4];
+          bool           any = fresh[0] || fresh[1];
+#pragma unroll
+          for (int cc = 0; cc < 4; cc++) {
+            const uint32_t r0 = w[cc] & 0xffffu, r1 = w[cc] >> 16;
+            const bool     h0 = r0 != 0xffffu && r0 < n_e, h1 = r1 != 0xffffu && r1 < n_e;
+            any |= h0 || h1;
+            const uint32_t i0 = img_i16(h0 ? r0 : 0u), i1 = img_i16(h1 ? r1 : 0u);
+            const uint32_t o0[4] = {old[0][k].x, old[0][k].y, old[0][k].z, old[0][k].w};
+            const uint32_t o1[4] = {old[1][k].x, old[1][k].y, old[1][k].z, old[1][k].w};
+            v[0][cc] = add_pairs16(o0[cc], (h0 ? (uint16_t)imgs[i0] : 0u) | ((h1 ? (uint16_t)imgs[i1] : 0u) << 16));
+            v[1][cc] = add_pairs16(o1[cc], (h0 ? (uint16_t)imgs[img + i0] : 0u) |
+                                               ((h1 ? (uint16_t)imgs[img + i1] : 0u) << 16));
+          }
+          if (!any) continue; // nothing to add to old buffers
+#pragma unroll
+          for (int l = 0; l < 2; l++) {
+            if (al && i + 3 < npairs) {
+              typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+              __builtin_nontemporal_store((u4v){v[l][0], v[l][1], v[l][2], v[l][3]}, (u4v*)(sb[l] + i));
+            } else {
+#pragma unroll
+              for (int cc = 0; cc < 4; cc++)
+                if (i + cc < npairs) sb[l][i + cc] = v[l][cc];
+            }
+          }
+        }
+      }
+      need[0] = need[1] = false; // done
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < 2; l++) {
+    if (!need[l]) continue;
+    const EqRmLayer& T      = R.layer[l];
+    const uint32_t   kx     = c < T.C1 ? 0u : 1u;
+    const uint32_t   npairs = T.buflen[kx] / 2;
+    const uint32_t*  inv32  = (const uint32_t*)T.inv[kx];
+    const uint16_t*  acc    = (const uint16_t*)(imgs + l * img);
+    uint32_t*        sb     = (uint32_t*)(P.sb + (size_t)slot[l] * P.sb_stride);
+    const bool       sb16   = ((uintptr_t)sb & 15) == 0;
+#pragma unroll 1
+    for (int rd = 0; rd < ER_R; rd++) {
+    uint4 iv[ER_Q], old[ER_Q];
+#pragma unroll
+    for (int k = 0; k < ER_Q; k++) {
+      const uint32_t i = 4 * (tid + (rd * ER_Q + k) * ER_THREADS);
+      iv[k]            = i + 3 < npairs ? *(const uint4*)(inv32 + i)
+                                        : make_uint4(i < npairs ? inv32[i] : 0xffffffffu,
+                                                     i + 1 < npairs ? inv32[i + 1] : 0xffffffffu,
+                                                     i + 2 < npairs ? inv32[i + 2] : 0xffffffffu, 0xffffffffu);
+      if (fresh[l]) {
+        old[k] = make_uint4(0u, 0u, 0u, 0u);
+      } else if (sb16 && i + 3 < npairs) {
+        old[k] = *(const uint4*)(sb + i);
+      } else {
+        old[k] = make_uint4(i < npairs ? sb[i] : 0u, i + 1 < npairs ? sb[i + 1] : 0u, i + 2 < npairs ? sb[i + 2] : 0u,
+                            i + 3 < npairs ? sb[i + 3] : 0u);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < ER_Q; k++) {
+      const uint32_t i = 4 * (tid + (rd * ER_Q + k) * ER_THREADS);
+      if (i >= npairs) continue;
+      const uint32_t w[4] = {iv[k].x, iv[k].y, iv[k].z, iv[k].w};
+      const uint32_t o[4] = {old[k].x, old[k].y, old[k].z, old[k].w};
+      uint32_t       v[4];
+      bool           any = fresh[l];
+#pragma unroll
+      for (int cc = 0; cc < 4; cc++) {
+        const uint32_t r0 = w[cc] & 0xffffu, r1 = w[cc] >> 16;
+        const bool     h0 = r0 != 0xffffu && r0 < n_e, h1 = r1 != 0xffffu && r1 < n_e;
+        any |= h0 || h1;
+        v[cc] = add_pairs16(o[cc], (h0 ? acc[img_i16(r0)] : 0u) | ((h1 ? acc[img_i16(r1)] : 0u) << 16));
+      }
+      if (!any) continue; // nothing to add to an old buffer
+      if (sb16 && i + 3 < npairs) {
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store((u4v){v[0], v[1], v[2], v[3]}, (u4v*)(sb + i));
+      } else {
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++)
+          if (i + cc < npairs) sb[i + cc] = v[cc];
+      }
+    }
+    }
+  }
+  // the slots' lazy reset is consumed (every thread has read the flags above; no other workgroup owns these slots)
+  if (tid < 2 && fresh[tid]) P.fresh[slot[tid]] = 0;
+}
+
+template <int QM0>
+static void launch_eq_rm_1(uint32_t qm1, const dim3& g, size_t lds, const PdschJobDev* jobs, const EqRmJob* rj,
+                           uint32_t max_c, uint32_t img, const EqRmPool& P, hipStream_t s)
+{
+  switch (qm1) {
+    case 0: hipLaunchKernelGGL((pdsch_eq_rm<QM0, 0>), g, dim3(ER_THREADS), lds, s, jobs, rj, max_c, img, P); break;
+    case 2: hipLaunchKernelGGL((pdsch_eq_rm<QM0, 2>), g, dim3(ER_THREADS), lds, s, jobs, rj, max_c, img, P); break;
+    case 4: hipLaunchKernelGGL((pdsch_eq_rm<QM0, 4>), g, dim3(ER_THREADS), lds, s, jobs, rj, max_c, img, P); break;
+    case 6: hipLaunchKernelGGL((pdsch_eq_rm<QM0, 6>), g, dim3(ER_THREADS), lds, s, jobs, rj, max_c, img, P); break;
+    default: hipLaunchKernelGGL((pdsch_eq_rm<QM0, 8>), g, dim3(ER_THREADS), lds, s, jobs, rj, max_c, img, P); break;
+  }
+}
+
+hipError_t pdsch_launch_eq_rm(const PdschJobDev* jobs, const EqRmJob* rj, uint32_t njobs, uint32_t max_c, uint32_t img,
+                              const uint32_t* keys, uint32_t nkeys, const EqRmPool& pool, hipStream_t s)
+{
+  if (!njobs || !max_c) return hipSuccess;
+  img = img_elems(img); // int16 per layer image (padded layout, 16-byte multiple)
+  hipLaunchKernelGGL(pdsch_csimax_cols, dim3(njobs), dim3(256), 0, s, jobs);
+  const size_t lds = 2 * (size_t)img * sizeof(int16_t);
+  for (uint32_t k = 0; k < nkeys; k++) {
+    const uint32_t q0 = keys[k] >> 4, q1 = keys[k] & 15;
+    for (uint32_t j0 = 0; j0 < njobs; j0 += 65535 / max_c) {
+      const uint32_t n = std::min(65535 / max_c, njobs - j0);
+      const dim3     g(n * max_c);
+      switch (q0) {
+        case 0: launch_eq_rm_1<0>(q1, g, lds, jobs + j0, rj + j0, max_c, img, pool, s); break;
+        case 2: launch_eq_rm_1<2>(q1, g, lds, jobs + j0, rj + j0, max_c, img, pool, s); break;
+        case 4: launch_eq_rm_1<4>(q1, g, lds, jobs + j0, rj + j0, max_c, img, pool, s); break;
+        case 6: launch_eq_rm_1<6>(q1, g, lds, jobs + j0, rj + j0, max_c, img, pool, s); break;
+        default: launch_eq_rm_1<8>(q1, g, lds, jobs + j0, rj + j0, max_c, img, pool, s); break;
       }
     }
   }

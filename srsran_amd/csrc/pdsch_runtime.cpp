@@ -25,6 +25,7 @@
 #include "host_staging.h"
 #include "lte_common.h"
 #include "pdsch_internal.h"
+#include "rm_tables.h"
 #include "runtime_internal.h"
 
 using namespace mi355;
@@ -144,6 +145,13 @@ struct JobPlan {
   bool        decode[2]{};
 };
 
+// a batch decoded through pdsch_eq_rm (pdsch_internal.h)
+struct EqRmPlan {
+  std::vector<EqRmJob> rj;
+  uint32_t             max_c = 0, img = 0;
+  EqRmPool             pool{};
+};
+
 } // namespace
 
 struct mi355_pdsch {
@@ -169,6 +177,12 @@ struct mi355_pdsch {
   HostStaging                          stage;
   hipEvent_t                           fe_done  = nullptr; // after the last front-end kernel of the previous batch
   bool                                 fe_armed = false;
+  // the last batch went through pdsch_eq_rm, which leaves no LLRs in e: mi355_pdsch_debug_stage produces them once,
+  // on demand, with pdsch_eq_llr over the same descriptors (still in the scratch until the next batch)
+  bool                                 e_pending = false;
+  const PdschJobDev*                   last_jobs_dev = nullptr;
+  uint32_t                             last_njobs = 0, last_max_fpairs = 0;
+  std::vector<uint32_t>                last_fkeys;
   std::mutex                           mu;
 };
 
@@ -334,7 +348,7 @@ static int plan_job(mi355_pdsch_t* q, const mi355_pdsch_job_t& j, const mi355_pd
 
 // front-end over planned jobs; fills P.d_off/csi_off/e_off and runs kernels A and B on s
 static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::vector<JobPlan>& plans, hipStream_t s,
-                        bool after_s = false)
+                        bool after_s = false, const EqRmPlan* er = nullptr)
 {
   const auto     t_in  = std::chrono::steady_clock::now();
   const uint32_t njobs = (uint32_t)plans.size();
@@ -397,7 +411,8 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   const size_t ncw = cws.size();
   // device scratch: [staged descriptors | d | csi | e]; the staged part mirrors the pinned host buffer
   const size_t staged = staged_size(njobs * sizeof(PdschJobDev)) + staged_size(ncw * sizeof(PdschCwDev)) +
-                        staged_size(new_ci.size() * 4) + staged_size(new_ci.size() * 8);
+                        staged_size(new_ci.size() * 4) + staged_size(new_ci.size() * 8) +
+                        (er ? staged_size(njobs * sizeof(EqRmJob)) : 0);
   auto           rnd    = [](size_t b) { return (b + 255) / 256 * 256; };
   const uint32_t nparts = (max_units + EQ_BLOCK_ITEMS - 1) / EQ_BLOCK_ITEMS; // equaliser blocks per job
   const size_t   need   = staged + rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2) + rnd((size_t)njobs * 2 * nparts * 4) +
@@ -413,6 +428,7 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   // every equaliser block that has work, read by the LLR kernel: no initialisation)
   const size_t o_jobs = 0, o_cws = o_jobs + staged_size(njobs * sizeof(PdschJobDev));
   const size_t o_nci = o_cws + staged_size(ncw * sizeof(PdschCwDev)), o_ndst = o_nci + staged_size(new_ci.size() * 4);
+  const size_t o_rj  = o_ndst + staged_size(new_ci.size() * 8);
   uint32_t*    d_cmax = (uint32_t*)(base + staged + rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2));
   uint32_t*    d_cfin = d_cmax + rnd((size_t)njobs * 2 * nparts * 4) / 4;
   std::vector<PdschJobDev> hj(njobs);
@@ -474,6 +490,7 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   q->stage.put(cws.data(), ncw * sizeof(PdschCwDev));
   q->stage.put(new_ci.data(), new_ci.size() * 4);
   q->stage.put(new_dst.data(), new_dst.size() * 8);
+  if (er) q->stage.put(er->rj.data(), njobs * sizeof(EqRmJob));
   // after_s: the previous batch may still be in flight; its front end (the only reader of the descriptors) is done
   // at fe_done
   const auto tb = now();
@@ -484,8 +501,16 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   CHECK_HIP(pdsch_launch_scr_pack((const uint32_t*)(base + o_nci), (uint32_t* const*)(base + o_ndst),
                                   (uint32_t)new_ci.size(), q->gold, PDSCH_GOLD_MAX / 32, s));
   const auto tl1 = now();
-  CHECK_HIP(pdsch_launch_fused((const PdschJobDev*)(base + o_jobs), njobs, max_fpairs, fkeys.data(),
-                               (uint32_t)fkeys.size(), s));
+  q->e_pending = er != nullptr;
+  if (er) {
+    CHECK_HIP(pdsch_launch_eq_rm((const PdschJobDev*)(base + o_jobs), (const EqRmJob*)(base + o_rj), njobs, er->max_c,
+                                 er->img, fkeys.data(), (uint32_t)fkeys.size(), er->pool, s));
+    q->last_jobs_dev = (const PdschJobDev*)(base + o_jobs), q->last_njobs = njobs, q->last_max_fpairs = max_fpairs;
+    q->last_fkeys = fkeys;
+  }
+  else
+    CHECK_HIP(pdsch_launch_fused((const PdschJobDev*)(base + o_jobs), njobs, max_fpairs, fkeys.data(),
+                                 (uint32_t)fkeys.size(), s));
   const auto tl2 = now();
   CHECK_HIP(pdsch_launch_llr((const PdschCwDev*)(base + o_cws), (uint32_t)ncw, max_pairs, s));
   const auto tl3 = now();
@@ -582,6 +607,14 @@ int mi355_pdsch_debug_stage(mi355_pdsch_t* q, uint32_t job, uint32_t cw, const f
                             const int16_t** e)
 {
   if (!q || job >= q->last.size() || cw > 1) return MI355_ERROR_INVALID_INPUTS;
+  if (q->e_pending) { // (debug path) the LLRs of the last batch, which pdsch_eq_rm kept in LDS only
+    CHECK_HIP(hipSetDevice(q->device));
+    CHECK_HIP(hipDeviceSynchronize()); // (the batch's stream may be the caller's, gone by now)
+    CHECK_HIP(pdsch_launch_fused(q->last_jobs_dev, q->last_njobs, q->last_max_fpairs, q->last_fkeys.data(),
+                                 (uint32_t)q->last_fkeys.size(), q->own));
+    CHECK_HIP(hipStreamSynchronize(q->own));
+    q->e_pending = false;
+  }
   const JobPlan& P = q->last[job];
   if (d) *d = (const float*)(q->d_arena + P.d_off[cw]);
   if (csi) *csi = q->csi_arena + P.csi_off[cw];
@@ -618,6 +651,69 @@ static void fill_results(mi355_pdsch_res_t* res, const std::vector<std::pair<uin
   }
 }
 
+// pdsch_eq_rm for the whole batch when every job qualifies: fused (port 0 / spatial multiplexing, row-invariant
+// estimates), 16-bit LLRs, the decoded transport blocks of a job with one modulation, TBS and E (so code block c of
+// either codeword comes from the same REs), E <= N for every code block (no wrap-around), valid softbuffers.
+// MI355_NO_EQRM (A/B, tests): never.
+static bool plan_eq_rm(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi355_pdsch_job_t* jobs,
+                       const std::vector<JobPlan>& plans, EqRmPlan& er)
+{
+  if (getenv("MI355_NO_EQRM") || q->llr8 || !pool || plans.empty()) return false;
+  const SoftbufferView v = softbuffer_view(pool);
+  er.rj.assign(plans.size(), EqRmJob{});
+  er.max_c = er.img = 0;
+  // a batch has few distinct TB sizes and (K, rv): segmentation and table look-ups of the previous TB are reused
+  uint32_t        seg_tbs = UINT32_MAX, tab_key[2] = {UINT32_MAX, UINT32_MAX};
+  CbSegm          seg{};
+  int             seg_err = 0;
+  const uint16_t* tab[2]  = {nullptr, nullptr};
+  auto inv_of = [&](uint32_t K, uint32_t rv, const uint16_t** out) {
+    const uint32_t key = K << 2 | rv;
+    for (int k = 0; k < 2; k++)
+      if (tab_key[k] == key) return *out = tab[k], 0;
+    const int e = dlsch_rm_inv(q->dlsch, K, rv, out);
+    tab_key[1] = tab_key[0], tab[1] = tab[0], tab_key[0] = key, tab[0] = *out;
+    return e;
+  };
+  for (size_t i = 0; i < plans.size(); i++) {
+    const JobPlan&             P   = plans[i];
+    const mi355_pdsch_cfg_t&   cfg = jobs[i].cfg;
+    const mi355_pdsch_grant_t& g   = cfg.grant;
+    if (!P.dev.fused) return false;
+    EqRmJob& R  = er.rj[i];
+    uint32_t nt = 0, tbs = 0, nbits = 0, n_max = 0;
+    for (uint32_t t = 0; t < 2; t++) {
+      if (!P.decode[t]) continue;
+      const mi355_ra_tb_t& tb = g.tb[t];
+      const uint32_t       qm = mod_bits(tb.mod);
+      if (nt && (qm != R.Qm || (uint32_t)tb.tbs != tbs || tb.nof_bits != nbits)) return false;
+      if (tb.tbs <= 0) return false;
+      if ((uint32_t)tb.tbs != seg_tbs) seg_tbs = (uint32_t)tb.tbs, seg_err = cbsegm(seg_tbs, &seg);
+      if (seg_err || seg.F || seg.C == 0 || seg.C > v.max_cb || cfg.softbuffer[t] >= v.nof_sb || tb.rv > 3 || qm == 0)
+        return false;
+      tbs = (uint32_t)tb.tbs, nbits = tb.nof_bits, nt++;
+      R.C = seg.C, R.Qm = qm, R.Gp = nbits / qm;
+      n_max                 = qm * (R.Gp / seg.C) + qm;
+      const uint32_t kmin   = seg.C1 ? (seg.C1 < seg.C ? std::min(seg.K1, seg.K2) : seg.K1) : seg.K2;
+      if (n_max > 3 * kmin + 12) return false;
+      EqRmLayer& L = R.layer[P.cw_of_tb[t] & 1];
+      for (uint32_t kx = 0; kx < 2; kx++) {
+        const uint32_t K = kx ? seg.K2 : seg.K1;
+        if (!K || (kx == 0 && !seg.C1) || (kx == 1 && seg.C1 == seg.C)) continue;
+        if (inv_of(K, tb.rv, &L.inv[kx])) return false;
+        L.N[kx]      = 3 * K + 12;
+        L.buflen[kx] = dlsch_rm_buflen(K);
+      }
+      L.C1    = seg.C1;
+      L.slot0 = cfg.softbuffer[t] * v.max_cb;
+    }
+    er.max_c = std::max(er.max_c, nt ? R.C : 0u);
+    er.img   = std::max(er.img, n_max);
+  }
+  er.pool = EqRmPool{v.buf, v.stride, v.cb_crc, v.fresh};
+  return er.max_c > 0;
+}
+
 int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi355_pdsch_job_t* jobs,
                                         uint32_t njobs, mi355_pdsch_res_t* res, void* stream, const float* d_noise,
                                         WaitHook hook, bool ce_invariant, PdschPending* pend, bool after_s)
@@ -640,8 +736,10 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
     plans[i].dev.fused = !q->llr8 && ce_invariant && (plans[i].dev.scheme == MI355_TXSCHEME_PORT0 ||
                                                       plans[i].dev.scheme == MI355_TXSCHEME_SPATIALMUX) ? 1u : 0u;
   }
-  const auto t1 = now();
-  int r = run_frontend(q, jobs, plans, s, after_s);
+  EqRmPlan   er;
+  const bool eqrm = plan_eq_rm(q, pool, jobs, plans, er);
+  const auto t1   = now();
+  int        r    = run_frontend(q, jobs, plans, s, after_s, eqrm ? &er : nullptr);
   if (r) return r;
   if (prof) {
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
@@ -699,7 +797,7 @@ int mi355::pdsch_decode_batch_dev_noise(mi355_pdsch_t* q, mi355_softbuffer_pool_
     // earlier ones still queued on s: its upload waits for their epilogue (done_ev)
     const bool after = after_s || (pend && pend->used > 0);
     r = dlsch_decode_dev_hook(q->dlsch, pool, q->e_arena, kv.second.data(), (uint32_t)kv.second.size(), nullptr,
-                              ret->data(), avg->data(), s, hook, q->llr8, dp, after);
+                              ret->data(), avg->data(), s, hook, q->llr8, dp, after, eqrm);
     hook = WaitHook{}; // once
     if (r) return r;
     if (pend)

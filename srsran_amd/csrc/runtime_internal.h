@@ -40,10 +40,24 @@ struct DlschPending {
 // llr8: int8 LLRs (srsUE's pdsch_8bit_decoder: sch.c:403-423 with llr_is_8bit), e_offset in int8 units
 // pend: leave the results in flight (see DlschPending; the hook is not run); after_s: the call's descriptor upload
 // waits for the stream's earlier work (an earlier call's decode may still be in flight on it)
+// rm_done: the softbuffers already hold this transmission's rate-dematched LLRs (pdsch_eq_rm): no rate dematching
 int dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const void* d_e_bits,
                           const mi355_dlsch_tb_t* tbs, uint32_t ntb, uint8_t* d_data, int32_t* ret, float* avg_iterations,
                           void* stream, WaitHook hook, bool llr8 = false, DlschPending* pend = nullptr,
-                          bool after_s = false);
+                          bool after_s = false, bool rm_done = false);
+
+// for a rate dematcher outside the DL-SCH (pdsch_eq_rm): the device table decoder position -> circular-buffer index
+// of (K, rv), the decoder buffer length of K, and the pool's buffers
+int      dlsch_rm_inv(mi355_dlsch_t* q, uint32_t K, uint32_t rv, const uint16_t** out);
+uint32_t dlsch_rm_buflen(uint32_t K);
+struct SoftbufferView {
+  int16_t* buf;
+  size_t   stride; // int16 per slot
+  uint8_t* cb_crc;
+  uint8_t* fresh;
+  uint32_t nof_sb, max_cb;
+};
+SoftbufferView softbuffer_view(mi355_softbuffer_pool_t* p);
 
 // A PDSCH batch decode left in flight (pdsch_decode_batch_dev_noise with pend): one DlschPending per
 // max-iterations group; collect() waits for all of them and fills the mi355_pdsch_res_t array of the call.

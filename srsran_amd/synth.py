@@ -205,6 +205,7 @@ class DlReceiver:
         """One batch: mi355_ue_dl_decode_batch (softbuffers of new TBs reset first: OFDM, estimation, PDSCH,
         DL-SCH) or, with the control channels, mi355_ue_dl_find_and_decode_batch.  With `stages` (dict) the
         two-call form (decode_fft_estimate, then decode_pdsch) is timed per stage instead."""
+        self.last_bound = bound
         import time
         jobs, sfs, cfgs, n, _ = bound
         C.memset(self.res, 0, C.sizeof(self.res))

@@ -148,3 +148,35 @@ def llr_spot_check(rx, k: int, ocfg: pc.Cfg, payload_bytes: list, decoded_job: i
         bits = np.unpackbits(np.asarray(payload_bytes[t], np.uint8))[: ocfg.tbs[t]]
         coded = oracle.dlsch_encode_tb(bits, ocfg.tbs[t], ocfg.qm[t] * Nl, nbits, ocfg.rv[t])
         assert np.array_equal(e_g > 0, coded == 1), (k, t, int(np.sum((e_g > 0) != (coded == 1))))
+        if getattr(rx, "last_bound", None) is not None and decoded_job is None:
+            softbuffer_check(rx, rx.last_bound[2][k].softbuffer[t], e_o[t], ocfg.tbs[t], ocfg.qm[t] * Nl, ocfg.rv[t],
+                             (k, t))
+
+
+def softbuffer_check(rx, sb: int, e_o: np.ndarray, tbs: int, qm: int, rv: int, what=None):
+    """The decoder buffers of softbuffer sb after a fresh-buffer decode (rate dematched by pdsch_eq_rm or
+    dlsch_rm_rx) equal the oracle's rate dematching of the oracle's LLRs (orc_dlsch_rm_tb: rm_turbo_rx_lut into
+    zeroed buffers), bit for bit over each code block's systematic, parity and tail positions."""
+    import ctypes as C
+    import oracle
+    from srsran_amd import lib
+    L = lib()
+    buf, stride, mcb = C.POINTER(C.c_int16)(), C.c_uint32(), C.c_uint32()
+    L.mi355_softbuffer_pool_buffer.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_int16)), C.POINTER(C.c_uint32),
+                                               C.POINTER(C.c_uint32)]
+    assert L.mi355_softbuffer_pool_buffer(rx.pool.h, C.byref(buf), C.byref(stride), C.byref(mcb)) == 0
+    seg = np.zeros(6, np.uint32)
+    oracle.lib().orc_cbsegm(tbs, seg)
+    Cn = int(seg[0])
+    want = np.zeros(Cn * 18600, np.int16)
+    e = np.ascontiguousarray(e_o, np.int16)
+    assert oracle.lib().orc_dlsch_rm_tb(e, e.size, tbs, qm, rv, want, 18600) == Cn
+    got = np.zeros((Cn, stride.value), np.int16)
+    base = C.cast(buf, C.c_void_p).value + 2 * sb * mcb.value * stride.value
+    L.mi355_memcpy_d2h(got.ctypes.data, base, got.nbytes)
+    for c in range(Cn):
+        K = int(seg[1]) if c < int(seg[3]) else int(seg[2])
+        cols = (np.r_[0:K, K + 32:2 * K + 32, 2 * K + 64:3 * K + 64, 3 * K + 96:3 * K + 108]
+                if oracle.lib().orc_tdec_nsb(K) else np.r_[0:3 * K + 12])  # sub-block layout or the natural one
+        w = want[c * 18600:(c + 1) * 18600]
+        assert np.array_equal(got[c, cols], w[cols]), (what, c, int(np.abs(got[c, cols].astype(np.int32) - w[cols]).max()))
