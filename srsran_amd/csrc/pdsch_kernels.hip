@@ -1040,7 +1040,10 @@ template <int QM> __device__ __forceinline__ void img_put(int16_t* im, uint32_t 
 }
 
 template <int QM0, int QM1>
-__global__ __launch_bounds__(ER_THREADS) void pdsch_eq_rm(const PdschJobDev* __restrict__ jobs,
+#ifndef PDSCH_ER_WAVES
+#define PDSCH_ER_WAVES 5
+#endif
+__global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSCH_ER_WAVES, 8))) void pdsch_eq_rm(const PdschJobDev* __restrict__ jobs,
                                                           const EqRmJob* __restrict__ rjobs, uint32_t max_c, uint32_t img,
                                                           EqRmPool P)
 {
@@ -1117,13 +1120,59 @@ __global__ __launch_bounds__(ER_THREADS) void pdsch_eq_rm(const PdschJobDev* __r
       img_put<QM1>(imgs + img, 2 * pr * QM1 - rp, n_e, o);
     }
   }
+  if (tid < 2) imgs[tid * img + n_e] = 0; // the zero slot: table entries without an LLR (RM_NONE, >= n_e) read it
   __syncthreads();
   // rate dematching of each layer's image into its softbuffer (dlsch_rm_rx's gather, E <= N); both layers through
   // one pass when they share the table (same K and rv: the usual case), so the table is read and decoded once
   {
     const uint32_t kx0 = c < R.layer[0].C1 ? 0u : 1u, kx1 = c < R.layer[1].C1 ? 0u : 1u;
-    if (need[0] && need[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
+    if (need[0] && need[1] && fresh[0] && fresh[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
         R.layer[0].buflen[kx0] == R.layer[1].buflen[kx1]) {
+      // the usual case, two fresh buffers: every position is written, a missing LLR reads the zero slot
+      const uint32_t  npairs = R.layer[0].buflen[kx0] / 2;
+      const uint32_t* inv32  = (const uint32_t*)R.layer[0].inv[kx0];
+      uint32_t*       sb[2]  = {(uint32_t*)(P.sb + (size_t)slot[0] * P.sb_stride),
+                                (uint32_t*)(P.sb + (size_t)slot[1] * P.sb_stride)};
+      const bool      al     = (((uintptr_t)sb[0] | (uintptr_t)sb[1]) & 15) == 0;
+      const uint16_t* a0     = (const uint16_t*)imgs;
+      const uint16_t* a1     = (const uint16_t*)(imgs + img);
+#pragma unroll 1
+      for (int rd = 0; rd < ER_R; rd++) {
+        uint4 iv[ER_Q];
+#pragma unroll
+        for (int k = 0; k < ER_Q; k++) {
+          const uint32_t i = 4 * (tid + (rd * ER_Q + k) * ER_THREADS);
+          iv[k]            = i + 3 < npairs ? *(const uint4*)(inv32 + i)
+                                            : make_uint4(i < npairs ? inv32[i] : 0xffffffffu,
+                                                         i + 1 < npairs ? inv32[i + 1] : 0xffffffffu,
+                                                         i + 2 < npairs ? inv32[i + 2] : 0xffffffffu, 0xffffffffu);
+        }
+#pragma unroll
+        for (int k = 0; k < ER_Q; k++) {
+          const uint32_t i = 4 * (tid + (rd * ER_Q + k) * ER_THREADS);
+          if (i >= npairs) continue;
+          const uint32_t w[4] = {iv[k].x, iv[k].y, iv[k].z, iv[k].w};
+          uint32_t       v0[4], v1[4];
+#pragma unroll
+          for (int cc = 0; cc < 4; cc++) {
+            const uint32_t r0 = min(w[cc] & 0xffffu, n_e), r1 = min(w[cc] >> 16, n_e);
+            v0[cc] = (uint32_t)a0[r0] | ((uint32_t)a0[r1] << 16);
+            v1[cc] = (uint32_t)a1[r0] | ((uint32_t)a1[r1] << 16);
+          }
+          typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+          if (al && i + 3 < npairs) {
+            __builtin_nontemporal_store((u4v){v0[0], v0[1], v0[2], v0[3]}, (u4v*)(sb[0] + i));
+            __builtin_nontemporal_store((u4v){v1[0], v1[1], v1[2], v1[3]}, (u4v*)(sb[1] + i));
+          } else {
+#pragma unroll
+            for (int cc = 0; cc < 4; cc++)
+              if (i + cc < npairs) sb[0][i + cc] = v0[cc], sb[1][i + cc] = v1[cc];
+          }
+        }
+      }
+      need[0] = need[1] = false; // done
+    } else if (need[0] && need[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
+               R.layer[0].buflen[kx0] == R.layer[1].buflen[kx1]) {
       const uint32_t  npairs = R.layer[0].buflen[kx0] / 2;
       const uint32_t* inv32  = (const uint32_t*)R.layer[0].inv[kx0];
       uint32_t*       sb[2]  = {(uint32_t*)(P.sb + (size_t)slot[0] * P.sb_stride),
@@ -1264,7 +1313,7 @@ hipError_t pdsch_launch_eq_rm(const PdschJobDev* jobs, const EqRmJob* rj, uint32
                               const uint32_t* keys, uint32_t nkeys, const EqRmPool& pool, hipStream_t s)
 {
   if (!njobs || !max_c) return hipSuccess;
-  img = img_elems(img); // int16 per layer image (padded layout, 16-byte multiple)
+  img = img_elems(img + 1); // int16 per layer image + the zero slot, 16-byte multiple
   hipLaunchKernelGGL(pdsch_csimax_cols, dim3(njobs), dim3(256), 0, s, jobs);
   const size_t lds = 2 * (size_t)img * sizeof(int16_t);
   for (uint32_t k = 0; k < nkeys; k++) {
