@@ -405,7 +405,8 @@ namespace {
 
 __device__ __forceinline__ int32_t x86_cvt_i32(float r) // r already rounded; cvt*ps2dq out-of-range rule
 {
-  return (r >= -2147483648.0f && r < 2147483648.0f) ? (int32_t)r : INT32_MIN;
+  // |r| < 2^31 or the "integer indefinite" INT32_MIN (also what -2^31 converts to; NaN fails the compare)
+  return fabsf(r) < 2147483648.0f ? (int32_t)r : INT32_MIN;
 }
 __device__ __forceinline__ int16_t sat16(int32_t v) { return (int16_t)max(-32768, min(32767, v)); }
 __device__ __forceinline__ int16_t f2s_trunc(float v) { return (int16_t)(uint16_t)(uint32_t)x86_cvt_i32(truncf(v)); }
@@ -566,9 +567,12 @@ __device__ __forceinline__ void llr_compute(const PdschCwDev& C, uint32_t pr, ui
   const GLB uint32_t* scr = gptr(C.scr);
   const uint64_t bits = (uint64_t)scr[w0] | ((sh + 2 * QM > 32 && (b0 + 2 * QM - 1) / 32 < (C.nof_bits + 31) / 32)
                                                 ? (uint64_t)scr[w0 + 1] << 32 : 0ull);
+  const uint32_t lo = (uint32_t)(bits >> sh); // the pair's 2 QM <= 16 sequence bits
 #pragma unroll
-  for (int k = 0; k < 2 * QM; k++)
-    if ((bits >> (sh + k)) & 1ull) o[k] = (int16_t)(uint16_t)(-(int32_t)o[k]);
+  for (int k = 0; k < 2 * QM; k++) { // -e as (e ^ m) - m with m = 0 / -1 (wrapping: -(-32768) = -32768)
+    const int32_t m = -(int32_t)((lo >> k) & 1u);
+    o[k]            = (int16_t)(uint16_t)(((int32_t)o[k] ^ m) - m);
+  }
   if (C.csi_enable) { // csi_correction (pdsch.c:628-741), SSE path
     const uint32_t nsym  = C.nof_bits / QM;
     const float    cmax  = nsym ? __uint_as_float(cmax_bits) : 1.0f;
