@@ -105,7 +105,16 @@ struct mi355_dlsch {
   bool       prof = false;
   HostStaging stage;
   HostStaging back; // pinned read-back of ret | avg
+  // bit h (odd): DEC2 half-iteration h runs speculatively (spec_policy); until a batch has been seen, the first one
+  std::atomic<uint32_t> spec_mask{1u << 1};
 };
+
+// MI355_TDEC_SPEC=0: no speculative DEC2 half-iterations (A/B timing)
+static bool spec_enabled()
+{
+  static const bool on = !getenv("MI355_TDEC_SPEC") || atoi(getenv("MI355_TDEC_SPEC")) != 0;
+  return on;
+}
 
 static uint32_t rm_buflen(uint32_t K) { return tdec_subblocks(K) ? 3 * (K + 32) + 12 : 3 * K + 12; }
 
@@ -487,6 +496,28 @@ mi355::DlschPending::~DlschPending()
   if (host) (void)hipHostFree(host);
 }
 
+// Speculative DEC2 (TdecRun::spec): half-iteration h (odd) does not write the next DEC1's a-priori (12 KB of a CB
+// half-iteration's ~100 KB of traffic); the code blocks its check leaves unfinished run it again (TdecRun::redo).  It
+// pays where at most ~10 % of the code blocks entering h fail there (each such block costs a whole DEC2 more), which
+// is judged from the previous batch: its per-TB average half-iteration counts (a TB whose blocks all stopped at h
+// averages h + 1).  The last allowed half-iteration never needs the a-priori and is always speculative.
+static uint32_t spec_policy(const float* avg, const int32_t* ret, uint32_t ntb, uint32_t max_its)
+{
+  uint32_t mask = 0;
+  for (uint32_t h = 1; h + 1 < max_its; h += 2) {
+    uint32_t run = 0, fail = 0;
+    for (uint32_t t = 0; t < ntb; t++) {
+      if (ret[t] != MI355_SUCCESS && ret[t] != MI355_ERROR) continue; // not decoded
+      const float a = avg[t];
+      if (!(a > 0.f)) continue;
+      run += a > (float)h + 0.5f;
+      fail += a > (float)h + 1.5f;
+    }
+    if (run && fail * 10 <= run) mask |= 1u << h;
+  }
+  return mask;
+}
+
 int mi355::DlschPending::collect()
 {
   if (!armed) return MI355_SUCCESS;
@@ -497,6 +528,7 @@ int mi355::DlschPending::collect()
     if (invalid[t]) ret[t] = MI355_ERROR_INVALID_INPUTS;
   }
   if (avg) memcpy(avg, host + avg_off, ntb * 4);
+  if (spec_mask) spec_mask->store(spec_policy((const float*)(host + avg_off), ret, ntb, max_its));
   return MI355_SUCCESS;
 }
 
@@ -742,7 +774,9 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     doff += (size_t)n * (K / 8);
   }
 
+  const uint32_t spec_mask = spec_enabled() ? q->spec_mask.load() : 0u;
   for (uint32_t h = 0; h < q->max_its; h++) {
+    const bool spec = (h & 1) && (h + 1 == q->max_its || ((spec_mask >> h) & 1u));
     for (auto& lv : live) {
       if (lv.t8) {
         T8Batch b{};
@@ -757,7 +791,22 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
       if (!lv.t8) {
         TdecRun rq{llr8 ? pool->buf + SB_CONV8 : pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, d_run + h, lv.n,
                    lv.K, h, h + 1, lv.dec, lv.K / 8, s, &ca, &fused};
+        bool taken = false;
+        rq.spec       = spec;
+        rq.spec_taken = &taken;
         if ((r = mi355_tdec_run_internal(lv.td, rq))) return r;
+        if (!fused) CHECK_HIP(dlsch_launch_check(ca, s));
+        if (taken && h + 1 < q->max_its) { // the a-priori for the blocks still running (a no-op when none is)
+          TdecRun rd = rq;
+          rd.remaining  = d_run + h + 1;
+          rd.chk        = nullptr;
+          rd.chk_fused  = nullptr;
+          rd.spec       = false;
+          rd.spec_taken = nullptr;
+          rd.redo       = true;
+          if ((r = mi355_tdec_run_internal(lv.td, rd))) return r;
+        }
+        continue;
       }
       if (!fused) CHECK_HIP(dlsch_launch_check(ca, s));
     }
@@ -788,6 +837,8 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     pend->avg_off = rnd(ntb * 4);
     pend->ret     = ret;
     pend->avg     = avg_iterations;
+    pend->spec_mask = &q->spec_mask;
+    pend->max_its   = q->max_its;
     pend->armed   = true;
     return MI355_SUCCESS;
   }
@@ -800,6 +851,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     if (tbd[t].invalid) ret[t] = MI355_ERROR_INVALID_INPUTS;
   }
   if (avg_iterations) memcpy(avg_iterations, q->back.host + rnd(ntb * 4), ntb * 4);
+  q->spec_mask.store(spec_policy((const float*)(q->back.host + rnd(ntb * 4)), ret, ntb, q->max_its));
   if (prof) {
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     fprintf(stderr, "[mi355 host] dlsch_decode_dev: plan+launch %.1f us, wait+readback %.1f us\n", us(t0, t1), us(t1, now()));

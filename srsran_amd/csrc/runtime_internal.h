@@ -7,6 +7,7 @@
 
 #include <memory>
 #include <utility>
+#include <atomic>
 #include <vector>
 
 namespace mi355 {
@@ -30,6 +31,8 @@ struct DlschPending {
   std::vector<uint8_t> invalid;
   int32_t*             ret = nullptr;
   float*               avg = nullptr;
+  std::atomic<uint32_t>* spec_mask = nullptr; // the decoder's speculation policy, refreshed from these results
+  uint32_t             max_its   = 0;
   DlschPending()                    = default;
   DlschPending(const DlschPending&) = delete;
   ~DlschPending();

@@ -37,6 +37,10 @@ struct TdecWinArgs {
   // the batch's code blocks.  chk.scale[128 + 8 * (C > 1) + l]: x^(8 * bytes after lane l's K/(8 NL)-byte chunk).
   DlschCheckArgs  chk;
   int             chk_on;
+  // speculative DEC2 (tdec_win_spec_ok, dec != nullptr, odd n): the decisions (and the fused check) only, A1 -- the
+  // next DEC1's a-priori -- is not written; the caller reruns the half-iteration (TdecRun::redo) for the code blocks
+  // the check left unfinished
+  int             spec;
 };
 
 struct TdecDecideArgs {
@@ -89,9 +93,16 @@ struct TdecRun {
   hipStream_t     stream;
   const DlschCheckArgs* chk = nullptr;       // DL-SCH: the check of each half-iteration, fused where the kernel can
   bool*                 chk_fused = nullptr; // set when it was (the caller then launches no dlsch_cb_check)
+  // spec: an odd (DEC2) half-iteration run speculatively where the kernel can (*spec_taken set): decisions without
+  // the next a-priori.  redo: the DEC2 half-iterations again without outputs, writing that a-priori for the code
+  // blocks not done (remaining: their count after the check; a no-op at 0)
+  bool  spec       = false;
+  bool* spec_taken = nullptr;
+  bool  redo       = false;
 };
 
 hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s);
+bool       tdec_win_spec_ok(int nsb, int L);
 hipError_t tdec_win_launch_decide(int nsb, const TdecDecideArgs& a, hipStream_t s);
 hipError_t tdec_gen_launch_prep(const TdecGenPrepArgs& a, hipStream_t s);
 hipError_t tdec_gen_launch_halfit(const TdecGenArgs& a, hipStream_t s);

@@ -458,9 +458,11 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   int16_t*        D16  = (int16_t*)a.D + (size_t)grp * Lp * 128;
   const uint32_t* tab  = (dec2 ? a.dstA : a.dstE) + l;
   const int       lane0 = cbg * NL; // first lane of this code block inside the 64-lane row
-  constexpr bool  wr_bits = !dec2 && OUTK == 1; // fused decision bytes (DEC1: ext1 in natural order)
-  constexpr bool  wr_bm   = dec2 && OUTK == 1;  // fused decision bytes (DEC2: app1 de-interleaved)
+  constexpr bool  dec_o   = OUTK == 1 || OUTK == 3;
+  constexpr bool  wr_bits = !dec2 && dec_o; // fused decision bytes (DEC1: ext1 in natural order)
+  constexpr bool  wr_bm   = dec2 && dec_o;  // fused decision bytes (DEC2: app1 de-interleaved)
   constexpr bool  wr_d    = OUTK == 2;
+  constexpr bool  wr_a1   = !(dec2 && OUTK == 3); // OUTK 3 (DEC2): the next DEC1's a-priori is not written
   // The decision bytes are collected in LDS as the code block's K/8 output bytes and stored at the end with 8-byte
   // stores: DEC2's land at scattered natural positions (row j' of windows wlo/whi) as a bitmap, DEC1's are one byte
   // per window and segment (narrow scattered global stores of either cost 15-25 % of the launch).  193 words per
@@ -606,9 +608,11 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
           bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
         } else {
           // a1 = app1 - ext1 (wrapping) of the next DEC1, turbodecoder_iter.h:108-110
-          const v2s av = out - xin[i];
-          A16[olo]     = av.x;
-          A16[ohi]     = av.y;
+          if constexpr (wr_a1) {
+            const v2s av = out - xin[i];
+            A16[olo]     = av.x;
+            A16[ohi]     = av.y;
+          }
           if constexpr (wr_bm) { // natural bit w*L + j': byte w*L/8 + j'/8, bit 7 - j'%8 (turbodecoder_win.h:973-993)
             const uint32_t jd = (tb & 0xffffu) >> 7, wlo = tb & 15u, whi = (tb >> 16) & 15u;
             const uint32_t blo = wlo * (L / 8) + (jd >> 3), bhi = whi * (L / 8) + (jd >> 3);
@@ -655,7 +659,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TDEC_WAVES_
 {
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t (*t4)[4][256] = nullptr;
-  if constexpr (OUTK == 1) {
+  if constexpr (OUTK == 1 || OUTK == 3) {
     __shared__ uint32_t crc_t4[2][4][256]; // CRC24A | CRC24B slice-by-4 tables (fused code-block check)
     if (a.chk_on) { // uniform: the whole block builds the tables before any wave decodes
       if (a.remaining && *a.remaining == 0) return; // every code block of the batch has finished
@@ -802,6 +806,12 @@ static void launch_mode_o(int mode, int blocks, const TdecWinArgs& a, hipStream_
 template <int NSB, int DIAG, bool FULL = false>
 static void launch_mode(int mode, int blocks, const TdecWinArgs& a, hipStream_t s)
 {
+  if constexpr (NSB == 16 && FULL && DIAG == 0) { // speculative DEC2 (tdec_win_spec_ok): decisions, no a-priori
+    if (a.dec && a.spec && mode == 2) {
+      launch_mode_o<NSB, DIAG, FULL, 3>(mode, blocks, a, s);
+      return;
+    }
+  }
   if (a.dec) {
     launch_mode_o<NSB, DIAG, FULL, 1>(mode, blocks, a, s);
   } else if (a.write_d) {
@@ -810,6 +820,8 @@ static void launch_mode(int mode, int blocks, const TdecWinArgs& a, hipStream_t 
     launch_mode_o<NSB, DIAG, FULL, 0>(mode, blocks, a, s);
   }
 }
+
+bool tdec_win_spec_ok(int nsb, int L) { return nsb == 16 && L % TDEC_SEG == 0 && diag_mode() == 0; }
 
 hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s)
 {

@@ -254,6 +254,7 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
   hipStream_t s = rq.stream ? rq.stream : q->own;
 
   const Geometry g = geometry(K, n, q->impl);
+  if (rq.redo && !g.nsb) return MI355_SUCCESS; // (speculation is taken by the window decoder only)
   KTables*       t = nullptr;
   int            r = get_tables(q, g, &t);
   if (r) return r;
@@ -282,9 +283,20 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
     // the decide pass
     const bool fuse = g.L % 8 == 0 && out_stride % 8 == 0 && (uintptr_t)d_out % 8 == 0;
     for (uint32_t h = h0; h < h1; h++) {
+      if (rq.redo) { // DEC2 again, a-priori only, for the code blocks the check left unfinished
+        if (!(h & 1)) continue;
+        TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, rq.remaining, A1, E, D, CK, t->dstE, t->dstA,
+                       (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, 0, nullptr, out_stride};
+        CHECK_HIP(tdec_win_launch_halfit(g.nsb, wa, s));
+        continue;
+      }
       TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, rq.remaining, A1, E, D, CK, t->dstE, t->dstA,
                      (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == h1,
                      (fuse && h + 1 == h1) ? d_out : nullptr, out_stride};
+      if (rq.spec && fuse && h + 1 == h1 && (h & 1) && tdec_win_spec_ok(g.nsb, g.L)) {
+        wa.spec = 1;
+        if (rq.spec_taken) *rq.spec_taken = true;
+      }
       if (rq.chk && fuse && h + 1 == h1) { // the DL-SCH check of this half-iteration in the kernel's epilogue
         wa.chk    = *rq.chk;
         wa.chk.h  = h;
@@ -300,7 +312,7 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
       CHECK_HIP(tdec_win_launch_halfit(g.nsb, wa, s));
       if (q->prof && e1) (void)hipEventRecord(e1, s);
     }
-    if (!fuse) {
+    if (!fuse && !rq.redo) {
       TdecDecideArgs da{D, d_out, out_stride, (int)n, (int)g.L, (int)g.Lp, rq.done, rq.remaining};
       CHECK_HIP(tdec_win_launch_decide(g.nsb, da, s));
     }

@@ -79,3 +79,21 @@ def test_dlsch_invalid_and_empty():
     rets, _, _ = dl.decode(pool, [dict(tbs=97896, Qm=8, rv=0, softbuffer=0), dict(tbs=0, Qm=2, rv=0, softbuffer=1)],
                            [e, e])
     assert rets == [-2, 0]
+
+
+@pytest.mark.parametrize("max_its", [2, 3, 6])
+def test_dlsch_speculative_dec2_matches_oracle(max_its):
+    """Speculative DEC2 half-iterations (dlsch_runtime.cpp spec_policy): the a-priori of the next DEC1 is written only
+    by a rerun for the code blocks the check leaves unfinished, and the policy follows the previous batch.  Batches of
+    the mixed cases alternate with all-high-SNR ones on one decoder, so the rerun runs with many, few and no blocks
+    and the policy changes between calls; every batch must still be the oracle's."""
+    dl = Dlsch(0, max_its)
+    pool = SoftbufferPool(len(CASES), 32)
+    hi = [(t, q, g, 30.0) for (t, q, g, _s) in CASES]
+    for k, cases in enumerate((CASES, hi, hi, CASES, hi)):
+        rng = np.random.default_rng(1000 * max_its + k)
+        llrs = [oracle.make_tb(rng, t, q, g, 0, snr)[1] for (t, q, g, snr) in cases]
+        pool.reset_all()
+        got = dl.decode(pool, [dict(tbs=t, Qm=q, rv=0, softbuffer=i) for i, (t, q, g, s) in enumerate(cases)], llrs)
+        want = _oracle(llrs, cases, [0] * len(cases), max_its, [oracle.Softbuffer() for _ in cases])
+        _check(got, want, cases)
