@@ -105,7 +105,7 @@ struct mi355_dlsch {
   bool       prof = false;
   HostStaging stage;
   HostStaging back; // pinned read-back of ret | avg
-  // bit h (odd): DEC2 half-iteration h runs speculatively (spec_policy); until a batch has been seen, the first one
+  // bit h: half-iteration h runs speculatively (spec_policy); until a batch has been seen, the first DEC2
   std::atomic<uint32_t> spec_mask{1u << 1};
 };
 
@@ -496,15 +496,16 @@ mi355::DlschPending::~DlschPending()
   if (host) (void)hipHostFree(host);
 }
 
-// Speculative DEC2 (TdecRun::spec): half-iteration h (odd) does not write the next DEC1's a-priori (12 KB of a CB
-// half-iteration's ~100 KB of traffic); the code blocks its check leaves unfinished run it again (TdecRun::redo).  It
-// pays where at most ~10 % of the code blocks entering h fail there (each such block costs a whole DEC2 more), which
-// is judged from the previous batch: its per-TB average half-iteration counts (a TB whose blocks all stopped at h
-// averages h + 1).  The last allowed half-iteration never needs the a-priori and is always speculative.
+// Speculative half-iterations (TdecRun::spec): half-iteration h does not write the next one's input (DEC1: the
+// extrinsic E, DEC2: the a-priori A1 -- 12 KB of a K = 6144 code block's ~100 KB of traffic); the code blocks its
+// check leaves unfinished run it again (TdecRun::redo).  It pays where at most ~10 % of the code blocks entering h
+// fail there (each such block costs a whole half-iteration more), which is judged from the previous batch: its per-TB
+// average half-iteration counts (a TB whose blocks all stopped at h averages h + 1).  The last allowed half-iteration
+// never needs that input and is always speculative.
 static uint32_t spec_policy(const float* avg, const int32_t* ret, uint32_t ntb, uint32_t max_its)
 {
   uint32_t mask = 0;
-  for (uint32_t h = 1; h + 1 < max_its; h += 2) {
+  for (uint32_t h = 0; h + 1 < max_its; h++) {
     uint32_t run = 0, fail = 0;
     for (uint32_t t = 0; t < ntb; t++) {
       if (ret[t] != MI355_SUCCESS && ret[t] != MI355_ERROR) continue; // not decoded
@@ -776,7 +777,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
 
   const uint32_t spec_mask = spec_enabled() ? q->spec_mask.load() : 0u;
   for (uint32_t h = 0; h < q->max_its; h++) {
-    const bool spec = (h & 1) && (h + 1 == q->max_its || ((spec_mask >> h) & 1u));
+    const bool spec = h + 1 == q->max_its || ((spec_mask >> h) & 1u);
     for (auto& lv : live) {
       if (lv.t8) {
         T8Batch b{};

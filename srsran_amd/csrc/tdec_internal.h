@@ -37,9 +37,9 @@ struct TdecWinArgs {
   // the batch's code blocks.  chk.scale[128 + 8 * (C > 1) + l]: x^(8 * bytes after lane l's K/(8 NL)-byte chunk).
   DlschCheckArgs  chk;
   int             chk_on;
-  // speculative DEC2 (tdec_win_spec_ok, dec != nullptr, odd n): the decisions (and the fused check) only, A1 -- the
-  // next DEC1's a-priori -- is not written; the caller reruns the half-iteration (TdecRun::redo) for the code blocks
-  // the check left unfinished
+  // speculative half-iteration (tdec_win_spec_ok, dec != nullptr): the decisions (and the fused check) only, the next
+  // half-iteration's input (DEC1: E, DEC2: A1) is not written; the caller reruns the half-iteration (TdecRun::redo)
+  // for the code blocks the check left unfinished
   int             spec;
 };
 
@@ -93,8 +93,8 @@ struct TdecRun {
   hipStream_t     stream;
   const DlschCheckArgs* chk = nullptr;       // DL-SCH: the check of each half-iteration, fused where the kernel can
   bool*                 chk_fused = nullptr; // set when it was (the caller then launches no dlsch_cb_check)
-  // spec: an odd (DEC2) half-iteration run speculatively where the kernel can (*spec_taken set): decisions without
-  // the next a-priori.  redo: the DEC2 half-iterations again without outputs, writing that a-priori for the code
+  // spec: the half-iteration run speculatively where the kernel can (*spec_taken set): decisions without the next
+  // half-iteration's input.  redo: the half-iterations again without decisions, writing that input for the code
   // blocks not done (remaining: their count after the check; a no-op at 0)
   bool  spec       = false;
   bool* spec_taken = nullptr;

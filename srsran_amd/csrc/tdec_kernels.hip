@@ -462,7 +462,8 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   constexpr bool  wr_bits = !dec2 && dec_o; // fused decision bytes (DEC1: ext1 in natural order)
   constexpr bool  wr_bm   = dec2 && dec_o;  // fused decision bytes (DEC2: app1 de-interleaved)
   constexpr bool  wr_d    = OUTK == 2;
-  constexpr bool  wr_a1   = !(dec2 && OUTK == 3); // OUTK 3 (DEC2): the next DEC1's a-priori is not written
+  constexpr bool  wr_a1   = !(dec2 && OUTK == 3);  // OUTK 3 (speculative, DEC2): the next DEC1's a-priori not written
+  constexpr bool  wr_e    = !(!dec2 && OUTK == 3); // OUTK 3 (DEC1): the next DEC2's input not written
   // The decision bytes are collected in LDS as the code block's K/8 output bytes and stored at the end with 8-byte
   // stores: DEC2's land at scattered natural positions (row j' of windows wlo/whi) as a bitmap, DEC1's are one byte
   // per window and segment (narrow scattered global stores of either cost 15-25 % of the launch).  193 words per
@@ -601,9 +602,11 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
         const uint32_t olo = (tb & 0xffffu) + lane0 * 2, ohi = (tb >> 16) + lane0 * 2;
         if constexpr (!dec2) {
           // e = ext1 - app1 (wrapping), turbodecoder_iter.h:118-120 of the next DEC2
-          const v2s ev = has_ap ? out - U(ca[i]) : out;
-          E16[olo]     = ev.x;
-          E16[ohi]     = ev.y;
+          if constexpr (wr_e) {
+            const v2s ev = has_ap ? out - U(ca[i]) : out;
+            E16[olo]     = ev.x;
+            E16[ohi]     = ev.y;
+          }
           if constexpr (wr_d) WG_AT(a.D, j) = W(out);
           bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
         } else {
@@ -806,8 +809,8 @@ static void launch_mode_o(int mode, int blocks, const TdecWinArgs& a, hipStream_
 template <int NSB, int DIAG, bool FULL = false>
 static void launch_mode(int mode, int blocks, const TdecWinArgs& a, hipStream_t s)
 {
-  if constexpr (NSB == 16 && FULL && DIAG == 0) { // speculative DEC2 (tdec_win_spec_ok): decisions, no a-priori
-    if (a.dec && a.spec && mode == 2) {
+  if constexpr (NSB == 16 && FULL && DIAG == 0) { // speculative (tdec_win_spec_ok): decisions, no next-half input
+    if (a.dec && a.spec) {
       launch_mode_o<NSB, DIAG, FULL, 3>(mode, blocks, a, s);
       return;
     }

@@ -283,8 +283,7 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
     // the decide pass
     const bool fuse = g.L % 8 == 0 && out_stride % 8 == 0 && (uintptr_t)d_out % 8 == 0;
     for (uint32_t h = h0; h < h1; h++) {
-      if (rq.redo) { // DEC2 again, a-priori only, for the code blocks the check left unfinished
-        if (!(h & 1)) continue;
+      if (rq.redo) { // again, the next half-iteration's input only, for the code blocks the check left unfinished
         TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, rq.remaining, A1, E, D, CK, t->dstE, t->dstA,
                        (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, 0, nullptr, out_stride};
         CHECK_HIP(tdec_win_launch_halfit(g.nsb, wa, s));
@@ -293,7 +292,7 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
       TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, rq.remaining, A1, E, D, CK, t->dstE, t->dstA,
                      (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == h1,
                      (fuse && h + 1 == h1) ? d_out : nullptr, out_stride};
-      if (rq.spec && fuse && h + 1 == h1 && (h & 1) && tdec_win_spec_ok(g.nsb, g.L)) {
+      if (rq.spec && fuse && h + 1 == h1 && tdec_win_spec_ok(g.nsb, g.L)) {
         wa.spec = 1;
         if (rq.spec_taken) *rq.spec_taken = true;
       }
