@@ -208,10 +208,29 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
     acc[2] += e.x;
     acc[3] += e.y;
   }
-  // RSSI over the reference symbols (chest_dl_rssi :569-581)
-  for (uint32_t k = threadIdx.x; k < nsym * nre; k += blockDim.x) {
-    const uint32_t l = k / nre;
-    acc[1] += cpw(g[crs_nsymbol(l, a.nsymb, port) * nre + k % nre]);
+  // RSSI over the reference symbols (chest_dl_rssi :569-581): rows as 16-byte pieces (rows are 96 nof_prb bytes
+  // long), every row's loads issued before the sums
+  if (((uintptr_t)g & 15) == 0 && nsym == 4 && nre / 2 <= 3 * 256 && blockDim.x == 256) {
+    float4 v[4][3];
+#pragma unroll
+    for (uint32_t l = 0; l < 4; l++) {
+      const float4* r4 = (const float4*)(g + crs_nsymbol(l, a.nsymb, port) * nre);
+#pragma unroll
+      for (uint32_t u = 0; u < 3; u++) {
+        const uint32_t k = threadIdx.x + 256 * u;
+        v[l][u]          = k < nre / 2 ? r4[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (uint32_t l = 0; l < 4; l++)
+#pragma unroll
+      for (uint32_t u = 0; u < 3; u++)
+        acc[1] += v[l][u].x * v[l][u].x + v[l][u].y * v[l][u].y + (v[l][u].z * v[l][u].z + v[l][u].w * v[l][u].w);
+  } else {
+    for (uint32_t k = threadIdx.x; k < nsym * nre; k += blockDim.x) {
+      const uint32_t l = k / nre;
+      acc[1] += cpw(g[crs_nsymbol(l, a.nsymb, port) * nre + k % nre]);
+    }
   }
   block_sum<4>(acc, red); // includes the barrier that publishes pe[]
 
