@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <cmath>
 #include <map>
+#include <unordered_map>
 #include <mutex>
 #include <stdio.h>
 #include <string.h>
@@ -163,10 +164,11 @@ struct mi355_pdsch {
   uint32_t                             max_its = 10; // SRSLTE_PDSCH_MAX_TDEC_ITERS
   uint32_t*                            gold   = nullptr;
   std::map<std::string, MapEntry>      maps; // extraction maps in HBM
-  MapEntry                             last_map{};   // the previous lookup (key below)
-  uint32_t                             last_map_hdr[4]{};
-  uint8_t                              last_map_prb[2][MI355_MAX_PRB]{};
-  std::map<uint32_t, uint32_t*>        scr;  // packed descrambling sequences per c_init (HBM)
+  // the previous lookup per subframe index (key below): a batch of consecutive subframes cycles through them
+  MapEntry                             last_map[10]{};
+  uint32_t                             last_map_hdr[10][4]{};
+  uint8_t                              last_map_prb[10][2][MI355_MAX_PRB]{};
+  std::unordered_map<uint32_t, uint32_t*> scr; // packed descrambling sequences per c_init (HBM)
   char*                                scratch = nullptr;
   size_t                               scratch_cap = 0;
   std::vector<JobPlan>                 last; // plans of the last call (debug_stage)
@@ -204,12 +206,12 @@ static int get_scratch(mi355_pdsch_t* q, size_t bytes, char** p)
 
 static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi, uint32_t sf, MapEntry* out)
 {
-  // consecutive jobs of a batch usually share the allocation: compare with the previous lookup first
-  const uint32_t np = q->cell.nof_prb;
-  if (q->last_map.d && q->last_map_hdr[0] == cfi && q->last_map_hdr[1] == sf && q->last_map_hdr[2] == g.nof_symb_slot[0] &&
-      q->last_map_hdr[3] == g.nof_symb_slot[1] && !memcmp(q->last_map_prb[0], g.prb_idx[0], np) &&
-      !memcmp(q->last_map_prb[1], g.prb_idx[1], np)) {
-    *out = q->last_map;
+  // the jobs of a batch usually share the allocation: compare with the previous lookup of this subframe index first
+  const uint32_t np = q->cell.nof_prb, z = sf % 10;
+  const uint32_t* lh = q->last_map_hdr[z];
+  if (q->last_map[z].d && lh[0] == cfi && lh[1] == sf && lh[2] == g.nof_symb_slot[0] && lh[3] == g.nof_symb_slot[1] &&
+      !memcmp(q->last_map_prb[z][0], g.prb_idx[0], np) && !memcmp(q->last_map_prb[z][1], g.prb_idx[1], np)) {
+    *out = q->last_map[z];
     return MI355_SUCCESS;
   }
   std::string key;
@@ -224,7 +226,7 @@ static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi,
       CHECK_HIP(hipDeviceSynchronize());
       for (auto& kv : q->maps) (void)hipFree(kv.second.d);
       q->maps.clear();
-      q->last_map = MapEntry{};
+      for (auto& m : q->last_map) m = MapEntry{};
     }
     std::vector<uint16_t> idx;
     idx.reserve(14 * 12 * q->cell.nof_prb);
@@ -250,12 +252,12 @@ static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi,
     if (!all.empty()) CHECK_HIP(hipMemcpy(e.d, all.data(), all.size() * 2, hipMemcpyHostToDevice));
     it = q->maps.emplace(key, e).first;
   }
-  *out        = it->second;
-  q->last_map = it->second;
+  *out           = it->second;
+  q->last_map[z] = it->second;
   const uint32_t h[4] = {cfi, sf, g.nof_symb_slot[0], g.nof_symb_slot[1]};
-  memcpy(q->last_map_hdr, h, sizeof(h));
-  memcpy(q->last_map_prb[0], g.prb_idx[0], np);
-  memcpy(q->last_map_prb[1], g.prb_idx[1], np);
+  memcpy(q->last_map_hdr[z], h, sizeof(h));
+  memcpy(q->last_map_prb[z][0], g.prb_idx[0], np);
+  memcpy(q->last_map_prb[z][1], g.prb_idx[1], np);
   return MI355_SUCCESS;
 }
 
