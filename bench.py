@@ -379,7 +379,7 @@ def Tm4Source(cell, n_max, device, ctrl=False, chunk=256):
 
 def Tm4Rx(cell, B, device, ctrl=False):
     """The UE side of one TM4 batch of B subframes (srsran_amd.synth.DlReceiver); the AVERAGE estimate is written to
-    row 0 only (mi355_chest_dl_cfg_t.ce_rows = 1: the fused chain reads nothing else)."""
+    row 0 only (mi355_ue_dl_set_ce_rows(1): the fused chain reads nothing else)."""
     from srsran_amd.synth import DlReceiver
     return DlReceiver(cell, 2, B, NB, device, ctrl=ctrl, max_cb=16, ce_rows=1)
 

@@ -48,11 +48,6 @@ typedef struct {
   uint32_t cfo_estimate_enable;
   uint32_t sync_error_enable;
   uint32_t cfo_estimate_sf_mask; /* subframes (bit tti % 10) in which the CFO is estimated (chest_dl.c:635) */
-  /* Estimate rows written by the batched decode calls (mi355_ue_dl_decode_batch, mi355_ue_dl_find_and_decode_batch)
-   * with the AVERAGE estimator, whose estimate is the same in every OFDM symbol: 0 = every row, as
-   * srslte_chest_dl_estimate promises (chest_dl.c:490-494); 1 = row 0 only (the chain reads nothing else: 14x fewer
-   * estimate bytes).  The standalone estimate calls always write every row.  Not part of srslte_chest_dl_cfg_t. */
-  uint32_t ce_rows;
 } mi355_chest_dl_cfg_t;
 
 /* srslte_chest_dl_res_t scalars (chest_dl.h:50-68); ce pointers live in the job */
@@ -107,6 +102,13 @@ int mi355_ue_dl_set_standard_rates(mi355_ue_dl_t* q, int enable);
 /* find_and_decode's pipelining: number of chunks a batch is split into (1..8; 0 = automatic, 2 from 256 subframes).
  * Results do not depend on it (subframes are independent); tests and A/B timing set it. */
 int mi355_ue_dl_set_chunks(mi355_ue_dl_t* q, uint32_t nof_chunks);
+
+/* Estimate rows written by the batched decode calls (mi355_ue_dl_decode_batch, mi355_ue_dl_find_and_decode_batch)
+ * with the AVERAGE estimator, whose estimate is the same in every OFDM symbol: 0 = every row (the default), as
+ * srslte_chest_dl_estimate promises (chest_dl.c:490-494); 1 = row 0 only (the chain reads nothing else: 14x fewer
+ * estimate bytes).  The standalone estimate calls always write every row.  A setter, not a field of
+ * mi355_chest_dl_cfg_t, so that struct keeps its layout. */
+int mi355_ue_dl_set_ce_rows(mi355_ue_dl_t* q, uint32_t ce_rows);
 
 /* Zero one link's estimator state (srslte_chest_dl_init / set_cell). */
 int mi355_ue_dl_reset_link(mi355_ue_dl_t* q, uint32_t link);

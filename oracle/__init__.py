@@ -71,6 +71,8 @@ def lib() -> C.CDLL:
         L.orc_pdsch_re_map.restype = C.c_uint32
         L.orc_pdsch_re_map.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_uint32,
                                        C.c_uint32, u8p, C.c_uint32, C.c_uint32, u32p]
+        L.orc_chest_filter.restype = C.c_uint32
+        L.orc_chest_filter.argtypes = [C.c_int, C.c_float, C.c_float, C.c_float, f32p]
         L.orc_crs_pilots.argtypes = [C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, f32p]
         L.orc_chest_estimate_port.argtypes = [f32p, C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, C.c_int,
                                               C.c_float, C.c_float, C.c_int, f32p, f32p]
@@ -192,6 +194,13 @@ def ref() -> C.CDLL:
         L.ref_predecoding.argtypes = [C.c_void_p] * 10 + [C.c_int] * 6 + [C.c_float, C.c_float, C.c_int]
         L.ref_front_predecode.argtypes = [f32p, f32p] + [C.c_int] * 6 + [C.c_float, C.c_float, f32p, f32p, f32p]
         L.ref_front_scramble_s.argtypes = [C.c_uint32, i16p, C.c_int]
+        L.ref_pdsch_get_map.restype = C.c_int
+        L.ref_pdsch_get_map.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
+                                        u8p, C.c_uint32, C.c_uint32, u32p]
+        L.ref_chest_filter.restype = C.c_uint32
+        L.ref_chest_filter.argtypes = [C.c_int, C.c_uint32, C.c_float, C.c_float, f32p]
+        L.ref_chest_noise_pilots.restype = C.c_float
+        L.ref_chest_noise_pilots.argtypes = [f32p, f32p, f32p, C.c_uint32]
         _REF = L
     return _REF
 
@@ -416,6 +425,52 @@ def ref_predecode(y: np.ndarray, h: np.ndarray, nof_layers: int, cb: int, tx_sch
         raise ValueError("ref_predecoding failed")
     nl = n // nof_ports if tx_scheme == 1 else n
     return np.stack(x)[:nof_layers, :nl].copy(), np.stack(csi)
+
+
+def chest_filter(filter_type: int, coef0: float, coef1: float, noise: float = 0.0) -> np.ndarray:
+    """orc_chest_filter: the estimator's smoothing taps (Gauss / 3-tap / none) as chest_dl.c sets them up."""
+    f = np.zeros(32, np.float32)
+    n = lib().orc_chest_filter(filter_type, coef0, coef1, noise, f)
+    return f[:n].copy()
+
+
+def ref_chest_filter(kind: int, order: int, sigma: float = 0.0, w: float = 0.0) -> np.ndarray:
+    """chest_common.c compiled from the reference (oracle/_ref): 0 Gauss(order, sigma), 1 3-tap(w), 2 triangle."""
+    f = np.zeros(64, np.float32)
+    n = ref().ref_chest_filter(kind, order, sigma, w, f)
+    return f[:n].copy()
+
+
+def ref_pdsch_re_map(nof_prb: int, nof_ports: int, cell_id: int, prb: np.ndarray, lstart: int, sf_idx: int,
+                     tdd: bool = False, cp_ext: bool = False, nof_symb_slot=(0, 0)) -> np.ndarray:
+    """The RE -> grid map in extraction order through the reference's compiled prb_dl.c primitives
+    (oracle/ref/ref_prb.c); same arguments as pdsch_re_map()."""
+    prb = np.ascontiguousarray(np.asarray(prb, np.uint8).reshape(2, nof_prb))
+    idx = np.zeros(14 * 12 * nof_prb, np.uint32)
+    n = ref().ref_pdsch_get_map(nof_prb, nof_ports, cell_id, int(tdd), int(cp_ext), nof_symb_slot[0],
+                                nof_symb_slot[1], prb, lstart, sf_idx, idx)
+    if n < 0:
+        raise ValueError("ref_pdsch_get_map: invalid configuration")
+    return idx[:n].copy()
+
+
+def ref_predecode_scalar(y: np.ndarray, h: np.ndarray, nof_layers: int, cb: int, tx_scheme: int, scaling: float,
+                         noise: float):
+    """The reference's srslte_predecoding_type on chunks shorter than one AVX2 vector (8 complex values), so every RE
+    takes the scalar bodies (precoding.c:309-357 single_csi tail, :1519-1548 2x2 MMSE tail -> mat.c:63-109,
+    :1802-1820 2x1 MRC tail, the diversity / CDD tails): the exact-division path, independent of the host CPU's
+    rcp_ps.  Same layout as predecode(); chunks are whole SFBC groups (4 REs for 4 ports, else 6)."""
+    y = np.ascontiguousarray(y, np.complex64)
+    n = y.shape[1]
+    nof_ports = h.shape[0]
+    ch = 4 if (tx_scheme == 1 and nof_ports == 4) else 6
+    xs, cs = [], []
+    for a in range(0, n, ch):
+        b = min(n, a + ch)
+        x, c = ref_predecode(y[:, a:b], h[:, :, a:b], nof_layers, cb, tx_scheme, scaling, noise)
+        xs.append(x)
+        cs.append(c[:, : b - a])
+    return np.concatenate(xs, 1), np.concatenate(cs, 1)
 
 
 def pdsch_c_init(rnti: int, cw: int, sf: int, cell_id: int) -> int:

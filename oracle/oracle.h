@@ -41,6 +41,7 @@ void orc_csi_correction_s(int qm, int16_t* e, const float* csi, uint32_t nof_bit
 uint32_t orc_pdsch_re_map(uint32_t nof_prb, uint32_t nof_ports, uint32_t cell_id, int tdd, int cp_ext,
                           uint32_t ns0, uint32_t ns1, const uint8_t* prb, uint32_t lstart_grant, uint32_t sf_idx,
                           uint32_t* idx);
+uint32_t orc_chest_filter(int filter_type, float coef0, float coef1, float noise, float* filt);
 void orc_crs_pilots(uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t p, uint32_t sf, float* out);
 int  orc_chest_estimate_port(const float* grid, uint32_t nof_prb, uint32_t cell_id, int cp_ext, uint32_t sf,
                              uint32_t port, int filter_type, float coef0, float coef1, int estimator_alg, float* ce,

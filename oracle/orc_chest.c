@@ -182,6 +182,33 @@ static float noise_refs(const cf* pe, uint32_t nsymbols, uint32_t nref, uint32_t
   return sum_power / (float)count * sqrtf(weight + 4.0f);
 }
 
+/* The smoothing filter chest_dl.c sets up for filter_type (:431-446): 0 Gauss (srslte_chest_set_smooth_filter_gauss,
+ * chest_common.c:70-88: order coef0, sigma coef1, or order 4 and sigma 200 x noise when coef0 <= 0; taps normalised by
+ * their sum, multiplied by its reciprocal), 1 the 3-tap (w, 1 - 2w, w) of srslte_chest_set_smooth_filter3_coeff
+ * (:62-68) with w = coef0, 2 none (length 0).  Returns the filter length. */
+uint32_t orc_chest_filter(int filter_type, float coef0, float coef1, float noise, float* filt)
+{
+  if (filter_type == 0) {
+    const uint32_t order = coef0 <= 0 ? 4 : (uint32_t)coef0;
+    const float    sd    = coef0 <= 0 ? noise * 200.0f : coef1;
+    const uint32_t flen  = order + 1;
+    const int      c     = (int)(flen - 1) / 2;
+    float          nrm   = 0;
+    for (int i = 0; i < (int)flen; i++) {
+      filt[i] = expf(-powf((float)(i - c), 2) / (2.0f * powf(sd, 2)));
+      nrm += filt[i];
+    }
+    for (uint32_t i = 0; i < flen; i++) filt[i] *= 1.0f / nrm;
+    return flen;
+  }
+  if (filter_type == 1) {
+    filt[0] = filt[2] = coef0;
+    filt[1]           = 1 - 2 * coef0;
+    return 3;
+  }
+  return 0;
+}
+
 /* One (rx antenna, port) estimate_port call.  grid: nsymb*2 x 12*nof_prb cf.  cfg: filter_type (0 gauss,
  * 1 triangle, 2 none), coef0/coef1 (filter_coef), estimator_alg (0 average, 1 interpolate).  ce: full grid
  * output (INTERPOLATE with 2 pilot symbols -- ports 2, 3 -- copies the buffer's row 0, which it never writes,
@@ -234,24 +261,8 @@ int orc_chest_estimate_port_st(const float* grid_f, uint32_t nof_prb, uint32_t c
   rssi /= (float)nsym;
   const float noise = noise_alg == 0 ? noise_refs(pe, nsym, nref, crs_fidx(cell_id, 0, port)) : noise_state;
 
-  float    filt[16];
-  uint32_t flen = 0;
-  if (filter_type == 0) {
-    const uint32_t order = coef0 <= 0 ? 4 : (uint32_t)coef0;
-    const float    sd    = coef0 <= 0 ? noise * 200.0f : coef1;
-    flen                 = order + 1;
-    const int c          = (int)(flen - 1) / 2;
-    float     nrm        = 0;
-    for (int i = 0; i < (int)flen; i++) {
-      filt[i] = expf(-powf((float)(i - c), 2) / (2.0f * powf(sd, 2)));
-      nrm += filt[i];
-    }
-    for (uint32_t i = 0; i < flen; i++) filt[i] *= 1.0f / nrm;
-  } else if (filter_type == 1) {
-    filt[0] = filt[2] = coef0;
-    filt[1]           = 1 - 2 * coef0;
-    flen              = 3;
-  }
+  float          filt[16];
+  const uint32_t flen = orc_chest_filter((int)filter_type, coef0, coef1, noise, filt);
 
   const cf* src = pe;
   uint32_t  nr  = nref;

@@ -276,6 +276,14 @@ int orc_ue_dl_front(const orc_front_cfg_t* c, const float* const* iq, int16_t* c
   if (stages.predecode((const float*)ys, (const float*)hs, R, P, c->nof_layers, c->cb, nre, c->scheme, scaling,
                        c->mmse ? noise : 0.0f, (float*)x, csi, csi + cst) < 0)
     return -1;
+  if (c->scheme == 1) { /* transmit diversity: srslte_layerdemap_diversity (layermap.c:139-148), d[L i + l] = x[l][i] */
+    cfl*           d = amalloc(sizeof(cfl) * nre * 2);
+    const uint32_t L = c->nof_layers, m = nre / L;
+    for (uint32_t l = 0; l < L; l++)
+      for (uint32_t i = 0; i < m; i++) d[(size_t)L * i + l] = x[(size_t)l * nre + i];
+    free(x);
+    x = d;
+  }
   for (uint32_t t = 0; t < c->nof_tb; t++) {
     const uint32_t qm = c->qm[t];
     stages.demod_soft_s(qm, (const float*)&x[(size_t)t * nre], e[t], nre);

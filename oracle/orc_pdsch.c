@@ -431,7 +431,7 @@ int orc_predecode(const float* yf, const float* hf, int nof_rx, int nof_ports, i
           const float c  = h[0].re * h[0].re + h[0].im * h[0].im + h[1].re * h[1].re + h[1].im * h[1].im;
           const float hh = norm / c;
           X(0, i)        = cscale(cadd(cmul(cconj(h[0]), Y(0, i)), cmul(cconj(h[1]), Y(1, i))), hh);
-          csi0[i]        = (float)(c / norm * M_SQRT1_2);
+          csi0[i]        = c / norm * (float)M_SQRT1_2; /* all float, as precoding.c:1819 */
         }
         return 0;
       }

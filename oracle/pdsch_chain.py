@@ -237,8 +237,9 @@ def rho_b_mask(cfg: Cfg) -> tuple[np.ndarray, float]:
     return sc, scaling
 
 
-def rx_front(cfg: Cfg, y: np.ndarray, ce: np.ndarray, noise: float):
-    """Everything of srslte_pdsch_decode up to the DL-SCH: returns (d[cw], csi[cw], e[tb])."""
+def rx_front(cfg: Cfg, y: np.ndarray, ce: np.ndarray, noise: float, predecoder=None):
+    """Everything of srslte_pdsch_decode up to the DL-SCH: returns (d[cw], csi[cw], e[tb]).  predecoder replaces the
+    oracle's equaliser (oracle.ref_predecode_scalar: the compiled reference's scalar path, tests only)."""
     idx = pdsch_re_map(cfg.nof_prb, cfg.nof_ports, cfg.cell_id, cfg.prb_mask(), cfg.lstart, cfg.sf_idx)
     nre = idx.size
     sc, scaling = rho_b_mask(cfg)
@@ -246,7 +247,7 @@ def rx_front(cfg: Cfg, y: np.ndarray, ce: np.ndarray, noise: float):
     ys = (y[:, idx] * sc[idx // row][None, :]).astype(np.complex64)
     hs = ce[:, :, idx]
     nz = noise if cfg.mmse else 0.0
-    x, csi = predecode(ys, hs, cfg.nof_layers, cfg.codebook(), cfg.scheme, scaling, nz)
+    x, csi = (predecoder or predecode)(ys, hs, cfg.nof_layers, cfg.codebook(), cfg.scheme, scaling, nz)
     d = [np.zeros(nre, np.complex64), np.zeros(nre, np.complex64)]
     if cfg.scheme == DIVERSITY:
         L = cfg.nof_layers

@@ -9,6 +9,7 @@
 #include <complex.h>
 #include <pthread.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "srslte/phy/common/sequence.h"
@@ -35,10 +36,11 @@ int ref_front_predecode(const float* y, const float* h, int nof_rx, int nof_port
 }
 
 #define SEQ_SLOTS 64
+/* sequences are heap objects handed out by pointer and never freed: a slot that is replaced (past 64 distinct c_init)
+ * leaks its old sequence, because another front_worker thread may still be scrambling through it */
 static struct {
-  uint32_t          c_init;
-  int               used;
-  srslte_sequence_t seq;
+  uint32_t           c_init;
+  srslte_sequence_t* seq;
 } seqs[SEQ_SLOTS];
 static pthread_mutex_t seq_mu = PTHREAD_MUTEX_INITIALIZER;
 
@@ -47,17 +49,20 @@ int ref_front_scramble_s(uint32_t c_init, int16_t* llr, int len)
   srslte_sequence_t* s = NULL;
   pthread_mutex_lock(&seq_mu);
   for (int i = 0; i < SEQ_SLOTS && !s; i++)
-    if (seqs[i].used && seqs[i].c_init == c_init && seqs[i].seq.cur_len >= (uint32_t)len) s = &seqs[i].seq;
+    if (seqs[i].seq && seqs[i].c_init == c_init && seqs[i].seq->cur_len >= (uint32_t)len) s = seqs[i].seq;
   if (!s) { /* a free slot (a batch has few distinct c_init: rnti, codeword, subframe); full: replace one */
     int k = -1;
     for (int i = 0; i < SEQ_SLOTS && k < 0; i++)
-      if (!seqs[i].used) k = i;
+      if (!seqs[i].seq) k = i;
     if (k < 0) k = (int)((c_init >> 9) % SEQ_SLOTS);
-    if (seqs[k].used) srslte_sequence_free(&seqs[k].seq); /* (only past 64 distinct sequences) */
-    memset(&seqs[k].seq, 0, sizeof(seqs[k].seq));
-    seqs[k].used   = srslte_sequence_LTE_pr(&seqs[k].seq, 8 * 14 * 1200, c_init) == 0;
-    seqs[k].c_init = c_init;
-    s              = seqs[k].used ? &seqs[k].seq : NULL;
+    srslte_sequence_t* n = calloc(1, sizeof(*n));
+    if (n && srslte_sequence_LTE_pr(n, 8 * 14 * 1200, c_init) == 0) {
+      seqs[k].seq    = n;
+      seqs[k].c_init = c_init;
+      s              = n;
+    } else {
+      free(n);
+    }
   }
   pthread_mutex_unlock(&seq_mu);
   if (!s) return -1;

@@ -202,16 +202,14 @@ static int crc_scales(mi355_dlsch_t* q, uint32_t K, const uint32_t** out)
 }
 
 // the TB epilogue's CRC24A of nbytes bytes by 256 threads (block_crc24_scaled4): thread t's factor
-// x^(8 * bytes after its chunk) mod P, chunk = ceil(nbytes / 256) rounded up to a word
+// x^(8 * bytes after its chunk) mod P, chunk = ceil(nbytes / 256) rounded up to a word.  Tables are never evicted:
+// descriptors planned earlier in the same call hold their pointers, and the cache is bounded by the distinct TB
+// byte counts a decoder ever sees (1 KB each; every size up to the largest TBS would be 48 MB, the LTE tables' 190
+// distinct sizes 190 KB).
 static int tb_crc_scales(mi355_dlsch_t* q, uint32_t nbytes, const uint32_t** out)
 {
   auto it = q->tb_scales.find(nbytes);
   if (it == q->tb_scales.end()) {
-    if (q->tb_scales.size() >= 512) { // bounded: distinct TB sizes
-      CHECK_HIP(hipDeviceSynchronize());
-      for (auto& kv : q->tb_scales) (void)hipFree(kv.second);
-      q->tb_scales.clear();
-    }
     std::vector<uint32_t> t(256);
     const uint32_t        chunk = ((nbytes + 255) / 256 + 3) / 4 * 4, poly = 0x1864CFB;
     for (uint32_t tid = 0; tid < 256; tid++) {

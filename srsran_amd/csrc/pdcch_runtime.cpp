@@ -215,10 +215,23 @@ int CtrlState::finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_c
   const float*    h_corr = (const float*)(back->host + b_cfi_);
   const DciHits*  h_hits = (const DciHits*)(back->host + b_cfi_ + b_corr_);
   constexpr uint32_t NC  = PDCCH_SLOTS * PDCCH_FMTS;
-  std::atomic<int>   err{0};
   // MI355_PDCCH_HMAX (tests): treat records with more matches than this as overflowing (0: always the full path)
   const char*        he   = getenv("MI355_PDCCH_HMAX");
   const uint32_t     hmax = he ? std::min<uint32_t>((uint32_t)atoi(he), PDCCH_HMAX) : PDCCH_HMAX;
+  // subframes with more matches than their record holds: their whole candidate arrays, in one batch of copies on
+  // the read-back stream (ordered behind the chunk's kernels by ev[chunk]), not on the null stream, which would
+  // serialise against the PDSCH / DL-SCH work the caller has already enqueued
+  std::vector<uint32_t> ovf_of;
+  std::vector<DciCand>  ovf;
+  for (uint32_t i = b; i < e; i++)
+    if (h_hits[i].n > hmax) ovf_of.push_back(i);
+  if (!ovf_of.empty()) {
+    ovf.resize(ovf_of.size() * NC);
+    for (size_t k = 0; k < ovf_of.size(); k++)
+      CHECK_HIP(hipMemcpyAsync(ovf.data() + k * NC, last_cand + (size_t)ovf_of[k] * NC, NC * sizeof(DciCand),
+                               hipMemcpyDeviceToHost, rb));
+    CHECK_HIP(hipStreamSynchronize(rb));
+  }
   host_parallel_for(e - b, 128, [&](uint32_t lo, uint32_t hi) { // subframes are independent
     DciCand cand[NC];
     for (uint32_t i = b + lo; i < b + hi; i++) {
@@ -229,10 +242,8 @@ int CtrlState::finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_c
       // the replay's view of the candidates: the matching ones, everything else "not decoded"
       const DciHits& H = h_hits[i];
       if (H.n > hmax) { // more matches than the record holds: the subframe's whole candidate array
-        if (hipMemcpy(cand, last_cand + (size_t)i * NC, sizeof(cand), hipMemcpyDeviceToHost) != hipSuccess) {
-          err = 1;
-          continue;
-        }
+        const size_t k = std::lower_bound(ovf_of.begin(), ovf_of.end(), i) - ovf_of.begin();
+        memcpy(cand, ovf.data() + k * NC, sizeof(cand));
       } else {
         memset(cand, 0, sizeof(cand));
         for (uint32_t k = 0; k < H.n; k++) {
@@ -246,7 +257,6 @@ int CtrlState::finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_c
                                            msgs + (size_t)i * MI355_MAX_DCI_MSG);
     }
   });
-  if (err) return MI355_ERROR;
   if (prof)
     fprintf(stderr, "[mi355 host] control stage: blind-search replay %.1f us for %u subframes\n",
             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tr0).count(), e - b);

@@ -211,7 +211,7 @@ __device__ __forceinline__ void eq_one(const PdschJobDev& J, uint32_t u, float n
           const float c  = h[0].re * h[0].re + h[0].im * h[0].im + h[1].re * h[1].re + h[1].im * h[1].im;
           const float hh = norm / c;
           st(d0, i, (cj(h[0]) * Y(0, i) + cj(h[1]) * Y(1, i)) * hh);
-          const float cv = (float)((double)(c / norm) * 0.70710678118654752);
+          const float cv = c / norm * (float)0.70710678118654752 /* _csi / norm * (float)M_SQRT1_2, all float (precoding.c:1819) */;
           csi0[i]    = cv;
           m0             = bmax(m0, cv);
         }
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) void pdsch_equalize(const PdschJobDev* __restr
         const float c  = h[0].re * h[0].re + h[0].im * h[0].im + h[1].re * h[1].re + h[1].im * h[1].im;
         const float hh = norm / c;
         st(d0, i, (cj(h[0]) * Y[k][0] + cj(h[1]) * Y[k][1]) * hh);
-        const float cv = (float)((double)(c / norm) * 0.70710678118654752);
+        const float cv = c / norm * (float)0.70710678118654752 /* _csi / norm * (float)M_SQRT1_2, all float (precoding.c:1819) */;
         csi0[i]        = cv;
         m0             = bmax(m0, cv);
       } else { // ccd_2x2_mmse_csi (precoding.c:1111-1128)
@@ -796,7 +796,7 @@ __device__ __forceinline__ void csi_of(const PdschJobDev& J, const cf (&H)[4], f
       h[r] = J.cb == 0 ? a + b : J.cb == 1 ? a - b : J.cb == 2 ? a + mulj(b) : a - mulj(b);
     }
     const float c = h[0].re * h[0].re + h[0].im * h[0].im + h[1].re * h[1].re + h[1].im * h[1].im;
-    c0            = (float)((double)(c / norm) * 0.70710678118654752);
+    c0            = c / norm * (float)0.70710678118654752 /* _csi / norm * (float)M_SQRT1_2, all float (precoding.c:1819) */;
     c1            = 0.f;
   }
 }
@@ -886,7 +886,7 @@ __device__ __forceinline__ void eq_re(const PdschJobDev& J, const cf (&h)[4], co
     const float c  = hv[0].re * hv[0].re + hv[0].im * hv[0].im + hv[1].re * hv[1].re + hv[1].im * hv[1].im;
     const float hh = norm / c;
     x0 = (cj(hv[0]) * y[0] + cj(hv[1]) * y[1]) * hh;
-    c0 = (float)((double)(c / norm) * 0.70710678118654752);
+    c0 = c / norm * (float)0.70710678118654752 /* _csi / norm * (float)M_SQRT1_2, all float (precoding.c:1819) */;
     x1 = mk(0.f, 0.f);
     c1 = 0.f;
   }

@@ -79,6 +79,7 @@ struct mi355_ue_dl {
   CtrlState*     ctrl     = nullptr;       // PCFICH / PDCCH stage, built on first use
   std::vector<std::unique_ptr<mi355::PdschPending>> pend; // find_and_decode: per chunk, decodes left in flight
   uint32_t       chunks = 0;                              // find_and_decode chunk count (0: automatic)
+  uint32_t       ce_rows = 0;                             // batched calls: 1 = AVERAGE estimate row 0 only (set_ce_rows)
   // find_and_decode's host arrays, kept from call to call: a batch's replay and grant building then write into
   // memory already mapped (1.5 MB of DCI messages and ~1 MB of job descriptors per 2,048 subframes otherwise newly
   // allocated, their first-touch page faults on the host's critical path between the chunks)
@@ -574,6 +575,14 @@ int mi355_ue_dl_set_chunks(mi355_ue_dl_t* q, uint32_t nof_chunks)
   return MI355_SUCCESS;
 }
 
+int mi355_ue_dl_set_ce_rows(mi355_ue_dl_t* q, uint32_t ce_rows)
+{
+  if (!q || ce_rows > 1) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  q->ce_rows = ce_rows;
+  return MI355_SUCCESS;
+}
+
 int mi355_ue_dl_reset_link(mi355_ue_dl_t* q, uint32_t link)
 {
   if (!q || link >= MI355_MAX_LINKS) return MI355_ERROR_INVALID_INPUTS;
@@ -636,7 +645,7 @@ int mi355_ue_dl_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, co
   int         r    = ofdm_run(q, sfjobs, njobs, s, &used);
   if (r) return r;
   float *d_out = nullptr, *d_noise = nullptr;
-  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise, chest_cfg->ce_rows == 1))) return r;
+  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise, q->ce_rows == 1))) return r;
   // the PDSCH jobs are planned on the host while the GPU demodulates and estimates
   std::vector<mi355_pdsch_job_t> jobs(njobs);
   for (uint32_t i = 0; i < njobs; i++) {
@@ -780,7 +789,7 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
   if ((r = ofdm_run(q, sfjobs, njobs, s, &used, defer))) return r;
   if (defer && (r = ofdm_launch_range(q, 0, end0, s))) return r;
   float *d_out = nullptr, *d_noise = nullptr;
-  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise, chest_cfg->ce_rows == 1, defer)))
+  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise, q->ce_rows == 1, defer)))
     return r;
   if (defer && (r = chest_launch_range(q, 0, end0, s))) return r;
   ChestFill fill{q, chest_cfg, nullptr, sfjobs, njobs, chest, false};

@@ -159,7 +159,8 @@ class DlReceiver:
         self.pool = SoftbufferPool(2 * B, max_cb=max_cb, device=device)
         self.ue = UeDl(cell, nof_rx, device)
         self.chest_cfg = default_chest_cfg()
-        self.chest_cfg.ce_rows = ce_rows  # 1: the AVERAGE estimate's row 0 only (the chain reads nothing else)
+        self.ce_rows = ce_rows  # 1: the AVERAGE estimate's row 0 only (the chain reads nothing else)
+        self.ue.set_ce_rows(ce_rows)
         self.L = _declare()
         self.L.mi355_softbuffer_reset_range.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
         self.chest = (ChestRes * B)()

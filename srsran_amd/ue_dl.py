@@ -18,7 +18,7 @@ MAX_LINKS = 65536
 class ChestCfg(C.Structure):
     _fields_ = [("estimator_alg", C.c_uint32), ("noise_alg", C.c_uint32), ("filter_type", C.c_uint32),
                 ("filter_coef", C.c_float * 2), ("rsrp_neighbour", C.c_uint32), ("cfo_estimate_enable", C.c_uint32),
-                ("sync_error_enable", C.c_uint32), ("cfo_estimate_sf_mask", C.c_uint32), ("ce_rows", C.c_uint32)]
+                ("sync_error_enable", C.c_uint32), ("cfo_estimate_sf_mask", C.c_uint32)]
 CE_ROWS_ALL, CE_ROWS_FIRST = 0, 1
 
 
@@ -58,6 +58,7 @@ def _declare():
     L.mi355_ue_dl_set_standard_rates.argtypes = [vp, i32]
     L.mi355_ue_dl_reset_link.argtypes = [vp, u32]
     L.mi355_ue_dl_set_chunks.argtypes = [vp, u32]
+    L.mi355_ue_dl_set_ce_rows.argtypes = [vp, u32]
     L.mi355_ofdm_rx_batch.argtypes = [vp, C.POINTER(DlSfJob), u32, vp]
     L.mi355_chest_dl_estimate_batch.argtypes = [vp, C.POINTER(DlSfJob), u32, C.POINTER(ChestCfg),
                                                 C.POINTER(ChestRes), vp]
@@ -97,6 +98,10 @@ class UeDl:
     def set_chunks(self, n: int):
         """find_and_decode's chunk count (0 = automatic)."""
         check(self.L.mi355_ue_dl_set_chunks(self.h, n), "set_chunks")
+
+    def set_ce_rows(self, n: int):
+        """Estimate rows the batched decode calls write (CE_ROWS_ALL / CE_ROWS_FIRST)."""
+        check(self.L.mi355_ue_dl_set_ce_rows(self.h, n), "set_ce_rows")
 
     def reset_link(self, link: int):
         check(self.L.mi355_ue_dl_reset_link(self.h, link), "reset_link")

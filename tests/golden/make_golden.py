@@ -27,6 +27,13 @@ Contents
                      saturating amplitudes), srslte_scrambling_s_offset (PDSCH c_init), and
                      srslte_predecoding_type with CSI (AVX2 build, MMSE) for every scheme srslte_pdsch_decode
                      uses -- the equaliser output is pinned within the reference's rcp tolerance.
+  ref_pins.npz       (``make_golden.py pins``) the reference's scalar equaliser path over full 100-PRB vectors
+                     (srslte_predecoding_type on chunks shorter than one AVX2 vector: precoding.c scalar tails,
+                     mat.c:63-109) for SISO 1/2 rx, SFBC 2 ports 1/2 rx, TM4 2x2 codebooks 0-2, 2x1 MRC codebooks
+                     0-3 and CDD, MMSE and ZF, inputs regenerated from their seeds (input SHA-256 recorded), outputs
+                     as SHA-256 plus their first 64 values; the PDSCH RE -> grid map through the compiled prb_dl.c
+                     primitives (oracle/ref/ref_prb.c) for 6-110 PRB x 1/2/4 ports x CFI 1-3 x subframes x FDD/TDD
+                     (SHA-256 per case); and the estimator's smoothing filters from the compiled chest_common.c.
 """
 from __future__ import annotations
 
@@ -321,6 +328,73 @@ def gen_pdsch_stages(rng):
     print("pdsch_stages.npz:", data["demod_n"], "demod,", data["scr_n"], "scrambling,", k, "predecoding cases")
 
 
+PIN_N = 14400  # PDSCH REs of a full-allocation 100-PRB 2-port subframe, CFI 1, no PBCH / sync (sf 1)
+
+
+def pin_inputs(seed: int, scheme: int, ports: int, rx: int, n: int):
+    """Inputs of one equaliser pin case (regenerated by tests/test_ref_pins.py from the same seed)."""
+    rng = np.random.default_rng(seed)
+    y = ((rng.standard_normal((rx, n)) + 1j * rng.standard_normal((rx, n))) / np.sqrt(2)).astype(np.complex64)
+    h = ((rng.standard_normal((ports, rx, n)) + 1j * rng.standard_normal((ports, rx, n))) / np.sqrt(2)).astype(
+        np.complex64)
+    return y, h
+
+
+# (scheme, ports, rx, layers, codebook, scaling, noise): every srslte_predecoding_type branch srslte_pdsch_decode takes
+PIN_CASES = [(0, 1, 1, 1, 0, 1.0, 0.01), (0, 1, 2, 1, 0, 0.8, 0.03), (0, 1, 2, 1, 0, 1.0, 0.0),
+             (1, 2, 1, 2, 0, 1.0, 0.0), (1, 2, 2, 2, 0, 0.7079, 0.0),
+             (2, 2, 2, 2, 0, 1.0, 0.02), (2, 2, 2, 2, 1, 1.0, 0.02), (2, 2, 2, 2, 2, 0.8, 0.05),
+             (2, 2, 2, 2, 1, 1.0, 0.0),
+             (2, 2, 2, 1, 0, 1.0, 0.02), (2, 2, 2, 1, 1, 1.0, 0.02), (2, 2, 2, 1, 2, 1.0, 0.02),
+             (2, 2, 2, 1, 3, 0.8, 0.02), (3, 2, 2, 2, 0, 1.0, 0.02)]
+
+# RE map pins: (nof_prb, ports, cell_id, cfi, sf, tdd, allocation seed or -1 for full)
+PIN_MAPS = [(p, a, c, f, s, t, -1 if k % 2 == 0 else k)
+            for k, (p, a, c, f, s, t) in enumerate(
+                (p, a, c, f, s, t) for p in (6, 7, 15, 25, 27, 50, 75, 100, 110) for a in (1, 2, 4)
+                for c in (0, 1, 2, 5, 301) for f in (1, 2, 3) for s in (0, 1, 5, 6) for t in (0, 1))]
+
+
+def pin_alloc(nof_prb: int, seed: int) -> np.ndarray:
+    if seed < 0:
+        return np.ones((2, nof_prb), np.uint8)
+    prb = (np.random.default_rng(seed).random(nof_prb) < 0.6).astype(np.uint8)
+    return np.stack([prb, prb])
+
+
+def sha(a: np.ndarray) -> str:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def gen_ref_pins():
+    data = {}
+    for k, (scheme, ports, rx, layers, cb, scaling, noise) in enumerate(PIN_CASES):
+        y, h = pin_inputs(9000 + k, scheme, ports, rx, PIN_N)
+        x, csi = oracle.ref_predecode_scalar(y, h, layers, cb, scheme, scaling, noise)
+        used = 2 if (layers == 2 and scheme >= 2) else 1
+        data[f"eq{k}_in_sha"] = np.array(sha(y) + sha(h))
+        data[f"eq{k}_x_sha"] = np.array(sha(x))
+        data[f"eq{k}_csi_sha"] = np.array(sha(csi[:used]))
+        data[f"eq{k}_x_head"] = x[:, :64].copy()
+        data[f"eq{k}_csi_head"] = csi[:used, :64].copy()
+    data["eq_n"] = np.int32(len(PIN_CASES))
+    shas = []
+    for (nof_prb, ports, cid, cfi, sf, tdd, seed) in PIN_MAPS:
+        m = oracle.ref_pdsch_re_map(nof_prb, ports, cid, pin_alloc(nof_prb, seed), cfi + (nof_prb < 10), sf,
+                                    tdd=bool(tdd))
+        shas.append(np.frombuffer(bytes.fromhex(sha(m.astype(np.uint32))), np.uint8))
+    data["map_sha"] = np.stack(shas)  # (cases, 32) SHA-256 digests
+    # smoothing filters: Gauss order 1..14 x sigma, 3-tap w, triangle lengths
+    for order in range(1, 15):
+        for j, sd in enumerate((0.1, 0.5, 1.0, 2.0, 3.7, 10.0)):
+            data[f"gauss{order}_{j}"] = oracle.ref_chest_filter(0, order, sd)
+    for j, w in enumerate((0.0, 0.1, 0.25, 0.3333)):
+        data[f"tri3_{j}"] = oracle.ref_chest_filter(1, 3, 0.0, w)
+    np.savez_compressed(os.path.join(OUT, "ref_pins.npz"), **data)
+    print("ref_pins.npz:", len(PIN_CASES), "equaliser cases,", len(PIN_MAPS), "RE maps")
+
+
 def gen_pdcch(rng):
     import ctypes as C
 
@@ -442,6 +516,9 @@ def main():
     if sys.argv[1:] == ["pdcch"]:
         gen_pdcch(np.random.default_rng(4004))
         return
+    if sys.argv[1:] == ["pins"]:
+        gen_ref_pins()
+        return
     if sys.argv[1:] == ["tdec8"]:
         gen_tdec8(np.random.default_rng(8008))
         return
@@ -454,6 +531,7 @@ def main():
     gen_pdsch_stages(np.random.default_rng(3003))
     gen_pdcch(np.random.default_rng(4004))
     gen_tdec8(np.random.default_rng(8008))
+    gen_ref_pins()
 
 
 if __name__ == "__main__":

@@ -133,7 +133,7 @@ def llr_spot_check(rx, k: int, ocfg: pc.Cfg, payload_bytes: list, decoded_job: i
 
     grids = np.stack([d2h(rx.grid_ptr(k, r)) for r in range(ocfg.nof_rx)])
     ces = np.stack([np.stack([d2h(rx.ce_ptr(k, p, r)) for r in range(ocfg.nof_rx)]) for p in range(ocfg.nof_ports)])
-    if rx.chest_cfg.ce_rows == 1:  # row 0 only was written: the AVERAGE estimate of every OFDM symbol
+    if getattr(rx, "ce_rows", 0) == 1:  # row 0 only was written: the AVERAGE estimate of every OFDM symbol
         nre = 12 * ocfg.nof_prb
         ces = np.tile(ces[:, :, :nre], (1, 1, 14))
     noise = rx.chest[k].noise_estimate

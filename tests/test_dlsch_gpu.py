@@ -97,3 +97,25 @@ def test_dlsch_speculative_dec2_matches_oracle(max_its):
         got = dl.decode(pool, [dict(tbs=t, Qm=q, rv=0, softbuffer=i) for i, (t, q, g, s) in enumerate(cases)], llrs)
         want = _oracle(llrs, cases, [0] * len(cases), max_its, [oracle.Softbuffer() for _ in cases])
         _check(got, want, cases)
+
+
+def test_dlsch_many_distinct_tb_sizes_one_call():
+    """the TB epilogue's per-size CRC factor tables (dlsch_runtime.cpp tb_crc_scales) must stay valid for
+    every TB planned in a call.  600 distinct single-CB TB sizes (more than the old 512-entry cap) in one batch, then
+    again in a second call; every TB passes its CRC with the transmitted payload."""
+    sizes = [40 + 8 * i for i in range(600)]  # K = tbs + 24 <= 4856: one code block each
+    rng = np.random.default_rng(512)
+    dl = Dlsch(0, 6)
+    pool = SoftbufferPool(len(sizes), 1)
+    for call in range(2):
+        pays, llrs = [], []
+        for t in sizes:
+            p, e = oracle.make_tb(rng, t, 2, 3 * t + 120, 0, 20.0)
+            pays.append(p)
+            llrs.append(e)
+        pool.reset_all()
+        rets, datas, _its = dl.decode(pool, [dict(tbs=t, Qm=2, rv=0, softbuffer=i) for i, t in enumerate(sizes)],
+                                      llrs)
+        assert rets == [0] * len(sizes), (call, [i for i, r in enumerate(rets) if r != 0][:8])
+        for i, t in enumerate(sizes):
+            np.testing.assert_array_equal(datas[i][: t // 8], pays[i][: t // 8], err_msg=f"call {call} tbs {t}")

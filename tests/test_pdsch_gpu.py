@@ -45,8 +45,8 @@ CFGS = [
 ]
 
 
-def _stage_check(pd, k, cfg, sf, job=0):
-    d_o, csi_o, e_o = pc.rx_front(cfg, sf.y, sf.ce, sf.noise)
+def _stage_check(pd, k, cfg, sf, job=0, predecoder=None):
+    d_o, csi_o, e_o = pc.rx_front(cfg, sf.y, sf.ce, sf.noise, predecoder=predecoder)
     nre = sf.nof_re
     ncw = cfg.nof_layers if cfg.scheme in (2, 3) else 1
     for cw in range(ncw):
@@ -68,6 +68,20 @@ def test_frontend_matches_oracle(k):
     assert ds.job.cfg.grant.nof_re == sf.nof_re
     pd.frontend([ds.job])
     _stage_check(pd, k, cfg, sf)
+
+
+@pytest.mark.skipif(not oracle.ref_available(), reason="oracle/_ref not built")
+@pytest.mark.parametrize("k", range(len(CFGS)))
+def test_frontend_matches_reference_scalar_equaliser(k):
+    """The GPU's equalised symbols, CSI and LLRs against the same chain with the equaliser taken from the COMPILED
+    reference (oracle/_ref: srslte_predecoding_type in chunks below one AVX2 vector, i.e. its exact-division scalar
+    path, precoding.c / mat.c) instead of the oracle restatement: bit-exact, every scheme of CFGS."""
+    cfg = CFGS[k]
+    sf = pc.synth_subframe(cfg, np.random.default_rng(700 + k), snr_db=25)
+    ds = DevSubframe(cfg, sf)
+    pd = P.Pdsch(cell_of(cfg), cfg.nof_rx)
+    pd.frontend([ds.job])
+    _stage_check(pd, k, cfg, sf, predecoder=oracle.ref_predecode_scalar)
 
 
 def test_decode_batch_matches_oracle():

@@ -253,7 +253,7 @@ def test_ue_dl_decode_interpolate():
 
 @pytest.mark.parametrize("ctrl", [False, True], ids=["decode_batch", "find_and_decode"])
 def test_ce_rows_first_only(ctrl):
-    """mi355_chest_dl_cfg_t.ce_rows = 1 (AVERAGE): the batched calls write row 0 of every estimate only -- the other
+    """mi355_ue_dl_set_ce_rows(1) (AVERAGE): the batched calls write row 0 of every estimate only -- the other
     13 rows keep whatever the buffer held -- and every result is the one of the all-rows run: estimator outputs,
     CFI / DCIs, CRCs, iteration counts, payloads and the soft bits of a sample."""
     import bench
