@@ -90,6 +90,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="skip the per-stage and MAP-kernel probes (profiling runs)")
+    ap.add_argument("--fanout", action="store_true",
+                    help="batch fan-out: rank 0 holds every rank's I/Q and scatters the shards over RCCL each step "
+                         "(pdsch / ue_dl / plumbing workloads); payload SHA-1s and CRC bitmaps gathered back")
     return ap.parse_args(argv)
 
 
@@ -195,6 +198,47 @@ def gather_bitmap(pg, local, bits: np.ndarray):
     if rank != 0:
         return None
     return np.concatenate([np.unpackbits(o.cpu().numpy())[: ns[r]] for r, o in enumerate(outs)])
+
+
+def gather_bytes(pg, local, b: bytes, n: int) -> list[bytes] | None:
+    """n bytes of every rank on rank 0 (all-gather of one uint8 tensor), None elsewhere; [b] without a group."""
+    if pg is None:
+        return [b]
+    import torch
+    t = torch.from_numpy(np.frombuffer(b, np.uint8).copy()).to(_dev(local))
+    assert t.numel() == n
+    outs = [torch.zeros_like(t) for _ in range(pg.get_world_size())]
+    pg.all_gather(outs, t)
+    return [o.cpu().numpy().tobytes() for o in outs] if pg.get_rank() == 0 else None
+
+
+def fanout_scatter(pg, full, recv) -> None:
+    """Batch fan-out (north star: "RCCL broadcast/gather over xGMI only for batch fan-out"): rank 0 holds
+    the I/Q of every rank's shard as one (world, shard bytes) tensor, and ONE scatter puts row r into rank r's
+    receive buffer -- srsUE's I/Q enters one host (srsue/src/phy/sync.cc:884-892), the decode fans out.  RCCL (or
+    gloo on CPU) moves (world - 1) shards over xGMI; without a process group it is a local copy."""
+    if pg is None:
+        recv.copy_(full[0])
+        return
+    pg.scatter(recv, list(full.unbind(0)) if pg.get_rank() == 0 else None, src=0)
+
+
+class TorchBuf:
+    """A torch device tensor as a raw buffer of the C ABI (.ptr): the fan-out's RCCL scatter writes where the decoder
+    reads, without a copy."""
+
+    def __init__(self, nbytes: int, local: int):
+        import torch
+        self.t = torch.empty(int(nbytes), dtype=torch.uint8, device=f"cuda:{local}")
+        self.ptr, self.nbytes = self.t.data_ptr(), int(nbytes)
+
+
+def plumbing_iq(first: int, n: int, nbytes: int) -> np.ndarray:
+    """The plumbing workload's fabricated "I/Q" of subframes [first, first + n): nbytes per subframe keyed by the
+    global index (the CPU stand-in for the GPU generator's index-keyed synthesis)."""
+    i = np.arange(first, first + n, dtype=np.uint64)[:, None]
+    j = np.arange(nbytes, dtype=np.uint64)[None, :]
+    return (((i * np.uint64(2654435761)) ^ (j * np.uint64(40503))) >> np.uint64(7)).astype(np.uint8)
 
 
 def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
@@ -361,7 +405,7 @@ def tm4_plans(cell, ctrl):
             for sf in range(10)}
 
 
-def Tm4Source(cell, n_max, device, ctrl=False, chunk=256):
+def Tm4Source(cell, n_max, device, ctrl=False, chunk=256, iq_buffer=None):
     """Up to n_max TM4 subframes resident in HBM (I/Q per rx antenna + the transmitted payloads), synthesised on the
     GPU by global subframe index with the product's eNodeB generator (srsran_amd.synth.DlSource): payloads keyed by
     index -> put_pdsch -> put_refs [-> control region] -> crossed 2x2 channel + AWGN keyed by index -> IFFT."""
@@ -372,7 +416,7 @@ def Tm4Source(cell, n_max, device, ctrl=False, chunk=256):
             super().generate(first, [self.plan_sf[(first + k) % 10] for k in range(n)], snr_db, seed, fading,
                              ctrl=self.ctrl)
 
-    src = _Tm4(cell, 2, n_max, NB, device, H=[[1, 1], [1, -1]], chunk=chunk)
+    src = _Tm4(cell, 2, n_max, NB, device, H=[[1, 1], [1, -1]], chunk=chunk, iq_buffer=iq_buffer)
     src.ctrl, src.plan_sf = ctrl, tm4_plans(cell, ctrl)
     return src
 
@@ -757,6 +801,111 @@ def run_pdsch(args, world, rank, local, pg):
     return res
 
 
+class FanShard:
+    """What a rank decodes in fan-out mode: its shard's I/Q in the scatter's receive buffer (rx-major per subframe,
+    as DlSource lays it out) and the subframes' plans (grants are known per subframe index)."""
+
+    def __init__(self, buf, plans, sf_len, nof_rx=2):
+        self.buf, self.plans, self.sf_len, self.nof_rx = buf, plans, sf_len, nof_rx
+
+    def iq_ptr(self, k: int, r: int) -> int:
+        return self.buf.ptr + (k * self.nof_rx + r) * self.sf_len * 8
+
+
+def tb_digest(pay: np.ndarray) -> bytes:
+    """SHA-1 over the TB payload bytes of a batch, (n, 2, >= NB) -> 20 bytes."""
+    return hashlib.sha1(np.ascontiguousarray(pay[:, :, :NB]).tobytes()).digest()
+
+
+def run_pdsch_fanout(args, world, rank, local, pg):
+    """configs[3]/[4] with the batch fan-out the north star names ("RCCL broadcast/gather over xGMI only for batch
+    fan-out"): the I/Q of all world x B subframes of a step is resident on rank 0 (synthesised there by global index),
+    and every step starts with ONE RCCL scatter of the shards (B x 368,640 bytes of I/Q per rank, over xGMI) into
+    each rank's receive buffer, which the decoder reads in place; the ranks decode their shard (decode_batch, or
+    find_and_decode with --workload ue_dl) and the CRC bitmaps plus per-rank payload SHA-1s are gathered back to
+    rank 0, which checks them against the transmitted payloads.  The timed step is scatter + decode.  Every rank also
+    synthesises its own shard locally once (the default mode's data) and checks the received I/Q equals it bit for
+    bit, so the decode results are those of local synthesis."""
+    import torch
+    from srsran_amd import lib
+    cell = tm4_setup()
+    B = args.subframes
+    ctrl = args.workload == "ue_dl"
+    sf_len = 15 * 1536
+    sf_bytes = 2 * sf_len * 8
+    lo = rank * B
+    plan_sf = tm4_plans(cell, ctrl)
+    src = full = None
+    if rank == 0:
+        full_buf = TorchBuf(world * B * sf_bytes, local)
+        src = Tm4Source(cell, world * B, local, ctrl, iq_buffer=full_buf)
+        src.generate(0, world * B, args.snr, args.seed)
+        full = full_buf.t.view(world, B * sf_bytes)
+    recv = TorchBuf(B * sf_bytes, local)
+    shard = FanShard(recv, [plan_sf[(lo + k) % 10] for k in range(B)], sf_len)
+    rx = Tm4Rx(cell, B, local, ctrl)
+    bound = rx.bind(shard, 0, B)
+
+    def step():
+        fanout_scatter(pg, full, recv.t)
+        torch.cuda.synchronize(local)
+        rx.step(bound)
+
+    for _ in range(args.warmup):
+        step()
+    lib().mi355_device_sync()
+    barrier(pg, local)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    lib().mi355_device_sync()
+    barrier(pg, local)
+    dt = max_over_ranks(pg, local, time.perf_counter() - t0)
+    # the scatter alone (same buffers), for the xGMI rate
+    barrier(pg, local)
+    t1 = time.perf_counter()
+    for _ in range(3):
+        fanout_scatter(pg, full, recv.t)
+    torch.cuda.synchronize(local)
+    barrier(pg, local)
+    dts = max_over_ranks(pg, local, time.perf_counter() - t1) / 3
+
+    bits = rx.crc_bits(B)
+    gathered = gather_bitmap(pg, local, bits)
+    digs = gather_bytes(pg, local, tb_digest(rx.received(B)), 20)
+    # received I/Q == this rank's own index-keyed synthesis of the same subframes (the default mode's input)
+    mine = TorchBuf(B * sf_bytes, local)
+    loc = Tm4Source(cell, B, local, ctrl, iq_buffer=mine)
+    loc.generate(lo, B, args.snr, args.seed)
+    same = int(sum_over_ranks(pg, local, float(torch.equal(mine.t, recv.t))))
+    loc.close()
+    ok_tbs = int(gathered.sum()) if rank == 0 else 0
+    mbps = whole_job_rate(world, B * 2 * TBS, args.steps, dt) / 1e6 * (ok_tbs / (2 * B * world))
+    res = {"metric": METRIC, "n_gpus": world, "value": round(mbps, 1), "unit": "Mbps", "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+           "code_blocks_per_s": round(world * 32 * B * args.steps / dt, 1),
+           "subframes_per_s": round(world * B * args.steps / dt, 1), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "fp32+int16", "data": "synthetic",
+           "config": {"workload": f"batch fan-out: rank 0 holds {world} x {B} TM4 subframes of I/Q (20 MHz, 2x2, QAM256, "
+                                  f"{args.snr:g} dB), one RCCL scatter per step, then each rank decodes its shard"
+                                  + (" with find_and_decode" if ctrl else " with decode_batch"),
+                      "subframes_per_gpu_batch": B, "parallelism": f"dp{world}+scatter"},
+           "crc_ok_tbs": f"{ok_tbs}/{2 * B * world}", "roofline": None,
+           "crc_bitmap": bitmap_summary(gathered, world * B) if rank == 0 else None}
+    if rank == 0:
+        want = [tb_digest(src.payloads(r * B, B)) for r in range(world)]
+        moved = (world - 1) * B * sf_bytes
+        res["fanout"] = {"bytes_per_subframe": sf_bytes, "bytes_scattered_per_step": moved,
+                         "scatter_ms": round(dts * 1e3, 3),
+                         "scatter_gbs": round(moved / dts / 1e9, 1) if world > 1 else None,
+                         "scatter_share_of_step": round(dts / (dt / args.steps), 3),
+                         "ranks_received_equal_local_synthesis": f"{same}/{world}",
+                         "payload_sha1_match": [d == w for d, w in zip(digs, want)]}
+        src.close()
+    rx.pool.close()
+    return res
+
+
 SISO_TBS, SISO_K, SISO_C = 15840, 5312, 3
 
 
@@ -1108,15 +1257,32 @@ def run_plumbing(args, world, rank, local, pg):
     (TB t of subframe i "fails" iff (i * 7 + t) % 13 == 0) so the gathered bitmap's order can be checked."""
     T = args.total_subframes or world * args.subframes
     lo, hi = shard_range(T, world, rank) if args.total_subframes else (rank * args.subframes, (rank + 1) * args.subframes)
+    fan = None
+    if args.fanout:  # rank 0 fabricates every shard's "I/Q" by global index and scatters it
+        import torch
+        assert not args.total_subframes, "--fanout uses equal shards of --subframes"
+        B, SFB = args.subframes, 64
+        full = torch.from_numpy(plumbing_iq(0, world * B, SFB).reshape(world, B * SFB)) if rank == 0 else None
+        recv = torch.empty(B * SFB, dtype=torch.uint8)
     barrier(pg, local)
     t0 = time.perf_counter()
+    if args.fanout:
+        fanout_scatter(pg, full, recv)
     i = np.arange(lo, hi, dtype=np.int64)
     bits = np.stack([(i * 7 + t) % 13 != 0 for t in range(2)], axis=1).reshape(-1).astype(np.uint8)
     time.sleep(0.02 * (rank + 1))
     barrier(pg, local)
     dt = max_over_ranks(pg, local, time.perf_counter() - t0)
     g = gather_bitmap(pg, local, bits)
-    return {"metric": "plumbing dry run (no decoding)", "value": None, "unit": None, "n_gpus": world,
+    if args.fanout:
+        got = recv.numpy().reshape(B, SFB)
+        eq = int(sum_over_ranks(pg, local, float(np.array_equal(got, plumbing_iq(lo, B, SFB)))))
+        dig = gather_bytes(pg, local, hashlib.sha1(got.tobytes()).digest(), 20)
+        if rank == 0:
+            want = [hashlib.sha1(plumbing_iq(r * B, B, SFB).tobytes()).digest() for r in range(world)]
+            fan = {"ranks_equal_local_synthesis": eq, "shard_sha1_match": dig == want,
+                   "bytes_per_subframe": SFB, "bytes_scattered_per_step": (world - 1) * B * SFB}
+    return {"fanout": fan,"metric": "plumbing dry run (no decoding)", "value": None, "unit": None, "n_gpus": world,
             "steps": 1, "warmup": 0, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
             "scaling": "weak" if not args.total_subframes else "strong", "vs_baseline": None, "dtype": None,
             "data": "synthetic", "config": {"workload": "plumbing", "total_subframes": T,
@@ -1137,6 +1303,8 @@ def main():
         res = run_plumbing(args, world, rank, local, pg)
     elif args.workload == "siso_qpsk":
         res = run_siso(args, world, rank, local, pg)
+    elif args.fanout:
+        res = run_pdsch_fanout(args, world, rank, local, pg)
     else:
         res = run_pdsch(args, world, rank, local, pg)
     if rank == 0:

@@ -38,7 +38,8 @@ class DlSource:
     per TB slot), synthesised on the GPU by global subframe index.  H: (nof_rx, nof_ports) test channel mixing
     the port grids (phy_dl_test's crossed 2x2 [[1,1],[1,-1]], identity for SISO)."""
 
-    def __init__(self, cell: P.Cell, nof_rx: int, n_max: int, nbytes: int, device: int = 0, H=None, chunk=256):
+    def __init__(self, cell: P.Cell, nof_rx: int, n_max: int, nbytes: int, device: int = 0, H=None, chunk=256,
+                 iq_buffer=None):
         from . import enb_dl
         from .tdec import DeviceBuffer
         from .ue_dl import symbol_sz
@@ -48,7 +49,11 @@ class DlSource:
         self.G, self.nre = 14 * 12 * cell.nof_prb, 12 * cell.nof_prb
         self.H = np.asarray(H if H is not None else np.eye(nof_rx, self.np), np.complex64)
         assert self.H.shape == (nof_rx, self.np)
-        self.d_iq = DeviceBuffer(n_max * nof_rx * self.sf_len * 8, device)
+        # iq_buffer: a caller-owned device buffer (.ptr, .nbytes) to synthesise into (bench.py --fanout: a torch
+        # tensor that RCCL scatters from)
+        if iq_buffer is not None:
+            assert iq_buffer.nbytes >= n_max * nof_rx * self.sf_len * 8
+        self.d_iq = iq_buffer if iq_buffer is not None else DeviceBuffer(n_max * nof_rx * self.sf_len * 8, device)
         self.d_pl = DeviceBuffer(n_max * 2 * nbytes, device)
         self.enb = enb_dl.EnbDl(cell, device)
         self.chunk = min(chunk, n_max)

@@ -86,3 +86,26 @@ def test_shard_range_covers_total():
         assert rs[0][0] == 0 and rs[-1][1] == T
         assert all(rs[r][1] == rs[r + 1][0] for r in range(N - 1))
         assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+
+
+def test_bench_fanout_scatter_equals_local_synthesis():
+    """--fanout (north star: RCCL broadcast/gather over xGMI only for batch fan-out): rank 0 holds every rank's
+    index-keyed input and scatters the shards; each rank's received shard must equal its own local synthesis of the
+    same subframe indices bit for bit, the gathered shard SHA-1s must equal rank 0's, and the CRC bitmap is the
+    default mode's."""
+    res = _run_bench(["--gpus", "2", "--workload", "plumbing", "--subframes", "300", "--fanout"])
+    fan = res["fanout"]
+    assert fan["ranks_equal_local_synthesis"] == 2
+    assert fan["shard_sha1_match"] is True
+    assert fan["bytes_scattered_per_step"] == 300 * 64
+    assert res["bitmap_bits"] == _expected_bits(0, 600)
+
+
+def test_fanout_scatter_world1_is_a_copy():
+    sys.path.insert(0, os.path.dirname(HERE))
+    import torch
+    import bench
+    full = torch.arange(12, dtype=torch.uint8).reshape(1, 12)
+    recv = torch.zeros(12, dtype=torch.uint8)
+    bench.fanout_scatter(None, full, recv)
+    assert torch.equal(recv, full[0])

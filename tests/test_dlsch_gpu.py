@@ -101,12 +101,17 @@ def test_dlsch_speculative_dec2_matches_oracle(max_its):
 
 def test_dlsch_many_distinct_tb_sizes_one_call():
     """the TB epilogue's per-size CRC factor tables (dlsch_runtime.cpp tb_crc_scales) must stay valid for
-    every TB planned in a call.  600 distinct single-CB TB sizes (more than the old 512-entry cap) in one batch, then
-    again in a second call; every TB passes its CRC with the transmitted payload."""
-    sizes = [40 + 8 * i for i in range(600)]  # K = tbs + 24 <= 4856: one code block each
+    every TB planned in a call.  600 distinct TB sizes (more than the old 512-entry cap) in one batch, then
+    again in a second call; every TB passes its CRC with the transmitted payload (1 to 6 code blocks per TB)."""
+    sizes = []
+    t = 40
+    while len(sizes) < 600:  # the first 600 TB sizes without filler bits (the oracle encoder's domain): 40..32536
+        if oracle.cbsegm(t)["F"] == 0:
+            sizes.append(t)
+        t += 8
     rng = np.random.default_rng(512)
     dl = Dlsch(0, 6)
-    pool = SoftbufferPool(len(sizes), 1)
+    pool = SoftbufferPool(len(sizes), 6)
     for call in range(2):
         pays, llrs = [], []
         for t in sizes:

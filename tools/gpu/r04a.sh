@@ -1,9 +1,12 @@
 #!/bin/bash
-# r04a: configs[2] SISO QPSK kernel trace + host phases; pdsch_eq_rm SQ counter passes (VALU / LDS / busy)
+# r04a: GPU suite after the reference-pin / ADVICE changes; configs[2] SISO QPSK kernel trace + host phases;
+# pdsch_eq_rm SQ counter passes (VALU / LDS / busy)
 set -e
 OUT=gpurun_out/r04a
 mkdir -p $OUT
 export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/gpu_suite.log 2>&1
+timeout -k 10 300 python3 -u bench.py --fanout --steps 3 --warmup 1 --subframes 1024 > $OUT/fanout.json 2> $OUT/fanout.err
 MI355_HOST_PROF=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/siso -o tr -- python3 bench.py --workload siso_qpsk --steps 3 --warmup 1 --no-cpu --no-roofline > $OUT/siso.json 2> $OUT/siso.err
 timeout -k 10 300 python3 -u bench.py --workload siso_qpsk --steps 5 --warmup 2 --no-cpu --no-roofline > $OUT/siso_plain.json 2> $OUT/siso_plain.err
 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU --output-format csv -d $OUT/sq1 -o sq -- python3 bench.py --steps 1 --warmup 1 --no-cpu --no-waterfall --no-roofline > $OUT/sq1.log 2>&1
