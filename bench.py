@@ -606,8 +606,22 @@ def map_probe(rx, ncb, local, K=6144):
     for _ in range(2):
         dec.run_dev(ptr, stride, ncb, K, 8, d_out.ptr)
     kms, kl = dec.kernel_stats()
+    # the kernel's bandwidth-only clone (mi355_tdec_set_diag(20): same grid, loads, checkpoint stores, extrinsic
+    # scatter, one xor per trellis step): the time this schedule's memory traffic alone takes on this box
+    old = lib().mi355_tdec_set_diag(20)
+    for _ in range(2):
+        dec.run_dev(ptr, stride, ncb, K, 8, d_out.ptr)
+    cms, cl = dec.kernel_stats()
+    lib().mi355_tdec_set_diag(old)
     dec.set_profiling(False)
     roof, valu = tdec_roofline(kms, kl, ncb, K)
+    if cl:
+        clone = cms / cl
+        roof["schedule_clone_ms"] = round(clone, 4)
+        roof["schedule_frac"] = round(clone / roof["avg_launch_ms"], 4)
+        roof["schedule_note"] = ("bandwidth-only clone of tdec_win_halfit (MI355_TDEC_DIAG 20) over the same "
+                                 "65,536-CB launches: schedule_frac = clone time / real time (1.0 = the trellis math "
+                                 "is fully hidden under this schedule's memory traffic)")
     fixed8 = {"code_blocks": ncb, "half_iterations": 8, "ms": round(wall * 1e3, 3),
               "code_blocks_per_s": round(ncb / wall, 1), "mbps": round(ncb * (K - 24) / wall / 1e6, 1),
               "note": f"the batch's {ncb:,} rate-dematched CBs decoded with a fixed 8 half-iterations (no early stop), "
@@ -1092,8 +1106,22 @@ def run_tdec(args, world, rank, local, pg):
     for _ in range(2):
         step()
     kms, kl = dec.kernel_stats()
+    # the kernel's bandwidth-only clone (mi355_tdec_set_diag(20): same grid, loads, checkpoint stores, extrinsic
+    # scatter, one xor per trellis step): the time this schedule's memory traffic alone takes on this box
+    old = lib().mi355_tdec_set_diag(20)
+    for _ in range(2):
+        dec.run_dev(ptr, stride, ncb, K, 8, d_out.ptr)
+    cms, cl = dec.kernel_stats()
+    lib().mi355_tdec_set_diag(old)
     dec.set_profiling(False)
     roof, valu = tdec_roofline(kms, kl, ncb, K)
+    if cl:
+        clone = cms / cl
+        roof["schedule_clone_ms"] = round(clone, 4)
+        roof["schedule_frac"] = round(clone / roof["avg_launch_ms"], 4)
+        roof["schedule_note"] = ("bandwidth-only clone of tdec_win_halfit (MI355_TDEC_DIAG 20) over the same "
+                                 "65,536-CB launches: schedule_frac = clone time / real time (1.0 = the trellis math "
+                                 "is fully hidden under this schedule's memory traffic)")
     cb_s = world * ncb * args.steps / dt
     res = {
         "metric": METRIC, "value": round(cb_s * K / 1e6, 1), "unit": "Mbps", "n_gpus": world,

@@ -91,6 +91,12 @@ int mi355_tdec_batch_run(mi355_tdec_batch_t* q,
 void mi355_tdec_batch_set_profiling(mi355_tdec_batch_t* q, int enable);
 int  mi355_tdec_batch_kernel_stats(mi355_tdec_batch_t* q, double* ms, uint32_t* launches);
 
+/* Measurement only: 20 = the window MAP kernel's bandwidth-only clone (same grid, occupancy, loads, checkpoint
+ * stores, extrinsic scatter and decision bytes, each trellis step replaced by one xor; its OUTPUTS ARE MEANINGLESS),
+ * 0 = the decoder.  Process-wide; bench.py times the clone against the real kernel (roofline.schedule_frac).  Other
+ * values are the MI355_TDEC_DIAG microbenchmark variants.  Returns the previous mode. */
+int mi355_tdec_set_diag(int mode);
+
 /* Number of trellis windows the reference AVX2 build uses for K (turbodecoder.c:381-393): 16, 8 or 0. */
 uint32_t mi355_tdec_autoimp_get_subblocks(uint32_t long_cb);
 

@@ -49,6 +49,7 @@ def _declare(L: C.CDLL) -> None:
     L.mi355_tdec_batch_set_impl.argtypes = [vp, i32]
     L.mi355_tdec_batch_set_profiling.argtypes = [vp, i32]
     L.mi355_tdec_batch_kernel_stats.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(u32)]
+    L.mi355_tdec_set_diag.argtypes = [i32]
     L.mi355_tdec_autoimp_get_subblocks.restype = u32
     L.mi355_tdec_autoimp_get_subblocks.argtypes = [u32]
     L.mi355_dev_alloc.restype = vp

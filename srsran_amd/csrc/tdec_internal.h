@@ -103,6 +103,7 @@ struct TdecRun {
 
 hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s);
 bool       tdec_win_spec_ok(int nsb, int L);
+int        tdec_set_diag(int mode);
 hipError_t tdec_win_launch_decide(int nsb, const TdecDecideArgs& a, hipStream_t s);
 hipError_t tdec_gen_launch_prep(const TdecGenPrepArgs& a, hipStream_t s);
 hipError_t tdec_gen_launch_halfit(const TdecGenArgs& a, hipStream_t s);

@@ -230,6 +230,9 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   if (a.remaining && *a.remaining == 0) return;  // every code block of the batch has finished
 
   const int  L = a.L, Lp = a.Lp, nseg = a.nseg;
+  // DIAG 20: the bandwidth-only clone (bench roofline.schedule_frac): every load, checkpoint store, extrinsic scatter
+  // and decision byte of the real kernel at the same grid and occupancy, with each trellis step replaced by one xor
+  constexpr bool CL     = DIAG == 20;
   constexpr bool dec2   = MODE == 2;
   constexpr bool has_ap = MODE == 1;
 
@@ -304,6 +307,10 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
       const int k = 8 * b + i;
       v2s       x = U(hi_lo(from_prev(xo[i]), xo[i]));
       if constexpr (has_ap) x = sadd(x, U(hi_lo(from_prev(ao[i]), ao[i])));
+      if constexpr (CL) {
+        aw[k & 7] = aw[k & 7] ^ x ^ U(yo[i]);
+        continue;
+      }
       v2s c0[8], c1[8];
       alpha_cands<true>(aw, x, U(hi_lo(from_prev(yo[i]), yo[i])), c0, c1);
 #pragma unroll
@@ -333,6 +340,10 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
       const int k = 8 * b + i;
       v2s       x = U(hi_lo(xo[i], from_next(xo[i])));
       if constexpr (has_ap) x = sadd(x, U(hi_lo(ao[i], from_next(ao[i]))));
+      if constexpr (CL) {
+        st[k & 7] = st[k & 7] ^ x ^ U(yo[i]);
+        continue;
+      }
       beta_step<true>(st, x, U(hi_lo(yo[i], from_next(yo[i]))), nw);
 #pragma unroll
       for (int s = 0; s < 8; s++) st[s] = nw[s];
@@ -409,9 +420,13 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
             st[0] = st[0] ^ x ^ U(sy[i]);
             continue;
           }
-          beta_step<true>(st, x, U(sy[i]), nw);
+          if constexpr (CL) {
+            st[i] = st[i] ^ x ^ U(sy[i]);
+          } else {
+            beta_step<true>(st, x, U(sy[i]), nw);
 #pragma unroll
-          for (int s = 0; s < 8; s++) st[s] = nw[s];
+            for (int s = 0; s < 8; s++) st[s] = nw[s];
+          }
           if (i == 0 && t > 0 && DIAG != 3) {
 #pragma unroll
             for (int s = 0; s < 8; s++) {
@@ -426,7 +441,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
               }
             }
           }
-          if ((i & 1) == 0 && k != 0) normalize<true>(st);
+          if (!CL && (i & 1) == 0 && k != 0) normalize<true>(st);
         }
       }
     };
@@ -543,11 +558,41 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     // steps 0..3, phase B rows 5..8 for alpha steps 4..7.
     // (TDEC_NPH = 1: all 8 rows live, one pass -- 32 more VGPRs, 2 fewer beta steps per segment)
     static_assert(SEG == 8, "two-phase recompute assumes 8-row segments");
-    constexpr int NPH = TDEC_NPH, RP = 8 / NPH;
+    constexpr int NPH = CL ? 0 : TDEC_NPH, RP = 8 / TDEC_NPH;
     v2s ck8[8], cur[8], R[RP][8];
 #pragma unroll
     for (int s = 0; s < 8; s++) ck8[s] = U(cc[s]);
     const bool ck_norm = (e & 1) == 0 && e != L;
+    if constexpr (CL) { // the clone: one xor per step in place of the beta rebuild, alpha and output; same stores
+#pragma unroll
+      for (int i = 0; i < SEG; i++) {
+        const int j = s0 + i;
+        if (FULL ? i < SEG : j < e) {
+          const v2s      out = xin[i] ^ U(cy[i]) ^ ck8[i] ^ st[i];
+          const uint32_t tb  = cd[i];
+          const uint32_t olo = (tb & 0xffffu) + lane0 * 2, ohi = (tb >> 16) + lane0 * 2;
+          if constexpr (!dec2) {
+            if constexpr (wr_e) {
+              E16[olo] = out.x;
+              E16[ohi] = out.y;
+            }
+            bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
+          } else {
+            if constexpr (wr_a1) {
+              A16[olo] = out.x;
+              A16[ohi] = out.y;
+            }
+            if constexpr (wr_bm) {
+              const uint32_t jd = (tb & 0xffffu) >> 7, wlo = tb & 15u, whi = (tb >> 16) & 15u;
+              const uint32_t blo = wlo * (L / 8) + (jd >> 3), bhi = whi * (L / 8) + (jd >> 3);
+              const uint32_t sh  = 7 - (jd & 7);
+              atomicOr(&bm[blo >> 2], (uint32_t)(out.x > 0) << (((blo & 3) << 3) + sh));
+              atomicOr(&bm[bhi >> 2], (uint32_t)(out.y > 0) << (((bhi & 3) << 3) + sh));
+            }
+          }
+        }
+      }
+    }
 
 #pragma unroll
     for (int ph = 0; ph < NPH; ph++) {
@@ -747,14 +792,22 @@ __global__ __launch_bounds__(256) void tdec_win_decide(TdecDecideArgs a)
 
 // ---------------------------------------------------------------------------- launchers
 
+static int g_diag = -1; // MI355_TDEC_DIAG, or mi355_tdec_set_diag
+
 static int diag_mode()
 {
-  static int m = -1;
-  if (m < 0) {
+  if (g_diag < 0) {
     const char* e = getenv("MI355_TDEC_DIAG");
-    m             = e ? atoi(e) : 0;
+    g_diag        = e ? atoi(e) : 0;
   }
-  return m;
+  return g_diag;
+}
+
+int tdec_set_diag(int mode)
+{
+  const int old = diag_mode();
+  g_diag        = mode < 0 ? 0 : mode;
+  return old;
 }
 
 // MI355_TDEC_LDS (diagnostic): reserve that many bytes of LDS per workgroup, capping the waves per CU
@@ -797,7 +850,7 @@ static void launch_mode_o(int mode, int blocks, const TdecWinArgs& a, hipStream_
 {
   // 16-byte pieces need every code block's buffer (and so the stream offsets, multiples of 16 bytes for these K)
   // 16-byte aligned
-  if constexpr (NSB == 16 && FULL && DIAG == 0) {
+  if constexpr (NSB == 16 && FULL && (DIAG == 0 || DIAG == 20)) {
     if (tx_enabled() && (uintptr_t)a.in % 16 == 0 && (a.in_stride * sizeof(int16_t)) % 16 == 0 && (a.L * 16 + 32) % 16 == 0) {
       launch_mode_t<NSB, DIAG, FULL, OUTK, true>(mode, blocks, a, s);
       return;
@@ -841,6 +894,8 @@ hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s)
       launch_mode<16, 4>(mode, blocks, a, s);
     } else if (dm == 2) {
       launch_mode<16, 2>(mode, blocks, a, s);
+    } else if (dm == 20 && a.L % TDEC_SEG == 0) { // the bandwidth-only clone (results meaningless)
+      launch_mode<16, 20, true>(mode, blocks, a, s);
     } else if (a.L % TDEC_SEG == 0) {
       launch_mode<16, 0, true>(mode, blocks, a, s);
     } else {

@@ -211,6 +211,8 @@ void mi355_tdec_batch_destroy(mi355_tdec_batch_t* q)
   delete q;
 }
 
+int mi355_tdec_set_diag(int mode) { return mi355::tdec_set_diag(mode); }
+
 void mi355_tdec_batch_set_profiling(mi355_tdec_batch_t* q, int enable)
 {
   if (q) q->prof = enable != 0;
