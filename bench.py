@@ -579,7 +579,10 @@ def cpu_baseline_pdsch(src, gpu_bufs, avg_its, budget_s, ocfg_of=None, K=6144, C
 
 
 def softbuffer_contents(rx, ncb):
+    """Device address and stride of the pool's decoder buffers, materialised (the fused rate dematcher leaves a fresh
+    buffer's empty parity rows unwritten; the turbo-only API and the CPU baseline read every row)."""
     from srsran_amd import lib
+    rx.pool.materialize()
     buf, stride, mcb = C.POINTER(C.c_int16)(), C.c_uint32(), C.c_uint32()
     lib().mi355_softbuffer_pool_buffer.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_int16)),
                                                    C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]

@@ -40,8 +40,14 @@ int mi355_softbuffer_reset_range(mi355_softbuffer_pool_t* p, uint32_t first, uin
  * tbs[i] bits (its code blocks' buffers logically zeroed, every CB CRC flag cleared) */
 int mi355_softbuffer_reset_tbs_batch(mi355_softbuffer_pool_t* p, const uint32_t* sbs, const uint32_t* tbs, uint32_t n,
                                      void* stream);
-/* device address of the pool's int16 code-block buffers (slot = sb * max_cb + cb, `stride` int16 apart) */
+/* device address of the pool's int16 code-block buffers (slot = sb * max_cb + cb, `stride` int16 apart).  A decoder
+ * buffer of the 16-window layout written fresh by the fused equaliser + rate dematcher leaves its parity rows without
+ * an LLR unwritten (logically zero; the decoder never reads them): call mi355_softbuffer_pool_materialize before
+ * reading buffer memory directly. */
 int mi355_softbuffer_pool_buffer(mi355_softbuffer_pool_t* p, int16_t** buf, uint32_t* stride, uint32_t* max_cb);
+/* Zero the unwritten (logically zero) parity rows of every code-block buffer of softbuffers [first, first + n) that
+ * holds data, so that the buffer memory reads exactly as the reference's softbuffer would (stream-ordered). */
+int mi355_softbuffer_pool_materialize(mi355_softbuffer_pool_t* p, uint32_t first, uint32_t n, void* stream);
 
 /* device address of the pool's per-code-block decoded bytes (slot = sb * max_cb + cb, `stride` bytes apart) and the
  * pool's softbuffer count */

@@ -6,6 +6,16 @@
 #define SB_STRIDE 18600 // SOFTBUFFER_SIZE (softbuffer.h:50): int16 per code-block softbuffer
 #define SB_DATA 768     // bytes of decoded CB data kept per code block (softbuffer.c:146)
 #define SB_CONV8 10240  // int16 offset in a slot of the converted copy of an int8 K <= 400 buffer (8-bit mode)
+// parity-row bitmaps of a 16-window decoder buffer (K multiple of 16, 800 < K <= 6144, L = K / 16 <= 384 rows): at int16
+// offset SB_ROWMASK of the slot (past the 3 (K + 32) + 12 = 18,540 entries of K = 6144), SB_ROWMASK_WORDS u32 for P0,
+// then as many for P1; bit j: row j (the 16 windows' entries of step j) holds an LLR.  Written by every 16-bit rate
+// dematcher into the slot (from rm_rowmin: fresh buffers, rows whose smallest circular index is < min(E, N); all
+// ones when combining), read by the window MAP kernel, which skips the parity loads of the other rows (zero).  Word
+// 2 SB_ROWMASK_WORDS holds K.  Rows without an LLR of a fresh buffer are left unwritten by the fused equaliser + rate
+// dematcher (pdsch_eq_rm) and read as zero by every reader: the MAP kernel, the combining rate dematchers and
+// mi355_softbuffer_pool_materialize (raw readers).
+#define SB_ROWMASK 18544
+#define SB_ROWMASK_WORDS 12
 
 namespace mi355 {
 
@@ -50,6 +60,7 @@ struct DlschRmArgs {
   const uint8_t*  sb_crc;
   uint8_t*        fresh;  // per slot: buffer logically zero (lazy srslte_softbuffer_rx_reset)
   uint32_t        fold2;  // LDS pairs: >= max over the launch's code blocks of min(n_e, N) / 2 (0: N / 2)
+  int             sparse; // fresh buffers: parity rows without an LLR are left unwritten (SB_ROWMASK)
 };
 
 // 8-bit rate dematching (srslte_rm_turbo_rx_lut_8bit into (int8_t*)softbuffer->buffer_f[cb], sch.c:403-407):
@@ -117,5 +128,7 @@ hipError_t dlsch_launch_epilogue(const DlschTbArgs& a, hipStream_t s);
 hipError_t dlsch_launch_reset(const DlschResetArgs& a, hipStream_t s);
 
 hipError_t dlsch_launch_rm8(const DlschRm8Args& a, hipStream_t s);
+hipError_t dlsch_launch_materialize(int16_t* sb, size_t stride, const uint8_t* fresh, size_t slot0, uint32_t nslots,
+                                    hipStream_t s);
 
 } // namespace mi355

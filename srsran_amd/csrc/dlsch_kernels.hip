@@ -58,7 +58,8 @@ __global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t acc32[]; // a.fold2 pairs, padded (img_u32)
   const uint16_t* acc   = (const uint16_t*)acc32;
-  const uint32_t  N     = a.N, tid = threadIdx.x, N2 = min(N / 2, a.fold2);
+  __shared__ uint32_t obm[2 * SB_ROWMASK_WORDS], nbm[2 * SB_ROWMASK_WORDS];
+  const uint32_t  N     = a.N, tid = threadIdx.x, N2 = min(N / 2, a.fold2), K = (N - 12) / 3;
   const uint32_t  pairs = a.buflen / 2;
   uint4           iv[RM_Q];
   uint32_t        iv_rv = 0xffffffffu;
@@ -97,7 +98,17 @@ __global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
 #pragma unroll
     for (int k = 0; k < RM_Q; k++)
       old[k] = fresh ? make_uint4(0u, 0u, 0u, 0u) : ld_quad(sb, tid + k * RM_THREADS, pairs, sb16, 0u);
-    __syncthreads(); // the previous code block's gathers from acc are complete
+    __syncthreads(); // the previous code block's gathers from acc (and its bitmaps) are complete
+    // the slot's parity-row bitmap (rm_image.h): the old one (rows it leaves undefined are read as zero), the new one
+    if (tid < 2 * SB_ROWMASK_WORDS) {
+      uint32_t*      bmg = rm_rowmask_of(a.sb + (size_t)d.slot * a.sb_stride);
+      const uint32_t nw  = rm_rowmask_word(a.inv[d.rv], a.buflen, fresh ? min(n_e, N) : 0x10000u, tid);
+      obm[tid]           = fresh ? 0xffffffffu : bmg[tid];
+      nbm[tid]           = nw;
+      bmg[tid]           = nw;
+    } else if (tid == 2 * SB_ROWMASK_WORDS) {
+      rm_rowmask_of(a.sb + (size_t)d.slot * a.sb_stride)[tid] = K;
+    }
 #pragma unroll
     for (int k = 0; k < RM_EQ; k++) {
       const uint32_t i = 4 * (tid + k * RM_THREADS);
@@ -121,10 +132,12 @@ __global__ __launch_bounds__(RM_THREADS) void dlsch_rm_rx(DlschRmArgs a)
     for (int k = 0; k < RM_Q; k++) {
       const uint32_t q = tid + k * RM_THREADS, i = 4 * q;
       if (i >= pairs) continue;
+      if (fresh && a.sparse && !rm_quad_defined(nbm, 2 * i, K)) continue; // an empty parity row stays unwritten
+      const bool     odef = fresh || rm_quad_defined(obm, 2 * i, K);          // old contents defined
       const uint32_t w[4] = {iv[k].x, iv[k].y, iv[k].z, iv[k].w};
-      const uint32_t o[4] = {old[k].x, old[k].y, old[k].z, old[k].w};
+      const uint32_t o[4] = {odef ? old[k].x : 0u, odef ? old[k].y : 0u, odef ? old[k].z : 0u, odef ? old[k].w : 0u};
       uint32_t       v[4];
-      bool           any = fresh;
+      bool           any = fresh || !odef;
 #pragma unroll
       for (int cc = 0; cc < 4; cc++) {
         const uint32_t r0 = w[cc] & 0xffffu, r1 = w[cc] >> 16;
@@ -360,6 +373,41 @@ __global__ __launch_bounds__(256) void dlsch_rm8_rx(DlschRm8Args a)
   }
   o[j] = (int8_t)v;
   if (a.conv) a.conv[(size_t)d.slot * (a.sb_stride / 2) + j] = (int16_t)(int8_t)v; // convert_8_to_16
+  // an int8 buffer has no parity-row bitmap: mark the 16-bit one dense (a later 16-bit combine reads every row)
+  if (j < 2 * SB_ROWMASK_WORDS) ((uint32_t*)(a.sb + (size_t)d.slot * a.sb_stride + 2 * SB_ROWMASK))[j] = 0xffffffffu;
+}
+
+// mi355_softbuffer_pool_materialize: one workgroup per slot holding data (not fresh): the parity rows its bitmap marks
+// undefined are zeroed, then the bitmap says dense
+__global__ __launch_bounds__(256) void sb_materialize(int16_t* sb, size_t stride, const uint8_t* fresh, size_t slot0)
+{
+  const size_t slot = slot0 + blockIdx.x;
+  if (fresh[slot]) return;
+  int16_t*        b  = sb + slot * stride;
+  uint32_t*       bm = rm_rowmask_of(b);
+  const uint32_t  K  = bm[2 * SB_ROWMASK_WORDS];
+  __shared__ uint32_t w[2 * SB_ROWMASK_WORDS];
+  if (threadIdx.x < 2 * SB_ROWMASK_WORDS) w[threadIdx.x] = bm[threadIdx.x];
+  __syncthreads();
+  if (K % 16 == 0 && K > 800 && K <= 6144) {
+    const uint32_t L = K / 16;
+    for (uint32_t r = threadIdx.x; r < 2 * L; r += blockDim.x) {
+      const uint32_t s = r / L, j = r % L;
+      if ((w[s * SB_ROWMASK_WORDS + (j >> 5)] >> (j & 31)) & 1u) continue;
+      uint4* row = (uint4*)(b + (s + 1) * (K + 32) + 16 * j);
+      row[0] = row[1] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * SB_ROWMASK_WORDS) bm[threadIdx.x] = 0xffffffffu;
+}
+
+hipError_t dlsch_launch_materialize(int16_t* sb, size_t stride, const uint8_t* fresh, size_t slot0, uint32_t nslots,
+                                    hipStream_t s)
+{
+  if (!nslots) return hipSuccess;
+  hipLaunchKernelGGL(sb_materialize, dim3(nslots), dim3(256), 0, s, sb, stride, fresh, slot0);
+  return hipGetLastError();
 }
 
 hipError_t dlsch_launch_rm8(const DlschRm8Args& a, hipStream_t s)

@@ -23,6 +23,7 @@
 #include "dlsch_internal.h"
 #include "host_staging.h"
 #include "tdec8_internal.h"
+#include "rm_image.h"
 #include "rm_tables.h"
 #include "runtime_internal.h"
 #include "tdec_internal.h"
@@ -116,6 +117,20 @@ static bool spec_enabled()
   return on;
 }
 
+// MI355_NO_ROWMASK=1 (A/B timing): the MAP kernel reads every parity row
+static bool no_rowmask()
+{
+  static const bool off = getenv("MI355_NO_ROWMASK") && atoi(getenv("MI355_NO_ROWMASK")) != 0;
+  return off;
+}
+
+// MI355_RM_SPARSE=0 (A/B timing): fresh decoder buffers written whole, zero parity rows included
+bool mi355::rm_sparse_writes()
+{
+  static const bool on = !getenv("MI355_RM_SPARSE") || atoi(getenv("MI355_RM_SPARSE")) != 0;
+  return on && !no_rowmask();
+}
+
 static uint32_t rm_buflen(uint32_t K) { return tdec_subblocks(K) ? 3 * (K + 32) + 12 : 3 * K + 12; }
 
 // inverse of the rate-dematching table: decoder-buffer position -> circular-buffer index (or RM_NONE)
@@ -125,8 +140,20 @@ static int rm_table(mi355_dlsch_t* q, uint32_t K, uint32_t rv, const uint16_t** 
   auto           it  = q->rm.find(key);
   if (it == q->rm.end()) {
     const std::vector<uint16_t> t = rm_rx_table(K, rv);
-    std::vector<uint16_t>       inv(rm_buflen(K) + 1, RM_NONE);
+    const uint32_t              buflen = rm_buflen(K);
+    std::vector<uint16_t>       inv(rm_rowmin_off(buflen) + rm_rowmin_len(), 0);
+    std::fill(inv.begin(), inv.begin() + buflen + 1, (uint16_t)RM_NONE);
     for (size_t r = 0; r < t.size(); r++) inv[t[r]] = (uint16_t)r;
+    if (tdec_subblocks(K) == 16) { // parity-row minima (rm_image.h), rows of the 16-window layout: L = K / 16
+      uint16_t*      rmin = inv.data() + rm_rowmin_off(buflen);
+      const uint32_t L    = K / 16;
+      for (uint32_t s = 0; s < 2; s++)
+        for (uint32_t j = 0; j < L; j++) {
+          uint16_t m = RM_NONE;
+          for (uint32_t w = 0; w < 16; w++) m = std::min(m, inv[(s + 1) * (K + 32) + j * 16 + w]);
+          rmin[s * 32 * SB_ROWMASK_WORDS + j] = m; // rows >= L stay 0 (defined)
+        }
+    }
     uint16_t* d = nullptr;
     CHECK_HIP(hipMalloc(&d, inv.size() * 2));
     CHECK_HIP(hipMemcpy(d, inv.data(), inv.size() * 2, hipMemcpyHostToDevice));
@@ -370,6 +397,16 @@ int mi355_softbuffer_pool_buffer(mi355_softbuffer_pool_t* p, int16_t** buf, uint
   if (buf) *buf = p->buf;
   if (stride) *stride = SB_STRIDE;
   if (max_cb) *max_cb = p->max_cb;
+  return MI355_SUCCESS;
+}
+
+int mi355_softbuffer_pool_materialize(mi355_softbuffer_pool_t* p, uint32_t first, uint32_t n, void* stream)
+{
+  if (!p || first > p->nof_sb || n > p->nof_sb - first) return MI355_ERROR_INVALID_INPUTS;
+  CHECK_HIP(hipSetDevice(p->device));
+  CHECK_HIP(dlsch_launch_materialize(p->buf, SB_STRIDE, p->fresh, (size_t)first * p->max_cb, n * p->max_cb,
+                                     (hipStream_t)stream));
+  if (!stream) CHECK_HIP(hipStreamSynchronize(nullptr));
   return MI355_SUCCESS;
 }
 
@@ -758,6 +795,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     ra.sb_stride = SB_STRIDE;
     ra.sb_crc    = pool->cb_crc;
     ra.fold2     = gi < fold2.size() ? fold2[gi] : 0;
+    ra.sparse    = rm_sparse_writes() ? 1 : 0;
     if (!rm_done) CHECK_HIP(dlsch_launch_rm(ra, s));
     auto it = q->dec.find(K);
     if (it == q->dec.end()) {
@@ -790,6 +828,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
       if (!lv.t8) {
         TdecRun rq{llr8 ? pool->buf + SB_CONV8 : pool->buf, SB_STRIDE, d_slot + lv.off, d_done + lv.off, d_run + h, lv.n,
                    lv.K, h, h + 1, lv.dec, lv.K / 8, s, &ca, &fused};
+        rq.rowmask = !llr8 && !no_rowmask(); // every 16-bit rate dematcher leaves the slots' parity-row bitmaps
         bool taken = false;
         rq.spec       = spec;
         rq.spec_taken = &taken;

@@ -89,6 +89,7 @@ struct EqRmPool {
   size_t         sb_stride; // int16 per slot
   const uint8_t* sb_crc;
   uint8_t*       fresh;
+  int            sparse; // fresh buffers: parity rows without an LLR are left unwritten (SB_ROWMASK, rm_image.h)
 };
 hipError_t pdsch_launch_eq_rm(const PdschJobDev* jobs, const EqRmJob* rj, uint32_t njobs, uint32_t max_c, uint32_t img,
                               const uint32_t* keys, uint32_t nkeys, const EqRmPool& pool, hipStream_t s);

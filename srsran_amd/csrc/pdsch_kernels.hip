@@ -1073,6 +1073,24 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     fresh[l] = need[l] && P.fresh[slot[l]] != 0;
   }
   if (!need[0] && !need[1]) return;
+  // the slots' parity-row bitmaps (rm_image.h; E <= N here): the old ones (rows they leave undefined are read as zero
+  // by a combining write), the new ones (a fresh buffer's rows without an LLR are not written, P.sparse)
+  __shared__ uint32_t obm[2][2 * SB_ROWMASK_WORDS], nbm[2][2 * SB_ROWMASK_WORDS];
+  if (tid < 2 * (2 * SB_ROWMASK_WORDS + 1)) {
+    const uint32_t l = tid / (2 * SB_ROWMASK_WORDS + 1), w = tid % (2 * SB_ROWMASK_WORDS + 1);
+    const uint32_t kx = c < R.layer[l].C1 ? 0u : 1u;
+    if (need[l]) {
+      uint32_t* bmg = rm_rowmask_of(P.sb + (size_t)slot[l] * P.sb_stride);
+      if (w < 2 * SB_ROWMASK_WORDS) {
+        const uint32_t nw = rm_rowmask_word(R.layer[l].inv[kx], R.layer[l].buflen[kx], fresh[l] ? n_e : 0x10000u, w);
+        obm[l][w] = fresh[l] ? 0xffffffffu : bmg[w];
+        nbm[l][w] = nw;
+        bmg[w]    = nw;
+      } else {
+        bmg[w] = (R.layer[l].N[kx] - 12) / 3; // K
+      }
+    }
+  }
   __shared__ PdschCwDev cwd[2];
   __shared__ uint32_t   cmb[2];
   if (tid < 2 && J.cw[tid]) {
@@ -1133,7 +1151,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     if (need[0] && need[1] && fresh[0] && fresh[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
         R.layer[0].buflen[kx0] == R.layer[1].buflen[kx1]) {
       // the usual case, two fresh buffers: every position is written, a missing LLR reads the zero slot
-      const uint32_t  npairs = R.layer[0].buflen[kx0] / 2;
+      const uint32_t  npairs = R.layer[0].buflen[kx0] / 2, Kc = (R.layer[0].N[kx0] - 12) / 3;
       const uint32_t* inv32  = (const uint32_t*)R.layer[0].inv[kx0];
       uint32_t*       sb[2]  = {(uint32_t*)(P.sb + (size_t)slot[0] * P.sb_stride),
                                 (uint32_t*)(P.sb + (size_t)slot[1] * P.sb_stride)};
@@ -1155,6 +1173,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
         for (int k = 0; k < ER_Q; k++) {
           const uint32_t i = 4 * (tid + (rd * ER_Q + k) * ER_THREADS);
           if (i >= npairs) continue;
+          if (P.sparse && !rm_quad_defined(nbm[0], 2 * i, Kc)) continue; // an empty parity row stays unwritten
           const uint32_t w[4] = {iv[k].x, iv[k].y, iv[k].z, iv[k].w};
           uint32_t       v0[4], v1[4];
 #pragma unroll
@@ -1177,7 +1196,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
       need[0] = need[1] = false; // done
     } else if (need[0] && need[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
                R.layer[0].buflen[kx0] == R.layer[1].buflen[kx1]) {
-      const uint32_t  npairs = R.layer[0].buflen[kx0] / 2;
+      const uint32_t  npairs = R.layer[0].buflen[kx0] / 2, Kc = (R.layer[0].N[kx0] - 12) / 3;
       const uint32_t* inv32  = (const uint32_t*)R.layer[0].inv[kx0];
       uint32_t*       sb[2]  = {(uint32_t*)(P.sb + (size_t)slot[0] * P.sb_stride),
                                 (uint32_t*)(P.sb + (size_t)slot[1] * P.sb_stride)};
@@ -1210,15 +1229,20 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
           if (i >= npairs) continue;
           const uint32_t w[4] = {iv[k].x, iv[k].y, iv[k].z, iv[k].w};
           uint32_t       v[2][4];
-          bool           any = fresh[0] || fresh[1];
+          // old contents of a row the old bitmap leaves undefined read as zero (and the quad is then rewritten)
+          const bool     od0 = fresh[0] || rm_quad_defined(obm[0], 2 * i, Kc);
+          const bool     od1 = fresh[1] || rm_quad_defined(obm[1], 2 * i, Kc);
+          bool           any = fresh[0] || fresh[1] || !od0 || !od1;
 #pragma unroll
           for (int cc = 0; cc < 4; cc++) {
             const uint32_t r0 = w[cc] & 0xffffu, r1 = w[cc] >> 16;
             const bool     h0 = r0 != 0xffffu && r0 < n_e, h1 = r1 != 0xffffu && r1 < n_e;
             any |= h0 || h1;
             const uint32_t i0 = img_i16(h0 ? r0 : 0u), i1 = img_i16(h1 ? r1 : 0u);
-            const uint32_t o0[4] = {old[0][k].x, old[0][k].y, old[0][k].z, old[0][k].w};
-            const uint32_t o1[4] = {old[1][k].x, old[1][k].y, old[1][k].z, old[1][k].w};
+            const uint32_t o0[4] = {od0 ? old[0][k].x : 0u, od0 ? old[0][k].y : 0u, od0 ? old[0][k].z : 0u,
+                                    od0 ? old[0][k].w : 0u};
+            const uint32_t o1[4] = {od1 ? old[1][k].x : 0u, od1 ? old[1][k].y : 0u, od1 ? old[1][k].z : 0u,
+                                    od1 ? old[1][k].w : 0u};
             v[0][cc] = add_pairs16(o0[cc], (h0 ? (uint16_t)imgs[i0] : 0u) | ((h1 ? (uint16_t)imgs[i1] : 0u) << 16));
             v[1][cc] = add_pairs16(o1[cc], (h0 ? (uint16_t)imgs[img + i0] : 0u) |
                                                ((h1 ? (uint16_t)imgs[img + i1] : 0u) << 16));
@@ -1245,7 +1269,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     if (!need[l]) continue;
     const EqRmLayer& T      = R.layer[l];
     const uint32_t   kx     = c < T.C1 ? 0u : 1u;
-    const uint32_t   npairs = T.buflen[kx] / 2;
+    const uint32_t   npairs = T.buflen[kx] / 2, Kc = (T.N[kx] - 12) / 3;
     const uint32_t*  inv32  = (const uint32_t*)T.inv[kx];
     const uint16_t*  acc    = (const uint16_t*)(imgs + l * img);
     uint32_t*        sb     = (uint32_t*)(P.sb + (size_t)slot[l] * P.sb_stride);
@@ -1273,10 +1297,12 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     for (int k = 0; k < ER_Q; k++) {
       const uint32_t i = 4 * (tid + (rd * ER_Q + k) * ER_THREADS);
       if (i >= npairs) continue;
+      if (fresh[l] && P.sparse && !rm_quad_defined(nbm[l], 2 * i, Kc)) continue; // an empty parity row: unwritten
+      const bool     odef = fresh[l] || rm_quad_defined(obm[l], 2 * i, Kc);
       const uint32_t w[4] = {iv[k].x, iv[k].y, iv[k].z, iv[k].w};
-      const uint32_t o[4] = {old[k].x, old[k].y, old[k].z, old[k].w};
+      const uint32_t o[4] = {odef ? old[k].x : 0u, odef ? old[k].y : 0u, odef ? old[k].z : 0u, odef ? old[k].w : 0u};
       uint32_t       v[4];
-      bool           any = fresh[l];
+      bool           any = fresh[l] || !odef;
 #pragma unroll
       for (int cc = 0; cc < 4; cc++) {
         const uint32_t r0 = w[cc] & 0xffffu, r1 = w[cc] >> 16;

@@ -712,7 +712,7 @@ static bool plan_eq_rm(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi
     er.max_c = std::max(er.max_c, nt ? R.C : 0u);
     er.img   = std::max(er.img, n_max);
   }
-  er.pool = EqRmPool{v.buf, v.stride, v.cb_crc, v.fresh};
+  er.pool = EqRmPool{v.buf, v.stride, v.cb_crc, v.fresh, rm_sparse_writes() ? 1 : 0};
   return er.max_c > 0;
 }
 

@@ -53,6 +53,7 @@ int dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool, const
 // of (K, rv), the decoder buffer length of K, and the pool's buffers
 int      dlsch_rm_inv(mi355_dlsch_t* q, uint32_t K, uint32_t rv, const uint16_t** out);
 uint32_t dlsch_rm_buflen(uint32_t K);
+bool     rm_sparse_writes(); // fresh decoder buffers: empty parity rows left unwritten (SB_ROWMASK)
 struct SoftbufferView {
   int16_t* buf;
   size_t   stride; // int16 per slot

@@ -41,6 +41,9 @@ struct TdecWinArgs {
   // half-iteration's input (DEC1: E, DEC2: A1) is not written; the caller reruns the half-iteration (TdecRun::redo)
   // for the code blocks the check left unfinished
   int             spec;
+  // the buffers are softbuffer-pool slots (in_stride == SB_STRIDE) carrying the parity-row bitmaps of the rate
+  // dematcher at SB_ROWMASK (dlsch_internal.h): parity rows without an LLR are not read
+  int             rowmask;
 };
 
 struct TdecDecideArgs {
@@ -99,6 +102,7 @@ struct TdecRun {
   bool  spec       = false;
   bool* spec_taken = nullptr;
   bool  redo       = false;
+  bool  rowmask    = false; // in are pool slots with parity-row bitmaps (TdecWinArgs::rowmask)
 };
 
 hipError_t tdec_win_launch_halfit(int nsb, const TdecWinArgs& a, hipStream_t s);

@@ -267,9 +267,45 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     __shared__ uint32_t tx_lds[4][2][SEG * 64];
     txb = &tx_lds[threadIdx.x >> 6][0][0];
   }
-  // 8 steps j0..j0+7 of a softbuffer stream as two 16-byte pieces
-  auto tx_load = [&](int so, int j0, uint32_t* r) {
-    const uint4 v0 = txin[so + j0 * 2], v1 = txin[so + (j0 + 4) * 2];
+  // Parity rows (a.rowmask, DL-SCH pool buffers of the 16-window layout): the rate dematcher leaves at int16 offset
+  // SB_ROWMASK of every code block's buffer a bitmap of the rows of its parity streams that hold an LLR (word k of P0,
+  // then of P1 from word SB_ROWMASK_WORDS; all ones when the buffer combines several transmissions).  The other rows
+  // are zero -- at code rate 0.85 (TM4 MCS 27) 7 of every 8 parity rows -- and are not read: a lane's parity load of
+  // row j is predicated on bit j of its code block's word.  ymask: the wave's code blocks' words of the parity stream
+  // this half-iteration reads (P0 for DEC1, P1 for DEC2).
+  constexpr bool RMK = NSB == 16 && !GI;
+  uint32_t*      ymask = nullptr;
+  if constexpr (RMK) {
+    __shared__ uint32_t ym_lds[4][G * SB_ROWMASK_WORDS];
+    ymask = ym_lds[threadIdx.x >> 6];
+#pragma unroll
+    for (int w = q; w < G * SB_ROWMASK_WORDS; w += 64) {
+      const int c2 = grp * G + w / SB_ROWMASK_WORDS;
+      uint32_t  v  = 0xffffffffu;
+      if (a.rowmask && c2 < a.ncb) {
+        const size_t b2 = a.in_idx ? a.in_idx[c2] : (size_t)c2;
+        v = ((const uint32_t*)(a.in + b2 * a.in_stride + SB_ROWMASK))[(dec2 ? SB_ROWMASK_WORDS : 0) + w % SB_ROWMASK_WORDS];
+      }
+      ymask[w] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // row j of code block c (of the wave) holds parity LLRs
+  auto yrow = [&](int c, int j) -> bool {
+    if constexpr (RMK) {
+      return (ymask[c * SB_ROWMASK_WORDS + (j >> 5)] >> (j & 31)) & 1u;
+    } else {
+      return true;
+    }
+  };
+  // 8 steps j0..j0+7 of a softbuffer stream as two 16-byte pieces (the parity stream's pieces of empty rows: zero)
+  auto tx_load = [&](int so, int j0, uint32_t* r, bool par = false) {
+    uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
+    const int tc = (q >> 1) & 7, jr = j0 + (q >> 4);
+    if (!par || yrow(tc, jr)) v0 = txin[so + j0 * 2];
+    if (!par || yrow(tc, jr + 4)) v1 = txin[so + (j0 + 4) * 2];
     r[0] = v0.x; r[1] = v0.y; r[2] = v0.z; r[3] = v0.w;
     r[4] = v1.x; r[5] = v1.y; r[6] = v1.z; r[7] = v1.w;
   };
@@ -299,7 +335,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     for (int i = 0; i < 8; i++) {
       const int j = (L - TDEC_WARMUP) + 8 * b + i;
       xo[i]       = X[j * xs];
-      yo[i]       = Y[j * ys];
+      yo[i]       = yrow(cbg, j) ? Y[j * ys] : 0u;
       if constexpr (has_ap) ao[i] = AP[j * 64];
     }
 #pragma unroll
@@ -332,7 +368,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     for (int i = 0; i < 8; i++) {
       const int j = 8 * b + i;
       xo[i]       = X[j * xs];
-      yo[i]       = Y[j * ys];
+      yo[i]       = yrow(cbg, j) ? Y[j * ys] : 0u;
       if constexpr (has_ap) ao[i] = AP[j * 64];
     }
 #pragma unroll
@@ -382,13 +418,13 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap) {
       if constexpr (TX) { // raw 16-byte pieces, transposed when the segment is consumed
         if constexpr (!dec2) tx_load(txoX, t * SEG, x);
-        tx_load(txoY, t * SEG, y);
+        tx_load(txoY, t * SEG, y, true);
       }
 #pragma unroll
       for (int i = 0; i < SEG; i++) {
         const int j = FULL ? t * SEG + i : min(t * SEG + i, L - 1); // clamp the ragged last segment
         if constexpr (!TX || dec2) x[i] = X[j * xs];
-        if constexpr (!TX) y[i] = Y[j * ys];
+        if constexpr (!TX) y[i] = yrow(cbg, j) ? Y[j * ys] : 0u;
         if constexpr (has_ap) ap[i] = AP[j * 64];
       }
     };
@@ -508,13 +544,13 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap, uint32_t* d, uint32_t* c) {
     if constexpr (TX) {
       if constexpr (!dec2) tx_load(txoX, t * SEG, x);
-      tx_load(txoY, t * SEG, y);
+      tx_load(txoY, t * SEG, y, true);
     }
 #pragma unroll
     for (int i = 0; i < SEG; i++) {
       const int j = FULL ? t * SEG + i : min(t * SEG + i, L - 1); // clamp the ragged last segment
       if constexpr (!TX || dec2) x[i] = Xf[j * xs];
-      if constexpr (!TX) y[i] = Yf[j * ys];
+      if constexpr (!TX) y[i] = yrow(cbg, j) ? Yf[j * ys] : 0u;
       if constexpr (has_ap) ap[i] = APf[j * 64];
       d[i]        = tab[(size_t)j * NL];
     }

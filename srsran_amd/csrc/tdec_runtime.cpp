@@ -288,12 +288,14 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
       if (rq.redo) { // again, the next half-iteration's input only, for the code blocks the check left unfinished
         TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, rq.remaining, A1, E, D, CK, t->dstE, t->dstA,
                        (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, 0, nullptr, out_stride};
+        wa.rowmask = rq.rowmask && g.nsb == 16 && in_stride == SB_STRIDE;
         CHECK_HIP(tdec_win_launch_halfit(g.nsb, wa, s));
         continue;
       }
       TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, rq.remaining, A1, E, D, CK, t->dstE, t->dstA,
                      (int)n, (int)g.L, (int)g.Lp, (int)g.nseg, (int)h, h + 1 == h1,
                      (fuse && h + 1 == h1) ? d_out : nullptr, out_stride};
+      wa.rowmask = rq.rowmask && g.nsb == 16 && in_stride == SB_STRIDE;
       if (rq.spec && fuse && h + 1 == h1 && tdec_win_spec_ok(g.nsb, g.L)) {
         wa.spec = 1;
         if (rq.spec_taken) *rq.spec_taken = true;

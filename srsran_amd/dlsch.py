@@ -26,6 +26,7 @@ def _declare():
     L.mi355_softbuffer_reset_tbs.argtypes = [vp, u32, u32, vp]
     L.mi355_softbuffer_reset_cb.argtypes = [vp, u32, u32, vp]
     L.mi355_softbuffer_reset_all.argtypes = [vp, vp]
+    L.mi355_softbuffer_pool_materialize.argtypes = [vp, u32, u32, vp]
     L.mi355_dlsch_create.argtypes = [C.POINTER(vp), i32]
     L.mi355_dlsch_destroy.argtypes = [vp]
     L.mi355_dlsch_set_max_iterations.argtypes = [vp, u32]
@@ -50,6 +51,14 @@ class SoftbufferPool:
 
     def reset_all(self):
         check(self.L.mi355_softbuffer_reset_all(self.h, None), "softbuffer_reset_all")
+        lib().mi355_device_sync()
+
+    def materialize(self, first: int = 0, n: int | None = None):
+        """Zero the unwritten (logically zero) parity rows of softbuffers [first, first + n) so their memory reads as
+        the reference's buffers would (mi355_softbuffer_pool_materialize); before raw reads of buffer memory."""
+        lib().mi355_device_sync()
+        n = self.nof_sb - first if n is None else n
+        check(self.L.mi355_softbuffer_pool_materialize(self.h, first, n, None), "softbuffer_pool_materialize")
         lib().mi355_device_sync()
 
     def close(self):

@@ -165,6 +165,7 @@ def softbuffer_check(rx, sb: int, e_o: np.ndarray, tbs: int, qm: int, rv: int, w
     L.mi355_softbuffer_pool_buffer.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_int16)), C.POINTER(C.c_uint32),
                                                C.POINTER(C.c_uint32)]
     assert L.mi355_softbuffer_pool_buffer(rx.pool.h, C.byref(buf), C.byref(stride), C.byref(mcb)) == 0
+    rx.pool.materialize(sb, 1)  # unwritten empty parity rows of fresh buffers -> the zeros they stand for
     seg = np.zeros(6, np.uint32)
     oracle.lib().orc_cbsegm(tbs, seg)
     Cn = int(seg[0])

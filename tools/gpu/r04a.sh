@@ -1,11 +1,16 @@
 #!/bin/bash
-# r04a: GPU suite after the reference-pin / ADVICE changes; configs[2] SISO QPSK kernel trace + host phases;
-# pdsch_eq_rm SQ counter passes (VALU / LDS / busy)
+# r04a: GPU suite (reference pins, ADVICE fixes, parity-row bitmaps); bench with the MAP clone; A/B of the parity-row
+# skip (MI355_NO_ROWMASK); fan-out at world 1; configs[2] SISO QPSK trace + host phases; pdsch_eq_rm SQ counters
 set -e
 OUT=gpurun_out/r04a
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/gpu_suite.log 2>&1
+timeout -k 10 400 python3 -u bench.py --no-waterfall > $OUT/bench.json 2> $OUT/bench.err
+for i in 1 2; do
+  MI355_NO_ROWMASK=1 timeout -k 10 200 python3 -u bench.py --no-cpu --no-waterfall --no-roofline > $OUT/ab_off_$i.json 2>> $OUT/ab.err
+  timeout -k 10 200 python3 -u bench.py --no-cpu --no-waterfall --no-roofline > $OUT/ab_on_$i.json 2>> $OUT/ab.err
+done
 timeout -k 10 300 python3 -u bench.py --fanout --steps 3 --warmup 1 --subframes 1024 > $OUT/fanout.json 2> $OUT/fanout.err
 MI355_HOST_PROF=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/siso -o tr -- python3 bench.py --workload siso_qpsk --steps 3 --warmup 1 --no-cpu --no-roofline > $OUT/siso.json 2> $OUT/siso.err
 timeout -k 10 300 python3 -u bench.py --workload siso_qpsk --steps 5 --warmup 2 --no-cpu --no-roofline > $OUT/siso_plain.json 2> $OUT/siso_plain.err
