@@ -75,6 +75,17 @@ int mi355_tdec_batch_halfit_dev(mi355_tdec_batch_t* q,
 #define MI355_TDEC_GENERIC 1
 int mi355_tdec_batch_set_impl(mi355_tdec_batch_t* q, int impl);
 
+/* The generic decoder's schedule (results are bit-exact either way): per_cb 1 = one workgroup per code block, its
+ * serial recursions split into chunks that start from guessed states and are rerun until every chunk boundary
+ * agrees with the exact state (turbodecoder_gen.c:58-198, all half-iterations in one launch); 0 = two code blocks
+ * per lane, fully serial; -1 (default) = per_cb unless the DL-SCH's early stop is wired or a large K <= 400 batch.
+ * warmup: rows / steps each chunk runs in front of itself to guess its entering state (default 32; 0 = guess the
+ * all-zero state, every chunk but the first then reruns: a test of the rerun path). */
+int mi355_tdec_batch_set_generic(mi355_tdec_batch_t* q, int per_cb, int warmup);
+/* Chunk reruns (wrong guesses) of the per-code-block generic decoder since the last call; the first call arms the
+ * counter and returns 0.  Synchronises the device. */
+int mi355_tdec_batch_generic_reruns(mi355_tdec_batch_t* q, uint32_t* reruns);
+
 /* Host-buffer convenience wrapper: copy in, decode, copy out, synchronise. */
 int mi355_tdec_batch_run(mi355_tdec_batch_t* q,
                          const int16_t*      in,

@@ -83,6 +83,24 @@ struct TdecGenDecideArgs {
   int             ncb, K, Kp;
 };
 
+// generic decoder, one workgroup per code block, half-iterations [h0, h1) in one launch (tdec_gen_cb.hip)
+#define TDEC_GEN_CB_L 12 // rows / steps per lane (chunk length)
+#define TDEC_GEN_CB_KP(K) (((K) + 3 + 7) / 8 * 8)
+struct TdecGenCbArgs {
+  const int16_t*  in;       // linear [x z z'] + 12 tails per code block (turbodecoder_gen.c:238-258)
+  size_t          in_stride;
+  const uint32_t* in_idx;   // nullable
+  uint16_t*       ws;       // [ncb][5][Kp]: S, P0, P1, E (natural order + DEC2 tail), A1 -- kept between launches
+  const uint16_t* pi;       // [K] QPP forward table
+  uint8_t*        out;      // decision bytes of half-iteration h1 - 1
+  size_t          out_stride;
+  uint32_t*       reruns;   // nullable: chunk reruns (wrong guesses) are added here
+  int             ncb, K, Kp, h0, h1, warm, persist;
+};
+int        tdec_gen_cb_threads(int K);
+size_t     tdec_gen_cb_lds(int K, int threads);
+hipError_t tdec_gen_cb_launch(const TdecGenCbArgs& a, hipStream_t s);
+
 // Host-side run request used by the batched API and by the DL-SCH decoder (dlsch_runtime.cpp).
 struct TdecRun {
   const int16_t*  in;

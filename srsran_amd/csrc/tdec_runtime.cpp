@@ -80,6 +80,9 @@ struct mi355_tdec_batch {
   std::map<uint32_t, KTables>  tables;     // window-mode tables per K
   std::map<uint32_t, KTables>  gtables;    // generic-mode tables per K
   int                          impl = MI355_TDEC_AUTO;
+  int                          gen_cb   = -1; // generic decoder: per-code-block workgroups (1), pair lanes (0), auto (-1)
+  int                          gen_warm = 32; // its guessed-state warm-up (rows / steps)
+  uint32_t*                    reruns   = nullptr; // device counter of its chunk reruns
   bool                         prof = false;
   std::vector<hipEvent_t>      ev;
   size_t                       ev_used = 0;
@@ -133,8 +136,9 @@ static int get_tables(mi355_tdec_batch_t* q, const Geometry& g, KTables** out)
   return MI355_SUCCESS;
 }
 
-static size_t ws_bytes(const Geometry& g, uint32_t n)
+static size_t ws_bytes(const Geometry& g, uint32_t n, bool cbk = false)
 {
+  if (cbk) return (size_t)n * 5 * TDEC_GEN_CB_KP(g.K) * 2 + 256;
   if (g.nsb) {
     const size_t arr = (size_t)g.ngrp * g.Lp * 64 * 4;
     return 3 * arr + (size_t)g.ngrp * g.nseg * 8 * 64 * 4 + 8 * 256;
@@ -207,6 +211,7 @@ void mi355_tdec_batch_destroy(mi355_tdec_batch_t* q)
   }
   for (auto e : q->ev) (void)hipEventDestroy(e);
   if (q->ws) (void)hipFree(q->ws);
+  if (q->reruns) (void)hipFree(q->reruns);
   if (q->own) (void)hipStreamDestroy(q->own);
   delete q;
 }
@@ -260,9 +265,13 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
   KTables*       t = nullptr;
   int            r = get_tables(q, g, &t);
   if (r) return r;
+  // the generic decoder with one workgroup per code block (tdec_gen_cb.hip) wherever no DL-SCH early stop is wired
+  // (the DL-SCH's K <= 400 blocks keep the two-per-lane kernel and its done flags)
+  const bool cbk = !g.nsb && !rq.done && !rq.remaining && !rq.chk &&
+                   (q->gen_cb == 1 || (q->gen_cb < 0 && (K > 400 || n <= 4096)));
   if (h0 == 0) {
-    if ((r = ensure_ws(q, ws_bytes(g, n)))) return r;
-  } else if (ws_bytes(g, n) > q->ws_cap) {
+    if ((r = ensure_ws(q, ws_bytes(g, n, cbk)))) return r;
+  } else if (ws_bytes(g, n, cbk) > q->ws_cap) {
     return MI355_ERROR; // continuation without a workspace holding the earlier half-iterations
   }
 
@@ -319,6 +328,31 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
       TdecDecideArgs da{D, d_out, out_stride, (int)n, (int)g.L, (int)g.Lp, rq.done, rq.remaining};
       CHECK_HIP(tdec_win_launch_decide(g.nsb, da, s));
     }
+  } else if (cbk) {
+    TdecGenCbArgs ca{};
+    ca.in         = d_in;
+    ca.in_stride  = in_stride;
+    ca.in_idx     = rq.in_idx;
+    ca.ws         = (uint16_t*)q->ws;
+    ca.pi         = t->pi;
+    ca.out        = d_out;
+    ca.out_stride = out_stride;
+    ca.reruns     = q->reruns;
+    ca.ncb        = (int)n;
+    ca.K          = (int)K;
+    ca.Kp         = TDEC_GEN_CB_KP((int)K);
+    ca.h0         = (int)h0;
+    ca.h1         = (int)h1;
+    ca.warm       = q->gen_warm;
+    ca.persist    = 1;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (q->prof) {
+      e0 = next_event(q);
+      e1 = next_event(q);
+      if (e0) (void)hipEventRecord(e0, s);
+    }
+    CHECK_HIP(tdec_gen_cb_launch(ca, s));
+    if (q->prof && e1) (void)hipEventRecord(e1, s);
   } else {
     const size_t arr = (size_t)g.npair * g.Kp * 4;
     auto*        S   = (uint32_t*)carve(arr);
@@ -380,6 +414,32 @@ int mi355_tdec_batch_halfit_dev(mi355_tdec_batch_t* q,
 {
   return mi355_tdec_run_internal(q, TdecRun{d_in, in_stride, nullptr, nullptr, nullptr, n, K, half_idx, half_idx + 1, d_out,
                                             out_stride, (hipStream_t)stream});
+}
+
+int mi355_tdec_batch_set_generic(mi355_tdec_batch_t* q, int per_cb, int warmup)
+{
+  if (!q || per_cb < -1 || per_cb > 1 || warmup < 0) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  q->gen_cb   = per_cb;
+  q->gen_warm = warmup;
+  return MI355_SUCCESS;
+}
+
+int mi355_tdec_batch_generic_reruns(mi355_tdec_batch_t* q, uint32_t* reruns)
+{
+  if (!q || !reruns) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  if (!q->reruns) {
+    CHECK_HIP(hipMalloc(&q->reruns, 4));
+    CHECK_HIP(hipMemset(q->reruns, 0, 4));
+    *reruns = 0;
+    return MI355_SUCCESS;
+  }
+  CHECK_HIP(hipDeviceSynchronize());
+  CHECK_HIP(hipMemcpy(reruns, q->reruns, 4, hipMemcpyDeviceToHost));
+  CHECK_HIP(hipMemset(q->reruns, 0, 4));
+  return MI355_SUCCESS;
 }
 
 int mi355_tdec_batch_set_impl(mi355_tdec_batch_t* q, int impl)

@@ -78,6 +78,21 @@ class TdecBatch:
         check(lib().mi355_tdec_batch_run_dev(self.h, d_in, in_stride, n, K, nhalf, d_out,
                                              out_stride or K // 8, stream), "mi355_tdec_batch_run_dev")
 
+    def set_impl(self, impl: int) -> None:
+        """0 = AUTO (by K, as the AVX2 build), 1 = GENERIC on the linear layout for every K."""
+        check(lib().mi355_tdec_batch_set_impl(self.h, impl), "mi355_tdec_batch_set_impl")
+
+    def set_generic(self, per_cb: int = -1, warmup: int = 32) -> None:
+        """Generic decoder schedule: per_cb 1 = workgroup per code block (chunked, verified), 0 = two blocks per
+        lane (serial), -1 = auto; warmup = the chunks' guess warm-up (0: every chunk but the first reruns)."""
+        check(lib().mi355_tdec_batch_set_generic(self.h, per_cb, warmup), "mi355_tdec_batch_set_generic")
+
+    def generic_reruns(self) -> int:
+        """Chunk reruns of the per-code-block generic decoder since the last call (first call arms, returns 0)."""
+        r = C.c_uint32()
+        check(lib().mi355_tdec_batch_generic_reruns(self.h, C.byref(r)), "generic_reruns")
+        return int(r.value)
+
     def set_profiling(self, on: bool) -> None:
         lib().mi355_tdec_batch_set_profiling(self.h, 1 if on else 0)
 
