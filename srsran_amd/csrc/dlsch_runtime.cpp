@@ -108,7 +108,53 @@ struct mi355_dlsch {
   HostStaging back; // pinned read-back of ret | avg
   // bit h: half-iteration h runs speculatively (spec_policy); until a batch has been seen, the first DEC2
   std::atomic<uint32_t> spec_mask{1u << 1};
+  // calls with at most this many code blocks decode their window-decoder groups on the latency path (tdec_win_lat:
+  // a workgroup per code block, every half-iteration and check in one launch); -1: MI355_DLSCH_LAT_CBS or the default
+  uint32_t* lat_reruns = nullptr;
 };
+
+// the latency path's limit (process-wide): one subframe's code blocks up to a few subframes (srsUE's per-TTI calls);
+// the throughput kernel wins once a batch fills the chip with waves of 8 code blocks.  MI355_DLSCH_LAT_CBS or 0 (off until
+// it beats the throughput path on one subframe).
+static std::atomic<int> g_lat_cbs{-1}, g_lat_warm{32};
+static uint64_t*        g_lat_prof = nullptr; // device counters of tdec_win_lat's phases (mi355_dlsch_latency_profile)
+static int lat_cbs_now()
+{
+  int v = g_lat_cbs.load();
+  if (v < 0) {
+    v = getenv("MI355_DLSCH_LAT_CBS") ? atoi(getenv("MI355_DLSCH_LAT_CBS")) : 0;
+    g_lat_cbs.store(v);
+  }
+  return v;
+}
+
+// measurement: enable = 1 arms the latency kernel's phase counters (zeroed), 0 disarms; out (nullable, 11 u64): the sums
+// since arming (cycles of load, beta first pass, beta reruns, rerun rounds, alpha first pass, alpha reruns, rounds,
+// decisions, check, half-iterations, code blocks)
+extern "C" int mi355_dlsch_latency_profile(int enable, uint64_t* out)
+{
+  if (out && g_lat_prof) {
+    if (hipDeviceSynchronize() != hipSuccess) return MI355_ERROR;
+    if (hipMemcpy(out, g_lat_prof, 11 * 8, hipMemcpyDeviceToHost) != hipSuccess) return MI355_ERROR;
+  }
+  if (enable) {
+    if (!g_lat_prof && hipMalloc(&g_lat_prof, 11 * 8) != hipSuccess) return MI355_ERROR;
+    if (hipMemset(g_lat_prof, 0, 11 * 8) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return MI355_ERROR;
+  } else if (g_lat_prof) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(g_lat_prof);
+    g_lat_prof = nullptr;
+  }
+  return MI355_SUCCESS;
+}
+
+extern "C" int mi355_dlsch_set_latency_path(int max_cbs, int warmup)
+{
+  const int old = lat_cbs_now();
+  if (max_cbs >= 0) g_lat_cbs.store(max_cbs);
+  if (warmup >= 0) g_lat_warm.store(warmup);
+  return old;
+}
 
 // MI355_TDEC_SPEC=0: no speculative DEC2 half-iterations (A/B timing)
 static bool spec_enabled()
@@ -811,10 +857,37 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     doff += (size_t)n * (K / 8);
   }
 
+  // latency path: small calls decode each window-decoder group in one launch (tdec_win_lat.hip)
+  std::vector<char> lat(live.size(), 0);
+  if (!llr8 && total_cb <= (size_t)lat_cbs_now()) {
+    for (size_t i = 0; i < live.size(); i++) {
+      Live&          lv  = live[i];
+      const uint32_t nsb = mi355_tdec_autoimp_get_subblocks(lv.K);
+      if (lv.t8 || nsb == 0 || tdec_lat_threads((int)nsb, (int)lv.K) > 256) continue;
+      TdecLatArgs la{};
+      la.in        = pool->buf;
+      la.in_stride = SB_STRIDE;
+      la.in_idx    = d_slot + lv.off;
+      if ((r = mi355_tdec_win_tables(lv.td, lv.K, &la.dstE, &la.dstA))) return r;
+      la.done    = d_done + lv.off;
+      la.chk     = DlschCheckArgs{d_cb + lv.off, (int)lv.n, lv.K, 0, q->max_its, lv.dec, lv.K / 8, d_data, d_done + lv.off,
+                              d_run, d_run + 1, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1], lv.scale};
+      la.reruns  = q->lat_reruns;
+      la.prof    = g_lat_prof;
+      la.ncb     = (int)lv.n;
+      la.K       = (int)lv.K;
+      la.warm    = g_lat_warm.load();
+      la.rowmask = nsb == 16 && !no_rowmask();
+      CHECK_HIP(tdec_lat_launch((int)nsb, la, s));
+      lat[i] = 1;
+    }
+  }
   const uint32_t spec_mask = spec_enabled() ? q->spec_mask.load() : 0u;
   for (uint32_t h = 0; h < q->max_its; h++) {
     const bool spec = h + 1 == q->max_its || ((spec_mask >> h) & 1u);
-    for (auto& lv : live) {
+    for (size_t li = 0; li < live.size(); li++) {
+      auto& lv = live[li];
+      if (lat[li]) continue;
       if (lv.t8) {
         T8Batch b{};
         b.in = (int8_t*)pool->buf, b.in_stride = SB_STRIDE * sizeof(int16_t), b.slot = d_slot + lv.off;

@@ -66,16 +66,20 @@ struct DciCand {
 
 // What the host replay of one subframe needs from its candidates (pdcch_compact): dci_blind_search (ue_dl.c:450-550)
 // acts only on candidates that decoded (status 2) with the searched RNTI as CRC remainder, so the read-back carries
-// those alone, in slot order: 96 bytes per subframe instead of 1,408.  n > PDCCH_HMAX: the host reads that subframe's
-// full candidate array instead.
-constexpr uint32_t PDCCH_HMAX = 4;
+// those alone, in slot order, as (slot, payload index) pairs into the subframe's distinct payloads (a DCI found at
+// several aggregation levels or in both search spaces decodes to the same bits): 128 bytes per subframe instead of
+// 1,408.  More than PDCCH_HMAX matches or PDCCH_HPAY distinct payloads: the host reads the full candidate array.
+constexpr uint32_t PDCCH_HMAX = 24;
+constexpr uint32_t PDCCH_HPAY = 4;
 struct DciHits {
-  uint32_t n;                 // matching candidates of the subframe
-  uint32_t slot[PDCCH_HMAX];  // slot * PDCCH_FMTS + format slot
-  uint32_t bits[PDCCH_HMAX][4];
-  uint32_t pad[3];
+  uint32_t n;                     // matching candidates of the subframe
+  uint32_t npay;                  // distinct payloads among them
+  uint8_t  slot[PDCCH_HMAX];      // slot * PDCCH_FMTS + format slot
+  uint8_t  pidx[PDCCH_HMAX];      // its payload in bits[]
+  uint32_t bits[PDCCH_HPAY][4];
+  uint32_t pad[2];
 };
-static_assert(sizeof(DciHits) == 96, "DciHits layout");
+static_assert(sizeof(DciHits) == 128, "DciHits layout");
 
 struct CompactArgs {
   const BlindJob* jobs;

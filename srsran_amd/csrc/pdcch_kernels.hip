@@ -685,13 +685,36 @@ __global__ __launch_bounds__(256) void pdcch_compact(CompactArgs a, uint32_t njo
   if (lane < NC) hit = c[lane].status == 2 && c[lane].crc_rem == rnti;
   const uint64_t mask = __builtin_amdgcn_ballot_w64(hit);
   DciHits*       h    = a.hits + job;
-  if (lane == 0) h->n = (uint32_t)__builtin_popcountll(mask);
+  uint32_t       b[4] = {0u, 0u, 0u, 0u};
+  if (hit) {
+#pragma unroll
+    for (int w = 0; w < 4; w++) b[w] = c[lane].bits[w];
+  }
+  // distinct payloads in slot order: the first unassigned hit's bits, every hit with the same bits joins it
+  uint64_t rem = mask;
+  uint32_t np = 0, mine = 0;
+  while (rem) { // wave-uniform
+    const int      f = __builtin_ctzll(rem);
+    const uint32_t f0 = __builtin_amdgcn_readlane(b[0], f), f1 = __builtin_amdgcn_readlane(b[1], f);
+    const uint32_t f2 = __builtin_amdgcn_readlane(b[2], f), f3 = __builtin_amdgcn_readlane(b[3], f);
+    const bool     same = hit && b[0] == f0 && b[1] == f1 && b[2] == f2 && b[3] == f3;
+    if (same) mine = np;
+    if ((int)lane == f && np < PDCCH_HPAY) {
+#pragma unroll
+      for (int w = 0; w < 4; w++) h->bits[np][w] = b[w];
+    }
+    np++;
+    rem &= ~__builtin_amdgcn_ballot_w64(same);
+  }
+  if (lane == 0) {
+    h->n    = (uint32_t)__builtin_popcountll(mask);
+    h->npay = np;
+  }
   if (hit) {
     const uint32_t rank = (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1));
     if (rank < PDCCH_HMAX) {
-      h->slot[rank] = lane;
-#pragma unroll
-      for (int w = 0; w < 4; w++) h->bits[rank][w] = c[lane].bits[w];
+      h->slot[rank] = (uint8_t)lane;
+      h->pidx[rank] = (uint8_t)mine;
     }
   }
 }

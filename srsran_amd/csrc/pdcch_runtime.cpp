@@ -224,7 +224,7 @@ int CtrlState::finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_c
   std::vector<uint32_t> ovf_of;
   std::vector<DciCand>  ovf;
   for (uint32_t i = b; i < e; i++)
-    if (h_hits[i].n > hmax) ovf_of.push_back(i);
+    if (h_hits[i].n > hmax || h_hits[i].npay > PDCCH_HPAY) ovf_of.push_back(i);
   if (!ovf_of.empty()) {
     ovf.resize(ovf_of.size() * NC);
     for (size_t k = 0; k < ovf_of.size(); k++)
@@ -241,7 +241,7 @@ int CtrlState::finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_c
       res[i].nof_cce     = regs.nregs[cfi - 1] / 9;
       // the replay's view of the candidates: the matching ones, everything else "not decoded"
       const DciHits& H = h_hits[i];
-      if (H.n > hmax) { // more matches than the record holds: the subframe's whole candidate array
+      if (H.n > hmax || H.npay > PDCCH_HPAY) { // more than the record holds: the subframe's whole candidate array
         const size_t k = std::lower_bound(ovf_of.begin(), ovf_of.end(), i) - ovf_of.begin();
         memcpy(cand, ovf.data() + k * NC, sizeof(cand));
       } else {
@@ -250,7 +250,7 @@ int CtrlState::finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_c
           DciCand& c = cand[H.slot[k]];
           c.status   = 2;
           c.crc_rem  = plan_of[i].rnti;
-          memcpy(c.bits, H.bits[k], sizeof(c.bits));
+          memcpy(c.bits, H.bits[H.pidx[k]], sizeof(c.bits));
         }
       }
       res[i].nof_dci = blind_search_replay(cell, res[i].nof_cce, rntis[i], cfgs[i], plan_of[i], cand,

@@ -385,12 +385,12 @@ hipError_t tdec_gen_cb_launch(const TdecGenCbArgs& a, hipStream_t s)
 {
   const int    T   = tdec_gen_cb_threads(a.K);
   const size_t lds = tdec_gen_cb_lds(a.K, T);
-  static bool  attr = false;
-  if (!attr) {
+  static size_t attr = 64 * 1024; // dynamic LDS beyond 64 KB is opted into per size (K = 6144: 90 KB)
+  if (lds > attr) {
     hipError_t e = hipFuncSetAttribute((const void*)tdec_gen_cb<TDEC_GEN_CB_L>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    attr = true;
+    attr = lds;
   }
   hipLaunchKernelGGL(tdec_gen_cb<TDEC_GEN_CB_L>, dim3(a.ncb), dim3(T), lds, s, a);
   return hipGetLastError();

@@ -101,6 +101,25 @@ int        tdec_gen_cb_threads(int K);
 size_t     tdec_gen_cb_lds(int K, int threads);
 hipError_t tdec_gen_cb_launch(const TdecGenCbArgs& a, hipStream_t s);
 
+// latency path of the DL-SCH: one workgroup per (window-decoder) code block, every half-iteration and the code-block
+// check in one launch (tdec_win_lat.hip)
+#define TDEC_LAT_LC 12 // steps per chunk
+struct TdecLatArgs {
+  const int16_t*  in;       // softbuffer-layout decoder buffers
+  size_t          in_stride;
+  const uint32_t* in_idx;   // buffer of batch code block b
+  const uint32_t* dstE;     // [L][NL] interleaver destinations (tdec_runtime.cpp get_tables)
+  const uint32_t* dstA;
+  uint8_t*        done;     // in: 3 = decoded earlier (skipped); out: 1 CRC ok / 2 given up
+  DlschCheckArgs  chk;      // desc, data, its, sb_crc, CRC tables and scales, max_its (h, dec, next unused)
+  uint32_t*       reruns;   // nullable: chunk reruns
+  uint64_t*       prof;     // nullable (measurement): [11] phase cycles / counts summed over code blocks (tdec_win_lat.hip)
+  int             ncb, K, warm, rowmask;
+};
+int        tdec_lat_threads(int nsb, int K);
+size_t     tdec_lat_lds(int K, int threads);
+hipError_t tdec_lat_launch(int nsb, const TdecLatArgs& a, hipStream_t s);
+
 // Host-side run request used by the batched API and by the DL-SCH decoder (dlsch_runtime.cpp).
 struct TdecRun {
   const int16_t*  in;
@@ -135,3 +154,5 @@ hipError_t tdec_gen_launch_decide(const TdecGenDecideArgs& a, hipStream_t s);
 
 struct mi355_tdec_batch;
 int mi355_tdec_run_internal(mi355_tdec_batch* q, const mi355::TdecRun& r);
+// the window decoder's interleaver destination tables of K (built on first use); 0 on success
+int mi355_tdec_win_tables(mi355_tdec_batch* q, uint32_t K, const uint32_t** dstE, const uint32_t** dstA);

@@ -278,15 +278,13 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   if constexpr (RMK) {
     __shared__ uint32_t ym_lds[4][G * SB_ROWMASK_WORDS];
     ymask = ym_lds[threadIdx.x >> 6];
+    // each code block's own NL lanes fill its words: the lanes of missing or finished code blocks have returned above
+    // (TX waves run all 8 code blocks, so every word a TX load reads is filled too)
 #pragma unroll
-    for (int w = q; w < G * SB_ROWMASK_WORDS; w += 64) {
-      const int c2 = grp * G + w / SB_ROWMASK_WORDS;
-      uint32_t  v  = 0xffffffffu;
-      if (a.rowmask && c2 < a.ncb) {
-        const size_t b2 = a.in_idx ? a.in_idx[c2] : (size_t)c2;
-        v = ((const uint32_t*)(a.in + b2 * a.in_stride + SB_ROWMASK))[(dec2 ? SB_ROWMASK_WORDS : 0) + w % SB_ROWMASK_WORDS];
-      }
-      ymask[w] = v;
+    for (int w = l; w < SB_ROWMASK_WORDS; w += NL) {
+      uint32_t v = 0xffffffffu;
+      if (a.rowmask) v = ((const uint32_t*)(a.in + bidx * a.in_stride + SB_ROWMASK))[(dec2 ? SB_ROWMASK_WORDS : 0) + w];
+      ymask[cbg * SB_ROWMASK_WORDS + w] = v;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

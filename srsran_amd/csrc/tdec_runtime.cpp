@@ -242,6 +242,19 @@ int mi355_tdec_batch_kernel_stats(mi355_tdec_batch_t* q, double* ms, uint32_t* l
 // Launch half-iterations [h0, h1) on the workspace; decisions after h1-1 when `decide`.
 } // extern "C"
 
+int mi355_tdec_win_tables(mi355_tdec_batch_t* q, uint32_t K, const uint32_t** dstE, const uint32_t** dstA)
+{
+  if (!q || cb_index(K) < 0 || mi355_tdec_autoimp_get_subblocks(K) == 0) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  const Geometry g = geometry(K, 1, MI355_TDEC_AUTO);
+  KTables*       t = nullptr;
+  const int      r = get_tables(q, g, &t);
+  if (r) return r;
+  *dstE = t->dstE;
+  *dstA = t->dstA;
+  return MI355_SUCCESS;
+}
+
 int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
 {
   const int16_t* d_in = rq.in;

@@ -10,6 +10,17 @@ from srsran_amd.dlsch import Dlsch, SoftbufferPool
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(params=[(512, 32), (0, 32), (512, 0)], ids=["latency", "throughput", "latency_warm0"], autouse=True)
+def dlsch_path(request):
+    """Every test on both turbo paths: the latency path (tdec_win_lat, one launch per K group for small calls), the
+    half-iteration-per-launch throughput path, and the latency path with no guess warm-up (every chunk guess wrong,
+    the rerun path carries the decode)."""
+    from srsran_amd import lib
+    old = lib().mi355_dlsch_set_latency_path(*request.param)
+    yield
+    lib().mi355_dlsch_set_latency_path(old, 32)
+
 # (tbs, Qm, G, snr_db): SISO QPSK MCS9 (C=3, K=5312), TM4 QAM256 MCS27 codeword (C=16, K=6144),
 # gamma != 0 cases, 16-window and 8-window and generic single-CB sizes
 CASES = [(15840, 2, 30000, 3.0), (97896, 8, 115200, 9.0), (97896, 8, 115200, 5.5), (30576, 6, 36300, 4.5),
