@@ -74,15 +74,13 @@ int mi355_dlsch_set_max_iterations(mi355_dlsch_t* q, uint32_t max_iterations);
 void mi355_dlsch_set_profiling(mi355_dlsch_t* q, int enable);
 
 /* Latency path (process-wide): a decode call with at most max_cbs code blocks decodes its window-decoder (K > 400)
- * groups with one workgroup per code block, every half-iteration and the CRC early stop in one launch, each window's
- * recursions split into chunks started from guessed states and rerun until every chunk boundary is exact (results
- * identical to the half-iteration-per-launch path).  warmup: the chunks' guess warm-up (0 = every guess wrong: a
- * test of the rerun path).  A negative argument keeps the current value.  Default max_cbs: MI355_DLSCH_LAT_CBS or
- * 0 (off).  Returns the previous max_cbs. */
-int mi355_dlsch_set_latency_path(int max_cbs, int warmup);
+ * groups with one wave per code block, every half-iteration and the CRC early stop in one launch, alpha and beta of
+ * each window run at the same time (results identical to the half-iteration-per-launch path).  A negative argument
+ * keeps the current value.  Default: MI355_DLSCH_LAT_CBS or 0 (off).  Returns the previous max_cbs. */
+int mi355_dlsch_set_latency_path(int max_cbs);
 /* Measurement: enable = 1 (re)arms the latency path's phase counters, 0 disarms them; out (nullable, 11 uint64) receives
- * their sums since arming: shader-clock cycles of the buffer load, beta first pass, beta reruns, (rerun rounds), alpha
- * first pass, alpha reruns, (rounds), decisions, code-block check, then half-iterations and code blocks.
+ * their sums since arming: shader-clock cycles of the buffer load, the first halves, the second halves (with the
+ * outputs), the decisions, the code-block check, (5-8 unused), then half-iterations and code blocks.
  * Synchronises the device. */
 int mi355_dlsch_latency_profile(int enable, uint64_t* out);
 int  mi355_dlsch_kernel_stats(mi355_dlsch_t* q, double* ms, uint32_t* launches);

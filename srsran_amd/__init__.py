@@ -48,7 +48,7 @@ def _declare(L: C.CDLL) -> None:
     L.mi355_tdec_batch_halfit_dev.argtypes = [vp, vp, sz, u32, u32, u32, vp, sz, vp]
     L.mi355_tdec_batch_set_impl.argtypes = [vp, i32]
     L.mi355_tdec_batch_set_generic.argtypes = [vp, i32, i32]
-    L.mi355_dlsch_set_latency_path.argtypes = [i32, i32]
+    L.mi355_dlsch_set_latency_path.argtypes = [i32]
     L.mi355_dlsch_latency_profile.argtypes = [i32, vp]
     L.mi355_tdec_batch_generic_reruns.argtypes = [vp, C.POINTER(u32)]
     L.mi355_tdec_batch_set_profiling.argtypes = [vp, i32]

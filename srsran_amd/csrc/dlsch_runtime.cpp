@@ -110,13 +110,12 @@ struct mi355_dlsch {
   std::atomic<uint32_t> spec_mask{1u << 1};
   // calls with at most this many code blocks decode their window-decoder groups on the latency path (tdec_win_lat:
   // a workgroup per code block, every half-iteration and check in one launch); -1: MI355_DLSCH_LAT_CBS or the default
-  uint32_t* lat_reruns = nullptr;
 };
 
 // the latency path's limit (process-wide): one subframe's code blocks up to a few subframes (srsUE's per-TTI calls);
 // the throughput kernel wins once a batch fills the chip with waves of 8 code blocks.  MI355_DLSCH_LAT_CBS or 0 (off until
 // it beats the throughput path on one subframe).
-static std::atomic<int> g_lat_cbs{-1}, g_lat_warm{32};
+static std::atomic<int> g_lat_cbs{-1};
 static uint64_t*        g_lat_prof = nullptr; // device counters of tdec_win_lat's phases (mi355_dlsch_latency_profile)
 static int lat_cbs_now()
 {
@@ -129,8 +128,7 @@ static int lat_cbs_now()
 }
 
 // measurement: enable = 1 arms the latency kernel's phase counters (zeroed), 0 disarms; out (nullable, 11 u64): the sums
-// since arming (cycles of load, beta first pass, beta reruns, rerun rounds, alpha first pass, alpha reruns, rounds,
-// decisions, check, half-iterations, code blocks)
+// since arming (include/srsran_amd/dlsch.h)
 extern "C" int mi355_dlsch_latency_profile(int enable, uint64_t* out)
 {
   if (out && g_lat_prof) {
@@ -148,11 +146,10 @@ extern "C" int mi355_dlsch_latency_profile(int enable, uint64_t* out)
   return MI355_SUCCESS;
 }
 
-extern "C" int mi355_dlsch_set_latency_path(int max_cbs, int warmup)
+extern "C" int mi355_dlsch_set_latency_path(int max_cbs)
 {
   const int old = lat_cbs_now();
   if (max_cbs >= 0) g_lat_cbs.store(max_cbs);
-  if (warmup >= 0) g_lat_warm.store(warmup);
   return old;
 }
 
@@ -863,7 +860,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
     for (size_t i = 0; i < live.size(); i++) {
       Live&          lv  = live[i];
       const uint32_t nsb = mi355_tdec_autoimp_get_subblocks(lv.K);
-      if (lv.t8 || nsb == 0 || tdec_lat_threads((int)nsb, (int)lv.K) > 256) continue;
+      if (lv.t8 || nsb == 0 || tdec_lat_lds((int)lv.K, (int)nsb) > 160 * 1024 - 64) continue;
       TdecLatArgs la{};
       la.in        = pool->buf;
       la.in_stride = SB_STRIDE;
@@ -872,11 +869,9 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
       la.done    = d_done + lv.off;
       la.chk     = DlschCheckArgs{d_cb + lv.off, (int)lv.n, lv.K, 0, q->max_its, lv.dec, lv.K / 8, d_data, d_done + lv.off,
                               d_run, d_run + 1, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1], lv.scale};
-      la.reruns  = q->lat_reruns;
       la.prof    = g_lat_prof;
       la.ncb     = (int)lv.n;
       la.K       = (int)lv.K;
-      la.warm    = g_lat_warm.load();
       la.rowmask = nsb == 16 && !no_rowmask();
       CHECK_HIP(tdec_lat_launch((int)nsb, la, s));
       lat[i] = 1;

@@ -1107,7 +1107,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   const GLB float2*   hp[4];
   h_ptrs(J, hp);
   const uint32_t re0 = rp / Qm, re1 = (rp + n_e) / Qm, pairs = (J.nof_re + 1) / 2;
-  const uint32_t p1  = min((re1 + 1) / 2, pairs);
+  const uint32_t p1  = P.diag == 2 ? 0u : min((re1 + 1) / 2, pairs);
   for (uint32_t pr = re0 / 2 + tid; pr < p1; pr += ER_THREADS) {
     const uint32_t m = map2[pr];
     cf             Y[2][2], H[2][4];
@@ -1144,6 +1144,10 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   }
   if (tid < 2) imgs[tid * img + n_e] = 0; // the zero slot: table entries without an LLR (RM_NONE, >= n_e) read it
   __syncthreads();
+  if (P.diag == 1) {
+    if (imgs[tid] == 12345 && imgs[img + tid] == 777) P.sb[tid] = 1; // keep the equaliser's work alive
+    return;
+  }
   // rate dematching of each layer's image into its softbuffer (dlsch_rm_rx's gather, E <= N); both layers through
   // one pass when they share the table (same K and rv: the usual case), so the table is read and decoded once
   {

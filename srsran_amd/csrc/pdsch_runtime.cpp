@@ -713,6 +713,8 @@ static bool plan_eq_rm(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi
     er.img   = std::max(er.img, n_max);
   }
   er.pool = EqRmPool{v.buf, v.stride, v.cb_crc, v.fresh, rm_sparse_writes() ? 1 : 0};
+  static const int eqrm_diag = getenv("MI355_EQRM_DIAG") ? atoi(getenv("MI355_EQRM_DIAG")) : 0;
+  er.pool.diag = eqrm_diag;
   return er.max_c > 0;
 }
 

@@ -128,6 +128,7 @@ struct Cb {
 // rows from k0 down to k1 (k0 >= k1), normalised as turbodecoder_gen.c:105-110
 __device__ __forceinline__ void beta_run(const Cb& cb, short s[8], int k0, int k1)
 {
+#pragma unroll 4
   for (int k = k0; k >= k1; k--) {
     short x, y;
     cb.in(k, x, y);
@@ -139,6 +140,7 @@ __device__ __forceinline__ void beta_run(const Cb& cb, short s[8], int k0, int k
 // alpha steps k0..k1 (1-based, input k-1) without outputs
 __device__ __forceinline__ void alpha_run(const Cb& cb, short s[8], int k0, int k1)
 {
+#pragma unroll 4
   for (int k = k0; k <= k1; k++) {
     short x, y, c0[8], c1[8];
     cb.in(k - 1, x, y);
@@ -149,14 +151,15 @@ __device__ __forceinline__ void alpha_run(const Cb& cb, short s[8], int k0, int 
   }
 }
 
-// the chunk's rows hi .. lo+1 (row lo+1+i in rows[i]); lo % 4 == 0
-template <int L>
+// the chunk's rows hi .. lo+1 (row lo+1+i in rows[i]); lo % 4 == 0.  FULL: K % L == 0, every chunk whole (no
+// per-step guards, so the unrolled steps' loads are issued together)
+template <int L, bool FULL>
 __device__ __forceinline__ void beta_chunk(const Cb& cb, short s[8], short rows[L][8], int lo, int hi)
 {
 #pragma unroll
   for (int i = L - 1; i >= 0; i--) {
     const int k = lo + 1 + i;
-    if (k <= hi) {
+    if (FULL || k <= hi) {
       short x, y;
       cb.in(k, x, y);
       beta_row(s, x, y);
@@ -170,13 +173,13 @@ __device__ __forceinline__ void beta_chunk(const Cb& cb, short s[8], short rows[
 // the chunk's alpha steps lo+1 .. hi with the output LLRs (turbodecoder_gen.c:166-194) and the extrinsic
 // scatter of turbodecoder_iter.h:104-128 folded in: DEC1 writes E = out - a-priori (natural order), DEC2
 // A1[pi[k]] = out - app2
-template <int L>
+template <int L, bool FULL>
 __device__ __forceinline__ void alpha_chunk(const Cb& cb, short s[8], const short rows[L][8], int lo, int hi)
 {
 #pragma unroll
   for (int i = 0; i < L; i++) {
     const int k = lo + 1 + i;
-    if (k <= hi) {
+    if (FULL || k <= hi) {
       short x, y, c0[8], c1[8];
       const int pos = k - 1;
       short     ain = 0;
@@ -214,7 +217,7 @@ __device__ __forceinline__ void alpha_chunk(const Cb& cb, short s[8], const shor
 
 } // namespace
 
-template <int L>
+template <int L, bool FULL>
 __global__ __launch_bounds__(512) void tdec_gen_cb(TdecGenCbArgs a)
 {
   extern __shared__ uint4 smem4[];
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(512) void tdec_gen_cb(TdecGenCbArgs a)
         beta_run(cb, st, k0, hi + 1);
       }
       gs[c] = pack(st);
-      beta_chunk<L>(cb, st, rows, lo, hi);
+      beta_chunk<L, FULL>(cb, st, rows, lo, hi);
       es[c] = pack(st);
     }
     for (;;) {
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(512) void tdec_gen_cb(TdecGenCbArgs a)
       if (bad) {
         gs[c] = nb;
         unpack(nb, st);
-        beta_chunk<L>(cb, st, rows, lo, hi);
+        beta_chunk<L, FULL>(cb, st, rows, lo, hi);
         es[c] = pack(st);
         reruns++;
       }
@@ -331,7 +334,7 @@ __global__ __launch_bounds__(512) void tdec_gen_cb(TdecGenCbArgs a)
         alpha_run(cb, st, k0, lo);
       }
       gs[c] = pack(st);
-      alpha_chunk<L>(cb, st, rows, lo, hi);
+      alpha_chunk<L, FULL>(cb, st, rows, lo, hi);
       es[c] = pack(st);
     }
     for (;;) {
@@ -345,7 +348,7 @@ __global__ __launch_bounds__(512) void tdec_gen_cb(TdecGenCbArgs a)
       if (bad) {
         gs[c] = pv;
         unpack(pv, st);
-        alpha_chunk<L>(cb, st, rows, lo, hi);
+        alpha_chunk<L, FULL>(cb, st, rows, lo, hi);
         es[c] = pack(st);
         reruns++;
       }
@@ -385,14 +388,19 @@ hipError_t tdec_gen_cb_launch(const TdecGenCbArgs& a, hipStream_t s)
 {
   const int    T   = tdec_gen_cb_threads(a.K);
   const size_t lds = tdec_gen_cb_lds(a.K, T);
-  static size_t attr = 64 * 1024; // dynamic LDS beyond 64 KB is opted into per size (K = 6144: 90 KB)
-  if (lds > attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)tdec_gen_cb<TDEC_GEN_CB_L>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const bool   full = a.K % TDEC_GEN_CB_L == 0;
+  const void*  f    = full ? (const void*)tdec_gen_cb<TDEC_GEN_CB_L, true> : (const void*)tdec_gen_cb<TDEC_GEN_CB_L, false>;
+  static size_t attr[2] = {64 * 1024, 64 * 1024}; // dynamic LDS beyond 64 KB is opted into per size (K = 6144: 90 KB)
+  if (lds > attr[full]) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    attr = lds;
+    attr[full] = lds;
   }
-  hipLaunchKernelGGL(tdec_gen_cb<TDEC_GEN_CB_L>, dim3(a.ncb), dim3(T), lds, s, a);
+  if (full) {
+    hipLaunchKernelGGL((tdec_gen_cb<TDEC_GEN_CB_L, true>), dim3(a.ncb), dim3(T), lds, s, a);
+  } else {
+    hipLaunchKernelGGL((tdec_gen_cb<TDEC_GEN_CB_L, false>), dim3(a.ncb), dim3(T), lds, s, a);
+  }
   return hipGetLastError();
 }
 

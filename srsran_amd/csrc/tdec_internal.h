@@ -101,9 +101,8 @@ int        tdec_gen_cb_threads(int K);
 size_t     tdec_gen_cb_lds(int K, int threads);
 hipError_t tdec_gen_cb_launch(const TdecGenCbArgs& a, hipStream_t s);
 
-// latency path of the DL-SCH: one workgroup per (window-decoder) code block, every half-iteration and the code-block
-// check in one launch (tdec_win_lat.hip)
-#define TDEC_LAT_LC 12 // steps per chunk
+// latency path of the DL-SCH: one wave per (window-decoder) code block, every half-iteration and the code-block check
+// in one launch, alpha and beta of each window at the same time (tdec_win_lat.hip)
 struct TdecLatArgs {
   const int16_t*  in;       // softbuffer-layout decoder buffers
   size_t          in_stride;
@@ -112,12 +111,10 @@ struct TdecLatArgs {
   const uint32_t* dstA;
   uint8_t*        done;     // in: 3 = decoded earlier (skipped); out: 1 CRC ok / 2 given up
   DlschCheckArgs  chk;      // desc, data, its, sb_crc, CRC tables and scales, max_its (h, dec, next unused)
-  uint32_t*       reruns;   // nullable: chunk reruns
   uint64_t*       prof;     // nullable (measurement): [11] phase cycles / counts summed over code blocks (tdec_win_lat.hip)
-  int             ncb, K, warm, rowmask;
+  int             ncb, K, rowmask;
 };
-int        tdec_lat_threads(int nsb, int K);
-size_t     tdec_lat_lds(int K, int threads);
+size_t     tdec_lat_lds(int K, int nsb);
 hipError_t tdec_lat_launch(int nsb, const TdecLatArgs& a, hipStream_t s);
 
 // Host-side run request used by the batched API and by the DL-SCH decoder (dlsch_runtime.cpp).

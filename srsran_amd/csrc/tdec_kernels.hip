@@ -56,6 +56,13 @@ __device__ __forceinline__ uint32_t from_next(uint32_t v)
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xf, 0xf, true);
 }
 
+// natural decision bit m (MSB first within its byte, turbodecoder_win.h:973-993) into an LDS byte bitmap
+__device__ __forceinline__ void bm_set(uint32_t* bm, uint32_t m, bool v)
+{
+  const uint32_t by = m >> 3;
+  if (v) atomicOr(&bm[by >> 2], 1u << (((by & 3) << 3) + 7 - (m & 7)));
+}
+
 // ---------------------------------------------------------------------------- trellis steps
 // State numbering reg0<<2|reg1<<1|reg2, branch metric u*x + p*y (turbocoder.c:403-421).
 
@@ -508,8 +515,10 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   const uint32_t* tab  = (dec2 ? a.dstA : a.dstE) + l;
   const int       lane0 = cbg * NL; // first lane of this code block inside the 64-lane row
   constexpr bool  dec_o   = OUTK == 1 || OUTK == 3;
-  constexpr bool  wr_bits = !dec2 && dec_o; // fused decision bytes (DEC1: ext1 in natural order)
-  constexpr bool  wr_bm   = dec2 && dec_o;  // fused decision bytes (DEC2: app1 de-interleaved)
+  // fused decision bytes: DEC1's ext1 in natural order as whole bytes per window and segment when windows are
+  // byte-aligned (FULL: L % 8 == 0), else (and DEC2's app1, de-interleaved) bit by bit into an LDS bitmap
+  constexpr bool  wr_bits = !dec2 && dec_o && FULL;
+  constexpr bool  wr_bm   = dec_o && (dec2 || !FULL);
   constexpr bool  wr_d    = OUTK == 2;
   constexpr bool  wr_a1   = !(dec2 && OUTK == 3);  // OUTK 3 (speculative, DEC2): the next DEC1's a-priori not written
   constexpr bool  wr_e    = !(!dec2 && OUTK == 3); // OUTK 3 (DEC1): the next DEC2's input not written
@@ -519,7 +528,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   // code block (not 192): the 8 code blocks of a wave start in different banks.
   constexpr int BMW = NSB == 16 ? 193 : 25; // u32 words per code block (K <= 6144 / K <= 800)
   uint32_t*     bm  = nullptr;
-  if constexpr (dec2 || wr_bits) {
+  if constexpr (dec2 || wr_bits || wr_bm) {
     __shared__ uint32_t bm_lds[4 * G * BMW];
     bm = bm_lds + ((threadIdx.x >> 6) * G + cbg) * BMW;
     if constexpr (wr_bm) {
@@ -611,6 +620,10 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
               E16[ohi] = out.y;
             }
             bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
+            if constexpr (wr_bm) {
+              bm_set(bm, 2 * l * L + j, out.x > 0);
+              bm_set(bm, (2 * l + 1) * L + j, out.y > 0);
+            }
           } else {
             if constexpr (wr_a1) {
               A16[olo] = out.x;
@@ -618,10 +631,8 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
             }
             if constexpr (wr_bm) {
               const uint32_t jd = (tb & 0xffffu) >> 7, wlo = tb & 15u, whi = (tb >> 16) & 15u;
-              const uint32_t blo = wlo * (L / 8) + (jd >> 3), bhi = whi * (L / 8) + (jd >> 3);
-              const uint32_t sh  = 7 - (jd & 7);
-              atomicOr(&bm[blo >> 2], (uint32_t)(out.x > 0) << (((blo & 3) << 3) + sh));
-              atomicOr(&bm[bhi >> 2], (uint32_t)(out.y > 0) << (((bhi & 3) << 3) + sh));
+              bm_set(bm, wlo * L + jd, out.x > 0);
+              bm_set(bm, whi * L + jd, out.y > 0);
             }
           }
         }
@@ -688,6 +699,10 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
           }
           if constexpr (wr_d) WG_AT(a.D, j) = W(out);
           bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
+          if constexpr (wr_bm) { // windows not byte-aligned: natural bits 2l L + j, (2l + 1) L + j
+            bm_set(bm, 2 * l * L + j, out.x > 0);
+            bm_set(bm, (2 * l + 1) * L + j, out.y > 0);
+          }
         } else {
           // a1 = app1 - ext1 (wrapping) of the next DEC1, turbodecoder_iter.h:108-110
           if constexpr (wr_a1) {
@@ -695,12 +710,10 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
             A16[olo]     = av.x;
             A16[ohi]     = av.y;
           }
-          if constexpr (wr_bm) { // natural bit w*L + j': byte w*L/8 + j'/8, bit 7 - j'%8 (turbodecoder_win.h:973-993)
+          if constexpr (wr_bm) { // natural bit w*L + j' (turbodecoder_win.h:973-993)
             const uint32_t jd = (tb & 0xffffu) >> 7, wlo = tb & 15u, whi = (tb >> 16) & 15u;
-            const uint32_t blo = wlo * (L / 8) + (jd >> 3), bhi = whi * (L / 8) + (jd >> 3);
-            const uint32_t sh  = 7 - (jd & 7);
-            atomicOr(&bm[blo >> 2], (uint32_t)(out.x > 0) << (((blo & 3) << 3) + sh));
-            atomicOr(&bm[bhi >> 2], (uint32_t)(out.y > 0) << (((bhi & 3) << 3) + sh));
+            bm_set(bm, wlo * L + jd, out.x > 0);
+            bm_set(bm, whi * L + jd, out.y > 0);
           }
           if constexpr (wr_d) {
             D16[olo] = out.x;

@@ -305,7 +305,10 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
     // the decisions of the last half-iteration are packed into bytes by the MAP kernel itself when the windows
     // are byte aligned (DEC1: in registers, natural order; DEC2: an LDS bitmap), which saves the D array and
     // the decide pass
-    const bool fuse = g.L % 8 == 0 && out_stride % 8 == 0 && (uintptr_t)d_out % 8 == 0;
+    // (windows not byte-aligned: through the LDS bitmap, when the K/8 bytes split evenly over the NL lanes' 8-byte
+    // stores and the fused check's chunks)
+    const bool fuse = (g.L % 8 == 0 || (K % 64 == 0 && (K / 8) % (g.nsb / 2) == 0)) && out_stride % 8 == 0 &&
+                      (uintptr_t)d_out % 8 == 0;
     for (uint32_t h = h0; h < h1; h++) {
       if (rq.redo) { // again, the next half-iteration's input only, for the code blocks the check left unfinished
         TdecWinArgs wa{d_in, in_stride, rq.in_idx, rq.done, rq.remaining, A1, E, D, CK, t->dstE, t->dstA,

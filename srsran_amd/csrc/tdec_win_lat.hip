@@ -4,19 +4,18 @@
 // cc_worker.cc:423-470: a few dozen code blocks per call).  The throughput kernel (tdec_kernels.hip) gives each
 // code block 8 lanes, one per pair of the reference's 16 windows, so a subframe's 32 blocks are 4 waves whose
 // 384-step recursions run serially, and every half-iteration is a launch of its own: 140 us per half-iteration.
-// Here ONE workgroup decodes one code block through all its half-iterations (sch.c:415-450: CRC early stop in the
-// kernel), with every window's recursions split further into chunks of LC steps:
-//   lane (chunk j, window pair l) runs rows / steps (j LC, (j + 1) LC] of windows 2l, 2l+1 (packed int16x2, the
-//   reference's saturating arithmetic and its loop-index normalisation, turbodecoder_win.h:480-832) from a GUESSED
-//   entering state -- W steps of the same window in front of the chunk from an all-zero state, or the exact window
-//   boundary where the chunk is near it -- and the chunks whose guess differs from the exact state their neighbour
-//   ends in are rerun until every boundary agrees (tdec_gen_cb.hip: a chunk entered in the reference's state computes
-//   the reference's values, so the result is exact for any input).
-// Inputs (softbuffer layout, rm_turbo.c:263-277), a-priori and extrinsic live in LDS for the whole decode; beta rows
-// stay in registers between the two passes of a chunk.  Decisions come from the extrinsic and a-priori arrays
-// (DEC1's output is E + A1 at the natural position, DEC2's A1 + E at the interleaved one), the code-block check is
-// dlsch_cb_check's (CRC24B / CRC24A over the K/8 decision bytes, payload bytes at cb * rlen / 8, done / iteration /
-// softbuffer-CRC flags).
+// Here ONE wave decodes one code block through all its half-iterations (sch.c:415-450: the CRC early stop in the
+// kernel), and each window's two recursions run at the same time (the "X" schedule): lane l of the first NL lanes runs
+// alpha forward over windows (2l, 2l+1) while lane l of the next NL runs beta backward over the same windows, each
+// storing its metrics for its first half of the window in LDS; past the middle the alpha lane produces the outputs of
+// the second half from the stored beta rows and the beta lane those of the first half from the stored alpha states.
+// Every value is the reference's (turbodecoder_win.h:480-832: the same saturating operations on the same operands,
+// the window boundaries from the same 40-step warm-ups, loop-index normalisation), so the serial path per
+// half-iteration is 40 + L steps instead of the throughput kernel's 40 + L backward and L forward, with no launch
+// per half-iteration.  Inputs, a-priori, extrinsic and metrics live in LDS (160 KB at K = 6144).  Decisions come
+// from the extrinsic and a-priori arrays (DEC1's output is E + A1 at the natural position, DEC2's A1 + E at the
+// interleaved one), the check is dlsch_cb_check's (CRC24B / CRC24A over the K/8 decision bytes, payload bytes at
+// cb * rlen / 8, done / iteration / softbuffer-CRC flags).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -223,259 +222,261 @@ template <int NSB> struct Blk {
   }
 };
 
-// rows a+1 .. kt (kt = b, or L - 1 below the boundary row of the last chunk) into rows[k - a - 1]
-template <int NSB, int LC>
-__device__ __forceinline__ void beta_chunk(const Blk<NSB>& B, int l, v2s s[8], v2s (&rows)[LC][8], int a, int kt)
+// output LLR of a step from its alpha entering state, inputs and beta row (turbodecoder_win.h:771-832); the next
+// alpha state in s when adv
+__device__ __forceinline__ v2s out_llr(v2s s[8], v2s x, v2s y, const v2s (&row)[8], bool adv)
 {
+  v2s c0[8], c1[8], t0[8], t1[8];
+  acands(s, x, y, c0, c1);
 #pragma unroll
-  for (int r = LC - 1; r >= 0; r--) {
-    const int k = a + 1 + r;
-    if (k <= kt) {
-      v2s x, y;
-      B.in(k, l, x, y);
-      bstep<true>(s, x, y);
-#pragma unroll
-      for (int i = 0; i < 8; i++) rows[r][i] = s[i];
-      if ((k & 1) == 0) snorm(s); // k >= 1
-    }
+  for (int q = 0; q < 8; q++) {
+    t0[q] = sadd2(row[q], c0[q]);
+    t1[q] = sadd2(row[q], c1[q]);
   }
+  const v2s m0 = vmax2(vmax2(vmax2(t0[0], t0[1]), vmax2(t0[2], t0[3])), vmax2(vmax2(t0[4], t0[5]), vmax2(t0[6], t0[7])));
+  const v2s m1 = vmax2(vmax2(vmax2(t1[0], t1[1]), vmax2(t1[2], t1[3])), vmax2(vmax2(t1[4], t1[5]), vmax2(t1[6], t1[7])));
+  if (adv) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) s[q] = vmax2(c0[q], c1[q]);
+  }
+  return ssub2(m1, m0);
 }
 
-// alpha steps a .. b-1 with the outputs (row k+1 = rows[k - a]); DEC1 writes E = out - a1 at the interleaved position,
-// DEC2 A1 = out - E at the natural one (turbodecoder_iter.h:104-128), destinations from the dstE / dstA tables
-template <int NSB, int LC>
-__device__ __forceinline__ void alpha_chunk(const Blk<NSB>& B, int l, v2s s[8], const v2s (&rows)[LC][8], int a, int b,
-                                            const uint32_t* tab)
+__device__ __forceinline__ void st8(uint32_t* p, const v2s s[8])
 {
-  constexpr int NL  = NSB / 2;
-  int16_t*      dst = (int16_t*)(B.dec2 ? B.a1 : B.ev);
-#pragma unroll
-  for (int i = 0; i < LC; i++) {
-    const int k = a + i;
-    if (k < b) {
-      v2s       x, y, c0[8], c1[8];
-      const int idx = k * NL + l;
-      v2s       ap  = spl(0);
-      if (!B.dec2) {
-        x = U2(B.xs[idx]);
-        if (B.has_ap) {
-          ap = U2(B.a1[idx]);
-          x  = sadd2(x, ap);
-        }
-        y = U2(B.p0[idx]);
-      } else {
-        x = U2(B.ev[idx]);
-        y = U2(B.p1[idx]);
-      }
-      const uint32_t tb = tab[(size_t)k * NL + l];
-      acands(s, x, y, c0, c1);
-      v2s t0[8], t1[8];
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        t0[q] = sadd2(rows[i][q], c0[q]);
-        t1[q] = sadd2(rows[i][q], c1[q]);
-      }
-      const v2s m0  = vmax2(vmax2(vmax2(t0[0], t0[1]), vmax2(t0[2], t0[3])), vmax2(vmax2(t0[4], t0[5]), vmax2(t0[6], t0[7])));
-      const v2s m1  = vmax2(vmax2(vmax2(t1[0], t1[1]), vmax2(t1[2], t1[3])), vmax2(vmax2(t1[4], t1[5]), vmax2(t1[6], t1[7])));
-      const v2s out = ssub2(m1, m0);
-#pragma unroll
-      for (int q = 0; q < 8; q++) s[q] = vmax2(c0[q], c1[q]);
-      if ((k & 1) == 0 && k != 0) snorm(s);
-      const v2s      o   = B.dec2 ? out - x : (B.has_ap ? out - ap : out);
-      const uint32_t olo = tb & 0xffffu, ohi = tb >> 16; // row j' * 128 + window
-      dst[(olo >> 7) * NSB + (olo & 127)] = o.x;
-      dst[(ohi >> 7) * NSB + (ohi & 127)] = o.y;
-    }
-  }
+  ((uint4*)p)[0] = make_uint4(W2(s[0]), W2(s[1]), W2(s[2]), W2(s[3]));
+  ((uint4*)p)[1] = make_uint4(W2(s[4]), W2(s[5]), W2(s[6]), W2(s[7]));
+}
+__device__ __forceinline__ void ld8(const uint32_t* p, v2s s[8])
+{
+  const uint4 u = ((const uint4*)p)[0], v = ((const uint4*)p)[1];
+  s[0] = U2(u.x); s[1] = U2(u.y); s[2] = U2(u.z); s[3] = U2(u.w);
+  s[4] = U2(v.x); s[5] = U2(v.y); s[6] = U2(v.z); s[7] = U2(v.w);
+}
+
+// natural decision bit m (MSB first within its byte, turbodecoder_win.h:973-993) into the LDS bitmap
+__device__ __forceinline__ void dbit(uint32_t* bits, uint32_t m, bool v)
+{
+  const uint32_t by = m >> 3;
+  if (v) atomicOr(&bits[by >> 2], 1u << (((by & 3) << 3) + 7 - (m & 7)));
 }
 
 } // namespace
 
-template <int NSB>
-__global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
+// LDS of one code block: systematic, the current half-iteration's parity stream, a1, ev and its interleaver
+// destination table (K/2 words each), alpha states of steps [0, H) and beta rows of steps [H, L) (8 words per lane
+// and step each), the CRC byte table, the decision bitmap (K/32 words)
+size_t tdec_lat_lds(int K, int nsb)
 {
-  constexpr int NL = NSB / 2, LC = TDEC_LAT_LC;
-  const int     cb = blockIdx.x, t = threadIdx.x, T = blockDim.x;
+  const int L = K / nsb, NL = nsb / 2;
+  return (size_t)K / 2 * 4 * 5 + (size_t)L * NL * 8 * 4 + 256 * 4 + (size_t)K / 8;
+}
+
+template <int NSB>
+__global__ __launch_bounds__(64) void tdec_win_lat(TdecLatArgs A)
+{
+  constexpr int NL = NSB / 2, BK = 8; // window pairs; steps per block of the unrolled loops
+  const int     cb = blockIdx.x, t = threadIdx.x;
   if (A.done[cb]) return; // decoded in an earlier transmission (dlsch_tb_prologue)
-  const DlschCheckArgs& C   = A.chk;
-  const CbDesc&         d   = C.desc[cb];
-  const int             K   = A.K, L = K / NSB, W = A.warm;
-  const int             S   = (L + LC - 1) / LC; // chunks per window
-  const int             j   = t / NL, l = t % NL;
-  const bool            act = j < S;
+  const DlschCheckArgs& C = A.chk;
+  const CbDesc&         d = C.desc[cb];
+  const int             K = A.K, L = K / NSB, H = L / 2;
 
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* xs  = lds;              // K/2 words each
-  uint32_t* p0  = xs + K / 2;
-  uint32_t* p1  = p0 + K / 2;
-  uint32_t* a1  = p1 + K / 2;
-  uint32_t* ev  = a1 + K / 2;
-  St8*      gs  = (St8*)(ev + K / 2); // [T] guessed entering states
-  St8*      es  = gs + T;             // [T] final states
-  uint32_t (*t4)[256] = (uint32_t (*)[256])(es + T); // CRC slice-by-4 table of this block's polynomial
-  uint8_t*  dec = (uint8_t*)(t4[4]);  // K/8 decision bytes
+  uint32_t* xs   = lds;                       // K/2 words each
+  uint32_t* pc   = xs + K / 2;                // P0 (DEC1) / P1 (DEC2) of this half-iteration
+  uint32_t* a1   = pc + K / 2;
+  uint32_t* ev   = a1 + K / 2;
+  uint32_t* tb   = ev + K / 2;                // dstE (DEC1) / dstA (DEC2), [L][NL]
+  uint32_t* am   = tb + K / 2;                // [H][NL][8] alpha entering states of steps 0 .. H-1
+  uint32_t* bm   = am + (size_t)H * NL * 8;   // [L-H][NL][8] beta rows k+1 of steps H .. L-1
+  uint32_t* tl   = bm + (size_t)(L - H) * NL * 8; // CRC byte table
+  uint32_t* bits = tl + 256;                  // K/8 decision bytes
   __shared__ int16_t  tail[12];
   __shared__ uint32_t fin_s;
 
-  // ---- the block's decoder buffer into LDS; parity rows the rate dematcher left without an LLR read as zero
   const size_t    bidx = A.in_idx ? A.in_idx[cb] : (size_t)cb;
   const int16_t*  in   = A.in + bidx * A.in_stride;
   const uint32_t* rmk  = A.rowmask ? (const uint32_t*)(in + SB_ROWMASK) : nullptr;
-  {
-    const int nq = K / 8; // uint4 pieces per stream (NSB int16 per row: 2 pieces a row at NSB = 16, 1 at 8)
-    for (int i = t; i < 3 * nq; i += T) {
-      const int s = i / nq, p = i % nq;
-      uint4     v = ((const uint4*)(in + (size_t)s * (K + 32)))[p];
+  // stream s (1 = P0, 2 = P1) of the decoder buffer into dst; parity rows the rate dematcher left without an LLR read
+  // as zero (rm_image.h)
+  auto load_stream = [&](int s, uint32_t* dst) {
+    const uint4* src = (const uint4*)(in + (size_t)s * (K + 32));
+    for (int i = t; i < K / 8; i += 64) {
+      uint4 v = src[i];
       if (rmk && s > 0) {
-        const int row = (p * 8) / NSB;
+        const int row = (i * 8) / NSB;
         if (!((rmk[(s - 1) * SB_ROWMASK_WORDS + (row >> 5)] >> (row & 31)) & 1u)) v = make_uint4(0u, 0u, 0u, 0u);
       }
-      ((uint4*)(s == 0 ? xs : s == 1 ? p0 : p1))[p] = v;
+      ((uint4*)dst)[i] = v;
     }
-    for (int i = t; i < K / 2; i += T) {
-      a1[i] = 0;
-      ev[i] = 0;
-    }
-    if (t < 12) tail[t] = in[3 * (K + 32) + t];
+  };
+  load_stream(0, xs);
+  for (int i = t; i < K / 2; i += 64) {
+    a1[i] = 0;
+    ev[i] = 0;
+  }
+  if (t < 12) tail[t] = in[3 * (K + 32) + t];
+  {
     const CrcTable* ct = d.C > 1 ? C.crc24b : C.crc24a;
-    for (int i = t; i < 256; i += T) t4[0][i] = ct->t[i];
-    __syncthreads();
-    for (int k = 1; k < 4; k++) {
-      for (int i = t; i < 256; i += T) t4[k][i] = crc24_step_table(t4[k - 1][i], t4[0]);
-      __syncthreads();
-    }
+    for (int i = t; i < 256; i += 64) tl[i] = ct->t[i];
   }
 
-  const int a  = j * LC;
-  const int b  = min(a + LC, L);
-  const bool top = b == L;
-  v2s       rows[LC][8];
-  v2s       st[8];
-  uint32_t  reruns = 0;
-  // A.prof (measurement): shader-clock cycles of each phase, taken by thread 0 after the barriers that end them
-  uint64_t  pc[12] = {};
-  uint64_t  tp     = A.prof ? __builtin_amdgcn_s_memtime() : 0;
-  auto      mark   = [&](int k) {
+  const bool alpha = t < NL, beta = t >= NL && t < 2 * NL;
+  const int  l     = alpha ? t : t - NL;
+  // A.prof (measurement): shader-clock cycles of each phase, taken by lane 0 after the barriers that end them
+  uint64_t pcy[11] = {};
+  uint64_t tp      = A.prof ? __builtin_amdgcn_s_memtime() : 0;
+  auto     mark    = [&](int k) {
     if (A.prof) {
       const uint64_t n = __builtin_amdgcn_s_memtime();
-      pc[k] += n - tp;
+      pcy[k] += n - tp;
       tp = n;
     }
   };
-  mark(0);
 
   for (uint32_t h = 0; h < C.max_its; h++) {
-    Blk<NSB> B{xs, p0, p1, a1, ev, tail, L, (h & 1) != 0, (h & 1) == 0 && h > 0};
-
-    // ------------------------------------------------ beta: guess, chunk, reruns
-    if (act) {
-      int kt = b;
-      if (top) { // row L: the window boundary, not a computed row
-        B.beta_boundary(l, st);
-#pragma unroll
-        for (int r = 0; r < LC; r++)
-          if (r == b - a - 1) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) rows[r][i] = st[i];
-          }
-        kt = L - 1;
-      } else if (b + W >= L) { // near the boundary: enter exactly
-        B.beta_boundary(l, st);
-        B.beta_run(l, st, L - 1, b + 1);
-      } else {
-        sfill(st, 0);
-        B.beta_run(l, st, b + W, b + 1);
-      }
-      gs[t] = spack(st);
-      beta_chunk<NSB, LC>(B, l, st, rows, a, kt);
-      es[t] = spack(st);
-    }
-    for (int rd = 0;; rd++) {
-      bool bad = false;
-      St8  nb{};
-      if (act && !top) {
-        nb  = es[t + NL];
-        bad = !seq(nb, gs[t]);
-      }
-      const int any = __syncthreads_or(bad);
-      mark(rd == 0 ? 1 : 2);
-      if (!any) break;
-      pc[3]++;
-      if (bad) {
-        gs[t] = nb;
-        sunpack(nb, st);
-        beta_chunk<NSB, LC>(B, l, st, rows, a, b);
-        es[t] = spack(st);
-        reruns++;
-      }
-      __syncthreads();
-    }
-
-    // ------------------------------------------------ alpha with outputs: guess, chunk, reruns
-    const uint32_t* tab = (B.dec2 ? A.dstA : A.dstE);
-    if (act) {
-      if (j == 0) {
-        B.alpha_boundary(l, st);
-      } else if (a <= W) {
-        B.alpha_boundary(l, st);
-        B.alpha_run(l, st, 0, a - 1);
-      } else {
-        sfill(st, 0);
-        B.alpha_run(l, st, a - W, a - 1);
-      }
-      gs[t] = spack(st);
-      alpha_chunk<NSB, LC>(B, l, st, rows, a, b, tab);
-      es[t] = spack(st);
-    }
-    for (int rd = 0;; rd++) {
-      bool bad = false;
-      St8  pv{};
-      if (act && j > 0) {
-        pv  = es[t - NL];
-        bad = !seq(pv, gs[t]);
-      }
-      const int any = __syncthreads_or(bad);
-      mark(rd == 0 ? 4 : 5);
-      if (!any) break;
-      pc[6]++;
-      if (bad) {
-        gs[t] = pv;
-        sunpack(pv, st);
-        alpha_chunk<NSB, LC>(B, l, st, rows, a, b, tab);
-        es[t] = spack(st);
-        reruns++;
-      }
-      __syncthreads();
-    }
-
-    // ------------------------------------------------ decisions (turbodecoder_win.h:973-993) and the check
-    // DEC1's output at natural m is E[inv m] + A1[m], DEC2's deinterleaved output A1[m] + E[inv m] (wrapping)
-    const int16_t* e16 = (const int16_t*)ev;
-    const int16_t* a16 = (const int16_t*)a1;
-    for (int by = t; by < K / 8; by += T) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const int      m = 8 * by + i, w = m / L, k = m - w * L;
-        const uint32_t tb = A.dstE[(size_t)k * NL + (w >> 1)];
-        const uint32_t o  = (w & 1) ? (tb >> 16) : (tb & 0xffffu);
-        const short    dv = (short)(e16[(o >> 7) * NSB + (o & 127)] + a16[k * NSB + w]);
-        v |= (uint32_t)(dv > 0) << (7 - i);
-      }
-      dec[by] = (uint8_t)v;
+    const bool dec2 = (h & 1) != 0, has_ap = !dec2 && h > 0;
+    // this half-iteration's parity stream and destination table; the decision bitmap cleared
+    load_stream(dec2 ? 2 : 1, pc);
+    {
+      const uint4* g = (const uint4*)(dec2 ? A.dstA : A.dstE);
+      for (int i = t; i < K / 8; i += 64) ((uint4*)tb)[i] = g[i];
+      for (int i = t; i < K / 32; i += 64) bits[i] = 0;
     }
     __syncthreads();
-    mark(7);
-    pc[9]++;
-    if (t < 64) {
-      const int      pc  = d.C > 1 ? 1 : 0;
-      const uint32_t crc = wave_crc24_scaled4(dec, K / 8, t4, pc ? C.crc24b->poly : C.crc24a->poly, C.scale + (pc ? 64 : 0));
+    mark(0);
+    Blk<NSB>       B{xs, pc, pc, a1, ev, tail, L, dec2, has_ap};
+    const uint32_t* X   = dec2 ? ev : xs;
+    int16_t*        dst = (int16_t*)(dec2 ? a1 : ev);
+    v2s             st[8];
+    // the 8 steps' inputs of lane l from step k0 on (k0 + i clamped to [0, L))
+    auto loadx = [&](int k0, int dir, uint32_t (&xv)[BK + 1], uint32_t (&yv)[BK + 1], uint32_t (&av)[BK + 1], int n) {
+#pragma unroll
+      for (int i = 0; i < BK + 1; i++) {
+        if (i < n) {
+          const int k = min(max(k0 + dir * i, 0), L - 1), ix = k * NL + l;
+          xv[i] = X[ix];
+          yv[i] = pc[ix];
+          av[i] = has_ap ? a1[ix] : 0u;
+        }
+      }
+    };
+    auto xin = [&](uint32_t xw, uint32_t yw, uint32_t aw, v2s& x, v2s& y, v2s& ap) {
+      ap = U2(aw);
+      x  = U2(xw);
+      if (has_ap) x = sadd2(x, ap);
+      y = U2(yw);
+    };
+    // output of step k (windows 2l, 2l+1): DEC1 E = out - a1 at the interleaved position, DEC2 A1 = out - E at the
+    // natural one; its decision bit at the natural position (DEC1: own, DEC2: the destination's)
+    auto put = [&](int k, v2s x, v2s ap, v2s out) {
+      const uint32_t e   = tb[k * NL + l];
+      const v2s      o   = dec2 ? out - x : (has_ap ? out - ap : out);
+      const uint32_t olo = e & 0xffffu, ohi = e >> 16; // row j' * 128 + window
+      dst[(olo >> 7) * NSB + (olo & 127)] = o.x;
+      dst[(ohi >> 7) * NSB + (ohi & 127)] = o.y;
+      if (dec2) {
+        dbit(bits, (olo & 127) * L + (olo >> 7), out.x > 0);
+        dbit(bits, (ohi & 127) * L + (ohi >> 7), out.y > 0);
+      } else {
+        dbit(bits, 2 * l * L + k, out.x > 0);
+        dbit(bits, (2 * l + 1) * L + k, out.y > 0);
+      }
+    };
+
+    // ------------------------------------------------ first halves: alpha over [0, H), beta over rows L .. H+1
+    if (alpha) {
+      B.alpha_boundary(l, st);
+      for (int k0 = 0; k0 < H; k0 += BK) {
+        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1];
+        loadx(k0, 1, xv, yv, av, BK);
+#pragma unroll
+        for (int i = 0; i < BK; i++) {
+          const int k = k0 + i;
+          if (k < H) {
+            v2s x, y, ap;
+            xin(xv[i], yv[i], av[i], x, y, ap);
+            st8(am + ((size_t)k * NL + l) * 8, st);
+            astep(st, x, y);
+            if ((k & 1) == 0 && k != 0) snorm(st);
+          }
+        }
+      }
+    } else if (beta) {
+      B.beta_boundary(l, st); // row L
+      st8(bm + ((size_t)(L - 1 - H) * NL + l) * 8, st);
+      for (int k0 = L - 1; k0 > H; k0 -= BK) { // rows k0, k0-1, ... > H: row k is the beta row of step k - 1
+        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1];
+        loadx(k0, -1, xv, yv, av, BK);
+#pragma unroll
+        for (int i = 0; i < BK; i++) {
+          const int k = k0 - i;
+          if (k > H) {
+            v2s x, y, ap;
+            xin(xv[i], yv[i], av[i], x, y, ap);
+            bstep<true>(st, x, y);
+            st8(bm + ((size_t)(k - 1 - H) * NL + l) * 8, st);
+            if ((k & 1) == 0) snorm(st); // k > H >= 1
+          }
+        }
+      }
+    }
+    __syncthreads();
+    mark(1);
+    // ------------------------------------------------ second halves with the outputs
+    if (alpha) {
+      for (int k0 = H; k0 < L; k0 += BK) { // step k with beta row k+1
+        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1];
+        loadx(k0, 1, xv, yv, av, BK);
+#pragma unroll
+        for (int i = 0; i < BK; i++) {
+          const int k = k0 + i;
+          if (k < L) {
+            v2s x, y, ap, row[8];
+            xin(xv[i], yv[i], av[i], x, y, ap);
+            ld8(bm + ((size_t)(k - H) * NL + l) * 8, row);
+            const v2s out = out_llr(st, x, y, row, true);
+            if ((k & 1) == 0 && k != 0) snorm(st);
+            put(k, x, ap, out);
+          }
+        }
+      }
+    } else if (beta) {
+      for (int k0 = H; k0 >= 1; k0 -= BK) { // row k, then the output of step k - 1 with its stored alpha state
+        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1];
+        loadx(k0, -1, xv, yv, av, BK + 1); // inputs of steps k0 .. k0 - 8
+#pragma unroll
+        for (int i = 0; i < BK; i++) {
+          const int k = k0 - i;
+          if (k >= 1) {
+            v2s x, y, ap, row[8], as[8];
+            xin(xv[i], yv[i], av[i], x, y, ap);
+            bstep<true>(st, x, y);
+#pragma unroll
+            for (int q = 0; q < 8; q++) row[q] = st[q];
+            if ((k & 1) == 0) snorm(st);
+            xin(xv[i + 1], yv[i + 1], av[i + 1], x, y, ap);
+            ld8(am + ((size_t)(k - 1) * NL + l) * 8, as);
+            put(k - 1, x, ap, out_llr(as, x, y, row, false));
+          }
+        }
+      }
+    }
+    __syncthreads();
+    mark(2);
+
+    // ------------------------------------------------ the check (sch.c:420-450)
+    {
+      const uint8_t* dec = (const uint8_t*)bits;
+      const int      pc2 = d.C > 1 ? 1 : 0;
+      const uint32_t crc = wave_crc24_scaled(dec, K / 8, tl, pc2 ? C.crc24b->poly : C.crc24a->poly, C.scale + (pc2 ? 64 : 0));
       const bool     ok  = crc == 0;
       const bool     fin = ok || h + 1 == C.max_its;
       if (fin) {
-        uint8_t*       dst = C.data + d.data_off + (size_t)d.cb * d.rlen / 8;
-        const uint32_t nb  = (d.cb + 1 == d.C) ? (uint32_t)K / 8 : d.rlen / 8;
-        for (uint32_t i = t; i < nb; i += 64) dst[i] = dec[i];
+        uint8_t*       dstp = C.data + d.data_off + (size_t)d.cb * d.rlen / 8;
+        const uint32_t nb   = (d.cb + 1 == d.C) ? (uint32_t)K / 8 : d.rlen / 8;
+        for (uint32_t i = t; i < nb; i += 64) dstp[i] = dec[i];
         if (t == 0) {
           C.its[cb] = h + 1;
           if (ok) {
@@ -489,42 +490,33 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
       if (t == 0) fin_s = fin;
     }
     __syncthreads();
-    mark(8);
+    mark(4);
+    pcy[9]++;
     if (fin_s) break;
   }
   if (A.prof && t == 0) {
-    pc[10] = 1;
+    pcy[10] = 1;
 #pragma unroll
-    for (int k = 0; k < 11; k++) atomicAdd((unsigned long long*)&A.prof[k], (unsigned long long)pc[k]);
+    for (int k = 0; k < 11; k++) atomicAdd((unsigned long long*)&A.prof[k], (unsigned long long)pcy[k]);
   }
-  if (A.reruns && reruns) atomicAdd(A.reruns, reruns);
-}
-
-size_t tdec_lat_lds(int K, int threads) { return (size_t)K / 2 * 4 * 5 + 2 * (size_t)threads * 32 + 4 * 256 * 4 + K / 8; }
-
-int tdec_lat_threads(int nsb, int K)
-{
-  const int L = K / nsb, S = (L + TDEC_LAT_LC - 1) / TDEC_LAT_LC;
-  return (S * (nsb / 2) + 63) / 64 * 64;
 }
 
 hipError_t tdec_lat_launch(int nsb, const TdecLatArgs& a, hipStream_t s)
 {
-  const int    T   = tdec_lat_threads(nsb, a.K);
-  const size_t lds = tdec_lat_lds(a.K, T);
-  if (T > 256) return hipErrorInvalidValue;
+  const size_t lds = tdec_lat_lds(a.K, nsb);
+  if (lds > 160 * 1024 - 64) return hipErrorInvalidValue;
   static size_t attr[2] = {64 * 1024, 64 * 1024};
   const int     ix      = nsb == 16 ? 0 : 1;
+  const void*   f       = nsb == 16 ? (const void*)tdec_win_lat<16> : (const void*)tdec_win_lat<8>;
   if (lds > attr[ix]) {
-    const void* f = nsb == 16 ? (const void*)tdec_win_lat<16> : (const void*)tdec_win_lat<8>;
-    hipError_t  e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr[ix] = lds;
   }
   if (nsb == 16) {
-    hipLaunchKernelGGL(tdec_win_lat<16>, dim3(a.ncb), dim3(T), lds, s, a);
+    hipLaunchKernelGGL(tdec_win_lat<16>, dim3(a.ncb), dim3(64), lds, s, a);
   } else {
-    hipLaunchKernelGGL(tdec_win_lat<8>, dim3(a.ncb), dim3(T), lds, s, a);
+    hipLaunchKernelGGL(tdec_win_lat<8>, dim3(a.ncb), dim3(64), lds, s, a);
   }
   return hipGetLastError();
 }

@@ -11,15 +11,14 @@ from srsran_amd.dlsch import Dlsch, SoftbufferPool
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[(512, 32), (0, 32), (512, 0)], ids=["latency", "throughput", "latency_warm0"], autouse=True)
+@pytest.fixture(params=[512, 0], ids=["latency", "throughput"], autouse=True)
 def dlsch_path(request):
-    """Every test on both turbo paths: the latency path (tdec_win_lat, one launch per K group for small calls), the
-    half-iteration-per-launch throughput path, and the latency path with no guess warm-up (every chunk guess wrong,
-    the rerun path carries the decode)."""
+    """Every test on both turbo paths: the latency path (tdec_win_lat: a wave per code block, all half-iterations in
+    one launch, for calls of at most 512 code blocks) and the half-iteration-per-launch throughput path."""
     from srsran_amd import lib
-    old = lib().mi355_dlsch_set_latency_path(*request.param)
+    old = lib().mi355_dlsch_set_latency_path(request.param)
     yield
-    lib().mi355_dlsch_set_latency_path(old, 32)
+    lib().mi355_dlsch_set_latency_path(old)
 
 # (tbs, Qm, G, snr_db): SISO QPSK MCS9 (C=3, K=5312), TM4 QAM256 MCS27 codeword (C=16, K=6144),
 # gamma != 0 cases, 16-window and 8-window and generic single-CB sizes

@@ -16,14 +16,13 @@ import oracle  # noqa: E402
 from srsran_amd import lib  # noqa: E402
 from srsran_amd.dlsch import Dlsch, SoftbufferPool  # noqa: E402
 
-NAMES = ["load", "beta_first", "beta_reruns", "beta_rounds", "alpha_first", "alpha_reruns", "alpha_rounds", "decisions",
-         "check", "half_its", "cbs"]
+NAMES = ["load", "first_halves", "second_halves", "decisions", "check", "-", "-", "-", "-", "half_its", "cbs"]
 rng = np.random.default_rng(1)
 for snr in (9.0, 5.5, 30.0):
     cases = [(97896, 8, 115200, snr)] * 2
     llrs = [oracle.make_tb(rng, t, q, g, 0, s)[1] for (t, q, g, s) in cases]
-    for path, warm in (("throughput", 32), ("latency", 32), ("latency", 16), ("latency", 64)):
-        lib().mi355_dlsch_set_latency_path(512 if path == "latency" else 0, warm)
+    for path in ("throughput", "latency"):
+        lib().mi355_dlsch_set_latency_path(512 if path == "latency" else 0)
         dl = Dlsch(0, 10)
         pool = SoftbufferPool(2, 32)
         tbs = [dict(tbs=t, Qm=q, rv=0, softbuffer=i) for i, (t, q, g, s) in enumerate(cases)]
@@ -38,13 +37,12 @@ for snr in (9.0, 5.5, 30.0):
         out = (C.c_uint64 * 11)()
         lib().mi355_dlsch_latency_profile(0, C.addressof(out))
         v = list(out)
-        res = {"snr": snr, "path": path, "warm": warm, "us_per_call": round(dt * 1e6, 1), "rets": list(got[0]),
+        res = {"snr": snr, "path": path, "us_per_call": round(dt * 1e6, 1), "rets": list(got[0]),
                "its": [round(float(x), 2) for x in got[2]]}
         if path == "latency" and v[10]:
             cb, hi = v[10], max(v[9], 1)
-            res["per_cb_half_it_kcycles"] = {NAMES[k]: round(v[k] / hi / 1e3, 2) for k in (1, 2, 4, 5, 7, 8)}
+            res["per_cb_half_it_kcycles"] = {NAMES[k]: round(v[k] / hi / 1e3, 2) for k in (1, 2, 3, 4)}
             res["load_kcycles_per_cb"] = round(v[0] / cb / 1e3, 2)
-            res["rounds_per_half_it"] = {"beta": round(v[3] / hi, 2), "alpha": round(v[6] / hi, 2)}
             res["half_its_per_cb"] = round(hi / cb, 2)
         print(json.dumps(res), flush=True)
         dl.close() if hasattr(dl, "close") else None
