@@ -72,7 +72,9 @@ def parse(argv=None):
                          "100 -t 1 -m 9 through find_and_decode; tdec: configs[1]; enb: the GPU "
                          "eNodeB generator (encode side, SURVEY 8f row 2); plumbing: CPU dry run of the multi-rank "
                          "launcher, sharding and CRC-bitmap gather (no GPU, no decoding)")
-    ap.add_argument("--subframes", type=int, default=2048, help="TM4 subframes per GPU per step (batch)")
+    ap.add_argument("--subframes", type=int, default=None,
+                    help="subframes per GPU per step (batch); default 2048, 8192 for --workload siso_qpsk (its 3 code "
+                         "blocks per subframe give a 2048-subframe chunk's MAP launch only 384 waves)")
     ap.add_argument("--total-subframes", type=int, default=0,
                     help="configs[4]: T subframes sharded contiguously over the ranks, each decoded once")
     ap.add_argument("--resident-gb", type=float, default=96.0, help="HBM budget for one rank's resident I/Q")
@@ -93,7 +95,10 @@ def parse(argv=None):
     ap.add_argument("--fanout", action="store_true",
                     help="batch fan-out: rank 0 holds every rank's I/Q and scatters the shards over RCCL each step "
                          "(pdsch / ue_dl / plumbing workloads); payload SHA-1s and CRC bitmaps gathered back")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.subframes is None:
+        args.subframes = 8192 if args.workload == "siso_qpsk" else 2048
+    return args
 
 
 # ====================================================================================== launcher / distributed

@@ -54,6 +54,8 @@ int mi355_softbuffer_pool_materialize(mi355_softbuffer_pool_t* p, uint32_t first
 int mi355_softbuffer_pool_data(mi355_softbuffer_pool_t* p, uint8_t** data, uint32_t* stride, uint32_t* nof_sb);
 /* host copy of softbuffer sb's per-code-block CRC flags (max_cb bytes, 1 = the CB passed in an earlier decode) */
 int mi355_softbuffer_get_cb_crc(mi355_softbuffer_pool_t* p, uint32_t sb, uint8_t* cb_crc, void* stream);
+/* The same copy enqueued on stream without waiting: cb_crc is valid once the caller has synchronised the stream. */
+int mi355_softbuffer_get_cb_crc_async(mi355_softbuffer_pool_t* p, uint32_t sb, uint8_t* cb_crc, void* stream);
 typedef struct {
   uint32_t tbs;         /* transport block size in bits (grant.tb[i].tbs) */
   uint32_t nof_e_bits;  /* coded LLRs of the codeword (grant.tb[i].nof_bits) */

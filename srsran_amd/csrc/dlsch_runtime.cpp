@@ -472,6 +472,15 @@ int mi355_softbuffer_get_cb_crc(mi355_softbuffer_pool_t* p, uint32_t sb, uint8_t
   return MI355_SUCCESS;
 }
 
+int mi355_softbuffer_get_cb_crc_async(mi355_softbuffer_pool_t* p, uint32_t sb, uint8_t* cb_crc, void* stream)
+{
+  if (!p || !cb_crc || sb >= p->nof_sb) return MI355_ERROR_INVALID_INPUTS;
+  CHECK_HIP(hipSetDevice(p->device));
+  CHECK_HIP(hipMemcpyAsync(cb_crc, p->cb_crc + (size_t)sb * p->max_cb, p->max_cb, hipMemcpyDeviceToHost,
+                           (hipStream_t)stream));
+  return MI355_SUCCESS;
+}
+
 int mi355_dlsch_create(mi355_dlsch_t** q, int device)
 {
   if (!q) return MI355_ERROR_INVALID_INPUTS;

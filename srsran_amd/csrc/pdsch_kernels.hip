@@ -1012,6 +1012,10 @@ hipError_t pdsch_launch_fused(const PdschJobDev* jobs, uint32_t njobs, uint32_t 
 #define PDSCH_ER_THREADS 256
 #endif
 constexpr uint32_t ER_THREADS = PDSCH_ER_THREADS;
+#ifndef PDSCH_ER_PF
+#define PDSCH_ER_PF 1
+#endif
+constexpr int      ER_PF      = PDSCH_ER_PF; // RE pairs per thread whose loads are in flight together (equaliser part)
 constexpr int      ER_Q       = 5;                                                                 // quads per round
 constexpr int      ER_R       = (3 * (6144 + 32) + 12 + 8 * ER_THREADS * ER_Q - 1) / (8 * ER_THREADS * ER_Q); // rounds
 constexpr int      ER_Q2      = 3; // quads per round when both layers share a pass
@@ -1108,38 +1112,52 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   h_ptrs(J, hp);
   const uint32_t re0 = rp / Qm, re1 = (rp + n_e) / Qm, pairs = (J.nof_re + 1) / 2;
   const uint32_t p1  = P.diag == 2 ? 0u : min((re1 + 1) / 2, pairs);
-  for (uint32_t pr = re0 / 2 + tid; pr < p1; pr += ER_THREADS) {
-    const uint32_t m = map2[pr];
-    cf             Y[2][2], H[2][4];
+  // ER_PF RE pairs per thread in flight: their map words first, then every gather of all of them, then the math
+  for (uint32_t pr0 = re0 / 2 + tid; pr0 < p1; pr0 += ER_PF * ER_THREADS) {
+    uint32_t m[ER_PF];
 #pragma unroll
-    for (int e = 0; e < 2; e++) {
-      const uint32_t g  = e ? (m >> 16) : (m & 0xffffu);
-      const uint32_t gc = g < 14 * row ? g : 0u; // the odd tail's second index is padding
-      const uint32_t l  = __umulhi(gc, magic);
-      const float    sc = ((rmask >> l) & 1u) ? rinv : 1.0f;
-#pragma unroll
-      for (int r = 0; r < 2; r++) Y[e][r] = ld(yp[r], gc) * sc;
-#pragma unroll
-      for (int q = 0; q < 4; q++) H[e][q] = ld(hp[q], gc - l * row);
+    for (int f = 0; f < ER_PF; f++) {
+      const uint32_t pr = pr0 + f * ER_THREADS;
+      m[f]              = map2[pr < p1 ? pr : pr0];
     }
-    const uint32_t ns = min(2u, J.nof_re - 2 * pr);
-    cf             xs[2][2];
-    float          cs[2][2];
+    cf Y[ER_PF][2][2], H[ER_PF][2][4];
 #pragma unroll
-    for (int e = 0; e < 2; e++) eq_re(J, H[e], Y[e], noise, xs[0][e], xs[1][e], cs[0][e], cs[1][e]);
-    if constexpr (QM0 != 0) {
-      const cf    x[2]   = {xs[0][0], xs[0][1]};
-      const float csi[2] = {cs[0][0], cs[0][1]};
-      int16_t     o[2 * QM0];
-      llr_compute<QM0>(cwd[0], pr, ns, x, csi, cmb[0], o);
-      img_put<QM0>(imgs, 2 * pr * QM0 - rp, n_e, o);
+    for (int f = 0; f < ER_PF; f++) {
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const uint32_t g  = e ? (m[f] >> 16) : (m[f] & 0xffffu);
+        const uint32_t gc = g < 14 * row ? g : 0u; // the odd tail's second index is padding
+        const uint32_t l  = __umulhi(gc, magic);
+        const float    sc = ((rmask >> l) & 1u) ? rinv : 1.0f;
+#pragma unroll
+        for (int r = 0; r < 2; r++) Y[f][e][r] = ld(yp[r], gc) * sc;
+#pragma unroll
+        for (int q = 0; q < 4; q++) H[f][e][q] = ld(hp[q], gc - l * row);
+      }
     }
-    if constexpr (QM1 != 0) {
-      const cf    x[2]   = {xs[1][0], xs[1][1]};
-      const float csi[2] = {cs[1][0], cs[1][1]};
-      int16_t     o[2 * QM1];
-      llr_compute<QM1>(cwd[1], pr, ns, x, csi, cmb[1], o);
-      img_put<QM1>(imgs + img, 2 * pr * QM1 - rp, n_e, o);
+#pragma unroll
+    for (int f = 0; f < ER_PF; f++) {
+      const uint32_t pr = pr0 + f * ER_THREADS;
+      if (pr >= p1) continue;
+      const uint32_t ns = min(2u, J.nof_re - 2 * pr);
+      cf             xs[2][2];
+      float          cs[2][2];
+#pragma unroll
+      for (int e = 0; e < 2; e++) eq_re(J, H[f][e], Y[f][e], noise, xs[0][e], xs[1][e], cs[0][e], cs[1][e]);
+      if constexpr (QM0 != 0) {
+        const cf    x[2]   = {xs[0][0], xs[0][1]};
+        const float csi[2] = {cs[0][0], cs[0][1]};
+        int16_t     o[2 * QM0];
+        llr_compute<QM0>(cwd[0], pr, ns, x, csi, cmb[0], o);
+        img_put<QM0>(imgs, 2 * pr * QM0 - rp, n_e, o);
+      }
+      if constexpr (QM1 != 0) {
+        const cf    x[2]   = {xs[1][0], xs[1][1]};
+        const float csi[2] = {cs[1][0], cs[1][1]};
+        int16_t     o[2 * QM1];
+        llr_compute<QM1>(cwd[1], pr, ns, x, csi, cmb[1], o);
+        img_put<QM1>(imgs + img, 2 * pr * QM1 - rp, n_e, o);
+      }
     }
   }
   if (tid < 2) imgs[tid * img + n_e] = 0; // the zero slot: table entries without an LLR (RM_NONE, >= n_e) read it

@@ -4,9 +4,9 @@
 // cc_worker.cc:423-470: a few dozen code blocks per call).  The throughput kernel (tdec_kernels.hip) gives each
 // code block 8 lanes, one per pair of the reference's 16 windows, so a subframe's 32 blocks are 4 waves whose
 // 384-step recursions run serially, and every half-iteration is a launch of its own: 140 us per half-iteration.
-// Here ONE wave decodes one code block through all its half-iterations (sch.c:415-450: the CRC early stop in the
-// kernel), and each window's two recursions run at the same time (the "X" schedule): lane l of the first NL lanes runs
-// alpha forward over windows (2l, 2l+1) while lane l of the next NL runs beta backward over the same windows, each
+// Here ONE workgroup of two waves decodes one code block through all its half-iterations (sch.c:415-450: the CRC
+// early stop in the kernel), and each window's two recursions run at the same time (the "X" schedule): lane l of wave 0
+// runs alpha forward over windows (2l, 2l+1) while lane l of wave 1 runs beta backward over the same windows, each
 // storing its metrics for its first half of the window in LDS; past the middle the alpha lane produces the outputs of
 // the second half from the stored beta rows and the beta lane those of the first half from the stored alpha states.
 // Every value is the reference's (turbodecoder_win.h:480-832: the same saturating operations on the same operands,
@@ -158,16 +158,41 @@ template <int NSB> struct Blk {
     }
   }
 
+  // x, y (and the a-priori) of windows (w, w + 1) at step k for odd w (-1 and NSB - 1 included: the half outside the
+  // code block reads a neighbouring word and is discarded): the pair straddles two words
+  __device__ __forceinline__ void odd_words(int k, int w, uint32_t (&o)[6]) const
+  {
+    const int       i = (k * NSB + w) >> 1;
+    const uint32_t* X = dec2 ? ev : xs;
+    const uint32_t* Y = dec2 ? p1 : p0;
+    o[0] = X[i], o[1] = X[i + 1], o[2] = Y[i], o[3] = Y[i + 1];
+    if (has_ap) o[4] = a1[i], o[5] = a1[i + 1];
+  }
+  __device__ __forceinline__ void odd_xy(const uint32_t (&o)[6], v2s& x, v2s& y) const
+  {
+    x = U2(__builtin_amdgcn_alignbit(o[1], o[0], 16));
+    if (has_ap) x = sadd2(x, U2(__builtin_amdgcn_alignbit(o[5], o[4], 16)));
+    y = U2(__builtin_amdgcn_alignbit(o[3], o[2], 16));
+  }
+
   // row L of windows (2l, 2l+1): the 40-step warm-up over the first steps of windows (2l+1, 2l+2) from -INF
-  // (turbodecoder_win.h:566-631); the last window's from the wrapping 3-step tail trellis (:500-548)
+  // (turbodecoder_win.h:566-631); the last window's from the wrapping 3-step tail trellis (:500-548).  The inputs of
+  // 8 steps are read before those steps run.
   __device__ void beta_boundary(int l, v2s s[8]) const
   {
     sfill(s, -TDEC_INF);
-    for (int k = TDEC_WARMUP - 1; k >= 0; k--) {
-      v2s x, y;
-      in_odd(k, 2 * l + 1, x, y);
-      bstep<true>(s, x, y);
-      if ((k & 1) == 0 && k != 0) snorm(s);
+    for (int b = TDEC_WARMUP / 8 - 1; b >= 0; b--) {
+      uint32_t o[8][6];
+#pragma unroll
+      for (int i = 0; i < 8; i++) odd_words(8 * b + i, 2 * l + 1, o[i]);
+#pragma unroll
+      for (int i = 7; i >= 0; i--) {
+        const int k = 8 * b + i;
+        v2s       x, y;
+        odd_xy(o[i], x, y);
+        bstep<true>(s, x, y);
+        if ((k & 1) == 0 && k != 0) snorm(s);
+      }
     }
     if (l == NL - 1) {
       const int16_t* T = tail + (dec2 ? 6 : 0);
@@ -187,11 +212,18 @@ template <int NSB> struct Blk {
   __device__ void alpha_boundary(int l, v2s s[8]) const
   {
     sfill(s, -TDEC_INF);
-    for (int k = 0; k < TDEC_WARMUP; k++) {
-      v2s x, y;
-      in_odd(L - TDEC_WARMUP + k, 2 * l - 1, x, y);
-      astep(s, x, y);
-      if ((k & 1) == 0 && k != 0) snorm(s);
+    for (int b = 0; b < TDEC_WARMUP / 8; b++) {
+      uint32_t o[8][6];
+#pragma unroll
+      for (int i = 0; i < 8; i++) odd_words(L - TDEC_WARMUP + 8 * b + i, 2 * l - 1, o[i]);
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int k = 8 * b + i;
+        v2s       x, y;
+        odd_xy(o[i], x, y);
+        astep(s, x, y);
+        if ((k & 1) == 0 && k != 0) snorm(s);
+      }
     }
     if (l == 0) {
       s[0].x = 0;
@@ -258,7 +290,7 @@ __device__ __forceinline__ void ld8(const uint32_t* p, v2s s[8])
 __device__ __forceinline__ void dbit(uint32_t* bits, uint32_t m, bool v)
 {
   const uint32_t by = m >> 3;
-  if (v) atomicOr(&bits[by >> 2], 1u << (((by & 3) << 3) + 7 - (m & 7)));
+  atomicOr(&bits[by >> 2], (uint32_t)v << (((by & 3) << 3) + 7 - (m & 7))); // (no branch: or-ing 0 is harmless)
 }
 
 } // namespace
@@ -269,18 +301,21 @@ __device__ __forceinline__ void dbit(uint32_t* bits, uint32_t m, bool v)
 size_t tdec_lat_lds(int K, int nsb)
 {
   const int L = K / nsb, NL = nsb / 2;
-  return (size_t)K / 2 * 4 * 5 + (size_t)L * NL * 8 * 4 + 256 * 4 + (size_t)K / 8;
+  return (size_t)K / 2 * 4 * 5 + (size_t)L * NL * 8 * 4 + 256 * 4 + (size_t)(K + 31) / 32 * 4;
 }
 
 template <int NSB>
-__global__ __launch_bounds__(64) void tdec_win_lat(TdecLatArgs A)
+__global__ __launch_bounds__(128) void tdec_win_lat(TdecLatArgs A)
 {
   constexpr int NL = NSB / 2, BK = 8; // window pairs; steps per block of the unrolled loops
   const int     cb = blockIdx.x, t = threadIdx.x;
   if (A.done[cb]) return; // decoded in an earlier transmission (dlsch_tb_prologue)
   const DlschCheckArgs& C = A.chk;
   const CbDesc&         d = C.desc[cb];
-  const int             K = A.K, L = K / NSB, H = L / 2;
+  // meeting point H: the alpha lane runs H state-only steps then L - H output steps, the beta lane L - H rows then H
+  // rows with outputs (a row and an output each); L / 3 balances the two (turbodecoder_win.h's output step costs
+  // about twice a recursion step)
+  const int             K = A.K, L = K / NSB, H = L / 3;
 
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* xs   = lds;                       // K/2 words each
@@ -302,7 +337,7 @@ __global__ __launch_bounds__(64) void tdec_win_lat(TdecLatArgs A)
   // as zero (rm_image.h)
   auto load_stream = [&](int s, uint32_t* dst) {
     const uint4* src = (const uint4*)(in + (size_t)s * (K + 32));
-    for (int i = t; i < K / 8; i += 64) {
+    for (int i = t; i < K / 8; i += 128) {
       uint4 v = src[i];
       if (rmk && s > 0) {
         const int row = (i * 8) / NSB;
@@ -312,18 +347,20 @@ __global__ __launch_bounds__(64) void tdec_win_lat(TdecLatArgs A)
     }
   };
   load_stream(0, xs);
-  for (int i = t; i < K / 2; i += 64) {
+  for (int i = t; i < K / 2; i += 128) {
     a1[i] = 0;
     ev[i] = 0;
   }
   if (t < 12) tail[t] = in[3 * (K + 32) + t];
   {
     const CrcTable* ct = d.C > 1 ? C.crc24b : C.crc24a;
-    for (int i = t; i < 256; i += 64) tl[i] = ct->t[i];
+    for (int i = t; i < 256; i += 128) tl[i] = ct->t[i];
   }
 
-  const bool alpha = t < NL, beta = t >= NL && t < 2 * NL;
-  const int  l     = alpha ? t : t - NL;
+  // the alpha lanes in wave 0, the beta lanes in wave 1: the two recursions run at the same time on different
+  // SIMDs (in one wave their divergent code paths would be issued one after the other)
+  const bool alpha = t < NL, beta = t >= 64 && t < 64 + NL;
+  const int  l     = alpha ? t : t - 64;
   // A.prof (measurement): shader-clock cycles of each phase, taken by lane 0 after the barriers that end them
   uint64_t pcy[11] = {};
   uint64_t tp      = A.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -341,8 +378,8 @@ __global__ __launch_bounds__(64) void tdec_win_lat(TdecLatArgs A)
     load_stream(dec2 ? 2 : 1, pc);
     {
       const uint4* g = (const uint4*)(dec2 ? A.dstA : A.dstE);
-      for (int i = t; i < K / 8; i += 64) ((uint4*)tb)[i] = g[i];
-      for (int i = t; i < K / 32; i += 64) bits[i] = 0;
+      for (int i = t; i < K / 8; i += 128) ((uint4*)tb)[i] = g[i];
+      for (int i = t; i < (K + 31) / 32; i += 128) bits[i] = 0; // (K/8 bytes need not fill whole words: K = 408)
     }
     __syncthreads();
     mark(0);
@@ -358,7 +395,7 @@ __global__ __launch_bounds__(64) void tdec_win_lat(TdecLatArgs A)
           const int k = min(max(k0 + dir * i, 0), L - 1), ix = k * NL + l;
           xv[i] = X[ix];
           yv[i] = pc[ix];
-          av[i] = has_ap ? a1[ix] : 0u;
+          av[i] = a1[ix]; // (read whatever the half-iteration: used only when it has an a-priori)
         }
       }
     };
@@ -370,8 +407,7 @@ __global__ __launch_bounds__(64) void tdec_win_lat(TdecLatArgs A)
     };
     // output of step k (windows 2l, 2l+1): DEC1 E = out - a1 at the interleaved position, DEC2 A1 = out - E at the
     // natural one; its decision bit at the natural position (DEC1: own, DEC2: the destination's)
-    auto put = [&](int k, v2s x, v2s ap, v2s out) {
-      const uint32_t e   = tb[k * NL + l];
+    auto put = [&](int k, uint32_t e, v2s x, v2s ap, v2s out) {
       const v2s      o   = dec2 ? out - x : (has_ap ? out - ap : out);
       const uint32_t olo = e & 0xffffu, ohi = e >> 16; // row j' * 128 + window
       dst[(olo >> 7) * NSB + (olo & 127)] = o.x;
@@ -385,89 +421,123 @@ __global__ __launch_bounds__(64) void tdec_win_lat(TdecLatArgs A)
       }
     };
 
-    // ------------------------------------------------ first halves: alpha over [0, H), beta over rows L .. H+1
+    // ------------------------------------------------ first parts: alpha over [0, H), beta over rows L .. H+1
+    // Every loop runs whole blocks of BK steps, their inputs (and stored rows, destinations) read before the steps,
+    // without per-step guards, then the remaining steps one by one.
+    auto a_step = [&](int k, uint32_t xw, uint32_t yw, uint32_t aw) {
+      v2s x, y, ap;
+      xin(xw, yw, aw, x, y, ap);
+      st8(am + ((size_t)k * NL + l) * 8, st);
+      astep(st, x, y);
+      if ((k & 1) == 0 && k != 0) snorm(st);
+    };
+    auto b_step = [&](int k, uint32_t xw, uint32_t yw, uint32_t aw) { // row k (> H), the beta row of step k - 1
+      v2s x, y, ap;
+      xin(xw, yw, aw, x, y, ap);
+      bstep<true>(st, x, y);
+      st8(bm + ((size_t)(k - 1 - H) * NL + l) * 8, st);
+      if ((k & 1) == 0) snorm(st);
+    };
     if (alpha) {
       B.alpha_boundary(l, st);
-      for (int k0 = 0; k0 < H; k0 += BK) {
+      const int kf = H / BK * BK;
+      for (int k0 = 0; k0 < kf; k0 += BK) {
         uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1];
         loadx(k0, 1, xv, yv, av, BK);
 #pragma unroll
-        for (int i = 0; i < BK; i++) {
-          const int k = k0 + i;
-          if (k < H) {
-            v2s x, y, ap;
-            xin(xv[i], yv[i], av[i], x, y, ap);
-            st8(am + ((size_t)k * NL + l) * 8, st);
-            astep(st, x, y);
-            if ((k & 1) == 0 && k != 0) snorm(st);
-          }
-        }
+        for (int i = 0; i < BK; i++) a_step(k0 + i, xv[i], yv[i], av[i]);
+      }
+      for (int k = kf; k < H; k++) {
+        const int ix = k * NL + l;
+        a_step(k, X[ix], pc[ix], a1[ix]);
       }
     } else if (beta) {
       B.beta_boundary(l, st); // row L
       st8(bm + ((size_t)(L - 1 - H) * NL + l) * 8, st);
-      for (int k0 = L - 1; k0 > H; k0 -= BK) { // rows k0, k0-1, ... > H: row k is the beta row of step k - 1
+      const int n = L - 1 - H, kf = L - 1 - n / BK * BK; // rows L-1 .. H+1
+      for (int k0 = L - 1; k0 > kf; k0 -= BK) {
         uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1];
         loadx(k0, -1, xv, yv, av, BK);
 #pragma unroll
-        for (int i = 0; i < BK; i++) {
-          const int k = k0 - i;
-          if (k > H) {
-            v2s x, y, ap;
-            xin(xv[i], yv[i], av[i], x, y, ap);
-            bstep<true>(st, x, y);
-            st8(bm + ((size_t)(k - 1 - H) * NL + l) * 8, st);
-            if ((k & 1) == 0) snorm(st); // k > H >= 1
-          }
-        }
+        for (int i = 0; i < BK; i++) b_step(k0 - i, xv[i], yv[i], av[i]);
+      }
+      for (int k = kf; k > H; k--) {
+        const int ix = k * NL + l;
+        b_step(k, X[ix], pc[ix], a1[ix]);
       }
     }
     __syncthreads();
     mark(1);
-    // ------------------------------------------------ second halves with the outputs
+    // ------------------------------------------------ second parts with the outputs
+    auto ao_step = [&](int k, uint32_t xw, uint32_t yw, uint32_t aw, const v2s (&row)[8], uint32_t e) {
+      v2s x, y, ap;
+      xin(xw, yw, aw, x, y, ap);
+      const v2s out = out_llr(st, x, y, row, true);
+      if ((k & 1) == 0 && k != 0) snorm(st);
+      put(k, e, x, ap, out);
+    };
+    // row k, then the output of step k - 1 from its stored alpha state
+    auto bo_step = [&](int k, uint32_t xw, uint32_t yw, uint32_t aw, uint32_t xw1, uint32_t yw1, uint32_t aw1,
+                       const v2s (&as)[8], uint32_t e) {
+      v2s x, y, ap, row[8];
+      xin(xw, yw, aw, x, y, ap);
+      bstep<true>(st, x, y);
+#pragma unroll
+      for (int q = 0; q < 8; q++) row[q] = st[q];
+      if ((k & 1) == 0) snorm(st);
+      xin(xw1, yw1, aw1, x, y, ap);
+      v2s a8[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) a8[q] = as[q];
+      put(k - 1, e, x, ap, out_llr(a8, x, y, row, false));
+    };
     if (alpha) {
-      for (int k0 = H; k0 < L; k0 += BK) { // step k with beta row k+1
-        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1];
+      const int kf = H + (L - H) / BK * BK;
+      for (int k0 = H; k0 < kf; k0 += BK) { // step k with beta row k+1
+        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1], ev8[BK];
+        v2s      rw[BK][8];
         loadx(k0, 1, xv, yv, av, BK);
 #pragma unroll
         for (int i = 0; i < BK; i++) {
-          const int k = k0 + i;
-          if (k < L) {
-            v2s x, y, ap, row[8];
-            xin(xv[i], yv[i], av[i], x, y, ap);
-            ld8(bm + ((size_t)(k - H) * NL + l) * 8, row);
-            const v2s out = out_llr(st, x, y, row, true);
-            if ((k & 1) == 0 && k != 0) snorm(st);
-            put(k, x, ap, out);
-          }
+          ld8(bm + ((size_t)(k0 + i - H) * NL + l) * 8, rw[i]);
+          ev8[i] = tb[(k0 + i) * NL + l];
         }
+#pragma unroll
+        for (int i = 0; i < BK; i++) ao_step(k0 + i, xv[i], yv[i], av[i], rw[i], ev8[i]);
+      }
+      for (int k = kf; k < L; k++) {
+        const int ix = k * NL + l;
+        v2s       rw[8];
+        ld8(bm + ((size_t)(k - H) * NL + l) * 8, rw);
+        ao_step(k, X[ix], pc[ix], a1[ix], rw, tb[ix]);
       }
     } else if (beta) {
-      for (int k0 = H; k0 >= 1; k0 -= BK) { // row k, then the output of step k - 1 with its stored alpha state
-        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1];
+      const int kf = H - H / BK * BK; // rows H .. kf+1 in whole blocks, then kf .. 1
+      for (int k0 = H; k0 > kf; k0 -= BK) {
+        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1], ev8[BK];
+        v2s      as[BK][8];
         loadx(k0, -1, xv, yv, av, BK + 1); // inputs of steps k0 .. k0 - 8
 #pragma unroll
         for (int i = 0; i < BK; i++) {
-          const int k = k0 - i;
-          if (k >= 1) {
-            v2s x, y, ap, row[8], as[8];
-            xin(xv[i], yv[i], av[i], x, y, ap);
-            bstep<true>(st, x, y);
-#pragma unroll
-            for (int q = 0; q < 8; q++) row[q] = st[q];
-            if ((k & 1) == 0) snorm(st);
-            xin(xv[i + 1], yv[i + 1], av[i + 1], x, y, ap);
-            ld8(am + ((size_t)(k - 1) * NL + l) * 8, as);
-            put(k - 1, x, ap, out_llr(as, x, y, row, false));
-          }
+          ld8(am + ((size_t)(k0 - i - 1) * NL + l) * 8, as[i]);
+          ev8[i] = tb[(k0 - i - 1) * NL + l];
         }
+#pragma unroll
+        for (int i = 0; i < BK; i++)
+          bo_step(k0 - i, xv[i], yv[i], av[i], xv[i + 1], yv[i + 1], av[i + 1], as[i], ev8[i]);
+      }
+      for (int k = kf; k >= 1; k--) {
+        const int ix = k * NL + l, ix1 = (k - 1) * NL + l;
+        v2s       as[8];
+        ld8(am + (size_t)ix1 * 8, as);
+        bo_step(k, X[ix], pc[ix], a1[ix], X[ix1], pc[ix1], a1[ix1], as, tb[ix1]);
       }
     }
     __syncthreads();
     mark(2);
 
-    // ------------------------------------------------ the check (sch.c:420-450)
-    {
+    // ------------------------------------------------ the check (sch.c:420-450), by wave 0
+    if (t < 64) {
       const uint8_t* dec = (const uint8_t*)bits;
       const int      pc2 = d.C > 1 ? 1 : 0;
       const uint32_t crc = wave_crc24_scaled(dec, K / 8, tl, pc2 ? C.crc24b->poly : C.crc24a->poly, C.scale + (pc2 ? 64 : 0));
@@ -514,9 +584,9 @@ hipError_t tdec_lat_launch(int nsb, const TdecLatArgs& a, hipStream_t s)
     attr[ix] = lds;
   }
   if (nsb == 16) {
-    hipLaunchKernelGGL(tdec_win_lat<16>, dim3(a.ncb), dim3(64), lds, s, a);
+    hipLaunchKernelGGL(tdec_win_lat<16>, dim3(a.ncb), dim3(128), lds, s, a);
   } else {
-    hipLaunchKernelGGL(tdec_win_lat<8>, dim3(a.ncb), dim3(64), lds, s, a);
+    hipLaunchKernelGGL(tdec_win_lat<8>, dim3(a.ncb), dim3(128), lds, s, a);
   }
   return hipGetLastError();
 }

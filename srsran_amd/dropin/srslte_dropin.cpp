@@ -348,6 +348,7 @@ struct PdschState {
   float*    d_stage   = nullptr;
   size_t    stage_cap = 0;
   uint8_t*  d_payload = nullptr;
+  size_t    pay_cap   = 0;
   PinnedBuf h_stage, h_payload;
 
   ~PdschState()
@@ -421,36 +422,42 @@ int pdsch_decode_dev(srslte_pdsch_t* q, PdschState* st, hipStream_t stream, srsl
     pay_total += (pay_len[t] + 255) / 256 * 256;
   }
   if (!run[0] && !run[1]) return SRSLTE_SUCCESS;
-  if (pay_total > st->h_payload.cap) {
+  if (pay_total > st->pay_cap) {
     if (st->d_payload) (void)hipFree(st->d_payload);
     st->d_payload = nullptr;
-    if (st->h_payload.reserve(pay_total) || hipMalloc(&st->d_payload, pay_total) != hipSuccess) return SRSLTE_ERROR;
+    st->pay_cap   = 0;
+    if (hipMalloc(&st->d_payload, pay_total) != hipSuccess) return SRSLTE_ERROR;
+    st->pay_cap = pay_total;
   }
+  // pinned read-back area: the payloads, then each decoded TB's code-block CRC flags
+  if (st->h_payload.reserve(pay_total + 2 * (size_t)A.max_cb)) return SRSLTE_ERROR;
   for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++) job.payload[t] = st->d_payload + pay_off[t];
   if (q->llr_is_8bit != st->llr8) { // cc_worker.cc:98-101 sets pdsch.llr_is_8bit (and dl_sch.llr_is_8bit)
     if (mi355_pdsch_set_llr_8bit(st->rx, q->llr_is_8bit)) return SRSLTE_ERROR;
     st->llr8 = q->llr_is_8bit;
   }
   if (mi355_pdsch_decode_batch(st->rx, A.pool, &job, 1, res, stream) != MI355_SUCCESS) return SRSLTE_ERROR;
+  // one payload copy for both TBs (consecutive in d_payload), the CRC flags behind it, one wait
+  uint8_t* hp = (uint8_t*)st->h_payload.p;
+  if (hipMemcpyAsync(hp, st->d_payload, pay_total, hipMemcpyDeviceToHost, stream) != hipSuccess) return SRSLTE_ERROR;
   for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++) {
     if (!run[t]) continue;
-    if (hipMemcpyAsync((char*)st->h_payload.p + pay_off[t], st->d_payload + pay_off[t], pay_len[t],
-                       hipMemcpyDeviceToHost, stream) != hipSuccess)
+    if (mi355_softbuffer_get_cb_crc_async(A.pool, (uint32_t)A.slot_of(cfg->softbuffers.rx[t]), hp + pay_total + t * A.max_cb,
+                                          stream) != MI355_SUCCESS)
       return SRSLTE_ERROR;
   }
   if (hipStreamSynchronize(stream) != hipSuccess) return SRSLTE_ERROR;
   for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++) {
     if (!run[t]) continue;
-    memcpy(data[t].payload, (char*)st->h_payload.p + pay_off[t], pay_len[t]);
+    memcpy(data[t].payload, hp + pay_off[t], pay_len[t]);
     data[t].crc                  = res[t].crc != 0;
     data[t].avg_iterations_block = res[t].avg_iterations_block;
     data[t].evm                  = NAN; // meas_evm_en is not implemented (EVM = NAN, as the reference without it)
     q->dl_sch.avg_iterations     = res[t].avg_iterations_block;
     // host mirror of the softbuffer's CRC state (sch.c:443, :470-487)
     srslte_softbuffer_rx_t* sbuf = cfg->softbuffers.rx[t];
-    std::vector<uint8_t>    f(A.max_cb);
-    if (mi355_softbuffer_get_cb_crc(A.pool, (uint32_t)A.slot_of(sbuf), f.data(), stream) == MI355_SUCCESS)
-      for (uint32_t i = 0; i < sbuf->max_cb; i++) sbuf->cb_crc[i] = f[i] != 0;
+    const uint8_t*          f    = hp + pay_total + t * A.max_cb;
+    for (uint32_t i = 0; i < sbuf->max_cb; i++) sbuf->cb_crc[i] = f[i] != 0;
     sbuf->tb_crc = data[t].crc;
   }
   return SRSLTE_SUCCESS;
@@ -527,18 +534,27 @@ int ue_fft_estimate(srslte_ue_dl_t* q, srslte_dl_sf_cfg_t* sf, srslte_ue_dl_cfg_
   job.tti = sf->tti;
   const size_t nin = (size_t)st->in_len * 2 * sizeof(float);
   if (st->h_in.reserve(nin * st->nof_rx)) return SRSLTE_ERROR;
+  uint32_t nstaged = 0; // host inputs staged contiguously (d_in[r] are consecutive): one upload for all of them
   for (uint32_t r = 0; r < st->nof_rx; r++) {
     if (!input[r]) return SRSLTE_ERROR_INVALID_INPUTS;
     if (is_device_ptr(input[r])) {
       job.in_buffer[r] = (const float*)input[r];
     } else {
-      char* h = (char*)st->h_in.p + r * nin;
-      memcpy(h, input[r], nin);
-      if (hipMemcpyAsync(st->d_in[r], h, nin, hipMemcpyHostToDevice, st->stream) != hipSuccess) return SRSLTE_ERROR;
+      memcpy((char*)st->h_in.p + r * nin, input[r], nin);
       job.in_buffer[r] = st->d_in[r];
+      nstaged++;
     }
     job.sf_symbols[r] = st->d_grid[r];
     for (uint32_t p = 0; p < q->cell.nof_ports; p++) job.ce[p][r] = st->d_ce[p][r];
+  }
+  if (nstaged == st->nof_rx) {
+    if (hipMemcpyAsync(st->d_in[0], st->h_in.p, nin * st->nof_rx, hipMemcpyHostToDevice, st->stream) != hipSuccess)
+      return SRSLTE_ERROR;
+  } else {
+    for (uint32_t r = 0; r < st->nof_rx; r++)
+      if (job.in_buffer[r] == st->d_in[r] &&
+          hipMemcpyAsync(st->d_in[r], (char*)st->h_in.p + r * nin, nin, hipMemcpyHostToDevice, st->stream) != hipSuccess)
+        return SRSLTE_ERROR;
   }
   mi355_chest_dl_cfg_t ccfg = chest_cfg_to_mi355(cfg->chest_cfg, sf->tti);
   st->est_valid             = false;
@@ -573,16 +589,11 @@ int ue_fft_estimate(srslte_ue_dl_t* q, srslte_dl_sf_cfg_t* sf, srslte_ue_dl_cfg_
     const size_t ng = (size_t)st->grid_len * 2 * sizeof(float);
     const size_t nb = ng * st->nof_rx * (1 + q->cell.nof_ports);
     if (st->h_back.reserve(nb)) return SRSLTE_ERROR;
-    size_t o = 0;
-    for (uint32_t r = 0; r < st->nof_rx; r++, o += ng)
-      if (hipMemcpyAsync((char*)st->h_back.p + o, st->d_grid[r], ng, hipMemcpyDeviceToHost, st->stream) != hipSuccess)
-        return SRSLTE_ERROR;
-    for (uint32_t p = 0; p < q->cell.nof_ports; p++)
-      for (uint32_t r = 0; r < st->nof_rx; r++, o += ng)
-        if (hipMemcpyAsync((char*)st->h_back.p + o, st->d_ce[p][r], ng, hipMemcpyDeviceToHost, st->stream) != hipSuccess)
-          return SRSLTE_ERROR;
+    // the grids and the estimates are consecutive in d_mem (srslte_ue_dl_set_cell): one read-back
+    if (hipMemcpyAsync(st->h_back.p, st->d_grid[0], nb, hipMemcpyDeviceToHost, st->stream) != hipSuccess)
+      return SRSLTE_ERROR;
     if (hipStreamSynchronize(st->stream) != hipSuccess) return SRSLTE_ERROR;
-    o = 0;
+    size_t o = 0;
     for (uint32_t r = 0; r < st->nof_rx; r++, o += ng) memcpy(q->sf_symbols[r], (char*)st->h_back.p + o, ng);
     for (uint32_t p = 0; p < q->cell.nof_ports; p++)
       for (uint32_t r = 0; r < st->nof_rx; r++, o += ng) memcpy(R.ce[p][r], (char*)st->h_back.p + o, ng);
@@ -941,11 +952,8 @@ int srslte_pdsch_decode(srslte_pdsch_t*        q,
     for (uint32_t r = 0; r < nrx; r++) {
       const float* d = (const float*)src[k][r];
       if (!is_device_ptr(src[k][r])) {
-        char* h = (char*)st->h_stage.p + k_stage * bytes;
-        memcpy(h, src[k][r], bytes);
-        float* dd = (float*)((char*)st->d_stage + k_stage * bytes);
-        if (hipMemcpyAsync(dd, h, bytes, hipMemcpyHostToDevice, st->stream) != hipSuccess) return SRSLTE_ERROR;
-        d = dd;
+        memcpy((char*)st->h_stage.p + k_stage * bytes, src[k][r], bytes);
+        d = (const float*)((char*)st->d_stage + k_stage * bytes);
         k_stage++;
       }
       if (k == 0)
@@ -953,6 +961,9 @@ int srslte_pdsch_decode(srslte_pdsch_t*        q,
       else
         ce[k - 1][r] = d;
     }
+  // the staged host buffers go up in one copy
+  if (k_stage && hipMemcpyAsync(st->d_stage, st->h_stage.p, k_stage * bytes, hipMemcpyHostToDevice, st->stream) != hipSuccess)
+    return SRSLTE_ERROR;
   const int ret = pdsch_decode_dev(q, st, st->stream, sf, cfg, channel->noise_estimate, grids, ce, data);
   if (cfg->meas_time_en) {
     gettimeofday(&t1, nullptr);
