@@ -167,6 +167,13 @@ static bool no_rowmask()
   return off;
 }
 
+// MI355_LAT_WAVES=4 (A/B timing): latency-path workgroups of four waves, the beta recursion in wave 2
+static bool lat_waves4()
+{
+  static const bool on = getenv("MI355_LAT_WAVES") && atoi(getenv("MI355_LAT_WAVES")) == 4;
+  return on;
+}
+
 // MI355_RM_SPARSE=0 (A/B timing): fresh decoder buffers written whole, zero parity rows included
 bool mi355::rm_sparse_writes()
 {
@@ -882,6 +889,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
       la.ncb     = (int)lv.n;
       la.K       = (int)lv.K;
       la.rowmask = nsb == 16 && !no_rowmask();
+      la.bwave   = lat_waves4() ? 2 : 1;
       CHECK_HIP(tdec_lat_launch((int)nsb, la, s));
       lat[i] = 1;
     }

@@ -113,6 +113,7 @@ struct TdecLatArgs {
   DlschCheckArgs  chk;      // desc, data, its, sb_crc, CRC tables and scales, max_its (h, dec, next unused)
   uint64_t*       prof;     // nullable (measurement): [11] phase cycles / counts summed over code blocks (tdec_win_lat.hip)
   int             ncb, K, rowmask;
+  int             bwave;    // the beta recursion's wave: 1 (two-wave workgroups) or 2 (four waves, MI355_LAT_WAVES=4)
 };
 size_t     tdec_lat_lds(int K, int nsb);
 hipError_t tdec_lat_launch(int nsb, const TdecLatArgs& a, hipStream_t s);

@@ -5,17 +5,17 @@
 // code block 8 lanes, one per pair of the reference's 16 windows, so a subframe's 32 blocks are 4 waves whose
 // 384-step recursions run serially, and every half-iteration is a launch of its own: 140 us per half-iteration.
 // Here ONE workgroup of two waves decodes one code block through all its half-iterations (sch.c:415-450: the CRC
-// early stop in the kernel), and each window's two recursions run at the same time (the "X" schedule): lane l of wave 0
-// runs alpha forward over windows (2l, 2l+1) while lane l of wave 1 runs beta backward over the same windows, each
-// storing its metrics for its first half of the window in LDS; past the middle the alpha lane produces the outputs of
-// the second half from the stored beta rows and the beta lane those of the first half from the stored alpha states.
-// Every value is the reference's (turbodecoder_win.h:480-832: the same saturating operations on the same operands,
-// the window boundaries from the same 40-step warm-ups, loop-index normalisation), so the serial path per
+// early stop in the kernel), and each window's two recursions run at the same time (the "X" schedule): wave 0 runs
+// alpha forward over every window pair while wave 1 runs beta backward, each storing its metrics for its half of the
+// windows in LDS; past the middle each continues over the other half, and every 64 / NL steps all 64 lanes of the
+// wave compute those steps' outputs from the stored rows of the other recursion.  In the recursions the 8 states of
+// a window pair sit in 8 lanes (distributed trellis, below): a step is a DPP exchange, two saturating adds and a max
+// per lane.  Every value is the reference's (turbodecoder_win.h:480-832: the same saturating operations on the same
+// operands, the window boundaries from the same 40-step warm-ups, loop-index normalisation), so the serial path per
 // half-iteration is 40 + L steps instead of the throughput kernel's 40 + L backward and L forward, with no launch
-// per half-iteration.  Inputs, a-priori, extrinsic and metrics live in LDS (160 KB at K = 6144).  Decisions come
-// from the extrinsic and a-priori arrays (DEC1's output is E + A1 at the natural position, DEC2's A1 + E at the
-// interleaved one), the check is dlsch_cb_check's (CRC24B / CRC24A over the K/8 decision bytes, payload bytes at
-// cb * rlen / 8, done / iteration / softbuffer-CRC flags).
+// per half-iteration.  Inputs, a-priori, extrinsic and metrics live in LDS (150 KB at K = 6144).  Decisions are bits
+// set by the output passes, the check is dlsch_cb_check's (CRC24B / CRC24A over the K/8 decision bytes, payload
+// bytes at cb * rlen / 8, done / iteration / softbuffer-CRC flags).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -74,45 +74,6 @@ __device__ __forceinline__ void acands(const v2s o[8], v2s x, v2s y, v2s c0[8], 
   c0[7] = o[6];            c1[7] = sadd2(o[7], xy);
 }
 
-__device__ __forceinline__ void astep(v2s s[8], v2s x, v2s y)
-{
-  v2s c0[8], c1[8];
-  acands(s, x, y, c0, c1);
-#pragma unroll
-  for (int i = 0; i < 8; i++) s[i] = vmax2(c0[i], c1[i]);
-}
-
-__device__ __forceinline__ void snorm(v2s s[8]) // turbodecoder_win.h:480-498 (16-bit: subtract state 0)
-{
-#pragma unroll
-  for (int i = 1; i < 8; i++) s[i] = ssub2(s[i], s[0]);
-  s[0] = spl(0);
-}
-
-__device__ __forceinline__ void sfill(v2s s[8], short v)
-{
-#pragma unroll
-  for (int i = 0; i < 8; i++) s[i] = spl(v);
-}
-
-struct St8 {
-  uint4 a, b;
-};
-__device__ __forceinline__ St8 spack(const v2s s[8])
-{
-  return St8{make_uint4(W2(s[0]), W2(s[1]), W2(s[2]), W2(s[3])), make_uint4(W2(s[4]), W2(s[5]), W2(s[6]), W2(s[7]))};
-}
-__device__ __forceinline__ void sunpack(const St8& p, v2s s[8])
-{
-  s[0] = U2(p.a.x); s[1] = U2(p.a.y); s[2] = U2(p.a.z); s[3] = U2(p.a.w);
-  s[4] = U2(p.b.x); s[5] = U2(p.b.y); s[6] = U2(p.b.z); s[7] = U2(p.b.w);
-}
-__device__ __forceinline__ bool seq(const St8& p, const St8& q)
-{
-  return p.a.x == q.a.x && p.a.y == q.a.y && p.a.z == q.a.z && p.a.w == q.a.w && p.b.x == q.b.x && p.b.y == q.b.y &&
-         p.b.z == q.b.z && p.b.w == q.b.w;
-}
-
 // one code block in LDS, window-interleaved int16 [step k][window w] (u32 pair (2l, 2l+1) at k * NL + l)
 template <int NSB> struct Blk {
   static constexpr int NL = NSB / 2;
@@ -124,39 +85,6 @@ template <int NSB> struct Blk {
   const int16_t*       tail;
   int                  L;
   bool                 dec2, has_ap;
-
-  // x = sat(S + a1) (DEC1) or E (DEC2), y = P0 / P1 of lane l's windows at step k
-  __device__ __forceinline__ void in(int k, int l, v2s& x, v2s& y) const
-  {
-    const int i = k * NL + l;
-    if (!dec2) {
-      x = U2(xs[i]);
-      if (has_ap) x = sadd2(x, U2(a1[i]));
-      y = U2(p0[i]);
-    } else {
-      x = U2(ev[i]);
-      y = U2(p1[i]);
-    }
-  }
-  // the same for windows (w, w + 1) with w odd or -1 / NSB - 1 (the neighbour pairs of the window boundaries); a
-  // window outside [0, NSB) reads 0 (its half is discarded)
-  __device__ __forceinline__ short in1(const uint32_t* s, int k, int w) const
-  {
-    if (w < 0 || w >= NSB) return 0;
-    const uint32_t v = s[(k * NSB + w) >> 1];
-    return (short)((w & 1) ? (v >> 16) : v);
-  }
-  __device__ __forceinline__ void in_odd(int k, int w, v2s& x, v2s& y) const
-  {
-    if (!dec2) {
-      x = (v2s){in1(xs, k, w), in1(xs, k, w + 1)};
-      if (has_ap) x = sadd2(x, (v2s){in1(a1, k, w), in1(a1, k, w + 1)});
-      y = (v2s){in1(p0, k, w), in1(p0, k, w + 1)};
-    } else {
-      x = (v2s){in1(ev, k, w), in1(ev, k, w + 1)};
-      y = (v2s){in1(p1, k, w), in1(p1, k, w + 1)};
-    }
-  }
 
   // x, y (and the a-priori) of windows (w, w + 1) at step k for odd w (-1 and NSB - 1 included: the half outside the
   // code block reads a neighbouring word and is discarded): the pair straddles two words
@@ -173,84 +101,6 @@ template <int NSB> struct Blk {
     x = U2(__builtin_amdgcn_alignbit(o[1], o[0], 16));
     if (has_ap) x = sadd2(x, U2(__builtin_amdgcn_alignbit(o[5], o[4], 16)));
     y = U2(__builtin_amdgcn_alignbit(o[3], o[2], 16));
-  }
-
-  // row L of windows (2l, 2l+1): the 40-step warm-up over the first steps of windows (2l+1, 2l+2) from -INF
-  // (turbodecoder_win.h:566-631); the last window's from the wrapping 3-step tail trellis (:500-548).  The inputs of
-  // 8 steps are read before those steps run.
-  __device__ void beta_boundary(int l, v2s s[8]) const
-  {
-    sfill(s, -TDEC_INF);
-    for (int b = TDEC_WARMUP / 8 - 1; b >= 0; b--) {
-      uint32_t o[8][6];
-#pragma unroll
-      for (int i = 0; i < 8; i++) odd_words(8 * b + i, 2 * l + 1, o[i]);
-#pragma unroll
-      for (int i = 7; i >= 0; i--) {
-        const int k = 8 * b + i;
-        v2s       x, y;
-        odd_xy(o[i], x, y);
-        bstep<true>(s, x, y);
-        if ((k & 1) == 0 && k != 0) snorm(s);
-      }
-    }
-    if (l == NL - 1) {
-      const int16_t* T = tail + (dec2 ? 6 : 0);
-      v2s            tr[8];
-      tr[0] = spl(0);
-#pragma unroll
-      for (int i = 1; i < 8; i++) tr[i] = spl(-TDEC_INF);
-#pragma unroll
-      for (int t = 2; t >= 0; t--) bstep<false>(tr, spl(T[2 * t]), spl(T[2 * t + 1]));
-#pragma unroll
-      for (int i = 0; i < 8; i++) s[i] = (v2s){s[i].x, tr[i].y};
-    }
-  }
-
-  // alpha entering step 0 of windows (2l, 2l+1): 40 steps over the last steps of windows (2l-1, 2l) from -INF
-  // (turbodecoder_win.h:705-757); window 0 starts in state 0
-  __device__ void alpha_boundary(int l, v2s s[8]) const
-  {
-    sfill(s, -TDEC_INF);
-    for (int b = 0; b < TDEC_WARMUP / 8; b++) {
-      uint32_t o[8][6];
-#pragma unroll
-      for (int i = 0; i < 8; i++) odd_words(L - TDEC_WARMUP + 8 * b + i, 2 * l - 1, o[i]);
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const int k = 8 * b + i;
-        v2s       x, y;
-        odd_xy(o[i], x, y);
-        astep(s, x, y);
-        if ((k & 1) == 0 && k != 0) snorm(s);
-      }
-    }
-    if (l == 0) {
-      s[0].x = 0;
-#pragma unroll
-      for (int i = 1; i < 8; i++) s[i].x = -TDEC_INF;
-    }
-  }
-
-  // beta rows k0 down to k1 (no storage), normalised after row k when k is even and not 0
-  __device__ void beta_run(int l, v2s s[8], int k0, int k1) const
-  {
-    for (int k = k0; k >= k1; k--) {
-      v2s x, y;
-      in(k, l, x, y);
-      bstep<true>(s, x, y);
-      if ((k & 1) == 0 && k != 0) snorm(s);
-    }
-  }
-  // alpha steps k0 .. k1
-  __device__ void alpha_run(int l, v2s s[8], int k0, int k1) const
-  {
-    for (int k = k0; k <= k1; k++) {
-      v2s x, y;
-      in(k, l, x, y);
-      astep(s, x, y);
-      if ((k & 1) == 0 && k != 0) snorm(s);
-    }
   }
 };
 
@@ -293,40 +143,118 @@ __device__ __forceinline__ void dbit(uint32_t* bits, uint32_t m, bool v)
   atomicOr(&bits[by >> 2], (uint32_t)v << (((by & 3) << 3) + 7 - (m & 7))); // (no branch: or-ing 0 is harmless)
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Distributed trellis: the 8 states of a window pair over 8 lanes (lane q of group p holds one state, both windows of
+// the pair packed as before), so one trellis step is one exchange with a partner lane, two saturating adds and a
+// max per lane instead of 26 packed operations in one lane.  Rotating layout: at phase K (steps taken mod 3) lane q
+// holds state rotl3(q, K) in the beta recursion and rotr3(q, K) in the alpha one; the two predecessors of every
+// successor then sit in lanes q and q ^ D (beta D = 4 >> K, alpha D = 1 << K) and each lane's successor is the
+// state it holds at phase K + 1 (the shift-register structure of the constituent code: beta successors 2j, 2j+1 of
+// j, j+4; alpha successors m, m+4 of 2m, 2m+1).  State 0 is always in lane q = 0.  The branch metric each lane adds
+// to its own and its partner's metric is one of 0, x, y, sat(x + y) (bstep / acands): by held state s, beta
+// (s & 3, 3 - (s & 3)), alpha (s >> 1, 3 - (s >> 1)) as (x bit, y bit) codes; the results are the register form's bit
+// for bit (same saturating operations on the same operands; max is symmetric).
+__device__ __forceinline__ uint32_t rotl3(uint32_t q, int K) { return ((q << K) | (q >> ((3 - K) % 3))) & 7u; }
+__device__ __forceinline__ uint32_t rotr3(uint32_t q, int K) { return ((q >> K) | (q << ((3 - K) % 3))) & 7u; }
+
+struct Lane8 {
+  uint32_t mxo[3], myo[3], mxp[3], myp[3]; // per phase: masks selecting x / y for the own and the partner metric
+  uint32_t held[3];                        // state held at phase K
+};
+__device__ __forceinline__ Lane8 lane8(uint32_t q, bool beta)
+{
+  Lane8 c;
+#pragma unroll
+  for (int K = 0; K < 3; K++) {
+    const uint32_t s  = beta ? rotl3(q, K) : rotr3(q, K);
+    const uint32_t go = beta ? (s & 3u) : (s >> 1), gp = 3u - go;
+    c.held[K] = s;
+    c.mxo[K]  = (go & 1u) ? ~0u : 0u;
+    c.myo[K]  = (go & 2u) ? ~0u : 0u;
+    c.mxp[K]  = (gp & 1u) ? ~0u : 0u;
+    c.myp[K]  = (gp & 2u) ? ~0u : 0u;
+  }
+  return c;
+}
+
+// the value of lane q ^ D within each group of 8 (DPP: quad permutes; 4 apart by row shifts under bank masks)
+template <int D> __device__ __forceinline__ v2s partner(v2s v)
+{
+  const int w = (int)W2(v);
+  if constexpr (D == 1) {
+    return U2((uint32_t)__builtin_amdgcn_mov_dpp(w, 0xB1, 0xF, 0xF, false)); // quad_perm [1,0,3,2]
+  } else if constexpr (D == 2) {
+    return U2((uint32_t)__builtin_amdgcn_mov_dpp(w, 0x4E, 0xF, 0xF, false)); // quad_perm [2,3,0,1]
+  } else {
+    const int r = __builtin_amdgcn_update_dpp(w, w, 0x114, 0xF, 0xA, false); // row_shr:4 into lanes 4-7 of each 8
+    return U2((uint32_t)__builtin_amdgcn_update_dpp(r, w, 0x104, 0xF, 0x5, false)); // row_shl:4 into lanes 0-3
+  }
+}
+// state 0's value (lane q = 0 of the group) in every lane of the group
+__device__ __forceinline__ v2s bcast0(v2s v)
+{
+  const int b = __builtin_amdgcn_mov_dpp((int)W2(v), 0x00, 0xF, 0xF, false); // quad_perm [0,0,0,0]
+  return U2((uint32_t)__builtin_amdgcn_update_dpp(b, b, 0x114, 0xF, 0xA, false));
+}
+// one trellis step at phase PH (saturating, turbodecoder_win.h:640-676 beta, :771-800 alpha)
+template <bool BETA, int PH> __device__ __forceinline__ v2s dstep(v2s st, v2s x, v2s y, const Lane8& c)
+{
+  constexpr int D  = BETA ? (4 >> PH) : (1 << PH);
+  const v2s     pr = partner<D>(st);
+  const v2s     go = sadd2(U2(W2(x) & c.mxo[PH]), U2(W2(y) & c.myo[PH]));
+  const v2s     gp = sadd2(U2(W2(x) & c.mxp[PH]), U2(W2(y) & c.myp[PH]));
+  return vmax2(sadd2(st, go), sadd2(pr, gp));
+}
+// turbodecoder_win.h:480-498 (16-bit: subtract state 0; state 0 itself becomes 0)
+__device__ __forceinline__ v2s dnorm(v2s st) { return ssub2(st, bcast0(st)); }
+
+template <int P> struct Par {
+  static constexpr int value = P;
+};
+// f(Par<I>{}) for I = B .. E-1 (compile-time indices for unrolled steps)
+template <int B, int E, typename F> __device__ __forceinline__ void sfor(F&& f)
+{
+  if constexpr (B < E) {
+    f(Par<B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
 } // namespace
 
-// LDS of one code block: systematic, the current half-iteration's parity stream, a1, ev and its interleaver
-// destination table (K/2 words each), alpha states of steps [0, H) and beta rows of steps [H, L) (8 words per lane
-// and step each), the CRC byte table, the decision bitmap (K/32 words)
+// LDS of one code block: systematic, the current half-iteration's parity stream, a1 and ev (K/2 words each), alpha
+// states of steps [0, H) and beta rows of steps [H, L) (8 words per lane and step each), the two waves' output
+// staging (64 x 8 words each), the CRC byte table, the decision bitmap ((K + 31) / 32 words)
 size_t tdec_lat_lds(int K, int nsb)
 {
   const int L = K / nsb, NL = nsb / 2;
-  return (size_t)K / 2 * 4 * 5 + (size_t)L * NL * 8 * 4 + 256 * 4 + (size_t)(K + 31) / 32 * 4;
+  return (size_t)K / 2 * 4 * 4 + (size_t)L * NL * 8 * 4 + 2 * 64 * 8 * 4 + 256 * 4 + (size_t)(K + 31) / 32 * 4;
 }
 
 template <int NSB>
-__global__ __launch_bounds__(128) void tdec_win_lat(TdecLatArgs A)
+__global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
 {
-  constexpr int NL = NSB / 2, BK = 8; // window pairs; steps per block of the unrolled loops
-  const int     cb = blockIdx.x, t = threadIdx.x;
+  // NL window pairs; PB steps per output pass (PB x NL = 64 lanes)
+  constexpr int NL = NSB / 2, PB = 64 / NL;
+  const int cb = blockIdx.x, t = threadIdx.x, nt = blockDim.x, bw = A.bwave;
   if (A.done[cb]) return; // decoded in an earlier transmission (dlsch_tb_prologue)
   const DlschCheckArgs& C = A.chk;
   const CbDesc&         d = C.desc[cb];
-  // meeting point H: the alpha lane runs H state-only steps then L - H output steps, the beta lane L - H rows then H
-  // rows with outputs (a row and an output each); L / 3 balances the two (turbodecoder_win.h's output step costs
-  // about twice a recursion step)
-  const int             K = A.K, L = K / NSB, H = L / 3;
+  // meeting point H: the alpha wave runs steps [0, H) storing its states, the beta wave rows L .. H+1 storing them;
+  // then each continues over the other half with the outputs, which are computed PB steps at a time by all 64
+  // lanes of the wave (the recursion itself runs on NL lanes): both waves do the same work when H = L / 2
+  const int K = A.K, L = K / NSB, H = L / 2;
 
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* xs   = lds;                       // K/2 words each
-  uint32_t* pc   = xs + K / 2;                // P0 (DEC1) / P1 (DEC2) of this half-iteration
+  uint32_t* xs   = lds;                           // K/2 words each
+  uint32_t* pc   = xs + K / 2;                    // P0 (DEC1) / P1 (DEC2) of this half-iteration
   uint32_t* a1   = pc + K / 2;
   uint32_t* ev   = a1 + K / 2;
-  uint32_t* tb   = ev + K / 2;                // dstE (DEC1) / dstA (DEC2), [L][NL]
-  uint32_t* am   = tb + K / 2;                // [H][NL][8] alpha entering states of steps 0 .. H-1
-  uint32_t* bm   = am + (size_t)H * NL * 8;   // [L-H][NL][8] beta rows k+1 of steps H .. L-1
-  uint32_t* tl   = bm + (size_t)(L - H) * NL * 8; // CRC byte table
-  uint32_t* bits = tl + 256;                  // K/8 decision bytes
+  uint32_t* am   = ev + K / 2;                    // [H][NL][8] alpha entering states of steps 0 .. H-1
+  uint32_t* bm   = am + (size_t)H * NL * 8;       // [L-H][NL][8] beta rows k+1 of steps H .. L-1
+  uint32_t* sgb  = bm + (size_t)(L - H) * NL * 8; // [2][PB][NL][8] per-wave output staging
+  uint32_t* tl   = sgb + 2 * 64 * 8;              // CRC byte table
+  uint32_t* bits = tl + 256;                      // K/8 decision bytes
   __shared__ int16_t  tail[12];
   __shared__ uint32_t fin_s;
 
@@ -337,7 +265,7 @@ __global__ __launch_bounds__(128) void tdec_win_lat(TdecLatArgs A)
   // as zero (rm_image.h)
   auto load_stream = [&](int s, uint32_t* dst) {
     const uint4* src = (const uint4*)(in + (size_t)s * (K + 32));
-    for (int i = t; i < K / 8; i += 128) {
+    for (int i = t; i < K / 8; i += nt) {
       uint4 v = src[i];
       if (rmk && s > 0) {
         const int row = (i * 8) / NSB;
@@ -347,20 +275,28 @@ __global__ __launch_bounds__(128) void tdec_win_lat(TdecLatArgs A)
     }
   };
   load_stream(0, xs);
-  for (int i = t; i < K / 2; i += 128) {
+  for (int i = t; i < K / 2; i += nt) {
     a1[i] = 0;
     ev[i] = 0;
   }
   if (t < 12) tail[t] = in[3 * (K + 32) + t];
   {
     const CrcTable* ct = d.C > 1 ? C.crc24b : C.crc24a;
-    for (int i = t; i < 256; i += 128) tl[i] = ct->t[i];
+    for (int i = t; i < 256; i += nt) tl[i] = ct->t[i];
   }
 
-  // the alpha lanes in wave 0, the beta lanes in wave 1: the two recursions run at the same time on different
-  // SIMDs (in one wave their divergent code paths would be issued one after the other)
-  const bool alpha = t < NL, beta = t >= 64 && t < 64 + NL;
-  const int  l     = alpha ? t : t - 64;
+  // wave 0 runs alpha, wave 1 (bw) beta: the two recursions at the same time on different SIMDs; in a recursion lane
+  // (p, q) = (lane / 8, lane % 8) holds one state of window pair p (distributed trellis), and in an output pass lane
+  // (i_p, lp) = (lane / NL, lane % NL) takes step i_p of the pass for pair lp
+  const int  wv = t >> 6, lane = t & 63, p = lane >> 3, q = lane & 7, i_p = lane / NL, lp = lane % NL;
+  const bool alpha = wv == 0, rec = lane < 8 * NL && (alpha || wv == bw);
+  const Lane8 cl = lane8((uint32_t)q, !alpha);
+  v2s         st   = spl(0);      // this lane's state
+  int         ka = 0, pha = 0;    // alpha: next step and its phase
+  int         kb = 0, phb = 0;    // beta: next row and the phase of the step computing it
+  uint32_t*  sg    = sgb + (alpha ? 0 : 64 * 8);
+  __shared__ uint32_t simd_s[4]; // (measurement) the SIMD each wave runs on
+  if (A.prof && lane == 0) simd_s[wv] = (__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4) & 3u) + 1u;
   // A.prof (measurement): shader-clock cycles of each phase, taken by lane 0 after the barriers that end them
   uint64_t pcy[11] = {};
   uint64_t tp      = A.prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -374,40 +310,24 @@ __global__ __launch_bounds__(128) void tdec_win_lat(TdecLatArgs A)
 
   for (uint32_t h = 0; h < C.max_its; h++) {
     const bool dec2 = (h & 1) != 0, has_ap = !dec2 && h > 0;
-    // this half-iteration's parity stream and destination table; the decision bitmap cleared
+    // this half-iteration's parity stream; the decision bitmap cleared
     load_stream(dec2 ? 2 : 1, pc);
-    {
-      const uint4* g = (const uint4*)(dec2 ? A.dstA : A.dstE);
-      for (int i = t; i < K / 8; i += 128) ((uint4*)tb)[i] = g[i];
-      for (int i = t; i < (K + 31) / 32; i += 128) bits[i] = 0; // (K/8 bytes need not fill whole words: K = 408)
-    }
+    for (int i = t; i < (K + 31) / 32; i += nt) bits[i] = 0; // (K/8 bytes need not fill whole words: K = 408)
     __syncthreads();
     mark(0);
-    Blk<NSB>       B{xs, pc, pc, a1, ev, tail, L, dec2, has_ap};
+    Blk<NSB>        B{xs, pc, pc, a1, ev, tail, L, dec2, has_ap};
     const uint32_t* X   = dec2 ? ev : xs;
+    const uint32_t* tbg = dec2 ? A.dstA : A.dstE; // [L][NL] output destinations (row j' * 128 + window per half)
     int16_t*        dst = (int16_t*)(dec2 ? a1 : ev);
-    v2s             st[8];
-    // the 8 steps' inputs of lane l from step k0 on (k0 + i clamped to [0, L))
-    auto loadx = [&](int k0, int dir, uint32_t (&xv)[BK + 1], uint32_t (&yv)[BK + 1], uint32_t (&av)[BK + 1], int n) {
-#pragma unroll
-      for (int i = 0; i < BK + 1; i++) {
-        if (i < n) {
-          const int k = min(max(k0 + dir * i, 0), L - 1), ix = k * NL + l;
-          xv[i] = X[ix];
-          yv[i] = pc[ix];
-          av[i] = a1[ix]; // (read whatever the half-iteration: used only when it has an a-priori)
-        }
-      }
-    };
     auto xin = [&](uint32_t xw, uint32_t yw, uint32_t aw, v2s& x, v2s& y, v2s& ap) {
       ap = U2(aw);
       x  = U2(xw);
       if (has_ap) x = sadd2(x, ap);
       y = U2(yw);
     };
-    // output of step k (windows 2l, 2l+1): DEC1 E = out - a1 at the interleaved position, DEC2 A1 = out - E at the
-    // natural one; its decision bit at the natural position (DEC1: own, DEC2: the destination's)
-    auto put = [&](int k, uint32_t e, v2s x, v2s ap, v2s out) {
+    // output of step k for pair pp (windows 2pp, 2pp+1): DEC1 E = out - a1 at the interleaved position, DEC2
+    // A1 = out - E at the natural one; its decision bit at the natural position (DEC1: own, DEC2: the destination's)
+    auto put = [&](int k, int pp, uint32_t e, v2s x, v2s ap, v2s out) {
       const v2s      o   = dec2 ? out - x : (has_ap ? out - ap : out);
       const uint32_t olo = e & 0xffffu, ohi = e >> 16; // row j' * 128 + window
       dst[(olo >> 7) * NSB + (olo & 127)] = o.x;
@@ -416,121 +336,213 @@ __global__ __launch_bounds__(128) void tdec_win_lat(TdecLatArgs A)
         dbit(bits, (olo & 127) * L + (olo >> 7), out.x > 0);
         dbit(bits, (ohi & 127) * L + (ohi >> 7), out.y > 0);
       } else {
-        dbit(bits, 2 * l * L + k, out.x > 0);
-        dbit(bits, (2 * l + 1) * L + k, out.y > 0);
+        dbit(bits, 2 * pp * L + k, out.x > 0);
+        dbit(bits, (2 * pp + 1) * L + k, out.y > 0);
+      }
+    };
+    // one output pass: lane (i_p, lp) outputs step k (valid when ok) from the alpha entering state at as and the
+    // beta row at bs (turbodecoder_win.h:771-832); e its destination word, loaded before the recursion steps
+    auto opass = [&](bool ok, int k, const uint32_t* as, const uint32_t* bs, uint32_t e) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (ok) {
+        const int ix = k * NL + lp;
+        v2s       x, y, ap, a8[8], row[8];
+        xin(X[ix], pc[ix], a1[ix], x, y, ap);
+        ld8(as, a8);
+        ld8(bs, row);
+        put(k, lp, e, x, ap, out_llr(a8, x, y, row, false));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // this lane's inputs of step k (pair p, the same in the group's 8 lanes)
+    auto inp = [&](int k, v2s& x, v2s& y) {
+      v2s ap;
+      const int ix = k * NL + p;
+      xin(X[ix], pc[ix], a1[ix], x, y, ap);
+    };
+    // the 8 steps' inputs from step k on in direction dir, read before the steps
+    auto load8 = [&](int k, int dir, v2s (&xv)[8], v2s (&yv)[8]) {
+      uint32_t xw[8], yw[8], aw[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int ix = (k + dir * i) * NL + p;
+        xw[i] = X[ix];
+        yw[i] = pc[ix];
+        aw[i] = a1[ix]; // (read whatever the half-iteration: used only when it has an a-priori)
+      }
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        v2s ap;
+        xin(xw[i], yw[i], aw[i], xv[i], yv[i], ap);
+      }
+    };
+    // alpha step k at phase PH: the entering state stored at S[base + k * rs + p * 8 + state], then the step and the
+    // normalisation after it when nrm (step k even and not 0)
+    auto a_one = [&](auto PH, int k, bool nrm, uint32_t* S, int base, int rs) {
+      constexpr int ph = decltype(PH)::value;
+      v2s           x, y;
+      inp(k, x, y);
+      S[base + k * rs + p * 8 + (int)cl.held[ph]] = W2(st);
+      st = dstep<false, ph>(st, x, y, cl);
+      if (nrm) st = dnorm(st);
+    };
+    // beta row k from row k+1 at phase PH (the row stored before its normalisation, at the phase after the step)
+    auto b_one = [&](auto PH, int k, bool nrm, uint32_t* S, int base, int rs) {
+      constexpr int ph = decltype(PH)::value;
+      v2s           x, y;
+      inp(k, x, y);
+      st = dstep<true, ph>(st, x, y, cl);
+      S[base + k * rs + p * 8 + (int)cl.held[(ph + 1) % 3]] = W2(st);
+      if (nrm) st = dnorm(st);
+    };
+    // 8 steps from k with the phase P0 and the parity Q0 of k template constants (normalisations placed at compile
+    // time; k >= 1)
+    auto a_blk = [&](auto P0, auto Q0, int k, uint32_t* S, int base, int rs) {
+      constexpr int P = decltype(P0)::value, Q = decltype(Q0)::value;
+      v2s           xv[8], yv[8];
+      load8(k, 1, xv, yv);
+      sfor<0, 8>([&](auto I) {
+        constexpr int i = decltype(I)::value, ph = (P + i) % 3;
+        S[base + (k + i) * rs + p * 8 + (int)cl.held[ph]] = W2(st);
+        st = dstep<false, ph>(st, xv[i], yv[i], cl);
+        if constexpr (((Q + i) & 1) == 0) st = dnorm(st);
+      });
+    };
+    auto b_blk = [&](auto P0, auto Q0, int k, uint32_t* S, int base, int rs) {
+      constexpr int P = decltype(P0)::value, Q = decltype(Q0)::value;
+      v2s           xv[8], yv[8];
+      load8(k, -1, xv, yv);
+      sfor<0, 8>([&](auto I) {
+        constexpr int i = decltype(I)::value, ph = (P + i) % 3;
+        st = dstep<true, ph>(st, xv[i], yv[i], cl);
+        S[base + (k - i) * rs + p * 8 + (int)cl.held[(ph + 1) % 3]] = W2(st);
+        if constexpr (((Q + i) & 1) == 0) st = dnorm(st);
+      });
+    };
+    // n alpha steps from k (k >= 1) / n beta rows from k down (rows >= 1) at phase ph: blocks of 8 dispatched on
+    // (phase, parity), then single steps; k and ph advanced
+    auto a_run = [&](int& k, int n, int& ph, uint32_t* S, int base, int rs) {
+      const int e = k + n;
+      for (; k + 8 <= e; k += 8, ph = (ph + 2) % 3) {
+        switch (ph * 2 + (k & 1)) {
+          case 0: a_blk(Par<0>{}, Par<0>{}, k, S, base, rs); break;
+          case 1: a_blk(Par<0>{}, Par<1>{}, k, S, base, rs); break;
+          case 2: a_blk(Par<1>{}, Par<0>{}, k, S, base, rs); break;
+          case 3: a_blk(Par<1>{}, Par<1>{}, k, S, base, rs); break;
+          case 4: a_blk(Par<2>{}, Par<0>{}, k, S, base, rs); break;
+          default: a_blk(Par<2>{}, Par<1>{}, k, S, base, rs); break;
+        }
+      }
+      for (; k < e; k++, ph = ph == 2 ? 0 : ph + 1) {
+        const bool nrm = (k & 1) == 0;
+        if (ph == 0) a_one(Par<0>{}, k, nrm, S, base, rs);
+        else if (ph == 1) a_one(Par<1>{}, k, nrm, S, base, rs);
+        else a_one(Par<2>{}, k, nrm, S, base, rs);
+      }
+    };
+    auto b_run = [&](int& k, int n, int& ph, uint32_t* S, int base, int rs) {
+      const int e = k - n;
+      for (; k - 8 >= e; k -= 8, ph = (ph + 2) % 3) {
+        switch (ph * 2 + (k & 1)) {
+          case 0: b_blk(Par<0>{}, Par<0>{}, k, S, base, rs); break;
+          case 1: b_blk(Par<0>{}, Par<1>{}, k, S, base, rs); break;
+          case 2: b_blk(Par<1>{}, Par<0>{}, k, S, base, rs); break;
+          case 3: b_blk(Par<1>{}, Par<1>{}, k, S, base, rs); break;
+          case 4: b_blk(Par<2>{}, Par<0>{}, k, S, base, rs); break;
+          default: b_blk(Par<2>{}, Par<1>{}, k, S, base, rs); break;
+        }
+      }
+      for (; k > e; k--, ph = ph == 2 ? 0 : ph + 1) {
+        const bool nrm = (k & 1) == 0;
+        if (ph == 0) b_one(Par<0>{}, k, nrm, S, base, rs);
+        else if (ph == 1) b_one(Par<1>{}, k, nrm, S, base, rs);
+        else b_one(Par<2>{}, k, nrm, S, base, rs);
       }
     };
 
     // ------------------------------------------------ first parts: alpha over [0, H), beta over rows L .. H+1
-    // Every loop runs whole blocks of BK steps, their inputs (and stored rows, destinations) read before the steps,
-    // without per-step guards, then the remaining steps one by one.
-    auto a_step = [&](int k, uint32_t xw, uint32_t yw, uint32_t aw) {
-      v2s x, y, ap;
-      xin(xw, yw, aw, x, y, ap);
-      st8(am + ((size_t)k * NL + l) * 8, st);
-      astep(st, x, y);
-      if ((k & 1) == 0 && k != 0) snorm(st);
-    };
-    auto b_step = [&](int k, uint32_t xw, uint32_t yw, uint32_t aw) { // row k (> H), the beta row of step k - 1
-      v2s x, y, ap;
-      xin(xw, yw, aw, x, y, ap);
-      bstep<true>(st, x, y);
-      st8(bm + ((size_t)(k - 1 - H) * NL + l) * 8, st);
-      if ((k & 1) == 0) snorm(st);
-    };
-    if (alpha) {
-      B.alpha_boundary(l, st);
-      const int kf = H / BK * BK;
-      for (int k0 = 0; k0 < kf; k0 += BK) {
-        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1];
-        loadx(k0, 1, xv, yv, av, BK);
+    constexpr int RS = NL * 8; // words per step of a state array
+    if (rec) {
+      st = spl(-TDEC_INF);
+      if (alpha) {
+        // alpha entering step 0 of windows (2p, 2p+1): 40 steps over the last steps of windows (2p-1, 2p) from -INF
+        // (turbodecoder_win.h:705-757); window 0 starts in state 0 (lane q = 0 at every phase)
+        sfor<0, TDEC_WARMUP / 8>([&](auto Bt) {
+          constexpr int b = decltype(Bt)::value;
+          uint32_t      o[8][6];
 #pragma unroll
-        for (int i = 0; i < BK; i++) a_step(k0 + i, xv[i], yv[i], av[i]);
-      }
-      for (int k = kf; k < H; k++) {
-        const int ix = k * NL + l;
-        a_step(k, X[ix], pc[ix], a1[ix]);
-      }
-    } else if (beta) {
-      B.beta_boundary(l, st); // row L
-      st8(bm + ((size_t)(L - 1 - H) * NL + l) * 8, st);
-      const int n = L - 1 - H, kf = L - 1 - n / BK * BK; // rows L-1 .. H+1
-      for (int k0 = L - 1; k0 > kf; k0 -= BK) {
-        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1];
-        loadx(k0, -1, xv, yv, av, BK);
+          for (int i = 0; i < 8; i++) B.odd_words(L - TDEC_WARMUP + 8 * b + i, 2 * p - 1, o[i]);
+          sfor<0, 8>([&](auto I) {
+            constexpr int i = decltype(I)::value, j = 8 * b + i;
+            v2s           x, y;
+            B.odd_xy(o[i], x, y);
+            st = dstep<false, j % 3>(st, x, y, cl);
+            if constexpr ((j & 1) == 0 && j != 0) st = dnorm(st);
+          });
+        });
+        if (p == 0) st.x = q == 0 ? (short)0 : (short)-TDEC_INF;
+        ka = 0, pha = TDEC_WARMUP % 3;
+        a_one(Par<TDEC_WARMUP % 3>{}, 0, false, am, 0, RS); // step 0 alone: no normalisation after it
+        ka = 1, pha = (TDEC_WARMUP + 1) % 3;
+        a_run(ka, H - 1, pha, am, 0, RS);
+      } else {
+        // row L of windows (2p, 2p+1): the 40-step warm-up over the first steps of windows (2p+1, 2p+2) from -INF
+        // (turbodecoder_win.h:566-631); the last window's from the wrapping 3-step tail trellis (:500-548)
+        sfor<0, TDEC_WARMUP / 8>([&](auto Bt) {
+          constexpr int b = TDEC_WARMUP / 8 - 1 - decltype(Bt)::value;
+          uint32_t      o[8][6];
 #pragma unroll
-        for (int i = 0; i < BK; i++) b_step(k0 - i, xv[i], yv[i], av[i]);
-      }
-      for (int k = kf; k > H; k--) {
-        const int ix = k * NL + l;
-        b_step(k, X[ix], pc[ix], a1[ix]);
+          for (int i = 0; i < 8; i++) B.odd_words(8 * b + i, 2 * p + 1, o[i]);
+          sfor<0, 8>([&](auto I) {
+            constexpr int i = 7 - decltype(I)::value, k = 8 * b + i, j = TDEC_WARMUP - 1 - k;
+            v2s           x, y;
+            B.odd_xy(o[i], x, y);
+            st = dstep<true, j % 3>(st, x, y, cl);
+            if constexpr ((k & 1) == 0 && k != 0) st = dnorm(st);
+          });
+        });
+        if (p == NL - 1) {
+          const int16_t* T = tail + (dec2 ? 6 : 0);
+          v2s            tr[8];
+          tr[0] = spl(0);
+#pragma unroll
+          for (int i = 1; i < 8; i++) tr[i] = spl(-TDEC_INF);
+#pragma unroll
+          for (int tt = 2; tt >= 0; tt--) bstep<false>(tr, spl(T[2 * tt]), spl(T[2 * tt + 1]));
+          const uint32_t hs = cl.held[TDEC_WARMUP % 3];
+          short          v  = tr[0].y;
+#pragma unroll
+          for (int i = 1; i < 8; i++) v = hs == (uint32_t)i ? tr[i].y : v;
+          st.y = v;
+        }
+        // row L is the beta row of step L-1; then rows L-1 .. H+1 (row k at bm[k-1-H])
+        bm[(L - 1 - H) * RS + p * 8 + (int)cl.held[TDEC_WARMUP % 3]] = W2(st);
+        kb = L - 1, phb = TDEC_WARMUP % 3;
+        b_run(kb, L - 1 - H, phb, bm, -(1 + H) * RS, RS);
       }
     }
     __syncthreads();
     mark(1);
-    // ------------------------------------------------ second parts with the outputs
-    auto ao_step = [&](int k, uint32_t xw, uint32_t yw, uint32_t aw, const v2s (&row)[8], uint32_t e) {
-      v2s x, y, ap;
-      xin(xw, yw, aw, x, y, ap);
-      const v2s out = out_llr(st, x, y, row, true);
-      if ((k & 1) == 0 && k != 0) snorm(st);
-      put(k, e, x, ap, out);
-    };
-    // row k, then the output of step k - 1 from its stored alpha state
-    auto bo_step = [&](int k, uint32_t xw, uint32_t yw, uint32_t aw, uint32_t xw1, uint32_t yw1, uint32_t aw1,
-                       const v2s (&as)[8], uint32_t e) {
-      v2s x, y, ap, row[8];
-      xin(xw, yw, aw, x, y, ap);
-      bstep<true>(st, x, y);
-#pragma unroll
-      for (int q = 0; q < 8; q++) row[q] = st[q];
-      if ((k & 1) == 0) snorm(st);
-      xin(xw1, yw1, aw1, x, y, ap);
-      v2s a8[8];
-#pragma unroll
-      for (int q = 0; q < 8; q++) a8[q] = as[q];
-      put(k - 1, e, x, ap, out_llr(a8, x, y, row, false));
-    };
+    // ------------------------------------------------ second parts: PB recursion steps, then their outputs
     if (alpha) {
-      const int kf = H + (L - H) / BK * BK;
-      for (int k0 = H; k0 < kf; k0 += BK) { // step k with beta row k+1
-        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1], ev8[BK];
-        v2s      rw[BK][8];
-        loadx(k0, 1, xv, yv, av, BK);
-#pragma unroll
-        for (int i = 0; i < BK; i++) {
-          ld8(bm + ((size_t)(k0 + i - H) * NL + l) * 8, rw[i]);
-          ev8[i] = tb[(k0 + i) * NL + l];
-        }
-#pragma unroll
-        for (int i = 0; i < BK; i++) ao_step(k0 + i, xv[i], yv[i], av[i], rw[i], ev8[i]);
+      for (int k0 = H; k0 < L; k0 += PB) { // steps k0 .. k0+n-1, with beta rows from the first part
+        const int      n = min(PB, L - k0), k = k0 + i_p;
+        const bool     ok = i_p < n;
+        const uint32_t e  = ok ? tbg[k * NL + lp] : 0u;
+        if (rec) a_run(ka, n, pha, sg, -k0 * RS, RS);
+        opass(ok, k, sg + (size_t)lane * 8, bm + ((size_t)(k - H) * NL + lp) * 8, e);
       }
-      for (int k = kf; k < L; k++) {
-        const int ix = k * NL + l;
-        v2s       rw[8];
-        ld8(bm + ((size_t)(k - H) * NL + l) * 8, rw);
-        ao_step(k, X[ix], pc[ix], a1[ix], rw, tb[ix]);
-      }
-    } else if (beta) {
-      const int kf = H - H / BK * BK; // rows H .. kf+1 in whole blocks, then kf .. 1
-      for (int k0 = H; k0 > kf; k0 -= BK) {
-        uint32_t xv[BK + 1], yv[BK + 1], av[BK + 1], ev8[BK];
-        v2s      as[BK][8];
-        loadx(k0, -1, xv, yv, av, BK + 1); // inputs of steps k0 .. k0 - 8
-#pragma unroll
-        for (int i = 0; i < BK; i++) {
-          ld8(am + ((size_t)(k0 - i - 1) * NL + l) * 8, as[i]);
-          ev8[i] = tb[(k0 - i - 1) * NL + l];
-        }
-#pragma unroll
-        for (int i = 0; i < BK; i++)
-          bo_step(k0 - i, xv[i], yv[i], av[i], xv[i + 1], yv[i + 1], av[i + 1], as[i], ev8[i]);
-      }
-      for (int k = kf; k >= 1; k--) {
-        const int ix = k * NL + l, ix1 = (k - 1) * NL + l;
-        v2s       as[8];
-        ld8(am + (size_t)ix1 * 8, as);
-        bo_step(k, X[ix], pc[ix], a1[ix], X[ix1], pc[ix1], a1[ix1], as, tb[ix1]);
+    } else if (wv == bw) {
+      for (int k0 = H; k0 >= 1; k0 -= PB) { // rows k0 .. k0-n+1 = beta rows of steps k0-1 .. k0-n
+        const int      n = min(PB, k0), k = k0 - 1 - i_p;
+        const bool     ok = i_p < n;
+        const uint32_t e  = ok ? tbg[k * NL + lp] : 0u;
+        if (rec) b_run(kb, n, phb, sg, k0 * RS, -RS);
+        opass(ok, k, am + ((size_t)k * NL + lp) * 8, sg + (size_t)lane * 8, e);
       }
     }
     __syncthreads();
@@ -566,6 +578,9 @@ __global__ __launch_bounds__(128) void tdec_win_lat(TdecLatArgs A)
   }
   if (A.prof && t == 0) {
     pcy[10] = 1;
+    pcy[5]  = simd_s[0];
+    pcy[6]  = simd_s[bw];
+    pcy[7]  = simd_s[0] == simd_s[bw];
 #pragma unroll
     for (int k = 0; k < 11; k++) atomicAdd((unsigned long long*)&A.prof[k], (unsigned long long)pcy[k]);
   }
@@ -584,9 +599,9 @@ hipError_t tdec_lat_launch(int nsb, const TdecLatArgs& a, hipStream_t s)
     attr[ix] = lds;
   }
   if (nsb == 16) {
-    hipLaunchKernelGGL(tdec_win_lat<16>, dim3(a.ncb), dim3(128), lds, s, a);
+    hipLaunchKernelGGL(tdec_win_lat<16>, dim3(a.ncb), dim3(64 * (2 * a.bwave)), lds, s, a);
   } else {
-    hipLaunchKernelGGL(tdec_win_lat<8>, dim3(a.ncb), dim3(128), lds, s, a);
+    hipLaunchKernelGGL(tdec_win_lat<8>, dim3(a.ncb), dim3(64 * (2 * a.bwave)), lds, s, a);
   }
   return hipGetLastError();
 }

@@ -16,12 +16,13 @@ import oracle  # noqa: E402
 from srsran_amd import lib  # noqa: E402
 from srsran_amd.dlsch import Dlsch, SoftbufferPool  # noqa: E402
 
-NAMES = ["load", "first_halves", "second_halves", "decisions", "check", "-", "-", "-", "-", "half_its", "cbs"]
+NAMES = ["load", "first_halves", "second_halves", "decisions", "check", "simd_alpha", "simd_beta", "same_simd", "-", "half_its", "cbs"]
 rng = np.random.default_rng(1)
-for snr in (9.0, 5.5, 30.0):
+QUICK = os.environ.get("LAT_PROBE_QUICK") == "1"  # the 30 dB latency case only
+for snr in ((30.0,) if QUICK else (9.0, 5.5, 30.0)):
     cases = [(97896, 8, 115200, snr)] * 2
     llrs = [oracle.make_tb(rng, t, q, g, 0, s)[1] for (t, q, g, s) in cases]
-    for path in ("throughput", "latency"):
+    for path in (("latency",) if QUICK else ("throughput", "latency")):
         lib().mi355_dlsch_set_latency_path(512 if path == "latency" else 0)
         dl = Dlsch(0, 10)
         pool = SoftbufferPool(2, 32)
@@ -44,5 +45,6 @@ for snr in (9.0, 5.5, 30.0):
             res["per_cb_half_it_kcycles"] = {NAMES[k]: round(v[k] / hi / 1e3, 2) for k in (1, 2, 3, 4)}
             res["load_kcycles_per_cb"] = round(v[0] / cb / 1e3, 2)
             res["half_its_per_cb"] = round(hi / cb, 2)
+            res["simd"] = {NAMES[k]: round(v[k] / cb - (k < 7), 2) for k in (5, 6, 7)}
         print(json.dumps(res), flush=True)
         dl.close() if hasattr(dl, "close") else None
