@@ -78,7 +78,7 @@ void mi355_dlsch_set_profiling(mi355_dlsch_t* q, int enable);
 /* Latency path (process-wide): a decode call with at most max_cbs code blocks decodes its window-decoder (K > 400)
  * groups with one wave per code block, every half-iteration and the CRC early stop in one launch, alpha and beta of
  * each window run at the same time (results identical to the half-iteration-per-launch path).  A negative argument
- * keeps the current value.  Default: MI355_DLSCH_LAT_CBS or 0 (off).  Returns the previous max_cbs. */
+ * keeps the current value.  Default: MI355_DLSCH_LAT_CBS or 256 (0: off).  Returns the previous max_cbs. */
 int mi355_dlsch_set_latency_path(int max_cbs);
 /* Measurement: enable = 1 (re)arms the latency path's phase counters, 0 disarms them; out (nullable, 11 uint64) receives
  * their sums since arming: shader-clock cycles of the buffer load, the first halves, the second halves (with the

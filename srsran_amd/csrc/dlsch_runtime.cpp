@@ -112,16 +112,18 @@ struct mi355_dlsch {
   // a workgroup per code block, every half-iteration and check in one launch); -1: MI355_DLSCH_LAT_CBS or the default
 };
 
-// the latency path's limit (process-wide): one subframe's code blocks up to a few subframes (srsUE's per-TTI calls);
-// the throughput kernel wins once a batch fills the chip with waves of 8 code blocks.  MI355_DLSCH_LAT_CBS or 0 (off until
-// it beats the throughput path on one subframe).
+// the latency path's limit (process-wide): calls with up to 256 code blocks (srsUE's per-TTI calls carry 1-32; one
+// code block per CU, so 256 fill the chip once) decode on tdec_win_lat.  Measured crossover (profiles/r04/
+// lat_path_crossover.jsonl, host time per call): the latency path is faster from 16 to 384 code blocks (263 vs 494 us
+// at 16, 765 vs 979 at 256); batch workloads of thousands stay on the throughput kernel.  MI355_DLSCH_LAT_CBS overrides
+// (0: off).
 static std::atomic<int> g_lat_cbs{-1};
 static uint64_t*        g_lat_prof = nullptr; // device counters of tdec_win_lat's phases (mi355_dlsch_latency_profile)
 static int lat_cbs_now()
 {
   int v = g_lat_cbs.load();
   if (v < 0) {
-    v = getenv("MI355_DLSCH_LAT_CBS") ? atoi(getenv("MI355_DLSCH_LAT_CBS")) : 0;
+    v = getenv("MI355_DLSCH_LAT_CBS") ? atoi(getenv("MI355_DLSCH_LAT_CBS")) : 256;
     g_lat_cbs.store(v);
   }
   return v;

@@ -208,6 +208,10 @@ template <bool BETA, int PH> __device__ __forceinline__ v2s dstep(v2s st, v2s x,
 // turbodecoder_win.h:480-498 (16-bit: subtract state 0; state 0 itself becomes 0)
 __device__ __forceinline__ v2s dnorm(v2s st) { return ssub2(st, bcast0(st)); }
 
+#ifndef LAT_DIAG
+#define LAT_DIAG 0 // (timing diagnostics, wrong results: 1 no output computation, 2 no output passes)
+#endif
+
 template <int P> struct Par {
   static constexpr int value = P;
 };
@@ -228,7 +232,7 @@ template <int B, int E, typename F> __device__ __forceinline__ void sfor(F&& f)
 size_t tdec_lat_lds(int K, int nsb)
 {
   const int L = K / nsb, NL = nsb / 2;
-  return (size_t)K / 2 * 4 * 4 + (size_t)L * NL * 8 * 4 + 2 * 64 * 8 * 4 + 256 * 4 + (size_t)(K + 31) / 32 * 4;
+  return (size_t)K / 2 * 4 * 4 + (size_t)L * NL * 8 * 4 + 4 * 64 * 8 * 4 + 256 * 4 + (size_t)(K + 31) / 32 * 4;
 }
 
 template <int NSB>
@@ -252,8 +256,8 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
   uint32_t* ev   = a1 + K / 2;
   uint32_t* am   = ev + K / 2;                    // [H][NL][8] alpha entering states of steps 0 .. H-1
   uint32_t* bm   = am + (size_t)H * NL * 8;       // [L-H][NL][8] beta rows k+1 of steps H .. L-1
-  uint32_t* sgb  = bm + (size_t)(L - H) * NL * 8; // [2][PB][NL][8] per-wave output staging
-  uint32_t* tl   = sgb + 2 * 64 * 8;              // CRC byte table
+  uint32_t* sgb  = bm + (size_t)(L - H) * NL * 8; // [2 waves][2][PB][NL][8] double-buffered output staging
+  uint32_t* tl   = sgb + 4 * 64 * 8;              // CRC byte table
   uint32_t* bits = tl + 256;                      // K/8 decision bytes
   __shared__ int16_t  tail[12];
   __shared__ uint32_t fin_s;
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
   v2s         st   = spl(0);      // this lane's state
   int         ka = 0, pha = 0;    // alpha: next step and its phase
   int         kb = 0, phb = 0;    // beta: next row and the phase of the step computing it
-  uint32_t*  sg    = sgb + (alpha ? 0 : 64 * 8);
+  uint32_t*  sg    = sgb + (alpha ? 0 : 2 * 64 * 8);
   __shared__ uint32_t simd_s[4]; // (measurement) the SIMD each wave runs on
   if (A.prof && lane == 0) simd_s[wv] = (__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4) & 3u) + 1u;
   // A.prof (measurement): shader-clock cycles of each phase, taken by lane 0 after the barriers that end them
@@ -339,24 +343,6 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
         dbit(bits, 2 * pp * L + k, out.x > 0);
         dbit(bits, (2 * pp + 1) * L + k, out.y > 0);
       }
-    };
-    // one output pass: lane (i_p, lp) outputs step k (valid when ok) from the alpha entering state at as and the
-    // beta row at bs (turbodecoder_win.h:771-832); e its destination word, loaded before the recursion steps
-    auto opass = [&](bool ok, int k, const uint32_t* as, const uint32_t* bs, uint32_t e) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (ok) {
-        const int ix = k * NL + lp;
-        v2s       x, y, ap, a8[8], row[8];
-        xin(X[ix], pc[ix], a1[ix], x, y, ap);
-        ld8(as, a8);
-        ld8(bs, row);
-        put(k, lp, e, x, ap, out_llr(a8, x, y, row, false));
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     // this lane's inputs of step k (pair p, the same in the group's 8 lanes)
     auto inp = [&](int k, v2s& x, v2s& y) {
@@ -528,21 +514,67 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
     __syncthreads();
     mark(1);
     // ------------------------------------------------ second parts: PB recursion steps, then their outputs
+    // The pass of chunk c reads its operands before chunk c+1's recursion steps and computes after them, so the LDS
+    // latency of those reads is hidden (staging double-buffered).
+    struct PassIn {
+      uint32_t xw, yw, aw, e;
+      v2s      a8[8], row[8];
+    };
+    auto pass_load = [&](bool ok, int k, const uint32_t* as, const uint32_t* bs, uint32_t e, PassIn& P) {
+      if (LAT_DIAG & 2) return;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (ok) {
+        const int ix = k * NL + lp;
+        P.xw = X[ix], P.yw = pc[ix], P.aw = a1[ix], P.e = e;
+        ld8(as, P.a8);
+        ld8(bs, P.row);
+      }
+    };
+    auto pass_do = [&](bool ok, int k, PassIn& P) {
+      if (LAT_DIAG & 3) return;
+      if (ok) {
+        v2s x, y, ap;
+        xin(P.xw, P.yw, P.aw, x, y, ap);
+        put(k, lp, P.e, x, ap, out_llr(P.a8, x, y, P.row, false));
+      }
+    };
     if (alpha) {
-      for (int k0 = H; k0 < L; k0 += PB) { // steps k0 .. k0+n-1, with beta rows from the first part
+      PassIn P{};
+      bool   okp = false;
+      int    kp  = 0;
+      for (int k0 = H, c = 0; k0 < L; k0 += PB, c++) { // steps k0 .. k0+n-1, with beta rows from the first part
         const int      n = min(PB, L - k0), k = k0 + i_p;
         const bool     ok = i_p < n;
         const uint32_t e  = ok ? tbg[k * NL + lp] : 0u;
-        if (rec) a_run(ka, n, pha, sg, -k0 * RS, RS);
-        opass(ok, k, sg + (size_t)lane * 8, bm + ((size_t)(k - H) * NL + lp) * 8, e);
+        uint32_t*      sc = sg + (c & 1) * 64 * 8;
+        if (c > 0) pass_load(okp, kp, sg + ((c - 1) & 1) * 64 * 8 + (size_t)lane * 8, bm + ((size_t)(kp - H) * NL + lp) * 8, P.e, P);
+        if (rec) a_run(ka, n, pha, sc, -k0 * RS, RS);
+        if (c > 0) pass_do(okp, kp, P);
+        okp = ok, kp = k, P.e = e;
+        if (k0 + PB >= L) { // the last chunk's pass
+          pass_load(ok, k, sc + (size_t)lane * 8, bm + ((size_t)(k - H) * NL + lp) * 8, e, P);
+          pass_do(ok, k, P);
+        }
       }
     } else if (wv == bw) {
-      for (int k0 = H; k0 >= 1; k0 -= PB) { // rows k0 .. k0-n+1 = beta rows of steps k0-1 .. k0-n
+      PassIn P{};
+      bool   okp = false;
+      int    kp  = 0;
+      for (int k0 = H, c = 0; k0 >= 1; k0 -= PB, c++) { // rows k0 .. k0-n+1 = beta rows of steps k0-1 .. k0-n
         const int      n = min(PB, k0), k = k0 - 1 - i_p;
         const bool     ok = i_p < n;
         const uint32_t e  = ok ? tbg[k * NL + lp] : 0u;
-        if (rec) b_run(kb, n, phb, sg, k0 * RS, -RS);
-        opass(ok, k, am + ((size_t)k * NL + lp) * 8, sg + (size_t)lane * 8, e);
+        uint32_t*      sc = sg + (c & 1) * 64 * 8;
+        if (c > 0) pass_load(okp, kp, am + ((size_t)kp * NL + lp) * 8, sg + ((c - 1) & 1) * 64 * 8 + (size_t)lane * 8, P.e, P);
+        if (rec) b_run(kb, n, phb, sc, k0 * RS, -RS);
+        if (c > 0) pass_do(okp, kp, P);
+        okp = ok, kp = k, P.e = e;
+        if (k0 - PB < 1) {
+          pass_load(ok, k, am + ((size_t)k * NL + lp) * 8, sc + (size_t)lane * 8, e, P);
+          pass_do(ok, k, P);
+        }
       }
     }
     __syncthreads();

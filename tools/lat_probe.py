@@ -19,6 +19,28 @@ from srsran_amd.dlsch import Dlsch, SoftbufferPool  # noqa: E402
 NAMES = ["load", "first_halves", "second_halves", "decisions", "check", "simd_alpha", "simd_beta", "same_simd", "-", "half_its", "cbs"]
 rng = np.random.default_rng(1)
 QUICK = os.environ.get("LAT_PROBE_QUICK") == "1"  # the 30 dB latency case only
+if os.environ.get("LAT_PROBE_SWEEP") == "1":  # crossover: host time per call of both paths vs transport blocks per call
+    for snr in (30.0, 9.0):
+        base = [oracle.make_tb(rng, 97896, 8, 115200, 0, snr)[1] for _ in range(2)]
+        for ntb in (1, 2, 4, 8, 12, 16, 24):
+            llrs = [base[i % 2] for i in range(ntb)]
+            tbs = [dict(tbs=97896, Qm=8, rv=0, softbuffer=i) for i in range(ntb)]
+            res = {"snr": snr, "tbs": ntb, "cbs": 16 * ntb}
+            for path in ("throughput", "latency"):
+                lib().mi355_dlsch_set_latency_path(100000 if path == "latency" else 0)
+                dl = Dlsch(0, 10)
+                pool = SoftbufferPool(ntb, 32)
+                pool.reset_all()
+                dl.decode(pool, tbs, llrs)
+                n = 10
+                t0 = time.perf_counter()
+                for _ in range(n):
+                    pool.reset_all()  # (a decoded softbuffer is skipped by the next call)
+                    got = dl.decode(pool, tbs, llrs)
+                res[path + "_us"] = round((time.perf_counter() - t0) / n * 1e6, 1)
+                res[path + "_ok"] = sum(1 for r in got[0] if r == 0)
+            print(json.dumps(res), flush=True)
+    sys.exit(0)
 for snr in ((30.0,) if QUICK else (9.0, 5.5, 30.0)):
     cases = [(97896, 8, 115200, snr)] * 2
     llrs = [oracle.make_tb(rng, t, q, g, 0, s)[1] for (t, q, g, s) in cases]
