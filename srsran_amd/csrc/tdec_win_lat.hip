@@ -177,7 +177,13 @@ __device__ __forceinline__ Lane8 lane8(uint32_t q, bool beta)
   return c;
 }
 
-// the value of lane q ^ D within each group of 8 (DPP: quad permutes; 4 apart by row shifts under bank masks)
+// Lane labels: group lane g (0..7) carries logical lane q = M(g), M(g) = g ^ (g & 4 ? 3 : 0) (lanes 4-7 reversed),
+// a linear involution of GF(2)^3 mapping the partner distances 1, 2, 4 of the logical lanes to g ^ 1, g ^ 2 and
+// g ^ 7: every exchange is one DPP (quad permutes, and row_half_mirror for the distance 4).  Logical lane 0 is group
+// lane 0.
+__device__ __forceinline__ uint32_t lane_logical(uint32_t g) { return g ^ ((g & 4u) ? 3u : 0u); }
+
+// the value of logical lane q ^ D within each group of 8
 template <int D> __device__ __forceinline__ v2s partner(v2s v)
 {
   const int w = (int)W2(v);
@@ -186,15 +192,19 @@ template <int D> __device__ __forceinline__ v2s partner(v2s v)
   } else if constexpr (D == 2) {
     return U2((uint32_t)__builtin_amdgcn_mov_dpp(w, 0x4E, 0xF, 0xF, false)); // quad_perm [2,3,0,1]
   } else {
-    const int r = __builtin_amdgcn_update_dpp(w, w, 0x114, 0xF, 0xA, false); // row_shr:4 into lanes 4-7 of each 8
-    return U2((uint32_t)__builtin_amdgcn_update_dpp(r, w, 0x104, 0xF, 0x5, false)); // row_shl:4 into lanes 0-3
+    return U2((uint32_t)__builtin_amdgcn_mov_dpp(w, 0x141, 0xF, 0xF, false)); // row_half_mirror: g ^ 7
   }
 }
-// state 0's value (lane q = 0 of the group) in every lane of the group
-__device__ __forceinline__ v2s bcast0(v2s v)
+// the value of group lane G in every lane of its group of 8 (quad broadcast, then the other quad by a row shift)
+template <int G> __device__ __forceinline__ v2s bcast(v2s v)
 {
-  const int b = __builtin_amdgcn_mov_dpp((int)W2(v), 0x00, 0xF, 0xF, false); // quad_perm [0,0,0,0]
-  return U2((uint32_t)__builtin_amdgcn_update_dpp(b, b, 0x114, 0xF, 0xA, false));
+  constexpr int qp = (G & 3) * 0x55; // quad_perm [G&3, G&3, G&3, G&3]
+  const int     b  = __builtin_amdgcn_mov_dpp((int)W2(v), qp, 0xF, 0xF, false);
+  if constexpr (G < 4) {
+    return U2((uint32_t)__builtin_amdgcn_update_dpp(b, b, 0x114, 0xF, 0xA, false)); // row_shr:4 into lanes 4-7
+  } else {
+    return U2((uint32_t)__builtin_amdgcn_update_dpp(b, b, 0x104, 0xF, 0x5, false)); // row_shl:4 into lanes 0-3
+  }
 }
 // one trellis step at phase PH (saturating, turbodecoder_win.h:640-676 beta, :771-800 alpha)
 template <bool BETA, int PH> __device__ __forceinline__ v2s dstep(v2s st, v2s x, v2s y, const Lane8& c)
@@ -205,8 +215,15 @@ template <bool BETA, int PH> __device__ __forceinline__ v2s dstep(v2s st, v2s x,
   const v2s     gp = sadd2(U2(W2(x) & c.mxp[PH]), U2(W2(y) & c.myp[PH]));
   return vmax2(sadd2(st, go), sadd2(pr, gp));
 }
-// turbodecoder_win.h:480-498 (16-bit: subtract state 0; state 0 itself becomes 0)
-__device__ __forceinline__ v2s dnorm(v2s st) { return ssub2(st, bcast0(st)); }
+// the step followed by turbodecoder_win.h:480-498's normalisation (16-bit: subtract the new state 0, held by logical
+// lane 0 = group lane 0 at every phase).  (Evaluating the new state 0 from the old states beside the step instead --
+// max(old state 0, sat(old state of logical lane D + sat(x + y))), bit for bit lane 0's value -- takes the two
+// broadcasts off the recursion's dependency chain but adds four DPP moves per normalised step: measured slower, r04aa.)
+template <bool BETA, int PH> __device__ __forceinline__ v2s dstep_n(v2s st, v2s x, v2s y, const Lane8& c)
+{
+  const v2s n = dstep<BETA, PH>(st, x, y, c);
+  return ssub2(n, bcast<0>(n));
+}
 
 #ifndef LAT_DIAG
 #define LAT_DIAG 0 // (timing diagnostics, wrong results: 1 no output computation, 2 no output passes)
@@ -292,7 +309,8 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
   // wave 0 runs alpha, wave 1 (bw) beta: the two recursions at the same time on different SIMDs; in a recursion lane
   // (p, q) = (lane / 8, lane % 8) holds one state of window pair p (distributed trellis), and in an output pass lane
   // (i_p, lp) = (lane / NL, lane % NL) takes step i_p of the pass for pair lp
-  const int  wv = t >> 6, lane = t & 63, p = lane >> 3, q = lane & 7, i_p = lane / NL, lp = lane % NL;
+  const int  wv = t >> 6, lane = t & 63, p = lane >> 3, q = (int)lane_logical(lane & 7), i_p = lane / NL,
+             lp = lane % NL;
   const bool alpha = wv == 0, rec = lane < 8 * NL && (alpha || wv == bw);
   const Lane8 cl = lane8((uint32_t)q, !alpha);
   v2s         st   = spl(0);      // this lane's state
@@ -373,17 +391,16 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
       v2s           x, y;
       inp(k, x, y);
       S[base + k * rs + p * 8 + (int)cl.held[ph]] = W2(st);
-      st = dstep<false, ph>(st, x, y, cl);
-      if (nrm) st = dnorm(st);
+      st = nrm ? dstep_n<false, ph>(st, x, y, cl) : dstep<false, ph>(st, x, y, cl);
     };
     // beta row k from row k+1 at phase PH (the row stored before its normalisation, at the phase after the step)
     auto b_one = [&](auto PH, int k, bool nrm, uint32_t* S, int base, int rs) {
       constexpr int ph = decltype(PH)::value;
       v2s           x, y;
       inp(k, x, y);
-      st = dstep<true, ph>(st, x, y, cl);
-      S[base + k * rs + p * 8 + (int)cl.held[(ph + 1) % 3]] = W2(st);
-      if (nrm) st = dnorm(st);
+      const v2s n = dstep<true, ph>(st, x, y, cl);
+      S[base + k * rs + p * 8 + (int)cl.held[(ph + 1) % 3]] = W2(n); // (before the normalisation)
+      st = nrm ? dstep_n<true, ph>(st, x, y, cl) : n;
     };
     // 8 steps from k with the phase P0 and the parity Q0 of k template constants (normalisations placed at compile
     // time; k >= 1)
@@ -394,8 +411,11 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
       sfor<0, 8>([&](auto I) {
         constexpr int i = decltype(I)::value, ph = (P + i) % 3;
         S[base + (k + i) * rs + p * 8 + (int)cl.held[ph]] = W2(st);
-        st = dstep<false, ph>(st, xv[i], yv[i], cl);
-        if constexpr (((Q + i) & 1) == 0) st = dnorm(st);
+        if constexpr (((Q + i) & 1) == 0) {
+          st = dstep_n<false, ph>(st, xv[i], yv[i], cl);
+        } else {
+          st = dstep<false, ph>(st, xv[i], yv[i], cl);
+        }
       });
     };
     auto b_blk = [&](auto P0, auto Q0, int k, uint32_t* S, int base, int rs) {
@@ -404,9 +424,13 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
       load8(k, -1, xv, yv);
       sfor<0, 8>([&](auto I) {
         constexpr int i = decltype(I)::value, ph = (P + i) % 3;
-        st = dstep<true, ph>(st, xv[i], yv[i], cl);
-        S[base + (k - i) * rs + p * 8 + (int)cl.held[(ph + 1) % 3]] = W2(st);
-        if constexpr (((Q + i) & 1) == 0) st = dnorm(st);
+        const v2s n = dstep<true, ph>(st, xv[i], yv[i], cl);
+        S[base + (k - i) * rs + p * 8 + (int)cl.held[(ph + 1) % 3]] = W2(n); // (before the normalisation)
+        if constexpr (((Q + i) & 1) == 0) {
+          st = dstep_n<true, ph>(st, xv[i], yv[i], cl);
+        } else {
+          st = n;
+        }
       });
     };
     // n alpha steps from k (k >= 1) / n beta rows from k down (rows >= 1) at phase ph: blocks of 8 dispatched on
@@ -466,8 +490,11 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
             constexpr int i = decltype(I)::value, j = 8 * b + i;
             v2s           x, y;
             B.odd_xy(o[i], x, y);
-            st = dstep<false, j % 3>(st, x, y, cl);
-            if constexpr ((j & 1) == 0 && j != 0) st = dnorm(st);
+            if constexpr ((j & 1) == 0 && j != 0) {
+              st = dstep_n<false, j % 3>(st, x, y, cl);
+            } else {
+              st = dstep<false, j % 3>(st, x, y, cl);
+            }
           });
         });
         if (p == 0) st.x = q == 0 ? (short)0 : (short)-TDEC_INF;
@@ -487,8 +514,11 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
             constexpr int i = 7 - decltype(I)::value, k = 8 * b + i, j = TDEC_WARMUP - 1 - k;
             v2s           x, y;
             B.odd_xy(o[i], x, y);
-            st = dstep<true, j % 3>(st, x, y, cl);
-            if constexpr ((k & 1) == 0 && k != 0) st = dnorm(st);
+            if constexpr ((k & 1) == 0 && k != 0) {
+              st = dstep_n<true, j % 3>(st, x, y, cl);
+            } else {
+              st = dstep<true, j % 3>(st, x, y, cl);
+            }
           });
         });
         if (p == NL - 1) {

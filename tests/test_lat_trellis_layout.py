@@ -88,18 +88,60 @@ def test_distributed_step_equals_register_step(beta):
             assert lanes == [s[held(q, k1, beta)] for q in range(8)], (trial, step)
 
 
+def lane_logical(gl):  # tdec_win_lat.hip lane_logical: group lane -> logical lane
+    return gl ^ (3 if gl & 4 else 0)
+
+
+def dstep_n_phys(phys, k, beta, x, y):
+    """The kernel's dstep_n on group lanes: partner by group-lane xor (1, 2, 7), the new state 0 from the old states
+    of logical lanes 0 and D (group lanes 0 and 1 / 2 / 7), subtracted."""
+    d = (4 >> k) if beta else (1 << k)
+    gd = 7 if d == 4 else d
+    s0 = max(phys[0], sadd(phys[gd], sadd(x, y)))
+    out = []
+    for gl in range(8):
+        s = held(lane_logical(gl), k, beta)
+        go = (s & 3) if beta else (s >> 1)
+        new = max(sadd(phys[gl], g(go, x, y)), sadd(phys[gl ^ gd], g(3 - go, x, y)))
+        out.append(sat(new - s0))
+    return out
+
+
+@pytest.mark.parametrize("beta", [False, True], ids=["alpha", "beta"])
+def test_group_lane_relabelling_and_early_normalisation(beta):
+    # M is a linear involution with M(0) = 0 mapping the logical partner distances 1, 2, 4 to group-lane xors 1, 2, 7
+    for a in range(8):
+        assert lane_logical(lane_logical(a)) == a
+        for b in range(8):
+            assert lane_logical(a ^ b) == lane_logical(a) ^ lane_logical(b)
+    assert lane_logical(0) == 0 and [lane_logical(d) for d in (1, 2, 4)] == [1, 2, 7]
+    rng = np.random.default_rng(11 + beta)
+    for trial in range(300):
+        s = [int(v) for v in rng.integers(-4000, 4000, 8)]
+        k0 = int(rng.integers(0, 3))
+        phys = [s[held(lane_logical(gl), k0, beta)] for gl in range(8)]
+        for step in range(9):
+            k = (k0 + step) % 3
+            lim = 32767 if trial % 2 else 300
+            x, y = (int(v) for v in rng.integers(-lim, lim + 1, 2))
+            s = snorm((bstep if beta else astep)(s, x, y))
+            phys = dstep_n_phys(phys, k, beta, x, y)
+            k1 = (k + 1) % 3
+            assert phys == [s[held(lane_logical(gl), k1, beta)] for gl in range(8)], (trial, step)
+
+
 def test_partner_exchanges_are_involutions_within_groups():
-    # the DPP patterns of partner<D>: quad_perm [1,0,3,2] (D = 1), [2,3,0,1] (D = 2), row_shr:4 into lanes 4-7 and
-    # row_shl:4 into lanes 0-3 of every 8 (D = 4) -- lane q of a group of 8 reads lane q ^ D of the same group
+    # the DPP patterns of partner<D>: quad_perm [1,0,3,2] (D = 1), [2,3,0,1] (D = 2), row_half_mirror (D = 4: group
+    # lane g reads 7 - g) -- a lane reads group lane g ^ (1, 2, 7) of its own group of 8
     def perm(d, lane):
-        q, base = lane & 7, lane & ~7
+        g = lane & 7
         if d == 1:
             return (lane & ~3) | [1, 0, 3, 2][lane & 3]
         if d == 2:
             return (lane & ~3) | [2, 3, 0, 1][lane & 3]
-        return lane - 4 if q >= 4 else lane + 4
+        return (lane & ~7) | (7 - g)
 
-    for d in (1, 2, 4):
+    for d, x in ((1, 1), (2, 2), (4, 7)):
         for lane in range(64):
-            assert perm(d, lane) == (lane ^ d)
+            assert perm(d, lane) == (lane ^ x)
             assert perm(d, lane) >> 3 == lane >> 3
