@@ -115,7 +115,8 @@ struct DlschTbArgs {
 struct DlschResetArgs {
   uint8_t* fresh;
   uint8_t* sb_crc;
-  size_t   slot0, ncb;
+  size_t   slot0, ncb; // fresh flags of code blocks [slot0, slot0 + ncb) set
+  size_t   ncrc;       // CB-CRC flags of [slot0, slot0 + ncrc) cleared (0: ncb)
 };
 
 hipError_t dlsch_launch_rm(const DlschRmArgs& a, hipStream_t s);

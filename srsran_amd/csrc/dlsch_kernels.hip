@@ -326,9 +326,8 @@ __global__ __launch_bounds__(256) void dlsch_tb_epilogue(DlschTbArgs a)
 __global__ __launch_bounds__(256) void dlsch_sb_reset(DlschResetArgs a)
 {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= a.ncb) return;
-  a.fresh[a.slot0 + g]  = 1;
-  a.sb_crc[a.slot0 + g] = 0;
+  if (g < a.ncb) a.fresh[a.slot0 + g] = 1;
+  if (g < (a.ncrc ? a.ncrc : a.ncb)) a.sb_crc[a.slot0 + g] = 0;
 }
 
 // one thread per (list entry, code block): lazy buffer reset for the TB's code blocks, every CB CRC flag cleared
@@ -454,8 +453,9 @@ hipError_t dlsch_launch_epilogue(const DlschTbArgs& a, hipStream_t s)
 
 hipError_t dlsch_launch_reset(const DlschResetArgs& a, hipStream_t s)
 {
-  if (!a.ncb) return hipSuccess;
-  hipLaunchKernelGGL(dlsch_sb_reset, dim3((unsigned)((a.ncb + 255) / 256)), dim3(256), 0, s, a);
+  const size_t n = a.ncb > a.ncrc ? a.ncb : a.ncrc;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(dlsch_sb_reset, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -372,11 +372,8 @@ int mi355_softbuffer_reset_cb(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t 
   CHECK_HIP(hipSetDevice(p->device));
   hipStream_t    s  = (hipStream_t)stream;
   const uint32_t nc = std::min(nof_cb, p->max_cb);
-  if (nc) {
-    DlschResetArgs a{p->fresh, p->cb_crc, (size_t)sb * p->max_cb, nc};
-    CHECK_HIP(dlsch_launch_reset(a, s));
-  }
-  CHECK_HIP(hipMemsetAsync(p->cb_crc + (size_t)sb * p->max_cb, 0, p->max_cb, s));
+  DlschResetArgs a{p->fresh, p->cb_crc, (size_t)sb * p->max_cb, nc, p->max_cb}; // one launch for both
+  CHECK_HIP(dlsch_launch_reset(a, s));
   return MI355_SUCCESS;
 }
 
@@ -438,7 +435,7 @@ int mi355_softbuffer_reset_range(mi355_softbuffer_pool_t* p, uint32_t first, uin
   if (!p || first + n > p->nof_sb) return MI355_ERROR_INVALID_INPUTS;
   if (!n) return MI355_SUCCESS;
   CHECK_HIP(hipSetDevice(p->device));
-  DlschResetArgs a{p->fresh, p->cb_crc, (size_t)first * p->max_cb, (size_t)n * p->max_cb};
+  DlschResetArgs a{p->fresh, p->cb_crc, (size_t)first * p->max_cb, (size_t)n * p->max_cb, 0};
   CHECK_HIP(dlsch_launch_reset(a, (hipStream_t)stream));
   return MI355_SUCCESS;
 }

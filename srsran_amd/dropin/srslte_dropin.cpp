@@ -19,6 +19,7 @@
 #include <sys/time.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -279,6 +280,10 @@ struct Arena {
   uint32_t                 stride = 0, data_stride = 0, max_cb = 0, nof_sb = 0;
   std::vector<uint32_t>    free_slots;
   hipStream_t              stream = nullptr;
+  // softbuffer resets run on this stream without a host wait; the event, recorded after the latest one, is what a
+  // decode on another stream waits for (on the GPU) before touching the softbuffers
+  hipEvent_t        ev_reset = nullptr;
+  std::atomic<bool> reset_pending{false};
 
   int init_locked()
   {
@@ -297,6 +302,7 @@ struct Arena {
     mi355_softbuffer_pool_data(pool, &data, &data_stride, nullptr);
     (void)hipSetDevice(device);
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return SRSLTE_ERROR;
+    if (hipEventCreateWithFlags(&ev_reset, hipEventDisableTiming) != hipSuccess) return SRSLTE_ERROR;
     for (uint32_t i = nof_sb; i-- > 0;) free_slots.push_back(i);
     return SRSLTE_SUCCESS;
   }
@@ -388,6 +394,8 @@ int pdsch_decode_dev(srslte_pdsch_t* q, PdschState* st, hipStream_t stream, srsl
 {
   Arena& A = arena();
   if (!A.pool) return SRSLTE_ERROR;
+  // softbuffer resets enqueued on the arena stream come first (a GPU-side wait, no host round trip)
+  if (A.reset_pending.load() && hipStreamWaitEvent(stream, A.ev_reset, 0) != hipSuccess) return SRSLTE_ERROR;
   mi355_pdsch_job_t job{};
   job.sf.tti = sf->tti;
   job.sf.cfi = sf->cfi;
@@ -659,8 +667,12 @@ void srslte_softbuffer_rx_reset_cb(srslte_softbuffer_rx_t* q, uint32_t nof_cb)
   Arena& A    = arena();
   const int s = A.slot_of(q);
   if (s < 0) return;
-  mi355_softbuffer_reset_cb(A.pool, (uint32_t)s, std::min(nof_cb, q->max_cb), A.stream);
-  (void)hipStreamSynchronize(A.stream);
+  {
+    std::lock_guard<std::mutex> lk(A.mu); // (the event is re-recorded after every reset)
+    mi355_softbuffer_reset_cb(A.pool, (uint32_t)s, std::min(nof_cb, q->max_cb), A.stream);
+    (void)hipEventRecord(A.ev_reset, A.stream);
+    A.reset_pending.store(true);
+  }
   memset(q->cb_crc, 0, q->max_cb * sizeof(bool));
   q->tb_crc = false;
 }
