@@ -619,7 +619,7 @@ def map_probe(rx, ncb, local, K=6144):
     old = lib().mi355_tdec_set_diag(20)
     d_junk = DeviceBuffer(ncb * (K // 8), local)  # the clone's decisions are meaningless: kept out of d_out
     for _ in range(2):
-        dec.run_dev(d_in.ptr, stride, ncb, K, nh, d_junk.ptr)
+        dec.run_dev(ptr, stride, ncb, K, 8, d_junk.ptr)
     cms, cl = dec.kernel_stats()
     lib().mi355_tdec_set_diag(old)
     d_junk.free()

@@ -118,7 +118,11 @@ struct mi355_dlsch {
 // at 16, 765 vs 979 at 256); batch workloads of thousands stay on the throughput kernel.  MI355_DLSCH_LAT_CBS overrides
 // (0: off).
 static std::atomic<int> g_lat_cbs{-1};
-static uint64_t*        g_lat_prof = nullptr; // device counters of tdec_win_lat's phases (mi355_dlsch_latency_profile)
+// device counters of tdec_win_lat's phases (mi355_dlsch_latency_profile): allocated once and never freed, so a decode on
+// another thread that snapshotted the pointer before a disarm still writes valid memory; armed = the pointer published
+static std::atomic<uint64_t*> g_lat_prof{nullptr};
+static uint64_t*              g_lat_prof_mem = nullptr;
+static std::mutex             g_lat_prof_mu;
 static int lat_cbs_now()
 {
   int v = g_lat_cbs.load();
@@ -133,17 +137,17 @@ static int lat_cbs_now()
 // since arming (include/srsran_amd/dlsch.h)
 extern "C" int mi355_dlsch_latency_profile(int enable, uint64_t* out)
 {
-  if (out && g_lat_prof) {
+  std::lock_guard<std::mutex> lk(g_lat_prof_mu);
+  if (out && g_lat_prof.load()) {
     if (hipDeviceSynchronize() != hipSuccess) return MI355_ERROR;
-    if (hipMemcpy(out, g_lat_prof, 11 * 8, hipMemcpyDeviceToHost) != hipSuccess) return MI355_ERROR;
+    if (hipMemcpy(out, g_lat_prof_mem, 11 * 8, hipMemcpyDeviceToHost) != hipSuccess) return MI355_ERROR;
   }
   if (enable) {
-    if (!g_lat_prof && hipMalloc(&g_lat_prof, 11 * 8) != hipSuccess) return MI355_ERROR;
-    if (hipMemset(g_lat_prof, 0, 11 * 8) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return MI355_ERROR;
-  } else if (g_lat_prof) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(g_lat_prof);
-    g_lat_prof = nullptr;
+    if (!g_lat_prof_mem && hipMalloc(&g_lat_prof_mem, 11 * 8) != hipSuccess) return MI355_ERROR;
+    if (hipMemset(g_lat_prof_mem, 0, 11 * 8) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return MI355_ERROR;
+    g_lat_prof.store(g_lat_prof_mem);
+  } else {
+    g_lat_prof.store(nullptr);
   }
   return MI355_SUCCESS;
 }
@@ -884,7 +888,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
       la.done    = d_done + lv.off;
       la.chk     = DlschCheckArgs{d_cb + lv.off, (int)lv.n, lv.K, 0, q->max_its, lv.dec, lv.K / 8, d_data, d_done + lv.off,
                               d_run, d_run + 1, d_its + lv.off, pool->cb_crc, &q->crc[0], &q->crc[1], lv.scale};
-      la.prof    = g_lat_prof;
+      la.prof    = g_lat_prof.load();
       la.ncb     = (int)lv.n;
       la.K       = (int)lv.K;
       la.rowmask = nsb == 16 && !no_rowmask();

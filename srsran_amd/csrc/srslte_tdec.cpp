@@ -17,6 +17,8 @@ struct CompatState {
   size_t              stride;
   mi355_tdec8_t*      dec8 = nullptr; // 8-bit decoder, created on first use
   int8_t*             din8 = nullptr;
+  hipStream_t         s    = nullptr; // this object's stream: a call waits on it alone, never on the device, so
+                                      // concurrent PHY workers (one srslte_tdec_t each) do not stall each other
 };
 
 int cb_index(uint32_t K)
@@ -47,10 +49,12 @@ int mi355_srslte_tdec_init_manual(mi355_srslte_tdec_t* h, uint32_t max_long_cb, 
   }
   auto* st   = new CompatState;
   st->stride = 3 * (size_t)(max_long_cb + 32) + 12;
-  if (mi355_tdec_batch_create(&st->dec, current_device()) != MI355_SUCCESS ||
+  if (hipStreamCreateWithFlags(&st->s, hipStreamNonBlocking) != hipSuccess ||
+      mi355_tdec_batch_create(&st->dec, current_device()) != MI355_SUCCESS ||
       hipMalloc(&st->din, st->stride * sizeof(int16_t)) != hipSuccess ||
       hipMalloc(&st->dout, max_long_cb / 8 + 8) != hipSuccess) {
     if (st->dec) mi355_tdec_batch_destroy(st->dec);
+    if (st->s) (void)hipStreamDestroy(st->s);
     delete st;
     return MI355_ERROR;
   }
@@ -76,6 +80,7 @@ void mi355_srslte_tdec_free(mi355_srslte_tdec_t* h)
   (void)hipFree(st->din);
   (void)hipFree(st->dout);
   if (st->din8) (void)hipFree(st->din8);
+  (void)hipStreamDestroy(st->s);
   delete st;
   memset(h, 0, sizeof(*h));
 }
@@ -122,13 +127,15 @@ void mi355_srslte_tdec_iteration(mi355_srslte_tdec_t* h, int16_t* input, uint8_t
   const uint32_t K   = h->current_long_cb;
   const bool     lin = h->dec_type == MI355_TDEC_GENERIC || mi355_tdec_autoimp_get_subblocks(K) == 0;
   const size_t   len = lin ? 3 * (size_t)K + 12 : 3 * (size_t)(K + 32) + 12;
-  if (hipMemcpy(st->din, input, len * sizeof(int16_t), hipMemcpyHostToDevice) != hipSuccess) return;
+  if (hipMemcpyAsync(st->din, input, len * sizeof(int16_t), hipMemcpyHostToDevice, st->s) != hipSuccess) return;
   if (mi355_tdec_batch_halfit_dev(st->dec, st->din, st->stride, 1, K, (uint32_t)h->n_iter, st->dout, K / 8,
-                                  nullptr) != MI355_SUCCESS) {
+                                  st->s) != MI355_SUCCESS) {
     return;
   }
-  (void)hipDeviceSynchronize();
-  if (hipMemcpy(output, st->dout, K / 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  if (hipMemcpyAsync(output, st->dout, K / 8, hipMemcpyDeviceToHost, st->s) != hipSuccess ||
+      hipStreamSynchronize(st->s) != hipSuccess) {
+    return;
+  }
   h->n_iter++;
 }
 
@@ -140,13 +147,17 @@ int mi355_srslte_tdec_run_all(mi355_srslte_tdec_t* h, int16_t* input, uint8_t* o
   const bool   lin = h->dec_type == MI355_TDEC_GENERIC || mi355_tdec_autoimp_get_subblocks(long_cb) == 0;
   const size_t len = lin ? 3 * (size_t)long_cb + 12 : 3 * (size_t)(long_cb + 32) + 12;
   const uint32_t nit = nof_iterations ? nof_iterations : 1; // do { } while (n_iter < nof_iterations)
-  if (hipMemcpy(st->din, input, len * sizeof(int16_t), hipMemcpyHostToDevice) != hipSuccess) return MI355_ERROR;
-  if (mi355_tdec_batch_run_dev(st->dec, st->din, st->stride, 1, long_cb, nit, st->dout, long_cb / 8, nullptr) !=
+  if (hipMemcpyAsync(st->din, input, len * sizeof(int16_t), hipMemcpyHostToDevice, st->s) != hipSuccess) {
+    return MI355_ERROR;
+  }
+  if (mi355_tdec_batch_run_dev(st->dec, st->din, st->stride, 1, long_cb, nit, st->dout, long_cb / 8, st->s) !=
       MI355_SUCCESS) {
     return MI355_ERROR;
   }
-  (void)hipDeviceSynchronize();
-  if (hipMemcpy(output, st->dout, long_cb / 8, hipMemcpyDeviceToHost) != hipSuccess) return MI355_ERROR;
+  if (hipMemcpyAsync(output, st->dout, long_cb / 8, hipMemcpyDeviceToHost, st->s) != hipSuccess ||
+      hipStreamSynchronize(st->s) != hipSuccess) {
+    return MI355_ERROR;
+  }
   h->n_iter = (int)nit;
   return MI355_SUCCESS;
 }
@@ -164,11 +175,15 @@ void mi355_srslte_tdec_iteration_8bit(mi355_srslte_tdec_t* h, int8_t* input, uin
     if (!st->dec8 && mi355_tdec8_create(&st->dec8, current_device()) != MI355_SUCCESS) return;
     if (!st->din8 && hipMalloc(&st->din8, st->stride) != hipSuccess) return;
     const size_t len = 3 * (size_t)(K + 32) + 12;
-    if (h->n_iter == 0 && hipMemcpy(st->din8, input, len, hipMemcpyHostToDevice) != hipSuccess) return;
-    if (mi355_tdec8_halfit_dev(st->dec8, st->din8, st->stride, 1, K, (uint32_t)h->n_iter, st->dout, K / 8, nullptr))
+    if (h->n_iter == 0 && hipMemcpyAsync(st->din8, input, len, hipMemcpyHostToDevice, st->s) != hipSuccess) return;
+    if (mi355_tdec8_halfit_dev(st->dec8, st->din8, st->stride, 1, K, (uint32_t)h->n_iter, st->dout, K / 8, st->s))
       return;
-    if (h->n_iter == 0) (void)hipMemcpy(input, st->din8, len, hipMemcpyDeviceToHost); // tails in the pads, as the reference
-    if (hipMemcpy(output, st->dout, K / 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    // tails in the pads, as the reference
+    if (h->n_iter == 0 && hipMemcpyAsync(input, st->din8, len, hipMemcpyDeviceToHost, st->s) != hipSuccess) return;
+    if (hipMemcpyAsync(output, st->dout, K / 8, hipMemcpyDeviceToHost, st->s) != hipSuccess ||
+        hipStreamSynchronize(st->s) != hipSuccess) {
+      return;
+    }
     h->n_iter++;
   } else if (mi355_tdec_autoimp_get_subblocks(K) == 0) {
     int16_t conv[3 * 400 + 12];

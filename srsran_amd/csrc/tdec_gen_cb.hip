@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "lds_optin.h"
 #include "tdec_internal.h"
 
 namespace mi355 {
@@ -390,12 +391,8 @@ hipError_t tdec_gen_cb_launch(const TdecGenCbArgs& a, hipStream_t s)
   const size_t lds = tdec_gen_cb_lds(a.K, T);
   const bool   full = a.K % TDEC_GEN_CB_L == 0;
   const void*  f    = full ? (const void*)tdec_gen_cb<TDEC_GEN_CB_L, true> : (const void*)tdec_gen_cb<TDEC_GEN_CB_L, false>;
-  static size_t attr[2] = {64 * 1024, 64 * 1024}; // dynamic LDS beyond 64 KB is opted into per size (K = 6144: 90 KB)
-  if (lds > attr[full]) {
-    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr[full] = lds;
-  }
+  // dynamic LDS beyond 64 KB is opted into per size (K = 6144: 90 KB)
+  if (hipError_t e = lds_optin(f, lds); e != hipSuccess) return e;
   if (full) {
     hipLaunchKernelGGL((tdec_gen_cb<TDEC_GEN_CB_L, true>), dim3(a.ncb), dim3(T), lds, s, a);
   } else {

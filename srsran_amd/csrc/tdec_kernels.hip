@@ -26,6 +26,8 @@
 //                  NATURAL position (the reference's app1 -= ext1 of the next DEC1); optionally D = E2
 //                  de-interleaved (= app1, what the reference decides on).
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -839,32 +841,30 @@ __global__ __launch_bounds__(256) void tdec_win_decide(TdecDecideArgs a)
 
 // ---------------------------------------------------------------------------- launchers
 
-static int g_diag = -1; // MI355_TDEC_DIAG, or mi355_tdec_set_diag
+static std::atomic<int> g_diag{-1}; // MI355_TDEC_DIAG, or mi355_tdec_set_diag
 
 static int diag_mode()
 {
-  if (g_diag < 0) {
+  int v = g_diag.load(std::memory_order_relaxed);
+  if (v < 0) {
     const char* e = getenv("MI355_TDEC_DIAG");
-    g_diag        = e ? atoi(e) : 0;
+    v             = e ? atoi(e) : 0;
+    g_diag.store(v, std::memory_order_relaxed);
   }
-  return g_diag;
+  return v;
 }
 
 int tdec_set_diag(int mode)
 {
   const int old = diag_mode();
-  g_diag        = mode < 0 ? 0 : mode;
+  g_diag.store(mode < 0 ? 0 : mode, std::memory_order_relaxed);
   return old;
 }
 
 // MI355_TDEC_LDS (diagnostic): reserve that many bytes of LDS per workgroup, capping the waves per CU
 static size_t diag_lds()
 {
-  static long m = -1;
-  if (m < 0) {
-    const char* e = getenv("MI355_TDEC_LDS");
-    m             = e ? atol(e) : 0;
-  }
+  static const long m = getenv("MI355_TDEC_LDS") ? atol(getenv("MI355_TDEC_LDS")) : 0;
   return (size_t)m;
 }
 
@@ -884,12 +884,8 @@ static void launch_mode_t(int mode, int blocks, const TdecWinArgs& a, hipStream_
 // MI355_TDEC_TX=0 (A/B timing): never take the 16-byte-load path
 static bool tx_enabled()
 {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("MI355_TDEC_TX");
-    m             = e ? atoi(e) != 0 : 1;
-  }
-  return m != 0;
+  static const bool on = !getenv("MI355_TDEC_TX") || atoi(getenv("MI355_TDEC_TX")) != 0;
+  return on;
 }
 
 template <int NSB, int DIAG, bool FULL, int OUTK>

@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "crc_device.h"
+#include "lds_optin.h"
 #include "tdec_internal.h"
 
 namespace mi355 {
@@ -652,14 +653,8 @@ hipError_t tdec_lat_launch(int nsb, const TdecLatArgs& a, hipStream_t s)
 {
   const size_t lds = tdec_lat_lds(a.K, nsb);
   if (lds > 160 * 1024 - 64) return hipErrorInvalidValue;
-  static size_t attr[2] = {64 * 1024, 64 * 1024};
-  const int     ix      = nsb == 16 ? 0 : 1;
-  const void*   f       = nsb == 16 ? (const void*)tdec_win_lat<16> : (const void*)tdec_win_lat<8>;
-  if (lds > attr[ix]) {
-    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    attr[ix] = lds;
-  }
+  const void* f = nsb == 16 ? (const void*)tdec_win_lat<16> : (const void*)tdec_win_lat<8>;
+  if (hipError_t e = lds_optin(f, lds); e != hipSuccess) return e;
   if (nsb == 16) {
     hipLaunchKernelGGL(tdec_win_lat<16>, dim3(a.ncb), dim3(64 * (2 * a.bwave)), lds, s, a);
   } else {

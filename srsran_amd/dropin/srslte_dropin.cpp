@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -282,8 +283,12 @@ struct Arena {
   hipStream_t              stream = nullptr;
   // softbuffer resets run on this stream without a host wait; the event, recorded after the latest one, is what a
   // decode on another stream waits for (on the GPU) before touching the softbuffers
-  hipEvent_t        ev_reset = nullptr;
-  std::atomic<bool> reset_pending{false};
+  // reset_gen counts the records; reset_seen[stream] is the generation a decode stream last waited for, so a stream
+  // waits only when a reset was enqueued since (the latest record covers every earlier reset: one in-order stream).
+  // Both under mu, together with the record and the wait (hipStreamWaitEvent binds the latest record at call time).
+  hipEvent_t                        ev_reset  = nullptr;
+  uint64_t                          reset_gen = 0;
+  std::map<hipStream_t, uint64_t>   reset_seen;
 
   int init_locked()
   {
@@ -320,6 +325,14 @@ Arena& arena()
 {
   static Arena a;
   return a;
+}
+
+// a decode stream about to be destroyed: its handle may be reused by a new stream, which must not inherit the record
+void arena_forget_stream(hipStream_t s)
+{
+  Arena&                      A = arena();
+  std::lock_guard<std::mutex> lk(A.mu);
+  A.reset_seen.erase(s);
 }
 
 // ---------------------------------------------------------------------------------------------------- PDSCH state
@@ -362,7 +375,10 @@ struct PdschState {
     if (own_rx && rx) mi355_pdsch_destroy(rx);
     if (d_stage) (void)hipFree(d_stage);
     if (d_payload) (void)hipFree(d_payload);
-    if (own_stream && stream) (void)hipStreamDestroy(stream);
+    if (own_stream && stream) {
+      arena_forget_stream(stream);
+      (void)hipStreamDestroy(stream);
+    }
   }
 };
 
@@ -395,7 +411,14 @@ int pdsch_decode_dev(srslte_pdsch_t* q, PdschState* st, hipStream_t stream, srsl
   Arena& A = arena();
   if (!A.pool) return SRSLTE_ERROR;
   // softbuffer resets enqueued on the arena stream come first (a GPU-side wait, no host round trip)
-  if (A.reset_pending.load() && hipStreamWaitEvent(stream, A.ev_reset, 0) != hipSuccess) return SRSLTE_ERROR;
+  {
+    std::lock_guard<std::mutex> lk(A.mu);
+    uint64_t& seen = A.reset_seen[stream];
+    if (seen != A.reset_gen) {
+      if (hipStreamWaitEvent(stream, A.ev_reset, 0) != hipSuccess) return SRSLTE_ERROR;
+      seen = A.reset_gen;
+    }
+  }
   mi355_pdsch_job_t job{};
   job.sf.tti = sf->tti;
   job.sf.cfi = sf->cfi;
@@ -499,7 +522,10 @@ struct UeDlState {
   {
     if (ue) mi355_ue_dl_destroy(ue);
     if (d_mem) (void)hipFree(d_mem);
-    if (stream) (void)hipStreamDestroy(stream);
+    if (stream) {
+      arena_forget_stream(stream);
+      (void)hipStreamDestroy(stream);
+    }
   }
 };
 
@@ -671,7 +697,7 @@ void srslte_softbuffer_rx_reset_cb(srslte_softbuffer_rx_t* q, uint32_t nof_cb)
     std::lock_guard<std::mutex> lk(A.mu); // (the event is re-recorded after every reset)
     mi355_softbuffer_reset_cb(A.pool, (uint32_t)s, std::min(nof_cb, q->max_cb), A.stream);
     (void)hipEventRecord(A.ev_reset, A.stream);
-    A.reset_pending.store(true);
+    A.reset_gen++;
   }
   memset(q->cb_crc, 0, q->max_cb * sizeof(bool));
   q->tb_crc = false;

@@ -241,3 +241,71 @@ def test_tti_latency_flow_decodes_every_tti():
     assert L.caller_tti_latency(C.byref(c), iq.ctypes.data, 10, 2, n, us.ctypes.data, ok.ctypes.data) == 0
     assert np.all(ok == 2), ok
     assert np.all(us > 0) and np.all(np.isfinite(us))
+
+
+def test_concurrent_workers_match_single_thread():
+    """srsUE runs up to 3 sf_worker threads, each calling the ue_dl / pdsch API on its own srslte_ue_dl_t at the same
+    time (srsue/src/phy/phy.cc:135-189, sf_worker.cc:182, thread_pool.cc:215-230).  Three host threads, each with its
+    own objects and softbuffers (caller_ue_dl: decode_pdsch, pdsch_decode on host copies, find_and_decode), decode
+    distinct TM4 subframes concurrently while a fourth runs srslte_tdec_run_all on the reference goldens: every
+    outcome and payload equals the single-thread run's.  ctypes releases the GIL around each foreign call, so the
+    drop-in really is entered from several threads at once."""
+    import threading
+    L = _caller()
+    case = CASES[0]
+    name, nprb, ports, nrx, tm, fmt, mcs, alt, cid = case
+    rnti = 0x46
+    groups = [[10 * 3 + 1, 10 * 3 + 4, 10 * 4 + 8], [10 * 5 + 2, 10 * 5 + 5, 10 * 6 + 7], [10 * 6 + 0, 10 * 7 + 6, 10 * 8 + 9]]
+    synth = [_synth(case, g, rnti) for g in groups]
+    c = CallerCfg(nof_prb=nprb, nof_ports=ports, nof_rx=nrx, cell_id=cid, rnti=rnti, tm=tm, use_tbs_index_alt=int(alt),
+                  decoder_type=1, csi_enable=1, max_nof_iterations=10, cfo_estimate_enable=1, estimator_alg=0,
+                  noise_alg=0, sync_error_enable=0)
+    maxb = max(t for _iq, ex in synth for e in ex for t in e[0].tbs) // 8 + 16
+
+    def run(k, out):
+        iq, _ex = synth[k]
+        nsf = iq.shape[0]
+        pay = np.zeros((nsf, 3, 2, maxb), np.uint8)
+        res = (SfRes * nsf)()
+        tt = np.array(groups[k], np.uint32)
+        rc = L.caller_ue_dl(C.byref(c), iq.ctypes.data, tt.ctypes.data, nsf, pay.ctypes.data, maxb, res)
+        out[k] = (rc, pay, [(r.ret_pdsch, r.ret_host, r.ret_fad, tuple(r.crc), tuple(r.crc_host), tuple(r.ack_fad))
+                            for r in res])
+
+    single = {}
+    for k in range(3):
+        run(k, single)
+    auto = tdec_auto_cases()
+    tdec_bad = []
+
+    def tdec_loop():
+        for _ in range(3):
+            for cs in auto:
+                K, trace = cs["K"], cs["trace"]
+                buf = np.ascontiguousarray(cs["buf"].astype(np.int16))
+                out = np.zeros(K // 8, np.uint8)
+                n = C.c_int(0)
+                if L.caller_tdec_run_all(buf.ctypes.data, out.ctypes.data, K, len(trace), 0, C.byref(n)) != 0 or \
+                        not np.array_equal(out, trace[-1]):
+                    tdec_bad.append(K)
+
+    for rep in range(2):
+        conc = {}
+        th = [threading.Thread(target=run, args=(k, conc)) for k in range(3)] + [threading.Thread(target=tdec_loop)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=240)
+        assert not any(t.is_alive() for t in th), "a worker thread hung"
+        assert not tdec_bad, tdec_bad
+        for k in range(3):
+            rc, pay, outc = conc[k]
+            assert rc == 0 and outc == single[k][2], (rep, k, outc, single[k][2])
+            assert np.array_equal(pay, single[k][1]), (rep, k)
+            _iq, ex = synth[k]
+            for i, (cfg, payload, g, m) in enumerate(ex):
+                for t in range(cfg.nof_tb):
+                    nb = cfg.tbs[t] // 8
+                    assert outc[i][3][t] and outc[i][5][t], (rep, k, i, t)
+                    for j in range(3):
+                        assert np.array_equal(pay[i, j, t, :nb], payload[t][:nb]), (rep, k, i, j, t)
