@@ -197,6 +197,17 @@ __device__ __forceinline__ void tdec_fused_check(const TdecWinArgs& a, int cb, i
 
 #define WG_AT(arr, j) (arr)[((size_t)grp * Lp + (j)) * 64 + q]
 
+// The body's LDS buffers, one per wave of the 256-thread workgroup, at file scope: a kernel that instantiates the body
+// twice (the 16-byte-load path and its 4-byte fallback) shares them between the two instead of allocating each twice,
+// which kept the workgroup at 2 per CU (2 waves per SIMD).  SEG 8 rows; bitmaps of 8 code blocks x 193 words (16
+// windows, K <= 6144) or 16 x 25 (8 windows, K <= 800).
+#define TDEC_BM_WORDS (8 * 193)
+__shared__ uint32_t tdec_tx_lds[4][2][TDEC_SEG * 64];         // TX transposition (systematic, parity)
+__shared__ uint32_t tdec_ym_lds[4][8 * SB_ROWMASK_WORDS];     // parity-row bitmaps of the wave's code blocks
+__shared__ uint32_t tdec_bm_lds[4 * TDEC_BM_WORDS];           // decision bytes / bitmaps
+__shared__ int16_t  tdec_stg_lds[4][TDEC_SEG * 128];          // staged output rows (STG)
+__shared__ uint32_t tdec_stg_row[4][TDEC_SEG];                // their destination rows j'
+
 // MODE: 0 = DEC1 without a-priori (n = 0), 1 = DEC1 with a-priori, 2 = DEC2.  A compile-time mode keeps
 // every load unconditional (a runtime "load or zero" select makes hipcc branch around each load and
 // wait for it, which serialises the memory pipeline).
@@ -208,6 +219,34 @@ __device__ __forceinline__ void tdec_fused_check(const TdecWinArgs& a, int cb, i
 #endif
 #ifndef TDEC_NPH
 #define TDEC_NPH 1
+#endif
+// forward pass: segments whose loads are in flight while one is consumed (2: the next one; 3: the next two, a third
+// register set)
+#ifndef TDEC_FPF
+#define TDEC_FPF 2
+#endif
+// the bandwidth-only clone (DIAG 20) with parts of its traffic removed (variant builds, tools/build_variant.sh): what
+// each part of the schedule costs -- NO_E: no extrinsic scatter, NO_CK: no checkpoint stores / loads, NO_FIN: the
+// forward pass loads no inputs, NO_TAB: no interleaver-table loads
+#ifndef TDEC_CLONE_NO_E
+#define TDEC_CLONE_NO_E 0
+#endif
+// extrinsic / a-priori outputs of a whole segment staged in LDS and stored as 16-byte row pieces (0: A/B builds, each
+// output as a scattered 2-byte store)
+#ifndef TDEC_STAGE_OUT
+#define TDEC_STAGE_OUT 1
+#endif
+#ifndef TDEC_CLONE_NO_CK
+#define TDEC_CLONE_NO_CK 0
+#endif
+#ifndef TDEC_CLONE_NO_FIN
+#define TDEC_CLONE_NO_FIN 0
+#endif
+#ifndef TDEC_CLONE_NO_TAB
+#define TDEC_CLONE_NO_TAB 0
+#endif
+#ifndef TDEC_CLONE_CK_HALF // every other checkpoint stored and loaded (the traffic of a 16-step spacing)
+#define TDEC_CLONE_CK_HALF 0
 #endif
 // OUTK: what the half-iteration emits besides the extrinsic (compile time, so the forward loop has no per-step
 // branches): 0 nothing, 1 decision bytes (a.dec: DEC1 from registers, DEC2 through an LDS bitmap), 2 the decision
@@ -273,8 +312,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   const int       txoY  = (dec2 ? (L * NSB + 32) : (L * NSB + 32) / 2) / 4; // parity stream (P1 for DEC2, else P0)
   uint32_t*       txb   = nullptr;
   if constexpr (TX) {
-    __shared__ uint32_t tx_lds[4][2][SEG * 64];
-    txb = &tx_lds[threadIdx.x >> 6][0][0];
+    txb = &tdec_tx_lds[threadIdx.x >> 6][0][0];
   }
   // Parity rows (a.rowmask, DL-SCH pool buffers of the 16-window layout): the rate dematcher leaves at int16 offset
   // SB_ROWMASK of every code block's buffer a bitmap of the rows of its parity streams that hold an LLR (word k of P0,
@@ -285,8 +323,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   constexpr bool RMK = NSB == 16 && !GI;
   uint32_t*      ymask = nullptr;
   if constexpr (RMK) {
-    __shared__ uint32_t ym_lds[4][G * SB_ROWMASK_WORDS];
-    ymask = ym_lds[threadIdx.x >> 6];
+    ymask = tdec_ym_lds[threadIdx.x >> 6];
     // each code block's own NL lanes fill its words: the lanes of missing or finished code blocks have returned above
     // (TX waves run all 8 code blocks, so every word a TX load reads is filled too)
 #pragma unroll
@@ -470,7 +507,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
 #pragma unroll
             for (int s = 0; s < 8; s++) st[s] = nw[s];
           }
-          if (i == 0 && t > 0 && DIAG != 3) {
+          if (i == 0 && t > 0 && DIAG != 3 && !(CL && TDEC_CLONE_NO_CK) && !(CL && TDEC_CLONE_CK_HALF && (t & 1))) {
 #pragma unroll
             for (int s = 0; s < 8; s++) {
               if constexpr (DIAG == 9) {
@@ -531,8 +568,8 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   constexpr int BMW = NSB == 16 ? 193 : 25; // u32 words per code block (K <= 6144 / K <= 800)
   uint32_t*     bm  = nullptr;
   if constexpr (dec2 || wr_bits || wr_bm) {
-    __shared__ uint32_t bm_lds[4 * G * BMW];
-    bm = bm_lds + ((threadIdx.x >> 6) * G + cbg) * BMW;
+    static_assert(G * BMW <= TDEC_BM_WORDS, "decision bitmaps of a wave");
+    bm = tdec_bm_lds + (threadIdx.x >> 6) * TDEC_BM_WORDS + cbg * BMW;
     if constexpr (wr_bm) {
       for (int w = l; w < K / 32; w += NL) bm[w] = 0;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -549,22 +586,77 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   const uint32_t* Yf  = FI ? (const uint32_t*)a.in + (dec2 ? (K + 32) : (K + 32) / 2) + l : Y;
   const uint32_t* APf = FI ? a.A1 + q : AP;
   const uint32_t* ckf = (DIAG == 8 || (DIAG >= 100 && (DIAG & 2))) ? a.ckpt + q : ck;
+  // The extrinsic (DEC1: E for DEC2) or a-priori (DEC2: A1 for the next DEC1) outputs.  Every step of a wave fills
+  // exactly one 256-byte row j' of the destination (the QPP interleaver is contention-free for windows of L steps), but
+  // as 128 scattered 2-byte lane stores, which cost the schedule a third of its time (bandwidth-only clone without
+  // them: 1.26 -> 0.82 ms per 65,536-CB launch, profiles/r05/clone_ab.txt).  STG (whole segments): the 8 steps' outputs
+  // are staged in LDS as the 8 rows they fill, [step][128 windows], and each code block's own lanes store its 32-byte
+  // slices of those rows as 16-byte pieces, two store instructions per segment instead of sixteen.
+  constexpr bool STG = FULL && !GI && TDEC_STAGE_OUT && (dec2 ? wr_a1 : wr_e);
+  int16_t*       O16 = dec2 ? A16 : E16;
+  int16_t*       stg = nullptr;
+  uint32_t*      stg_row = nullptr;
+  if constexpr (STG) {
+    stg     = tdec_stg_lds[threadIdx.x >> 6];
+    stg_row = tdec_stg_row[threadIdx.x >> 6];
+  }
+  auto put = [&](int i, uint32_t tb, v2s v) { // the two outputs of step i (destinations tb: j'*128 + window, lo | hi)
+    if constexpr (STG) {
+      stg[i * 128 + (tb & 127u) + 2 * lane0]         = v.x;
+      stg[i * 128 + ((tb >> 16) & 127u) + 2 * lane0] = v.y;
+      stg_row[i]                                     = (tb & 0xffffu) >> 7; // (the same j' from every lane)
+    } else {
+      O16[(tb & 0xffffu) + lane0 * 2] = v.x;
+      O16[(tb >> 16) + lane0 * 2]     = v.y;
+    }
+  };
+  auto flush = [&]() { // the staged rows of a segment: piece pc of row r for this code block
+    if constexpr (STG) {
+      static_assert(SEG == 8 && NL % 4 == 0, "rows of 8 steps, whole 16-byte pieces per code block");
+      constexpr int PPR = NL / 4; // 16-byte pieces of a code block per row
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const int      idx = k * NL + l, r = idx / PPR, pc = idx % PPR;
+        const uint32_t jr  = stg_row[r]; // the destination row of step r (shared by every window of it)
+        const uint4    v   = *(const uint4*)(stg + r * 128 + 2 * lane0 + pc * 8);
+        *(uint4*)(O16 + (size_t)jr * 128 + 2 * lane0 + pc * 8) = v;
+      }
+      // (the next segment's LDS writes follow these reads in the wave's in-order LDS queue; the fence keeps the
+      // compiler from moving them above)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  };
   uint32_t cx[SEG], cy[SEG], ca[SEG] = {}, cd[SEG], cc[8];
+  constexpr bool NFIN = CL && TDEC_CLONE_NO_FIN, NTAB = CL && TDEC_CLONE_NO_TAB, NCK = CL && TDEC_CLONE_NO_CK;
   auto     load = [&](int t, uint32_t* x, uint32_t* y, uint32_t* ap, uint32_t* d, uint32_t* c) {
-    if constexpr (TX) {
+    if constexpr (TX && !NFIN) {
       if constexpr (!dec2) tx_load(txoX, t * SEG, x);
       tx_load(txoY, t * SEG, y, true);
     }
 #pragma unroll
     for (int i = 0; i < SEG; i++) {
       const int j = FULL ? t * SEG + i : min(t * SEG + i, L - 1); // clamp the ragged last segment
-      if constexpr (!TX || dec2) x[i] = Xf[j * xs];
-      if constexpr (!TX) y[i] = yrow(cbg, j) ? Yf[j * ys] : 0u;
+      if constexpr (NFIN) {
+        x[i] = y[i] = (uint32_t)j;
+      } else {
+        if constexpr (!TX || dec2) x[i] = Xf[j * xs];
+        if constexpr (!TX) y[i] = yrow(cbg, j) ? Yf[j * ys] : 0u;
+      }
       if constexpr (has_ap) ap[i] = APf[j * 64];
-      d[i]        = tab[(size_t)j * NL];
+      if constexpr (NTAB) {
+        d[i] = (uint32_t)(j * 128 + 2 * l) | ((uint32_t)(j * 128 + 2 * l + 1) << 16);
+      } else {
+        d[i] = tab[(size_t)j * NL];
+      }
     }
 #pragma unroll
-    for (int s = 0; s < 8; s++) c[s] = ckf[((size_t)t * 8 + s) * 64];
+    for (int s = 0; s < 8; s++) {
+      c[s] = (NCK || (CL && TDEC_CLONE_CK_HALF && (t & 1))) ? (uint32_t)s : ckf[((size_t)t * 8 + s) * 64];
+    }
   };
   load(0, cx, cy, ca, cd, cc);
 
@@ -586,7 +678,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     const int s0 = t * SEG;
     const int e  = FULL ? s0 + SEG : ((s0 + SEG < L) ? s0 + SEG : L);
     uint32_t  bits = 0; // decision bits of the segment: window 2l in bits 8..15, 2l+1 in 0..7 (MSB first)
-    if (t + 1 < nseg) load(t + 1, nx, ny, na, nd, nc);
+    if (t + TDEC_FPF - 1 < nseg) load(t + TDEC_FPF - 1, nx, ny, na, nd, nc);
 
     v2s xin[SEG];
 #pragma unroll
@@ -615,22 +707,15 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
         if (FULL ? i < SEG : j < e) {
           const v2s      out = xin[i] ^ U(cy[i]) ^ ck8[i] ^ st[i];
           const uint32_t tb  = cd[i];
-          const uint32_t olo = (tb & 0xffffu) + lane0 * 2, ohi = (tb >> 16) + lane0 * 2;
           if constexpr (!dec2) {
-            if constexpr (wr_e) {
-              E16[olo] = out.x;
-              E16[ohi] = out.y;
-            }
+            if constexpr (wr_e && !TDEC_CLONE_NO_E) put(i, tb, out);
             bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
             if constexpr (wr_bm) {
               bm_set(bm, 2 * l * L + j, out.x > 0);
               bm_set(bm, (2 * l + 1) * L + j, out.y > 0);
             }
           } else {
-            if constexpr (wr_a1) {
-              A16[olo] = out.x;
-              A16[ohi] = out.y;
-            }
+            if constexpr (wr_a1 && !TDEC_CLONE_NO_E) put(i, tb, out);
             if constexpr (wr_bm) {
               const uint32_t jd = (tb & 0xffffu) >> 7, wlo = tb & 15u, whi = (tb >> 16) & 15u;
               bm_set(bm, wlo * L + jd, out.x > 0);
@@ -694,11 +779,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
         const uint32_t olo = (tb & 0xffffu) + lane0 * 2, ohi = (tb >> 16) + lane0 * 2;
         if constexpr (!dec2) {
           // e = ext1 - app1 (wrapping), turbodecoder_iter.h:118-120 of the next DEC2
-          if constexpr (wr_e) {
-            const v2s ev = has_ap ? out - U(ca[i]) : out;
-            E16[olo]     = ev.x;
-            E16[ohi]     = ev.y;
-          }
+          if constexpr (wr_e) put(i, tb, has_ap ? out - U(ca[i]) : out);
           if constexpr (wr_d) WG_AT(a.D, j) = W(out);
           bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
           if constexpr (wr_bm) { // windows not byte-aligned: natural bits 2l L + j, (2l + 1) L + j
@@ -707,11 +788,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
           }
         } else {
           // a1 = app1 - ext1 (wrapping) of the next DEC1, turbodecoder_iter.h:108-110
-          if constexpr (wr_a1) {
-            const v2s av = out - xin[i];
-            A16[olo]     = av.x;
-            A16[ohi]     = av.y;
-          }
+          if constexpr (wr_a1) put(i, tb, out - xin[i]);
           if constexpr (wr_bm) { // natural bit w*L + j' (turbodecoder_win.h:973-993)
             const uint32_t jd = (tb & 0xffffu) >> 7, wlo = tb & 15u, whi = (tb >> 16) & 15u;
             bm_set(bm, wlo * L + jd, out.x > 0);
@@ -725,17 +802,31 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
       }
     }
     }
+    flush();
     if constexpr (wr_bits) { // turbodecoder_win.h:973-993: bit = LLR > 0, natural order, MSB first
       uint8_t* bb = (uint8_t*)bm + (size_t)(2 * l) * (L / 8) + t;
       bb[0]       = (uint8_t)(bits >> 8);
       bb[L / 8]   = (uint8_t)bits;
     }
   };
+#if TDEC_FPF == 3
+  // three register sets rotating by position (loop unrolled three times): set A holds segment t, B t + 1, and the
+  // free one receives t + 2
+  uint32_t mx[SEG], my[SEG], ma[SEG] = {}, md[SEG], mc[8];
+  if (nseg > 1) load(1, nx, ny, na, nd, nc);
+#pragma unroll 1
+  for (int t = 0; t < nseg; t += 3) {
+    fseg(t, cx, cy, ca, cd, cc, mx, my, ma, md, mc);
+    if (t + 1 < nseg) fseg(t + 1, nx, ny, na, nd, nc, cx, cy, ca, cd, cc);
+    if (t + 2 < nseg) fseg(t + 2, mx, my, ma, md, mc, nx, ny, na, nd, nc);
+  }
+#else
 #pragma unroll 1
   for (int t = 0; t < nseg; t += 2) {
     fseg(t, cx, cy, ca, cd, cc, nx, ny, na, nd, nc);
     if (t + 1 < nseg) fseg(t + 1, nx, ny, na, nd, nc, cx, cy, ca, cd, cc);
   }
+#endif
   if constexpr (wr_bm || wr_bits) { // the code block's K/8 decision bytes, 8-byte stores by its NL lanes
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
