@@ -92,12 +92,18 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="skip the per-stage and MAP-kernel probes (profiling runs)")
+    ap.add_argument("--workers", type=int, default=None,
+                    help="pdsch / ue_dl: PHY worker threads, each with its own receive context (ue_dl, stream, "
+                         "softbuffers) decoding every W-th batch (srsUE's sf_worker pool, 3 by default); 1 = one "
+                         "synchronous loop.  Default 3 for pdsch, 2 for ue_dl (measured best, profiles/r05/workers_ab.txt)")
     ap.add_argument("--fanout", action="store_true",
                     help="batch fan-out: rank 0 holds every rank's I/Q and scatters the shards over RCCL each step "
                          "(pdsch / ue_dl / plumbing workloads); payload SHA-1s and CRC bitmaps gathered back")
     args = ap.parse_args(argv)
     if args.subframes is None:
         args.subframes = 8192 if args.workload == "siso_qpsk" else 2048
+    if args.workers is None:
+        args.workers = 2 if args.workload == "ue_dl" else 3
     return args
 
 
@@ -720,6 +726,11 @@ def run_pdsch(args, world, rank, local, pg):
         R, nsets = B, 1
     src = Tm4Source(cell, R, local, ctrl)
     rx = Tm4Rx(cell, B, local, ctrl)
+    # PHY workers (srsUE runs 3 sf_worker threads, srsue/src/phy/phy.cc:135-189): W receive contexts (own ue_dl, stream,
+    # softbuffer pool, grids), each host thread decoding every W-th batch, so one worker's host work between its
+    # synchronous calls (result read-back, next call's planning) overlaps the GPU work of the others
+    W = max(1, args.workers) if not args.total_subframes else 1
+    rxs = [rx] + [Tm4Rx(cell, B, local, ctrl) for _ in range(W - 1)]
     dt_total, ok_sample, sample_tbs, bits_all, its_all, batches = 0.0, 0, 0, [], [], 0
     for s in range(nsets):
         a = lo + s * R
@@ -727,29 +738,56 @@ def run_pdsch(args, world, rank, local, pg):
         if n:
             src.generate(a, n, args.snr, args.seed)
         bound = [rx.bind(src, k0, min(B, n - k0)) for k0 in range(0, n, B)]
+        wbound = [bound] + [[r.bind(src, k0, min(B, n - k0)) for k0 in range(0, n, B)] for r in rxs[1:]]
         if s == 0 and bound:
             for _ in range(args.warmup):
-                rx.step(bound[0])
+                for r, wb in zip(rxs, wbound):
+                    r.step(wb[0])
             lib().mi355_device_sync()
         reps = 1 if args.total_subframes else args.steps
         barrier(pg, local)
         lib().mi355_device_sync()
         t0 = time.perf_counter()
-        for _ in range(reps):
-            for b in bound:
-                rx.step(b)
-                if args.total_subframes:
-                    bits_all.append(rx.crc_bits(b[3]))
+        if W == 1:
+            for _ in range(reps):
+                for b in bound:
+                    rx.step(b)
+                    if args.total_subframes:
+                        bits_all.append(rx.crc_bits(b[3]))
+        else:
+            import threading
+            errs = []
+
+            def worker(w):
+                try:
+                    for _ in range(w, reps, W):
+                        for b in wbound[w]:
+                            rxs[w].step(b)
+                except Exception as e:  # noqa: BLE001 -- re-raised on the main thread
+                    errs.append(e)
+
+            th = [threading.Thread(target=worker, args=(w,)) for w in range(W)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            if errs:
+                raise errs[0]
         lib().mi355_device_sync()
         barrier(pg, local)
         dt_total += time.perf_counter() - t0
         batches += reps * len(bound)
-        if bound:  # payload check of the last batch decoded (all of it in the default mode)
-            ok_sample += rx.payload_ok(src, bound[-1])
-            sample_tbs += 2 * bound[-1][3]
+        if bound:  # payload check of the last batch decoded (all of it in the default mode), by every worker
+            wk = rxs[: min(W, reps)] if not args.total_subframes else rxs[:1]
+            for r, wb in zip(wk, wbound):
+                ok_sample += r.payload_ok(src, wb[-1])
+                sample_tbs += 2 * wb[-1][3]
             its_all.append(rx.avg_its(bound[-1][3]))
             if not args.total_subframes:
-                bits_all.append(rx.crc_bits(bound[-1][3]))
+                b = rx.crc_bits(bound[-1][3])
+                for r, wb in zip(wk[1:], wbound[1:]):
+                    b = b & r.crc_bits(wb[-1][3])  # a TB counts only if every worker decoded it
+                bits_all.append(b)
     dt = max_over_ranks(pg, local, dt_total)
     bits = np.concatenate(bits_all) if bits_all else np.zeros(0, np.uint8)
     gathered = gather_bitmap(pg, local, bits)
@@ -782,6 +820,9 @@ def run_pdsch(args, world, rank, local, pg):
     if ctrl:
         workload += ("; grants from the PCFICH/PDCCH blind search (DCI format 2 per subframe, find_and_decode = "
                      "phy_dl_test work_ue)")
+    if W > 1:
+        workload += (f"; {W} PHY worker threads (own ue_dl / stream / softbuffers each) decode alternate batches, "
+                     "every batch a synchronous call")
     if args.total_subframes:
         workload = (f"configs[4]: {args.total_subframes} subframes sharded contiguously over {world} GPU(s), each "
                     "decoded once; " + workload)
@@ -789,7 +830,7 @@ def run_pdsch(args, world, rank, local, pg):
         "higher_is_better": True, "scaling": "weak" if not args.total_subframes else "strong",
         "vs_baseline": None, "dtype": "fp32+int16", "data": "synthetic",
         "config": {"workload": workload, "subframes_per_gpu_batch": B, "code_blocks_per_gpu_batch": 32 * B,
-                   "total_subframes": args.total_subframes or None, "parallelism": f"dp{world}"},
+                   "total_subframes": args.total_subframes or None, "workers_per_gpu": W, "parallelism": f"dp{world}"},
         "crc_ok_tbs": f"{ok_tbs}/{2 * nsf}",
         "crc_bitmap": bitmap_summary(gathered, nsf) if rank == 0 else None,
         "payload_checked_tbs": f"{ok_sample_all}/{sample_all}",
@@ -820,7 +861,8 @@ def run_pdsch(args, world, rank, local, pg):
                 res["dropin_tti_latency"] = dropin_tti_latency(args, cell, local)
     if not ctrl and not args.total_subframes and not args.no_waterfall:
         res["e2e_waterfall"] = waterfall(args, cell, B, src, rx, pg, local, world)
-    rx.pool.close()
+    for r in rxs:
+        r.close()
     src.close()
     return res
 

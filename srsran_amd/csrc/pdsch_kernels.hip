@@ -1016,6 +1016,10 @@ constexpr uint32_t ER_THREADS = PDSCH_ER_THREADS;
 #define PDSCH_ER_PF 1
 #endif
 constexpr int      ER_PF      = PDSCH_ER_PF; // RE pairs per thread whose loads are in flight together (equaliser part)
+#ifndef PDSCH_ER_TPF
+#define PDSCH_ER_TPF 0
+#endif
+constexpr bool     ER_TPF     = PDSCH_ER_TPF; // first round of rate-dematching table words loaded before the equaliser
 constexpr int      ER_Q       = 5;                                                                 // quads per round
 constexpr int      ER_R       = (3 * (6144 + 32) + 12 + 8 * ER_THREADS * ER_Q - 1) / (8 * ER_THREADS * ER_Q); // rounds
 constexpr int      ER_Q2      = 3; // quads per round when both layers share a pass
@@ -1110,6 +1114,26 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   const GLB float2*   yp[2] = {gptr(J.y[0]), gptr(J.nof_rx > 1 ? J.y[1] : J.y[0])};
   const GLB float2*   hp[4];
   h_ptrs(J, hp);
+  // the usual rate-dematching case (two fresh buffers sharing one table, below): its first round of table words does
+  // not depend on the equaliser, so it is loaded now and arrives while the RE pairs are equalised
+  const uint32_t kx0 = c < R.layer[0].C1 ? 0u : 1u, kx1 = c < R.layer[1].C1 ? 0u : 1u;
+  const bool     lean = need[0] && need[1] && fresh[0] && fresh[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
+                    R.layer[0].buflen[kx0] == R.layer[1].buflen[kx1];
+  uint4 iv0[ER_Q];
+  if constexpr (ER_TPF) {
+    if (lean) {
+      const uint32_t  npairs = R.layer[0].buflen[kx0] / 2;
+      const uint32_t* inv32  = (const uint32_t*)R.layer[0].inv[kx0];
+#pragma unroll
+      for (int k = 0; k < ER_Q; k++) {
+        const uint32_t i = 4 * (tid + k * ER_THREADS);
+        iv0[k]           = i + 3 < npairs ? *(const uint4*)(inv32 + i)
+                                          : make_uint4(i < npairs ? inv32[i] : 0xffffffffu,
+                                                       i + 1 < npairs ? inv32[i + 1] : 0xffffffffu,
+                                                       i + 2 < npairs ? inv32[i + 2] : 0xffffffffu, 0xffffffffu);
+      }
+    }
+  }
   const uint32_t re0 = rp / Qm, re1 = (rp + n_e) / Qm, pairs = (J.nof_re + 1) / 2;
   const uint32_t p1  = P.diag == 2 ? 0u : min((re1 + 1) / 2, pairs);
   // ER_PF RE pairs per thread in flight: their map words first, then every gather of all of them, then the math
@@ -1169,9 +1193,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   // rate dematching of each layer's image into its softbuffer (dlsch_rm_rx's gather, E <= N); both layers through
   // one pass when they share the table (same K and rv: the usual case), so the table is read and decoded once
   {
-    const uint32_t kx0 = c < R.layer[0].C1 ? 0u : 1u, kx1 = c < R.layer[1].C1 ? 0u : 1u;
-    if (need[0] && need[1] && fresh[0] && fresh[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
-        R.layer[0].buflen[kx0] == R.layer[1].buflen[kx1]) {
+    if (lean) {
       // the usual case, two fresh buffers: every position is written, a missing LLR reads the zero slot
       const uint32_t  npairs = R.layer[0].buflen[kx0] / 2, Kc = (R.layer[0].N[kx0] - 12) / 3;
       const uint32_t* inv32  = (const uint32_t*)R.layer[0].inv[kx0];
@@ -1186,6 +1208,10 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
 #pragma unroll
         for (int k = 0; k < ER_Q; k++) {
           const uint32_t i = 4 * (tid + (rd * ER_Q + k) * ER_THREADS);
+          if (ER_TPF && rd == 0) {
+            iv[k] = iv0[k];
+            continue;
+          }
           iv[k]            = i + 3 < npairs ? *(const uint4*)(inv32 + i)
                                             : make_uint4(i < npairs ? inv32[i] : 0xffffffffu,
                                                          i + 1 < npairs ? inv32[i + 1] : 0xffffffffu,
