@@ -57,7 +57,6 @@ SURVEY_BYTES_PER_CB_DECODE = 37848
 METRIC = "PDSCH decoded Mbps + code-blocks/sec, 20 MHz TM4 QAM256, 1/2/4/8 GPU"
 TBS = 97896
 NB = TBS // 8
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_tdec_pmc.json")
 MAP_SOURCES = ("srsran_amd/csrc/tdec_kernels.hip", "srsran_amd/csrc/tdec_internal.h", "srsran_amd/csrc/lte_qpp_table.h")
 
 
@@ -311,13 +310,20 @@ def map_kernel_hash() -> str:
     return h.hexdigest()
 
 
-def load_pmc(ncb: int):
-    """PMC summary of the MAP kernel (tools/pmc_summary.py), accepted only if it was recorded on the current kernel
+def pmc_file(mode: str) -> str:
+    """The MAP kernel's PMC summary for a probe mode (tools/map_pmc_summary.py): e2e (pdsch / ue_dl probes), siso,
+    tdec."""
+    return os.path.join(ROOT, "profiles", f"map_pmc_{mode}.json")
+
+
+def load_pmc(ncb: int, mode: str = "e2e"):
+    """PMC summary of the MAP kernel for this probe mode, accepted only if it was recorded on the current kernel
     sources and the same launch size; otherwise (None, reason)."""
-    if not os.path.exists(PMC_FILE):
-        return None, "no PMC summary"
+    path = pmc_file(mode)
+    if not os.path.exists(path):
+        return None, f"no PMC summary for {mode} ({os.path.relpath(path, ROOT)})"
     try:
-        pmc = json.load(open(PMC_FILE))
+        pmc = json.load(open(path))
     except Exception as e:  # noqa: BLE001
         return None, f"unreadable PMC summary: {e}"
     if pmc.get("kernel_src_sha1") != map_kernel_hash():
@@ -327,7 +333,7 @@ def load_pmc(ncb: int):
     return pmc, None
 
 
-def tdec_roofline(ms, launches, ncb, K):
+def tdec_roofline(ms, launches, ncb, K, mode="e2e"):
     """Roofline of the MAP half-iteration kernel (tdec_win_halfit) from HIP-event timing on its stream.
     Primary (schema) entry: HBM against SURVEY 8(d)'s compulsory bytes, 37,848 B per CB per 8-half-iteration
     decode (= 4,731 B per CB half-iteration); roofline_valu: SURVEY's ~537.5 k int16 ops per CB half-iteration
@@ -337,7 +343,7 @@ def tdec_roofline(ms, launches, ncb, K):
     avg = ms / max(launches, 1)
     bytes_launch = SURVEY_BYTES_PER_CB_DECODE / 8 * ncb * K / 6144
     achieved = bytes_launch / (avg / 1e3) / 1e9
-    pmc, why = load_pmc(ncb)
+    pmc, why = load_pmc(ncb, mode)
     traffic = None
     if pmc:
         traffic = pmc["hbm_bytes_per_launch"]
@@ -352,7 +358,9 @@ def tdec_roofline(ms, launches, ncb, K):
     if why:
         roof["traffic_note"] = why
     else:
-        roof["traffic_source"] = f"{os.path.relpath(PMC_FILE, ROOT)} ({pmc.get('tag')}): 2 x FETCH_SIZE + WRITE_SIZE"
+        roof["traffic_source"] = (f"{os.path.relpath(pmc_file(mode), ROOT)} ({pmc.get('tag')}): 2 x FETCH_SIZE + "
+                                  "WRITE_SIZE, the same 8-half-iteration probe (tools/map_pmc.py)")
+        roof["traffic_bytes_per_cb_halfit"] = round(traffic / ncb)
         roof["traffic_gbs"] = round(traffic / (avg / 1e3) / 1e9, 1)
         roof["traffic_frac"] = round(traffic / (avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
     ops = SURVEY_OPS_PER_CB_HALFIT * ncb * K / 6144
@@ -601,7 +609,7 @@ def softbuffer_contents(rx, ncb):
     return C.cast(buf, C.c_void_p).value, stride.value
 
 
-def map_probe(rx, ncb, local, K=6144):
+def map_probe(rx, ncb, local, K=6144, mode="e2e"):
     """Dominant kernel: the MAP half-iteration over this batch's ncb code blocks (the first ncb softbuffer slots hold
     the rate-dematched LLRs of the last step), a fixed 8 half-iterations without early stop (configs[1]'s regime
     on the e2e code blocks), HIP events on the decoder's stream.  Returns (roofline, roofline_valu, fixed8 dict)."""
@@ -630,13 +638,13 @@ def map_probe(rx, ncb, local, K=6144):
     lib().mi355_tdec_set_diag(old)
     d_junk.free()
     dec.set_profiling(False)
-    roof, valu = tdec_roofline(kms, kl, ncb, K)
+    roof, valu = tdec_roofline(kms, kl, ncb, K, mode)
     if cl:
         clone = cms / cl
         roof["schedule_clone_ms"] = round(clone, 4)
         roof["schedule_frac"] = round(clone / roof["avg_launch_ms"], 4)
         roof["schedule_note"] = ("bandwidth-only clone of tdec_win_halfit (MI355_TDEC_DIAG 20) over the same "
-                                 "65,536-CB launches: schedule_frac = clone time / real time (1.0 = the trellis math "
+                                 f"{ncb:,}-CB launches: schedule_frac = clone time / real time (1.0 = the trellis math "
                                  "is fully hidden under this schedule's memory traffic)")
     fixed8 = {"code_blocks": ncb, "half_iterations": 8, "ms": round(wall * 1e3, 3),
               "code_blocks_per_s": round(ncb / wall, 1), "mbps": round(ncb * (K - 24) / wall / 1e6, 1),
@@ -1023,7 +1031,7 @@ def run_siso(args, world, rank, local, pg):
            "crc_ok_tbs": f"{ok_tbs}/{B * world}", "crc_bitmap": bitmap_summary(gathered, B * world) if rank == 0 else None,
            "payload_checked_tbs": f"{ok_pay}/{B * world}", "avg_half_iterations": round(its, 3)}
     if not args.no_roofline:
-        roof, valu, fixed8, (ptr, stride, _d_out) = map_probe(rx, SISO_C * B, local, K=SISO_K)
+        roof, valu, fixed8, (ptr, stride, _d_out) = map_probe(rx, SISO_C * B, local, K=SISO_K, mode="siso")
         res["roofline"], res["roofline_valu"], res["decoder_bound_fixed8"] = roof, valu, fixed8
         if rank == 0 and world == 1 and not args.no_cpu:
             from oracle import pdsch_chain as pc
@@ -1168,13 +1176,13 @@ def run_tdec(args, world, rank, local, pg):
     lib().mi355_tdec_set_diag(old)
     d_junk.free()
     dec.set_profiling(False)
-    roof, valu = tdec_roofline(kms, kl, ncb, K)
+    roof, valu = tdec_roofline(kms, kl, ncb, K, "tdec")
     if cl:
         clone = cms / cl
         roof["schedule_clone_ms"] = round(clone, 4)
         roof["schedule_frac"] = round(clone / roof["avg_launch_ms"], 4)
         roof["schedule_note"] = ("bandwidth-only clone of tdec_win_halfit (MI355_TDEC_DIAG 20) over the same "
-                                 "65,536-CB launches: schedule_frac = clone time / real time (1.0 = the trellis math "
+                                 f"{ncb:,}-CB launches: schedule_frac = clone time / real time (1.0 = the trellis math "
                                  "is fully hidden under this schedule's memory traffic)")
     cb_s = world * ncb * args.steps / dt
     res = {
