@@ -139,6 +139,12 @@ def dist_setup(expect_world: int | None = None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("BENCH_SHARE_GPU"):
+        # rehearsal of the multi-rank path on a one-GPU box (tests/test_dist_gpu.py): every rank decodes on device 0,
+        # the collectives go over gloo (RCCL refuses two ranks on one device)
+        if dist_backend() == "nccl":
+            raise SystemExit("bench.py: BENCH_SHARE_GPU needs BENCH_DIST_BACKEND=gloo")
+        local = 0
     if expect_world is not None and world != expect_world:
         raise SystemExit(f"bench.py: --gpus {expect_world} but the launcher started WORLD_SIZE={world} ranks")
     pg = None
