@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Per-kernel table of a tools/gpu/e2e_pmc.sh run: time (kernel trace), HBM bytes per launch (2 x FETCH_SIZE +
 WRITE_SIZE, MI355X_MICROARCH.md's gfx950 rule), SQ shares of wave time, LDS conflicts.  python3 tools/pmc_kernels.py
-gpurun_out/pmc_<tag> [min_us]"""
+gpurun_out/pmc_<tag> [min_us]
+(averages are over every launch of a kernel name, no-op launches included: a kernel whose later launches early-exit
+shows its real launch's bytes and time diluted by the call count)"""
 import collections
 import csv
 import glob
@@ -43,6 +45,7 @@ for k, (calls, us) in sorted(tr.items(), key=lambda kv: -kv[1][0] * kv[1][1]):
     valu = 100 * avg(ld[k], "SQ_ACTIVE_INST_VALU") / wc if wc else float("nan")
     vm = avg(sq[k], "SQ_INSTS_VMEM_RD") + avg(sq[k], "SQ_INSTS_VMEM_WR")
     lds = avg(ld[k], "SQ_INSTS_LDS")
-    conf = 100 * avg(ld[k], "SQ_LDS_BANK_CONFLICT") / avg(ld[k], "SQ_LDS_IDX_ACTIVE") if ld.get(k) else float("nan")
-    print(f"{k:52s} {calls:5d} {us:8.1f} {rd:8.1f} {w:8.1f} {(rd + w) / us / 1e3:6.2f} {valu:6.1f} {wait:6.1f} "
+    act = avg(ld[k], "SQ_LDS_IDX_ACTIVE") if ld.get(k) else 0.0
+    conf = 100 * avg(ld[k], "SQ_LDS_BANK_CONFLICT") / act if act else float("nan")
+    print(f"{k:52s} {calls:5d} {us:8.1f} {rd:8.1f} {w:8.1f} {(rd + w) / us:6.2f} {valu:6.1f} {wait:6.1f} "
           f"{lds / vm if vm else float('nan'):8.2f} {conf:8.1f}")
