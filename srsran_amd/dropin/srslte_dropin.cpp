@@ -506,8 +506,14 @@ struct UeDlState {
   float*         d_in[MI355_MAX_RX_ANT] = {};
   float*         d_grid[MI355_MAX_RX_ANT] = {};
   float*         d_ce[MI355_MAX_PORTS][MI355_MAX_RX_ANT] = {};
-  PinnedBuf      h_in, h_back;
+  PinnedBuf      h_in;
   bool           host_grids = true;
+  // the caller-visible q->sf_symbols / chest_res.ce: one pinned block, laid out as the device's [grid rx][ce port x rx]
+  // once the cell is set, so the read-back lands in them directly (no host copy); side stream: that read-back runs
+  // beside the control channels
+  cf_t*          h_block  = nullptr;
+  size_t         h_slot   = 0; // complex samples per buffer as allocated (max_prb)
+  hipStream_t    side     = nullptr;
   // last estimate and control-stage outcome
   bool                 est_valid = false;
   uint32_t             est_tti   = 0;
@@ -522,6 +528,7 @@ struct UeDlState {
   {
     if (ue) mi355_ue_dl_destroy(ue);
     if (d_mem) (void)hipFree(d_mem);
+    if (side) (void)hipStreamDestroy(side);
     if (stream) {
       arena_forget_stream(stream);
       (void)hipStreamDestroy(stream);
@@ -530,6 +537,25 @@ struct UeDlState {
 };
 
 UeDlState* ue_state(srslte_ue_dl_t* q) { return q ? (UeDlState*)q->mi355 : nullptr; }
+
+constexpr size_t ue_block_slots() { return SRSLTE_MAX_PORTS + SRSLTE_MAX_PORTS * SRSLTE_MAX_PORTS + 4; }
+
+// Point q->sf_symbols / chest_res.ce into the pinned block.  With a cell set (grid_len > 0), the grids of the nof_rx
+// antennas and the estimates [port][rx] sit back to back with stride grid_len, exactly as the device's d_grid / d_ce
+// (srslte_ue_dl_set_cell), so one read-back fills them all; the buffers the cell does not use follow, each a full
+// slot.  (grid_len <= h_slot, so the packed part takes at most nrx (1 + nports) slots and the rest 20 - nrx (1 + nports):
+// 20 in all.)
+void ue_point_buffers(srslte_ue_dl_t* q, UeDlState* st, size_t grid_len, uint32_t nrx, uint32_t nports)
+{
+  cf_t*  b    = st->h_block;
+  size_t used = grid_len * (size_t)nrx * (1 + nports), k = 0;
+  used        = (used + st->h_slot - 1) / st->h_slot * st->h_slot; // the packed part, in whole slots
+  for (uint32_t j = 0; j < SRSLTE_MAX_PORTS; j++) {
+    q->sf_symbols[j] = j < nrx ? b + j * grid_len : b + used + (k++) * st->h_slot;
+    for (uint32_t i = 0; i < SRSLTE_MAX_PORTS; i++)
+      q->chest_res.ce[i][j] = (i < nports && j < nrx) ? b + (nrx + i * nrx + j) * grid_len : b + used + (k++) * st->h_slot;
+  }
+}
 
 int ue_run_ctrl(srslte_ue_dl_t* q, UeDlState* st, srslte_dl_sf_cfg_t* sf, const srslte_ue_dl_cfg_t* cfg, uint16_t rnti)
 {
@@ -616,23 +642,21 @@ int ue_fft_estimate(srslte_ue_dl_t* q, srslte_dl_sf_cfg_t* sf, srslte_ue_dl_cfg_
   R.rssi_dbm   = c.rssi_dbm;
   R.cfo        = c.cfo;
   R.sync_error = c.sync_error;
-  // PCFICH (CFI into sf->cfi) and the PDCCH candidates of the UE's RNTI (estimate_pdcch_pcfich, ue_dl.c:348-381)
-  if (ue_run_ctrl(q, st, sf, cfg, q->pregen_rnti) != SRSLTE_SUCCESS) return SRSLTE_ERROR;
-  // host copies of the grid and the estimates (the reference's q->sf_symbols / chest_res.ce are host buffers)
+  // host copies of the grid and the estimates (the reference's q->sf_symbols / chest_res.ce are host buffers): the
+  // grids and the estimates are consecutive in d_mem and in the pinned block the caller's pointers are slots of
+  // (srslte_ue_dl_set_cell), so one read-back fills them, on the side stream while the control channels run (the
+  // estimation above has completed: decode_fft_estimate_batch returns after it)
+  bool back = false;
   if (st->host_grids) {
-    const size_t ng = (size_t)st->grid_len * 2 * sizeof(float);
-    const size_t nb = ng * st->nof_rx * (1 + q->cell.nof_ports);
-    if (st->h_back.reserve(nb)) return SRSLTE_ERROR;
-    // the grids and the estimates are consecutive in d_mem (srslte_ue_dl_set_cell): one read-back
-    if (hipMemcpyAsync(st->h_back.p, st->d_grid[0], nb, hipMemcpyDeviceToHost, st->stream) != hipSuccess)
+    const size_t nb = (size_t)st->grid_len * 2 * sizeof(float) * st->nof_rx * (1 + q->cell.nof_ports);
+    if (hipMemcpyAsync(st->h_block, st->d_grid[0], nb, hipMemcpyDeviceToHost, st->side) != hipSuccess)
       return SRSLTE_ERROR;
-    if (hipStreamSynchronize(st->stream) != hipSuccess) return SRSLTE_ERROR;
-    size_t o = 0;
-    for (uint32_t r = 0; r < st->nof_rx; r++, o += ng) memcpy(q->sf_symbols[r], (char*)st->h_back.p + o, ng);
-    for (uint32_t p = 0; p < q->cell.nof_ports; p++)
-      for (uint32_t r = 0; r < st->nof_rx; r++, o += ng) memcpy(R.ce[p][r], (char*)st->h_back.p + o, ng);
+    back = true;
   }
-  return SRSLTE_SUCCESS;
+  // PCFICH (CFI into sf->cfi) and the PDCCH candidates of the UE's RNTI (estimate_pdcch_pcfich, ue_dl.c:348-381)
+  const int rc = ue_run_ctrl(q, st, sf, cfg, q->pregen_rnti);
+  if (back && hipStreamSynchronize(st->side) != hipSuccess) return SRSLTE_ERROR;
+  return rc == SRSLTE_SUCCESS ? SRSLTE_SUCCESS : SRSLTE_ERROR;
 }
 
 } // namespace
@@ -1032,16 +1056,17 @@ int srslte_ue_dl_init(srslte_ue_dl_t* q, cf_t* in_buffer[SRSLTE_MAX_PORTS], uint
   for (uint32_t r = 0; r < nof_rx_antennas; r++) st->in_buffer[r] = in_buffer ? in_buffer[r] : nullptr;
   const size_t sflen_re = (size_t)max_prb * 12 * 14; // MAX_SFLEN_RE (ue_dl.c:29, normal CP)
   int          err      = 0;
-  for (int j = 0; j < SRSLTE_MAX_PORTS && !err; j++) {
-    q->sf_symbols[j] = (cf_t*)calloc(sflen_re, sizeof(cf_t));
-    err |= !q->sf_symbols[j];
-    for (int i = 0; i < SRSLTE_MAX_PORTS && !err; i++) { // srslte_chest_dl_res_init
-      q->chest_res.ce[i][j] = (cf_t*)calloc(sflen_re, sizeof(cf_t));
-      err |= !q->chest_res.ce[i][j];
-    }
-  }
   (void)hipSetDevice(st->device);
+  // q->sf_symbols[4] and chest_res.ce[4][4] (ue_dl.c:66-120, srslte_chest_dl_res_init) as slots of one zeroed pinned
+  // block: 20 buffers of sflen_re, 4 spare for set_cell's relayout
+  st->h_slot = sflen_re;
+  err        = hipHostMalloc((void**)&st->h_block, ue_block_slots() * sflen_re * sizeof(cf_t)) != hipSuccess;
+  if (!err) {
+    memset(st->h_block, 0, ue_block_slots() * sflen_re * sizeof(cf_t));
+    ue_point_buffers(q, st, 0, 0, 0);
+  }
   err = err || hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking) != hipSuccess;
+  err = err || hipStreamCreateWithFlags(&st->side, hipStreamNonBlocking) != hipSuccess;
   err = err || srslte_pdsch_init_ue(&q->pdsch, max_prb, nof_rx_antennas) != SRSLTE_SUCCESS;
   if (err) {
     srslte_ue_dl_free(q);
@@ -1057,11 +1082,10 @@ void srslte_ue_dl_free(srslte_ue_dl_t* q)
   PdschState* ps = pdsch_state(&q->pdsch);
   if (ps) ps->rx = nullptr, ps->own_rx = false; // the ue_dl's receiver, destroyed with the ue_dl
   srslte_pdsch_free(&q->pdsch);
-  delete ue_state(q);
-  for (int j = 0; j < SRSLTE_MAX_PORTS; j++) {
-    free(q->sf_symbols[j]);
-    for (int i = 0; i < SRSLTE_MAX_PORTS; i++) free(q->chest_res.ce[i][j]);
-  }
+  UeDlState* st = ue_state(q);
+  cf_t*      hb = st ? st->h_block : nullptr;
+  delete st;
+  if (hb) (void)hipHostFree(hb);
   memset(q, 0, sizeof(*q));
 }
 
@@ -1097,6 +1121,7 @@ int srslte_ue_dl_set_cell(srslte_ue_dl_t* q, srslte_cell_t cell)
   for (uint32_t r = 0; r < st->nof_rx; r++, p += 2 * (size_t)st->grid_len) st->d_grid[r] = p;
   for (uint32_t pt = 0; pt < cell.nof_ports; pt++)
     for (uint32_t r = 0; r < st->nof_rx; r++, p += 2 * (size_t)st->grid_len) st->d_ce[pt][r] = p;
+  ue_point_buffers(q, st, st->grid_len, st->nof_rx, cell.nof_ports);
   // the embedded PDSCH object decodes with the ue_dl's receiver, on the ue_dl's stream
   ps->rx         = mi355_ue_dl_pdsch(st->ue);
   ps->own_rx     = false;
