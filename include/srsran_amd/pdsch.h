@@ -125,6 +125,18 @@ int mi355_pdsch_decode_batch(mi355_pdsch_t*           q,
                              mi355_pdsch_res_t*       res,
                              void*                    stream);
 
+/* mi355_pdsch_decode_batch in two halves: launch enqueues the whole decode on `stream` (NULL: the receiver's own) and
+ * returns with the per-TB results in flight (res must stay valid); collect waits for them and fills res.  Work the
+ * caller enqueues on the same stream in between (e.g. the payload read-back) runs behind the decode, so one host wait
+ * can cover both.  One launch may be outstanding per receiver; mi355_pdsch_decode_batch = launch + collect. */
+int mi355_pdsch_decode_launch(mi355_pdsch_t*           q,
+                              mi355_softbuffer_pool_t* pool,
+                              const mi355_pdsch_job_t* jobs,
+                              uint32_t                 njobs,
+                              mi355_pdsch_res_t*       res,
+                              void*                    stream);
+int mi355_pdsch_decode_collect(mi355_pdsch_t* q);
+
 /* The DL-SCH decoder owned by this PDSCH receiver (borrowed: srslte_pdsch_t.dl_sch), e.g. for profiling. */
 mi355_dlsch_t* mi355_pdsch_dlsch(mi355_pdsch_t* q);
 

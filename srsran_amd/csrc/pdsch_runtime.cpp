@@ -157,6 +157,8 @@ struct EqRmPlan {
 
 struct mi355_pdsch {
   int                                  device = 0;
+  std::unique_ptr<mi355::PdschPending> api_pend;          // mi355_pdsch_decode_launch's results in flight
+  bool                                 api_armed = false;
   mi355_cell_t                         cell{};
   uint32_t                             nof_rx = 1;
   hipStream_t                          own    = nullptr;
@@ -637,6 +639,26 @@ int mi355_pdsch_decode_batch(mi355_pdsch_t*           q,
                              void*                    stream)
 {
   return mi355::pdsch_decode_batch_dev_noise(q, pool, jobs, njobs, res, stream, nullptr);
+}
+
+int mi355_pdsch_decode_launch(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi355_pdsch_job_t* jobs,
+                              uint32_t njobs, mi355_pdsch_res_t* res, void* stream)
+{
+  if (!q) return MI355_ERROR_INVALID_INPUTS;
+  if (q->api_armed) return MI355_ERROR; // the previous launch was not collected
+  if (!q->api_pend) q->api_pend.reset(new mi355::PdschPending);
+  const int r = mi355::pdsch_decode_batch_dev_noise(q, pool, jobs, njobs, res, stream, nullptr, mi355::WaitHook{}, false,
+                                                    q->api_pend.get());
+  q->api_armed = true; // collected even after an error (whatever groups were enqueued)
+  return r;
+}
+
+int mi355_pdsch_decode_collect(mi355_pdsch_t* q)
+{
+  if (!q) return MI355_ERROR_INVALID_INPUTS;
+  if (!q->api_armed) return MI355_SUCCESS;
+  q->api_armed = false;
+  return q->api_pend->collect();
 }
 
 } // extern "C"

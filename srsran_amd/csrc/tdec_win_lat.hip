@@ -350,6 +350,9 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
     };
     // output of step k for pair pp (windows 2pp, 2pp+1): DEC1 E = out - a1 at the interleaved position, DEC2
     // A1 = out - E at the natural one; its decision bit at the natural position (DEC1: own, DEC2: the destination's)
+    // DEC1's decisions of a pass are whole bytes when every pass covers 8 aligned steps of each window (L % 16 == 0:
+    // H and the pass bases are multiples of 8): built from two wave ballots in pass_do instead of per-bit LDS atomics
+    const bool bytes1 = !dec2 && NL == 8 && L % 16 == 0;
     auto put = [&](int k, int pp, uint32_t e, v2s x, v2s ap, v2s out) {
       const v2s      o   = dec2 ? out - x : (has_ap ? out - ap : out);
       const uint32_t olo = e & 0xffffu, ohi = e >> 16; // row j' * 128 + window
@@ -358,7 +361,7 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
       if (dec2) {
         dbit(bits, (olo & 127) * L + (olo >> 7), out.x > 0);
         dbit(bits, (ohi & 127) * L + (ohi >> 7), out.y > 0);
-      } else {
+      } else if (!bytes1) {
         dbit(bits, 2 * pp * L + k, out.x > 0);
         dbit(bits, (2 * pp + 1) * L + k, out.y > 0);
       }
@@ -563,12 +566,30 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
         ld8(bs, P.row);
       }
     };
-    auto pass_do = [&](bool ok, int k, PassIn& P) {
+    // fwd: the alpha wave's passes (step k = base + i_p), else the beta wave's (k = base + 7 - i_p)
+    auto pass_do = [&](bool ok, int k, PassIn& P, bool fwd) {
       if (LAT_DIAG & 3) return;
+      bool dx = false, dy = false;
       if (ok) {
         v2s x, y, ap;
         xin(P.xw, P.yw, P.aw, x, y, ap);
-        put(k, lp, P.e, x, ap, out_llr(P.a8, x, y, P.row, false));
+        const v2s out = out_llr(P.a8, x, y, P.row, false);
+        put(k, lp, P.e, x, ap, out);
+        dx = out.x > 0, dy = out.y > 0;
+      }
+      if (bytes1) { // (wave-uniform) lane i_p * 8 + lp holds step i_p of the pass for windows 2lp, 2lp + 1
+        const uint64_t bx = __builtin_amdgcn_ballot_w64(dx), by = __builtin_amdgcn_ballot_w64(dy);
+        if (i_p == 0) {
+          // bit i_p of the pair's column at bit 8 i_p, gathered into one byte: MSB first in step order
+          // (turbodecoder_win.h:973-993); the alpha pass's step i_p is bit 7 - i_p, the beta pass's bit i_p
+          const uint64_t col = 0x0101010101010101ull, mag = fwd ? 0x8040201008040201ull : 0x0102040810204080ull;
+          const uint32_t b0  = (uint32_t)((((bx >> lp) & col) * mag) >> 56);
+          const uint32_t b1  = (uint32_t)((((by >> lp) & col) * mag) >> 56);
+          const int      kb  = fwd ? k : k - 7; // the pass's first step (a multiple of 8)
+          uint8_t*       bb  = (uint8_t*)bits;
+          bb[(2 * lp * L + kb) >> 3]       = (uint8_t)b0;
+          bb[((2 * lp + 1) * L + kb) >> 3] = (uint8_t)b1;
+        }
       }
     };
     if (alpha) {
@@ -582,11 +603,11 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
         uint32_t*      sc = sg + (c & 1) * 64 * 8;
         if (c > 0) pass_load(okp, kp, sg + ((c - 1) & 1) * 64 * 8 + (size_t)lane * 8, bm + ((size_t)(kp - H) * NL + lp) * 8, P.e, P);
         if (rec) a_run(ka, n, pha, sc, -k0 * RS, RS);
-        if (c > 0) pass_do(okp, kp, P);
+        if (c > 0) pass_do(okp, kp, P, true);
         okp = ok, kp = k, P.e = e;
         if (k0 + PB >= L) { // the last chunk's pass
           pass_load(ok, k, sc + (size_t)lane * 8, bm + ((size_t)(k - H) * NL + lp) * 8, e, P);
-          pass_do(ok, k, P);
+          pass_do(ok, k, P, true);
         }
       }
     } else if (wv == bw) {
@@ -600,11 +621,11 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
         uint32_t*      sc = sg + (c & 1) * 64 * 8;
         if (c > 0) pass_load(okp, kp, am + ((size_t)kp * NL + lp) * 8, sg + ((c - 1) & 1) * 64 * 8 + (size_t)lane * 8, P.e, P);
         if (rec) b_run(kb, n, phb, sc, k0 * RS, -RS);
-        if (c > 0) pass_do(okp, kp, P);
+        if (c > 0) pass_do(okp, kp, P, false);
         okp = ok, kp = k, P.e = e;
         if (k0 - PB < 1) {
           pass_load(ok, k, am + ((size_t)k * NL + lp) * 8, sc + (size_t)lane * 8, e, P);
-          pass_do(ok, k, P);
+          pass_do(ok, k, P, false);
         }
       }
     }

@@ -467,16 +467,20 @@ int pdsch_decode_dev(srslte_pdsch_t* q, PdschState* st, hipStream_t stream, srsl
     if (mi355_pdsch_set_llr_8bit(st->rx, q->llr_is_8bit)) return SRSLTE_ERROR;
     st->llr8 = q->llr_is_8bit;
   }
-  if (mi355_pdsch_decode_batch(st->rx, A.pool, &job, 1, res, stream) != MI355_SUCCESS) return SRSLTE_ERROR;
-  // one payload copy for both TBs (consecutive in d_payload), the CRC flags behind it, one wait
-  uint8_t* hp = (uint8_t*)st->h_payload.p;
-  if (hipMemcpyAsync(hp, st->d_payload, pay_total, hipMemcpyDeviceToHost, stream) != hipSuccess) return SRSLTE_ERROR;
-  for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++) {
-    if (!run[t]) continue;
-    if (mi355_softbuffer_get_cb_crc_async(A.pool, (uint32_t)A.slot_of(cfg->softbuffers.rx[t]), hp + pay_total + t * A.max_cb,
-                                          stream) != MI355_SUCCESS)
-      return SRSLTE_ERROR;
+  // the decode with its per-TB results in flight, then one payload copy for both TBs (consecutive in d_payload) and
+  // the CRC flags behind it on the same stream, then the waits (the read-backs were enqueued before the first one)
+  if (mi355_pdsch_decode_launch(st->rx, A.pool, &job, 1, res, stream) != MI355_SUCCESS) {
+    (void)mi355_pdsch_decode_collect(st->rx);
+    return SRSLTE_ERROR;
   }
+  uint8_t* hp = (uint8_t*)st->h_payload.p;
+  bool     ok = hipMemcpyAsync(hp, st->d_payload, pay_total, hipMemcpyDeviceToHost, stream) == hipSuccess;
+  for (int t = 0; t < SRSLTE_MAX_CODEWORDS && ok; t++) {
+    if (!run[t]) continue;
+    ok = mi355_softbuffer_get_cb_crc_async(A.pool, (uint32_t)A.slot_of(cfg->softbuffers.rx[t]), hp + pay_total + t * A.max_cb,
+                                           stream) == MI355_SUCCESS;
+  }
+  if (mi355_pdsch_decode_collect(st->rx) != MI355_SUCCESS || !ok) return SRSLTE_ERROR;
   if (hipStreamSynchronize(stream) != hipSuccess) return SRSLTE_ERROR;
   for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++) {
     if (!run[t]) continue;
