@@ -102,7 +102,7 @@ def parse(argv=None):
     if args.subframes is None:
         args.subframes = 8192 if args.workload == "siso_qpsk" else 2048
     if args.workers is None:
-        args.workers = 2 if args.workload == "ue_dl" else 3
+        args.workers = 2 if args.workload in ("ue_dl", "siso_qpsk") else 3
     return args
 
 
@@ -723,6 +723,36 @@ def config1_generic(local, budget_s=2.0, with_cpu=True):
     return res
 
 
+def run_workers(rxs, work, reps):
+    """reps steps over W receive contexts: rxs[w] decodes work[w] (its list of bound batches) on steps w, w + W, ...,
+    each on a host thread of its own (W = 1: this thread).  Every call is synchronous, so a worker's host work between
+    calls overlaps the others' GPU work (srsUE's sf_worker pool)."""
+    W = len(rxs)
+    if W == 1:
+        for _ in range(reps):
+            for b in work[0]:
+                rxs[0].step(b)
+        return
+    import threading
+    errs = []
+
+    def worker(w):
+        try:
+            for _ in range(w, reps, W):
+                for b in work[w]:
+                    rxs[w].step(b)
+        except Exception as e:  # noqa: BLE001 -- re-raised on the main thread
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(w,)) for w in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
 def run_pdsch(args, world, rank, local, pg):
     from srsran_amd import lib
     cell = tm4_setup()
@@ -762,31 +792,13 @@ def run_pdsch(args, world, rank, local, pg):
         barrier(pg, local)
         lib().mi355_device_sync()
         t0 = time.perf_counter()
-        if W == 1:
+        if args.total_subframes:
             for _ in range(reps):
                 for b in bound:
                     rx.step(b)
-                    if args.total_subframes:
-                        bits_all.append(rx.crc_bits(b[3]))
+                    bits_all.append(rx.crc_bits(b[3]))
         else:
-            import threading
-            errs = []
-
-            def worker(w):
-                try:
-                    for _ in range(w, reps, W):
-                        for b in wbound[w]:
-                            rxs[w].step(b)
-                except Exception as e:  # noqa: BLE001 -- re-raised on the main thread
-                    errs.append(e)
-
-            th = [threading.Thread(target=worker, args=(w,)) for w in range(W)]
-            for t in th:
-                t.start()
-            for t in th:
-                t.join()
-            if errs:
-                raise errs[0]
+            run_workers(rxs, wbound, reps)
         lib().mi355_device_sync()
         barrier(pg, local)
         dt_total += time.perf_counter() - t0
@@ -1003,21 +1015,26 @@ def run_siso(args, world, rank, local, pg):
     plans = synth.phy_dl_test_plans(cell, 0, 9, False, nof_subframes=B, first=lo)
     src = synth.DlSource(cell, nrx, B, nb, local)
     src.generate(lo, plans, args.siso_snr, args.seed, ctrl=True)
-    rx = synth.DlReceiver(cell, nrx, B, nb, local, ctrl=True, max_cb=SISO_C, ce_rows=1)
-    bound = rx.bind(src, 0, B, tb_major=True)  # TB0 code blocks contiguous in the pool (MAP probe)
+    W = max(1, args.workers)
+    rxs = [synth.DlReceiver(cell, nrx, B, nb, local, ctrl=True, max_cb=SISO_C, ce_rows=1) for _ in range(W)]
+    rx = rxs[0]
+    wbound = [[r.bind(src, 0, B, tb_major=True)] for r in rxs]  # TB0 code blocks contiguous in the pool (MAP probe)
+    bound = wbound[0][0]
     for _ in range(args.warmup):
-        rx.step(bound)
+        for r, wb in zip(rxs, wbound):
+            r.step(wb[0])
     lib().mi355_device_sync()
     barrier(pg, local)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        rx.step(bound)
+    run_workers(rxs, wbound, args.steps)
     lib().mi355_device_sync()
     barrier(pg, local)
     dt = max_over_ranks(pg, local, time.perf_counter() - t0)
     bits = rx.crc_bits(B).reshape(B, 2)[:, 0].copy()  # one TB per subframe
+    for r in rxs[1: min(W, args.steps)]:
+        bits &= r.crc_bits(B).reshape(B, 2)[:, 0]  # a TB counts only if every worker decoded it
     gathered = gather_bitmap(pg, local, bits)
-    ok_pay = int(sum_over_ranks(pg, local, rx.payload_ok(src, bound)))
+    ok_pay = int(sum_over_ranks(pg, local, min(r.payload_ok(src, wb[0]) for r, wb in zip(rxs[: max(1, min(W, args.steps))], wbound))))
     its = rx.avg_its(B) * 2  # the disabled second TB reads 0
     ok_tbs = int(gathered.sum()) if rank == 0 else 0
     mbps = whole_job_rate(world, B * SISO_TBS, args.steps, dt) / 1e6 * (ok_tbs / (B * world))
@@ -1031,7 +1048,7 @@ def run_siso(args, world, rank, local, pg):
                                   "test's UE locations, TBS 15840 (3 x K=5312), "
                                   + ("no noise (as phy_dl_test)" if args.siso_snr is None else f"{args.siso_snr:g} dB"),
                       "subframes_per_gpu_batch": B, "code_blocks_per_gpu_batch": SISO_C * B,
-                      "parallelism": f"dp{world}"},
+                      "workers_per_gpu": W, "parallelism": f"dp{world}"},
            "code_blocks_per_s": round(world * SISO_C * B * args.steps / dt, 1),
            "subframes_per_s": round(world * B * args.steps / dt, 1),
            "crc_ok_tbs": f"{ok_tbs}/{B * world}", "crc_bitmap": bitmap_summary(gathered, B * world) if rank == 0 else None,
@@ -1052,7 +1069,8 @@ def run_siso(args, world, rank, local, pg):
             res["cpu_baseline"] = cpu_baseline_pdsch(src, gb, its, args.cpu_seconds, ocfg_of=ocfg, K=SISO_K,
                                                      C=SISO_C, ntb=1, tbs=SISO_TBS, max_cb=SISO_C, S_max=S,
                                                      label="SISO QPSK")
-    rx.close()
+    for r in rxs:
+        r.close()
     src.close()
     return res
 
