@@ -94,7 +94,8 @@ def parse(argv=None):
     ap.add_argument("--workers", type=int, default=None,
                     help="pdsch / ue_dl: PHY worker threads, each with its own receive context (ue_dl, stream, "
                          "softbuffers) decoding every W-th batch (srsUE's sf_worker pool, 3 by default); 1 = one "
-                         "synchronous loop.  Default 3 for pdsch, 2 for ue_dl (measured best, profiles/r05/workers_ab.txt)")
+                         "synchronous loop.  Default 3 (measured best with one find_and_decode chunk per call, "
+                         "profiles/r05/workers_ab.txt, uedl_chunks_ab.txt)")
     ap.add_argument("--fanout", action="store_true",
                     help="batch fan-out: rank 0 holds every rank's I/Q and scatters the shards over RCCL each step "
                          "(pdsch / ue_dl / plumbing workloads); payload SHA-1s and CRC bitmaps gathered back")
@@ -102,7 +103,7 @@ def parse(argv=None):
     if args.subframes is None:
         args.subframes = 8192 if args.workload == "siso_qpsk" else 2048
     if args.workers is None:
-        args.workers = 2 if args.workload in ("ue_dl", "siso_qpsk") else 3
+        args.workers = 3
     return args
 
 
@@ -775,6 +776,12 @@ def run_pdsch(args, world, rank, local, pg):
     # synchronous calls (result read-back, next call's planning) overlaps the GPU work of the others
     W = max(1, args.workers) if not args.total_subframes else 1
     rxs = [rx] + [Tm4Rx(cell, B, local, ctrl) for _ in range(W - 1)]
+    if ctrl and W > 1:
+        # find_and_decode's two-chunk pipelining overlaps one call's host replay with its own GPU work; with several
+        # workers the other workers' batches fill those gaps, and one chunk saves the second chunk's launches
+        # (profiles/r05/uedl_chunks_ab.txt: 3 workers x 1 chunk 3.55 ms vs 2 x 2 3.86-3.90 ms per 2,048 subframes)
+        for r in rxs:
+            r.ue.set_chunks(1)
     dt_total, ok_sample, sample_tbs, bits_all, its_all, batches = 0.0, 0, 0, [], [], 0
     for s in range(nsets):
         a = lo + s * R
@@ -1017,6 +1024,9 @@ def run_siso(args, world, rank, local, pg):
     src.generate(lo, plans, args.siso_snr, args.seed, ctrl=True)
     W = max(1, args.workers)
     rxs = [synth.DlReceiver(cell, nrx, B, nb, local, ctrl=True, max_cb=SISO_C, ce_rows=1) for _ in range(W)]
+    if W > 1:  # one find_and_decode chunk per call with several workers (as run_pdsch)
+        for r in rxs:
+            r.ue.set_chunks(1)
     rx = rxs[0]
     wbound = [[r.bind(src, 0, B, tb_major=True)] for r in rxs]  # TB0 code blocks contiguous in the pool (MAP probe)
     bound = wbound[0][0]
