@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes as C
+import gc
 import hashlib
 import json
 import math
@@ -91,6 +92,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="wall budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="skip the per-stage and MAP-kernel probes (profiling runs)")
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="ue_dl / siso_qpsk: find_and_decode chunks per call (default: 1 with several workers, else "
+                         "the library's choice)")
     ap.add_argument("--workers", type=int, default=None,
                     help="pdsch / ue_dl: PHY worker threads, each with its own receive context (ue_dl, stream, "
                          "softbuffers) decoding every W-th batch (srsUE's sf_worker pool, 3 by default); 1 = one "
@@ -724,34 +728,104 @@ def config1_generic(local, budget_s=2.0, with_cpu=True):
     return res
 
 
-def run_workers(rxs, work, reps):
-    """reps steps over W receive contexts: rxs[w] decodes work[w] (its list of bound batches) on steps w, w + W, ...,
-    each on a host thread of its own (W = 1: this thread).  Every call is synchronous, so a worker's host work between
-    calls overlaps the others' GPU work (srsUE's sf_worker pool)."""
-    W = len(rxs)
-    if W == 1:
-        for _ in range(reps):
-            for b in work[0]:
-                rxs[0].step(b)
-        return
-    import threading
-    errs = []
+class PhyWorkers:
+    """srsUE's sf_worker pool (srsue/src/phy/phy.cc:135-189): one persistent host thread per receive context for the
+    whole run (W = 1: the calling thread), so the warm-up steps and the timed steps run on the same threads -- a
+    thread's first HIP calls carry one-off runtime setup (tens of ms, seen as the timed region's first calls when each
+    run started fresh threads).  run(work, reps): reps steps, rxs[w] decoding work[w] (its list of bound batches) on
+    steps w, w + W, ...; every call is synchronous, so a worker's host work between calls overlaps the others' GPU
+    work.  Returns each call's wall time (s).  The cyclic garbage collector is paused for the calls (as timeit does;
+    the caller collects before the warm-up): a full collection over torch's heap takes ~75 ms, 20 steps.  BENCH_CALL_TRACE=<file>: the last run's calls as (worker, start ms, end ms) JSON."""
 
-    def worker(w):
+    def __init__(self, rxs):
+        import threading
+        self.rxs, self.W = rxs, len(rxs)
+        self.job, self.errs, self.stop = None, [], False
+        # worker w starts its first call of a run w ms after worker 0, as srsUE's workers receive subframes one TTI
+        # apart: three threads entering their launch phases at the same instant stall each other inside the HIP
+        # runtime for 15-50 ms on some boxes (profiles/r05/stagger_ab.txt), once per run
+        self.stagger = float(os.environ.get("BENCH_STAGGER_MS", "1")) * 1e-3
+        self.go = threading.Barrier(self.W + 1) if self.W > 1 else None
+        self.done = threading.Barrier(self.W + 1) if self.W > 1 else None
+        self.th = [threading.Thread(target=self._loop, args=(w,), daemon=True) for w in range(self.W)] \
+            if self.W > 1 else []
+        for t in self.th:
+            t.start()
+
+    def _steps(self, w):
+        work, reps, calls = self.job
+        if w and self.stagger:
+            time.sleep(w * self.stagger)
+        for _ in range(w, reps, self.W):
+            for b in work[w]:
+                t = time.perf_counter()
+                self.rxs[w].step(b)
+                calls[w].append((t, time.perf_counter()))
+
+    def _loop(self, w):
+        while True:
+            self.go.wait()
+            if self.stop:
+                return
+            try:
+                self._steps(w)
+            except Exception as e:  # noqa: BLE001 -- re-raised on the calling thread
+                self.errs.append(e)
+            self.done.wait()
+
+    def run(self, work, reps):
+        calls = [[] for _ in range(self.W)]
+        self.job, self.errs = (work, reps, calls), []
+        gc.disable()
         try:
-            for _ in range(w, reps, W):
-                for b in work[w]:
-                    rxs[w].step(b)
-        except Exception as e:  # noqa: BLE001 -- re-raised on the main thread
-            errs.append(e)
+            if self.W == 1:
+                self._steps(0)
+            else:
+                self.go.wait()
+                self.done.wait()
+                if self.errs:
+                    raise self.errs[0]
+        finally:
+            gc.enable()
+        trace = os.environ.get("BENCH_CALL_TRACE")
+        if trace:
+            t0 = min((c[0][0] for c in calls if c), default=0.0)
+            with open(trace, "w") as f:
+                json.dump([[w, round((a - t0) * 1e3, 3), round((b - t0) * 1e3, 3)] for w, cw in enumerate(calls)
+                           for a, b in cw], f)
+        return [b - a for cw in calls for a, b in cw]
 
-    th = [threading.Thread(target=worker, args=(w,)) for w in range(W)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    if errs:
-        raise errs[0]
+    def close(self):
+        if self.th:
+            self.stop = True
+            self.go.wait()
+            for t in self.th:
+                t.join()
+            self.th = []
+
+
+def chunks_for(args, W):
+    """find_and_decode chunks per call: --chunks, else 1 with several PHY workers, else the library's default (0)"""
+    if args.chunks is not None:
+        return args.chunks
+    return 1 if W > 1 else 0
+
+
+def run_workers(rxs, work, reps):
+    """one run of a PhyWorkers pool over rxs (threads started and joined here)"""
+    pool = PhyWorkers(rxs)
+    try:
+        return pool.run(work, reps)
+    finally:
+        pool.close()
+
+
+def call_stats(calls):
+    """p50 / max of the timed calls' wall times (a step far above p50 is a host-side stall inside the timed region)"""
+    if not calls:
+        return None
+    a = np.sort(np.asarray(calls)) * 1e3
+    return {"calls": int(a.size), "p50_ms": round(float(a[a.size // 2]), 3), "max_ms": round(float(a[-1]), 3)}
 
 
 def run_pdsch(args, world, rank, local, pg):
@@ -776,12 +850,13 @@ def run_pdsch(args, world, rank, local, pg):
     # synchronous calls (result read-back, next call's planning) overlaps the GPU work of the others
     W = max(1, args.workers) if not args.total_subframes else 1
     rxs = [rx] + [Tm4Rx(cell, B, local, ctrl) for _ in range(W - 1)]
-    if ctrl and W > 1:
+    if ctrl and chunks_for(args, W):
         # find_and_decode's two-chunk pipelining overlaps one call's host replay with its own GPU work; with several
         # workers the other workers' batches fill those gaps, and one chunk saves the second chunk's launches
-        # (profiles/r05/uedl_chunks_ab.txt: 3 workers x 1 chunk 3.55 ms vs 2 x 2 3.86-3.90 ms per 2,048 subframes)
+        # (profiles/r05/uedl_chunks_ab.txt)
         for r in rxs:
-            r.ue.set_chunks(1)
+            r.ue.set_chunks(chunks_for(args, W))
+    pool = PhyWorkers(rxs)
     dt_total, ok_sample, sample_tbs, bits_all, its_all, batches = 0.0, 0, 0, [], [], 0
     for s in range(nsets):
         a = lo + s * R
@@ -791,11 +866,16 @@ def run_pdsch(args, world, rank, local, pg):
         bound = [rx.bind(src, k0, min(B, n - k0)) for k0 in range(0, n, B)]
         wbound = [bound] + [[r.bind(src, k0, min(B, n - k0)) for k0 in range(0, n, B)] for r in rxs[1:]]
         if s == 0 and bound:
-            for _ in range(args.warmup):
-                for r, wb in zip(rxs, wbound):
-                    r.step(wb[0])
+            gc.collect()  # before the warm-up: the timed steps follow it without an idle gap (a collection over
+            # torch's heap is ~75 ms, long enough for the GPU to drop its clocks)
+            if args.total_subframes:
+                for _ in range(args.warmup):
+                    rx.step(bound[0])
+            else:  # every worker warms up on its own thread
+                pool.run([wb[:1] for wb in wbound], args.warmup * W)
             lib().mi355_device_sync()
         reps = 1 if args.total_subframes else args.steps
+        calls = []
         barrier(pg, local)
         lib().mi355_device_sync()
         t0 = time.perf_counter()
@@ -805,7 +885,7 @@ def run_pdsch(args, world, rank, local, pg):
                     rx.step(b)
                     bits_all.append(rx.crc_bits(b[3]))
         else:
-            run_workers(rxs, wbound, reps)
+            calls = pool.run(wbound, reps)
         lib().mi355_device_sync()
         barrier(pg, local)
         dt_total += time.perf_counter() - t0
@@ -821,6 +901,7 @@ def run_pdsch(args, world, rank, local, pg):
                 for r, wb in zip(wk[1:], wbound[1:]):
                     b = b & r.crc_bits(wb[-1][3])  # a TB counts only if every worker decoded it
                 bits_all.append(b)
+    pool.close()
     dt = max_over_ranks(pg, local, dt_total)
     bits = np.concatenate(bits_all) if bits_all else np.zeros(0, np.uint8)
     gathered = gather_bitmap(pg, local, bits)
@@ -844,7 +925,7 @@ def run_pdsch(args, world, rank, local, pg):
         res.update({"value": round(mbps, 1), "unit": "Mbps", "steps": args.steps, "warmup": args.warmup,
                     "ms_per_step": round(dt / args.steps * 1e3, 3),
                     "code_blocks_per_s": round(world * 32 * B * args.steps / dt, 1),
-                    "subframes_per_s": round(world * B * args.steps / dt, 1)})
+                    "subframes_per_s": round(world * B * args.steps / dt, 1), "worker_calls": call_stats(calls)})
         nsf = world * B
     workload = (f"srslte_ue_dl chain from time-domain I/Q: {B} subframes/GPU/batch, 20 MHz (100 PRB), TM4 2x2 "
                 "spatial multiplexing, 2 codewords QAM256 TBS 97896 (C=16, K=6144), MMSE+CSI, max 10 half-its with "
@@ -1024,22 +1105,23 @@ def run_siso(args, world, rank, local, pg):
     src.generate(lo, plans, args.siso_snr, args.seed, ctrl=True)
     W = max(1, args.workers)
     rxs = [synth.DlReceiver(cell, nrx, B, nb, local, ctrl=True, max_cb=SISO_C, ce_rows=1) for _ in range(W)]
-    if W > 1:  # one find_and_decode chunk per call with several workers (as run_pdsch)
+    if chunks_for(args, W):  # one find_and_decode chunk per call with several workers (as run_pdsch)
         for r in rxs:
-            r.ue.set_chunks(1)
+            r.ue.set_chunks(chunks_for(args, W))
     rx = rxs[0]
     wbound = [[r.bind(src, 0, B, tb_major=True)] for r in rxs]  # TB0 code blocks contiguous in the pool (MAP probe)
     bound = wbound[0][0]
-    for _ in range(args.warmup):
-        for r, wb in zip(rxs, wbound):
-            r.step(wb[0])
+    pool = PhyWorkers(rxs)
+    gc.collect()  # before the warm-up, so the timed steps follow it without an idle gap (as run_pdsch)
+    pool.run(wbound, args.warmup * W)  # every worker warms up on its own thread
     lib().mi355_device_sync()
     barrier(pg, local)
     t0 = time.perf_counter()
-    run_workers(rxs, wbound, args.steps)
+    calls = pool.run(wbound, args.steps)
     lib().mi355_device_sync()
     barrier(pg, local)
     dt = max_over_ranks(pg, local, time.perf_counter() - t0)
+    pool.close()
     bits = rx.crc_bits(B).reshape(B, 2)[:, 0].copy()  # one TB per subframe
     for r in rxs[1: min(W, args.steps)]:
         bits &= r.crc_bits(B).reshape(B, 2)[:, 0]  # a TB counts only if every worker decoded it
@@ -1051,7 +1133,8 @@ def run_siso(args, world, rank, local, pg):
     res = {"metric": "PDSCH decoded Mbps + code-blocks/sec, 20 MHz SISO QPSK MCS 9 (configs[2], phy_dl_test -p 100 "
                      "-t 1 -m 9)",
            "value": round(mbps, 1), "unit": "Mbps", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-           "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+           "ms_per_step": round(dt / args.steps * 1e3, 3), "worker_calls": call_stats(calls),
+           "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "fp32+int16", "data": "synthetic",
            "config": {"workload": f"phy_dl_test -p 100 -t 1 -m 9 work_ue as mi355_ue_dl_find_and_decode_batch: {B} "
                                   "subframes/GPU/batch from time-domain I/Q, 1 port / 1 rx, CFI 1, DCI format 1 at the "

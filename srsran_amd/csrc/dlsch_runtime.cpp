@@ -951,11 +951,11 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
       if (pend->host) (void)hipHostFree(pend->host);
       pend->host = nullptr;
       pend->cap  = 0;
-      CHECK_HIP(hipHostMalloc((void**)&pend->host, bytes + bytes / 2 + 4096, hipHostMallocDefault));
+      CHECK_HIP(stage_host_alloc((void**)&pend->host, bytes + bytes / 2 + 4096));
       pend->cap = bytes + bytes / 2 + 4096;
     }
     if (!pend->ev) CHECK_HIP(hipEventCreateWithFlags(&pend->ev, hipEventDisableTiming));
-    CHECK_HIP(hipMemcpyAsync(pend->host, d_ret, bytes, hipMemcpyDeviceToHost, s));
+    CHECK_HIP(stage_copy(pend->host, d_ret, bytes, s));
     CHECK_HIP(hipEventRecord(pend->ev, s));
     pend->invalid.resize(ntb);
     for (uint32_t t = 0; t < ntb; t++) pend->invalid[t] = tbd[t].invalid ? 1 : 0;
@@ -970,7 +970,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
   }
   if (hook.fn) hook.fn(hook.ctx);
   CHECK_HIP(q->back.reserve(rnd(ntb * 4) + ntb * 4));
-  CHECK_HIP(hipMemcpyAsync(q->back.host, d_ret, rnd(ntb * 4) + ntb * 4, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(stage_copy(q->back.host, d_ret, rnd(ntb * 4) + ntb * 4, s));
   CHECK_HIP(hipStreamSynchronize(s));
   memcpy(ret, q->back.host, ntb * 4);
   for (uint32_t t = 0; t < ntb; t++) {

@@ -1,12 +1,15 @@
-// srsran_amd/csrc/host_staging.h -- pinned host staging for the per-call descriptor uploads.  Descriptors are
-// packed into one page-locked buffer and sent with a single asynchronous copy (pageable copies are staged
-// synchronously by the runtime and dominate the host side of a batch call).  The buffer is refilled only
-// after the previous upload from it has completed (event), so asynchronous callers are safe too.
+// srsran_amd/csrc/host_staging.h -- pinned host staging for the per-call descriptor uploads and result read-backs.
+// Descriptors are packed into one page-locked, fine-grained buffer and moved by one stage_copy kernel on the
+// staging's own stream (stage_copy.h: no copy-engine submission, which can block a calling thread with several
+// workers).  The buffer is refilled only after the previous upload from it has completed (event), so asynchronous
+// callers are safe too.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <stddef.h>
 #include <string.h>
+
+#include "stage_copy.h"
 
 namespace mi355 {
 
@@ -40,7 +43,7 @@ struct HostStaging {
     host = nullptr;
     cap  = 0;
     const size_t c = bytes + bytes / 4 + 4096;
-    hipError_t   e = hipHostMalloc((void**)&host, c, hipHostMallocDefault);
+    hipError_t   e = stage_host_alloc((void**)&host, c);
     if (e == hipSuccess) cap = c;
     return e;
   }
@@ -66,11 +69,11 @@ struct HostStaging {
     used += (n + 255) / 256 * 256;
     return p;
   }
-  // one asynchronous copy of everything put so far to dst, ordered before the work enqueued on s after this
-  // call.  The copy runs on the staging's own stream, so it does not wait behind s's earlier kernels (the
-  // destination must not be in use by them: callers upload into per-call descriptor space) -- unless after_s:
-  // then it waits for them (the destination may still be read by work of an earlier call left in flight), or only
-  // for the event after (recorded by the caller after the last reader of the destination).
+  // one copy of everything put so far to dst, ordered before the work enqueued on s after this call.  The copy runs
+  // on the staging's own stream, so it does not wait behind s's earlier kernels (the destination must not be in use
+  // by them: callers upload into per-call descriptor space) -- unless after_s: then it waits for them (the
+  // destination may still be read by work of an earlier call left in flight), or only for the event after (recorded
+  // by the caller after the last reader of the destination).
   hipError_t upload(void* dst, hipStream_t s, bool after_s = false, hipEvent_t after = nullptr)
   {
     if (!used) return hipSuccess;
@@ -83,7 +86,7 @@ struct HostStaging {
       if (!sev && (e = hipEventCreateWithFlags(&sev, hipEventDisableTiming)) != hipSuccess) return e;
       if ((e = hipEventRecord(sev, s)) != hipSuccess || (e = hipStreamWaitEvent(cs, sev, 0)) != hipSuccess) return e;
     }
-    if ((e = hipMemcpyAsync(dst, host, used, hipMemcpyHostToDevice, cs)) != hipSuccess) return e;
+    if ((e = stage_copy(dst, host, used, cs)) != hipSuccess) return e;
     if ((e = hipEventRecord(ev, cs)) != hipSuccess) return e;
     pending = true;
     return hipStreamWaitEvent(s, ev, 0);

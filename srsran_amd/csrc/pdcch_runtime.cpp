@@ -192,11 +192,10 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
     // chunk (and to the PDSCH the caller enqueues) without device-to-host copies in its queue
     CHECK_HIP(hipEventRecord(kev[c], s));
     CHECK_HIP(hipStreamWaitEvent(rb, kev[c], 0));
-    CHECK_HIP(hipMemcpyAsync(back->host + 4 * (size_t)o, d_cfi + o, 4 * (size_t)m, hipMemcpyDeviceToHost, rb));
-    CHECK_HIP(hipMemcpyAsync(back->host + b_cfi + 12 * (size_t)o, d_corr + 3 * (size_t)o, 12 * (size_t)m,
-                             hipMemcpyDeviceToHost, rb));
-    CHECK_HIP(hipMemcpyAsync(back->host + b_cfi + b_corr + (size_t)o * sizeof(DciHits), d_hits + o,
-                             (size_t)m * sizeof(DciHits), hipMemcpyDeviceToHost, rb));
+    CHECK_HIP(stage_copy(back->host + 4 * (size_t)o, d_cfi + o, 4 * (size_t)m, rb));
+    CHECK_HIP(stage_copy(back->host + b_cfi + 12 * (size_t)o, d_corr + 3 * (size_t)o, 12 * (size_t)m, rb));
+    CHECK_HIP(stage_copy(back->host + b_cfi + b_corr + (size_t)o * sizeof(DciHits), d_hits + o,
+                         (size_t)m * sizeof(DciHits), rb));
     CHECK_HIP(hipEventRecord(ev[c], rb));
   }
   last_n = n, last_stride = stride, last_llr = d_llr, last_cand = d_cand;

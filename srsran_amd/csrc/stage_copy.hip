@@ -1,0 +1,73 @@
+// srsran_amd/csrc/stage_copy.hip -- the hot path's host <-> device transfers as plain kernels on the caller's stream.
+//
+// The per-call descriptor uploads and result read-backs are small (hundreds of bytes to ~1 MB).  As
+// hipMemcpyAsync calls they go to the SDMA engines, and with several PHY worker threads issuing them at once a
+// thread can block inside hipMemcpyAsync until well after the GPU has gone idle (15-50 ms, every thread of the pool
+// at once: profiles/r05/sdma_ab.txt, the HIP API trace in profiles/r05/worker_stall.txt).  A kernel that reads or
+// writes the page-locked, fine-grained staging buffer directly over the host link is ordered on the stream like any
+// other launch, so nothing on the host waits for a copy engine.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "stage_copy.h"
+
+namespace mi355 {
+
+namespace {
+
+constexpr uint32_t SC_THREADS = 256;
+
+// n16 16-byte pieces, SC_U per lane in flight (a host-link read is microseconds away), then the tail bytes
+// [16 * n16, n) one by one (thread 0 of block 0)
+constexpr uint32_t SC_U = 4;
+__global__ __launch_bounds__(SC_THREADS) void stage_copy16(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                           size_t n16, size_t n)
+{
+  const size_t stride = (size_t)gridDim.x * SC_THREADS;
+  for (size_t i0 = (size_t)blockIdx.x * SC_THREADS + threadIdx.x; i0 < n16; i0 += SC_U * stride) {
+    uint4 v[SC_U];
+#pragma unroll
+    for (uint32_t u = 0; u < SC_U; u++)
+      if (i0 + u * stride < n16) v[u] = src[i0 + u * stride];
+#pragma unroll
+    for (uint32_t u = 0; u < SC_U; u++)
+      if (i0 + u * stride < n16) dst[i0 + u * stride] = v[u];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (size_t b = 16 * n16; b < n; b++) ((uint8_t*)dst)[b] = ((const uint8_t*)src)[b];
+}
+
+// unaligned pointers: 4-byte words when both are 4-aligned, else bytes
+__global__ __launch_bounds__(SC_THREADS) void stage_copy4(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
+                                                          size_t n4, size_t n)
+{
+  const size_t stride = (size_t)gridDim.x * SC_THREADS;
+  for (size_t i = (size_t)blockIdx.x * SC_THREADS + threadIdx.x; i < n4; i += stride) dst[i] = src[i];
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (size_t b = 4 * n4; b < n; b++) ((uint8_t*)dst)[b] = ((const uint8_t*)src)[b];
+}
+
+} // namespace
+
+hipError_t stage_copy(void* dst, const void* src, size_t bytes, hipStream_t s)
+{
+  if (!bytes) return hipSuccess;
+  const uintptr_t a = (uintptr_t)dst | (uintptr_t)src;
+  if ((a & 15) == 0) {
+    const size_t n16 = bytes / 16;
+    // up to 128 workgroups x SC_U pieces per lane in flight (128 K requests: enough to cover the host link's latency)
+    const uint32_t g =
+        (uint32_t)std::min<size_t>(128, std::max<size_t>(1, (n16 + SC_U * SC_THREADS - 1) / (SC_U * SC_THREADS)));
+    hipLaunchKernelGGL(stage_copy16, dim3(g), dim3(SC_THREADS), 0, s, (uint4*)dst, (const uint4*)src, n16, bytes);
+  } else {
+    const size_t   n4 = (a & 3) == 0 ? bytes / 4 : 0;
+    const uint32_t g  = (uint32_t)std::min<size_t>(64, std::max<size_t>(1, (n4 + SC_THREADS - 1) / SC_THREADS));
+    hipLaunchKernelGGL(stage_copy4, dim3(g), dim3(SC_THREADS), 0, s, (uint32_t*)dst, (const uint32_t*)src, n4, bytes);
+  }
+  return hipGetLastError();
+}
+
+} // namespace mi355

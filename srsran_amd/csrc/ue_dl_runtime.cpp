@@ -449,7 +449,7 @@ static int chest_finish(mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const
   const size_t       nout = (size_t)njobs * P * R * CHEST_OUT;
   CHECK_HIP(q->back.reserve(nout * 4));
   const float* out = (const float*)q->back.host;
-  CHECK_HIP(hipMemcpyAsync(q->back.host, d_out, nout * 4, hipMemcpyDeviceToHost, s));
+  CHECK_HIP(stage_copy(q->back.host, d_out, nout * 4, s));
   CHECK_HIP(hipStreamSynchronize(s));
   for (uint32_t i = 0; i < njobs; i++) fill_res(q, cfg, &out[(size_t)i * R * P * CHEST_OUT], jobs[i], &res[i]);
   return MI355_SUCCESS;
@@ -486,7 +486,7 @@ static int chest_finish_async(mi355_ue_dl_t* q, ChestFill* f, const float* d_out
   f->out = (const float*)q->back.host;
   CHECK_HIP(hipEventRecord(q->ev_chest, s));
   CHECK_HIP(hipStreamWaitEvent(q->side, q->ev_chest, 0));
-  CHECK_HIP(hipMemcpyAsync(q->back.host, d_out, nout * 4, hipMemcpyDeviceToHost, q->side));
+  CHECK_HIP(stage_copy(q->back.host, d_out, nout * 4, q->side));
   return MI355_SUCCESS;
 }
 
