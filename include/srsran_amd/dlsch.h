@@ -56,6 +56,9 @@ int mi355_softbuffer_pool_data(mi355_softbuffer_pool_t* p, uint8_t** data, uint3
 int mi355_softbuffer_get_cb_crc(mi355_softbuffer_pool_t* p, uint32_t sb, uint8_t* cb_crc, void* stream);
 /* The same copy enqueued on stream without waiting: cb_crc is valid once the caller has synchronised the stream. */
 int mi355_softbuffer_get_cb_crc_async(mi355_softbuffer_pool_t* p, uint32_t sb, uint8_t* cb_crc, void* stream);
+/* device address of softbuffer sb's per-code-block CRC flags (max_cb bytes; valid until the pool is destroyed), for
+ * callers that read them back with their own copy */
+int mi355_softbuffer_cb_crc_dev(mi355_softbuffer_pool_t* p, uint32_t sb, const uint8_t** d_cb_crc);
 typedef struct {
   uint32_t tbs;         /* transport block size in bits (grant.tb[i].tbs) */
   uint32_t nof_e_bits;  /* coded LLRs of the codeword (grant.tb[i].nof_bits) */

@@ -491,6 +491,13 @@ int mi355_softbuffer_get_cb_crc_async(mi355_softbuffer_pool_t* p, uint32_t sb, u
   return MI355_SUCCESS;
 }
 
+int mi355_softbuffer_cb_crc_dev(mi355_softbuffer_pool_t* p, uint32_t sb, const uint8_t** d_cb_crc)
+{
+  if (!p || !d_cb_crc || sb >= p->nof_sb) return MI355_ERROR_INVALID_INPUTS;
+  *d_cb_crc = p->cb_crc + (size_t)sb * p->max_cb;
+  return MI355_SUCCESS;
+}
+
 int mi355_dlsch_create(mi355_dlsch_t** q, int device)
 {
   if (!q) return MI355_ERROR_INVALID_INPUTS;

@@ -58,13 +58,13 @@ hipError_t stage_copy(void* dst, const void* src, size_t bytes, hipStream_t s)
   const uintptr_t a = (uintptr_t)dst | (uintptr_t)src;
   if ((a & 15) == 0) {
     const size_t n16 = bytes / 16;
-    // up to 128 workgroups x SC_U pieces per lane in flight (128 K requests: enough to cover the host link's latency)
-    const uint32_t g =
-        (uint32_t)std::min<size_t>(128, std::max<size_t>(1, (n16 + SC_U * SC_THREADS - 1) / (SC_U * SC_THREADS)));
+    // one piece per lane up to 1,024 workgroups (a CU keeps only so many host-link reads in flight: spreading a copy
+    // over more CUs gets it done in fewer round trips), SC_U per lane beyond
+    const uint32_t g = (uint32_t)std::min<size_t>(1024, std::max<size_t>(1, (n16 + SC_THREADS - 1) / SC_THREADS));
     hipLaunchKernelGGL(stage_copy16, dim3(g), dim3(SC_THREADS), 0, s, (uint4*)dst, (const uint4*)src, n16, bytes);
   } else {
     const size_t   n4 = (a & 3) == 0 ? bytes / 4 : 0;
-    const uint32_t g  = (uint32_t)std::min<size_t>(64, std::max<size_t>(1, (n4 + SC_THREADS - 1) / SC_THREADS));
+    const uint32_t g  = (uint32_t)std::min<size_t>(1024, std::max<size_t>(1, (n4 + SC_THREADS - 1) / SC_THREADS));
     hipLaunchKernelGGL(stage_copy4, dim3(g), dim3(SC_THREADS), 0, s, (uint32_t*)dst, (const uint32_t*)src, n4, bytes);
   }
   return hipGetLastError();

@@ -30,6 +30,8 @@
 #include "srsran_amd/srslte_tdec.h"
 #include "srsran_amd/ue_dl.h"
 
+#include "../csrc/stage_copy.h"
+
 #define DROPIN_ERR(...) fprintf(stderr, "[srslte_mi355] " __VA_ARGS__)
 // SRSLTE_MI355_TRACE=1: one stderr line per entry point (integration debugging)
 #define TRACE()                                                                                                        \
@@ -345,7 +347,7 @@ struct PinnedBuf {
     if (p) (void)hipHostFree(p);
     p   = nullptr;
     cap = 0;
-    if (hipHostMalloc(&p, n) != hipSuccess) return -1;
+    if (mi355::stage_host_alloc(&p, n) != hipSuccess) return -1; // (read and written by stage_copy kernels)
     cap = n;
     return 0;
   }
@@ -474,11 +476,14 @@ int pdsch_decode_dev(srslte_pdsch_t* q, PdschState* st, hipStream_t stream, srsl
     return SRSLTE_ERROR;
   }
   uint8_t* hp = (uint8_t*)st->h_payload.p;
-  bool     ok = hipMemcpyAsync(hp, st->d_payload, pay_total, hipMemcpyDeviceToHost, stream) == hipSuccess;
+  // (copy kernels on the stream, not hipMemcpyAsync: copy-engine submissions from several PHY workers at once can
+  // block their threads, profiles/r05/worker_stall.txt)
+  bool     ok = mi355::stage_copy(hp, st->d_payload, pay_total, stream) == hipSuccess;
   for (int t = 0; t < SRSLTE_MAX_CODEWORDS && ok; t++) {
     if (!run[t]) continue;
-    ok = mi355_softbuffer_get_cb_crc_async(A.pool, (uint32_t)A.slot_of(cfg->softbuffers.rx[t]), hp + pay_total + t * A.max_cb,
-                                           stream) == MI355_SUCCESS;
+    const uint8_t* dcrc = nullptr;
+    ok = mi355_softbuffer_cb_crc_dev(A.pool, (uint32_t)A.slot_of(cfg->softbuffers.rx[t]), &dcrc) == MI355_SUCCESS &&
+         mi355::stage_copy(hp + pay_total + t * A.max_cb, dcrc, A.max_cb, stream) == hipSuccess;
   }
   if (mi355_pdsch_decode_collect(st->rx) != MI355_SUCCESS || !ok) return SRSLTE_ERROR;
   if (hipStreamSynchronize(stream) != hipSuccess) return SRSLTE_ERROR;
@@ -612,12 +617,11 @@ int ue_fft_estimate(srslte_ue_dl_t* q, srslte_dl_sf_cfg_t* sf, srslte_ue_dl_cfg_
     for (uint32_t p = 0; p < q->cell.nof_ports; p++) job.ce[p][r] = st->d_ce[p][r];
   }
   if (nstaged == st->nof_rx) {
-    if (hipMemcpyAsync(st->d_in[0], st->h_in.p, nin * st->nof_rx, hipMemcpyHostToDevice, st->stream) != hipSuccess)
-      return SRSLTE_ERROR;
+    if (mi355::stage_copy(st->d_in[0], st->h_in.p, nin * st->nof_rx, st->stream) != hipSuccess) return SRSLTE_ERROR;
   } else {
     for (uint32_t r = 0; r < st->nof_rx; r++)
       if (job.in_buffer[r] == st->d_in[r] &&
-          hipMemcpyAsync(st->d_in[r], (char*)st->h_in.p + r * nin, nin, hipMemcpyHostToDevice, st->stream) != hipSuccess)
+          mi355::stage_copy(st->d_in[r], (char*)st->h_in.p + r * nin, nin, st->stream) != hipSuccess)
         return SRSLTE_ERROR;
   }
   mi355_chest_dl_cfg_t ccfg = chest_cfg_to_mi355(cfg->chest_cfg, sf->tti);
@@ -653,7 +657,7 @@ int ue_fft_estimate(srslte_ue_dl_t* q, srslte_dl_sf_cfg_t* sf, srslte_ue_dl_cfg_
   bool back = false;
   if (st->host_grids) {
     const size_t nb = (size_t)st->grid_len * 2 * sizeof(float) * st->nof_rx * (1 + q->cell.nof_ports);
-    if (hipMemcpyAsync(st->h_block, st->d_grid[0], nb, hipMemcpyDeviceToHost, st->side) != hipSuccess)
+    if (mi355::stage_copy(st->h_block, st->d_grid[0], nb, st->side) != hipSuccess)
       return SRSLTE_ERROR;
     back = true;
   }
@@ -1028,7 +1032,7 @@ int srslte_pdsch_decode(srslte_pdsch_t*        q,
         ce[k - 1][r] = d;
     }
   // the staged host buffers go up in one copy
-  if (k_stage && hipMemcpyAsync(st->d_stage, st->h_stage.p, k_stage * bytes, hipMemcpyHostToDevice, st->stream) != hipSuccess)
+  if (k_stage && mi355::stage_copy(st->d_stage, st->h_stage.p, k_stage * bytes, st->stream) != hipSuccess)
     return SRSLTE_ERROR;
   const int ret = pdsch_decode_dev(q, st, st->stream, sf, cfg, channel->noise_estimate, grids, ce, data);
   if (cfg->meas_time_en) {
@@ -1064,7 +1068,7 @@ int srslte_ue_dl_init(srslte_ue_dl_t* q, cf_t* in_buffer[SRSLTE_MAX_PORTS], uint
   // q->sf_symbols[4] and chest_res.ce[4][4] (ue_dl.c:66-120, srslte_chest_dl_res_init) as slots of one zeroed pinned
   // block: 20 buffers of sflen_re, 4 spare for set_cell's relayout
   st->h_slot = sflen_re;
-  err        = hipHostMalloc((void**)&st->h_block, ue_block_slots() * sflen_re * sizeof(cf_t)) != hipSuccess;
+  err        = mi355::stage_host_alloc((void**)&st->h_block, ue_block_slots() * sflen_re * sizeof(cf_t)) != hipSuccess;
   if (!err) {
     memset(st->h_block, 0, ue_block_slots() * sflen_re * sizeof(cf_t));
     ue_point_buffers(q, st, 0, 0, 0);
