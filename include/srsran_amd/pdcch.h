@@ -197,6 +197,20 @@ int mi355_ue_dl_find_dl_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* sfj
                                   const mi355_chest_dl_res_t* chest, uint32_t njobs, mi355_ctrl_res_t* ctrl,
                                   mi355_dci_dl_t* dci, void* stream);
 
+/* srslte_ue_dl_decode_fft_estimate followed by the control-channel stage of mi355_ue_dl_find_dl_dci_batch in one
+ * call (the reference's decode_fft_estimate runs the PCFICH / PDCCH estimation itself, ue_dl.c:348-381): the noise
+ * estimate stays on the device between them, so the only host wait before the blind-search replay is the
+ * control read-back.  chest[] is filled as by decode_fft_estimate_batch, sfs / ctrl / dci as by find_dl_dci_batch.
+ * after_estimate(hook_arg), when given, is called once the estimator's kernels are enqueued on stream (before the
+ * control kernels): a caller's read-back of the grids / estimates enqueued there overlaps the control channels.
+ * Synchronous. */
+typedef void (*mi355_hook_fn)(void* arg);
+int mi355_ue_dl_fft_estimate_find_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* sfjobs, mi355_dl_sf_cfg_t* sfs,
+                                            const mi355_ue_dl_cfg_t* cfgs, const uint16_t* rntis,
+                                            const mi355_chest_dl_cfg_t* chest_cfg, mi355_chest_dl_res_t* chest,
+                                            uint32_t njobs, mi355_ctrl_res_t* ctrl, mi355_dci_dl_t* dci,
+                                            mi355_hook_fn after_estimate, void* hook_arg, void* stream);
+
 /* srslte_ue_dl_find_and_decode for a batch: OFDM + estimation + control channels + DCI -> grant + PDSCH decode.
  * cfgs[i].grant is overwritten from the first DCI found (its rnti / softbuffers / decoder fields are the
  * caller's); res[2*i + tb] as mi355_pdsch_decode_batch for subframes with a DCI (ret = 1 there, as the

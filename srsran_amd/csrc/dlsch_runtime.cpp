@@ -478,7 +478,7 @@ int mi355_softbuffer_get_cb_crc(mi355_softbuffer_pool_t* p, uint32_t sb, uint8_t
   CHECK_HIP(hipSetDevice(p->device));
   hipStream_t s = (hipStream_t)stream;
   CHECK_HIP(hipMemcpyAsync(cb_crc, p->cb_crc + (size_t)sb * p->max_cb, p->max_cb, hipMemcpyDeviceToHost, s));
-  CHECK_HIP(hipStreamSynchronize(s));
+  CHECK_HIP(wait_stream(s));
   return MI355_SUCCESS;
 }
 
@@ -627,7 +627,7 @@ int mi355::DlschPending::collect()
 {
   if (!armed) return MI355_SUCCESS;
   armed = false;
-  CHECK_HIP(hipEventSynchronize(ev));
+  CHECK_HIP(wait_event(ev));
   memcpy(ret, host, ntb * 4);
   for (uint32_t t = 0; t < ntb; t++) {
     if (invalid[t]) ret[t] = MI355_ERROR_INVALID_INPUTS;
@@ -978,7 +978,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
   if (hook.fn) hook.fn(hook.ctx);
   CHECK_HIP(q->back.reserve(rnd(ntb * 4) + ntb * 4));
   CHECK_HIP(stage_copy(q->back.host, d_ret, rnd(ntb * 4) + ntb * 4, s));
-  CHECK_HIP(hipStreamSynchronize(s));
+  CHECK_HIP(wait_stream(s));
   memcpy(ret, q->back.host, ntb * 4);
   for (uint32_t t = 0; t < ntb; t++) {
     if (tbd[t].invalid) ret[t] = MI355_ERROR_INVALID_INPUTS;

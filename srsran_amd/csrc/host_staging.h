@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "stage_copy.h"
@@ -34,7 +35,7 @@ struct HostStaging {
   {
     if (pending) {
       pending      = false;
-      hipError_t e = hipEventSynchronize(ev);
+      hipError_t e = wait_event(ev);
       if (e != hipSuccess) return e;
     }
     used = 0;
@@ -74,12 +75,28 @@ struct HostStaging {
   // by them: callers upload into per-call descriptor space) -- unless after_s: then it waits for them (the
   // destination may still be read by work of an earlier call left in flight), or only for the event after (recorded
   // by the caller after the last reader of the destination).
+  // Uploads up to STAGE_INLINE bytes (a few subframes' descriptors: srsUE's per-TTI calls) are copied in line on s
+  // instead: there is nothing of s's to overlap with on that scale, and the copy stream's two event hops cost more
+  // than the copy.
+  // (MI355_STAGE_INLINE=<bytes>: another threshold, 0 = always the copy stream; A/B timing)
+  static size_t inline_limit()
+  {
+    static const size_t v = getenv("MI355_STAGE_INLINE") ? (size_t)atoll(getenv("MI355_STAGE_INLINE")) : (64u << 10);
+    return v;
+  }
   hipError_t upload(void* dst, hipStream_t s, bool after_s = false, hipEvent_t after = nullptr)
   {
     if (!used) return hipSuccess;
     hipError_t e = hipSuccess;
-    if (!cs && (e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking)) != hipSuccess) return e;
     if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (used <= inline_limit()) {
+      if (after && (e = hipStreamWaitEvent(s, after, 0)) != hipSuccess) return e;
+      if ((e = stage_copy(dst, host, used, s)) != hipSuccess) return e;
+      if ((e = hipEventRecord(ev, s)) != hipSuccess) return e;
+      pending = true;
+      return hipSuccess;
+    }
+    if (!cs && (e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking)) != hipSuccess) return e;
     if (after) {
       if ((e = hipStreamWaitEvent(cs, after, 0)) != hipSuccess) return e;
     } else if (after_s) {

@@ -192,10 +192,11 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
     // chunk (and to the PDSCH the caller enqueues) without device-to-host copies in its queue
     CHECK_HIP(hipEventRecord(kev[c], s));
     CHECK_HIP(hipStreamWaitEvent(rb, kev[c], 0));
-    CHECK_HIP(stage_copy(back->host + 4 * (size_t)o, d_cfi + o, 4 * (size_t)m, rb));
-    CHECK_HIP(stage_copy(back->host + b_cfi + 12 * (size_t)o, d_corr + 3 * (size_t)o, 12 * (size_t)m, rb));
-    CHECK_HIP(stage_copy(back->host + b_cfi + b_corr + (size_t)o * sizeof(DciHits), d_hits + o,
-                         (size_t)m * sizeof(DciHits), rb));
+    const StageSeg segs[3] = {
+        {back->host + 4 * (size_t)o, d_cfi + o, (uint32_t)(4 * m)},
+        {back->host + b_cfi + 12 * (size_t)o, d_corr + 3 * (size_t)o, (uint32_t)(12 * m)},
+        {back->host + b_cfi + b_corr + (size_t)o * sizeof(DciHits), d_hits + o, (uint32_t)(m * sizeof(DciHits))}};
+    CHECK_HIP(stage_copy_multi(segs, 3, rb));
     CHECK_HIP(hipEventRecord(ev[c], rb));
   }
   last_n = n, last_stride = stride, last_llr = d_llr, last_cand = d_cand;
@@ -206,7 +207,7 @@ int CtrlState::finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_c
                       mi355_dci_msg_t* msgs)
 {
   if (chunk >= chunk_end.size()) return MI355_ERROR_INVALID_INPUTS;
-  CHECK_HIP(hipEventSynchronize(ev[chunk]));
+  CHECK_HIP(wait_event(ev[chunk]));
   static const bool prof = getenv("MI355_HOST_PROF") != nullptr;
   const auto        tr0  = std::chrono::steady_clock::now();
   const uint32_t    b    = chunk ? chunk_end[chunk - 1] : 0, e = chunk_end[chunk];
@@ -229,7 +230,7 @@ int CtrlState::finish(uint32_t chunk, const uint16_t* rntis, const mi355_ue_dl_c
     for (size_t k = 0; k < ovf_of.size(); k++)
       CHECK_HIP(hipMemcpyAsync(ovf.data() + k * NC, last_cand + (size_t)ovf_of[k] * NC, NC * sizeof(DciCand),
                                hipMemcpyDeviceToHost, rb));
-    CHECK_HIP(hipStreamSynchronize(rb));
+    CHECK_HIP(wait_stream(rb));
   }
   host_parallel_for(e - b, 128, [&](uint32_t lo, uint32_t hi) { // subframes are independent
     DciCand cand[NC];

@@ -602,7 +602,7 @@ int mi355_pdsch_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, uint32
   }
   int r = run_frontend(q, jobs, plans, s);
   if (r) return r;
-  CHECK_HIP(hipStreamSynchronize(s));
+  CHECK_HIP(wait_stream(s));
   q->last = plans;
   return MI355_SUCCESS;
 }

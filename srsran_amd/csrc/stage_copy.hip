@@ -50,7 +50,45 @@ __global__ __launch_bounds__(SC_THREADS) void stage_copy4(uint32_t* __restrict__
     for (size_t b = 4 * n4; b < n; b++) ((uint8_t*)dst)[b] = ((const uint8_t*)src)[b];
 }
 
+struct StageSegs {
+  StageSeg seg[STAGE_MAX_SEGS];
+};
+
+// workgroup (x, y): pieces of segment y; 16-byte pieces when the segment allows them, else 4-byte words, else bytes
+__global__ __launch_bounds__(SC_THREADS) void stage_copy_segs(StageSegs a)
+{
+  const StageSeg  g      = a.seg[blockIdx.y];
+  const size_t    stride = (size_t)gridDim.x * SC_THREADS, t0 = (size_t)blockIdx.x * SC_THREADS + threadIdx.x;
+  const uintptr_t al     = (uintptr_t)g.dst | (uintptr_t)g.src;
+  size_t          done   = 0;
+  if ((al & 15) == 0) {
+    const size_t n16 = g.bytes / 16;
+    for (size_t i = t0; i < n16; i += stride) ((uint4*)g.dst)[i] = ((const uint4*)g.src)[i];
+    done = 16 * n16;
+  } else if ((al & 3) == 0) {
+    const size_t n4 = g.bytes / 4;
+    for (size_t i = t0; i < n4; i += stride) ((uint32_t*)g.dst)[i] = ((const uint32_t*)g.src)[i];
+    done = 4 * n4;
+  }
+  for (size_t b = done + t0; b < g.bytes; b += stride) ((uint8_t*)g.dst)[b] = ((const uint8_t*)g.src)[b];
+}
+
 } // namespace
+
+hipError_t stage_copy_multi(const StageSeg* segs, int n, hipStream_t s)
+{
+  if (n <= 0) return hipSuccess;
+  if (n > STAGE_MAX_SEGS) return hipErrorInvalidValue;
+  StageSegs a{};
+  size_t    most = 0;
+  for (int k = 0; k < n; k++) {
+    a.seg[k] = segs[k];
+    most     = std::max<size_t>(most, segs[k].bytes);
+  }
+  const uint32_t g = (uint32_t)std::min<size_t>(1024, std::max<size_t>(1, (most / 16 + SC_THREADS - 1) / SC_THREADS));
+  hipLaunchKernelGGL(stage_copy_segs, dim3(g, n), dim3(SC_THREADS), 0, s, a);
+  return hipGetLastError();
+}
 
 hipError_t stage_copy(void* dst, const void* src, size_t bytes, hipStream_t s)
 {

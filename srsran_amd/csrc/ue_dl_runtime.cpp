@@ -450,7 +450,7 @@ static int chest_finish(mi355_ue_dl_t* q, const mi355_chest_dl_cfg_t* cfg, const
   CHECK_HIP(q->back.reserve(nout * 4));
   const float* out = (const float*)q->back.host;
   CHECK_HIP(stage_copy(q->back.host, d_out, nout * 4, s));
-  CHECK_HIP(hipStreamSynchronize(s));
+  CHECK_HIP(wait_stream(s));
   for (uint32_t i = 0; i < njobs; i++) fill_res(q, cfg, &out[(size_t)i * R * P * CHEST_OUT], jobs[i], &res[i]);
   return MI355_SUCCESS;
 }
@@ -471,7 +471,7 @@ struct ChestFill {
 static void chest_fill_cb(void* p)
 {
   ChestFill* f = (ChestFill*)p;
-  if (f->done || hipStreamSynchronize(f->q->side) != hipSuccess) return; // the read-back has landed
+  if (f->done || wait_stream(f->q->side) != hipSuccess) return; // the read-back has landed
   const uint32_t k = f->q->cell.nof_ports * f->q->nof_rx * CHEST_OUT;
   for (uint32_t i = 0; i < f->njobs; i++) fill_res(f->q, f->cfg, &f->out[(size_t)i * k], f->jobs[i], &f->res[i]);
   f->done = true;
@@ -600,7 +600,7 @@ int mi355_ofdm_rx_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_
   hipStream_t s = stream ? (hipStream_t)stream : q->own;
   int         r = ofdm_run(q, jobs, njobs, s);
   if (r) return r;
-  CHECK_HIP(hipStreamSynchronize(s));
+  CHECK_HIP(wait_stream(s));
   return MI355_SUCCESS;
 }
 
@@ -667,7 +667,7 @@ int mi355_ue_dl_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, co
   r = pdsch_decode_batch_dev_noise(q->pdsch, pool, jobs.data(), njobs, res, s, d_noise, WaitHook{chest_fill_cb, &fill},
                                    chest_cfg->estimator_alg == MI355_ESTIMATOR_ALG_AVERAGE);
   const auto t2 = now();
-  CHECK_HIP(hipStreamSynchronize(q->side));
+  CHECK_HIP(wait_stream(q->side));
   if (r) return r;
   if (!fill.done) chest_fill_cb(&fill); // no DL-SCH work in the batch: the hook did not run
   if (prof) {
@@ -753,6 +753,38 @@ int mi355_ue_dl_find_dl_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* sfj
     return r;
   for (uint32_t i = 0; i < njobs; i++) sfs[i].cfi = ctrl[i].cfi;
   return unpack_all(q, sfs, cfgs, njobs, ctrl, msgs.get(), dci);
+}
+
+int mi355_ue_dl_fft_estimate_find_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* sfjobs, mi355_dl_sf_cfg_t* sfs,
+                                            const mi355_ue_dl_cfg_t* cfgs, const uint16_t* rntis,
+                                            const mi355_chest_dl_cfg_t* chest_cfg, mi355_chest_dl_res_t* chest,
+                                            uint32_t njobs, mi355_ctrl_res_t* ctrl, mi355_dci_dl_t* dci,
+                                            mi355_hook_fn after_estimate, void* hook_arg, void* stream)
+{
+  if (!q || !chest_cfg || (njobs && (!sfjobs || !sfs || !cfgs || !rntis || !chest || !ctrl || !dci)))
+    return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t s = stream ? (hipStream_t)stream : q->own;
+  int         r = ctrl_ready(q);
+  if (r) return r;
+  size_t used = 0;
+  if ((r = ofdm_run(q, sfjobs, njobs, s, &used))) return r;
+  float *d_out = nullptr, *d_noise = nullptr;
+  if ((r = chest_launch_only(q, sfjobs, njobs, chest_cfg, s, used, &d_out, &d_noise))) return r;
+  // the estimator's results go back on the side stream while the control channels run
+  ChestFill fill{q, chest_cfg, nullptr, sfjobs, njobs, chest, false};
+  if ((r = chest_finish_async(q, &fill, d_out, s))) return r;
+  if (after_estimate) after_estimate(hook_arg);
+  if (q->fd_msgs.size() < (size_t)njobs * MI355_MAX_DCI_MSG) q->fd_msgs.resize((size_t)njobs * MI355_MAX_DCI_MSG);
+  mi355_dci_msg_t* const msgs = q->fd_msgs.data();
+  q->ctrl->ce_row = 0; // every row of the estimates is written here: read where they lie
+  r = q->ctrl->run(sfjobs, nullptr, d_noise, rntis, cfgs, njobs, s, ctrl, msgs);
+  chest_fill_cb(&fill); // (also after a failed control stage: the estimation itself succeeded)
+  if (r) return r;
+  if (!fill.done) return MI355_ERROR;
+  for (uint32_t i = 0; i < njobs; i++) sfs[i].cfi = ctrl[i].cfi;
+  return unpack_all(q, sfs, cfgs, njobs, ctrl, msgs, dci);
 }
 
 int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, const mi355_dl_sf_job_t* sfjobs,
@@ -923,7 +955,7 @@ int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t*
     Chunk& C = ck[c];
     for (size_t k = 0; k < C.jobs.size(); k++) res[2 * C.which[k]] = C.sub[2 * k], res[2 * C.which[k] + 1] = C.sub[2 * k + 1];
   }
-  CHECK_HIP(hipStreamSynchronize(q->side));
+  CHECK_HIP(wait_stream(q->side));
   if (!fill.done) chest_fill_cb(&fill);
   const auto t3 = now();
   if (prof) {

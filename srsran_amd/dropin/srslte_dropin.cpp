@@ -478,15 +478,18 @@ int pdsch_decode_dev(srslte_pdsch_t* q, PdschState* st, hipStream_t stream, srsl
   uint8_t* hp = (uint8_t*)st->h_payload.p;
   // (copy kernels on the stream, not hipMemcpyAsync: copy-engine submissions from several PHY workers at once can
   // block their threads, profiles/r05/worker_stall.txt)
-  bool     ok = mi355::stage_copy(hp, st->d_payload, pay_total, stream) == hipSuccess;
+  mi355::StageSeg segs[1 + SRSLTE_MAX_CODEWORDS] = {{hp, st->d_payload, (uint32_t)pay_total}};
+  int             nseg = 1;
+  bool            ok   = true;
   for (int t = 0; t < SRSLTE_MAX_CODEWORDS && ok; t++) {
     if (!run[t]) continue;
     const uint8_t* dcrc = nullptr;
-    ok = mi355_softbuffer_cb_crc_dev(A.pool, (uint32_t)A.slot_of(cfg->softbuffers.rx[t]), &dcrc) == MI355_SUCCESS &&
-         mi355::stage_copy(hp + pay_total + t * A.max_cb, dcrc, A.max_cb, stream) == hipSuccess;
+    ok = mi355_softbuffer_cb_crc_dev(A.pool, (uint32_t)A.slot_of(cfg->softbuffers.rx[t]), &dcrc) == MI355_SUCCESS;
+    segs[nseg++] = {hp + pay_total + t * A.max_cb, dcrc, (uint32_t)A.max_cb};
   }
+  ok = ok && mi355::stage_copy_multi(segs, nseg, stream) == hipSuccess; // the payloads and the CB flags, one launch
   if (mi355_pdsch_decode_collect(st->rx) != MI355_SUCCESS || !ok) return SRSLTE_ERROR;
-  if (hipStreamSynchronize(stream) != hipSuccess) return SRSLTE_ERROR;
+  if (mi355::wait_stream(stream) != hipSuccess) return SRSLTE_ERROR;
   for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++) {
     if (!run[t]) continue;
     memcpy(data[t].payload, hp + pay_off[t], pay_len[t]);
@@ -523,6 +526,7 @@ struct UeDlState {
   cf_t*          h_block  = nullptr;
   size_t         h_slot   = 0; // complex samples per buffer as allocated (max_prb)
   hipStream_t    side     = nullptr;
+  hipEvent_t     ev_est   = nullptr; // the estimator's kernels done (the side stream's read-back waits for it)
   // last estimate and control-stage outcome
   bool                 est_valid = false;
   uint32_t             est_tti   = 0;
@@ -538,6 +542,7 @@ struct UeDlState {
     if (ue) mi355_ue_dl_destroy(ue);
     if (d_mem) (void)hipFree(d_mem);
     if (side) (void)hipStreamDestroy(side);
+    if (ev_est) (void)hipEventDestroy(ev_est);
     if (stream) {
       arena_forget_stream(stream);
       (void)hipStreamDestroy(stream);
@@ -589,6 +594,29 @@ int ue_run_ctrl(srslte_ue_dl_t* q, UeDlState* st, srslte_dl_sf_cfg_t* sf, const 
   return SRSLTE_SUCCESS;
 }
 
+// srslte_chest_dl_res_t scalars of the last estimate
+void fill_chest_res(srslte_ue_dl_t* q, const UeDlState* st)
+{
+  srslte_chest_dl_res_t& R = q->chest_res;
+  const auto&            c = st->chest;
+  R.nof_re                 = c.nof_re;
+  R.noise_estimate         = c.noise_estimate;
+  R.noise_estimate_dbm     = c.noise_estimate_dbm;
+  R.snr_db                 = c.snr_db;
+  memcpy(R.snr_ant_port_db, c.snr_ant_port_db, sizeof(R.snr_ant_port_db));
+  R.rsrp       = c.rsrp;
+  R.rsrp_dbm   = c.rsrp_dbm;
+  R.rsrp_neigh = c.rsrp_neigh;
+  memcpy(R.rsrp_port_dbm, c.rsrp_port_dbm, sizeof(R.rsrp_port_dbm));
+  memcpy(R.rsrp_ant_port_dbm, c.rsrp_ant_port_dbm, sizeof(R.rsrp_ant_port_dbm));
+  R.rsrq    = c.rsrq;
+  R.rsrq_db = c.rsrq_db;
+  memcpy(R.rsrq_ant_port_db, c.rsrq_ant_port_db, sizeof(R.rsrq_ant_port_db));
+  R.rssi_dbm   = c.rssi_dbm;
+  R.cfo        = c.cfo;
+  R.sync_error = c.sync_error;
+}
+
 int ue_fft_estimate(srslte_ue_dl_t* q, srslte_dl_sf_cfg_t* sf, srslte_ue_dl_cfg_t* cfg, cf_t* const* input)
 {
   UeDlState* st = ue_state(q);
@@ -627,44 +655,55 @@ int ue_fft_estimate(srslte_ue_dl_t* q, srslte_dl_sf_cfg_t* sf, srslte_ue_dl_cfg_
   mi355_chest_dl_cfg_t ccfg = chest_cfg_to_mi355(cfg->chest_cfg, sf->tti);
   st->est_valid             = false;
   st->ctrl_valid            = false;
-  if (mi355_ue_dl_decode_fft_estimate_batch(st->ue, &job, 1, &ccfg, &st->chest, st->stream) != MI355_SUCCESS)
-    return SRSLTE_ERROR;
+  // OFDM, estimation and the PCFICH / PDCCH stage of the UE's RNTI (estimate_pdcch_pcfich, ue_dl.c:348-381) in one
+  // call, the noise estimate kept on the device; the host copies of the grid and the estimates (the reference's
+  // q->sf_symbols / chest_res.ce are host buffers: the grids and the estimates are consecutive in d_mem and in the
+  // pinned block the caller's pointers are slots of, srslte_ue_dl_set_cell) are read back on the side stream while
+  // the control channels run, enqueued by the hook once the estimator's kernels are
+  struct Back {
+    UeDlState* st;
+    size_t     nb;
+    bool       ok, armed;
+  } bk{st, (size_t)st->grid_len * 2 * sizeof(float) * st->nof_rx * (1 + q->cell.nof_ports), true, false};
+  auto hook = [](void* p) {
+    Back*      b  = (Back*)p;
+    UeDlState* us = b->st;
+    b->ok = (us->ev_est || hipEventCreateWithFlags(&us->ev_est, hipEventDisableTiming) == hipSuccess) &&
+            hipEventRecord(us->ev_est, us->stream) == hipSuccess && hipStreamWaitEvent(us->side, us->ev_est, 0) == hipSuccess &&
+            mi355::stage_copy(us->h_block, us->d_grid[0], b->nb, us->side) == hipSuccess;
+    b->armed = true;
+  };
+  mi355_dl_sf_cfg_t msf{sf->tti, sf->cfi};
+  mi355_ue_dl_cfg_t ucfg = ue_cfg_to_mi355(*cfg);
+  const uint16_t    rnti = q->pregen_rnti ? q->pregen_rnti : (uint16_t)SRSLTE_SIRNTI;
+  // (MI355_DROPIN_TWO_STEP=1: the former two calls, for A/B timing)
+  static const bool two_step = getenv("MI355_DROPIN_TWO_STEP") && atoi(getenv("MI355_DROPIN_TWO_STEP")) != 0;
+  const int         rf       = two_step ? MI355_ERROR
+                                        : mi355_ue_dl_fft_estimate_find_dci_batch(st->ue, &job, &msf, &ucfg, &rnti, &ccfg,
+                                                                                  &st->chest, 1, &st->ctrl, st->dci,
+                                                                                  st->host_grids ? +hook : nullptr, &bk,
+                                                                                  st->stream);
+  if (bk.armed && mi355::wait_stream(st->side) != hipSuccess) return SRSLTE_ERROR;
+  if (rf != MI355_SUCCESS || !bk.ok) {
+    // which half failed is not known here: the two-step form reports it as the reference would
+    if (mi355_ue_dl_decode_fft_estimate_batch(st->ue, &job, 1, &ccfg, &st->chest, st->stream) != MI355_SUCCESS)
+      return SRSLTE_ERROR;
+    st->est_valid = true;
+    st->est_tti   = sf->tti;
+    fill_chest_res(q, st);
+    if (st->host_grids && (mi355::stage_copy(st->h_block, st->d_grid[0], bk.nb, st->side) != hipSuccess ||
+                           mi355::wait_stream(st->side) != hipSuccess))
+      return SRSLTE_ERROR;
+    return ue_run_ctrl(q, st, sf, cfg, q->pregen_rnti) == SRSLTE_SUCCESS ? SRSLTE_SUCCESS : SRSLTE_ERROR;
+  }
   st->est_valid = true;
   st->est_tti   = sf->tti;
-  // srslte_chest_dl_res_t scalars
-  srslte_chest_dl_res_t& R = q->chest_res;
-  const auto&            c = st->chest;
-  R.nof_re                 = c.nof_re;
-  R.noise_estimate         = c.noise_estimate;
-  R.noise_estimate_dbm     = c.noise_estimate_dbm;
-  R.snr_db                 = c.snr_db;
-  memcpy(R.snr_ant_port_db, c.snr_ant_port_db, sizeof(R.snr_ant_port_db));
-  R.rsrp       = c.rsrp;
-  R.rsrp_dbm   = c.rsrp_dbm;
-  R.rsrp_neigh = c.rsrp_neigh;
-  memcpy(R.rsrp_port_dbm, c.rsrp_port_dbm, sizeof(R.rsrp_port_dbm));
-  memcpy(R.rsrp_ant_port_dbm, c.rsrp_ant_port_dbm, sizeof(R.rsrp_ant_port_dbm));
-  R.rsrq    = c.rsrq;
-  R.rsrq_db = c.rsrq_db;
-  memcpy(R.rsrq_ant_port_db, c.rsrq_ant_port_db, sizeof(R.rsrq_ant_port_db));
-  R.rssi_dbm   = c.rssi_dbm;
-  R.cfo        = c.cfo;
-  R.sync_error = c.sync_error;
-  // host copies of the grid and the estimates (the reference's q->sf_symbols / chest_res.ce are host buffers): the
-  // grids and the estimates are consecutive in d_mem and in the pinned block the caller's pointers are slots of
-  // (srslte_ue_dl_set_cell), so one read-back fills them, on the side stream while the control channels run (the
-  // estimation above has completed: decode_fft_estimate_batch returns after it)
-  bool back = false;
-  if (st->host_grids) {
-    const size_t nb = (size_t)st->grid_len * 2 * sizeof(float) * st->nof_rx * (1 + q->cell.nof_ports);
-    if (mi355::stage_copy(st->h_block, st->d_grid[0], nb, st->side) != hipSuccess)
-      return SRSLTE_ERROR;
-    back = true;
-  }
-  // PCFICH (CFI into sf->cfi) and the PDCCH candidates of the UE's RNTI (estimate_pdcch_pcfich, ue_dl.c:348-381)
-  const int rc = ue_run_ctrl(q, st, sf, cfg, q->pregen_rnti);
-  if (back && hipStreamSynchronize(st->side) != hipSuccess) return SRSLTE_ERROR;
-  return rc == SRSLTE_SUCCESS ? SRSLTE_SUCCESS : SRSLTE_ERROR;
+  fill_chest_res(q, st);
+  sf->cfi        = msf.cfi;
+  st->ctrl_valid = true;
+  st->ctrl_rnti  = rnti;
+  st->ctrl_cfg   = ucfg;
+  return SRSLTE_SUCCESS;
 }
 
 } // namespace
