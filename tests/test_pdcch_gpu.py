@@ -115,22 +115,10 @@ def _make_dci(D, cell, fmt, mcs, rnti):
     return d
 
 
-@pytest.mark.parametrize("full", [False, True], ids=["hits", "full_readback"])
-@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_find_and_decode_end_to_end(case, full, monkeypatch):
-    """Subframes synthesised with the product's eNodeB-side encoders (DCI pack, PCFICH / PDCCH, PDSCH) through a
-    frequency-selective channel; mi355_ue_dl_find_and_decode_batch must find exactly the transmitted DCI at its
-    UE-specific candidate, derive the transmitted grant and decode every TB with CRC ok.  The control-channel
-    LLRs and blind-search result are checked bit-exactly against the oracle on the GPU's own grids.
-    full: the replay reads every subframe's whole candidate array (the overflow path of the compact per-subframe
-    hit records, pdcch_runtime.cpp) instead of the records."""
-    if full:
-        monkeypatch.setenv("MI355_PDCCH_HMAX", "0")
+def _ctrl_subframes(case):
+    """The control-channel cases' subframes: (cell, rnti, subs, expect), see test_find_and_decode_end_to_end"""
     from srsran_amd import pdcch as D
     from srsran_amd import pdsch as S
-    from srsran_amd.dlsch import SoftbufferPool
-    from srsran_amd.tdec import DeviceBuffer
-    from srsran_amd.ue_dl import UeDl, default_chest_cfg
     from pdsch_jobs import DevIqSubframe
     name, nprb, ports, nrx, tm, fmt, mcs, alt, cid = case
     rng = np.random.default_rng(len(name) * 7 + nprb)
@@ -164,6 +152,26 @@ def test_find_and_decode_end_to_end(case, full, monkeypatch):
         iq, payload, _h, _s2 = uc.synth_iq(cfg, rng, snr_db=snr, ctrl=ctrl, channel=chan)
         subs.append(DevIqSubframe(cfg, iq, softbuffers=(2 * len(subs), 2 * len(subs) + 1)))
         expect.append((cfg, payload, g, m))
+    return cell, rnti, subs, expect
+
+
+@pytest.mark.parametrize("full", [False, True], ids=["hits", "full_readback"])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_find_and_decode_end_to_end(case, full, monkeypatch):
+    """Subframes synthesised with the product's eNodeB-side encoders (DCI pack, PCFICH / PDCCH, PDSCH) through a
+    frequency-selective channel; mi355_ue_dl_find_and_decode_batch must find exactly the transmitted DCI at its
+    UE-specific candidate, derive the transmitted grant and decode every TB with CRC ok.  The control-channel
+    LLRs and blind-search result are checked bit-exactly against the oracle on the GPU's own grids.
+    full: the replay reads every subframe's whole candidate array (the overflow path of the compact per-subframe
+    hit records, pdcch_runtime.cpp) instead of the records."""
+    if full:
+        monkeypatch.setenv("MI355_PDCCH_HMAX", "0")
+    from srsran_amd import pdcch as D
+    from srsran_amd import pdsch as S
+    from srsran_amd.dlsch import SoftbufferPool
+    from srsran_amd.ue_dl import UeDl, default_chest_cfg
+    name, nprb, ports, nrx, tm, fmt, mcs, alt, cid = case
+    cell, rnti, subs, expect = _ctrl_subframes(case)
     ue = UeDl(cell, nrx)
     pool = SoftbufferPool(2 * len(subs), max_cb=32)
     ucfg = D.UeDlCfg()
@@ -268,4 +276,48 @@ def test_blind_search_two_dcis(common_ss):
         found = P.find_dl_dci(o_llr, rg.nof_cce(cfi), sf_idx, rnti, nprb, ports, tm=tm, dci_common_ss=common_ss)
         assert [(f["format"], f["L"], f["ncce"]) for f in found] == [(d.format, d.location.L, d.location.ncce)
                                                                      for d in dcis[i]]
+    ue.close()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_fft_estimate_find_dci_matches_two_calls(case):
+    """mi355_ue_dl_fft_estimate_find_dci_batch (the drop-in's srslte_ue_dl_decode_fft_estimate: estimation and the
+    PCFICH / PDCCH stage in one call, noise kept on the device) gives exactly what decode_fft_estimate_batch followed
+    by find_dl_dci_batch gives on the same subframes: estimator results, CFIs, control results and DCIs; the hook
+    runs once, between the two stages."""
+    import ctypes as C
+
+    from srsran_amd import pdcch as D
+    from srsran_amd.ue_dl import ChestRes, DlSfJob, UeDl, default_chest_cfg
+    name, nprb, ports, nrx, tm, fmt, mcs, alt, cid = case
+    cell, rnti, subs, expect = _ctrl_subframes(case)
+    jobs = [s.sfjob for s in subs]
+    n = len(jobs)
+    ucfg = D.UeDlCfg()
+    ucfg.tm, ucfg.use_tbs_index_alt = tm, int(alt)
+    ue = UeDl(cell, nrx)
+    chest_a = ue.fft_estimate(jobs, default_chest_cfg())
+    cfis_a, ctrl_a, dcis_a = D.find_dl_dci(ue, jobs, [rnti] * n, [ucfg] * n, chest_a)
+    L = D._declare()
+    hook_t = C.CFUNCTYPE(None, C.c_void_p)
+    calls = []
+    hook = hook_t(lambda arg: calls.append(arg))
+    L.mi355_ue_dl_fft_estimate_find_dci_batch.argtypes = [
+        C.c_void_p, C.POINTER(DlSfJob), C.POINTER(D.DlSfCfg), C.POINTER(D.UeDlCfg), C.POINTER(C.c_uint16),
+        C.c_void_p, C.POINTER(ChestRes), C.c_uint32, C.POINTER(D.CtrlRes), C.POINTER(D.DciDl), hook_t, C.c_void_p,
+        C.c_void_p]
+    sfs = (D.DlSfCfg * n)(*[D.DlSfCfg(j.tti, 0) for j in jobs])
+    chest_b, ctrl_b = (ChestRes * n)(), (D.CtrlRes * n)()
+    dci_b = (D.DciDl * (n * D.MAX_DCI_MSG))()
+    cc = default_chest_cfg()
+    assert L.mi355_ue_dl_fft_estimate_find_dci_batch(ue.h, (DlSfJob * n)(*jobs), sfs, (D.UeDlCfg * n)(*([ucfg] * n)),
+                                                     (C.c_uint16 * n)(*([rnti] * n)), C.addressof(cc), chest_b, n,
+                                                     ctrl_b, dci_b, hook, 1234, None) == 0
+    assert calls == [1234]
+    assert bytes(chest_b) == bytes(chest_a)
+    assert [sfs[i].cfi for i in range(n)] == list(cfis_a) == [e[0].cfi for e in expect]
+    assert bytes(ctrl_b) == bytes(ctrl_a)
+    for i in range(n):
+        got = [bytes(dci_b[i * D.MAX_DCI_MSG + k]) for k in range(max(0, ctrl_b[i].nof_dci))]
+        assert got == [bytes(d) for d in dcis_a[i]] and len(got) == 1, (name, i)
     ue.close()
