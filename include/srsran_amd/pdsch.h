@@ -160,6 +160,10 @@ int mi355_pdsch_set_llr_8bit(mi355_pdsch_t* q, int enable);
 /* Run only the symbol-level front-end (extraction .. CSI weighting) of a job list, no DL-SCH decode. */
 int mi355_pdsch_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, uint32_t njobs, void* stream);
 
+/* measurement: enable = 1 arms pdsch_eq_rm's per-workgroup phase counters (zeroed), 0 disarms; out (nullable, 4 u64):
+ * workgroups, and the sums of their prologue, equaliser and rate-dematching shader cycles since arming */
+int mi355_pdsch_eqrm_profile(int enable, uint64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,6 +91,7 @@ struct EqRmPool {
   uint8_t*       fresh;
   int            sparse; // fresh buffers: parity rows without an LLR are left unwritten (SB_ROWMASK, rm_image.h)
   int            diag = 0; // measurement only (MI355_EQRM_DIAG): 1 = no rate dematching, 2 = no equalisation (wrong results)
+  unsigned long long* prof = nullptr; // measurement only (mi355_pdsch_eqrm_profile): per-workgroup phase cycle sums
 };
 hipError_t pdsch_launch_eq_rm(const PdschJobDev* jobs, const EqRmJob* rj, uint32_t njobs, uint32_t max_c, uint32_t img,
                               const uint32_t* keys, uint32_t nkeys, const EqRmPool& pool, hipStream_t s);

@@ -1025,6 +1025,13 @@ constexpr int      ER_R       = (3 * (6144 + 32) + 12 + 8 * ER_THREADS * ER_Q - 
 constexpr int      ER_Q2      = 3; // quads per round when both layers share a pass
 constexpr int      ER_R2      = (3 * (6144 + 32) + 12 + 8 * ER_THREADS * ER_Q2 - 1) / (8 * ER_THREADS * ER_Q2);
 
+__device__ __forceinline__ uint4 ldg_u4(const GLB uint32_t* p)
+{
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u        v = *(const GLB v4u*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ uint32_t add_pairs16(uint32_t a, uint32_t b) // two wrapping int16 additions
 {
   return ((a + b) & 0xffffu) | (((a >> 16) + (b >> 16)) << 16);
@@ -1081,6 +1088,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     fresh[l] = need[l] && P.fresh[slot[l]] != 0;
   }
   if (!need[0] && !need[1]) return;
+  const unsigned long long pt0 = P.prof ? clock64() : 0ull; // (phase profile: P.prof only)
   // the slots' parity-row bitmaps (rm_image.h; E <= N here): the old ones (rows they leave undefined are read as zero
   // by a combining write), the new ones (a fresh buffer's rows without an LLR are not written, P.sparse)
   __shared__ uint32_t obm[2][2 * SB_ROWMASK_WORDS], nbm[2][2 * SB_ROWMASK_WORDS];
@@ -1106,6 +1114,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     cmb[tid] = cwd[tid].csi_enable ? *gptr(cwd[tid].cmax_final) : 0u;
   }
   __syncthreads();
+  const unsigned long long pt1 = P.prof ? clock64() : 0ull;
   // equalise the RE pairs overlapping the span; keep the span's LLRs
   const float         noise = J.noise_dev ? *gptr(J.noise_dev) : J.noise;
   const uint32_t      row = J.row, magic = J.row_magic, rmask = J.rhob_mask;
@@ -1123,11 +1132,11 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   if constexpr (ER_TPF) {
     if (lean) {
       const uint32_t  npairs = R.layer[0].buflen[kx0] / 2;
-      const uint32_t* inv32  = (const uint32_t*)R.layer[0].inv[kx0];
+      const GLB uint32_t* inv32 = (const GLB uint32_t*)gptr(R.layer[0].inv[kx0]);
 #pragma unroll
       for (int k = 0; k < ER_Q; k++) {
         const uint32_t i = 4 * (tid + k * ER_THREADS);
-        iv0[k]           = i + 3 < npairs ? *(const uint4*)(inv32 + i)
+        iv0[k]           = i + 3 < npairs ? ldg_u4(inv32 + i)
                                           : make_uint4(i < npairs ? inv32[i] : 0xffffffffu,
                                                        i + 1 < npairs ? inv32[i + 1] : 0xffffffffu,
                                                        i + 2 < npairs ? inv32[i + 2] : 0xffffffffu, 0xffffffffu);
@@ -1186,6 +1195,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   }
   if (tid < 2) imgs[tid * img + n_e] = 0; // the zero slot: table entries without an LLR (RM_NONE, >= n_e) read it
   __syncthreads();
+  const unsigned long long pt2 = P.prof ? clock64() : 0ull;
   if (P.diag == 1) {
     if (imgs[tid] == 12345 && imgs[img + tid] == 777) P.sb[tid] = 1; // keep the equaliser's work alive
     return;
@@ -1196,9 +1206,9 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     if (lean) {
       // the usual case, two fresh buffers: every position is written, a missing LLR reads the zero slot
       const uint32_t  npairs = R.layer[0].buflen[kx0] / 2, Kc = (R.layer[0].N[kx0] - 12) / 3;
-      const uint32_t* inv32  = (const uint32_t*)R.layer[0].inv[kx0];
-      uint32_t*       sb[2]  = {(uint32_t*)(P.sb + (size_t)slot[0] * P.sb_stride),
-                                (uint32_t*)(P.sb + (size_t)slot[1] * P.sb_stride)};
+      const GLB uint32_t* inv32 = (const GLB uint32_t*)gptr(R.layer[0].inv[kx0]);
+      GLB uint32_t*   sb[2]  = {(GLB uint32_t*)gptr(P.sb + (size_t)slot[0] * P.sb_stride),
+                                (GLB uint32_t*)gptr(P.sb + (size_t)slot[1] * P.sb_stride)};
       const bool      al     = (((uintptr_t)sb[0] | (uintptr_t)sb[1]) & 15) == 0;
       const uint16_t* a0     = (const uint16_t*)imgs;
       const uint16_t* a1     = (const uint16_t*)(imgs + img);
@@ -1212,7 +1222,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
             iv[k] = iv0[k];
             continue;
           }
-          iv[k]            = i + 3 < npairs ? *(const uint4*)(inv32 + i)
+          iv[k]            = i + 3 < npairs ? ldg_u4(inv32 + i)
                                             : make_uint4(i < npairs ? inv32[i] : 0xffffffffu,
                                                          i + 1 < npairs ? inv32[i + 1] : 0xffffffffu,
                                                          i + 2 < npairs ? inv32[i + 2] : 0xffffffffu, 0xffffffffu);
@@ -1232,8 +1242,8 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
           }
           typedef uint32_t u4v __attribute__((ext_vector_type(4)));
           if (al && i + 3 < npairs) {
-            __builtin_nontemporal_store((u4v){v0[0], v0[1], v0[2], v0[3]}, (u4v*)(sb[0] + i));
-            __builtin_nontemporal_store((u4v){v1[0], v1[1], v1[2], v1[3]}, (u4v*)(sb[1] + i));
+            __builtin_nontemporal_store((u4v){v0[0], v0[1], v0[2], v0[3]}, (GLB u4v*)(sb[0] + i));
+            __builtin_nontemporal_store((u4v){v1[0], v1[1], v1[2], v1[3]}, (GLB u4v*)(sb[1] + i));
           } else {
 #pragma unroll
             for (int cc = 0; cc < 4; cc++)
@@ -1245,9 +1255,9 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     } else if (need[0] && need[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
                R.layer[0].buflen[kx0] == R.layer[1].buflen[kx1]) {
       const uint32_t  npairs = R.layer[0].buflen[kx0] / 2, Kc = (R.layer[0].N[kx0] - 12) / 3;
-      const uint32_t* inv32  = (const uint32_t*)R.layer[0].inv[kx0];
-      uint32_t*       sb[2]  = {(uint32_t*)(P.sb + (size_t)slot[0] * P.sb_stride),
-                                (uint32_t*)(P.sb + (size_t)slot[1] * P.sb_stride)};
+      const GLB uint32_t* inv32 = (const GLB uint32_t*)gptr(R.layer[0].inv[kx0]);
+      GLB uint32_t*   sb[2]  = {(GLB uint32_t*)gptr(P.sb + (size_t)slot[0] * P.sb_stride),
+                                (GLB uint32_t*)gptr(P.sb + (size_t)slot[1] * P.sb_stride)};
       const bool      al     = (((uintptr_t)sb[0] | (uintptr_t)sb[1]) & 15) == 0;
 #pragma unroll 1
       for (int rd = 0; rd < ER_R2; rd++) {
@@ -1255,7 +1265,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
 #pragma unroll
         for (int k = 0; k < ER_Q2; k++) {
           const uint32_t i = 4 * (tid + (rd * ER_Q2 + k) * ER_THREADS);
-          iv[k]            = i + 3 < npairs ? *(const uint4*)(inv32 + i)
+          iv[k]            = i + 3 < npairs ? ldg_u4(inv32 + i)
                                             : make_uint4(i < npairs ? inv32[i] : 0xffffffffu,
                                                          i + 1 < npairs ? inv32[i + 1] : 0xffffffffu,
                                                          i + 2 < npairs ? inv32[i + 2] : 0xffffffffu, 0xffffffffu);
@@ -1264,7 +1274,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
             if (fresh[l] || i >= npairs) {
               old[l][k] = make_uint4(0u, 0u, 0u, 0u);
             } else if (al && i + 3 < npairs) {
-              old[l][k] = *(const uint4*)(sb[l] + i);
+              old[l][k] = ldg_u4(sb[l] + i);
             } else {
               old[l][k] = make_uint4(sb[l][i], i + 1 < npairs ? sb[l][i + 1] : 0u, i + 2 < npairs ? sb[l][i + 2] : 0u,
                                      i + 3 < npairs ? sb[l][i + 3] : 0u);
@@ -1300,7 +1310,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
           for (int l = 0; l < 2; l++) {
             if (al && i + 3 < npairs) {
               typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-              __builtin_nontemporal_store((u4v){v[l][0], v[l][1], v[l][2], v[l][3]}, (u4v*)(sb[l] + i));
+              __builtin_nontemporal_store((u4v){v[l][0], v[l][1], v[l][2], v[l][3]}, (GLB u4v*)(sb[l] + i));
             } else {
 #pragma unroll
               for (int cc = 0; cc < 4; cc++)
@@ -1318,9 +1328,9 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     const EqRmLayer& T      = R.layer[l];
     const uint32_t   kx     = c < T.C1 ? 0u : 1u;
     const uint32_t   npairs = T.buflen[kx] / 2, Kc = (T.N[kx] - 12) / 3;
-    const uint32_t*  inv32  = (const uint32_t*)T.inv[kx];
+    const GLB uint32_t* inv32 = (const GLB uint32_t*)gptr(T.inv[kx]);
     const uint16_t*  acc    = (const uint16_t*)(imgs + l * img);
-    uint32_t*        sb     = (uint32_t*)(P.sb + (size_t)slot[l] * P.sb_stride);
+    GLB uint32_t*    sb     = (GLB uint32_t*)gptr(P.sb + (size_t)slot[l] * P.sb_stride);
     const bool       sb16   = ((uintptr_t)sb & 15) == 0;
 #pragma unroll 1
     for (int rd = 0; rd < ER_R; rd++) {
@@ -1328,14 +1338,14 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
 #pragma unroll
     for (int k = 0; k < ER_Q; k++) {
       const uint32_t i = 4 * (tid + (rd * ER_Q + k) * ER_THREADS);
-      iv[k]            = i + 3 < npairs ? *(const uint4*)(inv32 + i)
+      iv[k]            = i + 3 < npairs ? ldg_u4(inv32 + i)
                                         : make_uint4(i < npairs ? inv32[i] : 0xffffffffu,
                                                      i + 1 < npairs ? inv32[i + 1] : 0xffffffffu,
                                                      i + 2 < npairs ? inv32[i + 2] : 0xffffffffu, 0xffffffffu);
       if (fresh[l]) {
         old[k] = make_uint4(0u, 0u, 0u, 0u);
       } else if (sb16 && i + 3 < npairs) {
-        old[k] = *(const uint4*)(sb + i);
+        old[k] = ldg_u4(sb + i);
       } else {
         old[k] = make_uint4(i < npairs ? sb[i] : 0u, i + 1 < npairs ? sb[i + 1] : 0u, i + 2 < npairs ? sb[i + 2] : 0u,
                             i + 3 < npairs ? sb[i + 3] : 0u);
@@ -1361,7 +1371,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
       if (!any) continue; // nothing to add to an old buffer
       if (sb16 && i + 3 < npairs) {
         typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-        __builtin_nontemporal_store((u4v){v[0], v[1], v[2], v[3]}, (u4v*)(sb + i));
+        __builtin_nontemporal_store((u4v){v[0], v[1], v[2], v[3]}, (GLB u4v*)(sb + i));
       } else {
 #pragma unroll
         for (int cc = 0; cc < 4; cc++)
@@ -1372,6 +1382,16 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   }
   // the slots' lazy reset is consumed (every thread has read the flags above; no other workgroup owns these slots)
   if (tid < 2 && fresh[tid]) P.fresh[slot[tid]] = 0;
+  if (P.prof) { // phase profile: prologue, equaliser, rate dematching (the workgroup's last thread), whole workgroup
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned long long pt3 = clock64();
+      atomicAdd(&P.prof[0], 1ull);
+      atomicAdd(&P.prof[1], pt1 - pt0);
+      atomicAdd(&P.prof[2], pt2 - pt1);
+      atomicAdd(&P.prof[3], pt3 - pt2);
+    }
+  }
 }
 
 template <int QM0>

@@ -14,6 +14,7 @@
 #include <cmath>
 #include <map>
 #include <unordered_map>
+#include <atomic>
 #include <mutex>
 #include <stdio.h>
 #include <string.h>
@@ -39,6 +40,31 @@ using namespace mi355;
       return MI355_ERROR;                                                                                              \
     }                                                                                                                  \
   } while (0)
+
+namespace {
+std::atomic<unsigned long long*> g_eqrm_prof{nullptr};
+unsigned long long*              g_eqrm_prof_mem = nullptr;
+std::mutex                       g_eqrm_prof_mu;
+} // namespace
+
+// measurement: enable = 1 arms pdsch_eq_rm's phase counters (zeroed), 0 disarms; out (nullable, 4 u64): workgroups and
+// the sums of their prologue, equaliser and rate-dematching shader cycles since arming (include/srsran_amd/pdsch.h)
+extern "C" int mi355_pdsch_eqrm_profile(int enable, uint64_t* out)
+{
+  std::lock_guard<std::mutex> lk(g_eqrm_prof_mu);
+  if (out && g_eqrm_prof.load()) {
+    if (hipDeviceSynchronize() != hipSuccess) return MI355_ERROR;
+    if (hipMemcpy(out, g_eqrm_prof_mem, 4 * 8, hipMemcpyDeviceToHost) != hipSuccess) return MI355_ERROR;
+  }
+  if (enable) {
+    if (!g_eqrm_prof_mem && hipMalloc(&g_eqrm_prof_mem, 4 * 8) != hipSuccess) return MI355_ERROR;
+    if (hipMemset(g_eqrm_prof_mem, 0, 4 * 8) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return MI355_ERROR;
+    g_eqrm_prof.store(g_eqrm_prof_mem);
+  } else {
+    g_eqrm_prof.store(nullptr);
+  }
+  return MI355_SUCCESS;
+}
 
 namespace {
 
@@ -737,6 +763,7 @@ static bool plan_eq_rm(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi
   er.pool = EqRmPool{v.buf, v.stride, v.cb_crc, v.fresh, rm_sparse_writes() ? 1 : 0};
   static const int eqrm_diag = getenv("MI355_EQRM_DIAG") ? atoi(getenv("MI355_EQRM_DIAG")) : 0;
   er.pool.diag = eqrm_diag;
+  er.pool.prof = g_eqrm_prof.load();
   return er.max_c > 0;
 }
 
