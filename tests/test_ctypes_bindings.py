@@ -3,8 +3,8 @@ so a pointer went through as a 32-bit int): every `<lib>.<function>.argtypes = [
 bench and oracle glue is checked against the C prototype it binds --
 
 * same number of arguments;
-* a pointer type (POINTER, c_void_p, c_char_p, ndpointer, a ctypes array) exactly where the C parameter is a pointer
-  or an array, and a 64-bit scalar where the C parameter is size_t / 64-bit;
+* a pointer type (POINTER, c_void_p, c_char_p, ndpointer, CFUNCTYPE, a ctypes array) exactly where the C parameter
+  is a pointer, an array or a function-pointer typedef (`*_fn`), and a 64-bit scalar where the C parameter is size_t / 64-bit;
 * every function the Python side CALLS through a library handle has its argtypes declared somewhere, and one that
   returns a pointer or a 64-bit value has its restype declared.
 
@@ -90,7 +90,7 @@ def _expand(tok: str, al: dict[str, str]) -> str:
 
 def _is_ptr_py(tok: str) -> bool:
     # ndpointer aliases of oracle/__init__.py (i16p, u8p, f32p ...) count as pointers wherever they are imported from
-    return bool(re.search(r"POINTER|c_void_p|c_char_p|ndpointer|\*\s*\w|\b[iuf]\d+p\b", tok))
+    return bool(re.search(r"POINTER|c_void_p|c_char_p|ndpointer|CFUNCTYPE|\*\s*\w|\b[iuf]\d+p\b", tok))
 
 
 def _is_wide_py(tok: str) -> bool:
@@ -182,7 +182,7 @@ def test_argtypes_match_prototypes():
             bad.append(f"{path}:{line} {name}: {len(args)} argtypes for {len(cparams)} C parameters")
             continue
         for k, (a, c) in enumerate(zip(args, cparams)):
-            c_ptr = "*" in c or "[" in c
+            c_ptr = "*" in c or "[" in c or bool(re.search(r"\w+_fn\b", c))  # (function-pointer typedefs: *_fn)
             if c_ptr != _is_ptr_py(a):
                 bad.append(f"{path}:{line} {name} arg {k}: C `{c}` vs ctypes `{a}`")
             elif not c_ptr and bool(WIDE.search(c)) and not _is_wide_py(a):
