@@ -1020,7 +1020,10 @@ constexpr int      ER_PF      = PDSCH_ER_PF; // RE pairs per thread whose loads 
 #define PDSCH_ER_TPF 0
 #endif
 constexpr bool     ER_TPF     = PDSCH_ER_TPF; // first round of rate-dematching table words loaded before the equaliser
-constexpr int      ER_Q       = 5;                                                                 // quads per round
+#ifndef PDSCH_ER_Q
+#define PDSCH_ER_Q 5
+#endif
+constexpr int      ER_Q       = PDSCH_ER_Q; // quads per thread and round of the rate dematcher (table words in flight)
 constexpr int      ER_R       = (3 * (6144 + 32) + 12 + 8 * ER_THREADS * ER_Q - 1) / (8 * ER_THREADS * ER_Q); // rounds
 constexpr int      ER_Q2      = 3; // quads per round when both layers share a pass
 constexpr int      ER_R2      = (3 * (6144 + 32) + 12 + 8 * ER_THREADS * ER_Q2 - 1) / (8 * ER_THREADS * ER_Q2);

@@ -282,15 +282,12 @@ struct Arena {
   uint8_t*                 data   = nullptr;
   uint32_t                 stride = 0, data_stride = 0, max_cb = 0, nof_sb = 0;
   std::vector<uint32_t>    free_slots;
-  hipStream_t              stream = nullptr;
-  // softbuffer resets run on this stream without a host wait; the event, recorded after the latest one, is what a
-  // decode on another stream waits for (on the GPU) before touching the softbuffers
-  // reset_gen counts the records; reset_seen[stream] is the generation a decode stream last waited for, so a stream
-  // waits only when a reset was enqueued since (the latest record covers every earlier reset: one in-order stream).
-  // Both under mu, together with the record and the wait (hipStreamWaitEvent binds the latest record at call time).
-  hipEvent_t                        ev_reset  = nullptr;
-  uint64_t                          reset_gen = 0;
-  std::map<hipStream_t, uint64_t>   reset_seen;
+  hipStream_t              stream = nullptr; // slot initialisation (synchronous)
+  // srslte_softbuffer_rx_reset* only records the reset (slot -> code blocks to clear, the largest request): the next
+  // decode that uses the slot applies it on its own stream right before the decode (srsUE resets a TB's softbuffer in
+  // the worker that decodes it, just before the decode, cc_worker.cc:423-470).  No launch, no event and no
+  // cross-worker ordering per reset; the host copy of the CB flags is cleared at once.  Under mu.
+  std::map<uint32_t, uint32_t> pending_reset;
 
   int init_locked()
   {
@@ -309,7 +306,6 @@ struct Arena {
     mi355_softbuffer_pool_data(pool, &data, &data_stride, nullptr);
     (void)hipSetDevice(device);
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return SRSLTE_ERROR;
-    if (hipEventCreateWithFlags(&ev_reset, hipEventDisableTiming) != hipSuccess) return SRSLTE_ERROR;
     for (uint32_t i = nof_sb; i-- > 0;) free_slots.push_back(i);
     return SRSLTE_SUCCESS;
   }
@@ -333,8 +329,8 @@ Arena& arena()
 void arena_forget_stream(hipStream_t s)
 {
   Arena&                      A = arena();
-  std::lock_guard<std::mutex> lk(A.mu);
-  A.reset_seen.erase(s);
+  std::lock_guard<std::mutex> lk(A.mu); // (nothing is kept per decode stream since resets are deferred)
+  (void)s;
 }
 
 // ---------------------------------------------------------------------------------------------------- PDSCH state
@@ -412,15 +408,6 @@ int pdsch_decode_dev(srslte_pdsch_t* q, PdschState* st, hipStream_t stream, srsl
 {
   Arena& A = arena();
   if (!A.pool) return SRSLTE_ERROR;
-  // softbuffer resets enqueued on the arena stream come first (a GPU-side wait, no host round trip)
-  {
-    std::lock_guard<std::mutex> lk(A.mu);
-    uint64_t& seen = A.reset_seen[stream];
-    if (seen != A.reset_gen) {
-      if (hipStreamWaitEvent(stream, A.ev_reset, 0) != hipSuccess) return SRSLTE_ERROR;
-      seen = A.reset_gen;
-    }
-  }
   mi355_pdsch_job_t job{};
   job.sf.tti = sf->tti;
   job.sf.cfi = sf->cfi;
@@ -455,6 +442,20 @@ int pdsch_decode_dev(srslte_pdsch_t* q, PdschState* st, hipStream_t stream, srsl
     pay_total += (pay_len[t] + 255) / 256 * 256;
   }
   if (!run[0] && !run[1]) return SRSLTE_SUCCESS;
+  // the deferred softbuffer resets of the slots this decode uses, on its stream, in front of it
+  for (int t = 0; t < SRSLTE_MAX_CODEWORDS; t++) {
+    if (!run[t]) continue;
+    const uint32_t slot = job.cfg.softbuffer[t];
+    uint32_t       nc   = 0;
+    {
+      std::lock_guard<std::mutex> lk(A.mu);
+      auto                        it = A.pending_reset.find(slot);
+      if (it == A.pending_reset.end()) continue;
+      nc = it->second;
+      A.pending_reset.erase(it);
+    }
+    if (mi355_softbuffer_reset_cb(A.pool, slot, nc, stream) != MI355_SUCCESS) return SRSLTE_ERROR;
+  }
   if (pay_total > st->pay_cap) {
     if (st->d_payload) (void)hipFree(st->d_payload);
     st->d_payload = nullptr;
@@ -753,6 +754,7 @@ int srslte_softbuffer_rx_init(srslte_softbuffer_rx_t* q, uint32_t nof_prb)
     q->data[i]      = A.data + cb * A.data_stride;
   }
   // a fresh slot may hold a previous owner's state: start from the reset state
+  A.pending_reset.erase(slot);
   mi355_softbuffer_reset(A.pool, slot, A.stream);
   (void)hipStreamSynchronize(A.stream);
   return SRSLTE_SUCCESS;
@@ -765,10 +767,9 @@ void srslte_softbuffer_rx_reset_cb(srslte_softbuffer_rx_t* q, uint32_t nof_cb)
   const int s = A.slot_of(q);
   if (s < 0) return;
   {
-    std::lock_guard<std::mutex> lk(A.mu); // (the event is re-recorded after every reset)
-    mi355_softbuffer_reset_cb(A.pool, (uint32_t)s, std::min(nof_cb, q->max_cb), A.stream);
-    (void)hipEventRecord(A.ev_reset, A.stream);
-    A.reset_gen++;
+    std::lock_guard<std::mutex> lk(A.mu); // applied by the next decode of the slot (Arena::pending_reset)
+    uint32_t&                   nc = A.pending_reset[(uint32_t)s];
+    nc                             = std::max(nc, std::min(nof_cb, q->max_cb));
   }
   memset(q->cb_crc, 0, q->max_cb * sizeof(bool));
   q->tb_crc = false;
@@ -794,7 +795,10 @@ void srslte_softbuffer_rx_free(srslte_softbuffer_rx_t* q)
   {
     std::lock_guard<std::mutex> lk(A.mu);
     const int                   s = A.slot_of(q);
-    if (s >= 0) A.free_slots.push_back((uint32_t)s);
+    if (s >= 0) {
+      A.free_slots.push_back((uint32_t)s);
+      A.pending_reset.erase((uint32_t)s);
+    }
   }
   free(q->buffer_f);
   free(q->data);
