@@ -96,7 +96,7 @@ __device__ __forceinline__ void stage(const float2* __restrict__ src, float2* __
 __global__ __launch_bounds__(256) void ofdm_rx(OfdmArgs a)
 {
   __shared__ float2 buf[2][OFDM_MAX_N];
-  const OfdmJob  J    = a.jobs[blockIdx.y];
+  const OfdmJob  J    = a.jobs ? a.jobs[blockIdx.y] : a.inl[blockIdx.y];
   const uint32_t sym  = blockIdx.x; // 0 .. 2*nsymb-1
   const uint32_t slot = sym / a.nsymb, l = sym % a.nsymb;
   const float2*  in   = J.in + (size_t)slot * a.slot_sz + a.cp0 + (size_t)l * (a.N + a.cp1);
@@ -183,7 +183,7 @@ template <uint32_t N, uint32_t R0, uint32_t R1, uint32_t R2, uint32_t R3>
 __global__ __launch_bounds__(256) void ofdm_rx_n(OfdmArgs a)
 {
   __shared__ float2 buf[N], tw[N];
-  const OfdmJob  J    = a.jobs[blockIdx.y];
+  const OfdmJob  J    = a.jobs ? a.jobs[blockIdx.y] : a.inl[blockIdx.y];
   const uint32_t sym  = blockIdx.x; // 0 .. 2*nsymb-1
   const uint32_t slot = sym / a.nsymb, l = sym % a.nsymb;
   const float2*  in   = J.in + (size_t)slot * a.slot_sz + a.cp0 + (size_t)l * (N + a.cp1);
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256) void ofdm_rx_n(OfdmArgs a)
 __global__ __launch_bounds__(256) void ofdm_tx(OfdmArgs a, float scale)
 {
   __shared__ float2 buf[2][OFDM_MAX_N];
-  const OfdmJob  J    = a.jobs[blockIdx.y];
+  const OfdmJob  J    = a.jobs ? a.jobs[blockIdx.y] : a.inl[blockIdx.y];
   const uint32_t sym  = blockIdx.x;
   const uint32_t slot = sym / a.nsymb, l = sym % a.nsymb;
   const uint32_t N = a.N, half = a.nre / 2;

@@ -45,8 +45,10 @@ struct OfdmJob {
   float2*       out; // resource grid (nsymb*2 x nre)
 };
 
+constexpr uint32_t OFDM_INLINE_JOBS = 4; // jobs carried in the kernel arguments (one-subframe calls: no upload)
 struct OfdmArgs {
-  const OfdmJob* jobs;
+  const OfdmJob* jobs; // nullptr: inl[blockIdx.y]
+  OfdmJob        inl[OFDM_INLINE_JOBS];
   const float2*  tw; // W_N^m = exp(-2 pi i m / N), m < N
   uint32_t       N, nre, nsymb, cp0, cp1, slot_sz;
   uint32_t       nstages;

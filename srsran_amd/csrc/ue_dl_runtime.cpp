@@ -145,6 +145,19 @@ static int ofdm_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t nj
                     size_t* used = nullptr, bool defer = false)
 {
   const size_t nj = (size_t)njobs * q->nof_rx;
+  if (nj <= OFDM_INLINE_JOBS && !defer) { // srsUE's one-subframe calls: the jobs travel in the kernel arguments
+    OfdmArgs a = q->ofdm;
+    a.jobs     = nullptr;
+    for (uint32_t i = 0; i < njobs; i++) {
+      for (uint32_t r = 0; r < q->nof_rx; r++) {
+        if (!jobs[i].in_buffer[r] || !jobs[i].sf_symbols[r]) return MI355_ERROR_INVALID_INPUTS;
+        a.inl[(size_t)i * q->nof_rx + r] = OfdmJob{(const float2*)jobs[i].in_buffer[r], (float2*)jobs[i].sf_symbols[r]};
+      }
+    }
+    if (used) *used = 0;
+    CHECK_HIP(ofdm_launch_rx(a, (uint32_t)nj, s));
+    return MI355_SUCCESS;
+  }
   CHECK_HIP(q->st_ofdm.reserve(nj * sizeof(OfdmJob)));
   auto* oj = (OfdmJob*)q->st_ofdm.slot(nj * sizeof(OfdmJob));
   for (uint32_t i = 0; i < njobs; i++) {
