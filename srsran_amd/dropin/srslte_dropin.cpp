@@ -645,7 +645,14 @@ int ue_fft_estimate(srslte_ue_dl_t* q, srslte_dl_sf_cfg_t* sf, srslte_ue_dl_cfg_
     job.sf_symbols[r] = st->d_grid[r];
     for (uint32_t p = 0; p < q->cell.nof_ports; p++) job.ce[p][r] = st->d_ce[p][r];
   }
-  if (nstaged == st->nof_rx) {
+  // (MI355_DROPIN_IQ_COPY=1: staged samples copied to device memory first instead of read by the demodulator where
+  // they lie in page-locked host memory; A/B timing)
+  static const bool iq_copy = getenv("MI355_DROPIN_IQ_COPY") && atoi(getenv("MI355_DROPIN_IQ_COPY")) != 0;
+  if (nstaged == st->nof_rx && !iq_copy) {
+    // the OFDM demodulator reads each staged sample once, over the host link, from the fine-grained staging buffer:
+    // no copy kernel in front of it
+    for (uint32_t r = 0; r < st->nof_rx; r++) job.in_buffer[r] = (const float*)((char*)st->h_in.p + r * nin);
+  } else if (nstaged == st->nof_rx) {
     if (mi355::stage_copy(st->d_in[0], st->h_in.p, nin * st->nof_rx, st->stream) != hipSuccess) return SRSLTE_ERROR;
   } else {
     for (uint32_t r = 0; r < st->nof_rx; r++)
