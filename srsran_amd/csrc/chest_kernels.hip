@@ -178,6 +178,15 @@ __device__ void chest_tail(const ChestArgs& a, const ChestJob& J, const float2* 
   }
 }
 
+// entry k of a launch's (job, rx, port) list: the descriptor array, or the kernel arguments' copy of a one-subframe
+// call's entries (selected by constant indices: a per-thread index into the arguments would go through scratch)
+__device__ __forceinline__ ChestJob chest_job(const ChestArgs& a, size_t k)
+{
+  if (a.jobs) return a.jobs[k];
+  static_assert(CHEST_INLINE_JOBS == 4, "selection below");
+  return k == 0 ? a.inl[0] : k == 1 ? a.inl[1] : k == 2 ? a.inl[2] : a.inl[3];
+}
+
 __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
 {
   __shared__ float2 pe[4 * 2 * MAXPRB];
@@ -190,7 +199,7 @@ __global__ __launch_bounds__(256) void chest_estimate(ChestArgs a)
 
   // the blocks of one subframe's (rx, port) estimates read the same pilot rows: keep them on one L2
   const uint32_t blk  = xcd_chunk(blockIdx.x, gridDim.x);
-  const ChestJob J    = a.jobs[blk];
+  const ChestJob J    = chest_job(a, blk);
   const uint32_t nprb = a.nof_prb, nre = 12 * nprb, nref = 2 * nprb, port = J.port;
   const uint32_t nsym = port < 2 ? 4 : 2, np = nsym * nref;
   const float2*  crs  = a.pilots + (size_t)((port / 2) * 10 + J.sf) * (4 * nref);
@@ -422,7 +431,7 @@ __global__ __launch_bounds__(256) void chest_pre(ChestArgs a, uint32_t do_sync, 
   __shared__ float cfo_s;
   const uint32_t   P = a.nof_ports, R = a.nof_rx;
   const uint32_t   job = blockIdx.x / R, rx = blockIdx.x % R;
-  const ChestJob&  J0  = a.jobs[((size_t)job * R + rx) * P];
+  const ChestJob   J0  = chest_job(a, ((size_t)job * R + rx) * P);
   float2*          g   = J0.grid;
   const uint32_t   nprb = a.nof_prb, nre = 12 * nprb, nref = 2 * nprb;
   if (do_sync) {
@@ -479,7 +488,7 @@ __global__ __launch_bounds__(256) void chest_pre(ChestArgs a, uint32_t do_sync, 
         }
         const float pwr = tot[p * 9 + 8] / (float)(nsym * nref);
         const float se  = sum / (float)nsym;
-        a.jobs[((size_t)job * R + rx) * P + p].out[CHEST_O_SYNC] = se;
+        chest_job(a, ((size_t)job * R + rx) * P + p).out[CHEST_O_SYNC] = se;
         if (!isinf(sum) && !isnan(sum) && !isinf(pwr) && !isnan(pwr)) {
           sync_err += se * pwr;
           pwr_sum += pwr;
@@ -517,7 +526,7 @@ __global__ __launch_bounds__(256) void chest_pre(ChestArgs a, uint32_t do_sync, 
       np += v[1] / 5.0f;
       np += v[2] / 5.0f;
       np += v[3] / 5.0f;
-      for (uint32_t p = 0; p < P; p++) a.jobs[((size_t)job * R + rx) * P + p].out[CHEST_O_NOISE] = np;
+      for (uint32_t p = 0; p < P; p++) chest_job(a, ((size_t)job * R + rx) * P + p).out[CHEST_O_NOISE] = np;
     }
   }
 }
@@ -532,7 +541,7 @@ __global__ __launch_bounds__(256) void chest_resolve(ChestArgs a, uint32_t njobs
   for (uint32_t r = 0; r < R; r++) {
     float acc = 0.f;
     for (uint32_t p = 0; p < P; p++) {
-      const ChestJob& J = a.jobs[((size_t)i * R + r) * P + p];
+      const ChestJob  J = chest_job(a, ((size_t)i * R + r) * P + p);
       float           nf;
       if (a.noise_alg == 0 || (J.flags & CHEST_F_NOISE_SF05))
         nf = J.out[CHEST_O_NOISE];

@@ -79,8 +79,10 @@ struct ChestJob {
 };
 enum : uint32_t { CHEST_F_CFO = 1, CHEST_F_NOISE_SF05 = 2 };
 
+constexpr uint32_t CHEST_INLINE_JOBS = 4; // (job, rx, port) entries carried in the kernel arguments (one subframe)
 struct ChestArgs {
-  const ChestJob* jobs;
+  const ChestJob* jobs; // nullptr: inl[] (chest_job)
+  ChestJob        inl[CHEST_INLINE_JOBS];
   const float2*   pilots; // [pair][sf][4 * 2 * nof_prb]
   const float2*   pss;    // srslte_pss_generate(cell.id % 3), 62 values
   const float*    out_all; // out of job 0 (stride R * P * CHEST_OUT per job)

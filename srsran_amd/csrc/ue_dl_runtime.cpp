@@ -141,11 +141,19 @@ static int get_scratch(mi355_ue_dl_t* q, size_t bytes, char** p)
   return MI355_SUCCESS;
 }
 
+// one-subframe calls: OFDM / estimator descriptors in the kernel arguments (MI355_NO_INLINE_JOBS=1: always uploaded,
+// A/B timing)
+static bool inline_jobs()
+{
+  static const bool v = !(getenv("MI355_NO_INLINE_JOBS") && atoi(getenv("MI355_NO_INLINE_JOBS")) != 0);
+  return v;
+}
+
 static int ofdm_run(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, uint32_t njobs, hipStream_t s,
                     size_t* used = nullptr, bool defer = false)
 {
   const size_t nj = (size_t)njobs * q->nof_rx;
-  if (nj <= OFDM_INLINE_JOBS && !defer) { // srsUE's one-subframe calls: the jobs travel in the kernel arguments
+  if (nj <= OFDM_INLINE_JOBS && !defer && inline_jobs()) { // srsUE's one-subframe calls: jobs in the kernel arguments
     OfdmArgs a = q->ofdm;
     a.jobs     = nullptr;
     for (uint32_t i = 0; i < njobs; i++) {
@@ -328,8 +336,17 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
     maxl = std::max(maxl, jobs[i].link);
   }
   if (njobs && q->links.size() <= maxl) q->links.resize((size_t)maxl + 1);
-  CHECK_HIP(q->st_chest.reserve(ncj * sizeof(ChestJob)));
-  auto*        cj   = (ChestJob*)q->st_chest.slot(ncj * sizeof(ChestJob));
+  // srsUE's one-subframe calls: the (job, rx, port) entries travel in the kernel arguments, no descriptor upload
+  // (not for the deferred launches, the Wiener stage or the PSS automatic-sigma ranges, which address the array)
+  const bool pss_auto = cfg->noise_alg == MI355_NOISE_ALG_PSS && cfg->filter_type == MI355_CHEST_FILTER_GAUSS &&
+                        cfg->filter_coef[0] <= 0;
+  const bool inl      = ncj <= CHEST_INLINE_JOBS && !defer && !wiener && !pss_auto && inline_jobs();
+  ChestJob   inl_jobs[CHEST_INLINE_JOBS];
+  ChestJob*  cj = inl_jobs;
+  if (!inl) {
+    CHECK_HIP(q->st_chest.reserve(ncj * sizeof(ChestJob)));
+    cj = (ChestJob*)q->st_chest.slot(ncj * sizeof(ChestJob));
+  }
   const size_t nout = ncj * CHEST_OUT;
   char*        base = nullptr;
   const size_t jb   = (ncj * sizeof(ChestJob) + 255) / 256 * 256;
@@ -366,9 +383,14 @@ static int chest_launch_only(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* jobs, ui
     }
     if (is05) last05[jobs[i].link] = (int32_t)i;
   }
-  CHECK_HIP(q->st_chest.upload(base, s));
   ChestArgs ca{};
-  ca.jobs        = (const ChestJob*)base;
+  if (inl) {
+    ca.jobs = nullptr;
+    for (size_t k = 0; k < ncj; k++) ca.inl[k] = cj[k];
+  } else {
+    CHECK_HIP(q->st_chest.upload(base, s));
+    ca.jobs = (const ChestJob*)base;
+  }
   ca.pilots      = q->pilots;
   ca.pss         = q->pss;
   ca.out_all     = d_out;
