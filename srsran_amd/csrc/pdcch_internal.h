@@ -34,7 +34,8 @@ struct CtrlJob {
 };
 
 struct CtrlArgs {
-  const CtrlJob*  jobs;
+  const CtrlJob*  jobs;        // nullptr: inl (a one-subframe call's job in the kernel arguments)
+  CtrlJob         inl;
   const uint32_t* pcfich_re;   // [16]
   const uint32_t* pdcch_re;    // [3][PDCCH_MAX_REGS * 4]
   const uint32_t* pcfich_seq;  // [10] (32 scrambling bits per subframe, bit j = c(j))
@@ -82,13 +83,15 @@ struct DciHits {
 static_assert(sizeof(DciHits) == 128, "DciHits layout");
 
 struct CompactArgs {
-  const BlindJob* jobs;
+  const BlindJob* jobs; // nullptr: inl
   const DciCand*  cand; // [job][PDCCH_SLOTS][PDCCH_FMTS]
   DciHits*        hits; // [job]
+  BlindJob        inl;
 };
 
 struct BlindArgs {
-  const BlindJob* jobs;
+  const BlindJob* jobs; // nullptr: inl
+  BlindJob        inl;
   const float*    llr;
   uint32_t        llr_stride;
   const uint32_t* cfi;

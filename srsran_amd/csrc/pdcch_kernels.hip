@@ -114,7 +114,7 @@ __device__ __forceinline__ uint32_t seq_bit(const uint32_t* s, uint32_t i) { ret
 
 __global__ __launch_bounds__(256) void ctrl_llr(CtrlArgs a)
 {
-  const CtrlJob& J = a.jobs[blockIdx.x];
+  const CtrlJob& J = a.jobs ? a.jobs[blockIdx.x] : a.inl;
   __shared__ float    s_llr[32];
   __shared__ uint32_t s_cfi;
   const float         noise = J.d_noise ? *J.d_noise : J.noise;
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(64 * WAVES) void pdcch_blind(BlindArgs a)
   const uint32_t     job  = gw / (PDCCH_SLOTS * PDCCH_FMTS);
   const uint32_t     slot = (gw / PDCCH_FMTS) % PDCCH_SLOTS, fmt = gw % PDCCH_FMTS;
   DciCand*           out  = a.out + gw;
-  const BlindJob&    bj   = a.jobs[job]; // read in place (a private copy indexed by space / fmt would go to scratch)
+  const BlindJob&    bj   = a.jobs ? a.jobs[job] : a.inl; // read in place (a private copy indexed by space / fmt would go to scratch)
   const uint32_t     space = slot < MI355_MAX_CANDIDATES_UE ? 0u : 1u;
   const uint32_t     nbits = bj.nbits[space][fmt];
   const uint32_t     cfi   = a.cfi[job];
@@ -680,7 +680,7 @@ __global__ __launch_bounds__(256) void pdcch_compact(CompactArgs a, uint32_t njo
   const uint32_t lane = threadIdx.x & 63;
   if (job >= njobs) return;
   const DciCand* c   = a.cand + (size_t)job * NC;
-  const uint32_t rnti = a.jobs[job].rnti;
+  const uint32_t rnti = a.jobs ? a.jobs[job].rnti : a.inl.rnti;
   bool           hit  = false;
   if (lane < NC) hit = c[lane].status == 2 && c[lane].crc_rem == rnti;
   const uint64_t mask = __builtin_amdgcn_ballot_w64(hit);

@@ -132,7 +132,11 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
     bj[i]      = it->second;
     plan_of[i] = it->second;
   }
-  CHECK_HIP(st->upload(base, s));
+  // a one-subframe call (srsUE's per-TTI search): its two descriptors travel in the kernel arguments, no upload
+  // (MI355_NO_INLINE_JOBS=1: uploaded, A/B timing)
+  static const bool inl_ok = !(getenv("MI355_NO_INLINE_JOBS") && atoi(getenv("MI355_NO_INLINE_JOBS")) != 0);
+  const bool        inl    = inl_ok && n == 1 && nchunks == 1;
+  if (!inl) CHECK_HIP(st->upload(base, s));
   float*    d_llr  = (float*)(base + b_jobs + b_blind);
   uint32_t* d_cfi  = (uint32_t*)(base + b_jobs + b_blind + b_llr);
   float*    d_corr = (float*)(base + b_jobs + b_blind + b_llr + b_cfi);
@@ -163,7 +167,8 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
       if (e) return e;
     }
     CtrlArgs a{};
-    a.jobs       = (const CtrlJob*)base + o;
+    a.jobs       = inl ? nullptr : (const CtrlJob*)base + o;
+    if (inl) a.inl = cj[0];
     a.pcfich_re  = d_tab;
     a.pdcch_re   = d_tab + 16;
     a.pcfich_seq = d_tab + 16 + 3 * PDCCH_MAX_REGS * 4;
@@ -179,14 +184,16 @@ int CtrlState::launch(const mi355_dl_sf_job_t* sfjobs, const float* host_noise, 
     a.ce_row     = ce_row;
     CHECK_HIP(ctrl_launch_llr(a, m, s));
     BlindArgs b{};
-    b.jobs       = (const BlindJob*)(base + b_jobs) + o;
+    b.jobs       = inl ? nullptr : (const BlindJob*)(base + b_jobs) + o;
+    if (inl) b.inl = bj[0];
     b.llr        = d_llr + (size_t)o * stride;
     b.llr_stride = stride;
     b.cfi        = d_cfi + o;
     for (int k = 0; k < 3; k++) b.ncce[k] = regs.nregs[k] / 9;
     b.out = d_cand + (size_t)o * ncand;
     CHECK_HIP(ctrl_launch_blind(b, m, s));
-    CompactArgs h{(const BlindJob*)(base + b_jobs) + o, d_cand + (size_t)o * ncand, d_hits + o};
+    CompactArgs h{inl ? nullptr : (const BlindJob*)(base + b_jobs) + o, d_cand + (size_t)o * ncand, d_hits + o,
+                  inl ? bj[0] : BlindJob{}};
     CHECK_HIP(ctrl_launch_compact(h, m, s));
     // the read-backs run on a stream of their own behind the chunk's kernels: the compute stream goes on to the next
     // chunk (and to the PDSCH the caller enqueues) without device-to-host copies in its queue
