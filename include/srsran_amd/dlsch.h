@@ -29,7 +29,9 @@ typedef struct mi355_softbuffer_pool mi355_softbuffer_pool_t;
 
 int  mi355_softbuffer_pool_create(mi355_softbuffer_pool_t** p, uint32_t nof_sb, uint32_t max_cb, int device);
 void mi355_softbuffer_pool_destroy(mi355_softbuffer_pool_t* p);
-/* srslte_softbuffer_rx_reset / _reset_tbs / _reset_cb (softbuffer.c:128-154) on softbuffer `sb` */
+/* srslte_softbuffer_rx_reset / _reset_tbs / _reset_cb (softbuffer.c:128-154) on softbuffer `sb`.  The resets are
+ * ordered on `stream` before the work enqueued there next; stream NULL: done when the call returns (the pool has no
+ * stream of its own, and the null stream does not order against a decoder's non-blocking streams). */
 int mi355_softbuffer_reset(mi355_softbuffer_pool_t* p, uint32_t sb, void* stream);
 int mi355_softbuffer_reset_tbs(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t tbs, void* stream);
 int mi355_softbuffer_reset_cb(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t nof_cb, void* stream);

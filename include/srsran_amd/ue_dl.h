@@ -109,6 +109,9 @@ int mi355_ue_dl_set_chunks(mi355_ue_dl_t* q, uint32_t nof_chunks);
  * estimate bytes).  The standalone estimate calls always write every row.  A setter, not a field of
  * mi355_chest_dl_cfg_t, so that struct keeps its layout. */
 int mi355_ue_dl_set_ce_rows(mi355_ue_dl_t* q, uint32_t ce_rows);
+/* the object's own stream (the one its calls use when they are given NULL): work a caller orders in front of a call,
+ * e.g. a softbuffer reset, goes there */
+void* mi355_ue_dl_get_stream(mi355_ue_dl_t* q);
 
 /* Zero one link's estimator state (srslte_chest_dl_init / set_cell). */
 int mi355_ue_dl_reset_link(mi355_ue_dl_t* q, uint32_t link);

@@ -378,6 +378,7 @@ int mi355_softbuffer_reset_cb(mi355_softbuffer_pool_t* p, uint32_t sb, uint32_t 
   const uint32_t nc = std::min(nof_cb, p->max_cb);
   DlschResetArgs a{p->fresh, p->cb_crc, (size_t)sb * p->max_cb, nc, p->max_cb}; // one launch for both
   CHECK_HIP(dlsch_launch_reset(a, s));
+  if (!s) CHECK_HIP(hipStreamSynchronize(nullptr)); // (dlsch.h: NULL = done on return)
   return MI355_SUCCESS;
 }
 
@@ -421,6 +422,7 @@ int mi355_softbuffer_reset_tbs_batch(mi355_softbuffer_pool_t* p, const uint32_t*
   CHECK_HIP(dlsch_launch_reset_list(p->d_list[k], n, p->max_cb, p->fresh, p->cb_crc, s));
   CHECK_HIP(hipEventRecord(p->ev_list[k], s));
   p->ev_armed[k] = true;
+  if (!s) CHECK_HIP(hipStreamSynchronize(nullptr)); // (dlsch.h: NULL = done on return)
   return MI355_SUCCESS;
 }
 
@@ -441,6 +443,7 @@ int mi355_softbuffer_reset_range(mi355_softbuffer_pool_t* p, uint32_t first, uin
   CHECK_HIP(hipSetDevice(p->device));
   DlschResetArgs a{p->fresh, p->cb_crc, (size_t)first * p->max_cb, (size_t)n * p->max_cb, 0};
   CHECK_HIP(dlsch_launch_reset(a, (hipStream_t)stream));
+  if (!stream) CHECK_HIP(hipStreamSynchronize(nullptr)); // (dlsch.h: NULL = done on return)
   return MI355_SUCCESS;
 }
 

@@ -610,6 +610,8 @@ int mi355_ue_dl_set_chunks(mi355_ue_dl_t* q, uint32_t nof_chunks)
   return MI355_SUCCESS;
 }
 
+void* mi355_ue_dl_get_stream(mi355_ue_dl_t* q) { return q ? (void*)q->own : nullptr; }
+
 int mi355_ue_dl_set_ce_rows(mi355_ue_dl_t* q, uint32_t ce_rows)
 {
   if (!q || ce_rows > 1) return MI355_ERROR_INVALID_INPUTS;

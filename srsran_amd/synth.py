@@ -222,7 +222,8 @@ class DlReceiver:
                                                             self.ctrl_res, self.dci, self.res, None),
                   "ue_dl_find_and_decode_batch")
             return
-        check(self.L.mi355_softbuffer_reset_range(self.pool.h, 0, 2 * n, None), "softbuffer_reset_range")
+        # on the decoder's own stream, in front of its decode (a NULL-stream reset would not be ordered against it)
+        check(self.L.mi355_softbuffer_reset_range(self.pool.h, 0, 2 * n, self.ue.stream()), "softbuffer_reset_range")
         if stages is None:
             check(self.L.mi355_ue_dl_decode_batch(self.ue.h, self.pool.h, jobs, sfs, cfgs, C.byref(self.chest_cfg),
                                                   self.chest, self.pays, n, self.res, None), "ue_dl_decode_batch")

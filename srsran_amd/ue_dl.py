@@ -59,6 +59,8 @@ def _declare():
     L.mi355_ue_dl_reset_link.argtypes = [vp, u32]
     L.mi355_ue_dl_set_chunks.argtypes = [vp, u32]
     L.mi355_ue_dl_set_ce_rows.argtypes = [vp, u32]
+    L.mi355_ue_dl_get_stream.restype = vp
+    L.mi355_ue_dl_get_stream.argtypes = [vp]
     L.mi355_ofdm_rx_batch.argtypes = [vp, C.POINTER(DlSfJob), u32, vp]
     L.mi355_chest_dl_estimate_batch.argtypes = [vp, C.POINTER(DlSfJob), u32, C.POINTER(ChestCfg),
                                                 C.POINTER(ChestRes), vp]
@@ -94,6 +96,10 @@ class UeDl:
             self.L.mi355_ue_dl_pdsch(self.h)), cell, nof_rx_antennas
         self.pdsch.device = device
         self.pdsch.close = lambda: None
+
+    def stream(self):
+        """the object's own stream (its calls given NULL run there): work to order in front of a call goes here"""
+        return self.L.mi355_ue_dl_get_stream(self.h)
 
     def set_chunks(self, n: int):
         """find_and_decode's chunk count (0 = automatic)."""
