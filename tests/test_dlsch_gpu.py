@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 import oracle
+from srsran_amd import check, lib
 from srsran_amd.dlsch import Dlsch, SoftbufferPool
 
 pytestmark = pytest.mark.gpu
@@ -136,3 +137,40 @@ def test_dlsch_many_distinct_tb_sizes_one_call():
         assert rets == [0] * len(sz), (call, [i for i, r in enumerate(rets) if r != 0][:8])
         for i, t in enumerate(sz):
             np.testing.assert_array_equal(datas[i][: t // 8], pays[i][: t // 8], err_msg=f"call {call} tbs {t}")
+
+
+@pytest.mark.parametrize("kind", ["reset", "reset_range", "reset_tbs_batch"])
+def test_null_stream_reset_done_before_decode(kind):
+    """dlsch.h: a softbuffer reset given stream NULL has completed when the call returns.  The null stream does not
+    order against the decoder's own (non-blocking) stream, so a reset left pending there could land after the next
+    decode's rate dematcher read the CB CRC flags: that decode would skip every code block as already passed and
+    return the previous TB (profiles/r05/reset_race).  Each round: a clean TB decodes into softbuffer 0 (its flags
+    set), the raw C reset with NULL (no device sync around it), then pure-noise LLRs decode into the same softbuffer
+    at once; the result must be the oracle's decode of the noise from a fresh softbuffer (CRC failure)."""
+    import ctypes as C
+    L = lib()
+    L.mi355_softbuffer_reset_range.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+    L.mi355_softbuffer_reset_tbs_batch.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                                   C.c_uint32, C.c_void_p]
+    tbs, Qm, G = 15840, 2, 30000
+    rng = np.random.default_rng(77)
+    dl = Dlsch(0, 4)
+    pool = SoftbufferPool(2, 32)
+    desc = [dict(tbs=tbs, Qm=Qm, rv=0, softbuffer=0)]
+    for rnd in range(6):
+        pay, good = oracle.make_tb(rng, tbs, Qm, G, 0, 20.0)
+        pool.reset(0)
+        r, d, _ = dl.decode(pool, desc, [good])
+        assert r == [0] and np.array_equal(d[0][: tbs // 8], pay[: tbs // 8]), rnd
+        if kind == "reset":
+            check(L.mi355_softbuffer_reset(pool.h, 0, None), "softbuffer_reset")
+        elif kind == "reset_range":
+            check(L.mi355_softbuffer_reset_range(pool.h, 0, 2, None), "softbuffer_reset_range")
+        else:
+            sbs, tb = (C.c_uint32 * 1)(0), (C.c_uint32 * 1)(tbs)
+            check(L.mi355_softbuffer_reset_tbs_batch(pool.h, sbs, tb, 1, None), "softbuffer_reset_tbs_batch")
+        noise = rng.integers(-300, 301, G).astype(np.int16)
+        got = dl.decode(pool, desc, [noise])
+        want = _oracle([noise], [(tbs, Qm, G, 0.0)], [0], 4, [oracle.Softbuffer()])
+        _check(got, want, [(tbs, Qm, G, 0.0)])
+        assert got[0] == [-1], (rnd, got[0])
