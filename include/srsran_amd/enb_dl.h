@@ -92,6 +92,13 @@ int mi355_channel_grid_batch_at(mi355_enb_dl_t* q, const float* const* tx, float
 int mi355_enb_synth_payloads(mi355_enb_dl_t* q, uint8_t* out, uint64_t first_index, uint32_t n, uint32_t ntb,
                              uint32_t nbytes, uint64_t seed, void* stream);
 
+/* Payload check against mi355_enb_synth_payloads: ok[i * ntb + t] (device bytes) = 1 iff the nbytes at
+ * rx + (i * ntb + t) * rx_stride (device) equal the payload of subframe first_index + i, TB t, for the same seed --
+ * regenerated from the index, so a decoder's output is checked without the transmitted copy.  Asynchronous on stream
+ * (NULL: the object's own stream, waited on before returning). */
+int mi355_enb_payload_check(mi355_enb_dl_t* q, const uint8_t* rx, size_t rx_stride, uint64_t first_index, uint32_t n,
+                            uint32_t ntb, uint32_t nbytes, uint64_t seed, uint8_t* ok, void* stream);
+
 /* Multipath fading test channel in the resource grid (srslte_channel_fading_t, channel/fading.c): model is the
  * reference's string ("none<Fd>", "epa<Fd>", "eva<Fd>", "etu<Fd>", Fd the Doppler in Hz; parse_model,
  * fading.c:48-78), taps and powers of 36.104 B.2 (fading.c:33-46), per link (rx r, port p) the Jakes phases

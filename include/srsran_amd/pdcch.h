@@ -203,8 +203,13 @@ int mi355_ue_dl_find_dl_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* sfj
  * control read-back.  chest[] is filled as by decode_fft_estimate_batch, sfs / ctrl / dci as by find_dl_dci_batch.
  * after_estimate(hook_arg), when given, is called once the estimator's kernels are enqueued on stream (before the
  * control kernels): a caller's read-back of the grids / estimates enqueued there overlaps the control channels.
- * Synchronous. */
+ * Synchronous.  Returns MI355_ERROR_SECOND_STAGE when the estimation succeeded (chest[] filled, the per-link
+ * estimator state advanced once) and only the control stage failed: a caller retries that stage alone
+ * (mi355_ue_dl_find_dl_dci_batch), never the estimation. */
 typedef void (*mi355_hook_fn)(void* arg);
+/* Test hook: the control stage of the next n combined calls below fails after its estimation succeeded (they return
+ * MI355_ERROR_SECOND_STAGE).  Returns the previous count. */
+int mi355_debug_fail_ctrl_stages(int n);
 int mi355_ue_dl_fft_estimate_find_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* sfjobs, mi355_dl_sf_cfg_t* sfs,
                                             const mi355_ue_dl_cfg_t* cfgs, const uint16_t* rntis,
                                             const mi355_chest_dl_cfg_t* chest_cfg, mi355_chest_dl_res_t* chest,

@@ -34,6 +34,9 @@ extern "C" {
 #define MI355_SUCCESS 0
 #define MI355_ERROR -1
 #define MI355_ERROR_INVALID_INPUTS -2
+/* a combined call's first half succeeded and its second failed (mi355_ue_dl_fft_estimate_find_dci_batch: the
+ * estimation ran and chest[] is filled, the control-channel stage failed) */
+#define MI355_ERROR_SECOND_STAGE -3
 
 typedef struct mi355_tdec_batch mi355_tdec_batch_t;
 
@@ -111,13 +114,22 @@ int mi355_tdec_set_diag(int mode);
 /* Number of trellis windows the reference AVX2 build uses for K (turbodecoder.c:381-393): 16, 8 or 0. */
 uint32_t mi355_tdec_autoimp_get_subblocks(uint32_t long_cb);
 
-/* Minimal device-memory helpers so hosts without a HIP toolchain can stage buffers. */
+/* Minimal device-memory helpers so hosts without a HIP toolchain can stage buffers.  The copies and the memset are
+ * synchronous and ordered after EVERY stream of the device they touch, the library's non-blocking streams included
+ * (the null stream alone does not order against those): whatever the caller enqueued through the library before the
+ * call has finished when the copy starts, and it has landed when the call returns (tests/test_sync_contracts_gpu.py).
+ * They wait for the whole device, so they belong in set-up and read-back code, not in a worker's per-call loop. */
 void* mi355_dev_alloc(size_t bytes, int device);
 void  mi355_dev_free(void* p);
 int   mi355_memcpy_h2d(void* dst, const void* src, size_t bytes);
 int   mi355_memcpy_d2h(void* dst, const void* src, size_t bytes);
 int   mi355_memset_dev(void* dst, int value, size_t bytes);
 int   mi355_device_sync(void);
+/* Test hooks of the copy kernels behind the per-call staging (stage_copy.hip): page-locked fine-grained host memory,
+ * and nseg segments copied in one launch (nseg = 0: one stage_copy of bytes[0]).  Synchronous. */
+void* mi355_debug_stage_host_alloc(size_t bytes);
+void  mi355_debug_stage_host_free(void* p);
+int   mi355_debug_stage_copy(void* const* dst, const void* const* src, const uint32_t* bytes, int nseg);
 int   mi355_device_count(void);
 
 /* ------------------------------------------------------------------------------------------------ 8-bit path

@@ -519,3 +519,36 @@ class RefTdec:
             self.L.ref_tdec_free(self.h)
         except Exception:
             pass
+
+
+def ref_dlsch_decode_cbs(bufs: np.ndarray, K: int, tbs: int, max_half: int = 10, dec: "RefTdec | None" = None):
+    """decode_tb_cb + decode_tb of the reference (sch.c:382-486, :531-556) on fresh softbuffers, through the
+    REFERENCE's own AVX2 turbo decoder (oracle/_ref) and its CRC: every code block is decoded half-iteration by
+    half-iteration (srslte_tdec_iteration) until the CRC24B of its K decision bits (the TB CRC24A when C == 1) is zero
+    or max_half half-iterations ran; the TB passes when every block passed and the TB CRC over tbs bits equals the
+    transmitted parity and is non-zero (sch.c:543-549).  bufs: (C, stride) int16 decoder buffers of one TB (the
+    16-window layout).  Returns (tb_ok, data bytes (tbs/8 + 3), per-CB passed (C,), per-CB half-iterations (C,))."""
+    L = ref()
+    dec = dec or RefTdec()
+    C = bufs.shape[0]
+    rlen = K - 24 if C > 1 else K
+    data = np.zeros(C * rlen // 8 + K // 8, np.uint8)
+    ok = np.zeros(C, bool)
+    its = np.zeros(C, np.int32)
+    for c in range(C):
+        _, tr = dec.run(bufs[c], K, max_half, trace=True)
+        for h in range(max_half):
+            nb, poly = (K, CRC24B) if C > 1 else (tbs + 24, CRC24A)
+            if L.ref_crc_byte(poly[0], poly[1], np.ascontiguousarray(tr[h]), nb) == 0:
+                ok[c], its[c] = True, h + 1
+                break
+        else:
+            its[c] = max_half
+        data[c * rlen // 8: c * rlen // 8 + K // 8] = tr[its[c] - 1]
+    out = data[: tbs // 8 + 3].copy()
+    tb_ok = bool(ok.all())
+    if tb_ok:
+        par_rx = int(L.ref_crc_byte(CRC24A[0], CRC24A[1], np.ascontiguousarray(out), tbs))
+        par_tx = (int(out[tbs // 8]) << 16) | (int(out[tbs // 8 + 1]) << 8) | int(out[tbs // 8 + 2])
+        tb_ok = par_rx == par_tx and par_rx != 0
+    return tb_ok, out, ok, its

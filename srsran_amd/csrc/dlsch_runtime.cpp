@@ -99,6 +99,7 @@ struct mi355_dlsch {
   // (find_and_decode's second chunk) uploads at once instead of at the first one's end
   char*      scratch[2]     = {nullptr, nullptr};
   size_t     scratch_cap[2] = {0, 0};
+  std::vector<void*> retired; // outgrown scratch, freed at destroy (hipFree waits for the whole device)
   hipEvent_t done_ev[2]     = {nullptr, nullptr};
   bool       done_armed[2]  = {false, false};
   uint32_t   par            = 0;
@@ -316,9 +317,8 @@ static int tb_crc_scales(mi355_dlsch_t* q, uint32_t nbytes, const uint32_t** out
 static int scratch(mi355_dlsch_t* q, uint32_t k, size_t bytes, char** p)
 {
   if (bytes > q->scratch_cap[k]) {
-    if (q->scratch[k]) {
-      CHECK_HIP(hipDeviceSynchronize());
-      CHECK_HIP(hipFree(q->scratch[k]));
+    if (q->scratch[k]) { // may still be read by this object's batch in flight: retired, not freed
+      q->retired.push_back(q->scratch[k]);
       q->scratch[k]    = nullptr;
       q->done_armed[k] = false;
     }
@@ -533,6 +533,7 @@ void mi355_dlsch_destroy(mi355_dlsch_t* q)
   for (auto& kv : q->scales) (void)hipFree(kv.second);
   for (auto& kv : q->tb_scales) (void)hipFree(kv.second);
   (void)hipFree(q->crc);
+  for (void* r : q->retired) (void)hipFree(r);
   for (int k = 0; k < 2; k++) {
     (void)hipFree(q->scratch[k]);
     if (q->done_ev[k]) (void)hipEventDestroy(q->done_ev[k]);

@@ -84,6 +84,10 @@ hipError_t enb_launch_channel(const EnbChanJob* jobs, uint32_t njobs, uint32_t n
                               const EnbChanMat& H, float sigma, uint64_t seed, uint64_t first, hipStream_t s);
 hipError_t enb_launch_synth_payloads(uint8_t* out, uint64_t first, uint32_t n, uint32_t ntb, uint32_t nbytes,
                                      uint64_t seed, hipStream_t s);
+// ok[i * ntb + t] = 1 iff rx[(i * ntb + t) * rx_stride, + nbytes) equals subframe first + i's TB t as
+// enb_synth_payloads makes it (the payload regenerated from its index, no transmitted copy needed)
+hipError_t enb_launch_payload_check(const uint8_t* rx, size_t rx_stride, uint64_t first, uint32_t n, uint32_t ntb,
+                                    uint32_t nbytes, uint64_t seed, uint8_t* ok, hipStream_t s);
 hipError_t enb_launch_fading(const EnbFadingArgs& a, uint32_t njobs, hipStream_t s);
 
 // srslte_pdsch_encode scales the PDSCH by rho_a = 10^(p_a/20) (x sqrt(2) with 2+ ports) whatever cfg->power_scale

@@ -500,4 +500,29 @@ hipError_t enb_launch_synth_payloads(uint8_t* out, uint64_t first, uint32_t n, u
   return hipGetLastError();
 }
 
+// one workgroup per TB: each lane regenerates its 8-byte words of the payload and compares them with the received bytes
+__global__ __launch_bounds__(256) void enb_payload_check(const uint8_t* __restrict__ rx, size_t rx_stride, uint64_t first,
+                                                         uint32_t ntb, uint32_t nbytes, uint64_t seed,
+                                                         uint8_t* __restrict__ ok)
+{
+  const uint64_t it = blockIdx.x; // i * ntb + t
+  const uint64_t i = it / ntb, t = it % ntb;
+  const uint8_t* r = rx + it * rx_stride;
+  int            bad = 0;
+  for (uint32_t w = threadIdx.x; w < (nbytes + 7) / 8; w += 256) {
+    const uint64_t z = splitmix64(seed ^ (splitmix64(((first + i) << 8) | t) + w));
+    for (uint32_t b = 0; b < 8 && w * 8 + b < nbytes; b++) bad |= r[(size_t)w * 8 + b] != (uint8_t)(z >> (8 * b));
+  }
+  bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) ok[it] = bad ? 0 : 1;
+}
+
+hipError_t enb_launch_payload_check(const uint8_t* rx, size_t rx_stride, uint64_t first, uint32_t n, uint32_t ntb,
+                                    uint32_t nbytes, uint64_t seed, uint8_t* ok, hipStream_t s)
+{
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(enb_payload_check, dim3(n * ntb), dim3(256), 0, s, rx, rx_stride, first, ntb, nbytes, seed, ok);
+  return hipGetLastError();
+}
+
 } // namespace mi355

@@ -641,4 +641,18 @@ int mi355_enb_synth_payloads(mi355_enb_dl_t* q, uint8_t* out, uint64_t first_ind
   return MI355_SUCCESS;
 }
 
+int mi355_enb_payload_check(mi355_enb_dl_t* q, const uint8_t* rx, size_t rx_stride, uint64_t first_index, uint32_t n,
+                            uint32_t ntb, uint32_t nbytes, uint64_t seed, uint8_t* ok, void* stream)
+{
+  if (!q || (n && (!rx || !ok)) || ntb == 0 || ntb > 255 || nbytes == 0 || rx_stride < nbytes)
+    return MI355_ERROR_INVALID_INPUTS;
+  if (!n) return MI355_SUCCESS;
+  std::lock_guard<std::mutex> lk(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  hipStream_t s = stream ? (hipStream_t)stream : q->own;
+  CHECK_HIP(enb_launch_payload_check(rx, rx_stride, first_index, n, ntb, nbytes, seed, ok, s));
+  if (!stream) CHECK_HIP(hipStreamSynchronize(s));
+  return MI355_SUCCESS;
+}
+
 } // extern "C"

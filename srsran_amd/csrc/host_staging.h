@@ -2,7 +2,9 @@
 // Descriptors are packed into one page-locked, fine-grained buffer and moved by one stage_copy kernel on the
 // staging's own stream (stage_copy.h: no copy-engine submission, which can block a calling thread with several
 // workers).  The buffer is refilled only after the previous upload from it has completed (event), so asynchronous
-// callers are safe too.
+// callers are safe too -- at a price for in-line uploads (below): their event is recorded on the caller's compute
+// stream, so the next reserve() blocks the host until everything enqueued on that stream before the previous upload
+// has finished, not just the copy.  A caller that must not wait there keeps two stagings and alternates.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -70,14 +72,15 @@ struct HostStaging {
     used += (n + 255) / 256 * 256;
     return p;
   }
-  // one copy of everything put so far to dst, ordered before the work enqueued on s after this call.  The copy runs
-  // on the staging's own stream, so it does not wait behind s's earlier kernels (the destination must not be in use
-  // by them: callers upload into per-call descriptor space) -- unless after_s: then it waits for them (the
-  // destination may still be read by work of an earlier call left in flight), or only for the event after (recorded
-  // by the caller after the last reader of the destination).
-  // Uploads up to STAGE_INLINE bytes (a few subframes' descriptors: srsUE's per-TTI calls) are copied in line on s
-  // instead: there is nothing of s's to overlap with on that scale, and the copy stream's two event hops cost more
-  // than the copy.
+  // one copy of everything put so far to dst, ordered before the work enqueued on s after this call.  Above the
+  // in-line limit the copy runs on the staging's own stream, so it does not wait behind s's earlier kernels (the
+  // destination must not be in use by them: callers upload into per-call descriptor space) -- unless after_s: then it
+  // waits for them (the destination may still be read by work of an earlier call left in flight), or only for the
+  // event after (recorded by the caller after the last reader of the destination).
+  // Uploads up to the in-line limit (a few subframes' descriptors: srsUE's per-TTI calls) are copied in line on s
+  // instead, behind all of s's earlier work: there is nothing of s's to overlap with on that scale, and the copy
+  // stream's two event hops cost more than the copy.  The completion event is then s's, and the next reserve() waits
+  // for s up to this point (header note).
   // (MI355_STAGE_INLINE=<bytes>: another threshold, 0 = always the copy stream; A/B timing)
   static size_t inline_limit()
   {

@@ -160,6 +160,7 @@ uint32_t mod_bits(uint32_t mod)
 // g0 + t -> RE index or 0xffff (g1 - g0)], the inverse letting the single-RE equalisers walk the grid
 struct MapEntry {
   uint16_t* d = nullptr;
+  size_t    bytes = 0; // capacity of d
   uint32_t  n = 0, g0 = 0, g1 = 0, ncols = 0;
   const uint16_t* inv() const { return d + ((n + 1) & ~1u); }
   const uint16_t* cols() const { return inv() + (g1 - g0); } // distinct subcarriers of the REs
@@ -199,6 +200,10 @@ struct mi355_pdsch {
   std::unordered_map<uint32_t, uint32_t*> scr; // packed descrambling sequences per c_init (HBM)
   char*                                scratch = nullptr;
   size_t                               scratch_cap = 0;
+  // outgrown scratch buffers and evicted extraction maps: freed at destroy (hipFree waits for the whole device, which
+  // would stall every other worker's stream), the maps' buffers reused for new maps
+  std::vector<void*>                   retired;
+  std::vector<std::pair<void*, size_t>> map_free; // (buffer, bytes)
   std::vector<JobPlan>                 last; // plans of the last call (debug_stage)
   float2*                              d_arena   = nullptr;
   float*                               csi_arena = nullptr;
@@ -219,11 +224,9 @@ struct mi355_pdsch {
 static int get_scratch(mi355_pdsch_t* q, size_t bytes, char** p)
 {
   if (bytes > q->scratch_cap) {
-    if (q->scratch) {
-      CHECK_HIP(hipDeviceSynchronize());
-      CHECK_HIP(hipFree(q->scratch));
-      q->scratch = nullptr;
-    }
+    // the old scratch may still be read by this object's batch in flight: retired, not freed (no device-wide wait)
+    if (q->scratch) q->retired.push_back(q->scratch);
+    q->scratch = nullptr;
     const size_t cap = bytes + bytes / 4 + 4096;
     CHECK_HIP(hipMalloc(&q->scratch, cap));
     q->scratch_cap = cap;
@@ -251,8 +254,10 @@ static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi,
   auto it = q->maps.find(key);
   if (it == q->maps.end()) {
     if (q->maps.size() >= 8192) { // bound the cache
-      CHECK_HIP(hipDeviceSynchronize());
-      for (auto& kv : q->maps) (void)hipFree(kv.second.d);
+      // the maps' last readers are the front-end kernels of this object's previous batch (fe_done): once they are
+      // done the buffers are reused for new maps, without a free (hipFree would wait for the whole device)
+      if (q->fe_armed) CHECK_HIP(wait_event(q->fe_done));
+      for (auto& kv : q->maps) q->map_free.emplace_back(kv.second.d, kv.second.bytes);
       q->maps.clear();
       for (auto& m : q->last_map) m = MapEntry{};
     }
@@ -276,8 +281,26 @@ static int get_map(mi355_pdsch_t* q, const mi355_pdsch_grant_t& g, uint32_t cfi,
     std::copy(idx.begin(), idx.end(), all.begin());
     for (uint32_t i = 0; i < e.n; i++) all[((e.n + 1) & ~1u) + idx[i] - e.g0] = (uint16_t)i;
     std::copy(cols.begin(), cols.end(), all.begin() + ((e.n + 1) & ~1u) + (e.g1 - e.g0));
-    CHECK_HIP(hipMalloc(&e.d, std::max<size_t>(all.size(), 1) * sizeof(uint16_t)));
-    if (!all.empty()) CHECK_HIP(hipMemcpy(e.d, all.data(), all.size() * 2, hipMemcpyHostToDevice));
+    const size_t need = std::max<size_t>(all.size(), 1) * sizeof(uint16_t);
+    e.d               = nullptr;
+    for (size_t k = 0; k < q->map_free.size(); k++) // an evicted map's buffer that fits
+      if (q->map_free[k].second >= need) {
+        e.d     = (uint16_t*)q->map_free[k].first;
+        e.bytes = q->map_free[k].second;
+        q->map_free[k] = q->map_free.back();
+        q->map_free.pop_back();
+        break;
+      }
+    if (!e.d) {
+      CHECK_HIP(hipMalloc(&e.d, need));
+      e.bytes = need;
+    }
+    if (!all.empty()) {
+      CHECK_HIP(hipMemcpy(e.d, all.data(), all.size() * 2, hipMemcpyHostToDevice));
+      // (a pageable-source copy may return before its DMA lands; the kernels that read the map run on non-blocking
+      // streams the null stream does not order against)
+      CHECK_HIP(hipStreamSynchronize(nullptr));
+    }
     it = q->maps.emplace(key, e).first;
   }
   *out           = it->second;
@@ -596,6 +619,8 @@ void mi355_pdsch_destroy(mi355_pdsch_t* q)
   (void)hipSetDevice(q->device);
   (void)hipDeviceSynchronize();
   for (auto& kv : q->maps) (void)hipFree(kv.second.d);
+  for (auto& f : q->map_free) (void)hipFree(f.first);
+  for (void* r : q->retired) (void)hipFree(r);
   for (auto& kv : q->scr) (void)hipFree(kv.second);
   (void)hipFree(q->gold);
   (void)hipFree(q->scratch);

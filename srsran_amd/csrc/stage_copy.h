@@ -7,6 +7,9 @@
 #include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
+#if !(defined(__x86_64__) || defined(__i386__))
+#include <sched.h>
+#endif
 
 namespace mi355 {
 
@@ -25,6 +28,14 @@ hipError_t stage_copy_multi(const StageSeg* segs, int n, hipStream_t s);
 // Host waits on the per-call path: hipStreamSynchronize / hipEventSynchronize, or with MI355_SPIN_WAIT=1 a poll loop
 // (hipStreamQuery / hipEventQuery): a blocking wait is woken through the GPU's completion interrupt, which a per-TTI
 // call pays at each of its waits; the poll costs the waiting thread's core instead.
+inline void spin_pause()
+{
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#else
+  sched_yield();
+#endif
+}
 inline bool spin_waits()
 {
   static const bool v = getenv("MI355_SPIN_WAIT") && atoi(getenv("MI355_SPIN_WAIT")) != 0;
@@ -34,14 +45,14 @@ inline hipError_t wait_stream(hipStream_t s)
 {
   if (!spin_waits()) return hipStreamSynchronize(s);
   hipError_t e;
-  while ((e = hipStreamQuery(s)) == hipErrorNotReady) __builtin_ia32_pause();
+  while ((e = hipStreamQuery(s)) == hipErrorNotReady) spin_pause();
   return e;
 }
 inline hipError_t wait_event(hipEvent_t ev)
 {
   if (!spin_waits()) return hipEventSynchronize(ev);
   hipError_t e;
-  while ((e = hipEventQuery(ev)) == hipErrorNotReady) __builtin_ia32_pause();
+  while ((e = hipEventQuery(ev)) == hipErrorNotReady) spin_pause();
   return e;
 }
 

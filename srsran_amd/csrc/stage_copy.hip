@@ -40,7 +40,8 @@ __global__ __launch_bounds__(SC_THREADS) void stage_copy16(uint4* __restrict__ d
     for (size_t b = 16 * n16; b < n; b++) ((uint8_t*)dst)[b] = ((const uint8_t*)src)[b];
 }
 
-// unaligned pointers: 4-byte words when both are 4-aligned, else bytes
+// pointers not 16-byte aligned: 4-byte words when both are 4-aligned (the < 4 tail bytes by thread 0), else every
+// byte by the whole grid (grid-stride: no single-lane crawl over the host link)
 __global__ __launch_bounds__(SC_THREADS) void stage_copy4(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
                                                           size_t n4, size_t n)
 {
@@ -48,6 +49,12 @@ __global__ __launch_bounds__(SC_THREADS) void stage_copy4(uint32_t* __restrict__
   for (size_t i = (size_t)blockIdx.x * SC_THREADS + threadIdx.x; i < n4; i += stride) dst[i] = src[i];
   if (blockIdx.x == 0 && threadIdx.x == 0)
     for (size_t b = 4 * n4; b < n; b++) ((uint8_t*)dst)[b] = ((const uint8_t*)src)[b];
+}
+__global__ __launch_bounds__(SC_THREADS) void stage_copy1(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                          size_t n)
+{
+  const size_t stride = (size_t)gridDim.x * SC_THREADS;
+  for (size_t b = (size_t)blockIdx.x * SC_THREADS + threadIdx.x; b < n; b += stride) dst[b] = src[b];
 }
 
 struct StageSegs {
@@ -100,12 +107,50 @@ hipError_t stage_copy(void* dst, const void* src, size_t bytes, hipStream_t s)
     // over more CUs gets it done in fewer round trips), SC_U per lane beyond
     const uint32_t g = (uint32_t)std::min<size_t>(1024, std::max<size_t>(1, (n16 + SC_THREADS - 1) / SC_THREADS));
     hipLaunchKernelGGL(stage_copy16, dim3(g), dim3(SC_THREADS), 0, s, (uint4*)dst, (const uint4*)src, n16, bytes);
-  } else {
-    const size_t   n4 = (a & 3) == 0 ? bytes / 4 : 0;
+  } else if ((a & 3) == 0) {
+    const size_t   n4 = bytes / 4;
     const uint32_t g  = (uint32_t)std::min<size_t>(1024, std::max<size_t>(1, (n4 + SC_THREADS - 1) / SC_THREADS));
     hipLaunchKernelGGL(stage_copy4, dim3(g), dim3(SC_THREADS), 0, s, (uint32_t*)dst, (const uint32_t*)src, n4, bytes);
+  } else {
+    const uint32_t g = (uint32_t)std::min<size_t>(1024, std::max<size_t>(1, (bytes + SC_THREADS - 1) / SC_THREADS));
+    hipLaunchKernelGGL(stage_copy1, dim3(g), dim3(SC_THREADS), 0, s, (uint8_t*)dst, (const uint8_t*)src, bytes);
   }
   return hipGetLastError();
 }
 
 } // namespace mi355
+
+// test hooks (tests/test_stage_copy_gpu.py): the copy kernels over page-locked host buffers from stage_host_alloc
+extern "C" {
+
+void* mi355_debug_stage_host_alloc(size_t bytes)
+{
+  void* p = nullptr;
+  return mi355::stage_host_alloc(&p, bytes) == hipSuccess ? p : nullptr;
+}
+
+void mi355_debug_stage_host_free(void* p)
+{
+  if (p) (void)hipHostFree(p);
+}
+
+// nseg > 0: segment k copies bytes[k] from src[k] to dst[k], one stage_copy_multi launch; nseg == 0: stage_copy of
+// bytes[0] from src[0] to dst[0].  Synchronous (the library's null-stream-free path: its own stream, waited on).
+int mi355_debug_stage_copy(void* const* dst, const void* const* src, const uint32_t* bytes, int nseg)
+{
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -1;
+  hipError_t e;
+  if (nseg == 0) {
+    e = mi355::stage_copy(dst[0], src[0], bytes[0], s);
+  } else {
+    mi355::StageSeg segs[mi355::STAGE_MAX_SEGS];
+    for (int k = 0; k < nseg && k < mi355::STAGE_MAX_SEGS; k++) segs[k] = {dst[k], src[k], bytes[k]};
+    e = mi355::stage_copy_multi(segs, nseg, s);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipStreamDestroy(s);
+  return e == hipSuccess ? 0 : -1;
+}
+
+} // extern "C"

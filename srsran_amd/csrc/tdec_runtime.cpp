@@ -505,26 +505,61 @@ void mi355_dev_free(void* p)
   if (p) (void)hipFree(p);
 }
 
+} // extern "C"
+
+// The helpers below are synchronous and ordered after every stream of the device they touch (the library's
+// non-blocking streams included, which the null stream does not order against): the work a caller enqueued through
+// the library before the call has finished when the copy starts, and the copy has landed when the call returns.
+// They are utilities for hosts without a HIP toolchain (tests, bench set-up and read-back), never used on the
+// library's per-call paths.
+static int device_of(const void* p, int* dev)
+{
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError(); // (pageable host memory: not an error, it has no device)
+    return -1;
+  }
+  if (a.type != hipMemoryTypeDevice && a.type != hipMemoryTypeManaged) return -1;
+  *dev = a.device;
+  return 0;
+}
+
+static int sync_device_of(const void* p)
+{
+  int cur = 0, dev = 0;
+  CHECK_HIP(hipGetDevice(&cur));
+  if (device_of(p, &dev)) dev = cur;
+  if (dev != cur) CHECK_HIP(hipSetDevice(dev));
+  const hipError_t e = hipDeviceSynchronize();
+  if (dev != cur) (void)hipSetDevice(cur);
+  return e == hipSuccess ? MI355_SUCCESS : MI355_ERROR;
+}
+
+extern "C" {
+
 int mi355_memcpy_h2d(void* dst, const void* src, size_t bytes)
 {
-  // a pageable-source hipMemcpy may return once the data is staged, before the DMA lands; the library's own
-  // streams are non-blocking (not ordered after the null stream), so complete it before returning
+  if (!bytes) return MI355_SUCCESS;
+  if (sync_device_of(dst)) return MI355_ERROR; // earlier readers of dst (on any stream) are done
+  // a pageable-source hipMemcpy may return once the data is staged, before the DMA lands: complete it
   CHECK_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
-  CHECK_HIP(hipStreamSynchronize(nullptr));
-  return MI355_SUCCESS;
+  return sync_device_of(dst);
 }
 
 int mi355_memcpy_d2h(void* dst, const void* src, size_t bytes)
 {
+  if (!bytes) return MI355_SUCCESS;
+  if (sync_device_of(src)) return MI355_ERROR; // earlier writers of src (on any stream) are done
   CHECK_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
   return MI355_SUCCESS;
 }
 
 int mi355_memset_dev(void* dst, int value, size_t bytes)
 {
+  if (!bytes) return MI355_SUCCESS;
+  if (sync_device_of(dst)) return MI355_ERROR;
   CHECK_HIP(hipMemset(dst, value, bytes));
-  CHECK_HIP(hipStreamSynchronize(nullptr));
-  return MI355_SUCCESS;
+  return sync_device_of(dst);
 }
 
 int mi355_device_sync(void)

@@ -2,6 +2,7 @@
 // channel estimation over batches of subframes, and the srslte_ue_dl-level object owning the PDSCH receiver.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <functional>
 #include <cmath>
@@ -73,6 +74,7 @@ struct mi355_ue_dl {
   std::vector<ChestLink> links;
   char*          scratch = nullptr;
   size_t         scratch_cap = 0;
+  std::vector<void*> retired; // outgrown scratch, freed at destroy (hipFree waits for the whole device)
   HostStaging    st_ofdm, st_chest, back; // pinned descriptor uploads / estimator read-back
   hipStream_t    side     = nullptr;       // estimator read-back + fill_res overlapping the PDSCH decode
   hipEvent_t     ev_chest = nullptr;
@@ -128,11 +130,9 @@ static int set_dft(mi355_ue_dl_t* q)
 static int get_scratch(mi355_ue_dl_t* q, size_t bytes, char** p)
 {
   if (bytes > q->scratch_cap) {
-    if (q->scratch) {
-      CHECK_HIP(hipDeviceSynchronize());
-      CHECK_HIP(hipFree(q->scratch));
-      q->scratch = nullptr;
-    }
+    // may still be read by this object's batch in flight: retired, not freed (no device-wide wait)
+    if (q->scratch) q->retired.push_back(q->scratch);
+    q->scratch = nullptr;
     const size_t cap = bytes + bytes / 4 + 4096;
     CHECK_HIP(hipMalloc(&q->scratch, cap));
     q->scratch_cap = cap;
@@ -585,6 +585,7 @@ void mi355_ue_dl_destroy(mi355_ue_dl_t* q)
   (void)hipFree(q->pilots);
   (void)hipFree(q->pss);
   (void)hipFree(q->scratch);
+  for (void* r : q->retired) (void)hipFree(r);
   mi355_pdsch_destroy(q->pdsch);
   if (q->own) (void)hipStreamDestroy(q->own);
   if (q->side) (void)hipStreamDestroy(q->side);
@@ -792,6 +793,13 @@ int mi355_ue_dl_find_dl_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* sfj
   return unpack_all(q, sfs, cfgs, njobs, ctrl, msgs.get(), dci);
 }
 
+// test hook: the next n control stages of combined calls fail after their estimation (the drop-in's recovery path)
+static std::atomic<int> g_fail_ctrl{0};
+int mi355_debug_fail_ctrl_stages(int n)
+{
+  return g_fail_ctrl.exchange(n < 0 ? 0 : n);
+}
+
 int mi355_ue_dl_fft_estimate_find_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_job_t* sfjobs, mi355_dl_sf_cfg_t* sfs,
                                             const mi355_ue_dl_cfg_t* cfgs, const uint16_t* rntis,
                                             const mi355_chest_dl_cfg_t* chest_cfg, mi355_chest_dl_res_t* chest,
@@ -817,11 +825,12 @@ int mi355_ue_dl_fft_estimate_find_dci_batch(mi355_ue_dl_t* q, const mi355_dl_sf_
   mi355_dci_msg_t* const msgs = q->fd_msgs.data();
   q->ctrl->ce_row = 0; // every row of the estimates is written here: read where they lie
   r = q->ctrl->run(sfjobs, nullptr, d_noise, rntis, cfgs, njobs, s, ctrl, msgs);
+  if (!r && g_fail_ctrl.load() > 0 && g_fail_ctrl.fetch_sub(1) > 0) r = MI355_ERROR;
   chest_fill_cb(&fill); // (also after a failed control stage: the estimation itself succeeded)
-  if (r) return r;
   if (!fill.done) return MI355_ERROR;
+  if (r) return MI355_ERROR_SECOND_STAGE; // chest[] is valid: the caller retries the control stage only
   for (uint32_t i = 0; i < njobs; i++) sfs[i].cfi = ctrl[i].cfi;
-  return unpack_all(q, sfs, cfgs, njobs, ctrl, msgs, dci);
+  return unpack_all(q, sfs, cfgs, njobs, ctrl, msgs, dci) == MI355_SUCCESS ? MI355_SUCCESS : MI355_ERROR_SECOND_STAGE;
 }
 
 int mi355_ue_dl_find_and_decode_batch(mi355_ue_dl_t* q, mi355_softbuffer_pool_t* pool, const mi355_dl_sf_job_t* sfjobs,

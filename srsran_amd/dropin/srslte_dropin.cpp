@@ -325,13 +325,8 @@ Arena& arena()
   return a;
 }
 
-// a decode stream about to be destroyed: its handle may be reused by a new stream, which must not inherit the record
-void arena_forget_stream(hipStream_t s)
-{
-  Arena&                      A = arena();
-  std::lock_guard<std::mutex> lk(A.mu); // (nothing is kept per decode stream since resets are deferred)
-  (void)s;
-}
+// (softbuffer resets are deferred to the decoding worker's stream: nothing is tracked per decode stream, so a
+// destroyed stream needs no arena bookkeeping)
 
 // ---------------------------------------------------------------------------------------------------- PDSCH state
 struct PinnedBuf {
@@ -373,10 +368,7 @@ struct PdschState {
     if (own_rx && rx) mi355_pdsch_destroy(rx);
     if (d_stage) (void)hipFree(d_stage);
     if (d_payload) (void)hipFree(d_payload);
-    if (own_stream && stream) {
-      arena_forget_stream(stream);
-      (void)hipStreamDestroy(stream);
-    }
+    if (own_stream && stream) (void)hipStreamDestroy(stream);
   }
 };
 
@@ -544,10 +536,7 @@ struct UeDlState {
     if (d_mem) (void)hipFree(d_mem);
     if (side) (void)hipStreamDestroy(side);
     if (ev_est) (void)hipEventDestroy(ev_est);
-    if (stream) {
-      arena_forget_stream(stream);
-      (void)hipStreamDestroy(stream);
-    }
+    if (stream) (void)hipStreamDestroy(stream);
   }
 };
 
@@ -691,22 +680,23 @@ int ue_fft_estimate(srslte_ue_dl_t* q, srslte_dl_sf_cfg_t* sf, srslte_ue_dl_cfg_
                                                                                   &st->chest, 1, &st->ctrl, st->dci,
                                                                                   st->host_grids ? +hook : nullptr, &bk,
                                                                                   st->stream);
-  if (bk.armed && mi355::wait_stream(st->side) != hipSuccess) return SRSLTE_ERROR;
-  if (rf != MI355_SUCCESS || !bk.ok) {
-    // which half failed is not known here: the two-step form reports it as the reference would
+  const bool back_done = bk.armed && mi355::wait_stream(st->side) == hipSuccess && bk.ok;
+  if (two_step) { // the estimate, then the control channels (ue_dl.c:348-381 as two calls)
     if (mi355_ue_dl_decode_fft_estimate_batch(st->ue, &job, 1, &ccfg, &st->chest, st->stream) != MI355_SUCCESS)
       return SRSLTE_ERROR;
-    st->est_valid = true;
-    st->est_tti   = sf->tti;
-    fill_chest_res(q, st);
-    if (st->host_grids && (mi355::stage_copy(st->h_block, st->d_grid[0], bk.nb, st->side) != hipSuccess ||
-                           mi355::wait_stream(st->side) != hipSuccess))
-      return SRSLTE_ERROR;
-    return ue_run_ctrl(q, st, sf, cfg, q->pregen_rnti) == SRSLTE_SUCCESS ? SRSLTE_SUCCESS : SRSLTE_ERROR;
+  } else if (rf != MI355_SUCCESS && rf != MI355_ERROR_SECOND_STAGE) {
+    return SRSLTE_ERROR; // the estimation itself failed: reported, never re-run (its per-link state may have moved)
   }
+  // the estimation ran exactly once for this TTI: its results stand whichever later part failed
   st->est_valid = true;
   st->est_tti   = sf->tti;
   fill_chest_res(q, st);
+  if (st->host_grids && !back_done && // only the grid / estimate read-back failed or was not enqueued: redo it alone
+      (mi355::stage_copy(st->h_block, st->d_grid[0], bk.nb, st->side) != hipSuccess ||
+       mi355::wait_stream(st->side) != hipSuccess))
+    return SRSLTE_ERROR;
+  if (two_step || rf == MI355_ERROR_SECOND_STAGE) // the control stage alone, on the estimates just made
+    return ue_run_ctrl(q, st, sf, cfg, q->pregen_rnti) == SRSLTE_SUCCESS ? SRSLTE_SUCCESS : SRSLTE_ERROR;
   sf->cfi        = msf.cfi;
   st->ctrl_valid = true;
   st->ctrl_rnti  = rnti;

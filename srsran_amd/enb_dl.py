@@ -66,6 +66,7 @@ def _declare_gpu():
     L.mi355_channel_grid_batch_at.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), u32, u32, C.POINTER(C.c_float),
                                               C.c_float, C.c_uint64, C.c_uint64, vp]
     L.mi355_enb_synth_payloads.argtypes = [vp, vp, C.c_uint64, u32, u32, u32, C.c_uint64, vp]
+    L.mi355_enb_payload_check.argtypes = [vp, vp, C.c_size_t, C.c_uint64, u32, u32, u32, C.c_uint64, vp, vp]
     L.mi355_channel_fading_grid_batch.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), u32, u32, C.c_char_p,
                                                   C.POINTER(C.c_double), C.c_float, u32, vp]
     L._enb_gpu_declared = True
@@ -134,6 +135,13 @@ class EnbDl:
         """Device payloads of n subframes keyed by their global index (mi355_enb_synth_payloads)."""
         check(self.L.mi355_enb_synth_payloads(self.h, out, int(first_index), n, ntb, nbytes, int(seed) & (2**64 - 1),
                                               stream), "enb_synth_payloads")
+
+    def payload_check(self, rx: int, rx_stride: int, first_index: int, n: int, ntb: int, nbytes: int, seed: int,
+                      ok: int, stream=None):
+        """ok[i * ntb + t] (device bytes) = 1 iff the decoded bytes at rx + (i * ntb + t) * rx_stride equal the payload
+        synth_payloads made for subframe first_index + i, TB t (mi355_enb_payload_check; stream None: synchronous)."""
+        check(self.L.mi355_enb_payload_check(self.h, rx, rx_stride, int(first_index), n, ntb, nbytes,
+                                             int(seed) & (2**64 - 1), ok, stream), "enb_payload_check")
 
     def fading(self, tx, rx, nof_rx: int, model: str, t_sf, sigma: float, seed: int, stream=None):
         """Multipath fading (srslte_channel_fading_t: model "epa5", "eva70", "etu300", "none0" ...) + AWGN in the

@@ -110,5 +110,5 @@ def test_config4_total_subframes_two_resident_sets():
     assert res["resident_sets"] == 3
     assert res["crc_ok_tbs"] == "1200/1200"
     assert res["crc_bitmap"]["length_bits"] == 1200 and res["crc_bitmap"]["ok_tbs"] == 1200
-    ok, n = (int(v) for v in res["payload_checked_tbs"].split("/"))
-    assert ok == n > 0
+    assert res["payload_checked_tbs"] == "1200/1200"  # every TB's bytes, checked on the GPU after its call
+    assert res["config"]["workers_per_gpu"] == 3  # the PHY worker pool takes the resident sets' batches in turn

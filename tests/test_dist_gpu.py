@@ -39,9 +39,13 @@ def test_two_ranks_weak_scaling_on_one_gpu():
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
 def test_two_ranks_total_subframes_sharded_on_one_gpu():
-    """configs[4] plumbing with the real decode: 600 subframes over 2 ranks (300 each: batches of 256 + 44)."""
-    res = _run(["--gpus", "2", "--total-subframes", "600", "--subframes", "256", "--warmup", "1", "--workers", "1",
+    """configs[4] plumbing with the real decode: 600 subframes over 2 ranks (300 each: batches of 256 + 44, taken in
+    turn by 2 PHY workers per rank), every payload checked, per-rank host CPU reported."""
+    res = _run(["--gpus", "2", "--total-subframes", "600", "--subframes", "256", "--warmup", "1", "--workers", "2",
                 "--no-cpu", "--no-roofline", "--no-waterfall"])
     assert res["n_gpus"] == 2 and res["scaling"] == "strong"
     assert res["crc_ok_tbs"] == "1200/1200"
     assert res["crc_bitmap"]["subframes"] == 600 and res["crc_bitmap"]["ok_tbs"] == 1200
+    assert res["payload_checked_tbs"] == "1200/1200"
+    assert [p["subframes"] for p in res["per_rank"]] == [300, 300]
+    assert all(p["host_cpu_s"] > 0 and p["workers"] == 2 for p in res["per_rank"])

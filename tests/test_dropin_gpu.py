@@ -179,6 +179,40 @@ def test_ue_dl_drop_in_phy_dl_test_flow(case):
                 assert np.array_equal(pay[i, k, t, :nb], payload[t][:nb]), (name, i, k, t)
 
 
+def test_ctrl_stage_failure_does_not_rerun_estimation():
+    """srslte_ue_dl_decode_fft_estimate runs estimation + the control stage in one library call; when only the
+    control stage fails (MI355_ERROR_SECOND_STAGE, injected here on the first TTI), the drop-in re-runs the control
+    stage alone.  Re-running the estimation would advance the per-link estimator state (CFO average, noise
+    history) twice for one TTI, so every later TTI's estimates and decodes must equal a run without the fault."""
+    from srsran_amd import lib
+    L = _caller()
+    case = CASES[0]
+    name, nprb, ports, nrx, tm, fmt, mcs, alt, cid = case
+    rnti = 0x46
+    ttis = [10 * 7 + 0, 10 * 7 + 3, 10 * 8 + 6, 10 * 9 + 9]
+    iq, expect = _synth(case, ttis, rnti)
+    c = CallerCfg(nof_prb=nprb, nof_ports=ports, nof_rx=nrx, cell_id=cid, rnti=rnti, tm=tm, use_tbs_index_alt=int(alt),
+                  decoder_type=1, csi_enable=1, max_nof_iterations=10, cfo_estimate_enable=1, estimator_alg=0,
+                  noise_alg=0, sync_error_enable=0)
+    nsf, maxb = len(ttis), max(t for e in expect for t in e[0].tbs) // 8 + 16
+    tt = np.array(ttis, np.uint32)
+    fail = lib().mi355_debug_fail_ctrl_stages
+    lib().mi355_debug_fail_ctrl_stages.argtypes = [C.c_int]
+    lib().mi355_debug_fail_ctrl_stages.restype = C.c_int
+    runs = []
+    for nfail in (0, 1):
+        pay = np.zeros((nsf, 3, 2, maxb), np.uint8)
+        res = (SfRes * nsf)()
+        fail(nfail)
+        assert L.caller_ue_dl(C.byref(c), iq.ctypes.data, tt.ctypes.data, nsf, pay.ctypes.data, maxb, res) == 0
+        assert fail(0) == 0, "the injected control-stage failure was not consumed"
+        runs.append((bytes(res), pay))
+    assert runs[0][0] == runs[1][0], "a control-stage failure changed the estimates or decodes of later TTIs"
+    assert np.array_equal(runs[0][1], runs[1][1])
+    r = (SfRes * nsf).from_buffer_copy(runs[1][0])
+    assert all(r[i].ret_fft == 0 and r[i].nof_dci == 1 and r[i].crc[0] and r[i].crc[1] for i in range(nsf))
+
+
 def test_pdsch_drop_in_host_buffers_and_softbuffer_reuse():
     """srslte_pdsch_decode with a stand-alone object and host grids (pdsch_test.c:498); the second call on the same
     softbuffers skips every code block (cb_crc, sch.c:385) and restores bytes that were never saved (sch.c:462-484)."""

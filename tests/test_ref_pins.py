@@ -118,3 +118,21 @@ def test_smoothing_filter_auto_sigma_live():
         got = oracle.chest_filter(0, 0.0, 0.0, noise)
         want = oracle.ref_chest_filter(0, 4, noise * 200.0)
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32), err_msg=str(noise))
+
+
+@pytest.mark.skipif(not oracle.ref_available(), reason="oracle/_ref not built")
+@pytest.mark.parametrize("snr_db", [5.5, 5.7, 5.9, 6.0, 7.0, 9.0])
+def test_reference_early_stop_matches_oracle_decode_tb(snr_db):
+    """oracle.ref_dlsch_decode_cbs (bench's crc_parity_vs_avx2 checker: the reference's AVX2 decoder under sch.c's
+    per-CB early stop) == the oracle's decode_tb restatement, on a TM4 QAM256 TB (C = 16, K = 6144) from the waterfall
+    (some blocks fail) to the clean regime: TB CRC, payload, average half-iterations."""
+    rng = np.random.default_rng(int(snr_db * 10))
+    tbs, Qm, G = 97896, 8, 115200
+    payload, llr = oracle.make_tb(rng, tbs, Qm, G, 0, snr_db)
+    ret, data, its = oracle.dlsch_decode_tb(llr, tbs, Qm, 0, 10, oracle.Softbuffer())
+    bufs = np.stack([oracle.rm_turbo_rx(llr[c * 7200:(c + 1) * 7200], 6144, 0) for c in range(16)])
+    tb_ok, rdata, cb_ok, cb_its = oracle.ref_dlsch_decode_cbs(bufs, 6144, tbs, 10)
+    assert tb_ok == (ret == 0)
+    assert abs(cb_its.sum() / 16 - its) < 1e-5
+    if tb_ok:
+        assert np.array_equal(rdata[: tbs // 8], data[: tbs // 8]) and np.array_equal(rdata[: tbs // 8], payload)
