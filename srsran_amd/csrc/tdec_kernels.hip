@@ -239,6 +239,13 @@ __shared__ uint32_t tdec_stg_row[4][TDEC_SEG];                // their destinati
 #ifndef TDEC_CLONE_NO_CK
 #define TDEC_CLONE_NO_CK 0
 #endif
+// STG: segment t's staged output rows are stored right after segment t+1's loads are issued, not at the end of
+// segment t.  vmcnt counts loads and stores together in issue order, so a store issued before a load is waited for
+// with that load: flushed at the end of segment t, the stores sat in front of the next prefetch and every segment's
+// load wait also waited for the previous segment's stores to be acknowledged
+#ifndef TDEC_DEFER_FLUSH
+#define TDEC_DEFER_FLUSH 0
+#endif
 #ifndef TDEC_CLONE_NO_FIN
 #define TDEC_CLONE_NO_FIN 0
 #endif
@@ -679,6 +686,9 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     const int e  = FULL ? s0 + SEG : ((s0 + SEG < L) ? s0 + SEG : L);
     uint32_t  bits = 0; // decision bits of the segment: window 2l in bits 8..15, 2l+1 in 0..7 (MSB first)
     if (t + TDEC_FPF - 1 < nseg) load(t + TDEC_FPF - 1, nx, ny, na, nd, nc);
+    if constexpr (TDEC_DEFER_FLUSH) {
+      if (t > 0) flush(); // the previous segment's rows, behind this segment's prefetch
+    }
 
     v2s xin[SEG];
 #pragma unroll
@@ -802,7 +812,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
       }
     }
     }
-    flush();
+    if constexpr (!TDEC_DEFER_FLUSH) flush();
     if constexpr (wr_bits) { // turbodecoder_win.h:973-993: bit = LLR > 0, natural order, MSB first
       uint8_t* bb = (uint8_t*)bm + (size_t)(2 * l) * (L / 8) + t;
       bb[0]       = (uint8_t)(bits >> 8);
@@ -827,6 +837,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
     if (t + 1 < nseg) fseg(t + 1, nx, ny, na, nd, nc, cx, cy, ca, cd, cc);
   }
 #endif
+  if constexpr (TDEC_DEFER_FLUSH) flush(); // the last segment's rows
   if constexpr (wr_bm || wr_bits) { // the code block's K/8 decision bytes, 8-byte stores by its NL lanes
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
