@@ -90,6 +90,11 @@ struct mi355_dlsch {
   std::map<uint32_t, mi355_tdec_batch_t*> dec;         // one decoder workspace per K
   std::map<uint64_t, uint16_t*>          rm;           // (K << 2 | rv) -> device table
   std::map<uint64_t, uint16_t*>          rm8;          // the same for the 8-bit decoder layout
+  struct Compact {
+    uint16_t* d;
+    uint32_t  nq, qoff;
+  };
+  std::map<uint64_t, Compact>            rmc;          // (K, rv, E) -> compact image table (dlsch_rm_compact)
   std::map<uint32_t, mi355_tdec8_t*>     dec8;         // 8-bit decoder workspace per K
   std::map<uint32_t, uint32_t*>          scales;       // K -> per-lane CRC scale factors
   std::map<uint32_t, uint32_t*>          tb_scales;    // TB bytes -> per-thread CRC24A scale factors (epilogue)
@@ -529,6 +534,7 @@ void mi355_dlsch_destroy(mi355_dlsch_t* q)
   for (auto& kv : q->dec) mi355_tdec_batch_destroy(kv.second);
   for (auto& kv : q->rm) (void)hipFree(kv.second);
   for (auto& kv : q->rm8) (void)hipFree(kv.second);
+  for (auto& kv : q->rmc) (void)hipFree(kv.second.d);
   for (auto& kv : q->dec8) mi355_tdec8_destroy(kv.second);
   for (auto& kv : q->scales) (void)hipFree(kv.second);
   for (auto& kv : q->tb_scales) (void)hipFree(kv.second);
@@ -650,6 +656,53 @@ int mi355::dlsch_rm_inv(mi355_dlsch_t* q, uint32_t K, uint32_t rv, const uint16_
 }
 
 uint32_t mi355::dlsch_rm_buflen(uint32_t K) { return rm_buflen(K); }
+
+int mi355::dlsch_rm_compact(mi355_dlsch_t* q, uint32_t K, uint32_t rv, uint32_t E, const uint16_t** tab, uint32_t* nq,
+                            uint32_t* qoff)
+{
+  if (!q || rv > 3 || E == 0 || E > 3 * K + 12) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lock(q->mu);
+  CHECK_HIP(hipSetDevice(q->device));
+  const uint64_t key = ((((uint64_t)K << 2) | rv) << 16) | E;
+  auto           it  = q->rmc.find(key);
+  if (it == q->rmc.end()) {
+    const std::vector<uint16_t> t      = rm_rx_table(K, rv); // circular index r -> decoder position
+    const uint32_t              buflen = rm_buflen(K), nquad = (buflen + 7) / 8;
+    std::vector<uint16_t>       inv(buflen, (uint16_t)RM_NONE);
+    for (size_t r = 0; r < t.size(); r++) inv[t[r]] = (uint16_t)r;
+    // a parity row (16-window layout) is written iff one of its 16 positions receives an LLR r < E (rm_image.h)
+    auto defined = [&](uint32_t pos) {
+      if (tdec_subblocks(K) != 16) return true;
+      const uint32_t sl = K + 32, s = pos / sl;
+      if (s == 0 || s > 2) return true;
+      const uint32_t j = (pos - s * sl) >> 4;
+      if (j >= 32 * SB_ROWMASK_WORDS || j >= K / 16) return true;
+      for (uint32_t w = 0; w < 16; w++)
+        if (inv[s * sl + j * 16 + w] < E) return true;
+      return false;
+    };
+    std::vector<uint16_t> rank(nquad, 0xffff), qlist;
+    for (uint32_t qd = 0; qd < nquad; qd++)
+      if (defined(8 * qd)) rank[qd] = (uint16_t)qlist.size(), qlist.push_back((uint16_t)qd);
+    const uint32_t        off = (E + 7) / 8 * 8;
+    std::vector<uint16_t> all(off + qlist.size() + 8, 0);
+    for (uint32_t r = 0; r < E; r++) {
+      const uint32_t pos = t[r];
+      if (rank[pos / 8] == 0xffff) return MI355_ERROR; // (cannot happen: the quad holds LLR r < E)
+      all[r] = (uint16_t)(8 * rank[pos / 8] + pos % 8);
+    }
+    std::copy(qlist.begin(), qlist.end(), all.begin() + off);
+    uint16_t* d = nullptr;
+    CHECK_HIP(hipMalloc(&d, all.size() * 2));
+    CHECK_HIP(hipMemcpy(d, all.data(), all.size() * 2, hipMemcpyHostToDevice));
+    CHECK_HIP(hipStreamSynchronize(nullptr)); // (pageable source: landed before a non-blocking stream reads it)
+    it = q->rmc.emplace(key, mi355_dlsch::Compact{d, (uint32_t)qlist.size(), off}).first;
+  }
+  *tab  = it->second.d;
+  *nq   = it->second.nq;
+  *qoff = it->second.qoff;
+  return MI355_SUCCESS;
+}
 
 mi355::SoftbufferView mi355::softbuffer_view(mi355_softbuffer_pool_t* p)
 {

@@ -83,6 +83,10 @@ struct EqRmLayer {           // the transport block fed by one layer (codeword)
 struct EqRmJob {
   uint32_t  C, Qm, Gp; // code blocks (same in both codewords), bits per symbol, nof_e_bits / Qm
   EqRmLayer layer[2];  // by layer; a layer without a transport block to decode has J.cw[l] == nullptr
+  // the compact decoder-order image of layer 0's (K, rv) (dlsch_rm_compact) for [kx][E variant: n_e0, n_e0 + Qm]:
+  // LLR r -> image slot cmp[r], quad i of the image -> decoder quad cmp[cqoff + i], cnq quads (nullptr: not built)
+  const uint16_t* cmp[2][2];
+  uint32_t        cnq[2][2], cqoff[2][2];
 };
 struct EqRmPool {
   int16_t*       sb;
@@ -93,7 +97,8 @@ struct EqRmPool {
   int            diag = 0; // measurement only (MI355_EQRM_DIAG): 1 = no rate dematching, 2 = no equalisation (wrong results)
   unsigned long long* prof = nullptr; // measurement only (mi355_pdsch_eqrm_profile): per-workgroup phase cycle sums
 };
+// img: the largest E of the batch; cimg: int16 of its largest compact image (0: none)
 hipError_t pdsch_launch_eq_rm(const PdschJobDev* jobs, const EqRmJob* rj, uint32_t njobs, uint32_t max_c, uint32_t img,
-                              const uint32_t* keys, uint32_t nkeys, const EqRmPool& pool, hipStream_t s);
+                              uint32_t cimg, const uint32_t* keys, uint32_t nkeys, const EqRmPool& pool, hipStream_t s);
 
 } // namespace mi355

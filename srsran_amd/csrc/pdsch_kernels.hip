@@ -1061,6 +1061,38 @@ template <int QM> __device__ __forceinline__ void img_put(int16_t* im, uint32_t 
     if (b + k < n_e) im[img_i16(b + k)] = o[k];
 }
 
+// the compact image (dlsch_rm_compact): the slots of a pair's 2 QM LLRs at span offset b, loaded with the pair's map
+// word when the pair lies inside the span (QM 8: two 16-byte loads; b is a multiple of 8), else per LLR at the store
+constexpr int ER_CQ = 4; // compact quads per thread whose decoder positions are loaded together
+struct CmpSlots {
+  uint4 v[2];
+  bool  whole;
+};
+template <int QM> __device__ __forceinline__ CmpSlots cmp_slots(const GLB uint16_t* fw, uint32_t b, uint32_t n_e)
+{
+  CmpSlots s{};
+  s.whole = QM == 8 && b < n_e && b + 2 * QM <= n_e;
+  if (s.whole) {
+    s.v[0] = ldg_u4((const GLB uint32_t*)(fw + b));
+    s.v[1] = ldg_u4((const GLB uint32_t*)(fw + b + 8));
+  }
+  return s;
+}
+template <int QM>
+__device__ __forceinline__ void cmp_put(int16_t* im, const GLB uint16_t* fw, const CmpSlots& s, uint32_t b, uint32_t n_e,
+                                        const int16_t (&o)[2 * QM])
+{
+  if (s.whole) {
+    const uint32_t w[8] = {s.v[0].x, s.v[0].y, s.v[0].z, s.v[0].w, s.v[1].x, s.v[1].y, s.v[1].z, s.v[1].w};
+#pragma unroll
+    for (int k = 0; k < 2 * QM; k++) im[(w[k >> 1] >> (16 * (k & 1))) & 0xffffu] = o[k];
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 2 * QM; k++)
+    if (b + k < n_e) im[fw[b + k]] = o[k];
+}
+
 template <int QM0, int QM1>
 #ifndef PDSCH_ER_WAVES
 #define PDSCH_ER_WAVES 5
@@ -1116,6 +1148,23 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     cwd[tid] = *J.cw[tid];
     cmb[tid] = cwd[tid].csi_enable ? *gptr(cwd[tid].cmax_final) : 0u;
   }
+  // the usual rate-dematching case: two fresh buffers sharing one table (lean).  With the empty parity rows left
+  // unwritten (P.sparse) and its compact table built, the LLRs are scattered straight into a decoder-order image of
+  // the quads that are written (cm: dlsch_rm_compact), zeroed first, and the rate dematching becomes a stream of
+  // 16-byte image reads and softbuffer stores -- no table pass, no gathers through the inverse table
+  const uint32_t kx0 = c < R.layer[0].C1 ? 0u : 1u, kx1 = c < R.layer[1].C1 ? 0u : 1u;
+  const bool     lean = need[0] && need[1] && fresh[0] && fresh[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
+                    R.layer[0].buflen[kx0] == R.layer[1].buflen[kx1];
+  const uint32_t ev = c > R.C - gamma ? 1u : 0u;
+  const bool     cm = lean && P.sparse && R.cmp[kx0][ev] != nullptr;
+  const GLB uint16_t* fw = cm ? gptr(R.cmp[kx0][ev]) : nullptr;
+  const uint32_t      cnq = cm ? R.cnq[kx0][ev] : 0u;
+  if (cm) {
+    for (uint32_t i = tid; i < cnq; i += ER_THREADS) {
+      ((uint4*)imgs)[i]         = make_uint4(0u, 0u, 0u, 0u);
+      ((uint4*)(imgs + img))[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
   __syncthreads();
   const unsigned long long pt1 = P.prof ? clock64() : 0ull;
   // equalise the RE pairs overlapping the span; keep the span's LLRs
@@ -1128,9 +1177,6 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   h_ptrs(J, hp);
   // the usual rate-dematching case (two fresh buffers sharing one table, below): its first round of table words does
   // not depend on the equaliser, so it is loaded now and arrives while the RE pairs are equalised
-  const uint32_t kx0 = c < R.layer[0].C1 ? 0u : 1u, kx1 = c < R.layer[1].C1 ? 0u : 1u;
-  const bool     lean = need[0] && need[1] && fresh[0] && fresh[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
-                    R.layer[0].buflen[kx0] == R.layer[1].buflen[kx1];
   uint4 iv0[ER_Q];
   if constexpr (ER_TPF) {
     if (lean) {
@@ -1176,6 +1222,9 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
       const uint32_t pr = pr0 + f * ER_THREADS;
       if (pr >= p1) continue;
       const uint32_t ns = min(2u, J.nof_re - 2 * pr);
+      // the compact image slots of the pair's LLRs (whole pairs inside the span): in flight during the MMSE math
+      CmpSlots       fws[1];
+      if (cm) fws[0] = cmp_slots<(QM0 ? QM0 : QM1)>(fw, 2 * pr * (QM0 ? QM0 : QM1) - rp, n_e);
       cf             xs[2][2];
       float          cs[2][2];
 #pragma unroll
@@ -1185,18 +1234,26 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
         const float csi[2] = {cs[0][0], cs[0][1]};
         int16_t     o[2 * QM0];
         llr_compute<QM0>(cwd[0], pr, ns, x, csi, cmb[0], o);
-        img_put<QM0>(imgs, 2 * pr * QM0 - rp, n_e, o);
+        if (cm) {
+          cmp_put<QM0>(imgs, fw, fws[0], 2 * pr * QM0 - rp, n_e, o);
+        } else {
+          img_put<QM0>(imgs, 2 * pr * QM0 - rp, n_e, o);
+        }
       }
       if constexpr (QM1 != 0) {
         const cf    x[2]   = {xs[1][0], xs[1][1]};
         const float csi[2] = {cs[1][0], cs[1][1]};
         int16_t     o[2 * QM1];
         llr_compute<QM1>(cwd[1], pr, ns, x, csi, cmb[1], o);
-        img_put<QM1>(imgs + img, 2 * pr * QM1 - rp, n_e, o);
+        if (cm) { // (lean: one modulation, the same image slots)
+          cmp_put<QM1>(imgs + img, fw, fws[0], 2 * pr * QM1 - rp, n_e, o);
+        } else {
+          img_put<QM1>(imgs + img, 2 * pr * QM1 - rp, n_e, o);
+        }
       }
     }
   }
-  if (tid < 2) imgs[tid * img + n_e] = 0; // the zero slot: table entries without an LLR (RM_NONE, >= n_e) read it
+  if (tid < 2 && !cm) imgs[tid * img + n_e] = 0; // the zero slot: table entries without an LLR (RM_NONE, >= n_e)
   __syncthreads();
   const unsigned long long pt2 = P.prof ? clock64() : 0ull;
   if (P.diag == 1) {
@@ -1206,7 +1263,41 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   // rate dematching of each layer's image into its softbuffer (dlsch_rm_rx's gather, E <= N); both layers through
   // one pass when they share the table (same K and rv: the usual case), so the table is read and decoded once
   {
-    if (lean) {
+    if (cm) {
+      // the compact image in decoder order: quad i (16 bytes) of each layer's image to decoder quad cmp[cqoff + i]
+      const GLB uint16_t* ql     = fw + R.cqoff[kx0][ev];
+      const uint32_t      npairs = R.layer[0].buflen[kx0] / 2;
+      GLB uint32_t*       sb[2]  = {(GLB uint32_t*)gptr(P.sb + (size_t)slot[0] * P.sb_stride),
+                                    (GLB uint32_t*)gptr(P.sb + (size_t)slot[1] * P.sb_stride)};
+      const bool          al     = (((uintptr_t)sb[0] | (uintptr_t)sb[1]) & 15) == 0;
+      typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+#pragma unroll 1
+      for (uint32_t q0 = tid; q0 < cnq; q0 += ER_CQ * ER_THREADS) {
+        uint32_t qd[ER_CQ];
+#pragma unroll
+        for (int k = 0; k < ER_CQ; k++) {
+          const uint32_t qi = q0 + k * ER_THREADS;
+          qd[k]             = qi < cnq ? (uint32_t)ql[qi] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < ER_CQ; k++) {
+          const uint32_t qi = q0 + k * ER_THREADS;
+          if (qi >= cnq) continue;
+          const uint4    v0 = ((const uint4*)imgs)[qi], v1 = ((const uint4*)(imgs + img))[qi];
+          const uint32_t i  = 4 * qd[k];
+          if (al && i + 3 < npairs) {
+            __builtin_nontemporal_store((u4v){v0.x, v0.y, v0.z, v0.w}, (GLB u4v*)(sb[0] + i));
+            __builtin_nontemporal_store((u4v){v1.x, v1.y, v1.z, v1.w}, (GLB u4v*)(sb[1] + i));
+          } else {
+            const uint32_t a0[4] = {v0.x, v0.y, v0.z, v0.w}, a1[4] = {v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+            for (int cc = 0; cc < 4; cc++)
+              if (i + cc < npairs) sb[0][i + cc] = a0[cc], sb[1][i + cc] = a1[cc];
+          }
+        }
+      }
+      need[0] = need[1] = false; // done
+    } else if (lean) {
       // the usual case, two fresh buffers: every position is written, a missing LLR reads the zero slot
       const uint32_t  npairs = R.layer[0].buflen[kx0] / 2, Kc = (R.layer[0].N[kx0] - 12) / 3;
       const GLB uint32_t* inv32 = (const GLB uint32_t*)gptr(R.layer[0].inv[kx0]);
@@ -1411,10 +1502,11 @@ static void launch_eq_rm_1(uint32_t qm1, const dim3& g, size_t lds, const PdschJ
 }
 
 hipError_t pdsch_launch_eq_rm(const PdschJobDev* jobs, const EqRmJob* rj, uint32_t njobs, uint32_t max_c, uint32_t img,
-                              const uint32_t* keys, uint32_t nkeys, const EqRmPool& pool, hipStream_t s)
+                              uint32_t cimg, const uint32_t* keys, uint32_t nkeys, const EqRmPool& pool, hipStream_t s)
 {
   if (!njobs || !max_c) return hipSuccess;
-  img = img_elems(img + 1); // int16 per layer image + the zero slot, 16-byte multiple
+  // int16 per layer image: the circular-order image + the zero slot, or the compact decoder-order one (16-byte multiple)
+  img = std::max(img_elems(img + 1), img_elems(cimg));
   hipLaunchKernelGGL(pdsch_csimax_cols, dim3(njobs), dim3(256), 0, s, jobs);
   const size_t lds = 2 * (size_t)img * sizeof(int16_t);
   for (uint32_t k = 0; k < nkeys; k++) {

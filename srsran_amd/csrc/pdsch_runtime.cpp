@@ -176,7 +176,7 @@ struct JobPlan {
 // a batch decoded through pdsch_eq_rm (pdsch_internal.h)
 struct EqRmPlan {
   std::vector<EqRmJob> rj;
-  uint32_t             max_c = 0, img = 0;
+  uint32_t             max_c = 0, img = 0, cimg = 0;
   EqRmPool             pool{};
 };
 
@@ -557,7 +557,7 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   q->e_pending = er != nullptr;
   if (er) {
     CHECK_HIP(pdsch_launch_eq_rm((const PdschJobDev*)(base + o_jobs), (const EqRmJob*)(base + o_rj), njobs, er->max_c,
-                                 er->img, fkeys.data(), (uint32_t)fkeys.size(), er->pool, s));
+                                 er->img, er->cimg, fkeys.data(), (uint32_t)fkeys.size(), er->pool, s));
     q->last_jobs_dev = (const PdschJobDev*)(base + o_jobs), q->last_njobs = njobs, q->last_max_fpairs = max_fpairs;
     q->last_fkeys = fkeys;
   }
@@ -736,7 +736,13 @@ static bool plan_eq_rm(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi
   if (getenv("MI355_NO_EQRM") || q->llr8 || !pool || plans.empty()) return false;
   const SoftbufferView v = softbuffer_view(pool);
   er.rj.assign(plans.size(), EqRmJob{});
-  er.max_c = er.img = 0;
+  er.max_c = er.img = er.cimg = 0;
+  // (MI355_EQRM_COMPACT=0, A/B timing: the lean path gathers through the inverse table instead)
+  static const bool compact = !getenv("MI355_EQRM_COMPACT") || atoi(getenv("MI355_EQRM_COMPACT")) != 0;
+  struct CKey {
+    uint32_t        key = UINT32_MAX, E = 0, nq = 0, qoff = 0;
+    const uint16_t* tab = nullptr;
+  } ck[4]; // the last compact tables looked up (a batch has few (K, rv, E))
   // a batch has few distinct TB sizes and (K, rv): segmentation and table look-ups of the previous TB are reused
   uint32_t        seg_tbs = UINT32_MAX, tab_key[2] = {UINT32_MAX, UINT32_MAX};
   CbSegm          seg{};
@@ -781,6 +787,27 @@ static bool plan_eq_rm(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi
       }
       L.C1    = seg.C1;
       L.slot0 = cfg.softbuffer[t] * v.max_cb;
+      if (compact && rm_sparse_writes() && &L == &R.layer[0]) {
+        const uint32_t ne0 = qm * (R.Gp / seg.C), gamma = R.Gp % seg.C;
+        for (uint32_t kx = 0; kx < 2; kx++) {
+          const uint32_t K = kx ? seg.K2 : seg.K1;
+          if (!K || (kx == 0 && !seg.C1) || (kx == 1 && seg.C1 == seg.C)) continue;
+          for (uint32_t ev = 0; ev < (gamma ? 2u : 1u); ev++) {
+            const uint32_t E = ne0 + ev * qm, key = K << 2 | tb.rv;
+            CKey*          hit = nullptr;
+            for (auto& c : ck)
+              if (c.key == key && c.E == E) hit = &c;
+            if (!hit) {
+              for (int k = 3; k > 0; k--) ck[k] = ck[k - 1];
+              hit = &ck[0];
+              if (dlsch_rm_compact(q->dlsch, K, tb.rv, E, &hit->tab, &hit->nq, &hit->qoff)) return false;
+              hit->key = key, hit->E = E;
+            }
+            R.cmp[kx][ev] = hit->tab, R.cnq[kx][ev] = hit->nq, R.cqoff[kx][ev] = hit->qoff;
+            er.cimg       = std::max(er.cimg, 8 * hit->nq);
+          }
+        }
+      }
     }
     er.max_c = std::max(er.max_c, nt ? R.C : 0u);
     er.img   = std::max(er.img, n_max);
