@@ -246,6 +246,14 @@ __shared__ uint32_t tdec_stg_row[4][TDEC_SEG];                // their destinati
 #ifndef TDEC_DEFER_FLUSH
 #define TDEC_DEFER_FLUSH 0
 #endif
+// non-temporal (streaming) stores for the staged output rows (NT_OUT) and the beta checkpoints (NT_CK): neither is
+// re-read inside the launch by anyone but the storing wave (checkpoints) or at all (outputs, read by the next launch)
+#ifndef TDEC_NT_OUT
+#define TDEC_NT_OUT 0
+#endif
+#ifndef TDEC_NT_CK
+#define TDEC_NT_CK 0
+#endif
 #ifndef TDEC_CLONE_NO_FIN
 #define TDEC_CLONE_NO_FIN 0
 #endif
@@ -456,7 +464,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   // ckpt[nseg-1] = row L (not normalised)
 #pragma unroll
   for (int s = 0; s < 8; s++) {
-    if constexpr (DIAG == 9) {
+    if constexpr (DIAG == 9 || TDEC_NT_CK) {
       __builtin_nontemporal_store(W(st[s]), &ck[((size_t)(nseg - 1) * 8 + s) * 64]);
     } else {
       ck[((size_t)(nseg - 1) * 8 + s) * 64] = W(st[s]);
@@ -517,7 +525,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
           if (i == 0 && t > 0 && DIAG != 3 && !(CL && TDEC_CLONE_NO_CK) && !(CL && TDEC_CLONE_CK_HALF && (t & 1))) {
 #pragma unroll
             for (int s = 0; s < 8; s++) {
-              if constexpr (DIAG == 9) {
+              if constexpr (DIAG == 9 || TDEC_NT_CK) {
                 __builtin_nontemporal_store(W(st[s]), &ck[((size_t)(t - 1) * 8 + s) * 64]);
               } else if constexpr (DIAG == 10) { // every other checkpoint only
                 if (t & 1) ck[((size_t)(t - 1) * 8 + s) * 64] = W(st[s]);
@@ -599,7 +607,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   // them: 1.26 -> 0.82 ms per 65,536-CB launch, profiles/r05/clone_ab.txt).  STG (whole segments): the 8 steps' outputs
   // are staged in LDS as the 8 rows they fill, [step][128 windows], and each code block's own lanes store its 32-byte
   // slices of those rows as 16-byte pieces, two store instructions per segment instead of sixteen.
-  constexpr bool STG = FULL && !GI && TDEC_STAGE_OUT && (dec2 ? wr_a1 : wr_e);
+  constexpr bool STG = FULL && !GI && TDEC_STAGE_OUT && (dec2 ? wr_a1 : wr_e) && !(CL && TDEC_CLONE_NO_E);
   int16_t*       O16 = dec2 ? A16 : E16;
   int16_t*       stg = nullptr;
   uint32_t*      stg_row = nullptr;
@@ -629,7 +637,12 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
         const int      idx = k * NL + l, r = idx / PPR, pc = idx % PPR;
         const uint32_t jr  = stg_row[r]; // the destination row of step r (shared by every window of it)
         const uint4    v   = *(const uint4*)(stg + r * 128 + 2 * lane0 + pc * 8);
-        *(uint4*)(O16 + (size_t)jr * 128 + 2 * lane0 + pc * 8) = v;
+        if constexpr (TDEC_NT_OUT) {
+          typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store((u4v){v.x, v.y, v.z, v.w}, (u4v*)(O16 + (size_t)jr * 128 + 2 * lane0 + pc * 8));
+        } else {
+          *(uint4*)(O16 + (size_t)jr * 128 + 2 * lane0 + pc * 8) = v;
+        }
       }
       // (the next segment's LDS writes follow these reads in the wave's in-order LDS queue; the fence keeps the
       // compiler from moving them above)
