@@ -1322,7 +1322,7 @@ def waterfall(args, cell, B, src, rx, pg, local, world):
     return out
 
 
-def avx2_crc_parity(src, rx, S_max=64, max_half=10, K=6144, C=16):
+def avx2_crc_parity(src, rx, S_max=64, max_half=10, K=6144, ncb_tb=16):
     """Decoded-CRC parity of the GPU against the reference's AVX2 chain where code blocks fail:
     the first S resident subframes of the waterfall batch the GPU just decoded (EPA 28 dB, ~1/3 of the TBs fail) go
     through the CPU front end with the reference's own AVX2 stages (srslte_predecoding_type MMSE + CSI,
@@ -1385,7 +1385,7 @@ def avx2_crc_parity(src, rx, S_max=64, max_half=10, K=6144, C=16):
             ok_ref += tb_ok
             same_crc = tb_ok == bool(g_crc[t])
             same_pay = (not tb_ok) or np.array_equal(data[:NB], g_pay[t])
-            same_its = abs(float(cb_its.sum()) / C - g_its[t]) < 1e-4
+            same_its = abs(float(cb_its.sum()) / ncb_tb - g_its[t]) < 1e-4
             same_cb = np.array_equal(cb_ok, g_cb[t] != 0)
             tb_agree += same_crc
             pay_agree += same_crc and same_pay
@@ -1394,12 +1394,12 @@ def avx2_crc_parity(src, rx, S_max=64, max_half=10, K=6144, C=16):
             if not (same_crc and same_pay and same_its and same_cb):
                 d = np.abs(cpu_bufs[t][:, cols].astype(np.int32) - gpu_bufs[t][:, cols].astype(np.int32))
                 dis.append({"tb": t, "ref_crc": tb_ok, "gpu_crc": bool(g_crc[t]),
-                            "ref_half_its": round(float(cb_its.sum()) / C, 4), "gpu_half_its": round(g_its[t], 4),
+                            "ref_half_its": round(float(cb_its.sum()) / ncb_tb, 4), "gpu_half_its": round(g_its[t], 4),
                             "cbs_flag_differ": [int(c) for c in np.nonzero(cb_ok != (g_cb[t] != 0))[0]],
                             "softbuffer_entries_differing": int((d > 0).sum()), "max_abs_llr_diff": int(d.max())})
         legs[leg] = {"tbs": 2 * S, "ref_crc_ok": ok_ref, "gpu_crc_ok": int(g_crc.sum()),
                      "tb_crc_agree": tb_agree, "payload_agree": pay_agree, "tb_iterations_agree": its_agree,
-                     "cb_crc_flags_agree": f"{cb_agree}/{2 * S * C}", "disagreements": dis[:24],
+                     "cb_crc_flags_agree": f"{cb_agree}/{2 * S * ncb_tb}", "disagreements": dis[:24],
                      "disagreeing_tbs": len(dis)}
     d_all = np.abs(cpu_bufs[:, :, cols].astype(np.int32) - gpu_bufs[:, :, cols].astype(np.int32))
     dis = legs["avx2_chain"]["disagreements"]

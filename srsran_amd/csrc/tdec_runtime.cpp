@@ -141,7 +141,8 @@ static size_t ws_bytes(const Geometry& g, uint32_t n, bool cbk = false)
   if (cbk) return (size_t)n * 5 * TDEC_GEN_CB_KP(g.K) * 2 + 256;
   if (g.nsb) {
     const size_t arr = (size_t)g.ngrp * g.Lp * 64 * 4;
-    return 3 * arr + (size_t)g.ngrp * g.nseg * 8 * 64 * 4 + 8 * 256;
+    static const size_t pad = getenv("MI355_TDEC_WS_PAD") ? (size_t)atoll(getenv("MI355_TDEC_WS_PAD")) : 0;
+    return 3 * (arr + pad) + (size_t)g.ngrp * g.nseg * 8 * 64 * 4 + 8 * 256 + 3 * 256;
   }
   const size_t arr = (size_t)g.npair * g.Kp * 4;
   return 6 * arr + (size_t)g.npair * 16 + (size_t)g.npair * g.nseg * 32 + 8 * 256;
@@ -297,9 +298,12 @@ int mi355_tdec_run_internal(mi355_tdec_batch_t* q, const TdecRun& rq)
 
   if (g.nsb) {
     const size_t arr = (size_t)g.ngrp * g.Lp * 64 * 4;
-    auto*        A1  = (uint32_t*)carve(arr);
-    auto*        E   = (uint32_t*)carve(arr);
-    auto*        D   = (uint32_t*)carve(arr);
+    // (MI355_TDEC_WS_PAD=<bytes>, measurement: a gap between the workspace arrays, to test address aliasing of the
+    // a-priori / extrinsic streams)
+    static const size_t pad = getenv("MI355_TDEC_WS_PAD") ? (size_t)atoll(getenv("MI355_TDEC_WS_PAD")) : 0;
+    auto*        A1  = (uint32_t*)carve(arr + pad);
+    auto*        E   = (uint32_t*)carve(arr + pad);
+    auto*        D   = (uint32_t*)carve(arr + pad);
     auto*        CK  = (uint32_t*)carve((size_t)g.ngrp * g.nseg * 8 * 64 * 4);
 
     // the decisions of the last half-iteration are packed into bytes by the MAP kernel itself when the windows
