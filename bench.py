@@ -1382,14 +1382,14 @@ def avx2_crc_parity(src, rx, S_max=64, max_half=10, K=6144, ncb_tb=16):
         for t in range(2 * S):
             tb_ok, data, cb_ok, cb_its = oracle.ref_dlsch_decode_cbs(np.ascontiguousarray(bufs[t]), K, TBS, max_half,
                                                                     dec)
-            ok_ref += tb_ok
+            ok_ref += int(tb_ok)
             same_crc = tb_ok == bool(g_crc[t])
             same_pay = (not tb_ok) or np.array_equal(data[:NB], g_pay[t])
             same_its = abs(float(cb_its.sum()) / ncb_tb - g_its[t]) < 1e-4
             same_cb = np.array_equal(cb_ok, g_cb[t] != 0)
-            tb_agree += same_crc
-            pay_agree += same_crc and same_pay
-            its_agree += same_its
+            tb_agree += int(same_crc)
+            pay_agree += int(same_crc and same_pay)
+            its_agree += int(same_its)
             cb_agree += int((cb_ok == (g_cb[t] != 0)).sum())
             if not (same_crc and same_pay and same_its and same_cb):
                 d = np.abs(cpu_bufs[t][:, cols].astype(np.int32) - gpu_bufs[t][:, cols].astype(np.int32))
@@ -1717,7 +1717,8 @@ def main():
     else:
         res = run_pdsch(args, world, rank, local, pg)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        # (numpy scalars in the result -- counts, flags -- as plain JSON numbers)
+        print(json.dumps(res, default=lambda o: o.item() if hasattr(o, "item") else str(o)), flush=True)
     if pg is not None:
         pg.destroy_process_group()
 

@@ -681,17 +681,25 @@ int mi355::dlsch_rm_compact(mi355_dlsch_t* q, uint32_t K, uint32_t rv, uint32_t 
         if (inv[s * sl + j * 16 + w] < E) return true;
       return false;
     };
-    std::vector<uint16_t> rank(nquad, 0xffff), qlist;
-    for (uint32_t qd = 0; qd < nquad; qd++)
-      if (defined(8 * qd)) rank[qd] = (uint16_t)qlist.size(), qlist.push_back((uint16_t)qd);
-    const uint32_t        off = (E + 7) / 8 * 8;
-    std::vector<uint16_t> all(off + qlist.size() + 8, 0);
+    // quad entries: decoder quad index | (bit p: position 8 q + p receives an LLR r < E) << 16; the image slots of the
+    // other positions are never written, and the rate dematcher masks them to zero
+    std::vector<uint16_t> rank(nquad, 0xffff);
+    std::vector<uint32_t> qlist;
+    for (uint32_t qd = 0; qd < nquad; qd++) {
+      if (!defined(8 * qd)) continue;
+      uint32_t m = 0;
+      for (uint32_t p = 0; p < 8 && 8 * qd + p < buflen; p++) m |= (uint32_t)(inv[8 * qd + p] < E) << p;
+      rank[qd] = (uint16_t)qlist.size();
+      qlist.push_back(qd | m << 16);
+    }
+    const uint32_t        off = (E + 7) / 8 * 8; // u16 offset of the quad entries (16-byte aligned)
+    std::vector<uint16_t> all(off + 2 * qlist.size() + 8, 0);
     for (uint32_t r = 0; r < E; r++) {
       const uint32_t pos = t[r];
       if (rank[pos / 8] == 0xffff) return MI355_ERROR; // (cannot happen: the quad holds LLR r < E)
       all[r] = (uint16_t)(8 * rank[pos / 8] + pos % 8);
     }
-    std::copy(qlist.begin(), qlist.end(), all.begin() + off);
+    memcpy(all.data() + off, qlist.data(), qlist.size() * 4);
     uint16_t* d = nullptr;
     CHECK_HIP(hipMalloc(&d, all.size() * 2));
     CHECK_HIP(hipMemcpy(d, all.data(), all.size() * 2, hipMemcpyHostToDevice));

@@ -84,7 +84,8 @@ struct EqRmJob {
   uint32_t  C, Qm, Gp; // code blocks (same in both codewords), bits per symbol, nof_e_bits / Qm
   EqRmLayer layer[2];  // by layer; a layer without a transport block to decode has J.cw[l] == nullptr
   // the compact decoder-order image of layer 0's (K, rv) (dlsch_rm_compact) for [kx][E variant: n_e0, n_e0 + Qm]:
-  // LLR r -> image slot cmp[r], quad i of the image -> decoder quad cmp[cqoff + i], cnq quads (nullptr: not built)
+  // LLR r -> image slot cmp[r]; quad i of the image -> u32 at cmp + cqoff + 2 i (decoder quad | LLR mask << 16);
+  // cnq quads (nullptr: not built)
   const uint16_t* cmp[2][2];
   uint32_t        cnq[2][2], cqoff[2][2];
 };

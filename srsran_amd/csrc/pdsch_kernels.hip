@@ -1078,19 +1078,21 @@ template <int QM> __device__ __forceinline__ CmpSlots cmp_slots(const GLB uint16
   }
   return s;
 }
+// both layers' LLRs of the pair into the interleaved u32 image (layer 0 in the low half)
 template <int QM>
-__device__ __forceinline__ void cmp_put(int16_t* im, const GLB uint16_t* fw, const CmpSlots& s, uint32_t b, uint32_t n_e,
-                                        const int16_t (&o)[2 * QM])
+__device__ __forceinline__ void cmp_put2(uint32_t* im, const GLB uint16_t* fw, const CmpSlots& s, uint32_t b, uint32_t n_e,
+                                         const int16_t (&o0)[2 * QM], const int16_t (&o1)[2 * QM])
 {
+  auto wd = [&](int k) { return (uint32_t)(uint16_t)o0[k] | ((uint32_t)(uint16_t)o1[k] << 16); };
   if (s.whole) {
     const uint32_t w[8] = {s.v[0].x, s.v[0].y, s.v[0].z, s.v[0].w, s.v[1].x, s.v[1].y, s.v[1].z, s.v[1].w};
 #pragma unroll
-    for (int k = 0; k < 2 * QM; k++) im[(w[k >> 1] >> (16 * (k & 1))) & 0xffffu] = o[k];
+    for (int k = 0; k < 2 * QM; k++) im[(w[k >> 1] >> (16 * (k & 1))) & 0xffffu] = wd(k);
     return;
   }
 #pragma unroll
   for (int k = 0; k < 2 * QM; k++)
-    if (b + k < n_e) im[fw[b + k]] = o[k];
+    if (b + k < n_e) im[fw[b + k]] = wd(k);
 }
 
 template <int QM0, int QM1>
@@ -1148,24 +1150,20 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     cwd[tid] = *J.cw[tid];
     cmb[tid] = cwd[tid].csi_enable ? *gptr(cwd[tid].cmax_final) : 0u;
   }
+  __syncthreads();
   // the usual rate-dematching case: two fresh buffers sharing one table (lean).  With the empty parity rows left
   // unwritten (P.sparse) and its compact table built, the LLRs are scattered straight into a decoder-order image of
-  // the quads that are written (cm: dlsch_rm_compact), zeroed first, and the rate dematching becomes a stream of
-  // 16-byte image reads and softbuffer stores -- no table pass, no gathers through the inverse table
+  // the quads that are written (cm: dlsch_rm_compact), both layers interleaved as one u32 per position (layer 0 in
+  // the low half), and the rate dematching becomes a stream of image reads and 16-byte softbuffer stores, positions
+  // without an LLR masked to zero -- no table pass, no gathers through the inverse table, no zero fill
   const uint32_t kx0 = c < R.layer[0].C1 ? 0u : 1u, kx1 = c < R.layer[1].C1 ? 0u : 1u;
   const bool     lean = need[0] && need[1] && fresh[0] && fresh[1] && R.layer[0].inv[kx0] == R.layer[1].inv[kx1] &&
                     R.layer[0].buflen[kx0] == R.layer[1].buflen[kx1];
   const uint32_t ev = c > R.C - gamma ? 1u : 0u;
-  const bool     cm = lean && P.sparse && R.cmp[kx0][ev] != nullptr;
-  const GLB uint16_t* fw = cm ? gptr(R.cmp[kx0][ev]) : nullptr;
+  const bool     cm = lean && P.sparse && QM0 == QM1 && R.cmp[kx0][ev] != nullptr;
+  const GLB uint16_t* fw  = cm ? gptr(R.cmp[kx0][ev]) : nullptr;
   const uint32_t      cnq = cm ? R.cnq[kx0][ev] : 0u;
-  if (cm) {
-    for (uint32_t i = tid; i < cnq; i += ER_THREADS) {
-      ((uint4*)imgs)[i]         = make_uint4(0u, 0u, 0u, 0u);
-      ((uint4*)(imgs + img))[i] = make_uint4(0u, 0u, 0u, 0u);
-    }
-  }
-  __syncthreads();
+  uint32_t* const     im32 = (uint32_t*)imgs; // (cm) [slot] = layer 0 | layer 1 << 16
   const unsigned long long pt1 = P.prof ? clock64() : 0ull;
   // equalise the RE pairs overlapping the span; keep the span's LLRs
   const float         noise = J.noise_dev ? *gptr(J.noise_dev) : J.noise;
@@ -1229,27 +1227,30 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
       float          cs[2][2];
 #pragma unroll
       for (int e = 0; e < 2; e++) eq_re(J, H[f][e], Y[f][e], noise, xs[0][e], xs[1][e], cs[0][e], cs[1][e]);
+      if constexpr (QM0 != 0 && QM0 == QM1) {
+        if (cm) { // both layers' LLRs of a position in one u32 image word
+          const cf    x0[2] = {xs[0][0], xs[0][1]}, x1[2] = {xs[1][0], xs[1][1]};
+          const float c0[2] = {cs[0][0], cs[0][1]}, c1[2] = {cs[1][0], cs[1][1]};
+          int16_t     o0[2 * QM0], o1[2 * QM0];
+          llr_compute<QM0>(cwd[0], pr, ns, x0, c0, cmb[0], o0);
+          llr_compute<QM0>(cwd[1], pr, ns, x1, c1, cmb[1], o1);
+          cmp_put2<QM0>(im32, fw, fws[0], 2 * pr * QM0 - rp, n_e, o0, o1);
+          continue;
+        }
+      }
       if constexpr (QM0 != 0) {
         const cf    x[2]   = {xs[0][0], xs[0][1]};
         const float csi[2] = {cs[0][0], cs[0][1]};
         int16_t     o[2 * QM0];
         llr_compute<QM0>(cwd[0], pr, ns, x, csi, cmb[0], o);
-        if (cm) {
-          cmp_put<QM0>(imgs, fw, fws[0], 2 * pr * QM0 - rp, n_e, o);
-        } else {
-          img_put<QM0>(imgs, 2 * pr * QM0 - rp, n_e, o);
-        }
+        img_put<QM0>(imgs, 2 * pr * QM0 - rp, n_e, o);
       }
       if constexpr (QM1 != 0) {
         const cf    x[2]   = {xs[1][0], xs[1][1]};
         const float csi[2] = {cs[1][0], cs[1][1]};
         int16_t     o[2 * QM1];
         llr_compute<QM1>(cwd[1], pr, ns, x, csi, cmb[1], o);
-        if (cm) { // (lean: one modulation, the same image slots)
-          cmp_put<QM1>(imgs + img, fw, fws[0], 2 * pr * QM1 - rp, n_e, o);
-        } else {
-          img_put<QM1>(imgs + img, 2 * pr * QM1 - rp, n_e, o);
-        }
+        img_put<QM1>(imgs + img, 2 * pr * QM1 - rp, n_e, o);
       }
     }
   }
@@ -1265,7 +1266,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   {
     if (cm) {
       // the compact image in decoder order: quad i (16 bytes) of each layer's image to decoder quad cmp[cqoff + i]
-      const GLB uint16_t* ql     = fw + R.cqoff[kx0][ev];
+      const GLB uint32_t* ql     = (const GLB uint32_t*)(fw + R.cqoff[kx0][ev]);
       const uint32_t      npairs = R.layer[0].buflen[kx0] / 2;
       GLB uint32_t*       sb[2]  = {(GLB uint32_t*)gptr(P.sb + (size_t)slot[0] * P.sb_stride),
                                     (GLB uint32_t*)gptr(P.sb + (size_t)slot[1] * P.sb_stride)};
@@ -1277,14 +1278,23 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
 #pragma unroll
         for (int k = 0; k < ER_CQ; k++) {
           const uint32_t qi = q0 + k * ER_THREADS;
-          qd[k]             = qi < cnq ? (uint32_t)ql[qi] : 0u;
+          qd[k]             = qi < cnq ? ql[qi] : 0u;
         }
 #pragma unroll
         for (int k = 0; k < ER_CQ; k++) {
           const uint32_t qi = q0 + k * ER_THREADS;
           if (qi >= cnq) continue;
-          const uint4    v0 = ((const uint4*)imgs)[qi], v1 = ((const uint4*)(imgs + img))[qi];
-          const uint32_t i  = 4 * qd[k];
+          const uint4    wa = ((const uint4*)im32)[2 * qi], wb = ((const uint4*)im32)[2 * qi + 1];
+          const uint32_t m  = qd[k] >> 16;
+          uint32_t       w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+          for (int p = 0; p < 8; p++) w[p] = (m >> p) & 1u ? w[p] : 0u; // positions without an LLR: zero
+          // layer 0 = the low halves, layer 1 = the high halves, two positions per u32
+          const uint4    v0 = make_uint4(__builtin_amdgcn_perm(w[1], w[0], 0x05040100u), __builtin_amdgcn_perm(w[3], w[2], 0x05040100u),
+                                         __builtin_amdgcn_perm(w[5], w[4], 0x05040100u), __builtin_amdgcn_perm(w[7], w[6], 0x05040100u));
+          const uint4    v1 = make_uint4(__builtin_amdgcn_perm(w[1], w[0], 0x07060302u), __builtin_amdgcn_perm(w[3], w[2], 0x07060302u),
+                                         __builtin_amdgcn_perm(w[5], w[4], 0x07060302u), __builtin_amdgcn_perm(w[7], w[6], 0x07060302u));
+          const uint32_t i  = 4 * (qd[k] & 0xffffu);
           if (al && i + 3 < npairs) {
             __builtin_nontemporal_store((u4v){v0.x, v0.y, v0.z, v0.w}, (GLB u4v*)(sb[0] + i));
             __builtin_nontemporal_store((u4v){v1.x, v1.y, v1.z, v1.w}, (GLB u4v*)(sb[1] + i));

@@ -56,8 +56,9 @@ uint32_t dlsch_rm_buflen(uint32_t K);
 // the compact decoder-order image of (K, rv, E) for a fresh rate dematching of E <= N LLRs with the empty parity rows
 // left unwritten (pdsch_eq_rm's lean path): the quads (8 decoder positions) that are written -- every quad outside the
 // parity rows, and the parity rows holding an LLR (rm_quad_defined with the row minima below E) -- numbered in
-// decoder order; LLR r lands at image slot tab[r] (8 x its quad's number + its place in the quad), and tab[qoff + i]
-// is quad i's decoder quad index (decoder position / 8).  nq quads.  Cached per (K, rv, E).
+// decoder order; LLR r lands at image slot tab[r] (8 x its quad's number + its place in the quad), and the u32 at
+// tab + qoff + 2 i is quad i's decoder quad index (decoder position / 8) | its LLR-position mask << 16 (bit p: position
+// p of the quad receives an LLR; the others are zero).  nq quads.  Cached per (K, rv, E).
 int      dlsch_rm_compact(mi355_dlsch_t* q, uint32_t K, uint32_t rv, uint32_t E, const uint16_t** tab, uint32_t* nq,
                           uint32_t* qoff);
 bool     rm_sparse_writes(); // fresh decoder buffers: empty parity rows left unwritten (SB_ROWMASK)
