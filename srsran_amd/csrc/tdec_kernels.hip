@@ -254,6 +254,14 @@ __shared__ uint32_t tdec_stg_row[4][TDEC_SEG];                // their destinati
 #ifndef TDEC_NT_CK
 #define TDEC_NT_CK 0
 #endif
+// buffer stores with an explicit cache policy for the staged output rows (TDEC_OUT_AUX) and the checkpoints
+// (TDEC_CK_AUX): -1 = plain global stores; 16 = sc1 (write-through), 2 = nt, 17 = sc0 sc1
+#ifndef TDEC_OUT_AUX
+#define TDEC_OUT_AUX -1
+#endif
+#ifndef TDEC_CK_AUX
+#define TDEC_CK_AUX -1
+#endif
 #ifndef TDEC_CLONE_NO_FIN
 #define TDEC_CLONE_NO_FIN 0
 #endif
@@ -316,6 +324,9 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   const int       ys   = GI ? 64 : NL;
   const uint32_t* AP   = a.A1 + wg0;
   uint32_t*       ck   = a.ckpt + (size_t)grp * nseg * 8 * 64 + q;
+  // (TDEC_CK_AUX) the group's checkpoint block as a buffer resource, wave-uniform base
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t ckr =
+      __builtin_amdgcn_make_buffer_rsrc(a.ckpt + (size_t)grp * nseg * 8 * 64, 0, nseg * 8 * 64 * 4, 0x00020000);
 
   // TX: this lane's 16-byte piece of the code block it loads for (not its own), and the wave's transposition buffers
   const uint4*    txin  = nullptr;
@@ -531,6 +542,9 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
                 if (t & 1) ck[((size_t)(t - 1) * 8 + s) * 64] = W(st[s]);
               } else if constexpr (DIAG == 11 || (DIAG >= 100 && (DIAG & 4))) { // into group 0's region (cache resident)
                 a.ckpt[q + ((size_t)(t - 1) * 8 + s) * 64] = W(st[s]);
+              } else if constexpr (TDEC_CK_AUX >= 0) {
+                __builtin_amdgcn_raw_buffer_store_b32(W(st[s]), ckr, (int)((((t - 1) * 8 + s) * 64 + q) * 4), 0,
+                                                      TDEC_CK_AUX);
               } else {
                 ck[((size_t)(t - 1) * 8 + s) * 64] = W(st[s]);
               }
@@ -609,6 +623,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
   // slices of those rows as 16-byte pieces, two store instructions per segment instead of sixteen.
   constexpr bool STG = FULL && !GI && TDEC_STAGE_OUT && (dec2 ? wr_a1 : wr_e) && !(CL && TDEC_CLONE_NO_E);
   int16_t*       O16 = dec2 ? A16 : E16;
+  [[maybe_unused]] const __amdgpu_buffer_rsrc_t outr = __builtin_amdgcn_make_buffer_rsrc(O16, 0, Lp * 256, 0x00020000);
   int16_t*       stg = nullptr;
   uint32_t*      stg_row = nullptr;
   if constexpr (STG) {
@@ -637,8 +652,11 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
         const int      idx = k * NL + l, r = idx / PPR, pc = idx % PPR;
         const uint32_t jr  = stg_row[r]; // the destination row of step r (shared by every window of it)
         const uint4    v   = *(const uint4*)(stg + r * 128 + 2 * lane0 + pc * 8);
-        if constexpr (TDEC_NT_OUT) {
-          typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        if constexpr (TDEC_OUT_AUX >= 0) {
+          __builtin_amdgcn_raw_buffer_store_b128((u4v){v.x, v.y, v.z, v.w}, outr,
+                                                 (int)(((size_t)jr * 128 + 2 * lane0 + pc * 8) * 2), 0, TDEC_OUT_AUX);
+        } else if constexpr (TDEC_NT_OUT) {
           __builtin_nontemporal_store((u4v){v.x, v.y, v.z, v.w}, (u4v*)(O16 + (size_t)jr * 128 + 2 * lane0 + pc * 8));
         } else {
           *(uint4*)(O16 + (size_t)jr * 128 + 2 * lane0 + pc * 8) = v;
