@@ -36,6 +36,10 @@ struct PdschJobDev {
   uint32_t                 fused_key; // modulation orders of the layers' codewords: qm0 * 16 + qm1 (0: none)
   const uint16_t*          cols;  // distinct subcarriers of the PDSCH REs (csi maximum over them)
   uint32_t                 ncols;
+  // nullable (pdsch_eq_rm, 2x2 MMSE): per subcarrier k, 3 float4 at wtab + 3 k = the MMSE matrix W (w00, w01),
+  // (w10, w11) and the two layers' csi, written by pdsch_csimax_cols: the estimates are row-invariant, so the
+  // equaliser applies W to each RE instead of rebuilding it from the estimates in all 13 symbols
+  float4*                  wtab;
   const struct PdschCwDev* cw[2]; // codeword (TB) descriptor fed by layer 0 / 1, null when not decoded
 };
 

@@ -47,6 +47,14 @@ typedef float    vf4 __attribute__((ext_vector_type(4)));
 typedef uint32_t vu2 __attribute__((ext_vector_type(2)));
 typedef uint32_t vu4 __attribute__((ext_vector_type(4)));
 template <class T> __device__ __forceinline__ GLB T* gptr(T* p) { return (GLB T*)p; }
+#ifndef PDSCH_WTAB
+#define PDSCH_WTAB 1 // pdsch_eq_rm reads the two-layer MMSE matrices of PdschJobDev.wtab (0: A/B builds only)
+#endif
+#ifndef PDSCH_LLR2
+#define PDSCH_LLR2 1 // pdsch_eq_rm's two-layer 256QAM LLRs on packed int16 pairs (llr2_256qam; 0: A/B builds only)
+#endif
+typedef float fv2 __attribute__((ext_vector_type(2)));
+typedef float fv4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ cf ld(const GLB float2* p, uint32_t i)
 {
   const vf2 v = *(const GLB vf2*)(p + i);
@@ -54,9 +62,9 @@ __device__ __forceinline__ cf ld(const GLB float2* p, uint32_t i)
 }
 __device__ __forceinline__ void st(GLB float2* p, uint32_t i, cf v) { *(GLB vf2*)(p + i) = (vf2){v.re, v.im}; }
 
-// srslte_mat_2x2_mmse_csi_gen (mat.c:63-110)
-__device__ __forceinline__ void mmse_2x2_csi(cf y0, cf y1, cf h00, cf h01, cf h10, cf h11, cf& x0, cf& x1,
-                                             float& csi0, float& csi1, float noise, float norm)
+// srslte_mat_2x2_mmse_csi_gen (mat.c:63-110), the matrix part: W = (H^H H + N0 I)^-1 H^H (scaled) and the csi
+__device__ __forceinline__ void mmse_2x2_w(cf h00, cf h01, cf h10, cf h11, cf& w00, cf& w01, cf& w10, cf& w11,
+                                           float& csi0, float& csi1, float noise, float norm)
 {
   const cf c00 = cj(h00), c01 = cj(h01), c10 = cj(h10), c11 = cj(h11);
   const cf a00 = c00 * h00 + c10 * h10 + mk(noise, 0.f);
@@ -67,14 +75,27 @@ __device__ __forceinline__ void mmse_2x2_csi(cf y0, cf y1, cf h00, cf h01, cf h1
   const float dd = abs2(det);
   const cf    nm = mk(det.re / dd, -det.im / dd) * norm; // srslte_mat_cf_recip_gen
   const cf b00 = a11 * nm, b01 = (a01 * -1.f) * nm, b10 = (a10 * -1.f) * nm, b11 = a00 * nm;
-  const cf w00 = b00 * c00 + b01 * c01;
-  const cf w01 = b00 * c10 + b01 * c11;
-  const cf w10 = b10 * c00 + b11 * c01;
-  const cf w11 = b10 * c10 + b11 * c11;
-  x0           = y0 * w00 + y1 * w01;
-  x1           = y0 * w10 + y1 * w11;
-  csi0         = 1.0f / b00.re;
-  csi1         = 1.0f / b11.re;
+  w00  = b00 * c00 + b01 * c01;
+  w01  = b00 * c10 + b01 * c11;
+  w10  = b10 * c00 + b11 * c01;
+  w11  = b10 * c10 + b11 * c11;
+  csi0 = 1.0f / b00.re;
+  csi1 = 1.0f / b11.re;
+}
+
+// ... applied to one RE (mat.c:103-104)
+__device__ __forceinline__ void mmse_2x2_apply(cf y0, cf y1, cf w00, cf w01, cf w10, cf w11, cf& x0, cf& x1)
+{
+  x0 = y0 * w00 + y1 * w01;
+  x1 = y0 * w10 + y1 * w11;
+}
+
+__device__ __forceinline__ void mmse_2x2_csi(cf y0, cf y1, cf h00, cf h01, cf h10, cf h11, cf& x0, cf& x1,
+                                             float& csi0, float& csi1, float noise, float norm)
+{
+  cf w00, w01, w10, w11;
+  mmse_2x2_w(h00, h01, h10, h11, w00, w01, w10, w11, csi0, csi1, noise, norm);
+  mmse_2x2_apply(y0, y1, w00, w01, w10, w11, x0, x1);
 }
 
 // max in the unsigned order of the bit patterns (the order fold_max reduces in; IEEE order for csi >= 0)
@@ -765,6 +786,20 @@ __global__ __launch_bounds__(256) void pdsch_cmax_reduce(const PdschCwDev* __res
 // csi of the single-RE schemes depends on the channel estimate and the noise only, so with row-invariant
 // estimates it is a function of the subcarrier: the codeword maxima (csi_correction's srslte_vec_max_fi,
 // pdsch.c:653) are taken over the PDSCH subcarriers before any symbol is equalised.  One workgroup per job.
+// the effective 2x2 channel of the codebook (precoding.c:1519-1548): estimates H[port * 2 + rx]; the MMSE norm
+__device__ __forceinline__ float sm2_channel(const PdschJobDev& J, const cf (&H)[4], cf& h00, cf& h01, cf& h10,
+                                             cf& h11)
+{
+  if (J.cb == 0) {
+    h00 = H[0], h01 = H[2], h10 = H[1], h11 = H[3];
+  } else if (J.cb == 1) {
+    h00 = H[0] + H[2], h01 = H[0] - H[2], h10 = H[1] + H[3], h11 = H[1] - H[3];
+  } else {
+    h00 = H[0] + mulj(H[2]), h01 = H[0] - mulj(H[2]), h10 = H[1] + mulj(H[3]), h11 = H[1] - mulj(H[3]);
+  }
+  return J.cb == 0 ? 0x1.6a09e6p+0f / J.scaling : 2.0f / J.scaling;
+}
+
 __device__ __forceinline__ void csi_of(const PdschJobDev& J, const cf (&H)[4], float noise, float& c0, float& c1)
 {
   if (J.scheme == 0) { // precoding.c:345-355
@@ -775,18 +810,9 @@ __device__ __forceinline__ void csi_of(const PdschJobDev& J, const cf (&H)[4], f
     c0 = hh + noise;
     c1 = 0.f;
   } else if (J.nof_layers == 2) { // precoding.c:1519-1548
-    const float norm = J.cb == 0 ? 0x1.6a09e6p+0f / J.scaling : 2.0f / J.scaling;
-    const cf    g00 = H[0], g01 = H[1], g10 = H[2], g11 = H[3];
-    cf          h00, h01, h10, h11;
-    if (J.cb == 0) {
-      h00 = g00, h01 = g10, h10 = g01, h11 = g11;
-    } else if (J.cb == 1) {
-      h00 = g00 + g10, h01 = g00 - g10, h10 = g01 + g11, h11 = g01 - g11;
-    } else {
-      h00 = g00 + mulj(g10), h01 = g00 - mulj(g10), h10 = g01 + mulj(g11), h11 = g01 - mulj(g11);
-    }
-    cf x0, x1;
-    mmse_2x2_csi(mk(0.f, 0.f), mk(0.f, 0.f), h00, h01, h10, h11, x0, x1, c0, c1, noise, norm);
+    cf          h00, h01, h10, h11, w00, w01, w10, w11;
+    const float norm = sm2_channel(J, H, h00, h01, h10, h11);
+    mmse_2x2_w(h00, h01, h10, h11, w00, w01, w10, w11, c0, c1, noise, norm);
   } else { // precoding.c:1786-1820
     const float norm = 0x1.6a09e6p+0f / J.scaling;
     cf          h[2];
@@ -824,7 +850,17 @@ __global__ __launch_bounds__(256) void pdsch_csimax_cols(const PdschJobDev* __re
 #pragma unroll
     for (int q = 0; q < 4; q++) H[q] = ld(hp[q], k);
     float c0, c1;
-    csi_of(J, H, noise, c0, c1);
+    if (J.wtab) { // two layers (PdschJobDev.wtab): the subcarrier's MMSE matrix for pdsch_eq_rm
+      cf          h00, h01, h10, h11, w00, w01, w10, w11;
+      const float norm = sm2_channel(J, H, h00, h01, h10, h11);
+      mmse_2x2_w(h00, h01, h10, h11, w00, w01, w10, w11, c0, c1, noise, norm);
+      GLB fv4* wt = (GLB fv4*)gptr(J.wtab) + 3 * k;
+      wt[0]       = fv4{w00.re, w00.im, w01.re, w01.im};
+      wt[1]       = fv4{w10.re, w10.im, w11.re, w11.im};
+      wt[2]       = fv4{c0, c1, 0.f, 0.f};
+    } else {
+      csi_of(J, H, noise, c0, c1);
+    }
     b0 = max(b0, __float_as_uint(c0));
     b1 = max(b1, __float_as_uint(c1));
   }
@@ -865,15 +901,8 @@ __device__ __forceinline__ void eq_re(const PdschJobDev& J, const cf (&h)[4], co
     x1 = mk(0.f, 0.f);
     c1 = 0.f;
   } else if (J.nof_layers == 2) { // precoding.c:1519-1548
-    const float norm = J.cb == 0 ? 0x1.6a09e6p+0f / J.scaling : 2.0f / J.scaling;
     cf          h00, h01, h10, h11;
-    if (J.cb == 0) {
-      h00 = h[0], h01 = h[2], h10 = h[1], h11 = h[3];
-    } else if (J.cb == 1) {
-      h00 = h[0] + h[2], h01 = h[0] - h[2], h10 = h[1] + h[3], h11 = h[1] - h[3];
-    } else {
-      h00 = h[0] + mulj(h[2]), h01 = h[0] - mulj(h[2]), h10 = h[1] + mulj(h[3]), h11 = h[1] - mulj(h[3]);
-    }
+    const float norm = sm2_channel(J, h, h00, h01, h10, h11);
     mmse_2x2_csi(y[0], y[1], h00, h01, h10, h11, x0, x1, c0, c1, noise, norm);
   } else { // precoding.c:1786-1820
     const float norm = 0x1.6a09e6p+0f / J.scaling;
@@ -1012,10 +1041,6 @@ hipError_t pdsch_launch_fused(const PdschJobDev* jobs, uint32_t njobs, uint32_t 
 #define PDSCH_ER_THREADS 256
 #endif
 constexpr uint32_t ER_THREADS = PDSCH_ER_THREADS;
-#ifndef PDSCH_ER_PF
-#define PDSCH_ER_PF 1
-#endif
-constexpr int      ER_PF      = PDSCH_ER_PF; // RE pairs per thread whose loads are in flight together (equaliser part)
 #ifndef PDSCH_ER_TPF
 #define PDSCH_ER_TPF 0
 #endif
@@ -1078,21 +1103,70 @@ template <int QM> __device__ __forceinline__ CmpSlots cmp_slots(const GLB uint16
   }
   return s;
 }
-// both layers' LLRs of the pair into the interleaved u32 image (layer 0 in the low half)
+// both layers' LLRs of the pair into the interleaved u32 image (wd[k]: layer 0's LLR k in the low half)
 template <int QM>
 __device__ __forceinline__ void cmp_put2(uint32_t* im, const GLB uint16_t* fw, const CmpSlots& s, uint32_t b, uint32_t n_e,
-                                         const int16_t (&o0)[2 * QM], const int16_t (&o1)[2 * QM])
+                                         const uint32_t (&wd)[2 * QM])
 {
-  auto wd = [&](int k) { return (uint32_t)(uint16_t)o0[k] | ((uint32_t)(uint16_t)o1[k] << 16); };
   if (s.whole) {
     const uint32_t w[8] = {s.v[0].x, s.v[0].y, s.v[0].z, s.v[0].w, s.v[1].x, s.v[1].y, s.v[1].z, s.v[1].w};
 #pragma unroll
-    for (int k = 0; k < 2 * QM; k++) im[(w[k >> 1] >> (16 * (k & 1))) & 0xffffu] = wd(k);
+    for (int k = 0; k < 2 * QM; k++) im[(w[k >> 1] >> (16 * (k & 1))) & 0xffffu] = wd[k];
     return;
   }
 #pragma unroll
   for (int k = 0; k < 2 * QM; k++)
-    if (b + k < n_e) im[fw[b + k]] = wd(k);
+    if (b + k < n_e) im[fw[b + k]] = wd[k];
+}
+
+// llr_compute<8> of both layers at once, as the interleaved image words: the demapper's truncations as 32-bit
+// conversions whose low halves are paired by one byte permute, the descrambling and the csi weighting on the pair of
+// int16 (one packed subtract; two 24-bit multiplies and a permute of their high halves) -- the same wrapping int16
+// arithmetic as llr_compute, bit for bit
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int32_t cvt_trunc(float v) // x86_cvt_i32(truncf(v)): the conversion truncates itself
+{
+  return fabsf(v) < 2147483648.0f ? (int32_t)v : INT32_MIN;
+}
+__device__ __forceinline__ void llr2_256qam(uint32_t z, bool csi_on, const float (&csc)[2], uint32_t ns,
+                                            const cf (&x)[2][2], const float (&csi)[2][2], uint32_t (&wd)[16])
+{
+  // z: the pair's descrambling bits, layer 0 in the low half; csc: 32767 / cmax of each layer's codeword
+  const float k[4] = {0.f, 0x1.3a261cp-1f, 0x1.3a261cp-2f, 0x1.3a261cp-3f}; // -, {8,4,2} / sqrtf(170) (demod_symbol)
+#pragma unroll
+  for (int e = 0; e < 2; e++) {
+    int32_t cv[2] = {0, 0};
+    if (csi_on) {
+#pragma unroll
+      for (int l = 0; l < 2; l++) cv[l] = sat16(x86_cvt_i32(rintf(csi[l][e] * csc[l])));
+    }
+    float re[2], im[2];
+#pragma unroll
+    for (int l = 0; l < 2; l++) re[l] = -x[l][e].re, im[l] = -x[l][e].im;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      if (t) {
+#pragma unroll
+        for (int l = 0; l < 2; l++) re[l] = fabsf(re[l]) - k[t], im[l] = fabsf(im[l]) - k[t];
+      }
+#pragma unroll
+      for (int h = 0; h < 2; h++) { // LLR 2t (re) / 2t + 1 (im) of symbol e
+        const int      b = 8 * e + 2 * t + h;
+        const float*   v = h ? im : re;
+        uint32_t       w = (uint32_t)e < ns ? __builtin_amdgcn_perm((uint32_t)cvt_trunc(1000.0f * v[1]),
+                                                                    (uint32_t)cvt_trunc(1000.0f * v[0]), 0x05040100u)
+                                            : 0u;
+        const uint32_t m = __mul24((z >> b) & 0x00010001u, 0xffffu); // 0xffff in each half whose bit is set
+        w = __builtin_bit_cast(uint32_t, (u16x2)(__builtin_bit_cast(u16x2, w ^ m) - __builtin_bit_cast(u16x2, m)));
+        if (csi_on) {
+          const int32_t p0 = __mul24((int32_t)(int16_t)(w & 0xffffu), cv[0]);
+          const int32_t p1 = __mul24((int32_t)w >> 16, cv[1]);
+          w                = __builtin_amdgcn_perm((uint32_t)p1, (uint32_t)p0, 0x07060302u);
+        }
+        wd[b] = w;
+      }
+    }
+  }
 }
 
 template <int QM0, int QM1>
@@ -1173,6 +1247,7 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   const GLB float2*   yp[2] = {gptr(J.y[0]), gptr(J.nof_rx > 1 ? J.y[1] : J.y[0])};
   const GLB float2*   hp[4];
   h_ptrs(J, hp);
+  const GLB fv4*      wtp = (const GLB fv4*)gptr(J.wtab); // two layers: set by the host (run_frontend)
   // the usual rate-dematching case (two fresh buffers sharing one table, below): its first round of table words does
   // not depend on the equaliser, so it is loaded now and arrives while the RE pairs are equalised
   uint4 iv0[ER_Q];
@@ -1192,66 +1267,113 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   }
   const uint32_t re0 = rp / Qm, re1 = (rp + n_e) / Qm, pairs = (J.nof_re + 1) / 2;
   const uint32_t p1  = P.diag == 2 ? 0u : min((re1 + 1) / 2, pairs);
-  // ER_PF RE pairs per thread in flight: their map words first, then every gather of all of them, then the math
-  for (uint32_t pr0 = re0 / 2 + tid; pr0 < p1; pr0 += ER_PF * ER_THREADS) {
-    uint32_t m[ER_PF];
+  // two layers: the subcarrier's MMSE matrix and csi (pdsch_csimax_cols, PdschJobDev.wtab) instead of the estimates
+  constexpr bool WT = PDSCH_WTAB && QM0 != 0 && QM1 != 0;
+  // two 256QAM layers into the compact image: packed LLR pairs (llr2_256qam), the descrambling words loaded with the
+  // pair's other operands and the csi scales 32767 / cmax once per workgroup
+  constexpr bool L2 = PDSCH_LLR2 && QM0 == 8 && QM1 == 8;
+  bool                l2 = false, l2csi = false;
+  float               csc[2] = {0.f, 0.f};
+  const GLB uint32_t* scr[2] = {nullptr, nullptr};
+  if constexpr (L2) {
+    l2 = cm && cwd[0].csi_enable == cwd[1].csi_enable;
+    if (l2) {
+      l2csi = cwd[0].csi_enable != 0;
 #pragma unroll
-    for (int f = 0; f < ER_PF; f++) {
-      const uint32_t pr = pr0 + f * ER_THREADS;
-      m[f]              = map2[pr < p1 ? pr : pr0];
-    }
-    cf Y[ER_PF][2][2], H[ER_PF][2][4];
-#pragma unroll
-    for (int f = 0; f < ER_PF; f++) {
-#pragma unroll
-      for (int e = 0; e < 2; e++) {
-        const uint32_t g  = e ? (m[f] >> 16) : (m[f] & 0xffffu);
-        const uint32_t gc = g < 14 * row ? g : 0u; // the odd tail's second index is padding
-        const uint32_t l  = __umulhi(gc, magic);
-        const float    sc = ((rmask >> l) & 1u) ? rinv : 1.0f;
-#pragma unroll
-        for (int r = 0; r < 2; r++) Y[f][e][r] = ld(yp[r], gc) * sc;
-#pragma unroll
-        for (int q = 0; q < 4; q++) H[f][e][q] = ld(hp[q], gc - l * row);
+      for (int l = 0; l < 2; l++) {
+        scr[l]           = gptr(cwd[l].scr);
+        const float cmax = cwd[l].nof_bits / 8 ? __uint_as_float(cmb[l]) : 1.0f;
+        csc[l]           = 32767.0f / cmax;
       }
     }
+  }
+  // one RE pair per thread and round; the next round's map word is loaded while this round's pair is computed
+  const uint32_t pb    = re0 / 2 + tid;
+  uint32_t       mnext = pb < p1 ? map2[pb] : 0u;
+  for (uint32_t pr = pb; pr < p1; pr += ER_THREADS) {
+    const uint32_t m = mnext;
+    cf             Y[2][2], H[2][WT ? 1 : 4];
+    fv4            W[2][WT ? 2 : 1];
+    fv2            WC[2];
 #pragma unroll
-    for (int f = 0; f < ER_PF; f++) {
-      const uint32_t pr = pr0 + f * ER_THREADS;
-      if (pr >= p1) continue;
-      const uint32_t ns = min(2u, J.nof_re - 2 * pr);
-      // the compact image slots of the pair's LLRs (whole pairs inside the span): in flight during the MMSE math
-      CmpSlots       fws[1];
-      if (cm) fws[0] = cmp_slots<(QM0 ? QM0 : QM1)>(fw, 2 * pr * (QM0 ? QM0 : QM1) - rp, n_e);
-      cf             xs[2][2];
-      float          cs[2][2];
+    for (int e = 0; e < 2; e++) {
+      const uint32_t g  = e ? (m >> 16) : (m & 0xffffu);
+      const uint32_t gc = g < 14 * row ? g : 0u; // the odd tail's second index is padding
+      const uint32_t l  = __umulhi(gc, magic);
+      const float    sc = ((rmask >> l) & 1u) ? rinv : 1.0f;
 #pragma unroll
-      for (int e = 0; e < 2; e++) eq_re(J, H[f][e], Y[f][e], noise, xs[0][e], xs[1][e], cs[0][e], cs[1][e]);
-      if constexpr (QM0 != 0 && QM0 == QM1) {
-        if (cm) { // both layers' LLRs of a position in one u32 image word
-          const cf    x0[2] = {xs[0][0], xs[0][1]}, x1[2] = {xs[1][0], xs[1][1]};
-          const float c0[2] = {cs[0][0], cs[0][1]}, c1[2] = {cs[1][0], cs[1][1]};
-          int16_t     o0[2 * QM0], o1[2 * QM0];
-          llr_compute<QM0>(cwd[0], pr, ns, x0, c0, cmb[0], o0);
-          llr_compute<QM0>(cwd[1], pr, ns, x1, c1, cmb[1], o1);
-          cmp_put2<QM0>(im32, fw, fws[0], 2 * pr * QM0 - rp, n_e, o0, o1);
-          continue;
+      for (int r = 0; r < 2; r++) Y[e][r] = ld(yp[r], gc) * sc;
+      if constexpr (WT) {
+        const GLB fv4* wt = wtp + 3 * (gc - l * row);
+        W[e][0]           = wt[0];
+        W[e][1]           = wt[1];
+        WC[e]             = *(const GLB fv2*)(wt + 2);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++) H[e][q] = ld(hp[q], gc - l * row);
+      }
+    }
+    if (pr + ER_THREADS < p1) mnext = map2[pr + ER_THREADS];
+    const uint32_t ns = min(2u, J.nof_re - 2 * pr);
+    // the compact image slots of the pair's LLRs (whole pairs inside the span): in flight during the MMSE math
+    CmpSlots       fws[1];
+    if (cm) fws[0] = cmp_slots<(QM0 ? QM0 : QM1)>(fw, 2 * pr * (QM0 ? QM0 : QM1) - rp, n_e);
+    uint32_t lo[2] = {0u, 0u}; // (l2) the pair's 16 descrambling bits of each layer: bit 16 pr of the sequence
+    if constexpr (L2) {
+      if (l2) {
+#pragma unroll
+        for (int l = 0; l < 2; l++) lo[l] = scr[l][pr >> 1];
+      }
+    }
+    cf    xs[2][2];
+    float cs[2][2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      if constexpr (WT) {
+        const fv4* w = W[e];
+        mmse_2x2_apply(Y[e][0], Y[e][1], mk(w[0].x, w[0].y), mk(w[0].z, w[0].w), mk(w[1].x, w[1].y),
+                       mk(w[1].z, w[1].w), xs[0][e], xs[1][e]);
+        cs[0][e] = WC[e].x;
+        cs[1][e] = WC[e].y;
+      } else {
+        eq_re(J, H[e], Y[e], noise, xs[0][e], xs[1][e], cs[0][e], cs[1][e]);
+      }
+    }
+    if constexpr (QM0 != 0 && QM0 == QM1) {
+      if (cm) { // both layers' LLRs of a position in one u32 image word
+        uint32_t wd[2 * QM0];
+        if constexpr (L2) {
+          if (l2) {
+            const uint32_t sh = 16 * (pr & 1);
+            llr2_256qam(((lo[0] >> sh) & 0xffffu) | ((lo[1] >> sh) << 16), l2csi, csc, ns, xs, cs, wd);
+            cmp_put2<QM0>(im32, fw, fws[0], 2 * pr * QM0 - rp, n_e, wd);
+            continue;
+          }
         }
+        const cf    x0[2] = {xs[0][0], xs[0][1]}, x1[2] = {xs[1][0], xs[1][1]};
+        const float c0[2] = {cs[0][0], cs[0][1]}, c1[2] = {cs[1][0], cs[1][1]};
+        int16_t     o0[2 * QM0], o1[2 * QM0];
+        llr_compute<QM0>(cwd[0], pr, ns, x0, c0, cmb[0], o0);
+        llr_compute<QM0>(cwd[1], pr, ns, x1, c1, cmb[1], o1);
+#pragma unroll
+        for (int k = 0; k < 2 * QM0; k++) wd[k] = (uint32_t)(uint16_t)o0[k] | ((uint32_t)(uint16_t)o1[k] << 16);
+        cmp_put2<QM0>(im32, fw, fws[0], 2 * pr * QM0 - rp, n_e, wd);
+        continue;
       }
-      if constexpr (QM0 != 0) {
-        const cf    x[2]   = {xs[0][0], xs[0][1]};
-        const float csi[2] = {cs[0][0], cs[0][1]};
-        int16_t     o[2 * QM0];
-        llr_compute<QM0>(cwd[0], pr, ns, x, csi, cmb[0], o);
-        img_put<QM0>(imgs, 2 * pr * QM0 - rp, n_e, o);
-      }
-      if constexpr (QM1 != 0) {
-        const cf    x[2]   = {xs[1][0], xs[1][1]};
-        const float csi[2] = {cs[1][0], cs[1][1]};
-        int16_t     o[2 * QM1];
-        llr_compute<QM1>(cwd[1], pr, ns, x, csi, cmb[1], o);
-        img_put<QM1>(imgs + img, 2 * pr * QM1 - rp, n_e, o);
-      }
+    }
+    if constexpr (QM0 != 0) {
+      const cf    x[2]   = {xs[0][0], xs[0][1]};
+      const float csi[2] = {cs[0][0], cs[0][1]};
+      int16_t     o[2 * QM0];
+      llr_compute<QM0>(cwd[0], pr, ns, x, csi, cmb[0], o);
+      img_put<QM0>(imgs, 2 * pr * QM0 - rp, n_e, o);
+    }
+    if constexpr (QM1 != 0) {
+      const cf    x[2]   = {xs[1][0], xs[1][1]};
+      const float csi[2] = {cs[1][0], cs[1][1]};
+      int16_t     o[2 * QM1];
+      llr_compute<QM1>(cwd[1], pr, ns, x, csi, cmb[1], o);
+      img_put<QM1>(imgs + img, 2 * pr * QM1 - rp, n_e, o);
     }
   }
   if (tid < 2 && !cm) imgs[tid * img + n_e] = 0; // the zero slot: table entries without an LLR (RM_NONE, >= n_e)

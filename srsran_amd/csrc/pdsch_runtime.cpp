@@ -468,8 +468,14 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
                         (er ? staged_size(njobs * sizeof(EqRmJob)) : 0);
   auto           rnd    = [](size_t b) { return (b + 255) / 256 * 256; };
   const uint32_t nparts = (max_units + EQ_BLOCK_ITEMS - 1) / EQ_BLOCK_ITEMS; // equaliser blocks per job
+  // eq_rm's two-layer jobs: the per-subcarrier MMSE matrices (PdschJobDev.wtab), after the csi maxima
+  auto wtab_of = [&](const JobPlan& P) {
+    return er && P.dev.fused && P.dev.nof_layers == 2 && P.decode[0] && P.decode[1] ? rnd((size_t)P.dev.row * 48) : 0;
+  };
+  size_t nwt = 0;
+  for (const JobPlan& P : plans) nwt += wtab_of(P);
   const size_t   need   = staged + rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2) + rnd((size_t)njobs * 2 * nparts * 4) +
-                        rnd(ncw * 4);
+                        rnd(ncw * 4) + nwt;
   char* base = nullptr;
   int   r    = get_scratch(q, need, &base);
   if (r) return r;
@@ -484,6 +490,7 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
   const size_t o_rj  = o_ndst + staged_size(new_ci.size() * 8);
   uint32_t*    d_cmax = (uint32_t*)(base + staged + rnd(nd * 8) + rnd(nd * 4) + rnd(ne * 2));
   uint32_t*    d_cfin = d_cmax + rnd((size_t)njobs * 2 * nparts * 4) / 4;
+  char*        d_wt   = (char*)d_cfin + rnd(ncw * 4);
   std::vector<PdschJobDev> hj(njobs);
   const PdschCwDev*        d_cws = (const PdschCwDev*)(base + o_cws);
   std::vector<uint32_t>    fkeys; // (qm0, qm1) pairs of the fused jobs: one kernel instantiation each
@@ -507,6 +514,8 @@ static int run_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, std::ve
     JobPlan& P = plans[i];
     P.dev.cmax        = d_cmax + (size_t)2 * nparts * i;
     P.dev.cmax_stride = nparts;
+    P.dev.wtab        = wtab_of(P) ? (float4*)d_wt : nullptr;
+    d_wt += wtab_of(P);
     for (uint32_t cw = 0; cw < 2; cw++) {
       P.dev.d[cw]   = q->d_arena + P.d_off[cw];
       P.dev.csi[cw] = q->csi_arena + P.csi_off[cw];
