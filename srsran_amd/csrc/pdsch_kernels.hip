@@ -1200,6 +1200,12 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   }
   if (!need[0] && !need[1]) return;
   const unsigned long long pt0 = P.prof ? clock64() : 0ull; // (phase profile: P.prof only)
+  // the RE pairs overlapping the span; each thread's first map word is loaded now and arrives during the prologue
+  const uint32_t      re0 = rp / Qm, re1 = (rp + n_e) / Qm, pairs = (J.nof_re + 1) / 2;
+  const uint32_t      p1  = P.diag == 2 ? 0u : min((re1 + 1) / 2, pairs);
+  const GLB uint32_t* map2  = (const GLB uint32_t*)gptr(J.map);
+  const uint32_t      pb    = re0 / 2 + tid;
+  uint32_t            mnext = pb < p1 ? map2[pb] : 0u;
   // the slots' parity-row bitmaps (rm_image.h; E <= N here): the old ones (rows they leave undefined are read as zero
   // by a combining write), the new ones (a fresh buffer's rows without an LLR are not written, P.sparse)
   __shared__ uint32_t obm[2][2 * SB_ROWMASK_WORDS], nbm[2][2 * SB_ROWMASK_WORDS];
@@ -1220,9 +1226,13 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   }
   __shared__ PdschCwDev cwd[2];
   __shared__ uint32_t   cmb[2];
-  if (tid < 2 && J.cw[tid]) {
-    cwd[tid] = *J.cw[tid];
-    cmb[tid] = cwd[tid].csi_enable ? *gptr(cwd[tid].cmax_final) : 0u;
+  // the codeword descriptors and csi maxima (two dependent loads) by the second wave, while the first one does the
+  // parity-row bitmaps above
+  static_assert(ER_THREADS >= 128 && 2 * (2 * SB_ROWMASK_WORDS + 1) <= 64, "pdsch_eq_rm prologue waves");
+  if (tid - 64 < 2 && J.cw[tid - 64]) {
+    const uint32_t l = tid - 64;
+    cwd[l]           = *J.cw[l];
+    cmb[l]           = cwd[l].csi_enable ? *gptr(cwd[l].cmax_final) : 0u;
   }
   __syncthreads();
   // the usual rate-dematching case: two fresh buffers sharing one table (lean).  With the empty parity rows left
@@ -1243,7 +1253,6 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
   const float         noise = J.noise_dev ? *gptr(J.noise_dev) : J.noise;
   const uint32_t      row = J.row, magic = J.row_magic, rmask = J.rhob_mask;
   const float         rinv = J.rhob_inv;
-  const GLB uint32_t* map2 = (const GLB uint32_t*)gptr(J.map);
   const GLB float2*   yp[2] = {gptr(J.y[0]), gptr(J.nof_rx > 1 ? J.y[1] : J.y[0])};
   const GLB float2*   hp[4];
   h_ptrs(J, hp);
@@ -1265,8 +1274,6 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
       }
     }
   }
-  const uint32_t re0 = rp / Qm, re1 = (rp + n_e) / Qm, pairs = (J.nof_re + 1) / 2;
-  const uint32_t p1  = P.diag == 2 ? 0u : min((re1 + 1) / 2, pairs);
   // two layers: the subcarrier's MMSE matrix and csi (pdsch_csimax_cols, PdschJobDev.wtab) instead of the estimates
   constexpr bool WT = PDSCH_WTAB && QM0 != 0 && QM1 != 0;
   // two 256QAM layers into the compact image: packed LLR pairs (llr2_256qam), the descrambling words loaded with the
@@ -1288,8 +1295,6 @@ __global__ __launch_bounds__(ER_THREADS) __attribute__((amdgpu_waves_per_eu(PDSC
     }
   }
   // one RE pair per thread and round; the next round's map word is loaded while this round's pair is computed
-  const uint32_t pb    = re0 / 2 + tid;
-  uint32_t       mnext = pb < p1 ? map2[pb] : 0u;
   for (uint32_t pr = pb; pr < p1; pr += ER_THREADS) {
     const uint32_t m = mnext;
     cf             Y[2][2], H[2][WT ? 1 : 4];
