@@ -157,6 +157,12 @@ int mi355_pdsch_debug_stage(mi355_pdsch_t* q, uint32_t job, uint32_t cw, const f
  * and the 8-bit DL-SCH decode (see mi355_dlsch_decode8_dev).  mi355_pdsch_debug_stage's e then points to int8. */
 int mi355_pdsch_set_llr_8bit(mi355_pdsch_t* q, int enable);
 
+/* The channel estimates of the following decode calls (mi355_pdsch_decode_batch / _launch) are identical in every
+ * OFDM symbol, as the AVERAGE estimator writes them (chest_dl.c's subframe average): the equaliser reads their first
+ * row only, and port-0 / spatial-multiplexing jobs take the fused equaliser (pdsch_eq_llr / pdsch_eq_rm), whose results
+ * are the two-kernel path's bit for bit.  Default 0 (estimates may vary per symbol). */
+int mi355_pdsch_set_ce_invariant(mi355_pdsch_t* q, int enable);
+
 /* Run only the symbol-level front-end (extraction .. CSI weighting) of a job list, no DL-SCH decode. */
 int mi355_pdsch_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, uint32_t njobs, void* stream);
 

@@ -200,6 +200,10 @@ def synth_subframe(cfg: Cfg, rng: np.random.Generator, snr_db: float = 30.0, cha
         hb = (rng.standard_normal((cfg.nof_ports, cfg.nof_rx, 14 * cfg.nof_prb)) + 1j * rng.standard_normal(
             (cfg.nof_ports, cfg.nof_rx, 14 * cfg.nof_prb))) / np.sqrt(2)
         h = np.repeat(hb, 12, axis=2).astype(np.complex64)
+    elif channel == "static":  # Rayleigh, constant over each PRB and the whole subframe (row-invariant estimates)
+        hb = (rng.standard_normal((cfg.nof_ports, cfg.nof_rx, cfg.nof_prb)) + 1j * rng.standard_normal(
+            (cfg.nof_ports, cfg.nof_rx, cfg.nof_prb))) / np.sqrt(2)
+        h = np.tile(np.repeat(hb, 12, axis=2), (1, 1, 14)).astype(np.complex64)
     else:
         h = np.ones((cfg.nof_ports, cfg.nof_rx, G), np.complex64)
     txg = np.zeros((cfg.nof_ports, G), np.complex64)

@@ -209,6 +209,7 @@ struct mi355_pdsch {
   float*                               csi_arena = nullptr;
   int16_t*                             e_arena   = nullptr;
   bool                                 llr8      = false; // pdsch.llr_is_8bit (srsUE pdsch_8bit_decoder)
+  bool                                 ce_inv    = false; // mi355_pdsch_set_ce_invariant
   HostStaging                          stage;
   hipEvent_t                           fe_done  = nullptr; // after the last front-end kernel of the previous batch
   bool                                 fe_armed = false;
@@ -649,6 +650,14 @@ int mi355_pdsch_set_llr_8bit(mi355_pdsch_t* q, int enable)
   return MI355_SUCCESS;
 }
 
+int mi355_pdsch_set_ce_invariant(mi355_pdsch_t* q, int enable)
+{
+  if (!q) return MI355_ERROR_INVALID_INPUTS;
+  std::lock_guard<std::mutex> lk(q->mu);
+  q->ce_inv = enable != 0;
+  return MI355_SUCCESS;
+}
+
 int mi355_pdsch_frontend(mi355_pdsch_t* q, const mi355_pdsch_job_t* jobs, uint32_t njobs, void* stream)
 {
   if (!q || (njobs && !jobs)) return MI355_ERROR_INVALID_INPUTS;
@@ -698,7 +707,8 @@ int mi355_pdsch_decode_batch(mi355_pdsch_t*           q,
                              mi355_pdsch_res_t*       res,
                              void*                    stream)
 {
-  return mi355::pdsch_decode_batch_dev_noise(q, pool, jobs, njobs, res, stream, nullptr);
+  return mi355::pdsch_decode_batch_dev_noise(q, pool, jobs, njobs, res, stream, nullptr, mi355::WaitHook{},
+                                             q && q->ce_inv);
 }
 
 int mi355_pdsch_decode_launch(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi355_pdsch_job_t* jobs,
@@ -707,8 +717,8 @@ int mi355_pdsch_decode_launch(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, c
   if (!q) return MI355_ERROR_INVALID_INPUTS;
   if (q->api_armed) return MI355_ERROR; // the previous launch was not collected
   if (!q->api_pend) q->api_pend.reset(new mi355::PdschPending);
-  const int r = mi355::pdsch_decode_batch_dev_noise(q, pool, jobs, njobs, res, stream, nullptr, mi355::WaitHook{}, false,
-                                                    q->api_pend.get());
+  const int r = mi355::pdsch_decode_batch_dev_noise(q, pool, jobs, njobs, res, stream, nullptr, mi355::WaitHook{},
+                                                    q->ce_inv, q->api_pend.get());
   q->api_armed = true; // collected even after an error (whatever groups were enqueued)
   return r;
 }

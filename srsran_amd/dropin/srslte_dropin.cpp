@@ -356,6 +356,7 @@ struct PdschState {
   bool           own_rx = false;
   bool           llr8   = false;
   uint32_t       max_prb = 0;
+  bool           ce_inv  = false; // mi355_pdsch_set_ce_invariant's state on rx
   // device staging of host grids / estimates and of the payloads
   float*    d_stage   = nullptr;
   size_t    stage_cap = 0;
@@ -393,10 +394,11 @@ void pdsch_free_host(srslte_pdsch_t* q)
   }
 }
 
-// one PDSCH decode: grids[rx] / ce[p][rx] are device pointers (resident, or staged by the caller of this function)
+// one PDSCH decode: grids[rx] / ce[p][rx] are device pointers (resident, or staged by the caller of this function);
+// ce_inv: the estimates are the same in every OFDM symbol (this TTI's AVERAGE estimate, resident)
 int pdsch_decode_dev(srslte_pdsch_t* q, PdschState* st, hipStream_t stream, srslte_dl_sf_cfg_t* sf, srslte_pdsch_cfg_t* cfg,
-                     float noise,
-                     const float* const* grids, const float* const (*ce)[MI355_MAX_RX_ANT], srslte_pdsch_res_t* data)
+                     float noise, const float* const* grids, const float* const (*ce)[MI355_MAX_RX_ANT],
+                     srslte_pdsch_res_t* data, bool ce_inv)
 {
   Arena& A = arena();
   if (!A.pool) return SRSLTE_ERROR;
@@ -462,6 +464,10 @@ int pdsch_decode_dev(srslte_pdsch_t* q, PdschState* st, hipStream_t stream, srsl
     if (mi355_pdsch_set_llr_8bit(st->rx, q->llr_is_8bit)) return SRSLTE_ERROR;
     st->llr8 = q->llr_is_8bit;
   }
+  if (ce_inv != st->ce_inv) { // row-invariant estimates: the fused equaliser path (fewer launches per TTI)
+    if (mi355_pdsch_set_ce_invariant(st->rx, ce_inv)) return SRSLTE_ERROR;
+    st->ce_inv = ce_inv;
+  }
   // the decode with its per-TB results in flight, then one payload copy for both TBs (consecutive in d_payload) and
   // the CRC flags behind it on the same stream, then the waits (the read-backs were enqueued before the first one)
   if (mi355_pdsch_decode_launch(st->rx, A.pool, &job, 1, res, stream) != MI355_SUCCESS) {
@@ -522,6 +528,7 @@ struct UeDlState {
   hipEvent_t     ev_est   = nullptr; // the estimator's kernels done (the side stream's read-back waits for it)
   // last estimate and control-stage outcome
   bool                 est_valid = false;
+  bool                 est_avg   = false; // the resident estimate is the AVERAGE estimator's (row-invariant)
   uint32_t             est_tti   = 0;
   mi355_chest_dl_res_t chest{};
   bool                 ctrl_valid = false;
@@ -690,6 +697,7 @@ int ue_fft_estimate(srslte_ue_dl_t* q, srslte_dl_sf_cfg_t* sf, srslte_ue_dl_cfg_
   // the estimation ran exactly once for this TTI: its results stand whichever later part failed
   st->est_valid = true;
   st->est_tti   = sf->tti;
+  st->est_avg   = ccfg.estimator_alg == MI355_ESTIMATOR_ALG_AVERAGE;
   fill_chest_res(q, st);
   if (st->host_grids && !back_done && // only the grid / estimate read-back failed or was not enqueued: redo it alone
       (mi355::stage_copy(st->h_block, st->d_grid[0], bk.nb, st->side) != hipSuccess ||
@@ -1074,7 +1082,7 @@ int srslte_pdsch_decode(srslte_pdsch_t*        q,
   // the staged host buffers go up in one copy
   if (k_stage && mi355::stage_copy(st->d_stage, st->h_stage.p, k_stage * bytes, st->stream) != hipSuccess)
     return SRSLTE_ERROR;
-  const int ret = pdsch_decode_dev(q, st, st->stream, sf, cfg, channel->noise_estimate, grids, ce, data);
+  const int ret = pdsch_decode_dev(q, st, st->stream, sf, cfg, channel->noise_estimate, grids, ce, data, false);
   if (cfg->meas_time_en) {
     gettimeofday(&t1, nullptr);
     cfg->meas_time_value = (uint32_t)((t1.tv_sec - t0.tv_sec) * 1000000 + (t1.tv_usec - t0.tv_usec));
@@ -1298,7 +1306,10 @@ int srslte_ue_dl_decode_pdsch(srslte_ue_dl_t*     q,
     grids[r] = st->d_grid[r];
     for (uint32_t p = 0; p < q->cell.nof_ports; p++) ce[p][r] = st->d_ce[p][r];
   }
-  const int ret = pdsch_decode_dev(&q->pdsch, ps, st->stream, sf, pdsch_cfg, q->chest_res.noise_estimate, grids, ce, data);
+  // (MI355_DROPIN_CE_PER_SYMBOL=1: the per-symbol two-kernel path even on AVERAGE estimates, A/B timing)
+  static const bool per_sym = getenv("MI355_DROPIN_CE_PER_SYMBOL") && atoi(getenv("MI355_DROPIN_CE_PER_SYMBOL")) != 0;
+  const int ret = pdsch_decode_dev(&q->pdsch, ps, st->stream, sf, pdsch_cfg, q->chest_res.noise_estimate, grids, ce,
+                                   data, st->est_avg && !per_sym);
   if (pdsch_cfg->meas_time_en) {
     gettimeofday(&t1, nullptr);
     pdsch_cfg->meas_time_value = (uint32_t)((t1.tv_sec - t0.tv_sec) * 1000000 + (t1.tv_usec - t0.tv_usec));

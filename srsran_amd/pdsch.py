@@ -67,6 +67,7 @@ def _declare():
     L.mi355_pdsch_frontend.argtypes = [vp, C.POINTER(PdschJob), u32, vp]
     L.mi355_pdsch_debug_stage.argtypes = [vp, u32, u32, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
     L.mi355_pdsch_set_llr_8bit.argtypes = [vp, C.c_int]
+    L.mi355_pdsch_set_ce_invariant.argtypes = [vp, C.c_int]
     L.mi355_pdsch_re_map.restype = u32
     L.mi355_pdsch_re_map.argtypes = [C.POINTER(Cell), C.POINTER(PdschGrant), u32, u32, C.c_void_p]
     L._pdsch_declared = True
@@ -140,6 +141,10 @@ class Pdsch:
         """pdsch.llr_is_8bit (srsUE pdsch_8bit_decoder): int8 LLRs and the 8-bit DL-SCH."""
         check(self.L.mi355_pdsch_set_llr_8bit(self.h, int(enable)), "set_llr_8bit")
         self.llr8 = bool(enable)
+
+    def set_ce_invariant(self, enable: bool = True):
+        """The estimates of the next decodes are the same in every OFDM symbol (mi355_pdsch_set_ce_invariant)."""
+        check(self.L.mi355_pdsch_set_ce_invariant(self.h, int(enable)), "set_ce_invariant")
 
     def stage(self, job: int, cw: int, nof_re: int, nof_bits: int | None):
         """(d complex64[nof_re], csi float32[nof_re], e int16[nof_bits] (int8 in 8-bit mode) or None) of the last

@@ -158,3 +158,43 @@ def test_invalid_configs_rejected():
     bad.cfg.grant.tx_scheme = P.TXSCHEME_SPATIALMUX  # 1 port: predecoding error
     with pytest.raises(RuntimeError):
         pd.decode(pool, [bad])
+
+
+@pytest.mark.parametrize("k", [k for k, c in enumerate(CFGS) if c.scheme in (0, 2)])
+def test_ce_invariant_matches_per_symbol_path(k):
+    """mi355_pdsch_set_ce_invariant (the drop-in sets it on its own AVERAGE estimates): estimates equal in every OFDM
+    symbol decoded through the fused equaliser (row 0 read) and through the per-symbol two-kernel path -- the same
+    CRCs, iteration counts, payloads and decoder buffers."""
+    from srsran_amd import lib
+    import ctypes as C
+    cfg = CFGS[k]
+    sf = pc.synth_subframe(cfg, np.random.default_rng(900 + k), snr_db=26, channel="static")
+    out = []
+    for inv in (False, True):
+        ds = DevSubframe(cfg, sf)
+        pool = SoftbufferPool(2, max_cb=16)
+        pd = P.Pdsch(cell_of(cfg), cfg.nof_rx)
+        pd.set_ce_invariant(inv)
+        res = pd.decode(pool, [ds.job])
+        pool.materialize()
+        buf, stride, mcb = C.POINTER(C.c_int16)(), C.c_uint32(), C.c_uint32()
+        L = lib()
+        L.mi355_softbuffer_pool_buffer.argtypes = [C.c_void_p, C.POINTER(C.POINTER(C.c_int16)),
+                                                   C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.mi355_softbuffer_pool_buffer(pool.h, C.byref(buf), C.byref(stride), C.byref(mcb))
+        sb = np.zeros((2 * mcb.value, stride.value), np.int16)
+        L.mi355_memcpy_d2h(sb.ctypes.data, C.cast(buf, C.c_void_p).value, sb.nbytes)
+        out.append(([(int(res[t].crc), res[t].avg_iterations_block) for t in range(cfg.nof_tb)],
+                    [ds.payload_bytes(t)[:cfg.tbs[t] // 8] for t in range(cfg.nof_tb)], sb))
+        pool.close()
+    assert out[0][0] == out[1][0], (k, out[0][0], out[1][0])
+    assert all(c for c, _ in out[0][0]), k  # 26 dB, static channel: every TB decodes
+    for t in range(cfg.nof_tb):
+        np.testing.assert_array_equal(out[0][1][t], out[1][1][t], err_msg=f"cfg {k} tb {t}")
+        np.testing.assert_array_equal(out[1][1][t], sf.payload[t][:cfg.tbs[t] // 8], err_msg=f"cfg {k} tb {t}")
+    for t in range(cfg.nof_tb):  # the TB's code blocks (slots t * max_cb + c), decoder buffer 3 (K + 32) + 12
+        sg = oracle.cbsegm(cfg.tbs[t])
+        for c in range(sg["C"]):
+            n = 3 * ((sg["K1"] if c < sg["C1"] else sg["K2"]) + 32) + 12
+            np.testing.assert_array_equal(out[0][2][16 * t + c, :n], out[1][2][16 * t + c, :n],
+                                          err_msg=f"cfg {k} tb {t} cb {c} decoder buffer")
