@@ -231,6 +231,12 @@ __shared__ uint32_t tdec_stg_row[4][TDEC_SEG];                // their destinati
 #ifndef TDEC_CLONE_NO_E
 #define TDEC_CLONE_NO_E 0
 #endif
+// NO_E with KEEP: the values the removed stores would have written are kept alive (an empty asm use), so the loads
+// that feed them stay in the clone.  Without it, a launch that emits no decisions has no other use of the forward
+// pass's values and the compiler drops the forward pass's input and checkpoint loads with the stores.
+#ifndef TDEC_CLONE_KEEP
+#define TDEC_CLONE_KEEP 0
+#endif
 // extrinsic / a-priori outputs of a whole segment staged in LDS and stored as 16-byte row pieces (0: A/B builds, each
 // output as a scattered 2-byte store)
 #ifndef TDEC_STAGE_OUT
@@ -533,6 +539,8 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
 #pragma unroll
             for (int s = 0; s < 8; s++) st[s] = nw[s];
           }
+          // (stored before the normalise below: the forward pass's output sums of the segment's last step take this
+          // row as it is, saturating, so a normalised row without its zero state 0 would not be bit-exact)
           if (i == 0 && t > 0 && DIAG != 3 && !(CL && TDEC_CLONE_NO_CK) && !(CL && TDEC_CLONE_CK_HALF && (t & 1))) {
 #pragma unroll
             for (int s = 0; s < 8; s++) {
@@ -748,6 +756,7 @@ __device__ __forceinline__ void tdec_win_body(const TdecWinArgs& a, const int gl
         if (FULL ? i < SEG : j < e) {
           const v2s      out = xin[i] ^ U(cy[i]) ^ ck8[i] ^ st[i];
           const uint32_t tb  = cd[i];
+          if constexpr (TDEC_CLONE_NO_E && TDEC_CLONE_KEEP) asm volatile("" ::"v"(out), "v"(tb));
           if constexpr (!dec2) {
             if constexpr (wr_e && !TDEC_CLONE_NO_E) put(i, tb, out);
             bits |= ((uint32_t)(out.x > 0) << (15 - i)) | ((uint32_t)(out.y > 0) << (7 - i));
