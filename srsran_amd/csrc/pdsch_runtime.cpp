@@ -781,7 +781,7 @@ static bool plan_eq_rm(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi
     const mi355_pdsch_grant_t& g   = cfg.grant;
     if (!P.dev.fused) return false;
     EqRmJob& R  = er.rj[i];
-    uint32_t nt = 0, tbs = 0, nbits = 0, n_max = 0;
+    uint32_t nt = 0, tbs = 0, nbits = 0, n_max = 0, cimg = 0;
     for (uint32_t t = 0; t < 2; t++) {
       if (!P.decode[t]) continue;
       const mi355_ra_tb_t& tb = g.tb[t];
@@ -823,10 +823,18 @@ static bool plan_eq_rm(mi355_pdsch_t* q, mi355_softbuffer_pool_t* pool, const mi
               hit->key = key, hit->E = E;
             }
             R.cmp[kx][ev] = hit->tab, R.cnq[kx][ev] = hit->nq, R.cqoff[kx][ev] = hit->qoff;
-            er.cimg       = std::max(er.cimg, 8 * hit->nq);
+            cimg          = std::max(cimg, 8 * hit->nq);
           }
         }
       }
+    }
+    // the compact image serves two layers only (pdsch_eq_rm's cm: both fresh, one table): a one-layer job (SISO,
+    // transmit diversity, a single TB) keeps the circular-order image, and its compact size must not set the
+    // workgroup's LDS -- at QPSK K = 5312 it is 1.8x the circular image and halved the occupancy (SISO -9 %, r06u)
+    if (nt < 2) {
+      for (auto& row : R.cmp) row[0] = row[1] = nullptr;
+    } else {
+      er.cimg = std::max(er.cimg, cimg);
     }
     er.max_c = std::max(er.max_c, nt ? R.C : 0u);
     er.img   = std::max(er.img, n_max);
