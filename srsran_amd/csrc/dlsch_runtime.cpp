@@ -185,6 +185,13 @@ static bool lat_waves4()
   static const bool on = getenv("MI355_LAT_WAVES") && atoi(getenv("MI355_LAT_WAVES")) == 4;
   return on;
 }
+// latency path: two more waves per code block compute the second parts' output passes beside the recursions
+// (tdec_win_lat.hip); MI355_LAT_OWAVES=0 keeps them in the recursion waves (A/B timing)
+static bool lat_owaves()
+{
+  static const bool on = !getenv("MI355_LAT_OWAVES") || atoi(getenv("MI355_LAT_OWAVES")) != 0;
+  return on;
+}
 
 // MI355_RM_SPARSE=0 (A/B timing): fresh decoder buffers written whole, zero parity rows included
 bool mi355::rm_sparse_writes()
@@ -965,6 +972,7 @@ int mi355::dlsch_decode_dev_hook(mi355_dlsch_t* q, mi355_softbuffer_pool_t* pool
       la.K       = (int)lv.K;
       la.rowmask = nsb == 16 && !no_rowmask();
       la.bwave   = lat_waves4() ? 2 : 1;
+      la.owaves  = la.bwave == 1 && lat_owaves() ? 1 : 0;
       CHECK_HIP(tdec_lat_launch((int)nsb, la, s));
       lat[i] = 1;
     }

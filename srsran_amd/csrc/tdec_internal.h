@@ -114,6 +114,7 @@ struct TdecLatArgs {
   uint64_t*       prof;     // nullable (measurement): [11] phase cycles / counts summed over code blocks (tdec_win_lat.hip)
   int             ncb, K, rowmask;
   int             bwave;    // the beta recursion's wave: 1 (two-wave workgroups) or 2 (four waves, MI355_LAT_WAVES=4)
+  int             owaves;   // 1 (bwave 1): waves 2 and 3 compute the second parts' output passes (MI355_LAT_OWAVES)
 };
 size_t     tdec_lat_lds(int K, int nsb);
 hipError_t tdec_lat_launch(int nsb, const TdecLatArgs& a, hipStream_t s);

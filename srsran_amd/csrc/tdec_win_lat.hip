@@ -226,6 +226,15 @@ template <bool BETA, int PH> __device__ __forceinline__ v2s dstep_n(v2s st, v2s 
   return ssub2(n, bcast<0>(n));
 }
 
+// output waves (A.owaves): staging buffers per recursion (chunks in flight between a recursion wave and its output
+// wave) and whether a waiting wave sleeps between polls (each wave has a SIMD of its own: polling costs no issue slots)
+#ifndef LAT_RING
+#define LAT_RING 2
+#endif
+#ifndef LAT_SPIN_SLEEP
+#define LAT_SPIN_SLEEP 0
+#endif
+static_assert(LAT_RING >= 2, "the recursion waves' own passes double-buffer");
 #ifndef LAT_DIAG
 #define LAT_DIAG 0 // (timing diagnostics, wrong results: 1 no output computation, 2 no output passes)
 #endif
@@ -250,7 +259,7 @@ template <int B, int E, typename F> __device__ __forceinline__ void sfor(F&& f)
 size_t tdec_lat_lds(int K, int nsb)
 {
   const int L = K / nsb, NL = nsb / 2;
-  return (size_t)K / 2 * 4 * 4 + (size_t)L * NL * 8 * 4 + 4 * 64 * 8 * 4 + 256 * 4 + (size_t)(K + 31) / 32 * 4;
+  return (size_t)K / 2 * 4 * 4 + (size_t)L * NL * 8 * 4 + 2 * LAT_RING * 64 * 8 * 4 + 256 * 4 + (size_t)(K + 31) / 32 * 4;
 }
 
 template <int NSB>
@@ -274,11 +283,14 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
   uint32_t* ev   = a1 + K / 2;
   uint32_t* am   = ev + K / 2;                    // [H][NL][8] alpha entering states of steps 0 .. H-1
   uint32_t* bm   = am + (size_t)H * NL * 8;       // [L-H][NL][8] beta rows k+1 of steps H .. L-1
-  uint32_t* sgb  = bm + (size_t)(L - H) * NL * 8; // [2 waves][2][PB][NL][8] double-buffered output staging
-  uint32_t* tl   = sgb + 4 * 64 * 8;              // CRC byte table
+  uint32_t* sgb  = bm + (size_t)(L - H) * NL * 8; // [2 waves][LAT_RING][PB][NL][8] output staging
+  uint32_t* tl   = sgb + 2 * LAT_RING * 64 * 8;   // CRC byte table
   uint32_t* bits = tl + 256;                      // K/8 decision bytes
   __shared__ int16_t  tail[12];
   __shared__ uint32_t fin_s;
+  // A.owaves: chunk counters of the second parts -- [0] alpha chunks staged, [1] alpha chunks read, [2] / [3] beta;
+  // [4] set when a wait gave up (a bounded spin: a protocol fault ends the kernel with the code block failed)
+  __shared__ uint32_t sflg[5];
 
   const size_t    bidx = A.in_idx ? A.in_idx[cb] : (size_t)cb;
   const int16_t*  in   = A.in + bidx * A.in_stride;
@@ -313,11 +325,33 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
   const int  wv = t >> 6, lane = t & 63, p = lane >> 3, q = (int)lane_logical(lane & 7), i_p = lane / NL,
              lp = lane % NL;
   const bool alpha = wv == 0, rec = lane < 8 * NL && (alpha || wv == bw);
+  const bool ow    = A.owaves && (wv == 2 || wv == 3); // an output wave (A.owaves)
+  // wait until *f >= v (LDS, posted by another wave of the workgroup); false after ~2^24 polls (the kernel then ends
+  // with every code block failed rather than hang)
+  auto flag_wait = [&](volatile uint32_t* f, uint32_t v) -> bool {
+    for (uint32_t i = 0; *f < v; i++) {
+      if (i > (1u << 24) || sflg[4]) {
+        sflg[4] = 1;
+        return false;
+      }
+      if (LAT_SPIN_SLEEP) __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory"); // (the LDS reads after it are issued, and so performed, after the flag's)
+    return true;
+  };
+  // A wave's LDS instructions are performed in issue order, so the flag, written after the wave's staged states (or
+  // after its reads of them), is seen only once those are performed: an ordering point for the compiler is all it
+  // takes.  (A release fence here, which makes the recursion wave wait for its own stores every chunk, measured
+  // 48.6 k instead of 46.7 k cycles per second part, tools/gpu/r06o2.sh.)
+  auto flag_post = [&](volatile uint32_t* f, uint32_t v) {
+    asm volatile("" ::: "memory");
+    if (lane == 0) *f = v;
+  };
   const Lane8 cl = lane8((uint32_t)q, !alpha);
   v2s         st   = spl(0);      // this lane's state
   int         ka = 0, pha = 0;    // alpha: next step and its phase
   int         kb = 0, phb = 0;    // beta: next row and the phase of the step computing it
-  uint32_t*  sg    = sgb + (alpha ? 0 : 2 * 64 * 8);
+  uint32_t*  sg    = sgb + (alpha ? 0 : LAT_RING * 64 * 8);
   __shared__ uint32_t simd_s[4]; // (measurement) the SIMD each wave runs on
   if (A.prof && lane == 0) simd_s[wv] = (__builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4) & 3u) + 1u;
   // A.prof (measurement): shader-clock cycles of each phase, taken by lane 0 after the barriers that end them
@@ -336,6 +370,8 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
     // this half-iteration's parity stream; the decision bitmap cleared
     load_stream(dec2 ? 2 : 1, pc);
     for (int i = t; i < (K + 31) / 32; i += nt) bits[i] = 0; // (K/8 bytes need not fill whole words: K = 408)
+    if (t < 4) sflg[t] = 0;
+    if (h == 0 && t == 4) sflg[4] = 0;
     __syncthreads();
     mark(0);
     Blk<NSB>        B{xs, pc, pc, a1, ev, tail, L, dec2, has_ap};
@@ -592,7 +628,54 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
         }
       }
     };
-    if (alpha) {
+    if (ow) {
+      // Output waves (A.owaves): the recursion waves only stage each chunk's PB steps of states and post the chunk
+      // (cnt); wave 2 / 3 computes the alpha / beta wave's passes from them and posts each chunk it has read (rd), so
+      // the output math no longer sits in the recursion's serial path.  LAT_RING staging buffers per recursion: chunk c
+      // is written into buffer c % LAT_RING once chunk c - LAT_RING has been read.
+      const bool fa = wv == 2; // alpha's passes (else beta's)
+      PassIn     P{};
+      if (fa) {
+        // the pass's destinations are read one chunk ahead (global loads), as in the recursion waves' own passes
+        uint32_t e = i_p < min(PB, L - H) ? tbg[(H + i_p) * NL + lp] : 0u;
+        for (int k0 = H, c = 0; k0 < L; k0 += PB, c++) {
+          const int      n = min(PB, L - k0), k = k0 + i_p, k1 = k0 + PB;
+          const bool     ok = i_p < n;
+          const uint32_t en = (k1 < L && i_p < min(PB, L - k1)) ? tbg[(k1 + i_p) * NL + lp] : 0u;
+          if (!flag_wait(&sflg[0], (uint32_t)c + 1)) break;
+          pass_load(ok, k, sgb + (c % LAT_RING) * 64 * 8 + (size_t)lane * 8, bm + ((size_t)(k - H) * NL + lp) * 8, e, P);
+          flag_post(&sflg[1], (uint32_t)c + 1);
+          pass_do(ok, k, P, true);
+          e = en;
+        }
+      } else {
+        uint32_t e = i_p < min(PB, H) ? tbg[(H - 1 - i_p) * NL + lp] : 0u;
+        for (int k0 = H, c = 0; k0 >= 1; k0 -= PB, c++) {
+          const int      n = min(PB, k0), k = k0 - 1 - i_p, k1 = k0 - PB;
+          const bool     ok = i_p < n;
+          const uint32_t en = (k1 >= 1 && i_p < min(PB, k1)) ? tbg[(k1 - 1 - i_p) * NL + lp] : 0u;
+          if (!flag_wait(&sflg[2], (uint32_t)c + 1)) break;
+          pass_load(ok, k, am + ((size_t)k * NL + lp) * 8, sgb + (LAT_RING + c % LAT_RING) * 64 * 8 + (size_t)lane * 8, e, P);
+          flag_post(&sflg[3], (uint32_t)c + 1);
+          pass_do(ok, k, P, false);
+          e = en;
+        }
+      }
+    } else if (A.owaves && alpha) { // (a progress read that did not block measured slower: r06o2c)
+      for (int k0 = H, c = 0; k0 < L; k0 += PB, c++) {
+        const int n = min(PB, L - k0);
+        if (c >= LAT_RING && !flag_wait(&sflg[1], (uint32_t)(c - LAT_RING + 1))) break; // chunk c - LAT_RING read
+        if (rec) a_run(ka, n, pha, sg + (c % LAT_RING) * 64 * 8, -k0 * RS, RS);
+        flag_post(&sflg[0], (uint32_t)c + 1);
+      }
+    } else if (A.owaves && wv == bw) {
+      for (int k0 = H, c = 0; k0 >= 1; k0 -= PB, c++) {
+        const int n = min(PB, k0);
+        if (c >= LAT_RING && !flag_wait(&sflg[3], (uint32_t)(c - LAT_RING + 1))) break;
+        if (rec) b_run(kb, n, phb, sg + (c % LAT_RING) * 64 * 8, k0 * RS, -RS);
+        flag_post(&sflg[2], (uint32_t)c + 1);
+      }
+    } else if (alpha) {
       PassIn P{};
       bool   okp = false;
       int    kp  = 0;
@@ -637,8 +720,8 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
       const uint8_t* dec = (const uint8_t*)bits;
       const int      pc2 = d.C > 1 ? 1 : 0;
       const uint32_t crc = wave_crc24_scaled(dec, K / 8, tl, pc2 ? C.crc24b->poly : C.crc24a->poly, C.scale + (pc2 ? 64 : 0));
-      const bool     ok  = crc == 0;
-      const bool     fin = ok || h + 1 == C.max_its;
+      const bool     ok  = crc == 0 && !sflg[4];
+      const bool     fin = ok || h + 1 == C.max_its || sflg[4];
       if (fin) {
         uint8_t*       dstp = C.data + d.data_off + (size_t)d.cb * d.rlen / 8;
         const uint32_t nb   = (d.cb + 1 == d.C) ? (uint32_t)K / 8 : d.rlen / 8;
@@ -665,6 +748,7 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
     pcy[5]  = simd_s[0];
     pcy[6]  = simd_s[bw];
     pcy[7]  = simd_s[0] == simd_s[bw];
+    if (A.owaves) pcy[8] = (simd_s[2] == simd_s[0] || simd_s[2] == simd_s[bw]) + (simd_s[3] == simd_s[0] || simd_s[3] == simd_s[bw]);
 #pragma unroll
     for (int k = 0; k < 11; k++) atomicAdd((unsigned long long*)&A.prof[k], (unsigned long long)pcy[k]);
   }
@@ -676,10 +760,12 @@ hipError_t tdec_lat_launch(int nsb, const TdecLatArgs& a, hipStream_t s)
   if (lds > 160 * 1024 - 64) return hipErrorInvalidValue;
   const void* f = nsb == 16 ? (const void*)tdec_win_lat<16> : (const void*)tdec_win_lat<8>;
   if (hipError_t e = lds_optin(f, lds); e != hipSuccess) return e;
+  if (a.owaves && a.bwave != 1) return hipErrorInvalidValue; // (output waves 2 and 3 beside recursion waves 0 and 1)
+  const int nth = a.owaves ? 256 : 64 * (2 * a.bwave);
   if (nsb == 16) {
-    hipLaunchKernelGGL(tdec_win_lat<16>, dim3(a.ncb), dim3(64 * (2 * a.bwave)), lds, s, a);
+    hipLaunchKernelGGL(tdec_win_lat<16>, dim3(a.ncb), dim3(nth), lds, s, a);
   } else {
-    hipLaunchKernelGGL(tdec_win_lat<8>, dim3(a.ncb), dim3(64 * (2 * a.bwave)), lds, s, a);
+    hipLaunchKernelGGL(tdec_win_lat<8>, dim3(a.ncb), dim3(nth), lds, s, a);
   }
   return hipGetLastError();
 }

@@ -16,7 +16,7 @@ import oracle  # noqa: E402
 from srsran_amd import lib  # noqa: E402
 from srsran_amd.dlsch import Dlsch, SoftbufferPool  # noqa: E402
 
-NAMES = ["load", "first_halves", "second_halves", "decisions", "check", "simd_alpha", "simd_beta", "same_simd", "-", "half_its", "cbs"]
+NAMES = ["load", "first_halves", "second_halves", "decisions", "check", "simd_alpha", "simd_beta", "same_simd", "owave_shares_simd", "half_its", "cbs"]
 rng = np.random.default_rng(1)
 QUICK = os.environ.get("LAT_PROBE_QUICK") == "1"  # the 30 dB latency case only
 if os.environ.get("LAT_PROBE_SWEEP") == "1":  # crossover: host time per call of both paths vs transport blocks per call
@@ -67,6 +67,6 @@ for snr in ((30.0,) if QUICK else (9.0, 5.5, 30.0)):
             res["per_cb_half_it_kcycles"] = {NAMES[k]: round(v[k] / hi / 1e3, 2) for k in (1, 2, 3, 4)}
             res["load_kcycles_per_cb"] = round(v[0] / cb / 1e3, 2)
             res["half_its_per_cb"] = round(hi / cb, 2)
-            res["simd"] = {NAMES[k]: round(v[k] / cb - (k < 7), 2) for k in (5, 6, 7)}
+            res["simd"] = {NAMES[k]: round(v[k] / cb - (k < 7), 2) for k in (5, 6, 7, 8)}
         print(json.dumps(res), flush=True)
         dl.close() if hasattr(dl, "close") else None
