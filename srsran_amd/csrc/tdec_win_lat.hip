@@ -262,7 +262,9 @@ size_t tdec_lat_lds(int K, int nsb)
   return (size_t)K / 2 * 4 * 4 + (size_t)L * NL * 8 * 4 + 2 * LAT_RING * 64 * 8 * 4 + 256 * 4 + (size_t)(K + 31) / 32 * 4;
 }
 
-template <int NSB>
+// OW: output waves (A.owaves) -- a template parameter, so that each form is compiled without the other's inlined
+// recursion code (111 instead of 135 SGPRs spilled; the second parts measured the same, 46.2 vs 46.9 k cycles)
+template <int NSB, bool OW>
 __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
 {
   // NL window pairs; PB steps per output pass (PB x NL = 64 lanes)
@@ -325,7 +327,7 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
   const int  wv = t >> 6, lane = t & 63, p = lane >> 3, q = (int)lane_logical(lane & 7), i_p = lane / NL,
              lp = lane % NL;
   const bool alpha = wv == 0, rec = lane < 8 * NL && (alpha || wv == bw);
-  const bool ow    = A.owaves && (wv == 2 || wv == 3); // an output wave (A.owaves)
+  const bool ow    = OW && (wv == 2 || wv == 3); // an output wave (A.owaves)
   // wait until *f >= v (LDS, posted by another wave of the workgroup); false after ~2^24 polls (the kernel then ends
   // with every code block failed rather than hang)
   auto flag_wait = [&](volatile uint32_t* f, uint32_t v) -> bool {
@@ -661,21 +663,21 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
           e = en;
         }
       }
-    } else if (A.owaves && alpha) { // (a progress read that did not block measured slower: r06o2c)
+    } else if (OW && alpha) { // (a progress read that did not block measured slower: r06o2c)
       for (int k0 = H, c = 0; k0 < L; k0 += PB, c++) {
         const int n = min(PB, L - k0);
         if (c >= LAT_RING && !flag_wait(&sflg[1], (uint32_t)(c - LAT_RING + 1))) break; // chunk c - LAT_RING read
         if (rec) a_run(ka, n, pha, sg + (c % LAT_RING) * 64 * 8, -k0 * RS, RS);
         flag_post(&sflg[0], (uint32_t)c + 1);
       }
-    } else if (A.owaves && wv == bw) {
+    } else if (OW && wv == bw) {
       for (int k0 = H, c = 0; k0 >= 1; k0 -= PB, c++) {
         const int n = min(PB, k0);
         if (c >= LAT_RING && !flag_wait(&sflg[3], (uint32_t)(c - LAT_RING + 1))) break;
         if (rec) b_run(kb, n, phb, sg + (c % LAT_RING) * 64 * 8, k0 * RS, -RS);
         flag_post(&sflg[2], (uint32_t)c + 1);
       }
-    } else if (alpha) {
+    } else if (!OW && alpha) {
       PassIn P{};
       bool   okp = false;
       int    kp  = 0;
@@ -693,7 +695,7 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
           pass_do(ok, k, P, true);
         }
       }
-    } else if (wv == bw) {
+    } else if (!OW && wv == bw) {
       PassIn P{};
       bool   okp = false;
       int    kp  = 0;
@@ -748,7 +750,7 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
     pcy[5]  = simd_s[0];
     pcy[6]  = simd_s[bw];
     pcy[7]  = simd_s[0] == simd_s[bw];
-    if (A.owaves) pcy[8] = (simd_s[2] == simd_s[0] || simd_s[2] == simd_s[bw]) + (simd_s[3] == simd_s[0] || simd_s[3] == simd_s[bw]);
+    if (OW) pcy[8] = (simd_s[2] == simd_s[0] || simd_s[2] == simd_s[bw]) + (simd_s[3] == simd_s[0] || simd_s[3] == simd_s[bw]);
 #pragma unroll
     for (int k = 0; k < 11; k++) atomicAdd((unsigned long long*)&A.prof[k], (unsigned long long)pcy[k]);
   }
@@ -758,14 +760,23 @@ hipError_t tdec_lat_launch(int nsb, const TdecLatArgs& a, hipStream_t s)
 {
   const size_t lds = tdec_lat_lds(a.K, nsb);
   if (lds > 160 * 1024 - 64) return hipErrorInvalidValue;
-  const void* f = nsb == 16 ? (const void*)tdec_win_lat<16> : (const void*)tdec_win_lat<8>;
-  if (hipError_t e = lds_optin(f, lds); e != hipSuccess) return e;
   if (a.owaves && a.bwave != 1) return hipErrorInvalidValue; // (output waves 2 and 3 beside recursion waves 0 and 1)
+  const void* f = nsb == 16 ? (a.owaves ? (const void*)tdec_win_lat<16, true> : (const void*)tdec_win_lat<16, false>)
+                            : (a.owaves ? (const void*)tdec_win_lat<8, true> : (const void*)tdec_win_lat<8, false>);
+  if (hipError_t e = lds_optin(f, lds); e != hipSuccess) return e;
   const int nth = a.owaves ? 256 : 64 * (2 * a.bwave);
   if (nsb == 16) {
-    hipLaunchKernelGGL(tdec_win_lat<16>, dim3(a.ncb), dim3(nth), lds, s, a);
+    if (a.owaves) {
+      hipLaunchKernelGGL((tdec_win_lat<16, true>), dim3(a.ncb), dim3(nth), lds, s, a);
+    } else {
+      hipLaunchKernelGGL((tdec_win_lat<16, false>), dim3(a.ncb), dim3(nth), lds, s, a);
+    }
   } else {
-    hipLaunchKernelGGL(tdec_win_lat<8>, dim3(a.ncb), dim3(nth), lds, s, a);
+    if (a.owaves) {
+      hipLaunchKernelGGL((tdec_win_lat<8, true>), dim3(a.ncb), dim3(nth), lds, s, a);
+    } else {
+      hipLaunchKernelGGL((tdec_win_lat<8, false>), dim3(a.ncb), dim3(nth), lds, s, a);
+    }
   }
   return hipGetLastError();
 }
