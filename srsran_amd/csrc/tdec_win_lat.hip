@@ -236,7 +236,7 @@ template <bool BETA, int PH> __device__ __forceinline__ v2s dstep_n(v2s st, v2s 
 #endif
 static_assert(LAT_RING >= 2, "the recursion waves' own passes double-buffer");
 #ifndef LAT_DIAG
-#define LAT_DIAG 0 // (timing diagnostics, wrong results: 1 no output computation, 2 no output passes)
+#define LAT_DIAG 0 // (timing diagnostics, wrong results: 1 no output computation, 2 no output passes, 4 no output-wave handoff)
 #endif
 
 template <int P> struct Par {
@@ -630,7 +630,9 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
         }
       }
     };
-    if (ow) {
+    if (ow && (LAT_DIAG & 4)) {
+      // (diagnostic: no handoff at all -- the output waves idle, the recursion waves neither wait nor post)
+    } else if (ow) {
       // Output waves (A.owaves): the recursion waves only stage each chunk's PB steps of states and post the chunk
       // (cnt); wave 2 / 3 computes the alpha / beta wave's passes from them and posts each chunk it has read (rd), so
       // the output math no longer sits in the recursion's serial path.  LAT_RING staging buffers per recursion: chunk c
@@ -638,7 +640,8 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
       const bool fa = wv == 2; // alpha's passes (else beta's)
       PassIn     P{};
       if (fa) {
-        // the pass's destinations are read one chunk ahead (global loads), as in the recursion waves' own passes
+        // the pass's destinations are read one chunk ahead (global loads), as in the recursion waves' own passes (two
+        // chunks ahead measured the same, r06o6)
         uint32_t e = i_p < min(PB, L - H) ? tbg[(H + i_p) * NL + lp] : 0u;
         for (int k0 = H, c = 0; k0 < L; k0 += PB, c++) {
           const int      n = min(PB, L - k0), k = k0 + i_p, k1 = k0 + PB;
@@ -666,16 +669,16 @@ __global__ __launch_bounds__(256) void tdec_win_lat(TdecLatArgs A)
     } else if (OW && alpha) { // (a progress read that did not block measured slower: r06o2c)
       for (int k0 = H, c = 0; k0 < L; k0 += PB, c++) {
         const int n = min(PB, L - k0);
-        if (c >= LAT_RING && !flag_wait(&sflg[1], (uint32_t)(c - LAT_RING + 1))) break; // chunk c - LAT_RING read
+        if (!(LAT_DIAG & 4) && c >= LAT_RING && !flag_wait(&sflg[1], (uint32_t)(c - LAT_RING + 1))) break; // chunk c - LAT_RING read
         if (rec) a_run(ka, n, pha, sg + (c % LAT_RING) * 64 * 8, -k0 * RS, RS);
-        flag_post(&sflg[0], (uint32_t)c + 1);
+        if (!(LAT_DIAG & 4)) flag_post(&sflg[0], (uint32_t)c + 1);
       }
     } else if (OW && wv == bw) {
       for (int k0 = H, c = 0; k0 >= 1; k0 -= PB, c++) {
         const int n = min(PB, k0);
-        if (c >= LAT_RING && !flag_wait(&sflg[3], (uint32_t)(c - LAT_RING + 1))) break;
+        if (!(LAT_DIAG & 4) && c >= LAT_RING && !flag_wait(&sflg[3], (uint32_t)(c - LAT_RING + 1))) break;
         if (rec) b_run(kb, n, phb, sg + (c % LAT_RING) * 64 * 8, k0 * RS, -RS);
-        flag_post(&sflg[2], (uint32_t)c + 1);
+        if (!(LAT_DIAG & 4)) flag_post(&sflg[2], (uint32_t)c + 1);
       }
     } else if (!OW && alpha) {
       PassIn P{};
